@@ -1,0 +1,175 @@
+"""ORACLE / TEST INFRASTRUCTURE ONLY — ctypes wrapper of oracle/cdc_oracle.c.
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg.  Loads oracle/_build/liboracle.so (built by ``make -C oracle``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from functools import lru_cache
+
+import numpy as np
+
+from . import gorand, rollinghash
+from .splitter_ref import REGISTRY
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "liboracle.so")
+KIND = {"fixed": 0, "buzhash": 1, "rabinkarp": 2}
+MODES = {"getSplitPoints": 0, "getSplitPointsByteByByte": 1, "getSplitPointsRandomSlices": 2}
+
+_i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+_u64p = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
+_u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB
+
+
+@lru_cache(maxsize=1)
+def lib() -> C.CDLL:
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, "cdc_oracle.c")):
+        build()
+    L = C.CDLL(LIB)
+    L.orc_set_tables.argtypes = [_u32p, _u64p, _u64p, C.c_int]
+    L.orc_new.restype = C.c_void_p
+    L.orc_new.argtypes = [C.c_int, C.c_int64]
+    L.orc_free.argtypes = [C.c_void_p]
+    L.orc_reset.argtypes = [C.c_void_p]
+    L.orc_next.restype = C.c_int64
+    L.orc_next.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
+    L.orc_max_segment.restype = C.c_int64
+    L.orc_max_segment.argtypes = [C.c_void_p]
+    L.orc_feed.restype = C.c_int64
+    L.orc_feed.argtypes = [C.c_void_p, C.c_char_p, C.c_int64, C.c_int, C.c_uint64, _i64p, C.c_int64]
+    L.orc_split_stream.restype = C.c_int64
+    L.orc_split_stream.argtypes = [C.c_int, C.c_int64, C.c_void_p, C.c_int64, _i64p, C.c_int64]
+    L.orc_gorand_read.argtypes = [C.c_int64, _u64p, C.c_void_p, C.c_int64]
+    L.orc_gen_stream.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int64]
+    L.orc_split_batch.argtypes = [C.c_int, C.c_int64, C.POINTER(C.c_void_p), _i64p, C.c_int64,
+                                  _i64p, _i64p, _i64p, _i64p, C.c_int]
+    L.orc_split_prng_streams.argtypes = [C.c_int, C.c_int64, C.c_uint64, _u64p, C.c_int64, C.c_int64,
+                                         _i64p, _i64p, _i64p, _i64p, C.c_int]
+    L.orc_rolled_bytes.restype = C.c_int64
+    L.orc_rolled_bytes.argtypes = [C.c_int64, _i64p, C.c_int64]
+    out, mod = rollinghash.rabin_tables()
+    P, _ = rollinghash.rabin_polynomial()
+    L.orc_set_tables(np.ascontiguousarray(rollinghash.buzhash_table()), np.ascontiguousarray(out),
+                     np.ascontiguousarray(mod), P.bit_length() - 1 - 8)
+    return L
+
+
+def params(name: str) -> tuple[int, int]:
+    kind, size = REGISTRY[name]
+    return KIND[kind], size
+
+
+def min_size(name: str) -> int:
+    kind, size = REGISTRY[name]
+    return size if kind == "fixed" else size // 2
+
+
+def cut_capacity(name: str, n: int) -> int:
+    """Upper bound on chunks of an n-byte stream: every chunk but the last is >= min."""
+    return n // max(min_size(name), 1) + 1
+
+
+class OracleSplitter:
+    """Streaming handle over the C restatement (NextSplitPoint semantics)."""
+
+    def __init__(self, name: str):
+        k, size = params(name)
+        self._L = lib()
+        self._h = self._L.orc_new(k, size)
+
+    def next_split_point(self, b: bytes) -> int:
+        return self._L.orc_next(self._h, bytes(b), len(b))
+
+    def max_segment_size(self) -> int:
+        return self._L.orc_max_segment(self._h)
+
+    def reset(self):
+        self._L.orc_reset(self._h)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.orc_free(self._h)
+            self._h = None
+
+
+def feed(name: str, data: bytes, mode: str, seed: int = 1) -> np.ndarray:
+    """Split points (absolute end offsets) under one of the reference test feeders."""
+    k, size = params(name)
+    L = lib()
+    h = L.orc_new(k, size)
+    try:
+        cap = cut_capacity(name, len(data)) + 1
+        out = np.zeros(cap, dtype=np.int64)
+        n = L.orc_feed(h, data, len(data), MODES[mode], seed, out, cap)
+        assert n <= cap
+        return out[:n].copy()
+    finally:
+        L.orc_free(h)
+
+
+def split_stream(name: str, data) -> np.ndarray:
+    """Chunk end offsets of a whole stream, trailing chunk included (last == len)."""
+    k, size = params(name)
+    buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    n = buf.size
+    cap = cut_capacity(name, n)
+    out = np.zeros(max(cap, 1), dtype=np.int64)
+    cnt = lib().orc_split_stream(k, size, buf.ctypes.data, n, out, cap)
+    assert cnt <= cap
+    return out[:cnt].copy()
+
+
+def split_batch(name: str, streams: list, nthreads: int = 8):
+    """Threaded whole-stream split of many host buffers -> list of cut arrays."""
+    k, size = params(name)
+    arrs = [np.frombuffer(s, dtype=np.uint8) if not isinstance(s, np.ndarray) else s for s in streams]
+    lens = np.array([a.size for a in arrs], dtype=np.int64)
+    caps = np.array([cut_capacity(name, int(n)) for n in lens], dtype=np.int64)
+    base = np.zeros(len(arrs), dtype=np.int64)
+    if len(arrs) > 1:
+        base[1:] = np.cumsum(caps)[:-1]
+    cuts = np.zeros(max(int(caps.sum()), 1), dtype=np.int64)
+    counts = np.zeros(len(arrs), dtype=np.int64)
+    ptrs = (C.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    lib().orc_split_batch(k, size, ptrs, lens, len(arrs), cuts, base, caps, counts, nthreads)
+    return [cuts[base[i]:base[i] + counts[i]].copy() for i in range(len(arrs))]
+
+
+def split_prng_streams(name: str, seed: int, sids, stream_len: int, nthreads: int = 8):
+    """Generate counter-PRNG streams (same bytes as the GPU generator) and split them."""
+    k, size = params(name)
+    sids = np.ascontiguousarray(np.asarray(sids, dtype=np.uint64))
+    ns = sids.size
+    cap = cut_capacity(name, stream_len)
+    caps = np.full(ns, cap, dtype=np.int64)
+    base = np.arange(ns, dtype=np.int64) * cap
+    cuts = np.zeros(max(ns * cap, 1), dtype=np.int64)
+    counts = np.zeros(ns, dtype=np.int64)
+    lib().orc_split_prng_streams(k, size, seed, sids, ns, stream_len, cuts, base, caps, counts, nthreads)
+    return cuts.reshape(ns, cap), counts
+
+
+def gen_stream(seed: int, sid: int, n: int, offset: int = 0) -> np.ndarray:
+    out = np.empty(n, dtype=np.uint8)
+    lib().orc_gen_stream(seed, sid, offset, out.ctypes.data, n)
+    return out
+
+
+def gorand_read(seed: int, n: int) -> np.ndarray:
+    out = np.empty(n, dtype=np.uint8)
+    lib().orc_gorand_read(seed, np.ascontiguousarray(gorand.rng_cooked()), out.ctypes.data, n)
+    return out
+
+
+def rolled_bytes(name: str, cuts) -> int:
+    c = np.ascontiguousarray(np.asarray(cuts, dtype=np.int64))
+    return lib().orc_rolled_bytes(min_size(name), c, c.size)
