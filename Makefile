@@ -1,0 +1,36 @@
+# Builds the product library kopia_amd/libkcdc.so (gfx950 only) and the C
+# oracle used by the tests (oracle/_build/liboracle.so).
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
+CSRC := kopia_amd/csrc
+OBJ := build/obj
+SRCS := $(CSRC)/kcdc_kernels.hip $(CSRC)/kcdc_api.cpp $(CSRC)/kcdc_tables.cpp $(CSRC)/kcdc_registry.cpp
+OBJS := $(patsubst $(CSRC)/%,$(OBJ)/%.o,$(SRCS))
+LIB := kopia_amd/libkcdc.so
+
+all: $(LIB) oracle
+
+$(OBJ)/%.hip.o: $(CSRC)/%.hip $(CSRC)/kcdc_internal.h include/kcdc.h
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJ)/%.cpp.o: $(CSRC)/%.cpp $(CSRC)/kcdc_internal.h include/kcdc.h
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -s -C oracle
+
+asm: $(CSRC)/kcdc_kernels.hip
+	@mkdir -p build/asm
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $< -o build/asm/kcdc_kernels.s -Rpass-analysis=kernel-resource-usage 2> build/asm/resource.txt
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle clean asm

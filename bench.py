@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Splitter throughput benchmark (BASELINE.json metric) for the MI355X CDC splitter.
+
+Workload (BASELINE.json configs[1]): per GPU, 4096 independent 4 MiB streams of
+counter-PRNG bytes resident in HBM, split with the default algorithm
+DYNAMIC-4M-BUZHASH (repo/splitter/splitter.go:89).  One *step* = one launch of
+the batch splitter over all 4096 streams (the whole 16 GiB shard); cut lists stay
+in HBM.  For N > 1 GPUs every rank splits its own shard (stream ids offset by
+rank): weak scaling, no collective on the data path (the only collectives are
+the timing barrier and the max-over-ranks of the elapsed time).
+
+Prints ONE JSON line on rank 0 (the driver's contract).  Extra keys:
+  roofline     — dominant kernel's algorithmic bytes / kernel time vs HBM peak
+  cpu_baseline — the oracle's C restatement of the reference Go loop timed on
+                 this host (rank 0, N=1 only)
+  host_inclusive_gib_s — H2D + kernel + D2H rate through kcdc_split_batch_host
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from kopia_amd import _lib, batch  # noqa: E402
+from kopia_amd import splitter as ks  # noqa: E402
+
+METRIC = "splitter throughput GiB/s (device-resident) at 1/2/4/8 GPU; boundaries bit-exact"
+SEED = 0x6B6F706961
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
+GiB = float(1 << 30)
+
+
+def rolled_bytes(cuts: np.ndarray, min_size: int) -> int:
+    """Bytes the reference loop must read for one stream:
+    per chunk [s,e): (e-s) - max(min(min-1, e-s) - 64, 0)."""
+    if cuts.size == 0:
+        return 0
+    lens = np.diff(np.concatenate(([0], cuts)))
+    fastp = np.minimum(min_size - 1, lens)
+    return int(np.sum(lens - np.maximum(fastp - 64, 0)))
+
+
+def load_pmc_traffic(kernel_prefix: str):
+    """Measured HBM bytes per launch from a committed rocprofv3 --pmc summary
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        return d.get(kernel_prefix, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(name: str, ns: int, L: int, gpu_cuts: list, nthreads: int):
+    """Rank 0, N=1: the C restatement of the reference Go loop (oracle/, "port"),
+    timed on host cores over a sample of the same workload; also checks that the
+    GPU cut lists of the sample are bit-identical."""
+    from oracle import coracle  # oracle import confined to this leg
+    t0 = time.time()
+    streams = [None] * ns
+    # generate the sample (not timed), then time only the split
+    import concurrent.futures as cf
+    with cf.ThreadPoolExecutor(nthreads) as ex:
+        for i, s in enumerate(ex.map(lambda i: coracle.gen_stream(SEED, i, L), range(ns))):
+            streams[i] = s
+    gen_s = time.time() - t0
+    coracle.split_batch(name, streams[:8], nthreads=nthreads)  # warm
+    t0 = time.perf_counter()
+    want = coracle.split_batch(name, streams, nthreads=nthreads)
+    dt = time.perf_counter() - t0
+    mism = sum(1 for i in range(ns) if not np.array_equal(want[i], gpu_cuts[i]))
+    return {"value": round(ns * L / GiB / dt, 3), "unit": "GiB/s", "cores": nthreads, "kind": "port",
+            "sample": f"{ns} x {L >> 20} MiB counter-PRNG streams (stream ids 0..{ns - 1}, same bytes as GPU rank 0), "
+                      f"{name}, C restatement of repo/splitter/splitter_buzhash32.go:26-67 (oracle/cdc_oracle.c), "
+                      f"{nthreads} threads, {dt:.2f}s wall",
+            "sample_parity_mismatches": mism, "gen_seconds": round(gen_s, 2)}, streams
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--splitter", default="DYNAMIC-4M-BUZHASH")
+    ap.add_argument("--streams", type=int, default=4096)
+    ap.add_argument("--stream-mib", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-inclusive", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    name, ns, L = args.splitter, args.streams, args.stream_mib << 20
+    info = ks.lookup(name)
+    assert info is not None, name
+    data = torch.empty(ns * L, dtype=torch.uint8, device=dev)
+    batch.fill_prng(data, L, ns, L, SEED, first_sid=rank * ns)
+    b = batch.make_device_batch(name, [data.data_ptr() + i * L for i in range(ns)], [L] * ns, dev)
+    stream = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        batch.split_batch_device(name, b, stream)
+    torch.cuda.synchronize(dev)
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        batch.split_batch_device(name, b, stream)
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+
+    cuts = batch.read_cuts(b)
+    alg_bytes = sum(rolled_bytes(c, int(info.min_size)) for c in cuts)  # per launch, this rank
+    total_bytes = ns * L * world * args.steps
+    value = total_bytes / GiB / elapsed
+
+    out = {
+        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": f"config2: {ns} x {args.stream_mib} MiB independent streams per GPU "
+                               f"(counter-PRNG bytes, HBM-resident), {name}",
+                   "splitter": name, "streams_per_gpu": ns, "stream_bytes": L, "global_streams": ns * world,
+                   "parallelism": f"stream-sharded x{world}, no data-path collectives"},
+    }
+    traffic = load_pmc_traffic("split_batch_kernel")
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                       "kernel": "kcdc::dev::split_batch_kernel<buzhash>", "kernel_ms": round(kern_ms, 4),
+                       "algorithmic_bytes_per_launch": alg_bytes,
+                       "algorithmic_bytes_def": "bytes the reference loop rolls (min-size fast path skipped), "
+                                                "exact from the cut lists; SURVEY.md §8d",
+                       "stream_bytes_per_launch": ns * L,
+                       "stream_gbs": round(ns * L / (kern_ms * 1e-3) / 1e9, 1)}
+    out["cut_stats"] = {"chunks": int(sum(c.size for c in cuts)),
+                        "rolled_fraction": round(alg_bytes / (ns * L), 4)}
+
+    if rank == 0 and world == 1 and not args.no_host_inclusive:
+        # host-inclusive: pageable host buffers -> H2D -> kernel -> D2H (kcdc_split_batch_host)
+        nh = min(ns, 1024)
+        host = data[: nh * L].cpu().numpy()
+        views = [host[i * L:(i + 1) * L] for i in range(nh)]
+        batch.split_batch_host(name, views[:4], device=local)
+        t0 = time.perf_counter()
+        hc = batch.split_batch_host(name, views, device=local)
+        dt = time.perf_counter() - t0
+        assert all(np.array_equal(hc[i], cuts[i]) for i in range(nh))
+        out["host_inclusive_gib_s"] = round(nh * L / GiB / dt, 3)
+        del host, views
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        nthreads = min(16, os.cpu_count() or 1)
+        base, _ = cpu_baseline(name, ns, L, cuts, nthreads)
+        out["cpu_baseline"] = base
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

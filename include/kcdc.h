@@ -1,0 +1,154 @@
+/*
+ * kcdc.h — C ABI of the MI355X-native content-defined-chunking splitter for
+ * Kopia (library: kopia_amd/libkcdc.so, built for gfx950).
+ *
+ * This is the drop-in boundary for Kopia's `repo/splitter` package.  Every
+ * entry point below names the reference interface it replaces
+ * (paths relative to the kopia/kopia tree).  Plain pointers and sizes only;
+ * no torch or HIP types appear in the signatures (streams are passed as
+ * `void*` holding a hipStream_t, or NULL for the library's own stream).
+ *
+ * Semantics are bit-exact with the reference Go splitters: for any input bytes
+ * and any slicing of them, the split points are the ones Kopia computes.
+ *
+ * Errors: functions returning `int` return KCDC_OK (0) or a negative KCDC_E*
+ * code and set a thread-local message readable with kcdc_last_error().  There
+ * is NO silent CPU fallback: if the GPU path cannot run, the call fails.
+ */
+#ifndef KCDC_H
+#define KCDC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KCDC_OK 0
+#define KCDC_ENOENT (-2)     /* unknown splitter name */
+#define KCDC_EIO (-5)        /* HIP runtime / kernel error */
+#define KCDC_ENOMEM (-12)
+#define KCDC_EINVAL (-22)
+#define KCDC_ENODEV (-19)    /* no usable gfx950 device */
+#define KCDC_EOVERFLOW (-75) /* caller-provided cut capacity too small */
+
+#define KCDC_KIND_FIXED 0
+#define KCDC_KIND_BUZHASH 1
+#define KCDC_KIND_RABINKARP 2
+
+/* Parameters behind a registered name.
+ * Reference: newBuzHash32SplitterFactory repo/splitter/splitter_buzhash32.go:73-86,
+ * newRabinKarp64SplitterFactory splitter_rabinkarp64.go:73-83, Fixed splitter_fixed.go:33-37. */
+typedef struct kcdc_algo_info {
+    int32_t kind;      /* KCDC_KIND_* */
+    int32_t pooled;    /* 1 if the reference wraps the factory in pooled() (splitter.go:51-73) */
+    uint64_t avg;      /* average chunk size (FIXED: chunk length) */
+    uint64_t min_size; /* avg/2 (FIXED: chunk length) */
+    uint64_t max_size; /* 2*avg (FIXED: chunk length) == MaxSegmentSize() */
+    uint64_t mask;     /* avg-1 (FIXED: 0) */
+} kcdc_algo_info;
+
+/* ------------------------------------------------------------ diagnostics */
+const char* kcdc_last_error(void);
+const char* kcdc_version(void);
+/* Number of visible gfx950 devices (0 on a machine without one). */
+int kcdc_device_count(void);
+
+/* --------------------------------------------------------------- registry */
+/* SupportedAlgorithms() — repo/splitter/splitter.go:32-42 (sorted names).
+ * Writes up to `cap` name pointers (static storage) and returns the total count. */
+int kcdc_supported_algorithms(const char** names, int cap);
+/* DefaultAlgorithm — repo/splitter/splitter.go:89 ("DYNAMIC-4M-BUZHASH"). */
+const char* kcdc_default_algorithm(void);
+/* GetFactory(name) != nil — repo/splitter/splitter.go:84-86.  Returns KCDC_OK or KCDC_ENOENT. */
+int kcdc_lookup(const char* name, kcdc_algo_info* info);
+/* Factory().MaxSegmentSize() — splitter_buzhash32.go:69-71 / splitter_rabinkarp64.go:69-71 /
+ * splitter_fixed.go:29-31.  Returns < 0 (KCDC_ENOENT) for unknown names. */
+int64_t kcdc_max_segment_size(const char* name);
+/* Name for a NON-registered parameterisation, mirroring the unexported factory
+ * constructors the reference tests call directly: newBuzHash32SplitterFactory(avg)
+ * (splitter_buzhash32.go:73), newRabinKarp64SplitterFactory(avg)
+ * (splitter_rabinkarp64.go:73), Fixed(length) (splitter_fixed.go:33); see
+ * repo/splitter/splitter_test.go:27-52.  `avg` must be a power of two >= 2 for
+ * the rolling kinds (mask = avg-1), >= 1 for FIXED.  Returns an interned name
+ * (static storage, never in kcdc_supported_algorithms) accepted by every
+ * name-taking entry point, or NULL (KCDC_EINVAL). */
+const char* kcdc_custom_algorithm(int32_t kind, uint64_t avg);
+/* Upper bound on the number of chunks of a `stream_len`-byte stream (every chunk
+ * but the last is >= min size): size cut arrays with it. */
+uint64_t kcdc_cut_capacity(const char* name, uint64_t stream_len);
+
+/* Rolling-hash constants as derived by the library (buzhash32 byte table,
+ * Rabin-Karp polynomial and out/mod tables; rollinghash v4.0.0, go.mod:13).
+ * Any pointer may be NULL.  Host-only: works without a GPU. */
+int kcdc_tables(uint32_t* buzhash256, uint64_t* rabin_pol, uint64_t* rabin_out256, uint64_t* rabin_mod256);
+
+/* ------------------------------------------------ streaming Splitter handle
+ * Mirrors `type Splitter interface` (repo/splitter/splitter.go:20-29) and
+ * `type Factory func() Splitter` (:45).  One handle per object writer; calls on
+ * one handle must be serialised by the caller (objectWriter.mu,
+ * repo/object/object_writer.go:114), handles are independent of each other.
+ * `b` is borrowed for the call only (object_writer.go:121-129). */
+typedef struct kcdc_splitter kcdc_splitter;
+/* GetFactory(name)() — NULL on unknown name or no device (see kcdc_last_error). */
+kcdc_splitter* kcdc_splitter_new(const char* name, int device);
+/* NextSplitPoint(b) — returns n in 1..len (split AFTER byte n, n bytes consumed),
+ * -1 if no split point (all consumed), or a KCDC_E* code (< -1) on failure. */
+int64_t kcdc_splitter_next(kcdc_splitter* s, const uint8_t* b, size_t len);
+/* MaxSegmentSize() */
+int64_t kcdc_splitter_max_segment_size(const kcdc_splitter* s);
+/* Reset() — splitter_buzhash32.go:20-24: back to the 64-zero window, count 0. */
+void kcdc_splitter_reset(kcdc_splitter* s);
+/* Close() — splitter_pool.go:18-22: Reset and return to the name's pool (pooled
+ * names) or free.  The handle must not be used afterwards. */
+void kcdc_splitter_close(kcdc_splitter* s);
+
+/* ------------------------------------------------------ batch (hot path)
+ * Split `nstreams` independent streams in one launch; every stream starts from
+ * a fresh splitter (the pool's Reset-on-Close, splitter_pool.go:18-22).
+ * Output for stream i: counts[i] chunk END offsets written to
+ * cuts[cut_base[i] .. cut_base[i]+counts[i]), strictly increasing, the last one
+ * equal to lens[i] (the trailing chunk `Result()` flushes,
+ * repo/object/object_writer.go:264-277).  An empty stream yields 0 entries.
+ * Capacity for stream i is cut_base[i+1]-cut_base[i] (last: `cuts_cap`-cut_base[i]);
+ * size it with kcdc_cut_capacity().  counts[i] always receives the TRUE number of
+ * chunks; entries beyond the capacity are not written, so counts[i] > capacity
+ * signals overflow (the _host variant returns KCDC_EOVERFLOW).
+ *
+ * _device: every pointer (the array of stream pointers, lens, cuts, cut_base,
+ * counts) is device memory on the current device; the call is asynchronous on
+ * `hip_stream` (NULL = legacy default stream) except for error checking of
+ * the launch.  Stream bytes may have any alignment.  */
+int kcdc_split_batch_device(const char* name, const uint8_t* const* d_ptrs, const uint64_t* d_lens,
+                            uint32_t nstreams, uint64_t* d_cuts, uint64_t cuts_cap, const uint64_t* d_cut_base,
+                            uint64_t* d_counts, void* hip_stream);
+
+/* _host: host buffers in, host cut lists out (H2D + kernel + D2H through pinned
+ * staging, overlapped).  Synchronous.  This is the path the Go cgo shim calls
+ * (INTEGRATION.md). */
+int kcdc_split_batch_host(const char* name, const uint8_t* const* h_ptrs, const uint64_t* lens, uint32_t nstreams,
+                          uint64_t* cuts, uint64_t cuts_cap, const uint64_t* cut_base, uint64_t* counts, int device);
+
+/* ------------------------------------------- one long stream, tiled (config 3)
+ * Exact intra-stream parallel CDC of a single device-resident stream: candidate
+ * scan over all tiles in parallel, then chunk resolution on the device.  The
+ * cut set is identical to one sequential pass (no Concatenate seams; cf.
+ * snapshot/upload/upload.go:166-209, repo/object/object_manager.go:102-152).
+ * `workspace` must hold kcdc_long_workspace_bytes(name, len) bytes of device
+ * memory.  d_count receives the number of cuts written to d_cuts. */
+size_t kcdc_long_workspace_bytes(const char* name, uint64_t len);
+int kcdc_split_long_device(const char* name, const uint8_t* d_data, uint64_t len, uint64_t* d_cuts, uint64_t cuts_cap,
+                           uint64_t* d_count, void* workspace, size_t workspace_bytes, void* hip_stream);
+
+/* ------------------------------------------------- synthetic input (bench)
+ * Fill `nstreams` device streams of `stream_len` bytes each, laid out at
+ * d_data + i*stride, with the counter-PRNG bytes of stream id (first_sid + i)
+ * (bytes are a pure function of (seed, sid, offset); BASELINE.json configs 2-5). */
+int kcdc_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint32_t nstreams, uint64_t seed,
+                   uint64_t first_sid, void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KCDC_H */

@@ -1,0 +1,88 @@
+"""Loader for the native library ``kopia_amd/libkcdc.so`` (C ABI: include/kcdc.h).
+
+The library is built in-tree (``make`` or ``__graft_entry__.build()``).  There is
+no Python or CPU fallback: if the library is missing this module raises, and
+GPU entry points return KCDC_E* errors that the wrappers raise as exceptions.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from functools import lru_cache
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libkcdc.so")
+
+KCDC_OK = 0
+KCDC_ENOENT = -2
+KCDC_EIO = -5
+KCDC_ENOMEM = -12
+KCDC_ENODEV = -19
+KCDC_EINVAL = -22
+KCDC_EOVERFLOW = -75
+
+KIND_FIXED, KIND_BUZHASH, KIND_RABINKARP = 0, 1, 2
+
+
+class KcdcError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"kcdc error {code}: {msg}")
+        self.code = code
+
+
+class AlgoInfo(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("pooled", C.c_int32), ("avg", C.c_uint64), ("min_size", C.c_uint64),
+                ("max_size", C.c_uint64), ("mask", C.c_uint64)]
+
+
+_P = C.c_void_p
+_SIGS = {
+    "kcdc_last_error": (C.c_char_p, []),
+    "kcdc_version": (C.c_char_p, []),
+    "kcdc_device_count": (C.c_int, []),
+    "kcdc_supported_algorithms": (C.c_int, [C.POINTER(C.c_char_p), C.c_int]),
+    "kcdc_default_algorithm": (C.c_char_p, []),
+    "kcdc_lookup": (C.c_int, [C.c_char_p, C.POINTER(AlgoInfo)]),
+    "kcdc_max_segment_size": (C.c_int64, [C.c_char_p]),
+    "kcdc_cut_capacity": (C.c_uint64, [C.c_char_p, C.c_uint64]),
+    "kcdc_custom_algorithm": (C.c_char_p, [C.c_int32, C.c_uint64]),
+    "kcdc_tables": (C.c_int, [_P, _P, _P, _P]),
+    "kcdc_splitter_new": (_P, [C.c_char_p, C.c_int]),
+    "kcdc_splitter_next": (C.c_int64, [_P, _P, C.c_size_t]),
+    "kcdc_splitter_max_segment_size": (C.c_int64, [_P]),
+    "kcdc_splitter_reset": (None, [_P]),
+    "kcdc_splitter_close": (None, [_P]),
+    "kcdc_split_batch_device": (C.c_int, [C.c_char_p, _P, _P, C.c_uint32, _P, C.c_uint64, _P, _P, _P]),
+    "kcdc_split_batch_host": (C.c_int, [C.c_char_p, _P, _P, C.c_uint32, _P, C.c_uint64, _P, _P, C.c_int]),
+    "kcdc_long_workspace_bytes": (C.c_size_t, [C.c_char_p, C.c_uint64]),
+    "kcdc_split_long_device": (C.c_int, [C.c_char_p, _P, C.c_uint64, _P, C.c_uint64, _P, _P, C.c_size_t, _P]),
+    "kcdc_fill_prng": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, _P]),
+}
+
+
+@lru_cache(maxsize=1)
+def lib() -> C.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build()) first; "
+                          "there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
+def last_error() -> str:
+    msg = lib().kcdc_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int) -> int:
+    if rc < 0:
+        raise KcdcError(rc, last_error())
+    return rc
+
+
+def exported_symbols() -> list[str]:
+    return list(_SIGS)

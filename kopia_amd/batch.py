@@ -1,0 +1,91 @@
+"""Batch (hot-path) entry points over the C ABI, for device-resident torch tensors
+and for host buffers.  PyTorch is used only for device memory and streams."""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .splitter import cut_capacity
+
+
+@dataclass
+class DeviceBatch:
+    """Device-resident batch layout: streams at arbitrary device addresses."""
+    ptrs: "torch.Tensor"       # int64 [n] device pointers (on device)
+    lens: "torch.Tensor"       # int64 [n] (on device)
+    cut_base: "torch.Tensor"   # int64 [n] (on device)
+    cuts: "torch.Tensor"       # int64 [cap] (on device)
+    counts: "torch.Tensor"     # int64 [n] (on device)
+    cap: int
+    n: int
+
+
+def make_device_batch(name: str, ptr_list, len_list, device) -> DeviceBatch:
+    import torch
+    n = len(ptr_list)
+    caps = np.array([cut_capacity(name, int(L)) for L in len_list], dtype=np.int64)
+    base = np.zeros(n, dtype=np.int64)
+    if n > 1:
+        base[1:] = np.cumsum(caps)[:-1]
+    cap = int(caps.sum()) if n else 0
+    t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.int64)).to(device)
+    return DeviceBatch(ptrs=t(ptr_list), lens=t(len_list), cut_base=t(base),
+                       cuts=torch.zeros(max(cap, 1), dtype=torch.int64, device=device),
+                       counts=torch.zeros(max(n, 1), dtype=torch.int64, device=device), cap=cap, n=n)
+
+
+def split_batch_device(name: str, b: DeviceBatch, stream=None) -> None:
+    """Launch the splitter on the batch (asynchronous on `stream`, torch's current stream if None)."""
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream(b.cuts.device)
+    _lib.check(_lib.lib().kcdc_split_batch_device(
+        name.encode(), b.ptrs.data_ptr(), b.lens.data_ptr(), b.n, b.cuts.data_ptr(), b.cap,
+        b.cut_base.data_ptr(), b.counts.data_ptr(), C.c_void_p(stream.cuda_stream)))
+
+
+def read_cuts(b: DeviceBatch) -> list[np.ndarray]:
+    """Copy cut lists back (host); raises on capacity overflow."""
+    cuts = b.cuts.cpu().numpy()
+    counts = b.counts.cpu().numpy()[:b.n]
+    base = b.cut_base.cpu().numpy()
+    out = []
+    for i in range(b.n):
+        capi = (base[i + 1] if i + 1 < b.n else b.cap) - base[i]
+        if counts[i] > capi:
+            raise _lib.KcdcError(_lib.KCDC_EOVERFLOW, f"stream {i}: {counts[i]} cuts > capacity {capi}")
+        out.append(cuts[base[i]:base[i] + counts[i]].copy())
+    return out
+
+
+def split_batch_host(name: str, streams, device: int = 0) -> list[np.ndarray]:
+    """Host buffers in, cut lists out (H2D + kernel + D2H inside the library)."""
+    arrs = [np.frombuffer(s, dtype=np.uint8) if not isinstance(s, np.ndarray) else np.ascontiguousarray(s)
+            for s in streams]
+    n = len(arrs)
+    lens = np.array([a.size for a in arrs], dtype=np.uint64)
+    caps = np.array([cut_capacity(name, int(L)) for L in lens], dtype=np.uint64)
+    base = np.zeros(n, dtype=np.uint64)
+    if n > 1:
+        base[1:] = np.cumsum(caps)[:-1]
+    cap = int(caps.sum())
+    cuts = np.zeros(max(cap, 1), dtype=np.uint64)
+    counts = np.zeros(max(n, 1), dtype=np.uint64)
+    ptrs = (C.c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
+    _lib.check(_lib.lib().kcdc_split_batch_host(
+        name.encode(), C.cast(ptrs, C.c_void_p), lens.ctypes.data, n, cuts.ctypes.data, cap, base.ctypes.data,
+        counts.ctypes.data, device))
+    return [cuts[int(base[i]):int(base[i]) + int(counts[i])].astype(np.int64) for i in range(n)]
+
+
+def fill_prng(data: "torch.Tensor", stream_len: int, nstreams: int, stride: int, seed: int, first_sid: int = 0,
+              stream=None) -> None:
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream(data.device)
+    assert data.numel() * data.element_size() >= stride * (nstreams - 1) + stream_len
+    _lib.check(_lib.lib().kcdc_fill_prng(data.data_ptr(), stride, stream_len, nstreams, seed, first_sid,
+                                         C.c_void_p(stream.cuda_stream)))

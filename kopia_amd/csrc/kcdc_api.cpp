@@ -1,0 +1,441 @@
+// C ABI of libkcdc (include/kcdc.h): the drop-in boundary for Kopia's
+// repo/splitter package.  Host orchestration only; every byte of hashing runs
+// in the gfx950 kernels of kcdc_kernels.hip.  There is no CPU fallback.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/kcdc.h"
+#include "kcdc_internal.h"
+
+namespace kcdc {
+const char* last_error_cstr();
+}
+
+using namespace kcdc;
+
+namespace {
+
+int hip_err(hipError_t e, const char* what) { return set_error(KCDC_EIO, std::string(what) + ": " + hipGetErrorString(e)); }
+
+#define HIP_TRY(expr, what)                          \
+    do {                                             \
+        hipError_t e_ = (expr);                      \
+        if (e_ != hipSuccess) return hip_err(e_, what); \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+bool is_gfx950(int dev) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, dev) != hipSuccess) return false;
+    return std::strncmp(p.gcnArchName, "gfx950", 6) == 0;
+}
+
+int check_device(int dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return set_error(KCDC_ENODEV, "no HIP device visible");
+    if (dev < 0 || dev >= n) return set_error(KCDC_ENODEV, "device index out of range");
+    if (!is_gfx950(dev)) return set_error(KCDC_ENODEV, "device is not gfx950 (MI355X); kernels are gfx950-only");
+    return KCDC_OK;
+}
+
+}  // namespace
+
+// ======================================================= diagnostics / registry
+extern "C" const char* kcdc_last_error(void) { return kcdc::last_error_cstr(); }
+extern "C" const char* kcdc_version(void) { return "kcdc 0.1 (gfx950)"; }
+
+extern "C" int kcdc_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    int c = 0;
+    for (int i = 0; i < n; i++) c += is_gfx950(i) ? 1 : 0;
+    return c;
+}
+
+extern "C" int kcdc_supported_algorithms(const char** names, int cap) {
+    const int n = algo_count();
+    for (int i = 0; names && i < n && i < cap; i++) names[i] = algo_at(i).name;
+    return n;
+}
+
+extern "C" const char* kcdc_default_algorithm(void) { return "DYNAMIC-4M-BUZHASH"; }
+
+extern "C" int kcdc_lookup(const char* name, kcdc_algo_info* info) {
+    const Algo* a = find_algo(name);
+    if (!a) return set_error(KCDC_ENOENT, std::string("unknown splitter: ") + (name ? name : "(null)"));
+    if (info) {
+        info->kind = a->kind;
+        info->pooled = a->pooled ? 1 : 0;
+        info->avg = a->avg;
+        info->min_size = a->min_size();
+        info->max_size = a->max_size();
+        info->mask = a->mask();
+    }
+    return KCDC_OK;
+}
+
+extern "C" int64_t kcdc_max_segment_size(const char* name) {
+    const Algo* a = find_algo(name);
+    if (!a) return set_error(KCDC_ENOENT, std::string("unknown splitter: ") + (name ? name : "(null)"));
+    return static_cast<int64_t>(a->max_size());
+}
+
+extern "C" const char* kcdc_custom_algorithm(int32_t kind, uint64_t avg) {
+    const Algo* a = custom_algo(kind, avg);
+    if (!a) {
+        set_error(KCDC_EINVAL, "invalid custom splitter parameters");
+        return nullptr;
+    }
+    return a->name;
+}
+
+extern "C" uint64_t kcdc_cut_capacity(const char* name, uint64_t len) {
+    const Algo* a = find_algo(name);
+    if (!a) return 0;
+    return len / a->min_size() + 1;
+}
+
+extern "C" int kcdc_tables(uint32_t* buz, uint64_t* pol, uint64_t* out, uint64_t* mod) {
+    const Tables& t = tables();
+    if (buz) std::memcpy(buz, t.buz, sizeof(t.buz));
+    if (pol) *pol = t.rk_pol;
+    if (out) std::memcpy(out, t.rk_out, sizeof(t.rk_out));
+    if (mod) std::memcpy(mod, t.rk_mod, sizeof(t.rk_mod));
+    return KCDC_OK;
+}
+
+// ============================================================ streaming handle
+struct kcdc_splitter {
+    const Algo* algo = nullptr;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int64_t count = 0;              // rs.count (rolling) / s.cur (fixed)
+    uint8_t hist[kWindow] = {0};    // last 64 stream bytes (zeros before the start)
+    uint8_t* h_stage = nullptr;     // pinned: hist || slice
+    uint8_t* d_stage = nullptr;
+    size_t stage_cap = 0;
+    int64_t* d_out = nullptr;
+    int64_t* h_out = nullptr;
+};
+
+namespace {
+
+struct Pool {
+    std::mutex mu;
+    std::vector<kcdc_splitter*> free;
+};
+Pool g_pools[64];
+
+void push_hist(kcdc_splitter* s, const uint8_t* b, size_t n) {
+    if (n >= static_cast<size_t>(kWindow)) {
+        std::memcpy(s->hist, b + n - kWindow, kWindow);
+    } else if (n > 0) {
+        std::memmove(s->hist, s->hist + n, kWindow - n);
+        std::memcpy(s->hist + kWindow - n, b, n);
+    }
+}
+
+void destroy(kcdc_splitter* s) {
+    if (!s) return;
+    DeviceGuard g(s->device);
+    if (s->d_stage) (void)hipFree(s->d_stage);
+    if (s->h_stage) (void)hipHostFree(s->h_stage);
+    if (s->d_out) (void)hipFree(s->d_out);
+    if (s->h_out) (void)hipHostFree(s->h_out);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+}
+
+int ensure_stage(kcdc_splitter* s, size_t need) {
+    if (need <= s->stage_cap) return KCDC_OK;
+    size_t cap = std::max<size_t>(need, 1 << 20);
+    cap = std::min<size_t>(std::max(cap, s->stage_cap * 2), s->algo->max_size() + 2 * kWindow);
+    cap = std::max(cap, need);
+    if (s->d_stage) (void)hipFree(s->d_stage);
+    if (s->h_stage) (void)hipHostFree(s->h_stage);
+    s->d_stage = nullptr;
+    s->h_stage = nullptr;
+    s->stage_cap = 0;
+    HIP_TRY(hipMalloc(&s->d_stage, cap), "hipMalloc stage");
+    HIP_TRY(hipHostMalloc(&s->h_stage, cap, hipHostMallocDefault), "hipHostMalloc stage");
+    s->stage_cap = cap;
+    return KCDC_OK;
+}
+
+// First candidate index in slice b[0..n) given the 64-byte history, on the GPU.
+int64_t gpu_first_candidate(kcdc_splitter* s, const uint8_t* b, size_t n) {
+    const size_t total = kWindow + n;
+    int rc = ensure_stage(s, total);
+    if (rc) return rc;
+    std::memcpy(s->h_stage, s->hist, kWindow);
+    std::memcpy(s->h_stage + kWindow, b, n);
+    HIP_TRY(hipMemcpyAsync(s->d_stage, s->h_stage, total, hipMemcpyHostToDevice, s->stream), "H2D slice");
+    rc = launch_scan_first(*s->algo, s->d_stage, total, kWindow, static_cast<int64_t>(total) - 1, s->d_out, s->device,
+                           s->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(s->h_out, s->d_out, sizeof(int64_t), hipMemcpyDeviceToHost, s->stream), "D2H result");
+    HIP_TRY(hipStreamSynchronize(s->stream), "scan sync");
+    const int64_t f = s->h_out[0];
+    return f < 0 ? -1 : f - kWindow;
+}
+
+}  // namespace
+
+extern "C" kcdc_splitter* kcdc_splitter_new(const char* name, int device) {
+    const Algo* a = find_algo(name);
+    if (!a) {
+        set_error(KCDC_ENOENT, std::string("unknown splitter: ") + (name ? name : "(null)"));
+        return nullptr;
+    }
+    if (a->kind != kFixed && check_device(device) != KCDC_OK) return nullptr;
+    const int idx = algo_index(a);
+    if (a->pooled && idx >= 0) {  // pooled(): reuse a Reset splitter (splitter_pool.go:24-30)
+        Pool& p = g_pools[idx];
+        std::lock_guard<std::mutex> lk(p.mu);
+        for (size_t i = 0; i < p.free.size(); i++) {
+            if (p.free[i]->device == device) {
+                kcdc_splitter* s = p.free[i];
+                p.free.erase(p.free.begin() + static_cast<long>(i));
+                return s;
+            }
+        }
+    }
+    kcdc_splitter* s = new kcdc_splitter();
+    s->algo = a;
+    s->device = device;
+    if (a->kind != kFixed) {
+        DeviceGuard g(device);
+        int err = 0;
+        if (!device_tables(device, &err) || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+            hipMalloc(&s->d_out, sizeof(int64_t)) != hipSuccess ||
+            hipHostMalloc(&s->h_out, sizeof(int64_t), hipHostMallocDefault) != hipSuccess) {
+            if (!err) set_error(KCDC_EIO, "failed to allocate splitter device resources");
+            destroy(s);
+            return nullptr;
+        }
+    }
+    return s;
+}
+
+extern "C" int64_t kcdc_splitter_next(kcdc_splitter* s, const uint8_t* b, size_t len) {
+    if (!s) return set_error(KCDC_EINVAL, "null splitter");
+    if (len > 0 && !b) return set_error(KCDC_EINVAL, "null buffer");
+    const Algo& A = *s->algo;
+    const int64_t n = static_cast<int64_t>(len);
+    if (A.kind == kFixed) {  // splitter_fixed.go:15-26 (reads no data)
+        const int64_t need = static_cast<int64_t>(A.avg) - s->count;
+        if (n < need) {
+            s->count += n;
+            return -1;
+        }
+        s->count = 0;
+        return need;
+    }
+    DeviceGuard g(s->device);
+    const int64_t mn = static_cast<int64_t>(A.min_size()), mx = static_cast<int64_t>(A.max_size());
+    int64_t fast = 0;
+    const uint8_t* p = b;
+    int64_t rest = n;
+    int64_t left = mn - s->count - 1;
+    if (left > 0) {  // :29-40 below min size no position is tested; only the window moves
+        fast = std::min(left, rest);
+        push_hist(s, p, static_cast<size_t>(fast));
+        s->count += fast;
+        p += fast;
+        rest -= fast;
+    }
+    left = mx - s->count;
+    if (left > 0) {  // :42-58 test positions on the GPU
+        const int64_t fp = std::min(left, rest);
+        if (fp > 0) {
+            const int64_t f = gpu_first_candidate(s, p, static_cast<size_t>(fp));
+            if (f < -1) return f;  // error code
+            if (f >= 0) {
+                push_hist(s, p, static_cast<size_t>(f + 1));
+                s->count = 0;
+                return fast + f + 1;
+            }
+            push_hist(s, p, static_cast<size_t>(fp));
+            s->count += fp;
+            fast += fp;
+        }
+    }
+    if (s->count >= mx) {  // :60-64
+        s->count = 0;
+        return fast;
+    }
+    return -1;
+}
+
+extern "C" int64_t kcdc_splitter_max_segment_size(const kcdc_splitter* s) {
+    return s ? static_cast<int64_t>(s->algo->max_size()) : KCDC_EINVAL;
+}
+
+extern "C" void kcdc_splitter_reset(kcdc_splitter* s) {
+    if (!s) return;
+    s->count = 0;
+    std::memset(s->hist, 0, sizeof s->hist);
+}
+
+extern "C" void kcdc_splitter_close(kcdc_splitter* s) {
+    if (!s) return;
+    kcdc_splitter_reset(s);  // recyclableSplitter.Close: Reset, then pool.Put
+    if (s->algo->pooled && algo_index(s->algo) >= 0) {
+        Pool& p = g_pools[algo_index(s->algo)];
+        std::lock_guard<std::mutex> lk(p.mu);
+        p.free.push_back(s);
+        return;
+    }
+    destroy(s);
+}
+
+// ==================================================================== batch
+extern "C" int kcdc_split_batch_device(const char* name, const uint8_t* const* d_ptrs, const uint64_t* d_lens,
+                                       uint32_t nstreams, uint64_t* d_cuts, uint64_t cuts_cap,
+                                       const uint64_t* d_cut_base, uint64_t* d_counts, void* stream) {
+    const Algo* a = find_algo(name);
+    if (!a) return set_error(KCDC_ENOENT, std::string("unknown splitter: ") + (name ? name : "(null)"));
+    if (nstreams == 0) return KCDC_OK;
+    if (!d_ptrs || !d_lens || !d_cuts || !d_cut_base || !d_counts) return set_error(KCDC_EINVAL, "null argument");
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    int rc = check_device(dev);
+    if (rc) return rc;
+    SplitArgs s{d_ptrs, d_lens, nstreams, d_cuts, cuts_cap, d_cut_base, d_counts};
+    return launch_split_batch(*a, s, dev, stream);
+}
+
+namespace {
+struct HostCtx {
+    std::mutex mu;
+    uint8_t* d_data = nullptr;
+    size_t d_data_cap = 0;
+    void* d_meta = nullptr;
+    size_t d_meta_cap = 0;
+    hipStream_t stream = nullptr;
+};
+HostCtx g_host[64];
+
+int grow(void** p, size_t* cap, size_t need) {
+    if (need <= *cap) return KCDC_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    HIP_TRY(hipMalloc(p, need), "hipMalloc");
+    *cap = need;
+    return KCDC_OK;
+}
+}  // namespace
+
+extern "C" int kcdc_split_batch_host(const char* name, const uint8_t* const* h_ptrs, const uint64_t* lens,
+                                     uint32_t nstreams, uint64_t* cuts, uint64_t cuts_cap, const uint64_t* cut_base,
+                                     uint64_t* counts, int device) {
+    const Algo* a = find_algo(name);
+    if (!a) return set_error(KCDC_ENOENT, std::string("unknown splitter: ") + (name ? name : "(null)"));
+    if (nstreams == 0) return KCDC_OK;
+    if (!h_ptrs || !lens || !cuts || !cut_base || !counts) return set_error(KCDC_EINVAL, "null argument");
+    int rc = check_device(device);
+    if (rc) return rc;
+    DeviceGuard g(device);
+    HostCtx& C = g_host[device];
+    std::lock_guard<std::mutex> lk(C.mu);
+    if (!C.stream) HIP_TRY(hipStreamCreateWithFlags(&C.stream, hipStreamNonBlocking), "hipStreamCreate");
+    // Groups of streams whose bytes fit a 1 GiB device arena (a stream larger than
+    // that gets an arena of its own size).
+    const size_t kArena = size_t(1) << 30;
+    uint32_t i0 = 0;
+    while (i0 < nstreams) {
+        uint32_t i1 = i0;
+        size_t bytes = 0;
+        while (i1 < nstreams) {
+            const size_t sz = (lens[i1] + 255) & ~size_t(255);
+            if (i1 > i0 && bytes + sz > kArena) break;
+            bytes += sz;
+            i1++;
+        }
+        const uint32_t ng = i1 - i0;
+        uint64_t gcap = (i1 < nstreams ? cut_base[i1] : cuts_cap) - cut_base[i0];
+        rc = grow(reinterpret_cast<void**>(&C.d_data), &C.d_data_cap, std::max<size_t>(bytes, 256));
+        if (rc) return rc;
+        const size_t meta = ng * (sizeof(void*) + 3 * sizeof(uint64_t)) + gcap * sizeof(uint64_t) + 64;
+        rc = grow(&C.d_meta, &C.d_meta_cap, meta);
+        if (rc) return rc;
+        std::vector<const uint8_t*> dptr(ng);
+        std::vector<uint64_t> base(ng);
+        size_t off = 0;
+        for (uint32_t k = 0; k < ng; k++) {
+            dptr[k] = C.d_data + off;
+            base[k] = cut_base[i0 + k] - cut_base[i0];
+            if (lens[i0 + k])
+                HIP_TRY(hipMemcpyAsync(C.d_data + off, h_ptrs[i0 + k], lens[i0 + k], hipMemcpyHostToDevice, C.stream),
+                        "H2D stream");
+            off += (lens[i0 + k] + 255) & ~size_t(255);
+        }
+        char* m = static_cast<char*>(C.d_meta);
+        auto* d_ptrs = reinterpret_cast<const uint8_t**>(m);
+        auto* d_lens = reinterpret_cast<uint64_t*>(m + ng * sizeof(void*));
+        auto* d_base = d_lens + ng;
+        auto* d_cnt = d_base + ng;
+        auto* d_cuts = d_cnt + ng;
+        HIP_TRY(hipMemcpyAsync(d_ptrs, dptr.data(), ng * sizeof(void*), hipMemcpyHostToDevice, C.stream), "H2D meta");
+        HIP_TRY(hipMemcpyAsync(d_lens, lens + i0, ng * sizeof(uint64_t), hipMemcpyHostToDevice, C.stream), "H2D meta");
+        HIP_TRY(hipMemcpyAsync(d_base, base.data(), ng * sizeof(uint64_t), hipMemcpyHostToDevice, C.stream), "H2D meta");
+        SplitArgs s{d_ptrs, d_lens, ng, d_cuts, gcap, d_base, d_cnt};
+        rc = launch_split_batch(*a, s, device, C.stream);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(counts + i0, d_cnt, ng * sizeof(uint64_t), hipMemcpyDeviceToHost, C.stream), "D2H");
+        if (gcap)
+            HIP_TRY(hipMemcpyAsync(cuts + cut_base[i0], d_cuts, gcap * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                   C.stream),
+                    "D2H cuts");
+        HIP_TRY(hipStreamSynchronize(C.stream), "sync");
+        for (uint32_t k = i0; k < i1; k++) {
+            const uint64_t capk = (k + 1 < nstreams ? cut_base[k + 1] : cuts_cap) - cut_base[k];
+            if (counts[k] > capk) return set_error(KCDC_EOVERFLOW, "cut capacity too small for a stream");
+        }
+        i0 = i1;
+    }
+    return KCDC_OK;
+}
+
+// ================================================================ long stream
+extern "C" size_t kcdc_long_workspace_bytes(const char* name, uint64_t len) {
+    const Algo* a = find_algo(name);
+    return a ? long_workspace_bytes(*a, len) : 0;
+}
+
+extern "C" int kcdc_split_long_device(const char* name, const uint8_t* d_data, uint64_t len, uint64_t* d_cuts,
+                                      uint64_t cuts_cap, uint64_t* d_count, void* ws, size_t ws_bytes, void* stream) {
+    const Algo* a = find_algo(name);
+    if (!a) return set_error(KCDC_ENOENT, std::string("unknown splitter: ") + (name ? name : "(null)"));
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    int rc = check_device(dev);
+    if (rc) return rc;
+    return launch_split_long(*a, d_data, len, d_cuts, cuts_cap, d_count, ws, ws_bytes, dev, stream);
+}
+
+// =================================================================== data
+extern "C" int kcdc_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint32_t nstreams, uint64_t seed,
+                              uint64_t first_sid, void* stream) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    int rc = check_device(dev);
+    if (rc) return rc;
+    return launch_fill_prng(d_data, stride, stream_len, nstreams, seed, first_sid, stream);
+}

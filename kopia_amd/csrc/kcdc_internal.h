@@ -1,0 +1,68 @@
+// Internal declarations shared by the kcdc host code and the HIP kernels.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+namespace kcdc {
+
+constexpr int kWindow = 64;  // splitterSlidingWindowSize, repo/splitter/splitter.go:9
+
+struct Tables {
+    uint32_t buz[256];      // rollinghash buzhash32 byte table (GenerateHashes(1))
+    uint64_t rk_pol = 0;    // rollinghash rabinkarp64 polynomial (RandomPolynomial(1))
+    int rk_shift = 0;       // deg(P) - 8
+    uint64_t rk_out[256];   // b * x^(8*63) mod P
+    uint64_t rk_mod[256];   // (b * x^deg mod P) | (b << deg)
+};
+const Tables& tables();
+
+enum Kind : int32_t { kFixed = 0, kBuzhash = 1, kRabinKarp = 2 };
+
+struct Algo {
+    const char* name;
+    Kind kind;
+    bool pooled;
+    uint64_t avg;
+    uint64_t min_size() const { return kind == kFixed ? avg : avg / 2; }
+    uint64_t max_size() const { return kind == kFixed ? avg : avg * 2; }
+    uint64_t mask() const { return kind == kFixed ? 0 : avg - 1; }
+};
+// Registry lookup (repo/splitter/splitter.go:50-86); nullptr if unknown.
+const Algo* find_algo(const char* name);
+int algo_count();
+const Algo* custom_algo(int32_t kind, uint64_t avg);  // interned, nullptr if invalid
+int algo_index(const Algo* a);                         // registry index, -1 for custom
+const Algo& algo_at(int i);  // sorted by name
+
+// Thread-local error reporting.
+int set_error(int code, const std::string& msg);
+
+// ---- kernel launchers (kcdc_kernels.hip) ----
+struct DeviceTables;  // per-device copies of the hash tables
+const DeviceTables* device_tables(int device, int* err);
+
+struct SplitArgs {
+    const uint8_t* const* ptrs;
+    const uint64_t* lens;
+    uint32_t nstreams;
+    uint64_t* cuts;
+    uint64_t cuts_cap;
+    const uint64_t* cut_base;
+    uint64_t* counts;
+};
+// Launch the batch splitter for `algo` on `stream` (hipStream_t as void*).
+int launch_split_batch(const Algo& algo, const SplitArgs& a, int device, void* stream);
+// Single-region first-candidate scan used by the streaming handle:
+// bytes [0, len) of `d_buf` are the stream, positions < 0 are zero; returns via
+// d_out[0] the first candidate position in [lo, hi] or -1.
+int launch_scan_first(const Algo& algo, const uint8_t* d_buf, uint64_t len, int64_t lo, int64_t hi, int64_t* d_out,
+                      int device, void* stream);
+int launch_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint32_t nstreams, uint64_t seed,
+                     uint64_t first_sid, void* stream);
+size_t long_workspace_bytes(const Algo& algo, uint64_t len);
+int launch_split_long(const Algo& algo, const uint8_t* d_data, uint64_t len, uint64_t* d_cuts, uint64_t cuts_cap,
+                      uint64_t* d_count, void* ws, size_t ws_bytes, int device, void* stream);
+
+}  // namespace kcdc

@@ -1,0 +1,623 @@
+// MI355X (gfx950) kernels for Kopia's content-defined-chunking splitters.
+//
+// Reference semantics (bit-exact):
+//   buzhash32Splitter.NextSplitPoint   repo/splitter/splitter_buzhash32.go:26-67
+//   rabinKarp64Splitter.NextSplitPoint repo/splitter/splitter_rabinkarp64.go:26-67
+//   fixedSplitter.NextSplitPoint       repo/splitter/splitter_fixed.go:15-26
+//
+// Key identity: the rolling hash is never reset inside a
+// stream and always equals the hash of the 64 bytes ending at the current
+// position (zero bytes before the stream start).  So cand(p) := hash(p) & mask
+// == 0 is a pure function of bytes p-63..p, and the chunk rule is: from chunk
+// start s, cut after the first p in [s+min-1, s+max-1] with cand(p), else after
+// s+max-1.  The reference's fast path (only the last 64 of the first min-1
+// bytes are rolled) becomes "start scanning at s+min-64": bytes before that are
+// never read.
+//
+// Work decomposition — one wavefront per stream:
+//   the wave walks the stream chunk by chunk; for the current chunk it scans the
+//   test region [s+min-1, s+max-1] in TILES of 64 lanes x L bytes.  Lane l owns
+//   the L-byte segment l of the tile and warms its hash up on the 64 bytes before
+//   it, so all 64 lanes hash independently.  Per byte: one v_perm (table
+//   address), one LDS table read (the 1 KiB buzhash table is replicated 64x so
+//   lane l always hits bank l%32: conflict-free), one v_alignbit (rotl 1), one
+//   v_xor3 and the candidate test folded into a running min.  The outgoing byte's
+//   table value comes from a 64-entry register ring (the loop is unrolled by 64
+//   so the ring index is static).  A block whose running min is 0 is re-run in
+//   exact mode to find the first candidate; the earliest lane with a candidate
+//   (ballot + ffs) gives the tile's first candidate.
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <string>
+
+#include "kcdc_internal.h"
+
+namespace kcdc {
+namespace dev {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+constexpr int kWavesPerWG = 8;        // 512 threads; 16 waves/CU at 2 WGs/CU
+constexpr int64_t kLaneMax = 1024;    // max bytes per lane segment (tile = 64 KiB)
+
+#ifndef KCDC_SCHED_WINDOW
+#define KCDC_SCHED_WINDOW 16
+#endif
+constexpr int kSchedWindow = KCDC_SCHED_WINDOW;  // bytes per scheduling window in the hash loop
+
+enum Mode { kWarm = 0, kFast = 1, kExact = 2 };
+
+__device__ __forceinline__ uint32_t rotl1(uint32_t h) { return __builtin_amdgcn_alignbit(h, h, 31); }
+
+__device__ __forceinline__ uint32_t ufirst(uint64_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x >> 32));
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// Byte i of a 64-byte block held as 16 dwords.
+__device__ __forceinline__ uint32_t byte_at(const uint32_t (&dw)[16], int i) {
+    return __builtin_amdgcn_perm(0u, dw[i >> 2], 0x0c0c0c00u | static_cast<uint32_t>(i & 3));
+}
+
+// ---------------------------------------------------------------- loaders
+// A stream is addressed in "coordinates" c = position + off0 relative to the
+// 16-byte-aligned base `abase`; coordinates < off0 are the virtual zero bytes
+// before the stream start.  Loads go through a buffer descriptor whose range
+// check returns zeros for out-of-range (including negative) offsets.
+struct Loader {
+    __amdgpu_buffer_rsrc_t rsrc;
+    int64_t tb;    // coordinate of descriptor offset 0
+    int64_t off0;  // stream misalignment (0..15)
+
+    __device__ __forceinline__ void load(int64_t c, uint32_t (&dw)[16]) const {
+        const int32_t vo = static_cast<int32_t>(c - tb);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo + 16 * j, 0, 0);
+            dw[4 * j + 0] = v.x;
+            dw[4 * j + 1] = v.y;
+            dw[4 * j + 2] = v.z;
+            dw[4 * j + 3] = v.w;
+        }
+        if (c == 0 && off0) {  // zero the bytes that precede the stream in its first granule
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                const int64_t keep_from = off0 - 4 * d;  // first byte of dword d to keep
+                uint32_t m = keep_from <= 0 ? 0xFFFFFFFFu : (keep_from >= 4 ? 0u : (0xFFFFFFFFu << (8 * keep_from)));
+                dw[d] &= m;
+            }
+        }
+    }
+};
+
+__device__ __forceinline__ Loader make_loader(const uint8_t* abase, int64_t off0, int64_t nbytes_coord, int64_t tb) {
+    // tb >= 0 and a multiple of 16; the descriptor covers [tb, round_up16(nbytes_coord)).
+    int64_t nrec = ((nbytes_coord + 15) & ~int64_t(15)) - tb;
+    if (nrec > 0x7FFFFF00ll) nrec = 0x7FFFFF00ll;
+    if (nrec < 0) nrec = 0;
+    Loader L;
+    L.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(abase + tb), static_cast<short>(0),
+                                               static_cast<int>(nrec), 0x00020000);
+    L.tb = tb;
+    L.off0 = off0;
+    return L;
+}
+
+// ------------------------------------------------------------------ hashes
+// buzhash32: h(p) = rotl(h(p-1),1) ^ T[b[p-64]] ^ T[b[p]]  (rollinghash Roll with
+// window 64: rotl(T[leave], 64 % 32 = 0)).
+struct BuzShared {
+    uint32_t tab[256 * 64];  // tab[v*64 + r] = T[v]  (64 KiB, replica r read by lane r)
+};
+
+struct Buz {
+    const char* tab;  // LDS byte address of BuzShared::tab
+    uint32_t lane4;
+    uint32_t mask;
+    uint32_t h;
+    uint32_t prev[16];  // bytes of the previous block (the bytes leaving the window)
+    using State = uint32_t;
+    __device__ __forceinline__ State save() const { return h; }
+    __device__ __forceinline__ void restore(State s) { h = s; }
+
+    __device__ __forceinline__ uint32_t look(uint32_t dwv, int k) const {
+        // (byte_k << 8) | lane*4 in one v_perm: byte 0 from lane4, byte 1 = data byte k.
+        const uint32_t a = __builtin_amdgcn_perm(dwv, lane4, 0x0c0c0000u | ((4u + k) << 8));
+        return *reinterpret_cast<const uint32_t*>(tab + a);
+    }
+    __device__ __forceinline__ void clear() {
+        h = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) prev[i] = 0;
+    }
+    __device__ __forceinline__ void set_ring(const uint32_t (&p)[16]) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) prev[i] = p[i];
+    }
+    // kWarm: no test; kFast: returns min over the block of (h & mask) (0 => some
+    // position may be a candidate); kExact: index of the first i in [lo, hi] with
+    // (h & mask) == 0, else 64.
+    template <int MODE>
+    __device__ __forceinline__ uint32_t block(const uint32_t (&dw)[16], int lo, int hi) {
+        uint32_t m = 0xFFFFFFFFu, first = 64;
+#pragma unroll
+        for (int i = 0; i < 64; i++) {
+            if (kSchedWindow && i % kSchedWindow == 0) __builtin_amdgcn_sched_barrier(0);
+            // kWarm runs on a zero "previous block": T[0] terms are skipped there, which is
+            // exactly the G-recurrence warm-up (the window before is never reached).
+            const uint32_t to = MODE == kWarm ? 0u : look(prev[i >> 2], i & 3);
+            const uint32_t ti = look(dw[i >> 2], i & 3);
+            h = rotl1(h) ^ to ^ ti;
+            if (MODE == kFast) {
+                m = min(m, h & mask);
+                // Pin the running min every 4 bytes: otherwise the compiler re-associates the
+                // min into a tree at the block end and keeps all 64 hashes live (VGPR blow-up).
+                if ((i & 3) == 3) asm volatile("" : "+v"(m));
+            }
+            if (MODE == kExact) {
+                if (first == 64 && (h & mask) == 0 && i >= lo && i <= hi) first = i;
+                if ((i & 3) == 3) asm volatile("" : "+v"(first));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) prev[i] = dw[i];
+        return MODE == kFast ? m : first;
+    }
+    // Exact re-run of one block from state st0 (rare path, compact rolled loop):
+    // index of the first i in [lo, hi] with (h & mask) == 0, else 64.
+    __device__ __forceinline__ uint32_t exact(State st0, const uint32_t (&prv)[16],
+                                                        const uint32_t (&dw)[16], int lo, int hi) const {
+        uint32_t e[16], o[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) { e[j] = dw[j]; o[j] = prv[j]; }
+        uint32_t hh = st0, first = 64;
+#pragma unroll 1
+        for (int j = 0; j < 16; j++) {
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                hh = rotl1(hh) ^ look(o[0], b) ^ look(e[0], b);
+                const int i = 4 * j + b;
+                if (first == 64 && (hh & mask) == 0 && i >= lo && i <= hi) first = static_cast<uint32_t>(i);
+            }
+#pragma unroll
+            for (int k = 0; k < 15; k++) { e[k] = e[k + 1]; o[k] = o[k + 1]; }
+        }
+        return first;
+    }
+};
+
+// rabinkarp64: v ^= out[b[p-64]]; idx = v >> shift; v = (v << 8 | b[p]) ^ mod[idx].
+struct RabinShared {
+    uint64_t out[256];
+    uint64_t mod[256];
+};
+
+struct Rabin {
+    const RabinShared* tab;
+    uint32_t mask;
+    uint32_t shift;
+    uint64_t v;
+    uint32_t prev[16];  // bytes of the previous block (the bytes leaving the window)
+    using State = uint64_t;
+    __device__ __forceinline__ State save() const { return v; }
+    __device__ __forceinline__ void restore(State s) { v = s; }
+
+    __device__ __forceinline__ void clear() {
+        v = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) prev[i] = 0;
+    }
+    __device__ __forceinline__ void set_ring(const uint32_t (&p)[16]) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) prev[i] = p[i];
+    }
+    template <int MODE>
+    __device__ __forceinline__ uint32_t block(const uint32_t (&dw)[16], int lo, int hi) {
+        uint32_t m = 0xFFFFFFFFu, first = 64;
+#pragma unroll
+        for (int i = 0; i < 64; i++) {
+            const uint32_t bo = byte_at(prev, i);
+            const uint32_t bi = byte_at(dw, i);
+            uint64_t x = v ^ tab->out[bo];
+            const uint32_t idx = static_cast<uint32_t>(x >> shift) & 0xFFu;
+            x = (x << 8) | bi;
+            v = x ^ tab->mod[idx];
+            const uint32_t lv = static_cast<uint32_t>(v) & mask;
+            if (MODE == kFast) {
+                m = min(m, lv);
+                if ((i & 3) == 3) asm volatile("" : "+v"(m));
+            }
+            if (MODE == kExact) {
+                if (first == 64 && lv == 0 && i >= lo && i <= hi) first = i;
+                if ((i & 3) == 3) asm volatile("" : "+v"(first));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) prev[i] = dw[i];
+        return MODE == kFast ? m : first;
+    }
+    __device__ __forceinline__ uint32_t exact(State st0, const uint32_t (&prv)[16],
+                                                        const uint32_t (&dw)[16], int lo, int hi) const {
+        uint32_t e[16], o[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) { e[j] = dw[j]; o[j] = prv[j]; }
+        uint64_t vv = st0;
+        uint32_t first = 64;
+#pragma unroll 1
+        for (int j = 0; j < 16; j++) {
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                uint64_t x = vv ^ tab->out[(o[0] >> (8 * b)) & 0xFFu];
+                const uint32_t idx = static_cast<uint32_t>(x >> shift) & 0xFFu;
+                x = (x << 8) | ((e[0] >> (8 * b)) & 0xFFu);
+                vv = x ^ tab->mod[idx];
+                const int i = 4 * j + b;
+                if (first == 64 && (static_cast<uint32_t>(vv) & mask) == 0 && i >= lo && i <= hi)
+                    first = static_cast<uint32_t>(i);
+            }
+#pragma unroll
+            for (int k = 0; k < 15; k++) { e[k] = e[k + 1]; o[k] = o[k + 1]; }
+        }
+        return first;
+    }
+};
+
+// --------------------------------------------------------- region scanner
+// First candidate coordinate in [lo, hi] (inclusive, lo <= hi), or -1.
+// Wave-uniform in and out.  `H` is a prepared hash (tables + mask), copied per tile.
+template <class H>
+__device__ int64_t scan_region(H hash, const uint8_t* abase, int64_t off0, int64_t nbytes_coord, int64_t lo,
+                               int64_t hi, int lane) {
+    int64_t ct = lo & ~int64_t(63);
+    while (ct <= hi) {
+        const int64_t rem = hi - ct + 1;
+        int64_t per = (rem + kWave - 1) / kWave;
+        per = (per + 63) & ~int64_t(63);
+        const int64_t L = per < kLaneMax ? per : kLaneMax;
+        const int64_t tb = ct >= 64 ? ct - 64 : 0;
+        const Loader ld = make_loader(abase, off0, nbytes_coord, tb);
+
+        const int64_t c0 = ct + lane * L;
+        const int nb = static_cast<int>(L >> 6);
+        int64_t found = -1;
+        if (c0 <= hi) {
+            uint32_t cur[16], nxt[16];
+            hash.clear();
+            ld.load(c0 - 64, cur);
+            hash.template block<kWarm>(cur, 0, 0);  // 64-byte warm-up: h = hash of the window before c0
+            ld.load(c0, cur);
+            int k = 0;
+            for (;;) {
+                // fast scan: running min of (h & mask) per 64-byte block
+                bool hit = false;
+                typename H::State st0 = hash.save();
+                for (; k < nb; k++) {
+                    if (c0 + 64 * k > hi) break;
+#ifndef KCDC_EXP_NOPREFETCH
+                    if (k + 1 < nb) ld.load(c0 + 64 * (k + 1), nxt);
+#else
+                    ld.load(c0 + 64 * (k + 1), nxt);
+#endif
+                    st0 = hash.save();
+                    if (hash.template block<kFast>(cur, 0, 63) == 0) {
+                        hit = true;
+                        break;
+                    }
+#pragma unroll
+                    for (int i = 0; i < 16; i++) cur[i] = nxt[i];
+                }
+                if (!hit) break;
+#ifdef KCDC_EXP_NOEXACT
+                found = c0 + 64 * k; break;
+#endif
+                // rare: re-run block k exactly, in place (ends in the same state)
+                const int64_t c = c0 + 64 * k;
+                uint32_t prv[16];
+                ld.load(c - 64, prv);
+                const int64_t blo = lo - c, bhi = hi - c;
+                const uint32_t idx = hash.exact(st0, prv, cur, blo < 0 ? 0 : static_cast<int>(blo),
+                                                bhi > 63 ? 63 : static_cast<int>(bhi));
+                if (idx < 64) {
+                    found = c + idx;
+                    break;
+                }
+                if (++k >= nb) break;
+                ld.load(c0 + 64 * k, cur);
+            }
+        }
+        const uint64_t hit = __ballot(found >= 0);
+        if (hit) {
+            const int first = __builtin_ctzll(hit);
+            return uni64(static_cast<uint64_t>(__shfl(found, first)));
+        }
+        ct += kWave * L;
+    }
+    return -1;
+}
+
+
+// ------------------------------------------------------------ batch kernel
+struct BatchArgs {
+    const uint8_t* const* ptrs;
+    const uint64_t* lens;
+    uint64_t* cuts;
+    const uint64_t* cut_base;
+    uint64_t* counts;
+    uint64_t cuts_cap;
+    uint64_t min_size, max_size;
+    const uint32_t* buz;
+    const uint64_t* rk_out;
+    const uint64_t* rk_mod;
+    uint32_t nstreams;
+    uint32_t mask;
+    uint32_t rk_shift;
+};
+
+template <int KIND>
+struct HashSmem;
+template <>
+struct HashSmem<kBuzhash> {
+    BuzShared s;
+};
+template <>
+struct HashSmem<kRabinKarp> {
+    RabinShared s;
+};
+
+template <int KIND>
+__device__ __forceinline__ void fill_tables(HashSmem<KIND>& sm, const BatchArgs& a) {
+    if constexpr (KIND == kBuzhash) {
+        for (uint32_t i = threadIdx.x; i < 256u * 64u; i += blockDim.x) sm.s.tab[i] = a.buz[i >> 6];
+    } else {
+        for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) {
+            sm.s.out[i] = a.rk_out[i];
+            sm.s.mod[i] = a.rk_mod[i];
+        }
+    }
+    __syncthreads();
+}
+
+template <int KIND>
+__device__ __forceinline__ auto make_hash(HashSmem<KIND>& sm, const BatchArgs& a, int lane) {
+    if constexpr (KIND == kBuzhash) {
+        Buz h;
+        h.tab = reinterpret_cast<const char*>(sm.s.tab);
+        h.lane4 = static_cast<uint32_t>(lane) * 4u;
+        h.mask = a.mask;
+        h.h = 0;
+        return h;
+    } else {
+        Rabin h;
+        h.tab = &sm.s;
+        h.mask = a.mask;
+        h.shift = a.rk_shift;
+        h.v = 0;
+        return h;
+    }
+}
+
+// One wavefront per stream: walk the stream chunk by chunk.
+template <int KIND>
+__global__ __launch_bounds__(kWavesPerWG * kWave, 4) void split_batch_kernel(BatchArgs a) {
+    __shared__ HashSmem<KIND> sm;
+    fill_tables<KIND>(sm, a);
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint32_t sid = blockIdx.x * kWavesPerWG + wave;
+    if (sid >= a.nstreams) return;
+
+    const uint64_t p = uni64(reinterpret_cast<uint64_t>(a.ptrs[sid]));
+    const int64_t n = static_cast<int64_t>(uni64(a.lens[sid]));
+    const uint64_t cb = uni64(a.cut_base[sid]);
+    const uint64_t cend = sid + 1 < a.nstreams ? uni64(a.cut_base[sid + 1]) : a.cuts_cap;
+    const uint64_t cap = cend > cb ? cend - cb : 0;
+    const int64_t off0 = static_cast<int64_t>(p & 15u);
+    const uint8_t* abase = reinterpret_cast<const uint8_t*>(p - static_cast<uint64_t>(off0));
+    const int64_t mn = static_cast<int64_t>(a.min_size), mx = static_cast<int64_t>(a.max_size);
+    auto hash = make_hash<KIND>(sm, a, lane);
+
+    int64_t s = 0;
+    uint64_t cnt = 0;
+    while (s < n) {
+        const int64_t pf = s + mn - 1;
+        int64_t next;
+        if (pf >= n) {
+            next = n;  // trailing chunk shorter than min
+        } else {
+            const int64_t pl = s + mx - 1 < n - 1 ? s + mx - 1 : n - 1;
+            const int64_t f = scan_region(hash, abase, off0, off0 + n, pf + off0, pl + off0, lane);
+            if (f >= 0)
+                next = f - off0 + 1;
+            else if (s + mx - 1 <= n - 1)
+                next = s + mx;  // forced cut at max size (splitter_buzhash32.go:60-64)
+            else
+                next = n;       // trailing remainder
+        }
+        if (lane == 0 && cnt < cap) a.cuts[cb + cnt] = static_cast<uint64_t>(next);
+        cnt++;
+        s = next;
+    }
+    if (lane == 0) a.counts[sid] = cnt;
+}
+
+// FIXED-*: cuts every chunk length (splitter_fixed.go:15-26); reads no data.
+__global__ void split_fixed_kernel(BatchArgs a) {
+    const uint32_t sid = blockIdx.x;
+    if (sid >= a.nstreams) return;
+    const uint64_t n = a.lens[sid];
+    const uint64_t cb = a.cut_base[sid];
+    const uint64_t cend = sid + 1 < a.nstreams ? a.cut_base[sid + 1] : a.cuts_cap;
+    const uint64_t cap = cend > cb ? cend - cb : 0;
+    const uint64_t L = a.min_size;
+    const uint64_t full = n / L;
+    const uint64_t cnt = full + (n % L ? 1 : 0);
+    for (uint64_t k = threadIdx.x; k < cnt && k < cap; k += blockDim.x) a.cuts[cb + k] = k < full ? (k + 1) * L : n;
+    if (threadIdx.x == 0) a.counts[sid] = cnt;
+}
+
+// Streaming-handle support: first candidate in [lo, hi] of one aligned buffer.
+template <int KIND>
+__global__ __launch_bounds__(kWave) void scan_first_kernel(BatchArgs a, const uint8_t* buf, int64_t len, int64_t lo,
+                                                            int64_t hi, int64_t* out) {
+    __shared__ HashSmem<KIND> sm;
+    fill_tables<KIND>(sm, a);
+    const int lane = threadIdx.x & (kWave - 1);
+    auto hash = make_hash<KIND>(sm, a, lane);
+    const int64_t f = scan_region(hash, buf, 0, len, lo, hi, lane);
+    if (lane == 0) out[0] = f;
+}
+
+// ------------------------------------------------------ synthetic streams
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void fill_prng_kernel(uint8_t* data, uint64_t stride, uint64_t len, uint32_t nstreams, uint64_t seed,
+                                 uint64_t first_sid) {
+    const uint64_t words = len >> 3;
+    const uint64_t total = words * nstreams;
+    const uint64_t step = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < total; g += step) {
+        const uint64_t i = g / words, j = g - i * words;
+        const uint64_t key = mix64(seed ^ mix64(first_sid + i + 0x632BE59BD9B4E019ull));
+        reinterpret_cast<uint64_t*>(data + i * stride)[j] = mix64(key + (j + 1) * 0x9E3779B97F4A7C15ull);
+    }
+    if (len & 7) {  // tail bytes of each stream
+        for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < nstreams; i += step) {
+            const uint64_t key = mix64(seed ^ mix64(first_sid + i + 0x632BE59BD9B4E019ull));
+            const uint64_t w = mix64(key + (words + 1) * 0x9E3779B97F4A7C15ull);
+            for (uint64_t b = 0; b < (len & 7); b++) data[i * stride + words * 8 + b] = static_cast<uint8_t>(w >> (8 * b));
+        }
+    }
+}
+
+}  // namespace dev
+
+// ================================================================== host
+struct DeviceTables {
+    uint32_t* buz = nullptr;
+    uint64_t* rk_out = nullptr;
+    uint64_t* rk_mod = nullptr;
+};
+
+namespace {
+constexpr int kMaxDevices = 64;
+DeviceTables g_dev_tables[kMaxDevices];
+bool g_dev_ready[kMaxDevices];
+std::mutex g_dev_mu;
+
+int hip_fail(hipError_t e, const char* what) {
+    return set_error(-5, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+dev::BatchArgs base_args(const Algo& algo, const DeviceTables& t) {
+    dev::BatchArgs a{};
+    a.min_size = algo.min_size();
+    a.max_size = algo.max_size();
+    a.mask = static_cast<uint32_t>(algo.mask());
+    a.buz = t.buz;
+    a.rk_out = t.rk_out;
+    a.rk_mod = t.rk_mod;
+    a.rk_shift = static_cast<uint32_t>(tables().rk_shift);
+    return a;
+}
+}  // namespace
+
+const DeviceTables* device_tables(int device, int* err) {
+    *err = 0;
+    if (device < 0 || device >= kMaxDevices) {
+        *err = set_error(-22, "device index out of range");
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    if (g_dev_ready[device]) return &g_dev_tables[device];
+    const Tables& T = tables();
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) { *err = hip_fail(e, "hipSetDevice"); return nullptr; }
+    DeviceTables d;
+    e = hipMalloc(&d.buz, sizeof(T.buz));
+    if (e == hipSuccess) e = hipMalloc(&d.rk_out, sizeof(T.rk_out));
+    if (e == hipSuccess) e = hipMalloc(&d.rk_mod, sizeof(T.rk_mod));
+    if (e == hipSuccess) e = hipMemcpy(d.buz, T.buz, sizeof(T.buz), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d.rk_out, T.rk_out, sizeof(T.rk_out), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d.rk_mod, T.rk_mod, sizeof(T.rk_mod), hipMemcpyHostToDevice);
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) { *err = hip_fail(e, "table upload"); return nullptr; }
+    g_dev_tables[device] = d;
+    g_dev_ready[device] = true;
+    return &g_dev_tables[device];
+}
+
+int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* stream) {
+    int err = 0;
+    const DeviceTables* t = device_tables(device, &err);
+    if (!t) return err;
+    if (s.nstreams == 0) return 0;
+    dev::BatchArgs a = base_args(algo, *t);
+    a.ptrs = s.ptrs;
+    a.lens = s.lens;
+    a.nstreams = s.nstreams;
+    a.cuts = s.cuts;
+    a.cuts_cap = s.cuts_cap;
+    a.cut_base = s.cut_base;
+    a.counts = s.counts;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (algo.kind == kFixed) {
+        hipLaunchKernelGGL(dev::split_fixed_kernel, dim3(s.nstreams), dim3(256), 0, st, a);
+    } else {
+        const dim3 grid((s.nstreams + dev::kWavesPerWG - 1) / dev::kWavesPerWG);
+        const dim3 block(dev::kWavesPerWG * dev::kWave);
+        if (algo.kind == kBuzhash)
+            hipLaunchKernelGGL(dev::split_batch_kernel<kBuzhash>, grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL(dev::split_batch_kernel<kRabinKarp>, grid, block, 0, st, a);
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "split kernel launch");
+}
+
+int launch_scan_first(const Algo& algo, const uint8_t* d_buf, uint64_t len, int64_t lo, int64_t hi, int64_t* d_out,
+                      int device, void* stream) {
+    int err = 0;
+    const DeviceTables* t = device_tables(device, &err);
+    if (!t) return err;
+    dev::BatchArgs a = base_args(algo, *t);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (algo.kind == kBuzhash)
+        hipLaunchKernelGGL(dev::scan_first_kernel<kBuzhash>, dim3(1), dim3(dev::kWave), 0, st, a, d_buf,
+                           static_cast<int64_t>(len), lo, hi, d_out);
+    else if (algo.kind == kRabinKarp)
+        hipLaunchKernelGGL(dev::scan_first_kernel<kRabinKarp>, dim3(1), dim3(dev::kWave), 0, st, a, d_buf,
+                           static_cast<int64_t>(len), lo, hi, d_out);
+    else
+        return set_error(-22, "scan_first: FIXED splitters read no data");
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "scan kernel launch");
+}
+
+int launch_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint32_t nstreams, uint64_t seed,
+                     uint64_t first_sid, void* stream) {
+    if (stride % 8 != 0 || (nstreams > 1 && stride < stream_len))
+        return set_error(-22, "fill_prng: stride must be a multiple of 8 and >= stream_len");
+    if (nstreams == 0 || stream_len == 0) return 0;
+    hipLaunchKernelGGL(dev::fill_prng_kernel, dim3(4096), dim3(256), 0, static_cast<hipStream_t>(stream), d_data,
+                       stride, stream_len, nstreams, seed, first_sid);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "fill kernel launch");
+}
+
+size_t long_workspace_bytes(const Algo&, uint64_t) { return 0; }
+int launch_split_long(const Algo&, const uint8_t*, uint64_t, uint64_t*, uint64_t, uint64_t*, void*, size_t, int,
+                      void*) {
+    return set_error(-22, "kcdc_split_long_device: not implemented yet");
+}
+
+}  // namespace kcdc

@@ -103,13 +103,19 @@ class OracleSplitter:
 
 def feed(name: str, data: bytes, mode: str, seed: int = 1) -> np.ndarray:
     """Split points (absolute end offsets) under one of the reference test feeders."""
-    k, size = params(name)
+    kind, size = REGISTRY[name]
+    return feed_kind(kind, size, data, mode, seed)
+
+
+def feed_kind(kind: str, size: int, data: bytes, mode: str, seed: int = 1) -> np.ndarray:
+    """As feed() for an unregistered parameterisation (the KAT factories)."""
+    k = KIND[kind]
     L = lib()
     h = L.orc_new(k, size)
     try:
-        cap = cut_capacity(name, len(data)) + 1
+        cap = len(data) // max(1, size if kind == "fixed" else size // 2) + 2
         out = np.zeros(cap, dtype=np.int64)
-        n = L.orc_feed(h, data, len(data), MODES[mode], seed, out, cap)
+        n = L.orc_feed(h, bytes(data), len(data), MODES[mode], seed, out, cap)
         assert n <= cap
         return out[:n].copy()
     finally:

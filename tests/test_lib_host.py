@@ -1,0 +1,116 @@
+"""Host-side checks of the product library (CPU only, no GPU needed): it loads,
+exports every symbol include/kcdc.h declares, its registry matches the
+reference's, and its independently derived hash tables match the golden ones."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, golden
+from kopia_amd import _lib
+from kopia_amd import splitter as ks
+from oracle import splitter_ref as ref
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "kcdc.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(kcdc_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    L = _lib.lib()
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(L, s), f"libkcdc.so does not export {s}"
+    assert sorted(_lib.exported_symbols()) == syms
+
+
+def test_supported_algorithms_match_reference():
+    assert ks.SupportedAlgorithms() == ref.supported_algorithms()
+    assert _lib.lib().kcdc_default_algorithm().decode() == ref.DEFAULT_ALGORITHM == ks.DefaultAlgorithm
+
+
+@pytest.mark.parametrize("name", ref.supported_algorithms())
+def test_lookup_params(name):
+    kind, size = ref.REGISTRY[name]
+    info = ks.lookup(name)
+    assert info is not None
+    assert info.kind == {"fixed": 0, "buzhash": 1, "rabinkarp": 2}[kind]
+    assert info.avg == size
+    if kind == "fixed":
+        assert (info.min_size, info.max_size, info.mask) == (size, size, 0)
+    else:
+        assert (info.min_size, info.max_size, info.mask) == (size // 2, 2 * size, size - 1)
+    # pooled(...) everywhere except the two legacy names (splitter.go:75-80)
+    assert info.pooled == (0 if name in ("FIXED", "DYNAMIC") else 1)
+    assert ks.max_segment_size(name) == (size if kind == "fixed" else 2 * size)
+
+
+def test_max_segment_invariants():
+    """gather chunk allocator (internal/gather/gather_write_buffer_chunk_test.go:69-81)
+    and gRPC message limit (repo/grpc_repository_client_test.go:14-26)."""
+    for name in ks.SupportedAlgorithms():
+        m = ks.max_segment_size(name)
+        assert m <= (16 << 20) + 128 - 128
+        assert m <= (20 << 20) - 1024
+
+
+def test_unknown_name():
+    assert ks.GetFactory("nosuchsplitter") is None
+    assert ks.lookup("nosuchsplitter") is None
+    with pytest.raises(_lib.KcdcError):
+        ks.max_segment_size("nosuchsplitter")
+
+
+def test_custom_algorithm_names():
+    a = ks.custom_algorithm("buzhash", 32)
+    assert a == ks.custom_algorithm("buzhash", 32)
+    assert a not in ks.SupportedAlgorithms()
+    assert ks.max_segment_size(a) == 64
+    assert ks.max_segment_size(ks.custom_algorithm("fixed", 1000)) == 1000
+    with pytest.raises(_lib.KcdcError):
+        ks.custom_algorithm("buzhash", 1000)  # not a power of two
+
+
+def test_cut_capacity():
+    assert ks.cut_capacity("DYNAMIC-4M-BUZHASH", 4 << 20) == 3
+    assert ks.cut_capacity("FIXED-1M", 1441792) == 2
+
+
+def test_tables_match_golden():
+    buz = (C.c_uint32 * 256)()
+    pol = C.c_uint64()
+    out = (C.c_uint64 * 256)()
+    mod = (C.c_uint64 * 256)()
+    assert _lib.lib().kcdc_tables(buz, C.byref(pol), out, mod) == 0
+    g = golden("tables.json")
+    assert [f"{x:08x}" for x in buz] == g["buzhash"]
+    assert hex(pol.value) == g["rabin_pol"]
+    assert [f"{x:016x}" for x in out] == g["rabin_out"]
+    assert [f"{x:016x}" for x in mod] == g["rabin_mod"]
+
+
+def test_gpu_entry_points_fail_loudly_without_device():
+    if _lib.lib().kcdc_device_count() > 0:
+        pytest.skip("a gfx950 device is present")
+    # no silent CPU fallback: a dynamic splitter cannot be created without the GPU
+    with pytest.raises(_lib.KcdcError):
+        ks.Splitter("DYNAMIC-4M-BUZHASH")
+    data = np.zeros(10, dtype=np.uint8)
+    from kopia_amd import batch
+    with pytest.raises(_lib.KcdcError):
+        batch.split_batch_host("DYNAMIC-4M-BUZHASH", [data])
+
+
+def test_fixed_streaming_handle_needs_no_device():
+    """FIXED reads no data (splitter_fixed.go:15-26): pure host arithmetic."""
+    s = ks.GetFactory("FIXED-128K")()
+    data = bytes(300000)
+    assert s.MaxSegmentSize() == 128 << 10
+    assert s.NextSplitPoint(data[:100000]) == -1
+    assert s.NextSplitPoint(data[100000:]) == (128 << 10) - 100000
+    s.Close()
