@@ -65,6 +65,14 @@ def lib() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build()) first; "
                           "there is no CPU fallback")
+    # One HIP runtime per process: torch's wheel bundles libamdhip64 (SONAME
+    # libamdhip64.so.7, but its libraries NEED "libamdhip64.so" via RPATH).  If
+    # libkcdc.so loaded /opt/rocm's copy first, torch would map a second runtime
+    # and fail to initialise; loading torch first lets libkcdc bind to torch's copy.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
         f = getattr(L, name)

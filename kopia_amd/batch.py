@@ -89,3 +89,27 @@ def fill_prng(data: "torch.Tensor", stream_len: int, nstreams: int, stride: int,
     assert data.numel() * data.element_size() >= stride * (nstreams - 1) + stream_len
     _lib.check(_lib.lib().kcdc_fill_prng(data.data_ptr(), stride, stream_len, nstreams, seed, first_sid,
                                          C.c_void_p(stream.cuda_stream)))
+
+
+def split_long_device(name: str, data_ptr: int, length: int, device, stream=None):
+    """Exact intra-stream parallel CDC of ONE device-resident stream (config 3).
+    Returns (cuts tensor on device, count tensor on device); cuts[:count] valid."""
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream(device)
+    cap = cut_capacity(name, length)
+    ws_bytes = int(_lib.lib().kcdc_long_workspace_bytes(name.encode(), length))
+    ws = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=device)
+    cuts = torch.zeros(max(cap, 1), dtype=torch.int64, device=device)
+    count = torch.zeros(1, dtype=torch.int64, device=device)
+    _lib.check(_lib.lib().kcdc_split_long_device(
+        name.encode(), data_ptr, length, cuts.data_ptr(), cap, count.data_ptr(), ws.data_ptr(), ws.numel(),
+        C.c_void_p(stream.cuda_stream)))
+    return cuts, count, ws
+
+
+def read_long(cuts, count) -> np.ndarray:
+    n = int(count.item())
+    if n > cuts.numel():
+        raise _lib.KcdcError(_lib.KCDC_EOVERFLOW, f"{n} cuts > capacity {cuts.numel()}")
+    return cuts[:n].cpu().numpy()

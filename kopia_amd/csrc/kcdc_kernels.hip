@@ -497,6 +497,225 @@ __global__ void fill_prng_kernel(uint8_t* data, uint64_t stride, uint64_t len, u
     }
 }
 
+
+// ------------------------------------------- long single stream (config 3)
+// Phase 1: every 64 KiB segment is scanned by one wave (lane l: 1 KiB sub-range,
+// 64-byte warm-up), which stores the segment's first kSegK candidate positions
+// and whether it had more ("truncated").  Phase 2: exclusive prefix sum of the
+// stored counts.  Phase 3: compaction into one sorted candidate list.  Phase 4:
+// one wave walks the chunk rule over that list from LDS windows; where a
+// truncated (candidate-dense) segment may hide the candidate it needs, it rescans
+// that range with the same scan_region() the batch kernel uses.  The cut set is
+// therefore exactly the sequential one, for any data.
+constexpr int64_t kSegBytes = kWave * kLaneMax;  // 64 KiB
+constexpr int kSegK = 4;
+constexpr uint64_t kTruncBit = 1ull << 63;
+
+struct LongArgs {
+    const uint8_t* abase;
+    int64_t off0;
+    int64_t n;
+    int64_t nseg;
+    uint32_t* seg_cnt;   // stored count | (truncated << 31)
+    uint64_t* seg_cand;  // [nseg][kSegK] absolute positions
+    uint64_t* seg_off;   // exclusive prefix of stored counts
+    uint64_t* list;      // compacted candidates (kTruncBit marks the last stored of a truncated segment)
+    uint64_t* total;     // [1] number of list entries
+    uint64_t* cuts;
+    uint64_t cuts_cap;
+    uint64_t* count;
+};
+
+template <int KIND>
+__global__ __launch_bounds__(kWavesPerWG * kWave, 4) void cand_scan_kernel(BatchArgs a, LongArgs g) {
+    __shared__ HashSmem<KIND> sm;
+    fill_tables<KIND>(sm, a);
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int64_t seg = static_cast<int64_t>(blockIdx.x) * kWavesPerWG + wave;
+    if (seg >= g.nseg) return;
+    auto hash = make_hash<KIND>(sm, a, lane);
+    // Segments tile COORDINATES (position + off0) so every lane sub-range is 16-byte aligned.
+    const int64_t cs = seg * kSegBytes;
+    const int64_t lo = cs > g.off0 ? cs : g.off0;                                   // first coordinate tested
+    const int64_t hi = (cs + kSegBytes < g.off0 + g.n ? cs + kSegBytes : g.off0 + g.n) - 1;  // inclusive
+    const int64_t tb = cs >= 64 ? cs - 64 : 0;
+    const Loader ld = make_loader(g.abase, g.off0, g.off0 + g.n, tb);
+    const int64_t c0 = cs + lane * kLaneMax;
+    uint32_t found[kSegK];
+    int nf = 0;  // candidates found by this lane (kSegK + 1 means "more than kSegK")
+    if (c0 <= hi) {
+        uint32_t cur[16], nxt[16];
+        hash.clear();
+        ld.load(c0 - 64, cur);
+        hash.template block<kWarm>(cur, 0, 0);
+        ld.load(c0, cur);
+        for (int k = 0; k < static_cast<int>(kLaneMax / 64) && nf <= kSegK; k++) {
+            const int64_t c = c0 + 64 * k;
+            if (c > hi) break;
+            ld.load(c + 64, nxt);
+            const typename decltype(hash)::State st0 = hash.save();
+            if (hash.template block<kFast>(cur, 0, 63) == 0) {
+                uint32_t prv[16];
+                ld.load(c - 64, prv);
+                const int bhi = hi - c > 63 ? 63 : static_cast<int>(hi - c);
+                int from = lo > c ? static_cast<int>(lo - c) : 0;
+                while (from <= bhi && nf <= kSegK) {
+                    const uint32_t idx = hash.exact(st0, prv, cur, from, bhi);
+                    if (idx >= 64) break;
+                    if (nf < kSegK) found[nf] = static_cast<uint32_t>(c - cs) + idx;
+                    nf++;
+                    from = static_cast<int>(idx) + 1;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 16; i++) cur[i] = nxt[i];
+        }
+    }
+    // exclusive prefix of per-lane counts (segments are in lane order)
+    int incl = nf;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const int v = __shfl_up(incl, d);
+        if (lane >= d) incl += v;
+    }
+    const int tot = __shfl(incl, kWave - 1);
+    const int pre = incl - nf;
+    for (int j = 0; j < nf && j < kSegK; j++)
+        if (pre + j < kSegK) g.seg_cand[seg * kSegK + pre + j] = static_cast<uint64_t>(cs - g.off0) + found[j];
+    if (lane == 0) g.seg_cnt[seg] = (tot > kSegK ? 0x80000000u : 0u) | static_cast<uint32_t>(tot < kSegK ? tot : kSegK);
+}
+
+// Exclusive prefix sum of stored counts (one workgroup; the long path has at most
+// a few million segments).
+__global__ __launch_bounds__(1024) void seg_prefix_kernel(LongArgs g) {
+    __shared__ uint64_t wsum[16];
+    __shared__ uint64_t carry;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (t == 0) carry = 0;
+    __syncthreads();
+    constexpr int kItems = 8;
+    for (int64_t base = 0; base < g.nseg; base += 1024 * kItems) {
+        uint64_t v[kItems], sum = 0;
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+            const int64_t i = base + static_cast<int64_t>(t) * kItems + j;
+            v[j] = i < g.nseg ? (g.seg_cnt[i] & 0x7FFFFFFFu) : 0;
+            sum += v[j];
+        }
+        uint64_t incl = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t x = __shfl_up(incl, d);
+            if (lane >= d) incl += x;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        uint64_t wpre = 0;
+        for (int k = 0; k < w; k++) wpre += wsum[k];
+        uint64_t run = carry + wpre + incl - sum;
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+            const int64_t i = base + static_cast<int64_t>(t) * kItems + j;
+            if (i < g.nseg) g.seg_off[i] = run;
+            run += v[j];
+        }
+        __syncthreads();
+        if (t == 1023) carry = run;
+        __syncthreads();
+    }
+    if (t == 0) g.total[0] = carry;
+}
+
+__global__ void compact_kernel(LongArgs g) {
+    const int64_t seg = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (seg >= g.nseg) return;
+    const uint32_t c = g.seg_cnt[seg];
+    const uint32_t k = c & 0x7FFFFFFFu;
+    const uint64_t o = g.seg_off[seg];
+    for (uint32_t j = 0; j < k; j++) {
+        uint64_t v = g.seg_cand[seg * kSegK + j];
+        if ((c >> 31) && j + 1 == k) v |= kTruncBit;
+        g.list[o + j] = v;
+    }
+}
+
+constexpr int kResolveWin = 4096;  // candidate-list entries staged in LDS
+
+template <int KIND>
+__global__ __launch_bounds__(kWave) void resolve_kernel(BatchArgs a, LongArgs g, int64_t mn, int64_t mx) {
+    __shared__ HashSmem<KIND> sm;
+    __shared__ uint64_t win[kResolveWin];
+    fill_tables<KIND>(sm, a);
+    const int lane = threadIdx.x;
+    auto hash = make_hash<KIND>(sm, a, lane);
+    const int64_t total = static_cast<int64_t>(uni64(g.total[0]));
+    const int64_t n = g.n;
+    int64_t wbase = -1;  // list index of win[0]
+    auto load_win = [&](int64_t at) {
+        __syncthreads();
+        for (int j = lane; j < kResolveWin; j += kWave) win[j] = at + j < total ? g.list[at + j] : ~0ull >> 1;
+        __syncthreads();
+        wbase = at;
+    };
+    auto entry = [&](int64_t i) -> uint64_t {  // wave-uniform
+        if (i < wbase || i >= wbase + kResolveWin) load_win(i > 64 ? i - 64 : 0);
+        return win[i - wbase];
+    };
+    int64_t s = 0, i = 0;
+    uint64_t cnt = 0;
+    while (s < n) {
+        const int64_t lo = s + mn - 1;
+        int64_t next;
+        if (lo >= n) {
+            next = n;
+        } else {
+            const int64_t hi = s + mx - 1 < n - 1 ? s + mx - 1 : n - 1;
+            // advance i to the first entry >= lo, 64 entries per step
+            for (;;) {
+                if (i >= total) break;
+                if (i < wbase || i + kWave > wbase + kResolveWin) load_win(i > 64 ? i - 64 : 0);
+                const int64_t j = i + lane;
+                const bool ge = j >= total || static_cast<int64_t>(win[j - wbase] & ~kTruncBit) >= lo;
+                const uint64_t bal = __ballot(ge);
+                if (bal) {
+                    i += __builtin_ctzll(bal);
+                    break;
+                }
+                i += kWave;
+            }
+            if (i > total) i = total;
+            int64_t c = -1;
+            if (i > 0) {
+                const uint64_t e = entry(i - 1);
+                if (e & kTruncBit) {  // its segment may hold unlisted candidates >= lo
+                    // end (exclusive, in positions) of the coordinate segment holding entry e
+                    const int64_t seg_end =
+                        ((static_cast<int64_t>(e & ~kTruncBit) + g.off0) / kSegBytes + 1) * kSegBytes - g.off0;
+                    if (seg_end > lo) {
+                        const int64_t rh = seg_end - 1 < hi ? seg_end - 1 : hi;
+                        const int64_t f = scan_region(hash, g.abase, g.off0, g.off0 + n, lo + g.off0, rh + g.off0, lane);
+                        if (f >= 0) c = f - g.off0;
+                    }
+                }
+            }
+            if (c < 0 && i < total) {
+                const int64_t p = static_cast<int64_t>(entry(i) & ~kTruncBit);
+                if (p <= hi) c = p;
+            }
+            if (c >= 0)
+                next = c + 1;
+            else if (s + mx - 1 <= n - 1)
+                next = s + mx;
+            else
+                next = n;
+        }
+        if (lane == 0 && cnt < g.cuts_cap) g.cuts[cnt] = static_cast<uint64_t>(next);
+        cnt++;
+        s = next;
+    }
+    if (lane == 0) g.count[0] = cnt;
+}
 }  // namespace dev
 
 // ================================================================== host
@@ -614,10 +833,77 @@ int launch_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint
     return e == hipSuccess ? 0 : hip_fail(e, "fill kernel launch");
 }
 
-size_t long_workspace_bytes(const Algo&, uint64_t) { return 0; }
-int launch_split_long(const Algo&, const uint8_t*, uint64_t, uint64_t*, uint64_t, uint64_t*, void*, size_t, int,
-                      void*) {
-    return set_error(-22, "kcdc_split_long_device: not implemented yet");
+namespace {
+struct LongLayout {
+    int64_t nseg;
+    size_t off_cnt, off_cand, off_off, off_list, off_total, bytes;
+};
+LongLayout long_layout(uint64_t len) {
+    auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+    LongLayout L{};
+    L.nseg = static_cast<int64_t>((len + 15 + dev::kSegBytes - 1) / dev::kSegBytes);  // coordinates: + off0 < 16
+    const size_t ns = static_cast<size_t>(L.nseg);
+    size_t o = 0;
+    L.off_cnt = o;   o += al(ns * 4);
+    L.off_cand = o;  o += al(ns * dev::kSegK * 8);
+    L.off_off = o;   o += al(ns * 8);
+    L.off_list = o;  o += al(ns * dev::kSegK * 8);
+    L.off_total = o; o += 256;
+    L.bytes = o;
+    return L;
+}
+}  // namespace
+
+size_t long_workspace_bytes(const Algo& algo, uint64_t len) {
+    if (algo.kind == kFixed) return 0;
+    return long_layout(len).bytes;
+}
+
+int launch_split_long(const Algo& algo, const uint8_t* d_data, uint64_t len, uint64_t* d_cuts, uint64_t cuts_cap,
+                      uint64_t* d_count, void* ws, size_t ws_bytes, int device, void* stream) {
+    int err = 0;
+    const DeviceTables* t = device_tables(device, &err);
+    if (!t) return err;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (algo.kind == kFixed)  // reads no data; the batch entry point covers it
+        return set_error(-22, "kcdc_split_long_device: use kcdc_split_batch_device for FIXED splitters");
+    const LongLayout L = long_layout(len);
+    if (len == 0) {
+        const hipError_t e = hipMemsetAsync(d_count, 0, sizeof(uint64_t), st);
+        return e == hipSuccess ? 0 : hip_fail(e, "memset");
+    }
+    if (!ws || ws_bytes < L.bytes) return set_error(-22, "kcdc_split_long_device: workspace too small");
+    char* w = static_cast<char*>(ws);
+    dev::LongArgs g{};
+    const uint64_t p = reinterpret_cast<uint64_t>(d_data);
+    g.off0 = static_cast<int64_t>(p & 15u);
+    g.abase = reinterpret_cast<const uint8_t*>(p - static_cast<uint64_t>(g.off0));
+    g.n = static_cast<int64_t>(len);
+    g.nseg = (g.off0 + g.n + dev::kSegBytes - 1) / dev::kSegBytes;  // <= L.nseg
+    g.seg_cnt = reinterpret_cast<uint32_t*>(w + L.off_cnt);
+    g.seg_cand = reinterpret_cast<uint64_t*>(w + L.off_cand);
+    g.seg_off = reinterpret_cast<uint64_t*>(w + L.off_off);
+    g.list = reinterpret_cast<uint64_t*>(w + L.off_list);
+    g.total = reinterpret_cast<uint64_t*>(w + L.off_total);
+    g.cuts = d_cuts;
+    g.cuts_cap = cuts_cap;
+    g.count = d_count;
+    dev::BatchArgs a = base_args(algo, *t);
+    const dim3 grid(static_cast<unsigned>((L.nseg + dev::kWavesPerWG - 1) / dev::kWavesPerWG));
+    const dim3 block(dev::kWavesPerWG * dev::kWave);
+    const int64_t mn = static_cast<int64_t>(algo.min_size()), mx = static_cast<int64_t>(algo.max_size());
+    if (algo.kind == kBuzhash)
+        hipLaunchKernelGGL(dev::cand_scan_kernel<kBuzhash>, grid, block, 0, st, a, g);
+    else
+        hipLaunchKernelGGL(dev::cand_scan_kernel<kRabinKarp>, grid, block, 0, st, a, g);
+    hipLaunchKernelGGL(dev::seg_prefix_kernel, dim3(1), dim3(1024), 0, st, g);
+    hipLaunchKernelGGL(dev::compact_kernel, dim3(static_cast<unsigned>((L.nseg + 255) / 256)), dim3(256), 0, st, g);
+    if (algo.kind == kBuzhash)
+        hipLaunchKernelGGL(dev::resolve_kernel<kBuzhash>, dim3(1), dim3(dev::kWave), 0, st, a, g, mn, mx);
+    else
+        hipLaunchKernelGGL(dev::resolve_kernel<kRabinKarp>, dim3(1), dim3(dev::kWave), 0, st, a, g, mn, mx);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "long-stream kernel launch");
 }
 
 }  // namespace kcdc
