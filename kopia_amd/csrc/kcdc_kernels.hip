@@ -651,7 +651,7 @@ __global__ __launch_bounds__(kWave) void resolve_kernel(BatchArgs a, LongArgs g,
     auto hash = make_hash<KIND>(sm, a, lane);
     const int64_t total = static_cast<int64_t>(uni64(g.total[0]));
     const int64_t n = g.n;
-    int64_t wbase = -1;  // list index of win[0]
+    int64_t wbase = 0;  // list index of win[0]
     auto load_win = [&](int64_t at) {
         __syncthreads();
         for (int j = lane; j < kResolveWin; j += kWave) win[j] = at + j < total ? g.list[at + j] : ~0ull >> 1;
@@ -662,6 +662,7 @@ __global__ __launch_bounds__(kWave) void resolve_kernel(BatchArgs a, LongArgs g,
         if (i < wbase || i >= wbase + kResolveWin) load_win(i > 64 ? i - 64 : 0);
         return win[i - wbase];
     };
+    load_win(0);
     int64_t s = 0, i = 0;
     uint64_t cnt = 0;
     while (s < n) {
