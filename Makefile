@@ -34,3 +34,14 @@ clean:
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean asm
+
+# ---- experiment builds (A/B of compile-time tunables; not used by the product)
+VARIANTS ?= b64w8:-DKCDC_BLK=64,-DKCDC_BATCH_WAVES=8 b128w8:-DKCDC_BLK=128,-DKCDC_BATCH_WAVES=8 b128w12:-DKCDC_BLK=128,-DKCDC_BATCH_WAVES=12
+variants:
+	@mkdir -p build/variants
+	@for v in $(VARIANTS); do \
+	  n=$${v%%:*}; f=$$(echo $${v#*:} | tr ',' ' '); \
+	  echo "variant $$n: $$f"; \
+	  $(HIPCC) $(HIPFLAGS) $$f -shared -o build/variants/libkcdc_$$n.so $(CSRC)/kcdc_kernels.hip -x hip $(CSRC)/kcdc_api.cpp $(CSRC)/kcdc_tables.cpp $(CSRC)/kcdc_registry.cpp || exit 1; \
+	done
+.PHONY: variants

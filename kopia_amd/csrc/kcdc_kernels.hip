@@ -14,18 +14,19 @@
 // bytes are rolled) becomes "start scanning at s+min-64": bytes before that are
 // never read.
 //
-// Work decomposition — one wavefront per stream:
-//   the wave walks the stream chunk by chunk; for the current chunk it scans the
-//   test region [s+min-1, s+max-1] in TILES of 64 lanes x L bytes.  Lane l owns
-//   the L-byte segment l of the tile and warms its hash up on the 64 bytes before
-//   it, so all 64 lanes hash independently.  Per byte: one v_perm (table
-//   address), one LDS table read (the 1 KiB buzhash table is replicated 64x so
-//   lane l always hits bank l%32: conflict-free), one v_alignbit (rotl 1), one
-//   v_xor3 and the candidate test folded into a running min.  The outgoing byte's
-//   table value comes from a 64-entry register ring (the loop is unrolled by 64
-//   so the ring index is static).  A block whose running min is 0 is re-run in
-//   exact mode to find the first candidate; the earliest lane with a candidate
-//   (ballot + ffs) gives the tile's first candidate.
+// Work decomposition — one wavefront per stream (batch path):
+//   persistent waves pull stream ids from an atomic queue; a wave walks its
+//   stream chunk by chunk, scanning the test region [s+min-1, s+max-1] in TILES
+//   of 64 lanes x L bytes.  Lane l owns the L-byte segment l of the tile and
+//   warms its hash up on the 64 bytes before it, so the 64 lanes hash
+//   independently.  Each lane streams its segment in kBlk-byte steps (whole
+//   128-byte lines, 16-byte buffer loads, one step prefetched).  Per byte: two
+//   v_perm (table addresses for the entering and the leaving byte), two LDS
+//   table reads (the 1 KiB buzhash table is replicated 64x so lane l always hits
+//   bank l%32: conflict-free), v_alignbit (rotl 1), two XOR and the candidate
+//   test folded into a running min (v_bitop3 + v_min3).  A step whose running
+//   min is 0 is re-run exactly (rolled loop) to find the first candidate; the
+//   earliest lane with a candidate (ballot + ffs) gives the tile's answer.
 #include <hip/hip_runtime.h>
 
 #include <mutex>
@@ -39,27 +40,35 @@ namespace dev {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWave = 64;
-constexpr int kWavesPerWG = 8;        // 512 threads; 16 waves/CU at 2 WGs/CU
-constexpr int64_t kLaneMax = 1024;    // max bytes per lane segment (tile = 64 KiB)
-
+#ifndef KCDC_BLK
+#define KCDC_BLK 128
+#endif
+constexpr int kBlk = KCDC_BLK;          // bytes per lane per step (a multiple of 64)
+constexpr int kNdw = kBlk / 4;          // dwords per lane per step
+constexpr int64_t kLaneMax = 2048;      // max bytes per lane segment (tile = 128 KiB)
+#ifndef KCDC_BATCH_WAVES
+#define KCDC_BATCH_WAVES 8
+#endif
+constexpr int kBatchWaves = KCDC_BATCH_WAVES;  // waves per workgroup, persistent batch kernel
+constexpr int kScanWaves = 8;                  // waves per workgroup, long-path candidate scan
 #ifndef KCDC_SCHED_WINDOW
 #define KCDC_SCHED_WINDOW 16
 #endif
 constexpr int kSchedWindow = KCDC_SCHED_WINDOW;  // bytes per scheduling window in the hash loop
 
-enum Mode { kWarm = 0, kFast = 1, kExact = 2 };
+enum Mode { kWarm = 0, kFast = 1 };
 
 __device__ __forceinline__ uint32_t rotl1(uint32_t h) { return __builtin_amdgcn_alignbit(h, h, 31); }
 
-__device__ __forceinline__ uint32_t ufirst(uint64_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x));
     const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x >> 32));
     return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
-// Byte i of a 64-byte block held as 16 dwords.
-__device__ __forceinline__ uint32_t byte_at(const uint32_t (&dw)[16], int i) {
+// Byte i of a block held as dwords.
+template <int N>
+__device__ __forceinline__ uint32_t byte_at(const uint32_t (&dw)[N], int i) {
     return __builtin_amdgcn_perm(0u, dw[i >> 2], 0x0c0c0c00u | static_cast<uint32_t>(i & 3));
 }
 
@@ -73,10 +82,11 @@ struct Loader {
     int64_t tb;    // coordinate of descriptor offset 0
     int64_t off0;  // stream misalignment (0..15)
 
-    __device__ __forceinline__ void load(int64_t c, uint32_t (&dw)[16]) const {
+    template <int N>
+    __device__ __forceinline__ void load(int64_t c, uint32_t (&dw)[N]) const {
         const int32_t vo = static_cast<int32_t>(c - tb);
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < N / 4; j++) {
             const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo + 16 * j, 0, 0);
             dw[4 * j + 0] = v.x;
             dw[4 * j + 1] = v.y;
@@ -87,7 +97,8 @@ struct Loader {
 #pragma unroll
             for (int d = 0; d < 4; d++) {
                 const int64_t keep_from = off0 - 4 * d;  // first byte of dword d to keep
-                uint32_t m = keep_from <= 0 ? 0xFFFFFFFFu : (keep_from >= 4 ? 0u : (0xFFFFFFFFu << (8 * keep_from)));
+                const uint32_t m = keep_from <= 0 ? 0xFFFFFFFFu
+                                                  : (keep_from >= 4 ? 0u : (0xFFFFFFFFu << (8 * keep_from)));
                 dw[d] &= m;
             }
         }
@@ -108,6 +119,10 @@ __device__ __forceinline__ Loader make_loader(const uint8_t* abase, int64_t off0
 }
 
 // ------------------------------------------------------------------ hashes
+// Both hashes keep `prev`: the 64 bytes before the current step (the bytes that
+// leave the window while the step's bytes enter it).  block<MODE, N>(dw) rolls
+// the 4N bytes of dw; byte i leaves-byte is (prev ++ dw)[i].
+
 // buzhash32: h(p) = rotl(h(p-1),1) ^ T[b[p-64]] ^ T[b[p]]  (rollinghash Roll with
 // window 64: rotl(T[leave], 64 % 32 = 0)).
 struct BuzShared {
@@ -119,10 +134,9 @@ struct Buz {
     uint32_t lane4;
     uint32_t mask;
     uint32_t h;
-    uint32_t prev[16];  // bytes of the previous block (the bytes leaving the window)
+    uint32_t prev[16];
     using State = uint32_t;
     __device__ __forceinline__ State save() const { return h; }
-    __device__ __forceinline__ void restore(State s) { h = s; }
 
     __device__ __forceinline__ uint32_t look(uint32_t dwv, int k) const {
         // (byte_k << 8) | lane*4 in one v_perm: byte 0 from lane4, byte 1 = data byte k.
@@ -134,57 +148,55 @@ struct Buz {
 #pragma unroll
         for (int i = 0; i < 16; i++) prev[i] = 0;
     }
-    __device__ __forceinline__ void set_ring(const uint32_t (&p)[16]) {
+    // kWarm: no test (run on a zero history: the G-recurrence warm-up);
+    // kFast: returns the min over the step of (h & mask) (0 => maybe a candidate).
+    template <int MODE, int N>
+    __device__ __forceinline__ uint32_t block(const uint32_t (&dw)[N]) {
+        uint32_t m = 0xFFFFFFFFu;
 #pragma unroll
-        for (int i = 0; i < 16; i++) prev[i] = p[i];
-    }
-    // kWarm: no test; kFast: returns min over the block of (h & mask) (0 => some
-    // position may be a candidate); kExact: index of the first i in [lo, hi] with
-    // (h & mask) == 0, else 64.
-    template <int MODE>
-    __device__ __forceinline__ uint32_t block(const uint32_t (&dw)[16], int lo, int hi) {
-        uint32_t m = 0xFFFFFFFFu, first = 64;
-#pragma unroll
-        for (int i = 0; i < 64; i++) {
+        for (int i = 0; i < 4 * N; i++) {
             if (kSchedWindow && i % kSchedWindow == 0) __builtin_amdgcn_sched_barrier(0);
-            // kWarm runs on a zero "previous block": T[0] terms are skipped there, which is
-            // exactly the G-recurrence warm-up (the window before is never reached).
-            const uint32_t to = MODE == kWarm ? 0u : look(prev[i >> 2], i & 3);
             const uint32_t ti = look(dw[i >> 2], i & 3);
-            h = rotl1(h) ^ to ^ ti;
-            if (MODE == kFast) {
+            if (MODE == kWarm) {
+                h = rotl1(h) ^ ti;
+            } else {
+                const uint32_t to = i < 64 ? look(prev[i >> 2], i & 3) : look(dw[(i - 64) >> 2], i & 3);
+                h = rotl1(h) ^ to ^ ti;
                 m = min(m, h & mask);
                 // Pin the running min every 4 bytes: otherwise the compiler re-associates the
-                // min into a tree at the block end and keeps all 64 hashes live (VGPR blow-up).
+                // min into a tree at the step end and keeps every hash live (VGPR blow-up).
                 if ((i & 3) == 3) asm volatile("" : "+v"(m));
-            }
-            if (MODE == kExact) {
-                if (first == 64 && (h & mask) == 0 && i >= lo && i <= hi) first = i;
-                if ((i & 3) == 3) asm volatile("" : "+v"(first));
             }
         }
 #pragma unroll
-        for (int i = 0; i < 16; i++) prev[i] = dw[i];
-        return MODE == kFast ? m : first;
+        for (int i = 0; i < 16; i++) prev[i] = dw[N - 16 + i];
+        return m;
     }
-    // Exact re-run of one block from state st0 (rare path, compact rolled loop):
-    // index of the first i in [lo, hi] with (h & mask) == 0, else 64.
-    __device__ __forceinline__ uint32_t exact(State st0, const uint32_t (&prv)[16],
-                                                        const uint32_t (&dw)[16], int lo, int hi) const {
-        uint32_t e[16], o[16];
+    // Exact re-run of one step from state st0 with history prv (rare path, compact
+    // rolled loop): index of the first i in [lo, hi] with (h & mask) == 0, else 4N.
+    template <int N>
+    __device__ __forceinline__ uint32_t exact(State st0, const uint32_t (&prv)[16], const uint32_t (&dw)[N], int lo,
+                                              int hi) const {
+        uint32_t e[N], o[N];
 #pragma unroll
-        for (int j = 0; j < 16; j++) { e[j] = dw[j]; o[j] = prv[j]; }
-        uint32_t hh = st0, first = 64;
+        for (int j = 0; j < N; j++) {
+            e[j] = dw[j];
+            o[j] = j < 16 ? prv[j] : dw[j - 16];
+        }
+        uint32_t hh = st0, first = 4 * N;
 #pragma unroll 1
-        for (int j = 0; j < 16; j++) {
+        for (int j = 0; j < N; j++) {
 #pragma unroll
             for (int b = 0; b < 4; b++) {
                 hh = rotl1(hh) ^ look(o[0], b) ^ look(e[0], b);
                 const int i = 4 * j + b;
-                if (first == 64 && (hh & mask) == 0 && i >= lo && i <= hi) first = static_cast<uint32_t>(i);
+                if (first == 4 * N && (hh & mask) == 0 && i >= lo && i <= hi) first = static_cast<uint32_t>(i);
             }
 #pragma unroll
-            for (int k = 0; k < 15; k++) { e[k] = e[k + 1]; o[k] = o[k + 1]; }
+            for (int k = 0; k < N - 1; k++) {
+                e[k] = e[k + 1];
+                o[k] = o[k + 1];
+            }
         }
         return first;
     }
@@ -201,66 +213,61 @@ struct Rabin {
     uint32_t mask;
     uint32_t shift;
     uint64_t v;
-    uint32_t prev[16];  // bytes of the previous block (the bytes leaving the window)
+    uint32_t prev[16];
     using State = uint64_t;
     __device__ __forceinline__ State save() const { return v; }
-    __device__ __forceinline__ void restore(State s) { v = s; }
 
     __device__ __forceinline__ void clear() {
         v = 0;
 #pragma unroll
         for (int i = 0; i < 16; i++) prev[i] = 0;
     }
-    __device__ __forceinline__ void set_ring(const uint32_t (&p)[16]) {
-#pragma unroll
-        for (int i = 0; i < 16; i++) prev[i] = p[i];
+    __device__ __forceinline__ uint64_t roll(uint64_t x, uint32_t bo, uint32_t bi) const {
+        x ^= tab->out[bo];
+        const uint32_t idx = static_cast<uint32_t>(x >> shift) & 0xFFu;
+        return ((x << 8) | bi) ^ tab->mod[idx];
     }
-    template <int MODE>
-    __device__ __forceinline__ uint32_t block(const uint32_t (&dw)[16], int lo, int hi) {
-        uint32_t m = 0xFFFFFFFFu, first = 64;
+    template <int MODE, int N>
+    __device__ __forceinline__ uint32_t block(const uint32_t (&dw)[N]) {
+        uint32_t m = 0xFFFFFFFFu;
 #pragma unroll
-        for (int i = 0; i < 64; i++) {
-            const uint32_t bo = byte_at(prev, i);
-            const uint32_t bi = byte_at(dw, i);
-            uint64_t x = v ^ tab->out[bo];
-            const uint32_t idx = static_cast<uint32_t>(x >> shift) & 0xFFu;
-            x = (x << 8) | bi;
-            v = x ^ tab->mod[idx];
-            const uint32_t lv = static_cast<uint32_t>(v) & mask;
+        for (int i = 0; i < 4 * N; i++) {
+            const uint32_t bo = MODE == kWarm ? 0u : (i < 64 ? byte_at(prev, i) : byte_at(dw, i - 64));
+            v = roll(v, bo, byte_at(dw, i));
             if (MODE == kFast) {
-                m = min(m, lv);
+                m = min(m, static_cast<uint32_t>(v) & mask);
                 if ((i & 3) == 3) asm volatile("" : "+v"(m));
-            }
-            if (MODE == kExact) {
-                if (first == 64 && lv == 0 && i >= lo && i <= hi) first = i;
-                if ((i & 3) == 3) asm volatile("" : "+v"(first));
             }
         }
 #pragma unroll
-        for (int i = 0; i < 16; i++) prev[i] = dw[i];
-        return MODE == kFast ? m : first;
+        for (int i = 0; i < 16; i++) prev[i] = dw[N - 16 + i];
+        return m;
     }
-    __device__ __forceinline__ uint32_t exact(State st0, const uint32_t (&prv)[16],
-                                                        const uint32_t (&dw)[16], int lo, int hi) const {
-        uint32_t e[16], o[16];
+    template <int N>
+    __device__ __forceinline__ uint32_t exact(State st0, const uint32_t (&prv)[16], const uint32_t (&dw)[N], int lo,
+                                              int hi) const {
+        uint32_t e[N], o[N];
 #pragma unroll
-        for (int j = 0; j < 16; j++) { e[j] = dw[j]; o[j] = prv[j]; }
+        for (int j = 0; j < N; j++) {
+            e[j] = dw[j];
+            o[j] = j < 16 ? prv[j] : dw[j - 16];
+        }
         uint64_t vv = st0;
-        uint32_t first = 64;
+        uint32_t first = 4 * N;
 #pragma unroll 1
-        for (int j = 0; j < 16; j++) {
+        for (int j = 0; j < N; j++) {
 #pragma unroll
             for (int b = 0; b < 4; b++) {
-                uint64_t x = vv ^ tab->out[(o[0] >> (8 * b)) & 0xFFu];
-                const uint32_t idx = static_cast<uint32_t>(x >> shift) & 0xFFu;
-                x = (x << 8) | ((e[0] >> (8 * b)) & 0xFFu);
-                vv = x ^ tab->mod[idx];
+                vv = roll(vv, (o[0] >> (8 * b)) & 0xFFu, (e[0] >> (8 * b)) & 0xFFu);
                 const int i = 4 * j + b;
-                if (first == 64 && (static_cast<uint32_t>(vv) & mask) == 0 && i >= lo && i <= hi)
+                if (first == 4 * N && (static_cast<uint32_t>(vv) & mask) == 0 && i >= lo && i <= hi)
                     first = static_cast<uint32_t>(i);
             }
 #pragma unroll
-            for (int k = 0; k < 15; k++) { e[k] = e[k + 1]; o[k] = o[k + 1]; }
+            for (int k = 0; k < N - 1; k++) {
+                e[k] = e[k + 1];
+                o[k] = o[k + 1];
+            }
         }
         return first;
     }
@@ -268,7 +275,7 @@ struct Rabin {
 
 // --------------------------------------------------------- region scanner
 // First candidate coordinate in [lo, hi] (inclusive, lo <= hi), or -1.
-// Wave-uniform in and out.  `H` is a prepared hash (tables + mask), copied per tile.
+// Wave-uniform in and out.  `H` is a prepared hash (tables + mask).
 template <class H>
 __device__ int64_t scan_region(H hash, const uint8_t* abase, int64_t off0, int64_t nbytes_coord, int64_t lo,
                                int64_t hi, int lane) {
@@ -276,69 +283,63 @@ __device__ int64_t scan_region(H hash, const uint8_t* abase, int64_t off0, int64
     while (ct <= hi) {
         const int64_t rem = hi - ct + 1;
         int64_t per = (rem + kWave - 1) / kWave;
-        per = (per + 63) & ~int64_t(63);
+        per = (per + kBlk - 1) / kBlk * kBlk;
         const int64_t L = per < kLaneMax ? per : kLaneMax;
         const int64_t tb = ct >= 64 ? ct - 64 : 0;
         const Loader ld = make_loader(abase, off0, nbytes_coord, tb);
 
         const int64_t c0 = ct + lane * L;
-        const int nb = static_cast<int>(L >> 6);
+        const int nb = static_cast<int>(L / kBlk);
         int64_t found = -1;
         if (c0 <= hi) {
-            uint32_t cur[16], nxt[16];
-            hash.clear();
-            ld.load(c0 - 64, cur);
-            hash.template block<kWarm>(cur, 0, 0);  // 64-byte warm-up: h = hash of the window before c0
+            uint32_t cur[kNdw], nxt[kNdw];
+            {
+                uint32_t w[16];
+                hash.clear();
+                ld.load(c0 - 64, w);
+                hash.template block<kWarm>(w);  // h = hash of the 64-byte window before c0
+            }
             ld.load(c0, cur);
             int k = 0;
             for (;;) {
-                // fast scan: running min of (h & mask) per 64-byte block
                 bool hit = false;
                 typename H::State st0 = hash.save();
                 for (; k < nb; k++) {
-                    if (c0 + 64 * k > hi) break;
-#ifndef KCDC_EXP_NOPREFETCH
-                    if (k + 1 < nb) ld.load(c0 + 64 * (k + 1), nxt);
-#else
-                    ld.load(c0 + 64 * (k + 1), nxt);
-#endif
+                    if (c0 + kBlk * k > hi) break;
+                    if (k + 1 < nb) ld.load(c0 + kBlk * (k + 1), nxt);
                     st0 = hash.save();
-                    if (hash.template block<kFast>(cur, 0, 63) == 0) {
+                    if (hash.template block<kFast>(cur) == 0) {
                         hit = true;
                         break;
                     }
 #pragma unroll
-                    for (int i = 0; i < 16; i++) cur[i] = nxt[i];
+                    for (int i = 0; i < kNdw; i++) cur[i] = nxt[i];
                 }
                 if (!hit) break;
-#ifdef KCDC_EXP_NOEXACT
-                found = c0 + 64 * k; break;
-#endif
-                // rare: re-run block k exactly, in place (ends in the same state)
-                const int64_t c = c0 + 64 * k;
+                // rare: re-run step k exactly (the fast pass already left the end state)
+                const int64_t c = c0 + kBlk * k;
                 uint32_t prv[16];
                 ld.load(c - 64, prv);
                 const int64_t blo = lo - c, bhi = hi - c;
                 const uint32_t idx = hash.exact(st0, prv, cur, blo < 0 ? 0 : static_cast<int>(blo),
-                                                bhi > 63 ? 63 : static_cast<int>(bhi));
-                if (idx < 64) {
+                                                bhi > kBlk - 1 ? kBlk - 1 : static_cast<int>(bhi));
+                if (idx < static_cast<uint32_t>(kBlk)) {
                     found = c + idx;
                     break;
                 }
                 if (++k >= nb) break;
-                ld.load(c0 + 64 * k, cur);
+                ld.load(c0 + kBlk * k, cur);
             }
         }
         const uint64_t hit = __ballot(found >= 0);
         if (hit) {
             const int first = __builtin_ctzll(hit);
-            return uni64(static_cast<uint64_t>(__shfl(found, first)));
+            return static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, first))));
         }
         ct += kWave * L;
     }
     return -1;
 }
-
 
 // ------------------------------------------------------------ batch kernel
 struct BatchArgs {
@@ -347,6 +348,7 @@ struct BatchArgs {
     uint64_t* cuts;
     const uint64_t* cut_base;
     uint64_t* counts;
+    uint32_t* queue;  // persistent-wave work counter (zeroed before each launch)
     uint64_t cuts_cap;
     uint64_t min_size, max_size;
     const uint32_t* buz;
@@ -400,16 +402,9 @@ __device__ __forceinline__ auto make_hash(HashSmem<KIND>& sm, const BatchArgs& a
     }
 }
 
-// One wavefront per stream: walk the stream chunk by chunk.
-template <int KIND>
-__global__ __launch_bounds__(kWavesPerWG * kWave, 4) void split_batch_kernel(BatchArgs a) {
-    __shared__ HashSmem<KIND> sm;
-    fill_tables<KIND>(sm, a);
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uint32_t sid = blockIdx.x * kWavesPerWG + wave;
-    if (sid >= a.nstreams) return;
-
+// Split one stream (wave-uniform sid): walk it chunk by chunk.
+template <class H>
+__device__ __forceinline__ void split_one(const BatchArgs& a, const H& hash, uint32_t sid, int lane) {
     const uint64_t p = uni64(reinterpret_cast<uint64_t>(a.ptrs[sid]));
     const int64_t n = static_cast<int64_t>(uni64(a.lens[sid]));
     const uint64_t cb = uni64(a.cut_base[sid]);
@@ -418,8 +413,6 @@ __global__ __launch_bounds__(kWavesPerWG * kWave, 4) void split_batch_kernel(Bat
     const int64_t off0 = static_cast<int64_t>(p & 15u);
     const uint8_t* abase = reinterpret_cast<const uint8_t*>(p - static_cast<uint64_t>(off0));
     const int64_t mn = static_cast<int64_t>(a.min_size), mx = static_cast<int64_t>(a.max_size);
-    auto hash = make_hash<KIND>(sm, a, lane);
-
     int64_t s = 0;
     uint64_t cnt = 0;
     while (s < n) {
@@ -444,6 +437,22 @@ __global__ __launch_bounds__(kWavesPerWG * kWave, 4) void split_batch_kernel(Bat
     if (lane == 0) a.counts[sid] = cnt;
 }
 
+// Persistent waves; each pulls the next stream id from the queue counter.
+template <int KIND>
+__global__ __launch_bounds__(kBatchWaves * kWave, kBatchWaves / 4) void split_batch_kernel(BatchArgs a) {
+    __shared__ HashSmem<KIND> sm;
+    fill_tables<KIND>(sm, a);
+    const int lane = threadIdx.x & (kWave - 1);
+    const auto hash = make_hash<KIND>(sm, a, lane);
+    for (;;) {
+        uint32_t sid = 0;
+        if (lane == 0) sid = atomicAdd(a.queue, 1u);
+        sid = __builtin_amdgcn_readfirstlane(sid);
+        if (sid >= a.nstreams) break;
+        split_one(a, hash, sid, lane);
+    }
+}
+
 // FIXED-*: cuts every chunk length (splitter_fixed.go:15-26); reads no data.
 __global__ void split_fixed_kernel(BatchArgs a) {
     const uint32_t sid = blockIdx.x;
@@ -466,7 +475,7 @@ __global__ __launch_bounds__(kWave) void scan_first_kernel(BatchArgs a, const ui
     __shared__ HashSmem<KIND> sm;
     fill_tables<KIND>(sm, a);
     const int lane = threadIdx.x & (kWave - 1);
-    auto hash = make_hash<KIND>(sm, a, lane);
+    const auto hash = make_hash<KIND>(sm, a, lane);
     const int64_t f = scan_region(hash, buf, 0, len, lo, hi, lane);
     if (lane == 0) out[0] = f;
 }
@@ -497,17 +506,16 @@ __global__ void fill_prng_kernel(uint8_t* data, uint64_t stride, uint64_t len, u
     }
 }
 
-
 // ------------------------------------------- long single stream (config 3)
-// Phase 1: every 64 KiB segment is scanned by one wave (lane l: 1 KiB sub-range,
-// 64-byte warm-up), which stores the segment's first kSegK candidate positions
-// and whether it had more ("truncated").  Phase 2: exclusive prefix sum of the
-// stored counts.  Phase 3: compaction into one sorted candidate list.  Phase 4:
-// one wave walks the chunk rule over that list from LDS windows; where a
-// truncated (candidate-dense) segment may hide the candidate it needs, it rescans
-// that range with the same scan_region() the batch kernel uses.  The cut set is
-// therefore exactly the sequential one, for any data.
-constexpr int64_t kSegBytes = kWave * kLaneMax;  // 64 KiB
+// Phase 1: every 128 KiB segment (in coordinates) is scanned by one wave (lane
+// l: a 2 KiB sub-range with a 64-byte warm-up), which stores the segment's first
+// kSegK candidate positions and whether it had more ("truncated").  Phase 2:
+// exclusive prefix sum of the stored counts.  Phase 3: compaction into one
+// sorted candidate list.  Phase 4: one wave walks the chunk rule over that list
+// from LDS windows; where a truncated (candidate-dense) segment may hide the
+// candidate it needs, it rescans that range with the same scan_region() the
+// batch kernel uses.  The cut set is therefore exactly the sequential one.
+constexpr int64_t kSegBytes = kWave * kLaneMax;  // 128 KiB
 constexpr int kSegK = 4;
 constexpr uint64_t kTruncBit = 1ull << 63;
 
@@ -527,17 +535,17 @@ struct LongArgs {
 };
 
 template <int KIND>
-__global__ __launch_bounds__(kWavesPerWG * kWave, 4) void cand_scan_kernel(BatchArgs a, LongArgs g) {
+__global__ __launch_bounds__(kScanWaves * kWave, 2) void cand_scan_kernel(BatchArgs a, LongArgs g) {
     __shared__ HashSmem<KIND> sm;
     fill_tables<KIND>(sm, a);
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const int64_t seg = static_cast<int64_t>(blockIdx.x) * kWavesPerWG + wave;
+    const int64_t seg = static_cast<int64_t>(blockIdx.x) * kScanWaves + wave;
     if (seg >= g.nseg) return;
     auto hash = make_hash<KIND>(sm, a, lane);
     // Segments tile COORDINATES (position + off0) so every lane sub-range is 16-byte aligned.
     const int64_t cs = seg * kSegBytes;
-    const int64_t lo = cs > g.off0 ? cs : g.off0;                                   // first coordinate tested
+    const int64_t lo = cs > g.off0 ? cs : g.off0;                                             // first tested
     const int64_t hi = (cs + kSegBytes < g.off0 + g.n ? cs + kSegBytes : g.off0 + g.n) - 1;  // inclusive
     const int64_t tb = cs >= 64 ? cs - 64 : 0;
     const Loader ld = make_loader(g.abase, g.off0, g.off0 + g.n, tb);
@@ -545,31 +553,34 @@ __global__ __launch_bounds__(kWavesPerWG * kWave, 4) void cand_scan_kernel(Batch
     uint32_t found[kSegK];
     int nf = 0;  // candidates found by this lane (kSegK + 1 means "more than kSegK")
     if (c0 <= hi) {
-        uint32_t cur[16], nxt[16];
-        hash.clear();
-        ld.load(c0 - 64, cur);
-        hash.template block<kWarm>(cur, 0, 0);
+        uint32_t cur[kNdw], nxt[kNdw];
+        {
+            uint32_t w[16];
+            hash.clear();
+            ld.load(c0 - 64, w);
+            hash.template block<kWarm>(w);
+        }
         ld.load(c0, cur);
-        for (int k = 0; k < static_cast<int>(kLaneMax / 64) && nf <= kSegK; k++) {
-            const int64_t c = c0 + 64 * k;
+        for (int k = 0; k < static_cast<int>(kLaneMax / kBlk) && nf <= kSegK; k++) {
+            const int64_t c = c0 + kBlk * k;
             if (c > hi) break;
-            ld.load(c + 64, nxt);
+            if (k + 1 < static_cast<int>(kLaneMax / kBlk)) ld.load(c + kBlk, nxt);
             const typename decltype(hash)::State st0 = hash.save();
-            if (hash.template block<kFast>(cur, 0, 63) == 0) {
+            if (hash.template block<kFast>(cur) == 0) {
                 uint32_t prv[16];
                 ld.load(c - 64, prv);
-                const int bhi = hi - c > 63 ? 63 : static_cast<int>(hi - c);
+                const int bhi = hi - c > kBlk - 1 ? kBlk - 1 : static_cast<int>(hi - c);
                 int from = lo > c ? static_cast<int>(lo - c) : 0;
                 while (from <= bhi && nf <= kSegK) {
                     const uint32_t idx = hash.exact(st0, prv, cur, from, bhi);
-                    if (idx >= 64) break;
+                    if (idx >= static_cast<uint32_t>(kBlk)) break;
                     if (nf < kSegK) found[nf] = static_cast<uint32_t>(c - cs) + idx;
                     nf++;
                     from = static_cast<int>(idx) + 1;
                 }
             }
 #pragma unroll
-            for (int i = 0; i < 16; i++) cur[i] = nxt[i];
+            for (int i = 0; i < kNdw; i++) cur[i] = nxt[i];
         }
     }
     // exclusive prefix of per-lane counts (segments are in lane order)
@@ -583,11 +594,12 @@ __global__ __launch_bounds__(kWavesPerWG * kWave, 4) void cand_scan_kernel(Batch
     const int pre = incl - nf;
     for (int j = 0; j < nf && j < kSegK; j++)
         if (pre + j < kSegK) g.seg_cand[seg * kSegK + pre + j] = static_cast<uint64_t>(cs - g.off0) + found[j];
-    if (lane == 0) g.seg_cnt[seg] = (tot > kSegK ? 0x80000000u : 0u) | static_cast<uint32_t>(tot < kSegK ? tot : kSegK);
+    if (lane == 0)
+        g.seg_cnt[seg] = (tot > kSegK ? 0x80000000u : 0u) | static_cast<uint32_t>(tot < kSegK ? tot : kSegK);
 }
 
 // Exclusive prefix sum of stored counts (one workgroup; the long path has at most
-// a few million segments).
+// a few hundred thousand segments).
 __global__ __launch_bounds__(1024) void seg_prefix_kernel(LongArgs g) {
     __shared__ uint64_t wsum[16];
     __shared__ uint64_t carry;
@@ -596,17 +608,18 @@ __global__ __launch_bounds__(1024) void seg_prefix_kernel(LongArgs g) {
     __syncthreads();
     constexpr int kItems = 8;
     for (int64_t base = 0; base < g.nseg; base += 1024 * kItems) {
-        uint64_t v[kItems], sum = 0;
+        uint32_t v[kItems];
+        uint32_t sum = 0;
 #pragma unroll
         for (int j = 0; j < kItems; j++) {
             const int64_t i = base + static_cast<int64_t>(t) * kItems + j;
-            v[j] = i < g.nseg ? (g.seg_cnt[i] & 0x7FFFFFFFu) : 0;
+            v[j] = i < g.nseg ? (g.seg_cnt[i] & 0x7FFFFFFFu) : 0u;
             sum += v[j];
         }
-        uint64_t incl = sum;
+        uint32_t incl = sum;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t x = __shfl_up(incl, d);
+            const uint32_t x = __shfl_up(incl, d);
             if (lane >= d) incl += x;
         }
         if (lane == 63) wsum[w] = incl;
@@ -648,7 +661,7 @@ __global__ __launch_bounds__(kWave) void resolve_kernel(BatchArgs a, LongArgs g,
     __shared__ uint64_t win[kResolveWin];
     fill_tables<KIND>(sm, a);
     const int lane = threadIdx.x;
-    auto hash = make_hash<KIND>(sm, a, lane);
+    const auto hash = make_hash<KIND>(sm, a, lane);
     const int64_t total = static_cast<int64_t>(uni64(g.total[0]));
     const int64_t n = g.n;
     int64_t wbase = 0;  // list index of win[0]
@@ -695,7 +708,8 @@ __global__ __launch_bounds__(kWave) void resolve_kernel(BatchArgs a, LongArgs g,
                         ((static_cast<int64_t>(e & ~kTruncBit) + g.off0) / kSegBytes + 1) * kSegBytes - g.off0;
                     if (seg_end > lo) {
                         const int64_t rh = seg_end - 1 < hi ? seg_end - 1 : hi;
-                        const int64_t f = scan_region(hash, g.abase, g.off0, g.off0 + n, lo + g.off0, rh + g.off0, lane);
+                        const int64_t f =
+                            scan_region(hash, g.abase, g.off0, g.off0 + n, lo + g.off0, rh + g.off0, lane);
                         if (f >= 0) c = f - g.off0;
                     }
                 }
@@ -717,6 +731,7 @@ __global__ __launch_bounds__(kWave) void resolve_kernel(BatchArgs a, LongArgs g,
     }
     if (lane == 0) g.count[0] = cnt;
 }
+
 }  // namespace dev
 
 // ================================================================== host
@@ -724,17 +739,19 @@ struct DeviceTables {
     uint32_t* buz = nullptr;
     uint64_t* rk_out = nullptr;
     uint64_t* rk_mod = nullptr;
+    uint32_t* queues = nullptr;  // kQueueSlots work counters for the persistent batch kernel
+    int cus = 0;
 };
 
 namespace {
 constexpr int kMaxDevices = 64;
+constexpr int kQueueSlots = 64;  // counters stride 64 B; slot chosen round-robin per launch
 DeviceTables g_dev_tables[kMaxDevices];
 bool g_dev_ready[kMaxDevices];
+unsigned g_queue_next[kMaxDevices];
 std::mutex g_dev_mu;
 
-int hip_fail(hipError_t e, const char* what) {
-    return set_error(-5, std::string(what) + ": " + hipGetErrorString(e));
-}
+int hip_fail(hipError_t e, const char* what) { return set_error(-5, std::string(what) + ": " + hipGetErrorString(e)); }
 
 dev::BatchArgs base_args(const Algo& algo, const DeviceTables& t) {
     dev::BatchArgs a{};
@@ -761,16 +778,26 @@ const DeviceTables* device_tables(int device, int* err) {
     int prev = 0;
     (void)hipGetDevice(&prev);
     hipError_t e = hipSetDevice(device);
-    if (e != hipSuccess) { *err = hip_fail(e, "hipSetDevice"); return nullptr; }
+    if (e != hipSuccess) {
+        *err = hip_fail(e, "hipSetDevice");
+        return nullptr;
+    }
     DeviceTables d;
-    e = hipMalloc(&d.buz, sizeof(T.buz));
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, device);
+    if (e == hipSuccess) d.cus = prop.multiProcessorCount;
+    if (e == hipSuccess) e = hipMalloc(&d.buz, sizeof(T.buz));
     if (e == hipSuccess) e = hipMalloc(&d.rk_out, sizeof(T.rk_out));
     if (e == hipSuccess) e = hipMalloc(&d.rk_mod, sizeof(T.rk_mod));
+    if (e == hipSuccess) e = hipMalloc(&d.queues, kQueueSlots * 64);
     if (e == hipSuccess) e = hipMemcpy(d.buz, T.buz, sizeof(T.buz), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d.rk_out, T.rk_out, sizeof(T.rk_out), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d.rk_mod, T.rk_mod, sizeof(T.rk_mod), hipMemcpyHostToDevice);
     (void)hipSetDevice(prev);
-    if (e != hipSuccess) { *err = hip_fail(e, "table upload"); return nullptr; }
+    if (e != hipSuccess) {
+        *err = hip_fail(e, "table upload");
+        return nullptr;
+    }
     g_dev_tables[device] = d;
     g_dev_ready[device] = true;
     return &g_dev_tables[device];
@@ -793,12 +820,23 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
     if (algo.kind == kFixed) {
         hipLaunchKernelGGL(dev::split_fixed_kernel, dim3(s.nstreams), dim3(256), 0, st, a);
     } else {
-        const dim3 grid((s.nstreams + dev::kWavesPerWG - 1) / dev::kWavesPerWG);
-        const dim3 block(dev::kWavesPerWG * dev::kWave);
+        unsigned slot;
+        {
+            std::lock_guard<std::mutex> lk(g_dev_mu);
+            slot = g_queue_next[device]++ % kQueueSlots;
+        }
+        a.queue = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(t->queues) + 64 * slot);
+        hipError_t e = hipMemsetAsync(a.queue, 0, sizeof(uint32_t), st);
+        if (e != hipSuccess) return hip_fail(e, "queue reset");
+        // persistent grid: one workgroup per CU (the 64 KiB table fits twice per CU),
+        // never more workgroups than the streams need
+        const unsigned need = (s.nstreams + dev::kBatchWaves - 1) / dev::kBatchWaves;
+        const unsigned wgs = need < static_cast<unsigned>(t->cus) ? need : static_cast<unsigned>(t->cus);
+        const dim3 block(dev::kBatchWaves * dev::kWave);
         if (algo.kind == kBuzhash)
-            hipLaunchKernelGGL(dev::split_batch_kernel<kBuzhash>, grid, block, 0, st, a);
+            hipLaunchKernelGGL(dev::split_batch_kernel<kBuzhash>, dim3(wgs), block, 0, st, a);
         else
-            hipLaunchKernelGGL(dev::split_batch_kernel<kRabinKarp>, grid, block, 0, st, a);
+            hipLaunchKernelGGL(dev::split_batch_kernel<kRabinKarp>, dim3(wgs), block, 0, st, a);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "split kernel launch");
@@ -845,11 +883,16 @@ LongLayout long_layout(uint64_t len) {
     L.nseg = static_cast<int64_t>((len + 15 + dev::kSegBytes - 1) / dev::kSegBytes);  // coordinates: + off0 < 16
     const size_t ns = static_cast<size_t>(L.nseg);
     size_t o = 0;
-    L.off_cnt = o;   o += al(ns * 4);
-    L.off_cand = o;  o += al(ns * dev::kSegK * 8);
-    L.off_off = o;   o += al(ns * 8);
-    L.off_list = o;  o += al(ns * dev::kSegK * 8);
-    L.off_total = o; o += 256;
+    L.off_cnt = o;
+    o += al(ns * 4);
+    L.off_cand = o;
+    o += al(ns * dev::kSegK * 8);
+    L.off_off = o;
+    o += al(ns * 8);
+    L.off_list = o;
+    o += al(ns * dev::kSegK * 8);
+    L.off_total = o;
+    o += 256;
     L.bytes = o;
     return L;
 }
@@ -890,15 +933,15 @@ int launch_split_long(const Algo& algo, const uint8_t* d_data, uint64_t len, uin
     g.cuts_cap = cuts_cap;
     g.count = d_count;
     dev::BatchArgs a = base_args(algo, *t);
-    const dim3 grid(static_cast<unsigned>((L.nseg + dev::kWavesPerWG - 1) / dev::kWavesPerWG));
-    const dim3 block(dev::kWavesPerWG * dev::kWave);
+    const dim3 grid(static_cast<unsigned>((g.nseg + dev::kScanWaves - 1) / dev::kScanWaves));
+    const dim3 block(dev::kScanWaves * dev::kWave);
     const int64_t mn = static_cast<int64_t>(algo.min_size()), mx = static_cast<int64_t>(algo.max_size());
     if (algo.kind == kBuzhash)
         hipLaunchKernelGGL(dev::cand_scan_kernel<kBuzhash>, grid, block, 0, st, a, g);
     else
         hipLaunchKernelGGL(dev::cand_scan_kernel<kRabinKarp>, grid, block, 0, st, a, g);
     hipLaunchKernelGGL(dev::seg_prefix_kernel, dim3(1), dim3(1024), 0, st, g);
-    hipLaunchKernelGGL(dev::compact_kernel, dim3(static_cast<unsigned>((L.nseg + 255) / 256)), dim3(256), 0, st, g);
+    hipLaunchKernelGGL(dev::compact_kernel, dim3(static_cast<unsigned>((g.nseg + 255) / 256)), dim3(256), 0, st, g);
     if (algo.kind == kBuzhash)
         hipLaunchKernelGGL(dev::resolve_kernel<kBuzhash>, dim3(1), dim3(dev::kWave), 0, st, a, g, mn, mx);
     else
