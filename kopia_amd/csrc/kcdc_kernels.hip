@@ -40,12 +40,21 @@ namespace dev {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWave = 64;
+#ifndef KCDC_TRING
+#define KCDC_TRING 1
+#endif
+#ifndef KCDC_XOR3_ASM
+#define KCDC_XOR3_ASM 0
+#endif
 #ifndef KCDC_BLK
 #define KCDC_BLK 128
 #endif
 constexpr int kBlk = KCDC_BLK;          // bytes per lane per step (a multiple of 64)
 constexpr int kNdw = kBlk / 4;          // dwords per lane per step
-constexpr int64_t kLaneMax = 2048;      // max bytes per lane segment (tile = 128 KiB)
+#ifndef KCDC_LANE_MAX
+#define KCDC_LANE_MAX 2048
+#endif
+constexpr int64_t kLaneMax = KCDC_LANE_MAX;  // max bytes per lane segment (tile = 64 x kLaneMax)
 #ifndef KCDC_BATCH_WAVES
 #define KCDC_BATCH_WAVES 8
 #endif
@@ -56,9 +65,21 @@ constexpr int kScanWaves = 8;                  // waves per workgroup, long-path
 #endif
 constexpr int kSchedWindow = KCDC_SCHED_WINDOW;  // bytes per scheduling window in the hash loop
 
+
 enum Mode { kWarm = 0, kFast = 1 };
 
 __device__ __forceinline__ uint32_t rotl1(uint32_t h) { return __builtin_amdgcn_alignbit(h, h, 31); }
+
+// h' = rotl(h,1) ^ a ^ b as ONE v_xor3 (hipcc otherwise splits it into xor + bitop3).
+__device__ __forceinline__ uint32_t roll3(uint32_t h, uint32_t a, uint32_t b) {
+#if KCDC_XOR3_ASM && defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_xor3_b32 %0, %1, %2, %3" : "=v"(r) : "v"(rotl1(h)), "v"(a), "v"(b));
+    return r;
+#else
+    return rotl1(h) ^ a ^ b;
+#endif
+}
 
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x));
@@ -202,6 +223,104 @@ struct Buz {
     }
 };
 
+// buzhash32 with a register T-ring: ring[j] holds T[b] of the j-th of the 64 bytes
+// before the current step, so each byte costs ONE table read (the entering byte);
+// the leaving byte's value comes from the ring (first half of a 128-byte step) or
+// from the step's own first half (second half), and the second half refills the
+// ring in place.  No register rotation at the step boundary: ring[j] dies at byte
+// j and is reborn at byte 64+j.
+struct BuzRing {
+    const char* tab;
+    uint32_t lane4;
+    uint32_t mask;
+    uint32_t h;
+    uint32_t ring[64];
+    using State = uint32_t;
+    __device__ __forceinline__ State save() const { return h; }
+    __device__ __forceinline__ uint32_t look(uint32_t dwv, int k) const {
+        const uint32_t a = __builtin_amdgcn_perm(dwv, lane4, 0x0c0c0000u | ((4u + k) << 8));
+        return *reinterpret_cast<const uint32_t*>(tab + a);
+    }
+    __device__ __forceinline__ void clear() {
+        h = 0;
+#pragma unroll
+        for (int i = 0; i < 64; i++) ring[i] = 0;
+    }
+    template <int MODE, int N>
+    __device__ __forceinline__ uint32_t block(const uint32_t (&dw)[N]) {
+        static_assert(N == 16 || N == 32, "T-ring steps are 64 or 128 bytes");
+        uint32_t m = 0xFFFFFFFFu;
+        if constexpr (MODE == kWarm) {  // 64 bytes on a zero history: G-recurrence warm-up
+#pragma unroll
+            for (int i = 0; i < 64; i++) {
+                if (kSchedWindow && i % kSchedWindow == 0) __builtin_amdgcn_sched_barrier(0);
+                const uint32_t t = look(dw[i >> 2], i & 3);
+                h = rotl1(h) ^ t;
+                ring[i] = t;
+            }
+            return m;
+        } else if constexpr (N == 16) {
+#pragma unroll
+            for (int i = 0; i < 64; i++) {
+                if (kSchedWindow && i % kSchedWindow == 0) __builtin_amdgcn_sched_barrier(0);
+                const uint32_t t = look(dw[i >> 2], i & 3);
+                h = roll3(h, ring[i], t);
+                ring[i] = t;
+                m = min(m, h & mask);
+                if ((i & 3) == 3) asm volatile("" : "+v"(m));
+            }
+            return m;
+        } else {
+            uint32_t loc[64];
+#pragma unroll
+            for (int i = 0; i < 64; i++) {
+                if (kSchedWindow && i % kSchedWindow == 0) __builtin_amdgcn_sched_barrier(0);
+                const uint32_t t = look(dw[i >> 2], i & 3);
+                h = roll3(h, ring[i], t);
+                loc[i] = t;
+                m = min(m, h & mask);
+                if ((i & 3) == 3) asm volatile("" : "+v"(m));
+            }
+#pragma unroll
+            for (int i = 64; i < 128; i++) {
+                if (kSchedWindow && i % kSchedWindow == 0) __builtin_amdgcn_sched_barrier(0);
+                const uint32_t t = look(dw[i >> 2], i & 3);
+                h = roll3(h, loc[i - 64], t);
+                ring[i - 64] = t;
+                m = min(m, h & mask);
+                if ((i & 3) == 3) asm volatile("" : "+v"(m));
+            }
+            return m;
+        }
+    }
+    template <int N>
+    __device__ __forceinline__ uint32_t exact(State st0, const uint32_t (&prv)[16], const uint32_t (&dw)[N], int lo,
+                                              int hi) const {
+        uint32_t e[N], o[N];
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            e[j] = dw[j];
+            o[j] = j < 16 ? prv[j] : dw[j - 16];
+        }
+        uint32_t hh = st0, first = 4 * N;
+#pragma unroll 1
+        for (int j = 0; j < N; j++) {
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                hh = rotl1(hh) ^ look(o[0], b) ^ look(e[0], b);
+                const int i = 4 * j + b;
+                if (first == 4 * N && (hh & mask) == 0 && i >= lo && i <= hi) first = static_cast<uint32_t>(i);
+            }
+#pragma unroll
+            for (int k = 0; k < N - 1; k++) {
+                e[k] = e[k + 1];
+                o[k] = o[k + 1];
+            }
+        }
+        return first;
+    }
+};
+
 // rabinkarp64: v ^= out[b[p-64]]; idx = v >> shift; v = (v << 8 | b[p]) ^ mod[idx].
 struct RabinShared {
     uint64_t out[256];
@@ -306,14 +425,31 @@ __device__ int64_t scan_region(H hash, const uint8_t* abase, int64_t off0, int64
                 typename H::State st0 = hash.save();
                 for (; k < nb; k++) {
                     if (c0 + kBlk * k > hi) break;
+#ifndef KCDC_EXP_COMPONLY
                     if (k + 1 < nb) ld.load(c0 + kBlk * (k + 1), nxt);
+#endif
                     st0 = hash.save();
+#ifdef KCDC_EXP_MEMONLY  // ablation: loads only, no hashing (timing experiments)
+                    {
+                        uint32_t x = 1;
+#pragma unroll
+                        for (int i = 0; i < kNdw; i++) x |= cur[i];
+                        asm volatile("" : "+v"(x));
+                        if (x == 0) { hit = true; break; }
+                    }
+#else
                     if (hash.template block<kFast>(cur) == 0) {
                         hit = true;
                         break;
                     }
+#endif
+#ifndef KCDC_EXP_COMPONLY
 #pragma unroll
                     for (int i = 0; i < kNdw; i++) cur[i] = nxt[i];
+#else
+#pragma unroll
+                    for (int i = 0; i < kNdw; i++) cur[i] = cur[i] * 0x9E3779B1u + 1u;  // fresh bytes, no loads
+#endif
                 }
                 if (!hit) break;
                 // rare: re-run step k exactly (the fast pass already left the end state)
@@ -386,7 +522,11 @@ __device__ __forceinline__ void fill_tables(HashSmem<KIND>& sm, const BatchArgs&
 template <int KIND>
 __device__ __forceinline__ auto make_hash(HashSmem<KIND>& sm, const BatchArgs& a, int lane) {
     if constexpr (KIND == kBuzhash) {
+#if KCDC_TRING
+        BuzRing h;
+#else
         Buz h;
+#endif
         h.tab = reinterpret_cast<const char*>(sm.s.tab);
         h.lane4 = static_cast<uint32_t>(lane) * 4u;
         h.mask = a.mask;
@@ -444,10 +584,14 @@ __global__ __launch_bounds__(kBatchWaves * kWave, kBatchWaves / 4) void split_ba
     fill_tables<KIND>(sm, a);
     const int lane = threadIdx.x & (kWave - 1);
     const auto hash = make_hash<KIND>(sm, a, lane);
-    for (;;) {
-        uint32_t sid = 0;
-        if (lane == 0) sid = atomicAdd(a.queue, 1u);
-        sid = __builtin_amdgcn_readfirstlane(sid);
+    // Bounded: a wave can never take more than nstreams tickets (exit guaranteed).
+    for (uint32_t iter = 0; iter <= a.nstreams; iter++) {
+        // Lane 0 takes a ticket; broadcast it with an explicit cross-lane read.  (A bare
+        // readfirstlane of the lane-0-only atomic result is folded away by hipcc after
+        // its atomic optimizer rewrites the add, leaving lanes 1..63 with a stale id.)
+        uint32_t got = 0;
+        if (lane == 0) got = atomicAdd(a.queue, 1u);
+        const uint32_t sid = __builtin_amdgcn_readfirstlane(__shfl(got, 0));
         if (sid >= a.nstreams) break;
         split_one(a, hash, sid, lane);
     }

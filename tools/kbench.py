@@ -70,3 +70,16 @@ for r in range(args.rounds):
 res = {k: {"median_ms": float(np.median(v)), "min_ms": float(np.min(v)),
            "GiBps": ns * L / (1 << 30) / (np.median(v) * 1e-3)} for k, v in times.items()}
 print(json.dumps(res, indent=1))
+
+# reference: coalesced streaming read of the same 16 GiB with torch (sum of int64)
+x = data.view(torch.int64)
+x.sum()
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record(stream)
+for _ in range(3):
+    x.sum()
+e1.record(stream)
+torch.cuda.synchronize()
+ms = e0.elapsed_time(e1) / 3
+print(f"torch.sum over {ns * L / 2**30:.0f} GiB: {ms:.3f} ms = {ns * L / ms / 1e9:.0f} GB/s")
