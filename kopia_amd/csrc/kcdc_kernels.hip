@@ -293,6 +293,27 @@ struct BuzRing {
             return m;
         }
     }
+    // Half-steps of a 128-byte step for the LDS-DMA path (the two 64-byte pieces arrive
+    // separately): HALF 0 consumes the ring and fills loc, HALF 1 consumes loc and
+    // refills the ring.  Returns the running min of (h & mask) over the half.
+    template <int HALF>
+    __device__ __forceinline__ uint32_t half(const uint32_t (&dw)[16], uint32_t (&loc)[64], uint32_t m) {
+#pragma unroll
+        for (int i = 0; i < 64; i++) {
+            if (kSchedWindow && i % kSchedWindow == 0) __builtin_amdgcn_sched_barrier(0);
+            const uint32_t t = look(dw[i >> 2], i & 3);
+            if (HALF == 0) {
+                h = roll3(h, ring[i], t);
+                loc[i] = t;
+            } else {
+                h = roll3(h, loc[i], t);
+                ring[i] = t;
+            }
+            m = min(m, h & mask);
+            if ((i & 3) == 3) asm volatile("" : "+v"(m));
+        }
+        return m;
+    }
     template <int N>
     __device__ __forceinline__ uint32_t exact(State st0, const uint32_t (&prv)[16], const uint32_t (&dw)[N], int lo,
                                               int hi) const {
@@ -594,6 +615,193 @@ __global__ __launch_bounds__(kBatchWaves * kWave, kBatchWaves / 4) void split_ba
         const uint32_t sid = __builtin_amdgcn_readfirstlane(__shfl(got, 0));
         if (sid >= a.nstreams) break;
         split_one(a, hash, sid, lane);
+    }
+}
+
+// ------------------------------------------------ LDS-DMA fed batch path
+// The per-lane 16-byte loads of scan_region() touch 64 different cache lines per
+// instruction and are bound by the L1/L2 request rate, not HBM.  Here each
+// 64-byte piece of all 64 lane segments is fetched by 4 LDS-DMA instructions
+// (buffer_load_dwordx4 ... lds): DMA lane d of instruction i fetches chunk
+// (d&3)^((l>>2)&3) of lane l = 16i + d/4, so every 64-byte run is one coalesced
+// request, and lane l later reads chunk j at LDS granule 4l + (j ^ ((l>>2)&3)),
+// which makes every ds_read_b128 lane group hit 16 distinct 16-byte bank slots.
+// Two 4 KiB slots per wave: piece 2n (first half of step n) and 2n+1 (second
+// half); each half's DMA is issued one half-step before it is read.
+#ifndef KCDC_DMA
+#define KCDC_DMA 0
+#endif
+#ifndef KCDC_DMA_WAVES
+#define KCDC_DMA_WAVES 12
+#endif
+constexpr int kDmaWaves = KCDC_DMA_WAVES;
+constexpr int kSlot = 64 * kWave;  // 4 KiB: one 64-byte piece of every lane
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+struct DmaSmem {
+    BuzShared tab;
+    __attribute__((aligned(16))) uint8_t slot0[kDmaWaves][kSlot];
+    __attribute__((aligned(16))) uint8_t slot1[kDmaWaves][kSlot];
+};
+
+__device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t rsrc, int64_t tb, uint8_t* slot, int64_t ct,
+                                          int64_t L, int64_t piece, int lane) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int l = 16 * i + (lane >> 2);
+        const int jj = (lane & 3) ^ ((l >> 2) & 3);
+        const int64_t coord = ct + l * L + 64 * piece + 16 * jj;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(slot + 1024 * i), 16,
+                                                 static_cast<int>(coord - tb), 0, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void read_piece(const uint8_t* slot, int lane, int64_t c, int64_t off0,
+                                           uint32_t (&dw)[16]) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int q = 4 * lane + (j ^ ((lane >> 2) & 3));
+        const u32x4 v = *reinterpret_cast<const u32x4*>(slot + 16 * q);
+        dw[4 * j + 0] = v.x;
+        dw[4 * j + 1] = v.y;
+        dw[4 * j + 2] = v.z;
+        dw[4 * j + 3] = v.w;
+    }
+    if (c == 0 && off0) {  // bytes before the stream start are virtual zeros
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            const int64_t keep_from = off0 - 4 * d;
+            const uint32_t m = keep_from <= 0 ? 0xFFFFFFFFu
+                                              : (keep_from >= 4 ? 0u : (0xFFFFFFFFu << (8 * keep_from)));
+            dw[d] &= m;
+        }
+    }
+}
+
+// scan_region() with LDS-DMA feeding; buzhash T-ring only.  Wave-uniform control
+// flow around every DMA (DMA lanes fetch for other lanes).
+__device__ int64_t scan_region_dma(BuzRing hash, uint8_t* s0, uint8_t* s1, const uint8_t* abase, int64_t off0,
+                                   int64_t nbytes_coord, int64_t lo, int64_t hi, int lane) {
+    int64_t ct = lo & ~int64_t(127);
+    while (ct <= hi) {
+        const int64_t rem = hi - ct + 1;
+        int64_t per = (rem + kWave - 1) / kWave;
+        per = (per + 127) & ~int64_t(127);
+        const int64_t L = per < kLaneMax ? per : kLaneMax;
+        const int64_t tb = ct >= 64 ? ct - 64 : 0;
+        const Loader ld = make_loader(abase, off0, nbytes_coord, tb);
+        const int64_t c0 = ct + lane * L;
+        const int nb = static_cast<int>(L / 128);
+        int64_t found = -1;
+
+        // Explicit counted waits: hipcc does not track these LDS-DMAs across the loop
+        // (it emitted no vmcnt before the slot reads), so every slot read is preceded by
+        // s_waitcnt vmcnt(4) (the other slot's 4 DMAs may stay in flight) or vmcnt(0).
+        dma_piece(ld.rsrc, tb, s1, ct, L, -1, lane);
+        dma_piece(ld.rsrc, tb, s0, ct, L, 0, lane);
+        uint32_t dw[16], loc[64];
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        read_piece(s1, lane, c0 - 64, off0, dw);
+        hash.clear();
+        hash.template block<kWarm>(dw);
+        __builtin_amdgcn_sched_barrier(0);
+        dma_piece(ld.rsrc, tb, s1, ct, L, 1, lane);
+        for (int n = 0; n < nb; n++) {
+            const int64_t c = c0 + 128 * n;
+            const typename BuzRing::State st0 = hash.save();
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // piece 2n landed (2n+1 may be in flight)
+            read_piece(s0, lane, c, off0, dw);
+            uint32_t m = hash.template half<0>(dw, loc, 0xFFFFFFFFu);
+            __builtin_amdgcn_sched_barrier(0);
+            if (n + 1 < nb) {
+                dma_piece(ld.rsrc, tb, s0, ct, L, 2 * n + 2, lane);
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // piece 2n+1 landed
+            } else {
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            read_piece(s1, lane, c + 64, off0, dw);
+            m = hash.template half<1>(dw, loc, m);
+            __builtin_amdgcn_sched_barrier(0);
+            if (n + 1 < nb) dma_piece(ld.rsrc, tb, s1, ct, L, 2 * n + 3, lane);
+            if (m == 0 && found < 0 && c <= hi) {  // rare: exact re-run from global memory
+                uint32_t prv[16], cur[32];
+                ld.load(c - 64, prv);
+                ld.load(c, cur);
+                const int64_t blo = lo - c, bhi = hi - c;
+                const uint32_t idx = hash.exact(st0, prv, cur, blo < 0 ? 0 : static_cast<int>(blo),
+                                                bhi > 127 ? 127 : static_cast<int>(bhi));
+                if (idx < 128u) found = c + idx;
+            }
+        }
+        // drain this tile's DMAs before the slots are reused
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint64_t hit = __ballot(found >= 0);
+        if (hit) {
+            const int first = __builtin_ctzll(hit);
+            return static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, first))));
+        }
+        ct += kWave * L;
+    }
+    return -1;
+}
+
+__device__ __forceinline__ void split_one_dma(const BatchArgs& a, const BuzRing& hash, uint8_t* s0, uint8_t* s1,
+                                              uint32_t sid, int lane) {
+    const uint64_t p = uni64(reinterpret_cast<uint64_t>(a.ptrs[sid]));
+    const int64_t n = static_cast<int64_t>(uni64(a.lens[sid]));
+    const uint64_t cb = uni64(a.cut_base[sid]);
+    const uint64_t cend = sid + 1 < a.nstreams ? uni64(a.cut_base[sid + 1]) : a.cuts_cap;
+    const uint64_t cap = cend > cb ? cend - cb : 0;
+    const int64_t off0 = static_cast<int64_t>(p & 15u);
+    const uint8_t* abase = reinterpret_cast<const uint8_t*>(p - static_cast<uint64_t>(off0));
+    const int64_t mn = static_cast<int64_t>(a.min_size), mx = static_cast<int64_t>(a.max_size);
+    int64_t s = 0;
+    uint64_t cnt = 0;
+    while (s < n) {
+        const int64_t pf = s + mn - 1;
+        int64_t next;
+        if (pf >= n) {
+            next = n;
+        } else {
+            const int64_t pl = s + mx - 1 < n - 1 ? s + mx - 1 : n - 1;
+            const int64_t f = scan_region_dma(hash, s0, s1, abase, off0, off0 + n, pf + off0, pl + off0, lane);
+            if (f >= 0)
+                next = f - off0 + 1;
+            else if (s + mx - 1 <= n - 1)
+                next = s + mx;
+            else
+                next = n;
+        }
+        if (lane == 0 && cnt < cap) a.cuts[cb + cnt] = static_cast<uint64_t>(next);
+        cnt++;
+        s = next;
+    }
+    if (lane == 0) a.counts[sid] = cnt;
+}
+
+__global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_dma_kernel(BatchArgs a) {
+    __shared__ DmaSmem sm;
+    for (uint32_t i = threadIdx.x; i < 256u * 64u; i += blockDim.x) sm.tab.tab[i] = a.buz[i >> 6];
+    __syncthreads();
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    BuzRing hash;
+    hash.tab = reinterpret_cast<const char*>(sm.tab.tab);
+    hash.lane4 = static_cast<uint32_t>(lane) * 4u;
+    hash.mask = a.mask;
+    hash.h = 0;
+    uint8_t* s0 = sm.slot0[wave];
+    uint8_t* s1 = sm.slot1[wave];
+    for (uint32_t iter = 0; iter <= a.nstreams; iter++) {
+        uint32_t got = 0;
+        if (lane == 0) got = atomicAdd(a.queue, 1u);
+        const uint32_t sid = __builtin_amdgcn_readfirstlane(__shfl(got, 0));
+        if (sid >= a.nstreams) break;
+        split_one_dma(a, hash, s0, s1, sid, lane);
     }
 }
 
@@ -974,13 +1182,20 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         if (e != hipSuccess) return hip_fail(e, "queue reset");
         // persistent grid: one workgroup per CU (the 64 KiB table fits twice per CU),
         // never more workgroups than the streams need
-        const unsigned need = (s.nstreams + dev::kBatchWaves - 1) / dev::kBatchWaves;
-        const unsigned wgs = need < static_cast<unsigned>(t->cus) ? need : static_cast<unsigned>(t->cus);
-        const dim3 block(dev::kBatchWaves * dev::kWave);
-        if (algo.kind == kBuzhash)
-            hipLaunchKernelGGL(dev::split_batch_kernel<kBuzhash>, dim3(wgs), block, 0, st, a);
-        else
-            hipLaunchKernelGGL(dev::split_batch_kernel<kRabinKarp>, dim3(wgs), block, 0, st, a);
+        const unsigned cus = static_cast<unsigned>(t->cus);
+        if (algo.kind == kBuzhash && KCDC_DMA) {
+            const unsigned need = (s.nstreams + dev::kDmaWaves - 1) / dev::kDmaWaves;
+            hipLaunchKernelGGL(dev::split_batch_dma_kernel, dim3(need < cus ? need : cus),
+                               dim3(dev::kDmaWaves * dev::kWave), 0, st, a);
+        } else {
+            const unsigned need = (s.nstreams + dev::kBatchWaves - 1) / dev::kBatchWaves;
+            const dim3 block(dev::kBatchWaves * dev::kWave);
+            if (algo.kind == kBuzhash)
+                hipLaunchKernelGGL(dev::split_batch_kernel<kBuzhash>, dim3(need < cus ? need : cus), block, 0, st, a);
+            else
+                hipLaunchKernelGGL(dev::split_batch_kernel<kRabinKarp>, dim3(need < cus ? need : cus), block, 0, st,
+                                   a);
+        }
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "split kernel launch");
