@@ -46,6 +46,9 @@ constexpr int kWave = 64;
 #ifndef KCDC_XOR3_ASM
 #define KCDC_XOR3_ASM 0
 #endif
+#ifndef KCDC_LOOKAHEAD
+#define KCDC_LOOKAHEAD 0
+#endif
 #ifndef KCDC_BLK
 #define KCDC_BLK 128
 #endif
@@ -70,11 +73,12 @@ enum Mode { kWarm = 0, kFast = 1 };
 
 __device__ __forceinline__ uint32_t rotl1(uint32_t h) { return __builtin_amdgcn_alignbit(h, h, 31); }
 
-// h' = rotl(h,1) ^ a ^ b as ONE v_xor3 (hipcc otherwise splits it into xor + bitop3).
+// h' = rotl(h,1) ^ a ^ b as ONE v_bitop3 (truth table 0x96 = 3-input XOR; gfx950 has no
+// v_xor3).  hipcc otherwise emits xor + bitop3 per byte.
 __device__ __forceinline__ uint32_t roll3(uint32_t h, uint32_t a, uint32_t b) {
 #if KCDC_XOR3_ASM && defined(__HIP_DEVICE_COMPILE__)
     uint32_t r;
-    asm("v_xor3_b32 %0, %1, %2, %3" : "=v"(r) : "v"(rotl1(h)), "v"(a), "v"(b));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(rotl1(h)), "v"(a), "v"(b));
     return r;
 #else
     return rotl1(h) ^ a ^ b;
@@ -298,6 +302,38 @@ struct BuzRing {
     // refills the ring.  Returns the running min of (h & mask) over the half.
     template <int HALF>
     __device__ __forceinline__ uint32_t half(const uint32_t (&dw)[16], uint32_t (&loc)[64], uint32_t m) {
+#if KCDC_LOOKAHEAD
+        // Table reads software-pipelined one 16-byte window ahead: window w+1's 16
+        // ds_reads are issued before window w is rolled, so their LDS latency hides
+        // under window w's arithmetic (one exposed latency per 64 bytes, not per 16).
+        uint32_t tw[16], tn[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) tw[i] = look(dw[i >> 2], i & 3);
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (w < 3) {
+#pragma unroll
+                for (int i = 0; i < 16; i++) tn[i] = look(dw[(16 * (w + 1) + i) >> 2], i & 3);
+            }
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const int b = 16 * w + i;
+                if (HALF == 0) {
+                    h = roll3(h, ring[b], tw[i]);
+                    loc[b] = tw[i];
+                } else {
+                    h = roll3(h, loc[b], tw[i]);
+                    ring[b] = tw[i];
+                }
+                m = min(m, h & mask);
+                if ((i & 3) == 3) asm volatile("" : "+v"(m));
+            }
+#pragma unroll
+            for (int i = 0; i < 16; i++) tw[i] = tn[i];
+        }
+        return m;
+#endif
 #pragma unroll
         for (int i = 0; i < 64; i++) {
             if (kSchedWindow && i % kSchedWindow == 0) __builtin_amdgcn_sched_barrier(0);
@@ -713,10 +749,19 @@ __device__ int64_t scan_region_dma(BuzRing hash, uint8_t* s0, uint8_t* s1, const
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // piece 2n landed (2n+1 may be in flight)
             read_piece(s0, lane, c, off0, dw);
+#ifdef KCDC_EXP_MEMONLY
+            uint32_t m = 1;
+#pragma unroll
+            for (int i = 0; i < 16; i++) m |= dw[i];
+            asm volatile("" : "+v"(m));
+#else
             uint32_t m = hash.template half<0>(dw, loc, 0xFFFFFFFFu);
+#endif
             __builtin_amdgcn_sched_barrier(0);
             if (n + 1 < nb) {
+#ifndef KCDC_EXP_COMPONLY
                 dma_piece(ld.rsrc, tb, s0, ct, L, 2 * n + 2, lane);
+#endif
                 __builtin_amdgcn_sched_barrier(0);
                 asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // piece 2n+1 landed
             } else {
@@ -724,9 +769,17 @@ __device__ int64_t scan_region_dma(BuzRing hash, uint8_t* s0, uint8_t* s1, const
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             read_piece(s1, lane, c + 64, off0, dw);
+#ifdef KCDC_EXP_MEMONLY
+#pragma unroll
+            for (int i = 0; i < 16; i++) m |= dw[i];
+            asm volatile("" : "+v"(m));
+#else
             m = hash.template half<1>(dw, loc, m);
+#endif
             __builtin_amdgcn_sched_barrier(0);
+#ifndef KCDC_EXP_COMPONLY
             if (n + 1 < nb) dma_piece(ld.rsrc, tb, s1, ct, L, 2 * n + 3, lane);
+#endif
             if (m == 0 && found < 0 && c <= hi) {  // rare: exact re-run from global memory
                 uint32_t prv[16], cur[32];
                 ld.load(c - 64, prv);

@@ -1,0 +1,37 @@
+"""Turn a rocprofv3 `--pmc FETCH_SIZE` pass into per-launch HBM read bytes.
+
+usage: python tools/pmc_traffic.py <run_counter_collection.csv> <kernel substring> [out.json]
+
+FETCH_SIZE is reported in KiB and derives from TCC_EA0_RDREQ x 64 B; on gfx950 a
+wide (16 B/lane) read is tallied at half its bytes (/opt/skills/guides/
+MI355X_MICROARCH.md §HBM: "FETCH_SIZE reports exactly 1/2 of the bytes of a wide
+coalesced streaming read ... double it").  Both our kernels read 16 B per lane
+(buffer_load_dwordx4 / buffer_load_dwordx4 ... lds), so the correction factor 2
+is applied.  The raw KiB value is kept next to the corrected bytes.
+"""
+import csv
+import json
+import statistics
+import sys
+
+
+def main():
+    path, key = sys.argv[1], sys.argv[2]
+    out = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_traffic.json"
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if key in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE"]
+    if not vals:
+        sys.exit(f"no FETCH_SIZE rows for kernels matching {key!r}")
+    kib = statistics.median(vals)
+    try:
+        d = json.load(open(out))
+    except (OSError, ValueError):
+        d = {}
+    d[key] = {"fetch_size_kib_per_launch": kib, "correction": 2,
+              "hbm_bytes_per_launch": int(kib * 1024 * 2), "launches": len(vals), "source": path}
+    json.dump(d, open(out, "w"), indent=1)
+    print(json.dumps(d[key]))
+
+
+if __name__ == "__main__":
+    main()
