@@ -44,10 +44,10 @@ constexpr int kWave = 64;
 #define KCDC_TRING 1
 #endif
 #ifndef KCDC_XOR3_ASM
-#define KCDC_XOR3_ASM 0
+#define KCDC_XOR3_ASM 1
 #endif
 #ifndef KCDC_LOOKAHEAD
-#define KCDC_LOOKAHEAD 0
+#define KCDC_LOOKAHEAD 1
 #endif
 #ifndef KCDC_BLK
 #define KCDC_BLK 128
@@ -665,7 +665,7 @@ __global__ __launch_bounds__(kBatchWaves * kWave, kBatchWaves / 4) void split_ba
 // Two 4 KiB slots per wave: piece 2n (first half of step n) and 2n+1 (second
 // half); each half's DMA is issued one half-step before it is read.
 #ifndef KCDC_DMA
-#define KCDC_DMA 0
+#define KCDC_DMA 1
 #endif
 #ifndef KCDC_DMA_WAVES
 #define KCDC_DMA_WAVES 12
