@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <mutex>
+#include <vector>
 #include <string>
 
 #include "kcdc_internal.h"
@@ -542,6 +543,14 @@ struct BatchArgs {
     const uint64_t* cut_base;
     uint64_t* counts;
     uint32_t* queue;  // persistent-wave work counter (zeroed before each launch)
+    // Time-sliced stream queue (LDS-DMA kernel): header words kQHead (tickets taken),
+    // kQTail (streams yielded), kQDone (streams finished), kQErr (spin give-ups); ring[P]
+    // holds {push number + 1, sid} of yielded streams (0 = empty; zeroed per launch, reset
+    // on take); states[n] the yielded streams' progress.
+    uint32_t* ring;
+    uint64_t* states;
+    uint32_t ring_mask;
+    uint64_t* trace;  // KCDC_TRACE builds: per stream {start, end, workgroup | wave << 16} (else null)
     uint64_t cuts_cap;
     uint64_t min_size, max_size;
     const uint32_t* buz;
@@ -667,18 +676,37 @@ __global__ __launch_bounds__(kBatchWaves * kWave, kBatchWaves / 4) void split_ba
 #ifndef KCDC_DMA
 #define KCDC_DMA 1
 #endif
-#ifndef KCDC_DMA_WAVES
-#define KCDC_DMA_WAVES 12
+#ifndef KCDC_TRACE
+#define KCDC_TRACE 0  // timing-trace builds only (tools/trace_sched.py)
 #endif
-constexpr int kDmaWaves = KCDC_DMA_WAVES;
+#ifndef KCDC_DMA_WAVES
+// 8 waves x 2 slots (64 KiB table + 64 KiB slots; 2 waves/SIMD, no VGPR spills):
+// 4096 x 4 MiB 1.62 ms vs 12 waves 1.68, 7 waves 1.68; deeper pipelines were slower
+// (8 x 3 slots 1.68, 6 x 4 1.81, 4 x 6 2.00).
+#define KCDC_DMA_WAVES 8
+#endif
+#ifndef KCDC_DMA_SLOTS
+#define KCDC_DMA_SLOTS 2
+#endif
+constexpr int kDmaWaves = KCDC_DMA_WAVES;  // waves per workgroup (one workgroup per CU)
+constexpr int kDmaSlots = KCDC_DMA_SLOTS;  // 4 KiB LDS-DMA slots per wave (pipeline depth)
+#ifndef KCDC_YIELD_BYTES
+// Scanned bytes per visit before a stream is yielded while others wait (0 = never).
+// A hand-off costs ~30 us of wave time under full HBM load (sc1 progress stores,
+// drained waits, contended head/tail atomics), so the quantum is coarse: measured on
+// MI355X (8 waves/CU), 4096 x 4 MiB: never 1.62 ms, 512 KiB 1.69, 768 KiB 1.53,
+// 1 MiB 1.57, 2 MiB 1.69; 8192 x 8 MiB: never 8.62 ms, 768 KiB 7.58, 1 MiB 7.63.
+#define KCDC_YIELD_BYTES (768 << 10)
+#endif
+constexpr int64_t kYieldBytes = KCDC_YIELD_BYTES;
 constexpr int kSlot = 64 * kWave;  // 4 KiB: one 64-byte piece of every lane
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 struct DmaSmem {
     BuzShared tab;
-    __attribute__((aligned(16))) uint8_t slot0[kDmaWaves][kSlot];
-    __attribute__((aligned(16))) uint8_t slot1[kDmaWaves][kSlot];
+    __attribute__((aligned(16))) uint8_t slots[kDmaWaves][kDmaSlots][kSlot];
 };
+static_assert(sizeof(DmaSmem) <= 160 * 1024, "LDS-DMA slots + table exceed the CU's 160 KiB");
 
 __device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t rsrc, int64_t tb, uint8_t* slot, int64_t ct,
                                           int64_t L, int64_t piece, int lane) {
@@ -716,9 +744,17 @@ __device__ __forceinline__ void read_piece(const uint8_t* slot, int lane, int64_
 
 // scan_region() with LDS-DMA feeding; buzhash T-ring only.  Wave-uniform control
 // flow around every DMA (DMA lanes fetch for other lanes).
-__device__ int64_t scan_region_dma(BuzRing hash, uint8_t* s0, uint8_t* s1, const uint8_t* abase, int64_t off0,
-                                   int64_t nbytes_coord, int64_t lo, int64_t hi, int lane) {
-    int64_t ct = lo & ~int64_t(127);
+// Resumable: tiles start at ct_io (tile-aligned; lo & ~127 on a fresh scan).  After
+// each candidate-free tile `budget` is charged the tile's bytes; once it is spent the
+// scan returns kYield with ct_io = next tile.  (The caller sets an unreachable budget
+// when the stream must not be yielded: a runtime flag tested here instead pushes the
+// tile state onto the VALU path and every LDS-DMA into a waterfall loop.)
+constexpr int64_t kYield = -2;
+constexpr int64_t kNoYield = int64_t(1) << 62;
+__device__ int64_t scan_region_dma(BuzRing hash, uint8_t* sl, const uint8_t* abase, int64_t off0,
+                                   int64_t nbytes_coord, int64_t lo, int64_t hi, int lane, int64_t& ct_io,
+                                   int64_t& budget) {
+    int64_t ct = ct_io;
     while (ct <= hi) {
         const int64_t rem = hi - ct + 1;
         int64_t per = (rem + kWave - 1) / kWave;
@@ -730,56 +766,54 @@ __device__ int64_t scan_region_dma(BuzRing hash, uint8_t* s0, uint8_t* s1, const
         const int nb = static_cast<int>(L / 128);
         int64_t found = -1;
 
-        // Explicit counted waits: hipcc does not track these LDS-DMAs across the loop
-        // (it emitted no vmcnt before the slot reads), so every slot read is preceded by
-        // s_waitcnt vmcnt(4) (the other slot's 4 DMAs may stay in flight) or vmcnt(0).
-        dma_piece(ld.rsrc, tb, s1, ct, L, -1, lane);
-        dma_piece(ld.rsrc, tb, s0, ct, L, 0, lane);
+        // Pipeline of kDmaSlots 4 KiB slots: piece q (q = 0 is the 64-byte warm-up piece
+        // before each lane segment, q = 1.. the segment's pieces) lands in slot q % S and
+        // is fetched S - 1 pieces ahead of its use.  Explicit counted waits: hipcc does not
+        // track these LDS-DMAs across the loop (it emitted no vmcnt before the slot reads),
+        // so every slot read is preceded by vmcnt(4 (S-1)) (the S-1 younger pieces may stay
+        // in flight) or, in the last S-1 pieces of the tile, vmcnt(0).
+        constexpr int S = kDmaSlots;
+        const int Q = 2 * nb + 1;  // pieces in this tile
+#pragma unroll
+        for (int j = 0; j < S; j++)
+            if (j < Q) dma_piece(ld.rsrc, tb, sl + kSlot * j, ct, L, j - 1, lane);
         uint32_t dw[16], loc[64];
         __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        read_piece(s1, lane, c0 - 64, off0, dw);
+        if (S - 1 <= Q - 1)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (S - 1)) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        read_piece(sl, lane, c0 - 64, off0, dw);
         hash.clear();
         hash.template block<kWarm>(dw);
         __builtin_amdgcn_sched_barrier(0);
-        dma_piece(ld.rsrc, tb, s1, ct, L, 1, lane);
+        if (S < Q) dma_piece(ld.rsrc, tb, sl, ct, L, S - 1, lane);
+        int qs = 1 % S;  // slot of piece q
         for (int n = 0; n < nb; n++) {
             const int64_t c = c0 + 128 * n;
             const typename BuzRing::State st0 = hash.save();
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // piece 2n landed (2n+1 may be in flight)
-            read_piece(s0, lane, c, off0, dw);
-#ifdef KCDC_EXP_MEMONLY
-            uint32_t m = 1;
+            uint32_t m = 0xFFFFFFFFu;
 #pragma unroll
-            for (int i = 0; i < 16; i++) m |= dw[i];
-            asm volatile("" : "+v"(m));
+            for (int h = 0; h < 2; h++) {
+                const int q = 2 * n + 1 + h;
+                uint8_t* slot = sl + kSlot * qs;
+                __builtin_amdgcn_sched_barrier(0);
+                if (q + S - 1 <= Q - 1)
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (S - 1)) : "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                read_piece(slot, lane, c + 64 * h, off0, dw);
+#ifdef KCDC_EXP_MEMONLY
+#pragma unroll
+                for (int i = 0; i < 16; i++) m |= dw[i];
+                asm volatile("" : "+v"(m));
 #else
-            uint32_t m = hash.template half<0>(dw, loc, 0xFFFFFFFFu);
-#endif
-            __builtin_amdgcn_sched_barrier(0);
-            if (n + 1 < nb) {
-#ifndef KCDC_EXP_COMPONLY
-                dma_piece(ld.rsrc, tb, s0, ct, L, 2 * n + 2, lane);
+                m = h == 0 ? hash.template half<0>(dw, loc, m) : hash.template half<1>(dw, loc, m);
 #endif
                 __builtin_amdgcn_sched_barrier(0);
-                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // piece 2n+1 landed
-            } else {
-                __builtin_amdgcn_sched_barrier(0);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (q + S < Q) dma_piece(ld.rsrc, tb, slot, ct, L, q + S - 1, lane);
+                qs = qs + 1 == S ? 0 : qs + 1;
             }
-            read_piece(s1, lane, c + 64, off0, dw);
-#ifdef KCDC_EXP_MEMONLY
-#pragma unroll
-            for (int i = 0; i < 16; i++) m |= dw[i];
-            asm volatile("" : "+v"(m));
-#else
-            m = hash.template half<1>(dw, loc, m);
-#endif
-            __builtin_amdgcn_sched_barrier(0);
-#ifndef KCDC_EXP_COMPONLY
-            if (n + 1 < nb) dma_piece(ld.rsrc, tb, s1, ct, L, 2 * n + 3, lane);
-#endif
             if (m == 0 && found < 0 && c <= hi) {  // rare: exact re-run from global memory
                 uint32_t prv[16], cur[32];
                 ld.load(c - 64, prv);
@@ -798,12 +832,162 @@ __device__ int64_t scan_region_dma(BuzRing hash, uint8_t* s0, uint8_t* s1, const
             return static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, first))));
         }
         ct += kWave * L;
+        budget -= kWave * L;
+        if (ct <= hi && budget <= 0) {
+            ct_io = ct;
+            return kYield;
+        }
     }
     return -1;
 }
 
-__device__ __forceinline__ void split_one_dma(const BatchArgs& a, const BuzRing& hash, uint8_t* s0, uint8_t* s1,
-                                              uint32_t sid, int lane) {
+// ---------------------------------------------------- time-sliced stream queue
+// A persistent wave owns one stream at a time.  While streams are waiting for a wave
+// (the queue has a backlog) an owner yields its stream after kYieldBytes of scanning:
+// the stream's progress {s, ct, cnt} is published and the stream re-queued, so every
+// stream advances at the chip's shared rate instead of the last streams starting only
+// when the first ones finish (a measured 0.65 busy fraction for 4096 streams on 3072
+// waves, tools/trace_sched.py).  Hand-off follows cdna_hip_programming.md Guideline 16
+// R1/R2: progress words stored sc1 (relaxed agent atomics) and drained before the ring
+// entry {tag = push number + 1, sid} is stored; the taker polls its entry's tag and
+// loads the progress sc1.  Ring size P > nstreams + grid waves (host), so two live
+// tickets never share a slot; a pusher waits for its slot to be empty (reset on take).
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) uint64_t gu64;
+__device__ __forceinline__ uint32_t ld_agent(uint32_t* p) {
+    return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_agent64(uint64_t* p) {
+    return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent64(uint64_t* p, uint64_t v) {
+    __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t add_agent(uint32_t* p, uint32_t v) {
+    return __hip_atomic_fetch_add((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t bcast(uint32_t v) { return __builtin_amdgcn_readfirstlane(__shfl(v, 0)); }
+__device__ __forceinline__ uint64_t bcast64(uint64_t v) {
+    return (static_cast<uint64_t>(bcast(static_cast<uint32_t>(v >> 32))) << 32) | bcast(static_cast<uint32_t>(v));
+}
+// Header words (uint32 offsets) 2 KiB apart: hammered counters do not share DRAM pages.
+constexpr int kQHead = 0, kQDone = 512, kQTail = 1024, kQErr = 1536;
+constexpr size_t kQHeaderBytes = 8192;
+// KCDC_TRACE builds also count, in header words 1792..: [+0] yields, [+1] (unused),
+// [+2] entry-wait spins, [+3] slot-wait spins; 64-bit s_memrealtime (100 MHz) sums over
+// waves: [+4..5] in take_stream, [+6..7] in yield_stream, [+8..9] in run_stream.
+constexpr int kQStat = 1792;
+#if KCDC_TRACE
+#define KCDC_QSTAT(w, v) \
+    do { if (lane == 0) atomicAdd(a.queue + (w), (v)); } while (0)
+#define KCDC_QSTAT64(w, v) \
+    do { if (lane == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.queue + (w)), (v)); } while (0)
+#else
+#define KCDC_QSTAT(w, v) do {} while (0)
+#define KCDC_QSTAT64(w, v) do {} while (0)
+#endif
+constexpr uint32_t kSpinCap = 1u << 22;                          // give up (error word) after ~seconds
+
+struct Progress {
+    int64_t s;     // current chunk start
+    int64_t ct;    // next tile coordinate of the chunk's candidate scan (< 0: not started)
+    uint64_t cnt;  // cuts emitted
+};
+
+// Take the next stream; returns its id (progress in pr) or -1 when no stream is waiting.
+// No wave ever waits for work: when tickets taken >= initial + yielded streams, every
+// queued stream already has a taker (each yielder takes a ticket right after its push),
+// so the wave exits.  `more` reports whether streams were still waiting after this take
+// (the owner then yields after kYieldBytes; no polling while scanning).
+__device__ int64_t take_stream(const BatchArgs& a, int lane, Progress& pr, bool& more) {
+    uint32_t* q = a.queue;
+    const uint32_t n = a.nstreams;
+    uint32_t tail = 0, t = 0;
+    if (lane == 0) {
+        tail = ld_agent(q + kQTail);
+        t = n + tail > ld_agent(q + kQHead) ? add_agent(q + kQHead, 1u) : 0xFFFFFFFFu;
+    }
+    t = bcast(t);
+    if (t == 0xFFFFFFFFu) return -1;
+    tail = bcast(tail);
+    more = n + tail > t + 1;
+    if (t < n) {  // initial ticket: stream t from its start
+        pr.s = 0;
+        pr.ct = -1;
+        pr.cnt = 0;
+        return t;
+    }
+    const uint32_t e = t - n;  // the push this ticket takes
+    uint64_t* slot = reinterpret_cast<uint64_t*>(a.ring) + (e & a.ring_mask);
+    uint64_t v = 0;
+    for (uint32_t spin = 0;; spin++) {
+        uint32_t st = 0;  // 0 wait, 1 got it, 2 exit
+        if (lane == 0) {
+            v = ld_agent64(slot);
+            if (static_cast<uint32_t>(v >> 32) == e + 1u) {
+                st = 1;
+            } else if (ld_agent(q + kQDone) >= n) {
+                st = 2;
+            } else if (spin >= kSpinCap) {
+                add_agent(q + kQErr, 1u);
+                st = 2;
+            }
+        }
+        st = bcast(st);
+        if (st == 2) return -1;
+        if (st == 1) break;
+        KCDC_QSTAT(kQStat + 2, 1u);
+        __builtin_amdgcn_s_sleep(64);
+    }
+    const uint32_t sid = bcast(static_cast<uint32_t>(v));
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // progress loads stay behind the poll
+    uint64_t w0 = 0, w1 = 0, w2 = 0;
+    if (lane == 0) {
+        w0 = ld_agent64(a.states + 3ull * sid + 0);
+        w1 = ld_agent64(a.states + 3ull * sid + 1);
+        w2 = ld_agent64(a.states + 3ull * sid + 2);
+        st_agent64(slot, 0);  // free the slot for push e + P
+    }
+    pr.s = static_cast<int64_t>(bcast64(w0));
+    pr.ct = static_cast<int64_t>(bcast64(w1));
+    pr.cnt = bcast64(w2);
+    return sid;
+}
+
+// Re-queue a yielded stream with its progress.
+__device__ void yield_stream(const BatchArgs& a, int lane, uint32_t sid, const Progress& pr) {
+    uint32_t* q = a.queue;
+    KCDC_QSTAT(kQStat + 0, 1u);
+    if (lane == 0) {
+        st_agent64(a.states + 3ull * sid + 0, static_cast<uint64_t>(pr.s));
+        st_agent64(a.states + 3ull * sid + 1, static_cast<uint64_t>(pr.ct));
+        st_agent64(a.states + 3ull * sid + 2, pr.cnt);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // progress visible before the entry
+    uint32_t e = 0;
+    if (lane == 0) e = add_agent(q + kQTail, 1u);
+    e = bcast(e);
+    uint64_t* slot = reinterpret_cast<uint64_t*>(a.ring) + (e & a.ring_mask);
+    for (uint32_t spin = 0;; spin++) {
+        uint32_t st = 0;
+        if (lane == 0) {
+            if (ld_agent64(slot) == 0) {
+                st_agent64(slot, (static_cast<uint64_t>(e + 1u) << 32) | sid);
+                st = 1;
+            } else if (spin >= kSpinCap) {
+                add_agent(q + kQErr, 1u);
+                st = 1;
+            }
+        }
+        if (bcast(st)) break;
+        KCDC_QSTAT(kQStat + 3, 1u);
+        __builtin_amdgcn_s_sleep(4);
+    }
+}
+
+// Advance stream sid from pr: returns true when it is finished, false when yielded.
+__device__ __forceinline__ bool run_stream(const BatchArgs& a, const BuzRing& hash, uint8_t* sl,
+                                           uint32_t sid, Progress& pr, bool more, int lane) {
     const uint64_t p = uni64(reinterpret_cast<uint64_t>(a.ptrs[sid]));
     const int64_t n = static_cast<int64_t>(uni64(a.lens[sid]));
     const uint64_t cb = uni64(a.cut_base[sid]);
@@ -812,28 +996,33 @@ __device__ __forceinline__ void split_one_dma(const BatchArgs& a, const BuzRing&
     const int64_t off0 = static_cast<int64_t>(p & 15u);
     const uint8_t* abase = reinterpret_cast<const uint8_t*>(p - static_cast<uint64_t>(off0));
     const int64_t mn = static_cast<int64_t>(a.min_size), mx = static_cast<int64_t>(a.max_size);
-    int64_t s = 0;
-    uint64_t cnt = 0;
-    while (s < n) {
+    int64_t budget = more && kYieldBytes > 0 ? kYieldBytes : kNoYield;
+    while (pr.s < n) {
+        const int64_t s = pr.s;
         const int64_t pf = s + mn - 1;
         int64_t next;
         if (pf >= n) {
             next = n;
         } else {
             const int64_t pl = s + mx - 1 < n - 1 ? s + mx - 1 : n - 1;
-            const int64_t f = scan_region_dma(hash, s0, s1, abase, off0, off0 + n, pf + off0, pl + off0, lane);
+            if (pr.ct < 0) pr.ct = (pf + off0) & ~int64_t(127);
+            const int64_t f = scan_region_dma(hash, sl, abase, off0, off0 + n, pf + off0, pl + off0, lane, pr.ct,
+                                              budget);
+            if (f == kYield) return false;
             if (f >= 0)
                 next = f - off0 + 1;
             else if (s + mx - 1 <= n - 1)
-                next = s + mx;
+                next = s + mx;  // forced cut at max size (splitter_buzhash32.go:60-64)
             else
                 next = n;
         }
-        if (lane == 0 && cnt < cap) a.cuts[cb + cnt] = static_cast<uint64_t>(next);
-        cnt++;
-        s = next;
+        if (lane == 0 && pr.cnt < cap) a.cuts[cb + pr.cnt] = static_cast<uint64_t>(next);
+        pr.cnt++;
+        pr.s = next;
+        pr.ct = -1;
     }
-    if (lane == 0) a.counts[sid] = cnt;
+    if (lane == 0) a.counts[sid] = pr.cnt;
+    return true;
 }
 
 __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_dma_kernel(BatchArgs a) {
@@ -847,14 +1036,43 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
     hash.lane4 = static_cast<uint32_t>(lane) * 4u;
     hash.mask = a.mask;
     hash.h = 0;
-    uint8_t* s0 = sm.slot0[wave];
-    uint8_t* s1 = sm.slot1[wave];
-    for (uint32_t iter = 0; iter <= a.nstreams; iter++) {
-        uint32_t got = 0;
-        if (lane == 0) got = atomicAdd(a.queue, 1u);
-        const uint32_t sid = __builtin_amdgcn_readfirstlane(__shfl(got, 0));
-        if (sid >= a.nstreams) break;
-        split_one_dma(a, hash, s0, s1, sid, lane);
+    uint8_t* sl = sm.slots[wave][0];
+    for (;;) {
+        Progress pr;
+#if KCDC_TRACE
+        uint64_t tc = __builtin_amdgcn_s_memrealtime();
+#endif
+        bool more = false;
+        const int64_t got = take_stream(a, lane, pr, more);
+#if KCDC_TRACE
+        KCDC_QSTAT64(kQStat + 4, __builtin_amdgcn_s_memrealtime() - tc);
+        tc = __builtin_amdgcn_s_memrealtime();
+#endif
+        if (got < 0) break;
+        const uint32_t sid = static_cast<uint32_t>(got);
+#if KCDC_TRACE
+        if (lane == 0 && pr.s == 0 && pr.ct < 0) a.trace[3 * sid + 0] = __builtin_amdgcn_s_memrealtime();
+#endif
+        const bool fin = run_stream(a, hash, sl, sid, pr, more, lane);
+#if KCDC_TRACE
+        KCDC_QSTAT64(kQStat + 8, __builtin_amdgcn_s_memrealtime() - tc);
+        tc = __builtin_amdgcn_s_memrealtime();
+#endif
+        if (fin) {
+#if KCDC_TRACE
+            if (lane == 0) {
+                a.trace[3 * sid + 1] = __builtin_amdgcn_s_memrealtime();
+                a.trace[3 * sid + 2] = blockIdx.x | (wave << 16);
+            }
+#endif
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // cuts/counts stored before done
+            if (lane == 0) add_agent(a.queue + kQDone, 1u);
+        } else {
+            yield_stream(a, lane, sid, pr);
+#if KCDC_TRACE
+            KCDC_QSTAT64(kQStat + 6, __builtin_amdgcn_s_memrealtime() - tc);
+#endif
+        }
     }
 }
 
@@ -1144,14 +1362,22 @@ struct DeviceTables {
     uint32_t* buz = nullptr;
     uint64_t* rk_out = nullptr;
     uint64_t* rk_mod = nullptr;
-    uint32_t* queues = nullptr;  // kQueueSlots work counters for the persistent batch kernel
     int cus = 0;
 };
 
 namespace {
 constexpr int kMaxDevices = 64;
-constexpr int kQueueSlots = 64;  // counters stride 64 B; slot chosen round-robin per launch
+constexpr int kQueueSlots = 64;  // per-launch queue workspaces, chosen round-robin per launch
 DeviceTables g_dev_tables[kMaxDevices];
+// Queue workspace of one launch slot: header (256 B: head, tail, done, error words 64 B
+// apart) | ring (P x 8 B, P = pow2 > nstreams + grid waves) | progress (nstreams x 24 B).
+// Grow-only; a replaced buffer is retired, not freed (an earlier launch may still use it).
+struct QueueWs {
+    char* base = nullptr;
+    size_t bytes = 0;
+};
+QueueWs g_qws[kMaxDevices][kQueueSlots];
+std::vector<char*> g_retired;
 bool g_dev_ready[kMaxDevices];
 unsigned g_queue_next[kMaxDevices];
 std::mutex g_dev_mu;
@@ -1169,7 +1395,33 @@ dev::BatchArgs base_args(const Algo& algo, const DeviceTables& t) {
     a.rk_shift = static_cast<uint32_t>(tables().rk_shift);
     return a;
 }
+#if KCDC_TRACE
+char* g_last_ws = nullptr;
+uint64_t* g_trace = nullptr;
+uint64_t g_trace_n = 0;
+int trace_reserve(uint64_t nstreams) {
+    if (g_trace_n >= nstreams) return 0;
+    if (g_trace) (void)hipFree(g_trace);
+    g_trace = nullptr;
+    g_trace_n = 0;
+    if (hipMalloc(&g_trace, 3 * 8 * nstreams) != hipSuccess) return -1;
+    g_trace_n = nstreams;
+    return 0;
+}
+#endif
 }  // namespace
+
+#if KCDC_TRACE
+// Trace builds only: copy {start, end, workgroup | wave << 16} per stream of the last batch.
+extern "C" int kcdc_debug_queue_copy(uint32_t* host) {  // the last launch's queue header
+    if (!g_last_ws) return -22;
+    return hipMemcpy(host, g_last_ws, dev::kQHeaderBytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -5;
+}
+extern "C" int kcdc_debug_trace_copy(uint64_t* host, uint64_t nstreams) {
+    if (!g_trace || nstreams > g_trace_n) return -22;
+    return hipMemcpy(host, g_trace, 3 * 8 * nstreams, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -5;
+}
+#endif
 
 const DeviceTables* device_tables(int device, int* err) {
     *err = 0;
@@ -1194,7 +1446,6 @@ const DeviceTables* device_tables(int device, int* err) {
     if (e == hipSuccess) e = hipMalloc(&d.buz, sizeof(T.buz));
     if (e == hipSuccess) e = hipMalloc(&d.rk_out, sizeof(T.rk_out));
     if (e == hipSuccess) e = hipMalloc(&d.rk_mod, sizeof(T.rk_mod));
-    if (e == hipSuccess) e = hipMalloc(&d.queues, kQueueSlots * 64);
     if (e == hipSuccess) e = hipMemcpy(d.buz, T.buz, sizeof(T.buz), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d.rk_out, T.rk_out, sizeof(T.rk_out), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d.rk_mod, T.rk_mod, sizeof(T.rk_mod), hipMemcpyHostToDevice);
@@ -1225,29 +1476,59 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
     if (algo.kind == kFixed) {
         hipLaunchKernelGGL(dev::split_fixed_kernel, dim3(s.nstreams), dim3(256), 0, st, a);
     } else {
-        unsigned slot;
+        const unsigned cus = static_cast<unsigned>(t->cus);
+        const bool dma = algo.kind == kBuzhash && KCDC_DMA;
+        const unsigned wg_waves = dma ? dev::kDmaWaves : dev::kBatchWaves;
+        const unsigned need = (s.nstreams + wg_waves - 1) / wg_waves;
+        const unsigned grid = need < cus ? need : cus;
+        uint64_t ring = 1;
+        while (ring <= static_cast<uint64_t>(s.nstreams) + grid * wg_waves) ring <<= 1;
+        const size_t ring_bytes = dma ? 8 * ring : 0;
+        const size_t hdr = dev::kQHeaderBytes;
+        const size_t bytes = hdr + ring_bytes + (dma ? 24ull * s.nstreams : 0);
+        char* ws = nullptr;
         {
             std::lock_guard<std::mutex> lk(g_dev_mu);
-            slot = g_queue_next[device]++ % kQueueSlots;
+            const unsigned slot = g_queue_next[device]++ % kQueueSlots;
+            QueueWs& q = g_qws[device][slot];
+            if (q.bytes < bytes) {
+                int prev = 0;
+                (void)hipGetDevice(&prev);
+                (void)hipSetDevice(device);
+                char* nb = nullptr;
+                size_t nbytes = bytes > 2 * q.bytes ? bytes : 2 * q.bytes;
+                hipError_t e = hipMalloc(&nb, nbytes);
+                (void)hipSetDevice(prev);
+                if (e != hipSuccess) return hip_fail(e, "queue workspace");
+                if (q.base) g_retired.push_back(q.base);
+                q.base = nb;
+                q.bytes = nbytes;
+            }
+            ws = q.base;
         }
-        a.queue = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(t->queues) + 64 * slot);
-        hipError_t e = hipMemsetAsync(a.queue, 0, sizeof(uint32_t), st);
+        a.queue = reinterpret_cast<uint32_t*>(ws);
+#if KCDC_TRACE
+        g_last_ws = ws;
+#endif
+        a.ring = reinterpret_cast<uint32_t*>(ws + hdr);
+        a.states = reinterpret_cast<uint64_t*>(ws + hdr + ring_bytes);
+        a.ring_mask = static_cast<uint32_t>(ring - 1);
+#if KCDC_TRACE
+        if (trace_reserve(s.nstreams) != 0) return set_error(-12, "trace buffer");
+        a.trace = g_trace;
+#endif
+        // header + ring zeroed per launch (the ring is also left empty by every finished launch)
+        hipError_t e = hipMemsetAsync(ws, 0, hdr + ring_bytes, st);
         if (e != hipSuccess) return hip_fail(e, "queue reset");
-        // persistent grid: one workgroup per CU (the 64 KiB table fits twice per CU),
-        // never more workgroups than the streams need
-        const unsigned cus = static_cast<unsigned>(t->cus);
-        if (algo.kind == kBuzhash && KCDC_DMA) {
-            const unsigned need = (s.nstreams + dev::kDmaWaves - 1) / dev::kDmaWaves;
-            hipLaunchKernelGGL(dev::split_batch_dma_kernel, dim3(need < cus ? need : cus),
-                               dim3(dev::kDmaWaves * dev::kWave), 0, st, a);
+        // persistent grid: one workgroup per CU, never more workgroups than the streams need
+        if (dma) {
+            hipLaunchKernelGGL(dev::split_batch_dma_kernel, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0, st, a);
         } else {
-            const unsigned need = (s.nstreams + dev::kBatchWaves - 1) / dev::kBatchWaves;
             const dim3 block(dev::kBatchWaves * dev::kWave);
             if (algo.kind == kBuzhash)
-                hipLaunchKernelGGL(dev::split_batch_kernel<kBuzhash>, dim3(need < cus ? need : cus), block, 0, st, a);
+                hipLaunchKernelGGL(dev::split_batch_kernel<kBuzhash>, dim3(grid), block, 0, st, a);
             else
-                hipLaunchKernelGGL(dev::split_batch_kernel<kRabinKarp>, dim3(need < cus ? need : cus), block, 0, st,
-                                   a);
+                hipLaunchKernelGGL(dev::split_batch_kernel<kRabinKarp>, dim3(grid), block, 0, st, a);
         }
     }
     const hipError_t e = hipGetLastError();

@@ -1,0 +1,76 @@
+"""Codegen guards for the LDS-DMA batch kernel (CPU: hipcc cross-compiles gfx950).
+
+Two silent performance cliffs were hit while developing split_batch_dma_kernel
+(kopia_amd/csrc/kcdc_kernels.hip) and are pinned here:
+* a runtime flag tested inside the tile loop made hipcc treat the tile state as
+  divergent: every LDS-DMA (buffer_load ... lds, which needs SGPR operands) was
+  wrapped in a readfirstlane waterfall loop and the kernel ran at half speed;
+* scratch spills in the tile loop count in vmcnt, so the kernel's hand-counted
+  `s_waitcnt vmcnt(N)` drains the DMA prefetch (44 vmcnt(0) instead of ~20).
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "kopia_amd", "csrc", "kcdc_kernels.hip")
+HIPCC = "/opt/rocm/bin/hipcc"
+KERNEL = "_ZN4kcdc3dev22split_batch_dma_kernelENS0_9BatchArgsE"
+
+
+def _blocks(asm: str):
+    """Basic blocks of the DMA kernel: (label, [instructions])."""
+    m = re.search(rf"^{KERNEL}:(.*?)s_endpgm", asm, re.S | re.M)
+    assert m, "DMA kernel not found in the device assembly"
+    out, cur = [], ["entry", []]
+    out.append(cur)
+    for line in m.group(1).split("\n"):
+        lm = re.match(r"^(\.LBB\S+):", line)
+        if lm:
+            cur = [lm.group(1), []]
+            out.append(cur)
+        elif line.startswith("\t") and not line.strip().startswith((";", ".")):
+            cur[1].append(line.strip())
+    return out
+
+
+@pytest.fixture(scope="module")
+def dma_asm(tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    out = tmp_path_factory.mktemp("asm") / "k.s"
+    res = tmp_path_factory.mktemp("asm") / "res.txt"
+    with open(res, "w") as rf:
+        subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S", SRC,
+                        "-o", str(out), "-Rpass-analysis=kernel-resource-usage"], check=True, stderr=rf)
+    return open(out).read(), open(res).read()
+
+
+def test_dma_not_in_waterfall_loops(dma_asm):
+    asm, _ = dma_asm
+    for label, ins in _blocks(asm):
+        if any("buffer_load_dwordx4" in i and " lds" in i for i in ins):
+            assert not any(i.startswith("s_cbranch_execnz " + label) for i in ins), \
+                f"LDS-DMA in a readfirstlane waterfall loop at {label}"
+            assert not any(i.startswith("v_readfirstlane") for i in ins), f"readfirstlane next to LDS-DMA at {label}"
+
+
+def test_no_scratch_in_hash_or_dma_blocks(dma_asm):
+    asm, _ = dma_asm
+    hot = 0
+    for label, ins in _blocks(asm):
+        is_hash = sum(1 for i in ins if i.startswith("v_bitop3_b32")) >= 32
+        is_dma = any("buffer_load_dwordx4" in i and " lds" in i for i in ins)
+        hot += is_hash
+        if is_hash or is_dma:
+            assert not any(i.startswith("scratch_") for i in ins), f"scratch access in hot block {label}"
+    assert hot >= 2, "expected the two unrolled 64-byte half-steps"
+
+
+def test_no_vgpr_spills(dma_asm):
+    _, res = dma_asm
+    sect = res[res.index("Function Name: " + KERNEL):]
+    m = re.search(r"VGPRs Spill: (\d+)", sect)
+    assert m and int(m.group(1)) == 0, "VGPR spills in the DMA kernel"
