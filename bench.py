@@ -36,7 +36,7 @@ from kopia_amd import splitter as ks  # noqa: E402
 METRIC = "splitter throughput GiB/s (device-resident) at 1/2/4/8 GPU; boundaries bit-exact"
 SEED = 0x6B6F706961
 # dominant kernel per splitter kind (kcdc_kernels.hip launch_split_batch)
-BATCH_KERNEL = {0: "kcdc::dev::split_fixed_kernel", 1: "kcdc::dev::split_batch_dma_kernel",
+BATCH_KERNEL = {0: "kcdc::dev::split_fixed_kernel", 1: "kcdc::dev::split_batch_dma_kernel<true>",
                 2: "kcdc::dev::split_batch_kernel<rabinkarp>"}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 GiB = float(1 << 30)

@@ -50,6 +50,9 @@ constexpr int kWave = 64;
 #ifndef KCDC_LOOKAHEAD
 #define KCDC_LOOKAHEAD 1
 #endif
+#ifndef KCDC_LA_W
+#define KCDC_LA_W 4  // 128-byte steps: table reads issued this many bytes ahead (VGPR bound)
+#endif
 #ifndef KCDC_BLK
 #define KCDC_BLK 128
 #endif
@@ -73,14 +76,14 @@ constexpr int kSchedWindow = KCDC_SCHED_WINDOW;  // bytes per scheduling window 
 enum Mode { kWarm = 0, kFast = 1 };
 
 __device__ __forceinline__ uint32_t rotl1(uint32_t h) { return __builtin_amdgcn_alignbit(h, h, 31); }
+__device__ __forceinline__ uint32_t rotl_n(uint32_t v, uint32_t r) { return r ? (v << r) | (v >> (32 - r)) : v; }
 
 // h' = rotl(h,1) ^ a ^ b as ONE v_bitop3 (truth table 0x96 = 3-input XOR; gfx950 has no
-// v_xor3).  hipcc otherwise emits xor + bitop3 per byte.
+// v_xor3).  hipcc otherwise emits xor + bitop3 per byte.  The builtin, not inline asm:
+// the hazard recognizer pads every inline-asm VALU with an s_nop (76 per 128 bytes).
 __device__ __forceinline__ uint32_t roll3(uint32_t h, uint32_t a, uint32_t b) {
 #if KCDC_XOR3_ASM && defined(__HIP_DEVICE_COMPILE__)
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(rotl1(h)), "v"(a), "v"(b));
-    return r;
+    return __builtin_amdgcn_bitop3_b32(rotl1(h), a, b, 0x96);
 #else
     return rotl1(h) ^ a ^ b;
 #endif
@@ -301,7 +304,9 @@ struct BuzRing {
     // Half-steps of a 128-byte step for the LDS-DMA path (the two 64-byte pieces arrive
     // separately): HALF 0 consumes the ring and fills loc, HALF 1 consumes loc and
     // refills the ring.  Returns the running min of (h & mask) over the half.
-    template <int HALF>
+    // TOP (mask rotated to the top bits): the running min is over the raw hash and the
+    // caller tests m <= buz_lim; otherwise over h & mask and the caller tests m == 0.
+    template <int HALF, bool TOP>
     __device__ __forceinline__ uint32_t half(const uint32_t (&dw)[16], uint32_t (&loc)[64], uint32_t m) {
 #if KCDC_LOOKAHEAD
         // Table reads software-pipelined one 16-byte window ahead: window w+1's 16
@@ -327,7 +332,7 @@ struct BuzRing {
                     h = roll3(h, loc[b], tw[i]);
                     ring[b] = tw[i];
                 }
-                m = min(m, h & mask);
+                m = min(m, TOP ? h : h & mask);
                 if ((i & 3) == 3) asm volatile("" : "+v"(m));
             }
 #pragma unroll
@@ -346,10 +351,103 @@ struct BuzRing {
                 h = roll3(h, loc[i], t);
                 ring[i] = t;
             }
-            m = min(m, h & mask);
+            m = min(m, TOP ? h : h & mask);
             if ((i & 3) == 3) asm volatile("" : "+v"(m));
         }
         return m;
+    }
+    // A whole 128-byte step (the 128-byte-run DMA path): bytes 0..63 consume the ring and
+    // fill loc, bytes 64..127 consume loc and refill the ring (loc[b] can take ring[b]'s
+    // register).  Table reads run one 16-byte window ahead of the arithmetic.
+    // HEADMASK: positions 0..62 are or-ed with hmask before the min (a lane whose state
+    // has a stand-in history masks them with all ones; its predecessor tests them).
+    template <bool TOP, bool HEADMASK = false>
+    __device__ __forceinline__ uint32_t step128(const uint32_t (&dw)[32], uint32_t hmask = 0) {
+        constexpr int W = KCDC_LA_W;  // bytes per lookahead window
+        uint32_t loc[64];
+        uint32_t m = 0xFFFFFFFFu;
+        uint32_t tw[W], tn[W];
+#pragma unroll
+        for (int i = 0; i < W; i++) tw[i] = look(dw[i >> 2], i & 3);
+#pragma unroll
+        for (int w = 0; w < 128 / W; w++) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (w < 128 / W - 1) {
+#pragma unroll
+                for (int i = 0; i < W; i++) tn[i] = look(dw[(W * (w + 1) + i) >> 2], i & 3);
+            }
+#pragma unroll
+            for (int i = 0; i < W; i++) {
+                const int b = W * w + i;
+                if (b < 64) {
+                    h = roll3(h, ring[b], tw[i]);
+                    loc[b] = tw[i];
+                } else {
+                    h = roll3(h, loc[b - 64], tw[i]);
+                    ring[b - 64] = tw[i];
+                }
+                const uint32_t t = TOP ? h : h & mask;
+                m = min(m, HEADMASK && b < 63 ? (t | hmask) : t);
+                if ((i & 3) == 3) asm volatile("" : "+v"(m));
+            }
+#pragma unroll
+            for (int i = 0; i < W; i++) tw[i] = tn[i];
+        }
+        return m;
+    }
+    // Tile-end extension: continue into the successor lane's segment head nx (its first
+    // 64 bytes), whose first 63 positions that lane tested only against a stand-in
+    // history.  All 64 bytes are rolled (position 63 is tested twice, harmlessly) so the
+    // ring keeps its phase: ring[0] is again the oldest byte, a consistent state.
+    template <bool TOP>
+    __device__ __forceinline__ uint32_t extend64(const uint32_t (&nx)[16]) {
+        uint32_t m = 0xFFFFFFFFu;
+        uint32_t t[16];
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 16; i++) t[i] = look(nx[(16 * w + i) >> 2], i & 3);
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const int b = 16 * w + i;
+                h = roll3(h, ring[b], t[i]);
+                ring[b] = t[i];
+                m = min(m, TOP ? h : h & mask);
+                if ((i & 3) == 3) asm volatile("" : "+v"(m));
+            }
+        }
+        return m;
+    }
+    // Lane 0 takes lane 63's state (readlane/writelane); the other lanes keep theirs.
+    // Lane 0 so continues from the true state at the end of the previous tile; every other
+    // lane holds SOME consistent state (a real 64-byte history), which makes its hash
+    // exact from its 64th byte on.
+    __device__ __forceinline__ void carry_from_last_lane(bool lane0) {
+        const uint32_t hl = __builtin_amdgcn_readlane(h, kWave - 1);
+        h = lane0 ? hl : h;
+#pragma unroll
+        for (int i = 0; i < 64; i++) {
+            const uint32_t v = __builtin_amdgcn_readlane(ring[i], kWave - 1);
+            ring[i] = lane0 ? v : ring[i];
+        }
+    }
+    // Exact first candidate among positions [lo, hi] of cur (4N bytes) from a zero state
+    // warmed on the true previous 64 bytes prv (rare path; independent of the ring).
+    template <int N>
+    __device__ __forceinline__ uint32_t exact_cold(const uint32_t (&prv)[16], const uint32_t (&cur)[N], int lo,
+                                                   int hi) const {
+        uint32_t hh = 0, o[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) o[j] = prv[j];
+#pragma unroll 1
+        for (int j = 0; j < 16; j++) {
+#pragma unroll
+            for (int b = 0; b < 4; b++) hh = rotl1(hh) ^ look(o[0], b);
+#pragma unroll
+            for (int k = 0; k < 15; k++) o[k] = o[k + 1];
+        }
+        return exact(hh, prv, cur, lo, hi);
     }
     template <int N>
     __device__ __forceinline__ uint32_t exact(State st0, const uint32_t (&prv)[16], const uint32_t (&dw)[N], int lo,
@@ -557,8 +655,14 @@ struct BatchArgs {
     const uint64_t* rk_out;
     const uint64_t* rk_mod;
     uint32_t nstreams;
-    uint32_t mask;
+    uint32_t mask;     // buzhash: the candidate mask in the rotated frame (below); rabin: as is
     uint32_t rk_shift;
+    // buzhash rotated frame: the tables hold rotl(T, buz_rot), so every hash value is
+    // rotl(H, buz_rot) and the test is (h & mask) == 0 with mask = rotl(avg - 1, buz_rot).
+    // For avg a power of two buz_rot = 32 - log2(avg) moves the mask to the top bits and
+    // "candidate" becomes h <= buz_lim (= ~mask): the hot loop's test is a bare v_min3.
+    uint32_t buz_rot;
+    uint32_t buz_lim;  // ~mask when mask is a top-bits mask (else unused)
 };
 
 template <int KIND>
@@ -575,7 +679,7 @@ struct HashSmem<kRabinKarp> {
 template <int KIND>
 __device__ __forceinline__ void fill_tables(HashSmem<KIND>& sm, const BatchArgs& a) {
     if constexpr (KIND == kBuzhash) {
-        for (uint32_t i = threadIdx.x; i < 256u * 64u; i += blockDim.x) sm.s.tab[i] = a.buz[i >> 6];
+        for (uint32_t i = threadIdx.x; i < 256u * 64u; i += blockDim.x) sm.s.tab[i] = rotl_n(a.buz[i >> 6], a.buz_rot);
     } else {
         for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) {
             sm.s.out[i] = a.rk_out[i];
@@ -699,17 +803,56 @@ constexpr int kDmaSlots = KCDC_DMA_SLOTS;  // 4 KiB LDS-DMA slots per wave (pipe
 #define KCDC_YIELD_BYTES (768 << 10)
 #endif
 constexpr int64_t kYieldBytes = KCDC_YIELD_BYTES;
-constexpr int kSlot = 64 * kWave;  // 4 KiB: one 64-byte piece of every lane
+#ifndef KCDC_DMA_RUN
+#define KCDC_DMA_RUN 128
+#endif
+#ifndef KCDC_X_EXT
+#define KCDC_X_EXT 1
+#endif
+#ifndef KCDC_X_PF
+#define KCDC_X_PF 1
+#endif
+#ifndef KCDC_X_HM
+#define KCDC_X_HM 1
+#endif
+#ifndef KCDC_X_CA
+#define KCDC_X_CA 1
+#endif
+#ifndef KCDC_X_EC
+#define KCDC_X_EC 1
+#endif
+#ifndef KCDC_DMA_AUX
+#define KCDC_DMA_AUX 2  // nt: once-read stream bytes (membench: 128-B runs 6.65 vs 6.38 TB/s)
+#endif
+// Bytes of each lane segment one DMA round fetches: 64 (two half-step pieces per step,
+// kDmaSlots-deep LDS pipeline) or 128 (one whole cache line per lane segment per step,
+// staged through ONE 8 KiB slot per wave: the step's bytes move to VGPRs at its start,
+// which frees the slot for the next step's DMA while the step is hashed).
+constexpr int kRun = KCDC_DMA_RUN;
+constexpr int kSlot = 64 * kWave;                            // 4 KiB: one 64-byte piece of every lane
+constexpr int kSlotBytes = kRun == 128 ? 128 * kWave : kSlot;  // LDS bytes per slot
+constexpr int kNSlots = kRun == 128 ? 1 : kDmaSlots;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-struct DmaSmem {
-    BuzShared tab;
-    __attribute__((aligned(16))) uint8_t slots[kDmaWaves][kDmaSlots][kSlot];
+// The table and the DMA slots are SEPARATE __shared__ objects: LDS lowering then gives
+// them distinct alias scopes, so the waitcnt pass knows a table read cannot alias an
+// in-flight LDS-DMA into a slot.  In one struct every table read waited vmcnt(0) for the
+// DMA just issued, which serialised the prefetch with the hashing.
+struct DmaSlots {
+    __attribute__((aligned(16))) uint8_t b[kDmaWaves][kNSlots][kSlotBytes];
 };
-static_assert(sizeof(DmaSmem) <= 160 * 1024, "LDS-DMA slots + table exceed the CU's 160 KiB");
+// Each lane's segment head (first 64 bytes) for its predecessor's tile-end extension.
+struct HeadStash {
+    __attribute__((aligned(16))) uint32_t w[kDmaWaves][16][kWave];  // [wave][dword][lane]: conflict-free
+};
+static_assert(sizeof(DmaSlots) + sizeof(BuzShared) + (kRun == 128 ? sizeof(HeadStash) : 0) <= 160 * 1024,
+              "LDS-DMA slots + table + head stash exceed the CU's 160 KiB");
 
 __device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t rsrc, int64_t tb, uint8_t* slot, int64_t ct,
                                           int64_t L, int64_t piece, int lane) {
+#ifdef KCDC_EXP_COMPONLY  // ablation: hashing only (slots keep a fixed random pattern)
+    return;
+#endif
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int l = 16 * i + (lane >> 2);
@@ -742,6 +885,63 @@ __device__ __forceinline__ void read_piece(const uint8_t* slot, int lane, int64_
     }
 }
 
+// 128-byte runs: DMA lane d of instruction i (0..7) fetches chunk (d&7) ^ sw(l) of lane
+// l = 8i + d/8, so lane l's line lands at slot + 128 l with chunk j at granule j ^ sw(l);
+// sw(l) = (l >> 1) & 7 gives every ds_read_b128 lane group 16 distinct 16-byte bank slots.
+__device__ __forceinline__ void dma_step128(__amdgpu_buffer_rsrc_t rsrc, int64_t tb, uint8_t* slot, int64_t ct,
+                                            int64_t L, int64_t n, int lane) {
+#ifdef KCDC_EXP_COMPONLY
+    return;
+#endif
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int l = 8 * i + (lane >> 3);
+        const int jj = (lane & 7) ^ ((l >> 1) & 7);
+        const int64_t coord = ct + l * L + 128 * n + 16 * jj;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(slot + 1024 * i), 16,
+                                                 static_cast<int>(coord - tb), 0, 0, KCDC_DMA_AUX);
+    }
+}
+
+__device__ __forceinline__ void read_step128(const uint8_t* slot, int lane, int64_t c, int64_t off0,
+                                             uint32_t (&dw)[32]) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(slot + 128 * lane + 16 * (j ^ ((lane >> 1) & 7)));
+        dw[4 * j + 0] = v.x;
+        dw[4 * j + 1] = v.y;
+        dw[4 * j + 2] = v.z;
+        dw[4 * j + 3] = v.w;
+    }
+    if (c == 0 && off0) {  // bytes before the stream start are virtual zeros
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            const int64_t keep_from = off0 - 4 * d;
+            const uint32_t m = keep_from <= 0 ? 0xFFFFFFFFu
+                                              : (keep_from >= 4 ? 0u : (0xFFFFFFFFu << (8 * keep_from)));
+            dw[d] &= m;
+        }
+    }
+}
+
+// Geometry of the tile starting at ct (lane segments of L bytes, nb 128-byte steps).
+struct TileGeom {
+    int64_t L;
+    int nb;
+    Loader ld;
+};
+__device__ __forceinline__ TileGeom tile_geom(int64_t ct, int64_t hi, const uint8_t* abase, int64_t off0,
+                                              int64_t nbytes_coord) {
+    const int64_t rem = hi - ct + 1;
+    int64_t per = (rem + kWave - 1) / kWave;
+    per = (per + 127) & ~int64_t(127);
+    TileGeom g;
+    g.L = per < kLaneMax ? per : kLaneMax;
+    g.nb = static_cast<int>(g.L / 128);
+    g.ld = make_loader(abase, off0, nbytes_coord, ct >= 64 ? ct - 64 : 0);
+    return g;
+}
+
 // scan_region() with LDS-DMA feeding; buzhash T-ring only.  Wave-uniform control
 // flow around every DMA (DMA lanes fetch for other lanes).
 // Resumable: tiles start at ct_io (tile-aligned; lo & ~127 on a fresh scan).  After
@@ -751,10 +951,120 @@ __device__ __forceinline__ void read_piece(const uint8_t* slot, int lane, int64_
 // tile state onto the VALU path and every LDS-DMA into a waterfall loop.)
 constexpr int64_t kYield = -2;
 constexpr int64_t kNoYield = int64_t(1) << 62;
-__device__ int64_t scan_region_dma(BuzRing hash, uint8_t* sl, const uint8_t* abase, int64_t off0,
+template <bool TOP>
+__device__ int64_t scan_region_dma(BuzRing hash, uint32_t lim, uint8_t* sl, uint32_t* hs, const uint8_t* abase, int64_t off0,
                                    int64_t nbytes_coord, int64_t lo, int64_t hi, int lane, int64_t& ct_io,
                                    int64_t& budget) {
     int64_t ct = ct_io;
+#if KCDC_DMA_RUN == 128
+    // Tiles of one visit are contiguous (tile t+1 starts where lane 63 of tile t ends).
+    // Only the first tile warms every lane on the 64 bytes before its segment (one 64-byte
+    // DMA piece); a later ("cold") tile carries lane 63's state into lane 0 and lets every
+    // other lane keep its own old state as a stand-in history: its first 63 positions are
+    // masked, and at the tile end its predecessor rolls 63 positions on into that head
+    // (extend64, the head bytes read from an LDS stash).  No warm-up bytes are
+    // read after the first tile, and the next tile's first step is prefetched during the
+    // last step of the current one, so a visit is one continuous DMA pipeline.
+    if (ct > hi) return -1;
+    TileGeom g = tile_geom(ct, hi, abase, off0, nbytes_coord);
+    {   // first tile of the visit: warm-up piece (64 bytes before each lane segment)
+        uint32_t w16[16];
+        dma_piece(g.ld.rsrc, g.ld.tb, sl, ct, g.L, -1, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        read_piece(sl, lane, ct + lane * g.L - 64, off0, w16);
+        hash.clear();
+        hash.template block<kWarm>(w16);  // consumes w16: the slot reads have completed
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    dma_step128(g.ld.rsrc, g.ld.tb, sl, ct, g.L, 0, lane);
+    bool cold = false;
+    for (;;) {
+        const int64_t c0 = ct + lane * g.L;
+        const int64_t ct_next = ct + kWave * g.L;
+        const bool more = ct_next <= hi && budget - kWave * g.L > 0;  // another tile follows
+        TileGeom gn = g;
+        if (more) gn = tile_geom(ct_next, hi, abase, off0, nbytes_coord);
+        if (KCDC_X_CA && cold) hash.carry_from_last_lane(lane == 0);
+        const uint32_t hmask = lane == 0 ? 0u : 0xFFFFFFFFu;
+        int64_t found = -1;
+        for (int n = 0; n < g.nb; n++) {
+            const int64_t c = c0 + 128 * n;
+            const typename BuzRing::State st0 = hash.save();
+            uint32_t dw[32];
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            read_step128(sl, lane, c, off0, dw);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot free: refill it
+            __builtin_amdgcn_sched_barrier(0);
+            if (n + 1 < g.nb)
+                dma_step128(g.ld.rsrc, g.ld.tb, sl, ct, g.L, n + 1, lane);
+            else if (KCDC_X_PF && more)
+                dma_step128(gn.ld.rsrc, gn.ld.tb, sl, ct_next, gn.L, 0, lane);
+            __builtin_amdgcn_sched_barrier(0);
+            uint32_t m;
+            if (n == 0) {
+#pragma unroll
+                for (int i = 0; i < 16; i++) hs[kWave * i + lane] = dw[i];
+                m = KCDC_X_HM && cold ? hash.template step128<TOP, true>(dw, hmask) : hash.template step128<TOP>(dw);
+            } else {
+#ifdef KCDC_EXP_MEMONLY
+                m = 0;
+#pragma unroll
+                for (int i = 0; i < 32; i++) m |= dw[i];
+                asm volatile("" : "+v"(m));
+#else
+                m = hash.template step128<TOP>(dw);
+#endif
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (m <= lim && found < 0 && c <= hi) {  // rare: exact re-run from global memory
+                uint32_t prv[16], cur[32];
+                g.ld.load(c - 64, prv);
+                g.ld.load(c, cur);
+                const int64_t blo = lo - c, bhi = hi - c;
+                const int ilo = blo < 0 ? 0 : static_cast<int>(blo), ihi = bhi > 127 ? 127 : static_cast<int>(bhi);
+                const uint32_t idx = KCDC_X_EC && n == 0 ? hash.exact_cold(prv, cur, ilo, ihi) : hash.exact(st0, prv, cur, ilo, ihi);
+                if (idx < 128u) found = c + idx;
+            }
+        }
+        if (KCDC_X_EXT && cold) {  // lanes 0..62: the successor's first 63 positions
+            uint32_t nx[16];
+#pragma unroll
+            for (int i = 0; i < 16; i++) nx[i] = hs[kWave * i + ((lane + 1) & (kWave - 1))];
+            if (lane != kWave - 1) {
+                const uint32_t m = hash.template extend64<TOP>(nx);
+                const int64_t c = c0 + g.L;  // successor's segment start
+                if (m <= lim && found < 0 && c <= hi) {
+                    uint32_t prv[16], cur[16];
+                    g.ld.load(c - 64, prv);
+                    g.ld.load(c, cur);
+                    const int64_t blo = lo - c, bhi = hi - c;
+                    const uint32_t idx = hash.exact_cold(prv, cur, blo < 0 ? 0 : static_cast<int>(blo),
+                                                         bhi > 63 ? 63 : static_cast<int>(bhi));
+                    if (idx < 64u) found = c + idx;
+                }
+            }
+        }
+        const uint64_t hit = __ballot(found >= 0);
+        if (hit) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a prefetched step may be in flight
+            const int first = __builtin_ctzll(hit);
+            return static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, first))));
+        }
+        budget -= kWave * g.L;
+        ct = ct_next;
+        if (!more) break;
+        g = gn;
+        cold = true;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (ct <= hi) {  // budget spent: yield with the next tile
+        ct_io = ct;
+        return kYield;
+    }
+    return -1;
+#endif
     while (ct <= hi) {
         const int64_t rem = hi - ct + 1;
         int64_t per = (rem + kWave - 1) / kWave;
@@ -808,13 +1118,13 @@ __device__ int64_t scan_region_dma(BuzRing hash, uint8_t* sl, const uint8_t* aba
                 for (int i = 0; i < 16; i++) m |= dw[i];
                 asm volatile("" : "+v"(m));
 #else
-                m = h == 0 ? hash.template half<0>(dw, loc, m) : hash.template half<1>(dw, loc, m);
+                m = h == 0 ? hash.template half<0, TOP>(dw, loc, m) : hash.template half<1, TOP>(dw, loc, m);
 #endif
                 __builtin_amdgcn_sched_barrier(0);
                 if (q + S < Q) dma_piece(ld.rsrc, tb, slot, ct, L, q + S - 1, lane);
                 qs = qs + 1 == S ? 0 : qs + 1;
             }
-            if (m == 0 && found < 0 && c <= hi) {  // rare: exact re-run from global memory
+            if (m <= lim && found < 0 && c <= hi) {  // rare: exact re-run from global memory
                 uint32_t prv[16], cur[32];
                 ld.load(c - 64, prv);
                 ld.load(c, cur);
@@ -986,7 +1296,8 @@ __device__ void yield_stream(const BatchArgs& a, int lane, uint32_t sid, const P
 }
 
 // Advance stream sid from pr: returns true when it is finished, false when yielded.
-__device__ __forceinline__ bool run_stream(const BatchArgs& a, const BuzRing& hash, uint8_t* sl,
+template <bool TOP>
+__device__ __forceinline__ bool run_stream(const BatchArgs& a, const BuzRing& hash, uint8_t* sl, uint32_t* hs,
                                            uint32_t sid, Progress& pr, bool more, int lane) {
     const uint64_t p = uni64(reinterpret_cast<uint64_t>(a.ptrs[sid]));
     const int64_t n = static_cast<int64_t>(uni64(a.lens[sid]));
@@ -1006,7 +1317,7 @@ __device__ __forceinline__ bool run_stream(const BatchArgs& a, const BuzRing& ha
         } else {
             const int64_t pl = s + mx - 1 < n - 1 ? s + mx - 1 : n - 1;
             if (pr.ct < 0) pr.ct = (pf + off0) & ~int64_t(127);
-            const int64_t f = scan_region_dma(hash, sl, abase, off0, off0 + n, pf + off0, pl + off0, lane, pr.ct,
+            const int64_t f = scan_region_dma<TOP>(hash, TOP ? a.buz_lim : 0u, sl, hs, abase, off0, off0 + n, pf + off0, pl + off0, lane, pr.ct,
                                               budget);
             if (f == kYield) return false;
             if (f >= 0)
@@ -1025,18 +1336,32 @@ __device__ __forceinline__ bool run_stream(const BatchArgs& a, const BuzRing& ha
     return true;
 }
 
+template <bool TOP>
 __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_dma_kernel(BatchArgs a) {
-    __shared__ DmaSmem sm;
-    for (uint32_t i = threadIdx.x; i < 256u * 64u; i += blockDim.x) sm.tab.tab[i] = a.buz[i >> 6];
+    __shared__ BuzShared smtab;
+    __shared__ DmaSlots smslots;
+#if KCDC_DMA_RUN == 128
+    __shared__ HeadStash smheads;
+#endif
+    for (uint32_t i = threadIdx.x; i < 256u * 64u; i += blockDim.x) smtab.tab[i] = rotl_n(a.buz[i >> 6], a.buz_rot);
     __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     BuzRing hash;
-    hash.tab = reinterpret_cast<const char*>(sm.tab.tab);
+    hash.tab = reinterpret_cast<const char*>(smtab.tab);
     hash.lane4 = static_cast<uint32_t>(lane) * 4u;
     hash.mask = a.mask;
     hash.h = 0;
-    uint8_t* sl = sm.slots[wave][0];
+    uint8_t* sl = smslots.b[wave][0];
+#if KCDC_DMA_RUN == 128
+    uint32_t* hs = &smheads.w[wave][0][0];
+#else
+    uint32_t* hs = nullptr;
+#endif
+#ifdef KCDC_EXP_COMPONLY
+    for (int i = lane; i < kNSlots * kSlotBytes / 4; i += kWave)
+        reinterpret_cast<uint32_t*>(sl)[i] = static_cast<uint32_t>((i + 1) * 2654435761u) ^ (wave * 0x9E3779B9u);
+#endif
     for (;;) {
         Progress pr;
 #if KCDC_TRACE
@@ -1053,7 +1378,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
 #if KCDC_TRACE
         if (lane == 0 && pr.s == 0 && pr.ct < 0) a.trace[3 * sid + 0] = __builtin_amdgcn_s_memrealtime();
 #endif
-        const bool fin = run_stream(a, hash, sl, sid, pr, more, lane);
+        const bool fin = run_stream<TOP>(a, hash, sl, hs, sid, pr, more, lane);
 #if KCDC_TRACE
         KCDC_QSTAT64(kQStat + 8, __builtin_amdgcn_s_memrealtime() - tc);
         tc = __builtin_amdgcn_s_memrealtime();
@@ -1384,11 +1709,36 @@ std::mutex g_dev_mu;
 
 int hip_fail(hipError_t e, const char* what) { return set_error(-5, std::string(what) + ": " + hipGetErrorString(e)); }
 
+// Rotated buzhash frame for a reference mask (avg - 1).  A contiguous low mask of k bits
+// (avg a power of two, the registered splitters) rotates to the top k bits: rot = 32 - k,
+// and h & mask == 0 <=> h <= ~mask.  Any other mask keeps rot = 0 (top = false).
+struct BuzFrame {
+    uint32_t rot, mask, lim;
+    bool top;
+};
+BuzFrame buz_frame(uint32_t mask) {
+    BuzFrame f{0, mask, 0, false};
+    if ((mask & (mask + 1u)) == 0) {  // 0b0..01..1 (including 0 and all ones)
+        const uint32_t k = static_cast<uint32_t>(__builtin_popcount(mask));
+        f.rot = (32u - k) & 31u;
+        f.mask = f.rot ? (mask << f.rot) | (mask >> (32u - f.rot)) : mask;
+        f.lim = ~f.mask;
+        f.top = true;
+    }
+    return f;
+}
+
 dev::BatchArgs base_args(const Algo& algo, const DeviceTables& t) {
     dev::BatchArgs a{};
     a.min_size = algo.min_size();
     a.max_size = algo.max_size();
     a.mask = static_cast<uint32_t>(algo.mask());
+    if (algo.kind == kBuzhash) {
+        const BuzFrame f = buz_frame(a.mask);
+        a.buz_rot = f.rot;
+        a.mask = f.mask;
+        a.buz_lim = f.lim;
+    }
     a.buz = t.buz;
     a.rk_out = t.rk_out;
     a.rk_mod = t.rk_mod;
@@ -1522,7 +1872,12 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         if (e != hipSuccess) return hip_fail(e, "queue reset");
         // persistent grid: one workgroup per CU, never more workgroups than the streams need
         if (dma) {
-            hipLaunchKernelGGL(dev::split_batch_dma_kernel, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0, st, a);
+            if (buz_frame(static_cast<uint32_t>(algo.mask())).top)
+                hipLaunchKernelGGL(dev::split_batch_dma_kernel<true>, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0,
+                                   st, a);
+            else
+                hipLaunchKernelGGL(dev::split_batch_dma_kernel<false>, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0,
+                                   st, a);
         } else {
             const dim3 block(dev::kBatchWaves * dev::kWave);
             if (algo.kind == kBuzhash)
