@@ -29,6 +29,7 @@
 //   earliest lane with a candidate (ballot + ffs) gives the tile's answer.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <mutex>
 #include <vector>
 #include <string>
@@ -51,7 +52,7 @@ constexpr int kWave = 64;
 #define KCDC_LOOKAHEAD 1
 #endif
 #ifndef KCDC_LA_W
-#define KCDC_LA_W 4  // 128-byte steps: table reads issued this many bytes ahead (VGPR bound)
+#define KCDC_LA_W 16  // 128-byte steps: table reads issued this many bytes ahead (VGPR bound)
 #endif
 #ifndef KCDC_BLK
 #define KCDC_BLK 128
@@ -108,6 +109,7 @@ __device__ __forceinline__ uint32_t byte_at(const uint32_t (&dw)[N], int i) {
 // check returns zeros for out-of-range (including negative) offsets.
 struct Loader {
     __amdgpu_buffer_rsrc_t rsrc;
+    u32x4 d;       // the same descriptor as four dwords (operand of the inline-asm LDS-DMA)
     int64_t tb;    // coordinate of descriptor offset 0
     int64_t off0;  // stream misalignment (0..15)
 
@@ -142,6 +144,11 @@ __device__ __forceinline__ Loader make_loader(const uint8_t* abase, int64_t off0
     Loader L;
     L.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(abase + tb), static_cast<short>(0),
                                                static_cast<int>(nrec), 0x00020000);
+    const uint64_t base = reinterpret_cast<uint64_t>(abase + tb);
+    L.d.x = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(base));
+    L.d.y = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(base >> 32) & 0xFFFFu);  // stride 0
+    L.d.z = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nrec));
+    L.d.w = 0x00020000u;
     L.tb = tb;
     L.off0 = off0;
     return L;
@@ -359,13 +366,13 @@ struct BuzRing {
     // A whole 128-byte step (the 128-byte-run DMA path): bytes 0..63 consume the ring and
     // fill loc, bytes 64..127 consume loc and refill the ring (loc[b] can take ring[b]'s
     // register).  Table reads run one 16-byte window ahead of the arithmetic.
-    // HEADMASK: positions 0..62 are or-ed with hmask before the min (a lane whose state
-    // has a stand-in history masks them with all ones; its predecessor tests them).
-    template <bool TOP, bool HEADMASK = false>
-    __device__ __forceinline__ uint32_t step128(const uint32_t (&dw)[32], uint32_t hmask = 0) {
+    // Positions 0..62 keep their own running min m0, or-ed with hmask at the end (a lane
+    // whose state has a stand-in history passes all ones: its predecessor tests them).
+    template <bool TOP>
+    __device__ __forceinline__ uint32_t step128(const uint32_t (&dw)[32], uint32_t hmask) {
         constexpr int W = KCDC_LA_W;  // bytes per lookahead window
         uint32_t loc[64];
-        uint32_t m = 0xFFFFFFFFu;
+        uint32_t m = 0xFFFFFFFFu, m0 = 0xFFFFFFFFu;
         uint32_t tw[W], tn[W];
 #pragma unroll
         for (int i = 0; i < W; i++) tw[i] = look(dw[i >> 2], i & 3);
@@ -387,13 +394,18 @@ struct BuzRing {
                     ring[b - 64] = tw[i];
                 }
                 const uint32_t t = TOP ? h : h & mask;
-                m = min(m, HEADMASK && b < 63 ? (t | hmask) : t);
-                if ((i & 3) == 3) asm volatile("" : "+v"(m));
+                if (b < 63) {
+                    m0 = min(m0, t);
+                    if ((b & 3) == 3) asm volatile("" : "+v"(m0));
+                } else {
+                    m = min(m, t);
+                    if ((b & 3) == 3) asm volatile("" : "+v"(m));
+                }
             }
 #pragma unroll
             for (int i = 0; i < W; i++) tw[i] = tn[i];
         }
-        return m;
+        return min(m, m0 | hmask);
     }
     // Tile-end extension: continue into the successor lane's segment head nx (its first
     // 64 bytes), whose first 63 positions that lane tested only against a stand-in
@@ -806,20 +818,8 @@ constexpr int64_t kYieldBytes = KCDC_YIELD_BYTES;
 #ifndef KCDC_DMA_RUN
 #define KCDC_DMA_RUN 128
 #endif
-#ifndef KCDC_X_EXT
-#define KCDC_X_EXT 1
-#endif
-#ifndef KCDC_X_PF
-#define KCDC_X_PF 1
-#endif
-#ifndef KCDC_X_HM
-#define KCDC_X_HM 1
-#endif
-#ifndef KCDC_X_CA
-#define KCDC_X_CA 1
-#endif
-#ifndef KCDC_X_EC
-#define KCDC_X_EC 1
+#ifndef KCDC_COLD
+#define KCDC_COLD 1  // cold tiles (carry + extension) instead of a warm-up per tile
 #endif
 #ifndef KCDC_DMA_AUX
 #define KCDC_DMA_AUX 2  // nt: once-read stream bytes (membench: 128-B runs 6.65 vs 6.38 TB/s)
@@ -848,7 +848,26 @@ struct HeadStash {
 static_assert(sizeof(DmaSlots) + sizeof(BuzShared) + (kRun == 128 ? sizeof(HeadStash) : 0) <= 160 * 1024,
               "LDS-DMA slots + table + head stash exceed the CU's 160 KiB");
 
-__device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t rsrc, int64_t tb, uint8_t* slot, int64_t ct,
+// One LDS-DMA wave instruction (64 lanes x 16 B -> 1 KiB at LDS address m0), written as
+// inline asm so the waitcnt pass does not see an LDS-DMA: with several DMA sites and slots
+// it ran out of alias-tracking slots and made table reads wait vmcnt for in-flight slot
+// fills.  Every slot read here is preceded by an explicit s_waitcnt; M0 is used by no other
+// code in these kernels.
+#if KCDC_DMA_AUX == 2
+#define KCDC_DMA_POLICY " nt"
+#else
+#define KCDC_DMA_POLICY ""
+#endif
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {  // LDS byte address of a __shared__ pointer
+    return __builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr_t)(const_cast<void*>(p)))));
+}
+__device__ __forceinline__ void dma_lds16(const u32x4& d, uint32_t m0, int32_t voff) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen" KCDC_DMA_POLICY " lds"
+                 :: "s"(m0), "v"(voff), "s"(d) : "memory");
+}
+
+__device__ __forceinline__ void dma_piece(const Loader& ld, int64_t tb, uint32_t slot, int64_t ct,
                                           int64_t L, int64_t piece, int lane) {
 #ifdef KCDC_EXP_COMPONLY  // ablation: hashing only (slots keep a fixed random pattern)
     return;
@@ -858,8 +877,7 @@ __device__ __forceinline__ void dma_piece(__amdgpu_buffer_rsrc_t rsrc, int64_t t
         const int l = 16 * i + (lane >> 2);
         const int jj = (lane & 3) ^ ((l >> 2) & 3);
         const int64_t coord = ct + l * L + 64 * piece + 16 * jj;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(slot + 1024 * i), 16,
-                                                 static_cast<int>(coord - tb), 0, 0, 0);
+        dma_lds16(ld.d, slot + 1024u * i, static_cast<int32_t>(coord - tb));
     }
 }
 
@@ -888,7 +906,7 @@ __device__ __forceinline__ void read_piece(const uint8_t* slot, int lane, int64_
 // 128-byte runs: DMA lane d of instruction i (0..7) fetches chunk (d&7) ^ sw(l) of lane
 // l = 8i + d/8, so lane l's line lands at slot + 128 l with chunk j at granule j ^ sw(l);
 // sw(l) = (l >> 1) & 7 gives every ds_read_b128 lane group 16 distinct 16-byte bank slots.
-__device__ __forceinline__ void dma_step128(__amdgpu_buffer_rsrc_t rsrc, int64_t tb, uint8_t* slot, int64_t ct,
+__device__ __forceinline__ void dma_step128(const Loader& ld, int64_t tb, uint32_t slot, int64_t ct,
                                             int64_t L, int64_t n, int lane) {
 #ifdef KCDC_EXP_COMPONLY
     return;
@@ -898,8 +916,7 @@ __device__ __forceinline__ void dma_step128(__amdgpu_buffer_rsrc_t rsrc, int64_t
         const int l = 8 * i + (lane >> 3);
         const int jj = (lane & 7) ^ ((l >> 1) & 7);
         const int64_t coord = ct + l * L + 128 * n + 16 * jj;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(slot + 1024 * i), 16,
-                                                 static_cast<int>(coord - tb), 0, 0, KCDC_DMA_AUX);
+        dma_lds16(ld.d, slot + 1024u * i, static_cast<int32_t>(coord - tb));
     }
 }
 
@@ -967,25 +984,25 @@ __device__ int64_t scan_region_dma(BuzRing hash, uint32_t lim, uint8_t* sl, uint
     // last step of the current one, so a visit is one continuous DMA pipeline.
     if (ct > hi) return -1;
     TileGeom g = tile_geom(ct, hi, abase, off0, nbytes_coord);
-    {   // first tile of the visit: warm-up piece (64 bytes before each lane segment)
-        uint32_t w16[16];
-        dma_piece(g.ld.rsrc, g.ld.tb, sl, ct, g.L, -1, lane);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        read_piece(sl, lane, ct + lane * g.L - 64, off0, w16);
-        hash.clear();
-        hash.template block<kWarm>(w16);  // consumes w16: the slot reads have completed
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    dma_step128(g.ld.rsrc, g.ld.tb, sl, ct, g.L, 0, lane);
     bool cold = false;
     for (;;) {
+        if (!cold) {  // first tile of the visit: warm-up piece (64 bytes before each lane segment)
+            uint32_t w16[16];
+            dma_piece(g.ld, g.ld.tb, lds_addr(sl), ct, g.L, -1, lane);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            read_piece(sl, lane, ct + lane * g.L - 64, off0, w16);
+            hash.clear();
+            hash.template block<kWarm>(w16);  // consumes w16: the slot reads have completed
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            dma_step128(g.ld, g.ld.tb, lds_addr(sl), ct, g.L, 0, lane);
+        }
         const int64_t c0 = ct + lane * g.L;
         const int64_t ct_next = ct + kWave * g.L;
         const bool more = ct_next <= hi && budget - kWave * g.L > 0;  // another tile follows
         TileGeom gn = g;
         if (more) gn = tile_geom(ct_next, hi, abase, off0, nbytes_coord);
-        if (KCDC_X_CA && cold) hash.carry_from_last_lane(lane == 0);
+        if (cold) hash.carry_from_last_lane(lane == 0);
         const uint32_t hmask = lane == 0 ? 0u : 0xFFFFFFFFu;
         int64_t found = -1;
         for (int n = 0; n < g.nb; n++) {
@@ -998,25 +1015,22 @@ __device__ int64_t scan_region_dma(BuzRing hash, uint32_t lim, uint8_t* sl, uint
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot free: refill it
             __builtin_amdgcn_sched_barrier(0);
             if (n + 1 < g.nb)
-                dma_step128(g.ld.rsrc, g.ld.tb, sl, ct, g.L, n + 1, lane);
-            else if (KCDC_X_PF && more)
-                dma_step128(gn.ld.rsrc, gn.ld.tb, sl, ct_next, gn.L, 0, lane);
+                dma_step128(g.ld, g.ld.tb, lds_addr(sl), ct, g.L, n + 1, lane);
+            else if (KCDC_COLD && more)
+                dma_step128(gn.ld, gn.ld.tb, lds_addr(sl), ct_next, gn.L, 0, lane);
             __builtin_amdgcn_sched_barrier(0);
-            uint32_t m;
             if (n == 0) {
 #pragma unroll
                 for (int i = 0; i < 16; i++) hs[kWave * i + lane] = dw[i];
-                m = KCDC_X_HM && cold ? hash.template step128<TOP, true>(dw, hmask) : hash.template step128<TOP>(dw);
-            } else {
-#ifdef KCDC_EXP_MEMONLY
-                m = 0;
-#pragma unroll
-                for (int i = 0; i < 32; i++) m |= dw[i];
-                asm volatile("" : "+v"(m));
-#else
-                m = hash.template step128<TOP>(dw);
-#endif
             }
+#ifdef KCDC_EXP_MEMONLY
+            uint32_t m = 0;
+#pragma unroll
+            for (int i = 0; i < 32; i++) m |= dw[i];
+            asm volatile("" : "+v"(m));
+#else
+            const uint32_t m = hash.template step128<TOP>(dw, n == 0 && cold ? hmask : 0u);
+#endif
             __builtin_amdgcn_sched_barrier(0);
             if (m <= lim && found < 0 && c <= hi) {  // rare: exact re-run from global memory
                 uint32_t prv[16], cur[32];
@@ -1024,11 +1038,11 @@ __device__ int64_t scan_region_dma(BuzRing hash, uint32_t lim, uint8_t* sl, uint
                 g.ld.load(c, cur);
                 const int64_t blo = lo - c, bhi = hi - c;
                 const int ilo = blo < 0 ? 0 : static_cast<int>(blo), ihi = bhi > 127 ? 127 : static_cast<int>(bhi);
-                const uint32_t idx = KCDC_X_EC && n == 0 ? hash.exact_cold(prv, cur, ilo, ihi) : hash.exact(st0, prv, cur, ilo, ihi);
+                const uint32_t idx = n == 0 ? hash.exact_cold(prv, cur, ilo, ihi) : hash.exact(st0, prv, cur, ilo, ihi);
                 if (idx < 128u) found = c + idx;
             }
         }
-        if (KCDC_X_EXT && cold) {  // lanes 0..62: the successor's first 63 positions
+        if (cold) {  // lanes 0..62: the successor's first 63 positions
             uint32_t nx[16];
 #pragma unroll
             for (int i = 0; i < 16; i++) nx[i] = hs[kWave * i + ((lane + 1) & (kWave - 1))];
@@ -1056,7 +1070,7 @@ __device__ int64_t scan_region_dma(BuzRing hash, uint32_t lim, uint8_t* sl, uint
         ct = ct_next;
         if (!more) break;
         g = gn;
-        cold = true;
+        cold = KCDC_COLD;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (ct <= hi) {  // budget spent: yield with the next tile
@@ -1086,7 +1100,7 @@ __device__ int64_t scan_region_dma(BuzRing hash, uint32_t lim, uint8_t* sl, uint
         const int Q = 2 * nb + 1;  // pieces in this tile
 #pragma unroll
         for (int j = 0; j < S; j++)
-            if (j < Q) dma_piece(ld.rsrc, tb, sl + kSlot * j, ct, L, j - 1, lane);
+            if (j < Q) dma_piece(ld, tb, lds_addr(sl + kSlot * j), ct, L, j - 1, lane);
         uint32_t dw[16], loc[64];
         __builtin_amdgcn_sched_barrier(0);
         if (S - 1 <= Q - 1)
@@ -1097,7 +1111,7 @@ __device__ int64_t scan_region_dma(BuzRing hash, uint32_t lim, uint8_t* sl, uint
         hash.clear();
         hash.template block<kWarm>(dw);
         __builtin_amdgcn_sched_barrier(0);
-        if (S < Q) dma_piece(ld.rsrc, tb, sl, ct, L, S - 1, lane);
+        if (S < Q) dma_piece(ld, tb, lds_addr(sl), ct, L, S - 1, lane);
         int qs = 1 % S;  // slot of piece q
         for (int n = 0; n < nb; n++) {
             const int64_t c = c0 + 128 * n;
@@ -1121,7 +1135,7 @@ __device__ int64_t scan_region_dma(BuzRing hash, uint32_t lim, uint8_t* sl, uint
                 m = h == 0 ? hash.template half<0, TOP>(dw, loc, m) : hash.template half<1, TOP>(dw, loc, m);
 #endif
                 __builtin_amdgcn_sched_barrier(0);
-                if (q + S < Q) dma_piece(ld.rsrc, tb, slot, ct, L, q + S - 1, lane);
+                if (q + S < Q) dma_piece(ld, tb, lds_addr(slot), ct, L, q + S - 1, lane);
                 qs = qs + 1 == S ? 0 : qs + 1;
             }
             if (m <= lim && found < 0 && c <= hi) {  // rare: exact re-run from global memory
@@ -1295,6 +1309,85 @@ __device__ void yield_stream(const BatchArgs& a, int lane, uint32_t sid, const P
     }
 }
 
+// ------------------------------------------------ packed-entry stream queue (KCDC_SCHED 1)
+// Fewer round trips per hand-off than take_stream/yield_stream: a take is one atomic
+// (with the pushed count read beside it) and a yielded stream's progress travels inside
+// its 64-byte ring entry: three 16-byte sc1 stores, each
+// carrying the entry tag (push number + 1), so the taker needs no separate progress
+// loads and the pusher no drain before its flag (MI355X_MICROARCH.md: a tagged 16-byte
+// sc1 granule is read untorn).  Ticket t < n is stream t from its start; ticket t >= n is
+// ring entry e = t - n, polled until its tag matches or every stream is done.  A
+// ticket's holder always polls it, so every pushed entry has a taker (no deadlock);
+// waves exit only once kQDone reaches n.
+#ifndef KCDC_SCHED
+#define KCDC_SCHED 2
+#endif
+constexpr int kEntryBytes = 64;
+__device__ __forceinline__ uint32_t reserve_ticket(const BatchArgs& a, int lane) {
+    uint32_t t = 0;
+    if (lane == 0) t = add_agent(a.queue + kQHead, 1u);
+    return bcast(t);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ring_rsrc(const BatchArgs& a) {
+    return __builtin_amdgcn_make_buffer_rsrc(a.ring, static_cast<short>(0),
+                                             static_cast<int>((a.ring_mask + 1u) * kEntryBytes), 0x00020000);
+}
+// Resolve ticket t into (sid, progress); false when every stream is done (wave exits).
+__device__ bool resolve_ticket(const BatchArgs& a, int lane, uint32_t t, uint32_t& sid, Progress& pr) {
+    const uint32_t n = a.nstreams;
+    if (t < n) {
+        sid = t;
+        pr.s = 0;
+        pr.ct = -1;
+        pr.cnt = 0;
+        return true;
+    }
+    const uint32_t e = t - n;
+    const __amdgpu_buffer_rsrc_t r = ring_rsrc(a);
+    const int off = static_cast<int>((e & a.ring_mask) * kEntryBytes) + 16 * (lane & 3);
+    for (uint32_t spin = 0;; spin++) {
+        u32x4 v = {0, 0, 0, 0};
+        if (lane < 3) v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16 /* sc1 */);
+        const bool ok = lane >= 3 || v.x == e + 1u;
+        if (__ballot(!ok) == 0) {
+            sid = __builtin_amdgcn_readlane(v.y, 0);
+            pr.cnt = __builtin_amdgcn_readlane(v.z, 0);
+            pr.s = static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(v.z, 1))) << 32) |
+                                        static_cast<uint32_t>(__builtin_amdgcn_readlane(v.y, 1)));
+            pr.ct = static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(v.z, 2))) << 32) |
+                                         static_cast<uint32_t>(__builtin_amdgcn_readlane(v.y, 2)));
+            return true;
+        }
+        uint32_t st = 0;  // 0 wait, 2 exit
+        if (lane == 0) {
+            if (ld_agent(a.queue + kQDone) >= n) {
+                st = 2;
+            } else if (spin >= kSpinCap) {
+                add_agent(a.queue + kQErr, 1u);
+                st = 2;
+            }
+        }
+        if (bcast(st) == 2) return false;
+        __builtin_amdgcn_s_sleep(32);
+    }
+}
+// Re-queue stream sid with its progress (one atomic for the entry number, one store).
+__device__ void push_stream(const BatchArgs& a, int lane, uint32_t sid, const Progress& pr) {
+    uint32_t e = 0;
+    if (lane == 0) e = add_agent(a.queue + kQTail, 1u);
+    e = bcast(e);
+    const uint64_t s = static_cast<uint64_t>(pr.s), ct = static_cast<uint64_t>(pr.ct);
+    u32x4 v;
+    v.x = e + 1u;
+    v.y = lane == 0 ? sid : lane == 1 ? static_cast<uint32_t>(s) : static_cast<uint32_t>(ct);
+    v.z = lane == 0 ? static_cast<uint32_t>(pr.cnt) : lane == 1 ? static_cast<uint32_t>(s >> 32)
+                                                                : static_cast<uint32_t>(ct >> 32);
+    v.w = 0;
+    if (lane < 3)
+        __builtin_amdgcn_raw_buffer_store_b128(v, ring_rsrc(a), static_cast<int>((e & a.ring_mask) * kEntryBytes) + 16 * lane,
+                                               0, 16 /* sc1 */);
+}
+
 // Advance stream sid from pr: returns true when it is finished, false when yielded.
 template <bool TOP>
 __device__ __forceinline__ bool run_stream(const BatchArgs& a, const BuzRing& hash, uint8_t* sl, uint32_t* hs,
@@ -1362,6 +1455,49 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
     for (int i = lane; i < kNSlots * kSlotBytes / 4; i += kWave)
         reinterpret_cast<uint32_t*>(sl)[i] = static_cast<uint32_t>((i + 1) * 2654435761u) ^ (wave * 0x9E3779B9u);
 #endif
+#if KCDC_SCHED == 1
+    for (;;) {
+        Progress pr;
+        uint32_t sid;
+#if KCDC_TRACE
+        uint64_t tc = __builtin_amdgcn_s_memrealtime();
+#endif
+        // take a ticket; in the same round trip read how many streams were pushed
+        uint32_t t = 0, tail = 0;
+        if (lane == 0) t = add_agent(a.queue + kQHead, 1u);
+        if (lane == 1) tail = ld_agent(a.queue + kQTail);
+        t = __builtin_amdgcn_readlane(t, 0);
+        tail = __builtin_amdgcn_readlane(tail, 1);
+        if (!resolve_ticket(a, lane, t, sid, pr)) break;
+        // streams are waiting beyond this ticket => time-slice this one
+        const bool more = t + 1 < a.nstreams + tail;
+#if KCDC_TRACE
+        KCDC_QSTAT64(kQStat + 4, __builtin_amdgcn_s_memrealtime() - tc);
+        tc = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0 && pr.s == 0 && pr.ct < 0) a.trace[3 * sid + 0] = tc;
+#endif
+        const bool fin = run_stream<TOP>(a, hash, sl, hs, sid, pr, more, lane);
+#if KCDC_TRACE
+        KCDC_QSTAT64(kQStat + 8, __builtin_amdgcn_s_memrealtime() - tc);
+        tc = __builtin_amdgcn_s_memrealtime();
+#endif
+        if (fin) {
+#if KCDC_TRACE
+            if (lane == 0) {
+                a.trace[3 * sid + 1] = __builtin_amdgcn_s_memrealtime();
+                a.trace[3 * sid + 2] = blockIdx.x | (wave << 16);
+            }
+#endif
+            if (lane == 0) add_agent(a.queue + kQDone, 1u);
+        } else {
+            push_stream(a, lane, sid, pr);
+#if KCDC_TRACE
+            KCDC_QSTAT(kQStat + 0, 1u);
+            KCDC_QSTAT64(kQStat + 6, __builtin_amdgcn_s_memrealtime() - tc);
+#endif
+        }
+    }
+#else
     for (;;) {
         Progress pr;
 #if KCDC_TRACE
@@ -1399,6 +1535,523 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
 #endif
         }
     }
+#endif
+}
+
+// ========================================= pipelined persistent kernel (KCDC_SCHED 2)
+// One per-wave state machine over tiles.  Every tile warms its 64 lanes on the 64 bytes
+// before their segments (a 4 KiB piece in the wave's warm slot) and hashes 16 steps of
+// 128-byte runs (8 KiB step slot).  The warm piece and first step of the NEXT tile are
+// DMA'd during the current tile's last step, so a tile boundary exposes no latency:
+//  * next tile of the same region: always known in advance;
+//  * next stream (quantum spent, or the region's last tile with no further region): the
+//    next ticket is taken by an atomic at the START of that tile and its ring entry
+//    (progress + stream parameters, 7 tagged 16-byte sc1 granules) loaded mid-tile, so
+//    both global round trips (~5 us each under full HBM load) hide under the hashing.
+// Only a candidate that ends a region early (the next region is not known before the
+// tile ends) and the first tile of the launch expose a DMA latency.
+#ifndef KCDC_PIPE_YIELD_BYTES
+#define KCDC_PIPE_YIELD_BYTES (768 << 10)
+#endif
+constexpr int64_t kPipeYield = KCDC_PIPE_YIELD_BYTES;
+constexpr int kPEntryLanes = 7;
+constexpr int kPEntryStride = 128;
+
+struct WarmSlots {
+    __attribute__((aligned(16))) uint8_t b[kDmaWaves][kSlot];  // 4 KiB: the 64 bytes before each lane segment
+};
+
+struct PStream {
+    uint32_t sid;
+    int64_t n, off0;
+    const uint8_t* abase;
+    uint64_t cb, cap, cnt;
+    int64_t s, ct;  // chunk start; next tile coordinate of its region scan (< 0: region not set up)
+};
+
+__device__ __forceinline__ void pstream_fresh(PStream& st, uint32_t sid, uint64_t p, uint64_t n, uint64_t cb,
+                                              uint64_t cend) {
+    st.sid = sid;
+    st.n = static_cast<int64_t>(n);
+    st.off0 = static_cast<int64_t>(p & 15u);
+    st.abase = reinterpret_cast<const uint8_t*>(p - static_cast<uint64_t>(st.off0));
+    st.cb = cb;
+    st.cap = cend > cb ? cend - cb : 0;
+    st.cnt = 0;
+    st.s = 0;
+    st.ct = -1;
+}
+
+// Pin every field to a scalar register: the uniformity analysis otherwise loses track of
+// values carried through the switch paths, and each LDS-DMA (its buffer descriptor must be
+// scalar) then sits in a readfirstlane waterfall loop.
+__device__ __forceinline__ void uniformize(PStream& st) {
+    st.sid = __builtin_amdgcn_readfirstlane(st.sid);
+    st.n = static_cast<int64_t>(uni64(static_cast<uint64_t>(st.n)));
+    st.off0 = static_cast<int64_t>(uni64(static_cast<uint64_t>(st.off0)));
+    st.abase = reinterpret_cast<const uint8_t*>(uni64(reinterpret_cast<uint64_t>(st.abase)));
+    st.cb = uni64(st.cb);
+    st.cap = uni64(st.cap);
+    st.cnt = uni64(st.cnt);
+    st.s = static_cast<int64_t>(uni64(static_cast<uint64_t>(st.s)));
+    st.ct = static_cast<int64_t>(uni64(static_cast<uint64_t>(st.ct)));
+}
+
+__device__ __forceinline__ void emit_cut(const BatchArgs& a, PStream& st, int lane, int64_t v) {
+    if (lane == 0 && st.cnt < st.cap) a.cuts[st.cb + st.cnt] = static_cast<uint64_t>(v);
+    st.cnt++;
+}
+
+// Set up the next region to scan (chunks whose test range starts past the end are cut
+// at once); returns false when the stream is finished (all cuts emitted).
+__device__ __forceinline__ bool pstream_region(const BatchArgs& a, PStream& st, int lane) {
+    while (st.ct < 0) {
+        if (st.s >= st.n) return false;
+        const int64_t pf = st.s + static_cast<int64_t>(a.min_size) - 1;
+        if (pf >= st.n) {  // last chunk [s, n): nothing to test (splitter_buzhash32.go:29-40, 60-67)
+            emit_cut(a, st, lane, st.n);
+            st.s = st.n;
+            return false;
+        }
+        st.ct = (pf + st.off0) & ~int64_t(127);
+    }
+    return true;
+}
+
+// Ring entry of a yielded stream: granule l (< 7) = {tag, lo, hi, l == 0 ? sid : 0} of
+// word l in {cnt, s, ct, ptr, n, cb, cap}.  Written by lane 0 alone (7 uniform 16-byte
+// stores): a per-lane select chain over the words miscompiled (a word's high half read
+// an undefined register).
+__device__ __forceinline__ u32x4 pgranule(uint32_t tag, uint64_t w, uint32_t x) {
+    u32x4 v;
+    v.x = tag;
+    v.y = static_cast<uint32_t>(w);
+    v.z = static_cast<uint32_t>(w >> 32);
+    v.w = x;
+    return v;
+}
+// readlane returns int: widen through uint32_t, or a low word with bit 31 set sign-extends
+// into the high word (it did: pointers came back as 0xFFFFFFFF'xxxxxxxx).
+__device__ __forceinline__ uint64_t rl64(const u32x4& v, int l) {
+    const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(v.y, l));
+    const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readlane(v.z, l));
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+__device__ __forceinline__ void pentry_decode(PStream& st, const u32x4& v) {
+    st.sid = __builtin_amdgcn_readlane(v.w, 0);
+    st.cnt = rl64(v, 0);
+    st.s = static_cast<int64_t>(rl64(v, 1));
+    st.ct = static_cast<int64_t>(rl64(v, 2));
+    const uint64_t p = rl64(v, 3);
+    st.off0 = static_cast<int64_t>(p & 15u);
+    st.abase = reinterpret_cast<const uint8_t*>(p - static_cast<uint64_t>(st.off0));
+    st.n = static_cast<int64_t>(rl64(v, 4));
+    st.cb = rl64(v, 5);
+    st.cap = rl64(v, 6);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pring_rsrc(const BatchArgs& a) {
+    return __builtin_amdgcn_make_buffer_rsrc(a.ring, static_cast<short>(0),
+                                             static_cast<int>((a.ring_mask + 1u) * kPEntryStride), 0x00020000);
+}
+// Every lane loads (lane & 7): no divergent load, so no copy of the result that would
+// make the compiler wait for it early.
+__device__ __forceinline__ u32x4 pentry_load(const BatchArgs& a, int lane, uint32_t e) {
+    return __builtin_amdgcn_raw_buffer_load_b128(pring_rsrc(a),
+                                                 static_cast<int>((e & a.ring_mask) * kPEntryStride) + 16 * (lane & 7), 0,
+                                                 16 /* sc1 */);
+}
+__device__ __forceinline__ bool pentry_ok(const u32x4& v, int lane, uint32_t e) {
+    return __ballot(lane < kPEntryLanes && v.x != e + 1u) == 0;
+}
+
+#ifndef KCDC_DEBUG_CHECKS
+#define KCDC_DEBUG_CHECKS 0
+#endif
+// Debug builds: validate a resolved stream against the batch arrays; on a mismatch record
+// {code, sid, ticket, detail} in header words kQStat+16.. and return false (wave exits).
+__device__ __forceinline__ bool pcheck(const BatchArgs& a, int lane, const PStream& st, uint32_t tk, uint32_t where) {
+#if KCDC_DEBUG_CHECKS
+    uint32_t code = 0;
+    uint64_t detail = 0;
+    if (st.sid >= a.nstreams) {
+        code = 1;
+        detail = st.sid;
+    } else {
+        const uint64_t p = uni64(reinterpret_cast<uint64_t>(a.ptrs[st.sid]));
+        const uint64_t cb = uni64(a.cut_base[st.sid]);
+        if (reinterpret_cast<uint64_t>(st.abase) + static_cast<uint64_t>(st.off0) != p) {
+            code = 2;
+            detail = reinterpret_cast<uint64_t>(st.abase);
+        } else if (static_cast<uint64_t>(st.n) != uni64(a.lens[st.sid])) {
+            code = 3;
+            detail = static_cast<uint64_t>(st.n);
+        } else if (st.cb != cb) {
+            code = 4;
+            detail = st.cb;
+        } else if (st.cnt > st.cap) {
+            code = 5;
+            detail = st.cnt;
+        } else if (st.cap != (st.sid + 1 < a.nstreams ? uni64(a.cut_base[st.sid + 1]) : a.cuts_cap) - cb) {
+            code = 7;
+            detail = st.cap;
+        } else if (st.s < 0 || st.s > st.n) {
+            code = 6;
+            detail = static_cast<uint64_t>(st.s);
+        }
+    }
+    if (code) {
+        if (lane == 0) {
+            if (atomicAdd(a.queue + kQErr, 1u) == 0) {
+                a.queue[kQStat + 16] = code | (where << 8);
+                a.queue[kQStat + 17] = st.sid;
+                a.queue[kQStat + 18] = tk;
+                a.queue[kQStat + 19] = static_cast<uint32_t>(detail);
+                a.queue[kQStat + 20] = static_cast<uint32_t>(detail >> 32);
+                a.queue[kQStat + 21] = static_cast<uint32_t>(st.s);
+                a.queue[kQStat + 22] = static_cast<uint32_t>(st.ct);
+                a.queue[kQStat + 23] = static_cast<uint32_t>(st.cnt);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        return false;
+    }
+#endif
+    return true;
+}
+
+// Queue counter: ONE 64-bit word {head = tickets taken (low), tail = entries reserved
+// (high)} at header words 0..1, so a wave that yields one stream and takes the next does
+// both with one atomic.  Entries 0..n-1 are the streams' initial states (init_ring_kernel
+// writes them and sets tail = n); a reserved entry that ends up unused (its stream
+// finished in the tile) is written as a tombstone (sid 0xFFFFFFFF), which a taker skips.
+constexpr int kQHT = 0;
+constexpr uint32_t kTombstone = 0xFFFFFFFFu;
+__device__ __forceinline__ uint64_t qht_add(const BatchArgs& a, int lane, uint64_t inc) {
+    uint64_t v = 0;
+    if (lane == 0)
+        v = __hip_atomic_fetch_add((gu64*)(reinterpret_cast<uint64_t*>(a.queue + kQHT)), inc, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    return v;  // lane 0's register
+}
+__device__ __forceinline__ uint64_t qht_value(uint32_t lo_raw, uint32_t hi_raw) {
+    const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(lo_raw, 0));
+    const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readlane(hi_raw, 0));
+    return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+__device__ __forceinline__ uint64_t qht_take(const BatchArgs& a, int lane, uint64_t inc) {  // blocking
+    const uint64_t raw = qht_add(a, lane, inc);
+    return qht_value(static_cast<uint32_t>(raw), static_cast<uint32_t>(raw >> 32));
+}
+
+// Blocking resolution of ticket t (its ring entry, polled): 1 resolved, 2 tombstone (take
+// another ticket), 0 every stream is done (the wave exits).
+__device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st) {
+    const uint32_t n = a.nstreams;
+    for (uint32_t spin = 0;; spin++) {
+        const u32x4 v = pentry_load(a, lane, t);
+        if (pentry_ok(v, lane, t)) {
+            if (static_cast<uint32_t>(__builtin_amdgcn_readlane(v.w, 0)) == kTombstone) return 2;
+            pentry_decode(st, v);
+            return 1;
+        }
+        uint32_t stop = 0;
+        if (lane == 0) {
+            if (ld_agent(a.queue + kQDone) >= n) {
+                stop = 1;
+            } else if (spin >= kSpinCap) {
+                add_agent(a.queue + kQErr, 1u);
+                stop = 1;
+            }
+        }
+        if (bcast(stop)) return 0;
+        __builtin_amdgcn_s_sleep(16);
+    }
+}
+
+// Write entry e (tag e + 1): the stream's state, or a tombstone.
+__device__ __forceinline__ void pwrite(const BatchArgs& a, int lane, uint32_t e, const PStream& st, bool tomb) {
+    const uint32_t tag = e + 1u;
+    const uint64_t p = reinterpret_cast<uint64_t>(st.abase) + static_cast<uint64_t>(st.off0);
+    const __amdgpu_buffer_rsrc_t r = pring_rsrc(a);
+    const int base = static_cast<int>((e & a.ring_mask) * kPEntryStride);
+    if (lane == 0) {
+        __builtin_amdgcn_raw_buffer_store_b128(pgranule(tag, st.cnt, tomb ? kTombstone : st.sid), r, base + 0, 0,
+                                               16 /* sc1 */);
+        __builtin_amdgcn_raw_buffer_store_b128(pgranule(tag, static_cast<uint64_t>(st.s), 0), r, base + 16, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(pgranule(tag, static_cast<uint64_t>(st.ct), 0), r, base + 32, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(pgranule(tag, p, 0), r, base + 48, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(pgranule(tag, static_cast<uint64_t>(st.n), 0), r, base + 64, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(pgranule(tag, st.cb, 0), r, base + 80, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(pgranule(tag, st.cap, 0), r, base + 96, 0, 16);
+    }
+}
+
+// Mid-tile fetch of ring entry e by LDS-DMA (sc1) into the wave's warm slot, which is idle
+// between the tile's warm-up and its last step; read back after the last step's explicit
+// vmcnt wait.  A compiler-visible load instead would be in flight when the step's
+// (inline-asm, invisible) LDS-DMAs issue, and the waitcnt pass would then put a vmcnt
+// wait into the hash loop that also drains those DMAs.
+__device__ __forceinline__ void pentry_dma(const BatchArgs& a, int lane, uint32_t e, uint32_t m0) {
+    u32x4 d;
+    const uint64_t base = reinterpret_cast<uint64_t>(a.ring);
+    d.x = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(base));
+    d.y = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(base >> 32) & 0xFFFFu);
+    d.z = __builtin_amdgcn_readfirstlane((a.ring_mask + 1u) * kPEntryStride);
+    d.w = 0x00020000u;
+    const int32_t off = static_cast<int32_t>((e & a.ring_mask) * kPEntryStride) + 16 * (lane & 7);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen sc1 lds"
+                 :: "s"(m0), "v"(off), "s"(d) : "memory");
+}
+
+// Region bounds (coordinates) of the stream's current chunk.
+__device__ __forceinline__ void pregion(const BatchArgs& a, const PStream& st, int64_t& lo, int64_t& hi) {
+    const int64_t mn = static_cast<int64_t>(a.min_size), mx = static_cast<int64_t>(a.max_size);
+    lo = st.s + mn - 1 + st.off0;
+    hi = (st.s + mx - 1 < st.n - 1 ? st.s + mx - 1 : st.n - 1) + st.off0;
+}
+
+__device__ __forceinline__ void ptile_issue(const PStream& st, int64_t hi, uint32_t wl, uint32_t sl, int lane) {
+    const TileGeom g = tile_geom(st.ct, hi, st.abase, st.off0, st.off0 + st.n);
+    dma_piece(g.ld, g.ld.tb, wl, st.ct, g.L, -1, lane);
+    dma_step128(g.ld, g.ld.tb, sl, st.ct, g.L, 0, lane);
+}
+
+template <bool TOP>
+__global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_pipe_kernel(BatchArgs a) {
+    __shared__ BuzShared smtab;
+    __shared__ DmaSlots smslots;
+    __shared__ WarmSlots smwarm;
+    for (uint32_t i = threadIdx.x; i < 256u * 64u; i += blockDim.x) smtab.tab[i] = rotl_n(a.buz[i >> 6], a.buz_rot);
+    __syncthreads();
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    BuzRing hash;
+    hash.tab = reinterpret_cast<const char*>(smtab.tab);
+    hash.lane4 = static_cast<uint32_t>(lane) * 4u;
+    hash.mask = a.mask;
+    hash.h = 0;
+    uint8_t* sl = smslots.b[wave][0];
+    uint8_t* wl = smwarm.b[wave];
+    const uint32_t sl32 = lds_addr(sl), wl32 = lds_addr(wl);
+    const uint32_t lim = TOP ? a.buz_lim : 0u;
+    const int64_t mx = static_cast<int64_t>(a.max_size);
+
+    PStream cur;
+    int64_t budget = kNoYield;
+    // Blocking take of the next stream with a region to scan (t: a ticket already held,
+    // or ~0u to take one); false when every stream is done.  No LDS-DMA may be in flight.
+    auto take_blocking = [&](uint32_t t) -> bool {
+        for (;;) {
+            bool more = true;  // a held ticket's queue depth is unknown: allow yields
+            if (t == 0xFFFFFFFFu) {
+                const uint64_t ht = qht_take(a, lane, 1);
+                t = static_cast<uint32_t>(ht);
+                more = static_cast<uint64_t>(t) + 1 < (ht >> 32);
+            }
+            const uint32_t held = t;
+            const int r = presolve(a, lane, held, cur);
+            if (r == 0) return false;
+            t = 0xFFFFFFFFu;
+            if (r == 2) continue;  // tombstone
+            uniformize(cur);
+            if (!pcheck(a, lane, cur, held, 1)) return false;
+            budget = more && kPipeYield > 0 ? kPipeYield : kNoYield;
+            if (pstream_region(a, cur, lane)) return true;
+            if (lane == 0) {  // nothing left to scan
+                a.counts[cur.sid] = cur.cnt;
+                add_agent(a.queue + kQDone, 1u);
+            }
+        }
+    };
+    if (!take_blocking(0xFFFFFFFFu)) return;
+    bool issued = false;  // this tile's warm piece + step 0 are in flight
+    for (;;) {
+        uniformize(cur);
+        if (!pcheck(a, lane, cur, 0xFFFFFFFFu, 5)) return;
+        int64_t lo, hi;
+        pregion(a, cur, lo, hi);
+        const TileGeom g = tile_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n);
+        const int64_t ct = cur.ct, ct_next = ct + kWave * g.L;
+        const bool last_of_region = ct_next > hi;
+        const bool budget_out = budget - kWave * g.L <= 0;
+        bool ends_nocand = false;  // no candidate in this tile => the stream is finished
+        if (last_of_region) {
+            const int64_t s2 = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;
+            ends_nocand = s2 >= cur.n || s2 + static_cast<int64_t>(a.min_size) - 1 >= cur.n;
+        }
+        // The visit's last tile (absent a candidate): take the next ticket now, and reserve
+        // this stream's entry too when it will be yielded -- one atomic, hidden by the DMAs.
+        const bool switching = budget_out || ends_nocand;
+        const bool reserve = budget_out && !ends_nocand;
+        uint64_t ht_raw = 0;
+        if (switching) ht_raw = qht_add(a, lane, 1ull + (reserve ? (1ull << 32) : 0ull));
+        if (!issued) ptile_issue(cur, hi, wl32, sl32, lane);
+        const int64_t c0 = ct + lane * g.L;
+        uint32_t ht_lo = static_cast<uint32_t>(ht_raw), ht_hi = static_cast<uint32_t>(ht_raw >> 32);
+        {
+            uint32_t w16[16];
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(ht_lo), "+v"(ht_hi) :: "memory");
+            read_piece(wl, lane, c0 - 64, cur.off0, w16);
+            hash.clear();
+            hash.template block<kWarm>(w16);
+        }
+        uint32_t tk = 0, pe = 0;
+        bool nmore = false;
+        if (switching) {
+            const uint64_t ht = qht_value(ht_lo, ht_hi);
+            tk = static_cast<uint32_t>(ht);
+            pe = static_cast<uint32_t>(ht >> 32);
+            nmore = static_cast<uint64_t>(tk) + 1 < (ht >> 32) + (reserve ? 1u : 0u);
+        }
+        int nstate = 0;  // 0: next stream unresolved, 2: resolved, 3: + its first tile prefetched
+        PStream nx;
+        nx.ct = -1;
+        bool next_issued = false;
+        int64_t found = -1;
+        const int poll_step = g.nb > 1 ? g.nb / 2 : 0;
+        for (int n = 0; n < g.nb; n++) {
+            const int64_t c = c0 + 128 * n;
+            const typename BuzRing::State st0 = hash.save();
+            uint32_t dw[32];
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            read_step128(sl, lane, c, cur.off0, dw);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot free: refill it
+            __builtin_amdgcn_sched_barrier(0);
+            if (switching && n == poll_step) {
+                pentry_dma(a, lane, tk, wl32);
+                if (n == g.nb - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing to hide it under
+            }
+            if (n + 1 < g.nb) {
+                dma_step128(g.ld, g.ld.tb, sl32, ct, g.L, n + 1, lane);
+            } else if (!switching) {  // next tile of this region
+                if (!last_of_region) {
+                    PStream t2 = cur;
+                    t2.ct = ct_next;
+                    ptile_issue(t2, hi, wl32, sl32, lane);
+                    next_issued = true;
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#ifdef KCDC_EXP_MEMONLY
+            uint32_t m = 0;
+#pragma unroll
+            for (int i = 0; i < 32; i++) m |= dw[i];
+            asm volatile("" : "+v"(m));
+#else
+            const uint32_t m = hash.template step128<TOP>(dw, 0u);
+#endif
+            __builtin_amdgcn_sched_barrier(0);
+            if (m <= lim && found < 0 && c <= hi) {  // rare: exact re-run from global memory
+                uint32_t prv[16], cur32[32];
+                g.ld.load(c - 64, prv);
+                g.ld.load(c, cur32);
+                const int64_t blo = lo - c, bhi = hi - c;
+                const uint32_t idx = hash.exact(st0, prv, cur32, blo < 0 ? 0 : static_cast<int>(blo),
+                                                bhi > 127 ? 127 : static_cast<int>(bhi));
+                if (idx < 128u) found = c + idx;
+                // a wait the waitcnt pass sees: its scoreboard otherwise keeps these loads
+                // pending around the loop and waits for them in the hash loop (draining DMAs)
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+            }
+        }
+        // ---- end of tile
+        if (switching) {  // next stream: its entry landed in the warm slot (the last step's wait drained it)
+            const u32x4 ev = *reinterpret_cast<const u32x4*>(wl + 16 * (lane & 7));
+            if (pentry_ok(ev, lane, tk) && static_cast<uint32_t>(__builtin_amdgcn_readlane(ev.w, 0)) != kTombstone) {
+                pentry_decode(nx, ev);
+                uniformize(nx);
+                if (!pcheck(a, lane, nx, tk, 2)) return;
+                nstate = 2;
+                if (nx.ct < 0 && nx.s < nx.n && nx.s + static_cast<int64_t>(a.min_size) - 1 < nx.n)
+                    nx.ct = (nx.s + static_cast<int64_t>(a.min_size) - 1 + nx.off0) & ~int64_t(127);
+                if (nx.ct >= 0) {  // prefetch its first tile now, under this tile's bookkeeping
+                    int64_t nlo, nhi;
+                    pregion(a, nx, nlo, nhi);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // entry read before the slot refill
+                    ptile_issue(nx, nhi, wl32, sl32, lane);
+                    nstate = 3;
+                }
+            }
+        }
+        const uint64_t hit = __ballot(found >= 0);
+        bool region_changed = true;
+        if (hit) {
+            const int first = __builtin_ctzll(hit);
+            const int64_t f = static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, first))));
+            const int64_t next = f - cur.off0 + 1;
+            emit_cut(a, cur, lane, next);
+            cur.s = next;
+            cur.ct = -1;
+        } else if (last_of_region) {  // forced cut at max size (splitter_buzhash32.go:60-64) or the end
+            const int64_t next = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;
+            emit_cut(a, cur, lane, next);
+            cur.s = next;
+            cur.ct = -1;
+        } else {
+            cur.ct = ct_next;
+            budget -= kWave * g.L;
+            region_changed = false;
+        }
+        const bool live = pstream_region(a, cur, lane);
+        if (!live && lane == 0) {
+            a.counts[cur.sid] = cur.cnt;
+            add_agent(a.queue + kQDone, 1u);
+        }
+        if (!switching && live) {  // same stream, next tile
+            issued = next_issued && !region_changed;
+            if (next_issued && region_changed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stale prefetch
+            continue;
+        }
+        // ---- switch streams
+        if (reserve) {
+            pwrite(a, lane, pe, cur, !live);
+        } else if (live) {  // a candidate kept the stream alive past its predicted last tile
+            const uint64_t ht = qht_take(a, lane, 1ull << 32);
+            pwrite(a, lane, static_cast<uint32_t>(ht >> 32), cur, false);
+        }
+        if (nstate >= 2) {
+            cur = nx;
+            issued = nstate == 3;
+            budget = nmore && kPipeYield > 0 ? kPipeYield : kNoYield;
+            if (pstream_region(a, cur, lane)) continue;
+            if (lane == 0) {  // nothing left to scan in it
+                a.counts[cur.sid] = cur.cnt;
+                add_agent(a.queue + kQDone, 1u);
+            }
+            if (!take_blocking(0xFFFFFFFFu)) return;
+            issued = false;
+            continue;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no prefetch may remain in flight
+        if (!take_blocking(switching ? tk : 0xFFFFFFFFu)) return;
+        issued = false;
+    }
+}
+
+// Before each pipelined launch: zero the queue header (tail := n) and write ring entries
+// 0..n-1 = every stream's initial state; later entries get tag 0 (never a valid tag).
+__global__ void init_ring_kernel(BatchArgs a, uint32_t nslots) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < kQHeaderBytes / 4) a.queue[i] = i == static_cast<uint32_t>(kQHT) + 1u ? a.nstreams : 0u;  // tail = n
+    if (i >= nslots * 8u) return;
+    const uint32_t e = i >> 3, g = i & 7u;
+    u32x4 v = {0, 0, 0, 0};
+    if (e < a.nstreams && g < static_cast<uint32_t>(kPEntryLanes)) {
+        const uint64_t p = reinterpret_cast<uint64_t>(a.ptrs[e]);
+        const uint64_t cb = a.cut_base[e];
+        const uint64_t cend = e + 1 < a.nstreams ? a.cut_base[e + 1] : a.cuts_cap;
+        const uint64_t w = g == 0 ? 0ull                           // cnt
+                         : g == 1 ? 0ull                           // s
+                         : g == 2 ? ~0ull                          // ct = -1: region not set up
+                         : g == 3 ? p
+                         : g == 4 ? a.lens[e]
+                         : g == 5 ? cb
+                                  : (cend > cb ? cend - cb : 0ull);
+        v = pgranule(e + 1u, w, g == 0 ? e : 0u);
+    }
+    *reinterpret_cast<u32x4*>(reinterpret_cast<uint8_t*>(a.ring) + static_cast<size_t>(e) * kPEntryStride + 16 * g) = v;
 }
 
 // FIXED-*: cuts every chunk length (splitter_fixed.go:15-26); reads no data.
@@ -1745,8 +2398,10 @@ dev::BatchArgs base_args(const Algo& algo, const DeviceTables& t) {
     a.rk_shift = static_cast<uint32_t>(tables().rk_shift);
     return a;
 }
-#if KCDC_TRACE
+#if KCDC_TRACE || KCDC_DEBUG_CHECKS
 char* g_last_ws = nullptr;
+#endif
+#if KCDC_TRACE
 uint64_t* g_trace = nullptr;
 uint64_t g_trace_n = 0;
 int trace_reserve(uint64_t nstreams) {
@@ -1761,12 +2416,14 @@ int trace_reserve(uint64_t nstreams) {
 #endif
 }  // namespace
 
-#if KCDC_TRACE
-// Trace builds only: copy {start, end, workgroup | wave << 16} per stream of the last batch.
+#if KCDC_TRACE || KCDC_DEBUG_CHECKS
+// Trace / debug builds only: copy the last launch's queue header.
 extern "C" int kcdc_debug_queue_copy(uint32_t* host) {  // the last launch's queue header
     if (!g_last_ws) return -22;
     return hipMemcpy(host, g_last_ws, dev::kQHeaderBytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -5;
 }
+#endif
+#if KCDC_TRACE
 extern "C" int kcdc_debug_trace_copy(uint64_t* host, uint64_t nstreams) {
     if (!g_trace || nstreams > g_trace_n) return -22;
     return hipMemcpy(host, g_trace, 3 * 8 * nstreams, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -5;
@@ -1832,8 +2489,11 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         const unsigned need = (s.nstreams + wg_waves - 1) / wg_waves;
         const unsigned grid = need < cus ? need : cus;
         uint64_t ring = 1;
-        while (ring <= static_cast<uint64_t>(s.nstreams) + grid * wg_waves) ring <<= 1;
-        const size_t ring_bytes = dma ? 8 * ring : 0;
+        // KCDC_SCHED 1: a reserved ticket may be polled up to a quantum after it was taken,
+        // while the other waves keep pushing: size the ring with ample margin
+        const uint64_t live = static_cast<uint64_t>(s.nstreams) + (KCDC_SCHED >= 1 ? 8ull : 1ull) * grid * wg_waves;
+        while (ring <= live) ring <<= 1;
+        const size_t ring_bytes = dma ? (KCDC_SCHED == 2 ? 128 : KCDC_SCHED == 1 ? 64 : 8) * ring : 0;
         const size_t hdr = dev::kQHeaderBytes;
         const size_t bytes = hdr + ring_bytes + (dma ? 24ull * s.nstreams : 0);
         char* ws = nullptr;
@@ -1857,7 +2517,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
             ws = q.base;
         }
         a.queue = reinterpret_cast<uint32_t*>(ws);
-#if KCDC_TRACE
+#if KCDC_TRACE || KCDC_DEBUG_CHECKS
         g_last_ws = ws;
 #endif
         a.ring = reinterpret_cast<uint32_t*>(ws + hdr);
@@ -1868,16 +2528,36 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         a.trace = g_trace;
 #endif
         // header + ring zeroed per launch (the ring is also left empty by every finished launch)
-        hipError_t e = hipMemsetAsync(ws, 0, hdr + ring_bytes, st);
-        if (e != hipSuccess) return hip_fail(e, "queue reset");
+#if KCDC_SCHED == 2
+        if (dma) {
+            const uint32_t slots = static_cast<uint32_t>(ring);
+            const uint64_t threads = std::max<uint64_t>(8ull * slots, dev::kQHeaderBytes / 4);
+            hipLaunchKernelGGL(dev::init_ring_kernel, dim3(static_cast<unsigned>((threads + 255) / 256)), dim3(256), 0, st, a,
+                               slots);
+        } else
+#endif
+        {
+            hipError_t e = hipMemsetAsync(ws, 0, hdr + ring_bytes, st);
+            if (e != hipSuccess) return hip_fail(e, "queue reset");
+        }
         // persistent grid: one workgroup per CU, never more workgroups than the streams need
         if (dma) {
-            if (buz_frame(static_cast<uint32_t>(algo.mask())).top)
+            const bool top = buz_frame(static_cast<uint32_t>(algo.mask())).top;
+#if KCDC_SCHED == 2
+            if (top)
+                hipLaunchKernelGGL(dev::split_batch_pipe_kernel<true>, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0,
+                                   st, a);
+            else
+                hipLaunchKernelGGL(dev::split_batch_pipe_kernel<false>, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0,
+                                   st, a);
+#else
+            if (top)
                 hipLaunchKernelGGL(dev::split_batch_dma_kernel<true>, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0,
                                    st, a);
             else
                 hipLaunchKernelGGL(dev::split_batch_dma_kernel<false>, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0,
                                    st, a);
+#endif
         } else {
             const dim3 block(dev::kBatchWaves * dev::kWave);
             if (algo.kind == kBuzhash)

@@ -21,7 +21,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "kopia_amd", "csrc", "kcdc_kernels.hip")
 HIPCC = "/opt/rocm/bin/hipcc"
-KERNEL = "_ZN4kcdc3dev22split_batch_dma_kernelILb1EEEvNS0_9BatchArgsE"  # <TOP = true>
+KERNEL = "_ZN4kcdc3dev23split_batch_pipe_kernelILb1EEEvNS0_9BatchArgsE"  # <TOP = true>, KCDC_SCHED 2
 
 
 def _blocks(asm: str):

@@ -12,6 +12,7 @@ if [ "${2:-}" != "skip-tests" ]; then
 fi
 timeout -k 10 300 python -u tools/kbench.py --rounds 5 --reps 5 > $OUT/kbench.log 2>&1 || { tail -30 $OUT/kbench.log; exit 1; }
 cat $OUT/kbench.log
+[ "${3:-}" = "nopmc" ] && exit 0
 for pass in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS" \
             "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_WAVES SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_COUNT"; do
   n=$(echo $pass | cut -d' ' -f1)
