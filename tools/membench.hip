@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdint>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                            \
@@ -110,6 +111,7 @@ struct Cfg {
     Cfg{"run" #RUN "_s" #S "_w" #W "_aux" #AUX, seg_kernel<RUN, S, W, AUX>, RUN, S, W}
 
 int main(int argc, char** argv) {
+    const bool calib = argc > 1 && std::string(argv[1]) == "calib";  // one config, 4 launches (FETCH_SIZE calibration)
     const int64_t L = 2048;
     const int64_t total = int64_t(16) << 30;
     const uint32_t ntiles = static_cast<uint32_t>(total / (64 * L));
@@ -128,8 +130,9 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (int rep = 0; rep < 3; rep++) {
-      for (int layout = 0; layout < 3; layout++) {
+    if (calib) cfgs = {CFG(128, 2, 8, 2)};
+    for (int rep = 0; rep < (calib ? 1 : 3); rep++) {
+      for (int layout = 0; layout < (calib ? 1 : 3); layout++) {
         for (auto& c : cfgs) {
             const size_t lds = static_cast<size_t>(c.w) * c.s * 64 * c.run;
             if (lds > 160 * 1024) {
