@@ -1554,6 +1554,22 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
 #define KCDC_PIPE_YIELD_BYTES (768 << 10)
 #endif
 constexpr int64_t kPipeYield = KCDC_PIPE_YIELD_BYTES;
+#ifndef KCDC_PIPE_TAIL_YIELD_BYTES
+#define KCDC_PIPE_TAIL_YIELD_BYTES (768 << 10)  // = the long quantum: short tail quanta measured no gain (128K 1.366 vs 1.347 ms)
+#endif
+#ifndef KCDC_PIPE_TAIL_BACKLOG
+#define KCDC_PIPE_TAIL_BACKLOG 512
+#endif
+// Quantum of a visit from the number of streams queued behind the taken ticket: none
+// waiting -> run to completion; a long queue -> long quanta (few hand-offs); a short queue
+// (the end of the batch) -> short quanta, so streams finish together instead of the last
+// ones running a whole long quantum alone (the final idle tail was ~1 quantum per wave).
+constexpr int64_t kPipeTailYield = KCDC_PIPE_TAIL_YIELD_BYTES;
+constexpr int64_t kPipeTailBacklog = KCDC_PIPE_TAIL_BACKLOG;
+__device__ __forceinline__ int64_t pipe_quantum(int64_t backlog) {
+    if (backlog <= 0 || kPipeYield <= 0) return kNoYield;
+    return backlog > kPipeTailBacklog ? kPipeYield : kPipeTailYield;
+}
 constexpr int kPEntryLanes = 7;
 constexpr int kPEntryStride = 128;
 
@@ -1833,6 +1849,22 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
     uint8_t* sl = smslots.b[wave][0];
     uint8_t* wl = smwarm.b[wave];
     const uint32_t sl32 = lds_addr(sl), wl32 = lds_addr(wl);
+#if KCDC_TRACE  // per wave at trace[4 * global wave]: start, end, ticks in blocking takes, count
+    const uint32_t gw = blockIdx.x * kDmaWaves + wave;
+    uint64_t tr_block = 0, tr_nblock = 0, tr_last = 0;
+    if (lane == 0) a.trace[4 * gw] = __builtin_amdgcn_s_memrealtime();
+#define KCDC_PRET                                                                 \
+    do {                                                                          \
+        if (lane == 0) {                                                          \
+            a.trace[4 * gw + 1] = __builtin_amdgcn_s_memrealtime();                \
+            a.trace[4 * gw + 2] = tr_block;                                       \
+            a.trace[4 * gw + 3] = tr_last;                                        \
+        }                                                                         \
+        return;                                                                   \
+    } while (0)
+#else
+#define KCDC_PRET return
+#endif
     const uint32_t lim = TOP ? a.buz_lim : 0u;
     const int64_t mx = static_cast<int64_t>(a.max_size);
 
@@ -1840,13 +1872,24 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
     int64_t budget = kNoYield;
     // Blocking take of the next stream with a region to scan (t: a ticket already held,
     // or ~0u to take one); false when every stream is done.  No LDS-DMA may be in flight.
-    auto take_blocking = [&](uint32_t t) -> bool {
+    auto take_blocking = [&](uint32_t t, int64_t backlog_hint) -> bool {
+#if KCDC_TRACE
+        const uint64_t tb0 = __builtin_amdgcn_s_memrealtime();
+        tr_last = tb0;
+        struct Acc {
+            uint64_t t0, &sum, &cnt;
+            __device__ ~Acc() {
+                sum += __builtin_amdgcn_s_memrealtime() - t0;
+                cnt++;
+            }
+        } acc{tb0, tr_block, tr_nblock};
+#endif
         for (;;) {
-            bool more = true;  // a held ticket's queue depth is unknown: allow yields
+            int64_t backlog = backlog_hint;  // queue depth behind a ticket already held (caller's estimate)
             if (t == 0xFFFFFFFFu) {
                 const uint64_t ht = qht_take(a, lane, 1);
                 t = static_cast<uint32_t>(ht);
-                more = static_cast<uint64_t>(t) + 1 < (ht >> 32);
+                backlog = static_cast<int64_t>(ht >> 32) - static_cast<int64_t>(t) - 1;
             }
             const uint32_t held = t;
             const int r = presolve(a, lane, held, cur);
@@ -1855,7 +1898,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             if (r == 2) continue;  // tombstone
             uniformize(cur);
             if (!pcheck(a, lane, cur, held, 1)) return false;
-            budget = more && kPipeYield > 0 ? kPipeYield : kNoYield;
+            budget = pipe_quantum(backlog);
             if (pstream_region(a, cur, lane)) return true;
             if (lane == 0) {  // nothing left to scan
                 a.counts[cur.sid] = cur.cnt;
@@ -1863,7 +1906,11 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             }
         }
     };
-    if (!take_blocking(0xFFFFFFFFu)) return;
+    {
+        const uint32_t gw0 = blockIdx.x * kDmaWaves + wave;  // first ticket: preassigned (see init_ring_kernel)
+        const int64_t nw = static_cast<int64_t>(gridDim.x) * kDmaWaves;
+        if (!take_blocking(gw0 < a.nstreams ? gw0 : 0xFFFFFFFFu, static_cast<int64_t>(a.nstreams) - nw)) KCDC_PRET;
+    }
     bool issued = false;  // this tile's warm piece + step 0 are in flight
     for (;;) {
         uniformize(cur);
@@ -1884,7 +1931,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         const bool switching = budget_out || ends_nocand;
         const bool reserve = budget_out && !ends_nocand;
         uint64_t ht_raw = 0;
-        if (switching) ht_raw = qht_add(a, lane, 1ull + (reserve ? (1ull << 32) : 0ull));
+        if (switching) ht_raw = qht_add(a, lane, 1);  // the next stream's ticket
         if (!issued) ptile_issue(cur, hi, wl32, sl32, lane);
         const int64_t c0 = ct + lane * g.L;
         uint32_t ht_lo = static_cast<uint32_t>(ht_raw), ht_hi = static_cast<uint32_t>(ht_raw >> 32);
@@ -1897,13 +1944,13 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             hash.template block<kWarm>(w16);
         }
         uint32_t tk = 0, pe = 0;
-        bool nmore = false;
+        int64_t nbacklog = 0;
         if (switching) {
             const uint64_t ht = qht_value(ht_lo, ht_hi);
             tk = static_cast<uint32_t>(ht);
-            pe = static_cast<uint32_t>(ht >> 32);
-            nmore = static_cast<uint64_t>(tk) + 1 < (ht >> 32) + (reserve ? 1u : 0u);
+            nbacklog = static_cast<int64_t>(ht >> 32) + (reserve ? 1 : 0) - static_cast<int64_t>(tk) - 1;
         }
+        uint64_t pe_raw = 0;
         int nstate = 0;  // 0: next stream unresolved, 2: resolved, 3: + its first tile prefetched
         PStream nx;
         nx.ct = -1;
@@ -1919,6 +1966,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             read_step128(sl, lane, c, cur.off0, dw);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot free: refill it
             __builtin_amdgcn_sched_barrier(0);
+            if (reserve && n == g.nb - 1) pe_raw = qht_add(a, lane, 1ull << 32);  // this stream's entry, late
             if (switching && n == poll_step) {
                 pentry_dma(a, lane, tk, wl32);
                 if (n == g.nb - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing to hide it under
@@ -1957,24 +2005,6 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             }
         }
         // ---- end of tile
-        if (switching) {  // next stream: its entry landed in the warm slot (the last step's wait drained it)
-            const u32x4 ev = *reinterpret_cast<const u32x4*>(wl + 16 * (lane & 7));
-            if (pentry_ok(ev, lane, tk) && static_cast<uint32_t>(__builtin_amdgcn_readlane(ev.w, 0)) != kTombstone) {
-                pentry_decode(nx, ev);
-                uniformize(nx);
-                if (!pcheck(a, lane, nx, tk, 2)) return;
-                nstate = 2;
-                if (nx.ct < 0 && nx.s < nx.n && nx.s + static_cast<int64_t>(a.min_size) - 1 < nx.n)
-                    nx.ct = (nx.s + static_cast<int64_t>(a.min_size) - 1 + nx.off0) & ~int64_t(127);
-                if (nx.ct >= 0) {  // prefetch its first tile now, under this tile's bookkeeping
-                    int64_t nlo, nhi;
-                    pregion(a, nx, nlo, nhi);
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // entry read before the slot refill
-                    ptile_issue(nx, nhi, wl32, sl32, lane);
-                    nstate = 3;
-                }
-            }
-        }
         const uint64_t hit = __ballot(found >= 0);
         bool region_changed = true;
         if (hit) {
@@ -2004,37 +2034,62 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             if (next_issued && region_changed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stale prefetch
             continue;
         }
-        // ---- switch streams
+        // ---- switch streams: requeue this one first (its reserve atomic was issued in the
+        // last step, so no prefetch DMA is in flight behind it), then prefetch the next
         if (reserve) {
+            pe = static_cast<uint32_t>(qht_value(static_cast<uint32_t>(pe_raw), static_cast<uint32_t>(pe_raw >> 32)) >> 32);
             pwrite(a, lane, pe, cur, !live);
         } else if (live) {  // a candidate kept the stream alive past its predicted last tile
             const uint64_t ht = qht_take(a, lane, 1ull << 32);
             pwrite(a, lane, static_cast<uint32_t>(ht >> 32), cur, false);
         }
+        if (switching) {  // next stream: its entry landed in the warm slot (the last step's wait drained it)
+            const u32x4 ev = *reinterpret_cast<const u32x4*>(wl + 16 * (lane & 7));
+            if (pentry_ok(ev, lane, tk) && static_cast<uint32_t>(__builtin_amdgcn_readlane(ev.w, 0)) != kTombstone) {
+                pentry_decode(nx, ev);
+                uniformize(nx);
+                if (!pcheck(a, lane, nx, tk, 2)) return;
+                nstate = 2;
+                if (nx.ct < 0 && nx.s < nx.n && nx.s + static_cast<int64_t>(a.min_size) - 1 < nx.n)
+                    nx.ct = (nx.s + static_cast<int64_t>(a.min_size) - 1 + nx.off0) & ~int64_t(127);
+                if (nx.ct >= 0) {  // prefetch its first tile now, under this tile's bookkeeping
+                    int64_t nlo, nhi;
+                    pregion(a, nx, nlo, nhi);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // entry read before the slot refill
+                    ptile_issue(nx, nhi, wl32, sl32, lane);
+                    nstate = 3;
+                }
+            }
+        }
         if (nstate >= 2) {
             cur = nx;
             issued = nstate == 3;
-            budget = nmore && kPipeYield > 0 ? kPipeYield : kNoYield;
+            budget = pipe_quantum(nbacklog);
             if (pstream_region(a, cur, lane)) continue;
             if (lane == 0) {  // nothing left to scan in it
                 a.counts[cur.sid] = cur.cnt;
                 add_agent(a.queue + kQDone, 1u);
             }
-            if (!take_blocking(0xFFFFFFFFu)) return;
+            if (!take_blocking(0xFFFFFFFFu, 0)) KCDC_PRET;
             issued = false;
             continue;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no prefetch may remain in flight
-        if (!take_blocking(switching ? tk : 0xFFFFFFFFu)) return;
+        if (!take_blocking(switching ? tk : 0xFFFFFFFFu, nbacklog)) KCDC_PRET;
         issued = false;
     }
 }
 
 // Before each pipelined launch: zero the queue header (tail := n) and write ring entries
 // 0..n-1 = every stream's initial state; later entries get tag 0 (never a valid tag).
-__global__ void init_ring_kernel(BatchArgs a, uint32_t nslots) {
+// Head starts at min(n, launch waves): wave w's first ticket is w, taken without an atomic
+// (2048 waves hitting one counter at launch serialised for ~100 us).
+__global__ void init_ring_kernel(BatchArgs a, uint32_t nslots, uint32_t nwaves) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < kQHeaderBytes / 4) a.queue[i] = i == static_cast<uint32_t>(kQHT) + 1u ? a.nstreams : 0u;  // tail = n
+    if (i < kQHeaderBytes / 4)
+        a.queue[i] = i == static_cast<uint32_t>(kQHT) + 1u ? a.nstreams  // tail = n
+                   : i == static_cast<uint32_t>(kQHT) ? (nwaves < a.nstreams ? nwaves : a.nstreams)
+                                                      : 0u;
     if (i >= nslots * 8u) return;
     const uint32_t e = i >> 3, g = i & 7u;
     u32x4 v = {0, 0, 0, 0};
@@ -2524,7 +2579,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         a.states = reinterpret_cast<uint64_t*>(ws + hdr + ring_bytes);
         a.ring_mask = static_cast<uint32_t>(ring - 1);
 #if KCDC_TRACE
-        if (trace_reserve(s.nstreams) != 0) return set_error(-12, "trace buffer");
+        if (trace_reserve(std::max<uint64_t>(s.nstreams, 2ull * grid * wg_waves)) != 0) return set_error(-12, "trace buffer");
         a.trace = g_trace;
 #endif
         // header + ring zeroed per launch (the ring is also left empty by every finished launch)
@@ -2533,7 +2588,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
             const uint32_t slots = static_cast<uint32_t>(ring);
             const uint64_t threads = std::max<uint64_t>(8ull * slots, dev::kQHeaderBytes / 4);
             hipLaunchKernelGGL(dev::init_ring_kernel, dim3(static_cast<unsigned>((threads + 255) / 256)), dim3(256), 0, st, a,
-                               slots);
+                               slots, grid * wg_waves);
         } else
 #endif
         {

@@ -28,7 +28,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // layout 0: tile t at t*64L (linear).  layout 1: 4096 "streams" of 4 MiB, tile t is tile
 // t/4096 of stream t%4096 (concurrent tiles share their offset mod 4 MiB, as in the batch
 // splitter).  layout 2: as 1 with the tile index skewed by the stream id.
-template <int RUN, int S, int W, int AUX>
+template <int RUN, int S, int W, int AUX, int D = 0>
 __global__ __launch_bounds__(W * 64) void seg_kernel(const uint8_t* base, int64_t L, uint32_t ntiles,
                                                      uint32_t* counter, uint32_t* out, int layout) {
     constexpr int kSlot = 64 * RUN;       // bytes per round
@@ -83,6 +83,11 @@ __global__ __launch_bounds__(W * 64) void seg_kernel(const uint8_t* base, int64_
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             if (r + S < rounds) issue(r + S, slot);
+            // emulated hashing: D dependent VALU ops (rotate + xor chains, 2 per iteration)
+#pragma unroll 16
+            for (int k = 0; k < D; k++) {
+                acc = __builtin_amdgcn_alignbit(acc, acc, 31) ^ (acc + k);
+            }
             qs = qs + 1 == S ? 0 : qs + 1;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -109,6 +114,8 @@ struct Cfg {
 
 #define CFG(RUN, S, W, AUX) \
     Cfg{"run" #RUN "_s" #S "_w" #W "_aux" #AUX, seg_kernel<RUN, S, W, AUX>, RUN, S, W}
+#define CFGD(RUN, S, W, AUX, D) \
+    Cfg{"run" #RUN "_s" #S "_w" #W "_aux" #AUX "_d" #D, seg_kernel<RUN, S, W, AUX, D>, RUN, S, W}
 
 int main(int argc, char** argv) {
     const bool calib = argc > 1 && std::string(argv[1]) == "calib";  // one config, 4 launches (FETCH_SIZE calibration)
@@ -131,8 +138,13 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     if (calib) cfgs = {CFG(128, 2, 8, 2)};
-    for (int rep = 0; rep < (calib ? 1 : 3); rep++) {
-      for (int layout = 0; layout < (calib ? 1 : 3); layout++) {
+    const bool depth = argc > 1 && std::string(argv[1]) == "depth";  // pipeline depth vs emulated compute
+    if (depth)
+        cfgs = {CFGD(128, 1, 8, 2, 0),   CFGD(128, 2, 8, 2, 0),   CFGD(128, 1, 8, 2, 200), CFGD(128, 2, 8, 2, 200),
+                CFGD(128, 1, 8, 2, 400), CFGD(128, 2, 8, 2, 400), CFGD(64, 3, 8, 0, 200),  CFGD(64, 3, 8, 0, 100),
+                CFGD(128, 2, 6, 2, 200), CFGD(128, 2, 6, 2, 400), CFGD(64, 2, 8, 0, 100),  CFGD(64, 4, 8, 0, 100)};
+    for (int rep = 0; rep < (calib ? 1 : 2); rep++) {
+      for (int layout = (depth ? 1 : 0); layout < (calib ? 1 : depth ? 2 : 3); layout++) {
         for (auto& c : cfgs) {
             const size_t lds = static_cast<size_t>(c.w) * c.s * 64 * c.run;
             if (lds > 160 * 1024) {
