@@ -1570,7 +1570,24 @@ __device__ __forceinline__ int64_t pipe_quantum(int64_t backlog) {
     if (backlog <= 0 || kPipeYield <= 0) return kNoYield;
     return backlog > kPipeTailBacklog ? kPipeYield : kPipeTailYield;
 }
-constexpr int kPEntryLanes = 7;
+constexpr int kPEntryLanes = 8;
+// Probe entries (sid | kProbeBit): when waves wait for work at the end of a batch, an owner
+// with at least two tiles of its region left queues a probe that scans the region's upper
+// half while the owner scans the lower half; a handshake word (pword) decides which of the
+// two finishes the region.  Off by default: correct (debug-checked parity), but no faster on
+// the 4096 x 4 MiB batch -- the tail's idle waves are largely compensated by their SIMD
+// siblings running alone.
+constexpr uint32_t kProbeBit = 0x80000000u;
+#ifndef KCDC_PROBES
+#define KCDC_PROBES 0
+#endif
+constexpr int64_t kProbeMinHalf = int64_t(64) * KCDC_LANE_MAX;  // one full tile
+#ifndef KCDC_PROBE_BACKLOG
+#define KCDC_PROBE_BACKLOG 64
+#endif
+// Owners poll the queue counter (are waves waiting?) only in visits taken with a backlog
+// below this: a per-tile load of the hammered counter costs ~10% outside the tail.
+constexpr int64_t kProbeBacklog = KCDC_PROBE_BACKLOG;
 constexpr int kPEntryStride = 128;
 
 struct WarmSlots {
@@ -1578,11 +1595,13 @@ struct WarmSlots {
 };
 
 struct PStream {
-    uint32_t sid;
+    uint32_t sid;    // | kProbeBit for a probe
     int64_t n, off0;
     const uint8_t* abase;
     uint64_t cb, cap, cnt;
-    int64_t s, ct;  // chunk start; next tile coordinate of its region scan (< 0: region not set up)
+    int64_t s, ct;   // chunk start (a probe carries its owner's); next tile coordinate (< 0: not set up)
+    uint32_t epoch;  // the stream's probe epoch (one per region that spawned a probe)
+    int64_t aux;     // owner: coordinate where this region's probe starts (0: none); probe: range end
 };
 
 __device__ __forceinline__ void pstream_fresh(PStream& st, uint32_t sid, uint64_t p, uint64_t n, uint64_t cb,
@@ -1596,6 +1615,8 @@ __device__ __forceinline__ void pstream_fresh(PStream& st, uint32_t sid, uint64_
     st.cnt = 0;
     st.s = 0;
     st.ct = -1;
+    st.epoch = 0;
+    st.aux = 0;
 }
 
 // Pin every field to a scalar register: the uniformity analysis otherwise loses track of
@@ -1611,6 +1632,8 @@ __device__ __forceinline__ void uniformize(PStream& st) {
     st.cnt = uni64(st.cnt);
     st.s = static_cast<int64_t>(uni64(static_cast<uint64_t>(st.s)));
     st.ct = static_cast<int64_t>(uni64(static_cast<uint64_t>(st.ct)));
+    st.epoch = __builtin_amdgcn_readfirstlane(st.epoch);
+    st.aux = static_cast<int64_t>(uni64(static_cast<uint64_t>(st.aux)));
 }
 
 __device__ __forceinline__ void emit_cut(const BatchArgs& a, PStream& st, int lane, int64_t v) {
@@ -1664,6 +1687,8 @@ __device__ __forceinline__ void pentry_decode(PStream& st, const u32x4& v) {
     st.n = static_cast<int64_t>(rl64(v, 4));
     st.cb = rl64(v, 5);
     st.cap = rl64(v, 6);
+    st.aux = static_cast<int64_t>(rl64(v, 7));
+    st.epoch = static_cast<uint32_t>(__builtin_amdgcn_readlane(v.w, 7));
 }
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t pring_rsrc(const BatchArgs& a) {
     return __builtin_amdgcn_make_buffer_rsrc(a.ring, static_cast<short>(0),
@@ -1689,16 +1714,17 @@ __device__ __forceinline__ bool pcheck(const BatchArgs& a, int lane, const PStre
 #if KCDC_DEBUG_CHECKS
     uint32_t code = 0;
     uint64_t detail = 0;
-    if (st.sid >= a.nstreams) {
+    const uint32_t sid = st.sid & ~kProbeBit;
+    if (sid >= a.nstreams) {
         code = 1;
         detail = st.sid;
     } else {
-        const uint64_t p = uni64(reinterpret_cast<uint64_t>(a.ptrs[st.sid]));
-        const uint64_t cb = uni64(a.cut_base[st.sid]);
+        const uint64_t p = uni64(reinterpret_cast<uint64_t>(a.ptrs[sid]));
+        const uint64_t cb = uni64(a.cut_base[sid]);
         if (reinterpret_cast<uint64_t>(st.abase) + static_cast<uint64_t>(st.off0) != p) {
             code = 2;
             detail = reinterpret_cast<uint64_t>(st.abase);
-        } else if (static_cast<uint64_t>(st.n) != uni64(a.lens[st.sid])) {
+        } else if (static_cast<uint64_t>(st.n) != uni64(a.lens[sid])) {
             code = 3;
             detail = static_cast<uint64_t>(st.n);
         } else if (st.cb != cb) {
@@ -1707,10 +1733,10 @@ __device__ __forceinline__ bool pcheck(const BatchArgs& a, int lane, const PStre
         } else if (st.cnt > st.cap) {
             code = 5;
             detail = st.cnt;
-        } else if (st.cap != (st.sid + 1 < a.nstreams ? uni64(a.cut_base[st.sid + 1]) : a.cuts_cap) - cb) {
+        } else if (st.cap != (sid + 1 < a.nstreams ? uni64(a.cut_base[sid + 1]) : a.cuts_cap) - cb) {
             code = 7;
             detail = st.cap;
-        } else if (st.s < 0 || st.s > st.n) {
+        } else if (!(st.sid & kProbeBit) && (st.s < 0 || st.s > st.n)) {
             code = 6;
             detail = static_cast<uint64_t>(st.s);
         }
@@ -1799,6 +1825,8 @@ __device__ __forceinline__ void pwrite(const BatchArgs& a, int lane, uint32_t e,
         __builtin_amdgcn_raw_buffer_store_b128(pgranule(tag, static_cast<uint64_t>(st.n), 0), r, base + 64, 0, 16);
         __builtin_amdgcn_raw_buffer_store_b128(pgranule(tag, st.cb, 0), r, base + 80, 0, 16);
         __builtin_amdgcn_raw_buffer_store_b128(pgranule(tag, st.cap, 0), r, base + 96, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(pgranule(tag, static_cast<uint64_t>(st.aux), st.epoch), r, base + 112,
+                                               0, 16);
     }
 }
 
@@ -1821,9 +1849,43 @@ __device__ __forceinline__ void pentry_dma(const BatchArgs& a, int lane, uint32_
 
 // Region bounds (coordinates) of the stream's current chunk.
 __device__ __forceinline__ void pregion(const BatchArgs& a, const PStream& st, int64_t& lo, int64_t& hi) {
+    if (st.sid & kProbeBit) {  // a probe scans [ct, aux] (coordinates); s stays the owner's
+        lo = st.ct;
+        hi = st.aux;
+        return;
+    }
     const int64_t mn = static_cast<int64_t>(a.min_size), mx = static_cast<int64_t>(a.max_size);
     lo = st.s + mn - 1 + st.off0;
     hi = (st.s + mx - 1 < st.n - 1 ? st.s + mx - 1 : st.n - 1) + st.off0;
+}
+
+// Probe handshake: one 64-bit word per stream (16-B stride in the queue workspace),
+// lo = epoch << 2 | state, hi = the probe's first candidate - (s + off0) + 1 (0: none).
+// state 0: probe running (or none out), 1: the probe posted its candidate, 2: the owner
+// found nothing below the probe's start and handed the region over.  Whoever arrives
+// second finishes the region; the owner cancels a probe by moving to the next epoch.
+// Invariant: while a stream has no probe out its word is {epoch, 0, 0}.
+__device__ __forceinline__ uint64_t pword(uint32_t epoch, uint32_t state, uint32_t cand) {
+    return (static_cast<uint64_t>(cand) << 32) | ((epoch & 0x3FFFFFFFu) << 2) | state;
+}
+__device__ __forceinline__ uint64_t* probe_word(const BatchArgs& a, uint32_t sid) {
+    return reinterpret_cast<uint64_t*>(reinterpret_cast<uint32_t*>(a.states) + 4ull * (sid & ~kProbeBit));
+}
+// Lane 0 compare-and-swaps the word; returns the value it found (== expect: swapped).
+__device__ __forceinline__ uint64_t probe_cas(const BatchArgs& a, int lane, uint32_t sid, uint64_t expect,
+                                              uint64_t desired) {
+    uint64_t old = expect;
+    if (lane == 0)
+        __hip_atomic_compare_exchange_strong((gu64*)probe_word(a, sid), &old, desired, __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return qht_value(static_cast<uint32_t>(old), static_cast<uint32_t>(old >> 32));
+}
+__device__ __forceinline__ void probe_reset(const BatchArgs& a, int lane, uint32_t sid, uint32_t epoch) {
+    if (lane == 0) st_agent64(probe_word(a, sid), pword(epoch, 0, 0));
+}
+// A probe's per-tile poll of the word (lane 0; consume it behind a wait point).
+__device__ __forceinline__ uint64_t probe_poll(const BatchArgs& a, int lane, uint32_t sid) {
+    return lane == 0 ? ld_agent64(probe_word(a, sid)) : 0ull;
 }
 
 __device__ __forceinline__ void ptile_issue(const PStream& st, int64_t hi, uint32_t wl, uint32_t sl, int lane) {
@@ -1870,6 +1932,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
 
     PStream cur;
     int64_t budget = kNoYield;
+    bool dry = false;  // the queue was (nearly) dry when this stream was taken: probes may pay
     // Blocking take of the next stream with a region to scan (t: a ticket already held,
     // or ~0u to take one); false when every stream is done.  No LDS-DMA may be in flight.
     auto take_blocking = [&](uint32_t t, int64_t backlog_hint) -> bool {
@@ -1898,7 +1961,8 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             if (r == 2) continue;  // tombstone
             uniformize(cur);
             if (!pcheck(a, lane, cur, held, 1)) return false;
-            budget = pipe_quantum(backlog);
+            budget = (cur.sid & kProbeBit) ? kNoYield : pipe_quantum(backlog);
+            dry = backlog < kProbeBacklog;
             if (pstream_region(a, cur, lane)) return true;
             if (lane == 0) {  // nothing left to scan
                 a.counts[cur.sid] = cur.cnt;
@@ -1921,24 +1985,45 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         const int64_t ct = cur.ct, ct_next = ct + kWave * g.L;
         const bool last_of_region = ct_next > hi;
         const bool budget_out = budget - kWave * g.L <= 0;
-        bool ends_nocand = false;  // no candidate in this tile => the stream is finished
-        if (last_of_region) {
+        const bool is_probe = (cur.sid & kProbeBit) != 0;
+        bool ends_nocand = false;  // no candidate in this tile => the stream (or probe) is finished
+        if (is_probe) {
+            ends_nocand = last_of_region;
+        } else if (last_of_region) {
             const int64_t s2 = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;
             ends_nocand = s2 >= cur.n || s2 + static_cast<int64_t>(a.min_size) - 1 >= cur.n;
         }
+        // The owner's last tile below its probe's start: it hands the region over (or takes
+        // the probe's posted answer) at the tile end.
+        const bool lower_end = KCDC_PROBES && !is_probe && cur.aux > 0 && ct_next >= cur.aux;
         // The visit's last tile (absent a candidate): take the next ticket now, and reserve
         // this stream's entry too when it will be yielded -- one atomic, hidden by the DMAs.
-        const bool switching = budget_out || ends_nocand;
-        const bool reserve = budget_out && !ends_nocand;
+        const bool switching = budget_out || ends_nocand || lower_end;
+        const bool reserve = budget_out && !ends_nocand && !lower_end;
         uint64_t ht_raw = 0;
         if (switching) ht_raw = qht_add(a, lane, 1);  // the next stream's ticket
+        // May this tile spawn a probe (no probe out, the queue dry: waves wait for work, room
+        // for two halves)?  A probe polls its stream's handshake word (cancelled?) every tile.
+        const bool may_split = KCDC_PROBES && dry && !is_probe && cur.aux == 0 && !last_of_region &&
+                               hi - ct_next + 1 >= 2 * kProbeMinHalf;
+        u32x4 pr = {0, 0, 0, 0};
+        if (is_probe) {
+            const uint64_t w = probe_poll(a, lane, cur.sid);
+            pr.x = static_cast<uint32_t>(w);
+            pr.y = static_cast<uint32_t>(w >> 32);
+        }
+        uint64_t qc_raw = 0;
+        if (may_split && lane == 0) qc_raw = ld_agent64(reinterpret_cast<uint64_t*>(a.queue + kQHT));
         if (!issued) ptile_issue(cur, hi, wl32, sl32, lane);
         const int64_t c0 = ct + lane * g.L;
         uint32_t ht_lo = static_cast<uint32_t>(ht_raw), ht_hi = static_cast<uint32_t>(ht_raw >> 32);
+        uint32_t qc_lo = static_cast<uint32_t>(qc_raw), qc_hi = static_cast<uint32_t>(qc_raw >> 32);
         {
             uint32_t w16[16];
             __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(ht_lo), "+v"(ht_hi) :: "memory");
+            asm volatile("s_waitcnt vmcnt(0)"
+                         : "+v"(ht_lo), "+v"(ht_hi), "+v"(qc_lo), "+v"(qc_hi), "+v"(pr.x), "+v"(pr.y), "+v"(pr.z),
+                           "+v"(pr.w)::"memory");
             read_piece(wl, lane, c0 - 64, cur.off0, w16);
             hash.clear();
             hash.template block<kWarm>(w16);
@@ -1950,14 +2035,24 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             tk = static_cast<uint32_t>(ht);
             nbacklog = static_cast<int64_t>(ht >> 32) + (reserve ? 1 : 0) - static_cast<int64_t>(tk) - 1;
         }
+        // a probe whose owner moved on (found a cut below it): drop it, skip the tile
+        const bool probe_dead = is_probe && (static_cast<uint32_t>(__builtin_amdgcn_readlane(pr.x, 0)) >> 2) !=
+                                                (cur.epoch & 0x3FFFFFFFu);
+        bool split = false;
+        if (may_split) {
+            const uint64_t qc = qht_value(qc_lo, qc_hi);
+            split = static_cast<uint32_t>(qc) >= static_cast<uint32_t>(qc >> 32);  // head >= tail: waves wait
+        }
+        const uint64_t nres = (reserve ? 1u : 0u) + (split ? 1u : 0u);  // entries this tile will write
         uint64_t pe_raw = 0;
+        bool res_issued = false;
         int nstate = 0;  // 0: next stream unresolved, 2: resolved, 3: + its first tile prefetched
         PStream nx;
         nx.ct = -1;
         bool next_issued = false;
         int64_t found = -1;
         const int poll_step = g.nb > 1 ? g.nb / 2 : 0;
-        for (int n = 0; n < g.nb; n++) {
+        for (int n = 0; n < (probe_dead ? 0 : g.nb); n++) {
             const int64_t c = c0 + 128 * n;
             const typename BuzRing::State st0 = hash.save();
             uint32_t dw[32];
@@ -1966,7 +2061,10 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             read_step128(sl, lane, c, cur.off0, dw);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot free: refill it
             __builtin_amdgcn_sched_barrier(0);
-            if (reserve && n == g.nb - 1) pe_raw = qht_add(a, lane, 1ull << 32);  // this stream's entry, late
+            if (nres && n == g.nb - 1) {  // this stream's entry (and its probe's), reserved late
+                pe_raw = qht_add(a, lane, nres << 32);
+                res_issued = true;
+            }
             if (switching && n == poll_step) {
                 pentry_dma(a, lane, tk, wl32);
                 if (n == g.nb - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing to hide it under
@@ -2005,8 +2103,48 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             }
         }
         // ---- end of tile
+        if (probe_dead) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's DMAs, unused
+        if (nres && !res_issued) {
+            pe_raw = qht_add(a, lane, nres << 32);
+            res_issued = true;
+        }
         const uint64_t hit = __ballot(found >= 0);
         bool region_changed = true;
+        bool live;
+        int64_t probe_at = 0;  // probe spawned by this tile (start coordinate)
+        const int64_t forced = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;  // max-size cut / the end
+        if (is_probe) {  // post the first candidate of [start, aux] to the owner; no cuts
+            region_changed = hit || last_of_region || probe_dead;
+            live = !region_changed;
+            if (!region_changed) {
+                cur.ct = ct_next;
+            } else if (!probe_dead) {
+                int64_t cand = -1;
+                if (hit) {
+                    const int first = __builtin_ctzll(hit);
+                    cand = static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, first))));
+                }
+                const uint32_t rel = cand >= 0 ? static_cast<uint32_t>(cand - cur.s - cur.off0 + 1) : 0u;
+                const uint64_t ex = pword(cur.epoch, 0, 0);
+                const uint64_t old = probe_cas(a, lane, cur.sid, ex, pword(cur.epoch, 1, rel));
+                if (old == pword(cur.epoch, 2, 0)) {  // the owner handed the region over: finish it
+                    const int64_t next = cand >= 0 ? cand - cur.off0 + 1 : forced;
+                    cur.sid &= ~kProbeBit;
+                    cur.aux = 0;
+                    cur.epoch++;
+                    probe_reset(a, lane, cur.sid, cur.epoch);
+                    emit_cut(a, cur, lane, next);
+                    cur.s = next;
+                    cur.ct = -1;
+                    live = pstream_region(a, cur, lane);
+                    if (!live && lane == 0) {
+                        a.counts[cur.sid] = cur.cnt;
+                        add_agent(a.queue + kQDone, 1u);
+                    }
+                }
+            }
+        } else {
+        bool handed = false;  // the probe finishes this region
         if (hit) {
             const int first = __builtin_ctzll(hit);
             const int64_t f = static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, first))));
@@ -2014,20 +2152,58 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             emit_cut(a, cur, lane, next);
             cur.s = next;
             cur.ct = -1;
+        } else if (lower_end) {  // nothing below the probe: hand over, unless it has posted
+            const uint64_t ex = pword(cur.epoch, 0, 0);
+            const uint64_t old = probe_cas(a, lane, cur.sid, ex, pword(cur.epoch, 2, 0));
+            if (old == ex) {
+                handed = true;
+            } else {  // {epoch, 1, rel}: the probe's first candidate, or none up to the region end
+                const uint32_t rel = static_cast<uint32_t>(old >> 32);
+                const int64_t next = rel ? cur.s + static_cast<int64_t>(rel) : forced;
+                emit_cut(a, cur, lane, next);
+                cur.s = next;
+                cur.ct = -1;
+            }
         } else if (last_of_region) {  // forced cut at max size (splitter_buzhash32.go:60-64) or the end
-            const int64_t next = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;
-            emit_cut(a, cur, lane, next);
-            cur.s = next;
+            emit_cut(a, cur, lane, forced);
+            cur.s = forced;
             cur.ct = -1;
         } else {
             cur.ct = ct_next;
             budget -= kWave * g.L;
             region_changed = false;
+            if (split) probe_at = ct_next + (((hi - ct_next + 1) / 2) & ~(kProbeMinHalf - 1));
         }
-        const bool live = pstream_region(a, cur, lane);
-        if (!live && lane == 0) {
-            a.counts[cur.sid] = cur.cnt;
-            add_agent(a.queue + kQDone, 1u);
+        if (handed) {
+            live = false;
+        } else {
+            if (region_changed && cur.aux != 0) {  // the region that spawned a probe is over: cancel it
+                cur.aux = 0;
+                cur.epoch++;
+                probe_reset(a, lane, cur.sid, cur.epoch);
+            }
+            live = pstream_region(a, cur, lane);
+            if (!live && lane == 0) {
+                a.counts[cur.sid] = cur.cnt;
+                add_agent(a.queue + kQDone, 1u);
+            }
+        }
+        }  // owner
+        if (split) {  // write the probe entry, or a tombstone: the region ended in this tile, or no
+                      // wave was waiting for the entry (the reserve atomic returned head <= e)
+            const uint64_t r_old = qht_value(static_cast<uint32_t>(pe_raw), static_cast<uint32_t>(pe_raw >> 32));
+            const uint32_t e = static_cast<uint32_t>(r_old >> 32) + (reserve ? 1u : 0u);
+            const bool waiter = static_cast<uint32_t>(r_old) > e;
+            PStream pb = cur;
+            pb.sid = cur.sid | kProbeBit;
+            pb.ct = probe_at;
+            pb.aux = hi;
+            const bool spawn = probe_at != 0 && waiter;
+            pwrite(a, lane, e, pb, !spawn);
+            if (spawn) {
+                cur.aux = probe_at;
+                budget = kNoYield;  // not yielded while its probe is out
+            }
         }
         if (!switching && live) {  // same stream, next tile
             issued = next_issued && !region_changed;
@@ -2043,7 +2219,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             const uint64_t ht = qht_take(a, lane, 1ull << 32);
             pwrite(a, lane, static_cast<uint32_t>(ht >> 32), cur, false);
         }
-        if (switching) {  // next stream: its entry landed in the warm slot (the last step's wait drained it)
+        if (switching && !probe_dead) {  // next stream: its entry landed in the warm slot (the last step's wait drained it)
             const u32x4 ev = *reinterpret_cast<const u32x4*>(wl + 16 * (lane & 7));
             if (pentry_ok(ev, lane, tk) && static_cast<uint32_t>(__builtin_amdgcn_readlane(ev.w, 0)) != kTombstone) {
                 pentry_decode(nx, ev);
@@ -2064,7 +2240,8 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         if (nstate >= 2) {
             cur = nx;
             issued = nstate == 3;
-            budget = pipe_quantum(nbacklog);
+            budget = (cur.sid & kProbeBit) ? kNoYield : pipe_quantum(nbacklog);
+            dry = nbacklog < kProbeBacklog;
             if (pstream_region(a, cur, lane)) continue;
             if (lane == 0) {  // nothing left to scan in it
                 a.counts[cur.sid] = cur.cnt;
@@ -2103,10 +2280,15 @@ __global__ void init_ring_kernel(BatchArgs a, uint32_t nslots, uint32_t nwaves) 
                          : g == 3 ? p
                          : g == 4 ? a.lens[e]
                          : g == 5 ? cb
-                                  : (cend > cb ? cend - cb : 0ull);
+                         : g == 6 ? (cend > cb ? cend - cb : 0ull)
+                                  : 0ull;                          // aux 0, epoch 0
         v = pgranule(e + 1u, w, g == 0 ? e : 0u);
     }
     *reinterpret_cast<u32x4*>(reinterpret_cast<uint8_t*>(a.ring) + static_cast<size_t>(e) * kPEntryStride + 16 * g) = v;
+    if (g == 0 && e < a.nstreams) {  // probe result slot of stream e: epoch 0, not done
+        const u32x4 z = {0, 0, 0, 0};
+        *reinterpret_cast<u32x4*>(reinterpret_cast<uint32_t*>(a.states) + 4ull * e) = z;
+    }
 }
 
 // FIXED-*: cuts every chunk length (splitter_fixed.go:15-26); reads no data.

@@ -143,8 +143,14 @@ int main(int argc, char** argv) {
         cfgs = {CFGD(128, 1, 8, 2, 0),   CFGD(128, 2, 8, 2, 0),   CFGD(128, 1, 8, 2, 200), CFGD(128, 2, 8, 2, 200),
                 CFGD(128, 1, 8, 2, 400), CFGD(128, 2, 8, 2, 400), CFGD(64, 3, 8, 0, 200),  CFGD(64, 3, 8, 0, 100),
                 CFGD(128, 2, 6, 2, 200), CFGD(128, 2, 6, 2, 400), CFGD(64, 2, 8, 0, 100),  CFGD(64, 4, 8, 0, 100)};
+    // occupancy: 128-B runs at 8 waves/CU vs 64-B runs at 12 (the LDS the splitter can afford),
+    // emulated hashing ~4 VALU per byte
+    const bool occ = argc > 1 && std::string(argv[1]) == "occ";
+    if (occ)
+        cfgs = {CFGD(128, 1, 8, 2, 250), CFGD(64, 1, 8, 2, 125), CFGD(64, 1, 12, 2, 125), CFGD(64, 1, 16, 2, 125),
+                CFGD(128, 1, 12, 2, 250), CFGD(64, 2, 12, 2, 125), CFGD(128, 1, 8, 2, 300), CFGD(64, 1, 12, 2, 150)};
     for (int rep = 0; rep < (calib ? 1 : 2); rep++) {
-      for (int layout = (depth ? 1 : 0); layout < (calib ? 1 : depth ? 2 : 3); layout++) {
+      for (int layout = (depth || occ ? 1 : 0); layout < (calib ? 1 : depth || occ ? 2 : 3); layout++) {
         for (auto& c : cfgs) {
             const size_t lds = static_cast<size_t>(c.w) * c.s * 64 * c.run;
             if (lds > 160 * 1024) {
