@@ -141,12 +141,32 @@ size_t kcdc_long_workspace_bytes(const char* name, uint64_t len);
 int kcdc_split_long_device(const char* name, const uint8_t* d_data, uint64_t len, uint64_t* d_cuts, uint64_t cuts_cap,
                            uint64_t* d_count, void* workspace, size_t workspace_bytes, void* hip_stream);
 
+/* ------------------------------------------- many streams of any sizes (config 5)
+ * Splits n streams of arbitrary lengths (e.g. the files of one upload,
+ * snapshot/upload/upload.go:769-782) with the same output contract as
+ * kcdc_split_batch_device, routing each stream to the path that finishes it
+ * soonest: streams that one wavefront would still be scanning after the rest
+ * of the batch is done (the largest ones, >= 1 MiB) go through the long-stream
+ * path, the others through one batch launch.  Boundaries are identical either
+ * way.  h_dptrs (device addresses), h_lens and h_cut_base are HOST arrays;
+ * d_cuts and d_counts are device memory.  Asynchronous on `hip_stream`
+ * (stream-ordered allocations for scratch). */
+int kcdc_split_files_device(const char* name, const uint8_t* const* h_dptrs, const uint64_t* h_lens, uint32_t n,
+                            uint64_t* d_cuts, uint64_t cuts_cap, const uint64_t* h_cut_base, uint64_t* d_counts,
+                            void* hip_stream);
+
 /* ------------------------------------------------- synthetic input (bench)
  * Fill `nstreams` device streams of `stream_len` bytes each, laid out at
  * d_data + i*stride, with the counter-PRNG bytes of stream id (first_sid + i)
  * (bytes are a pure function of (seed, sid, offset); BASELINE.json configs 2-5). */
 int kcdc_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint32_t nstreams, uint64_t seed,
                    uint64_t first_sid, void* hip_stream);
+
+/* rand.New(rand.NewSource(seed)).Read(out[:n]) of Go math/rand: the input of
+ * `kopia benchmark splitter` (cli/command_benchmark_splitters.go:66-75, one Rand
+ * read block after block, so consecutive blocks are one continuous read).
+ * Host-only (no GPU needed). */
+int kcdc_gorand_read(int64_t seed, uint8_t* out, uint64_t n);
 
 #ifdef __cplusplus
 }

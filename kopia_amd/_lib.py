@@ -57,6 +57,8 @@ _SIGS = {
     "kcdc_long_workspace_bytes": (C.c_size_t, [C.c_char_p, C.c_uint64]),
     "kcdc_split_long_device": (C.c_int, [C.c_char_p, _P, C.c_uint64, _P, C.c_uint64, _P, _P, C.c_size_t, _P]),
     "kcdc_fill_prng": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, _P]),
+    "kcdc_split_files_device": (C.c_int, [C.c_char_p, _P, _P, C.c_uint32, _P, C.c_uint64, _P, _P, _P]),
+    "kcdc_gorand_read": (C.c_int, [C.c_int64, _P, C.c_uint64]),
 }
 
 

@@ -113,3 +113,47 @@ def read_long(cuts, count) -> np.ndarray:
     if n > cuts.numel():
         raise _lib.KcdcError(_lib.KCDC_EOVERFLOW, f"{n} cuts > capacity {cuts.numel()}")
     return cuts[:n].cpu().numpy()
+
+
+def split_files_device(name: str, ptr_list, len_list, device, stream=None):
+    """Streams of any sizes (config 5): each goes to the batch or the long-stream path,
+    whichever finishes it sooner (kcdc_split_files_device).  Asynchronous on `stream`.
+    Returns (cuts, counts, cut_base, cap) with cuts/counts on the device."""
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream(device)
+    n = len(ptr_list)
+    lens = np.ascontiguousarray(np.asarray(len_list, dtype=np.uint64))
+    caps = np.array([cut_capacity(name, int(L)) for L in lens], dtype=np.uint64)
+    base = np.zeros(max(n, 1), dtype=np.uint64)
+    if n > 1:
+        base[1:n] = np.cumsum(caps)[:-1]
+    cap = int(caps.sum()) if n else 0
+    ptrs = np.ascontiguousarray(np.asarray(ptr_list, dtype=np.uint64))
+    cuts = torch.zeros(max(cap, 1), dtype=torch.int64, device=device)
+    counts = torch.zeros(max(n, 1), dtype=torch.int64, device=device)
+    _lib.check(_lib.lib().kcdc_split_files_device(
+        name.encode(), ptrs.ctypes.data, lens.ctypes.data, n, cuts.data_ptr(), cap, base.ctypes.data,
+        counts.data_ptr(), C.c_void_p(stream.cuda_stream)))
+    return cuts, counts, base[:n].astype(np.int64), cap
+
+
+def read_files(cuts, counts, base, cap) -> list[np.ndarray]:
+    """Cut lists of split_files_device (host); raises on capacity overflow."""
+    c = cuts.cpu().numpy()
+    k = counts.cpu().numpy()[:len(base)]
+    out = []
+    for i in range(len(base)):
+        capi = (base[i + 1] if i + 1 < len(base) else cap) - base[i]
+        if k[i] > capi:
+            raise _lib.KcdcError(_lib.KCDC_EOVERFLOW, f"stream {i}: {k[i]} cuts > capacity {capi}")
+        out.append(c[base[i]:base[i] + k[i]].copy())
+    return out
+
+
+def gorand_read(seed: int, n: int) -> np.ndarray:
+    """Go ``rand.New(rand.NewSource(seed)).Read`` of n bytes (the library's host restatement;
+    input generator of ``kopia benchmark splitter``)."""
+    out = np.empty(max(n, 1), dtype=np.uint8)
+    _lib.check(_lib.lib().kcdc_gorand_read(seed, out.ctypes.data, n))
+    return out[:n]

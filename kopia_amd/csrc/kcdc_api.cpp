@@ -430,6 +430,107 @@ extern "C" int kcdc_split_long_device(const char* name, const uint8_t* d_data, u
     return launch_split_long(*a, d_data, len, d_cuts, cuts_cap, d_count, ws, ws_bytes, dev, stream);
 }
 
+// ================================================================ mixed sizes
+namespace {
+// Single-wave scan rate of the batch kernel and its whole-GPU rate (bytes/s, MI355X, round-1
+// measurements): a stream whose lone-wave time exceeds the batch's aggregate time would be the
+// batch's tail, so it goes to the long (intra-stream parallel) path instead.
+constexpr double kWaveRate = 6e9, kBatchRate = 1.2e13;
+constexpr uint64_t kLongMin = uint64_t(1) << 20;
+}  // namespace
+
+extern "C" int kcdc_split_files_device(const char* name, const uint8_t* const* h_dptrs, const uint64_t* h_lens,
+                                       uint32_t n, uint64_t* d_cuts, uint64_t cuts_cap, const uint64_t* h_cut_base,
+                                       uint64_t* d_counts, void* stream) {
+    const Algo* a = find_algo(name);
+    if (!a) return set_error(KCDC_ENOENT, std::string("unknown splitter: ") + (name ? name : "(null)"));
+    if (n == 0) return KCDC_OK;
+    if (!h_dptrs || !h_lens || !d_cuts || !h_cut_base || !d_counts) return set_error(KCDC_EINVAL, "null argument");
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    int rc = check_device(dev);
+    if (rc) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    for (uint32_t i = 0; i < n; i++)
+        if (h_cut_base[i] > cuts_cap || (i + 1 < n && h_cut_base[i + 1] < h_cut_base[i]))
+            return set_error(KCDC_EINVAL, "cut_base must be non-decreasing and within cuts_cap");
+    // Route: largest streams first to the long path while a lone wave on one would outlast
+    // the rest of the batch (FIXED reads no data: always the batch entry point).
+    std::vector<uint32_t> order(n);
+    for (uint32_t i = 0; i < n; i++) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return h_lens[x] > h_lens[y]; });
+    double rest = 0;
+    for (uint32_t i = 0; i < n; i++) rest += static_cast<double>(h_lens[i]);
+    std::vector<char> is_long(n, 0);
+    if (a->kind != kFixed)
+        for (uint32_t k = 0; k < n; k++) {
+            const uint32_t i = order[k];
+            const double L = static_cast<double>(h_lens[i]);
+            if (h_lens[i] < kLongMin || L / kWaveRate <= (rest - L) / kBatchRate) break;
+            is_long[i] = 1;
+            rest -= L;
+        }
+    std::vector<const uint8_t*> bp;
+    std::vector<uint64_t> bl, bb;
+    std::vector<uint32_t> bidx;
+    size_t ws_max = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (is_long[i]) {
+            ws_max = std::max(ws_max, long_workspace_bytes(*a, h_lens[i]));
+        } else {
+            bidx.push_back(i);
+            bp.push_back(h_dptrs[i]);
+            bl.push_back(h_lens[i]);
+            bb.push_back(h_cut_base[i]);
+        }
+    }
+    if (!bidx.empty()) {  // one batch launch over the small streams, each keeping its cut range
+        // counts[] of the batch go to a scratch array and are scattered to d_counts
+        const uint32_t nb = static_cast<uint32_t>(bidx.size());
+        const size_t meta = nb * (sizeof(void*) + 3 * sizeof(uint64_t));
+        char* m = nullptr;
+        HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&m), meta, st), "hipMallocAsync meta");
+        auto* d_ptrs = reinterpret_cast<const uint8_t**>(m);
+        auto* d_lens = reinterpret_cast<uint64_t*>(m + nb * sizeof(void*));
+        auto* d_base = d_lens + nb;
+        auto* d_cnt = d_base + nb;
+        // The batch kernel takes stream k's capacity as base[k+1]-base[k], which here spans the
+        // ranges of any long streams between them: a stream that overflows its own range (the
+        // caller sized it too small) can spill into theirs, but counts[i] still exceeds the
+        // capacity the caller computed, and the long streams' cuts are written afterwards.
+        HIP_TRY(hipMemcpyAsync(d_ptrs, bp.data(), nb * sizeof(void*), hipMemcpyHostToDevice, st), "H2D meta");
+        HIP_TRY(hipMemcpyAsync(d_lens, bl.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st), "H2D meta");
+        HIP_TRY(hipMemcpyAsync(d_base, bb.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st), "H2D meta");
+        SplitArgs sa{d_ptrs, d_lens, nb, d_cuts, cuts_cap, d_base, d_cnt};
+        rc = launch_split_batch(*a, sa, dev, stream);
+        if (rc) {
+            (void)hipFreeAsync(m, st);
+            return rc;
+        }
+        for (uint32_t k = 0; k < nb; k++)  // runs of consecutive indices copy as one
+            if (k == 0 || bidx[k] != bidx[k - 1] + 1) {
+                uint32_t e = k + 1;
+                while (e < nb && bidx[e] == bidx[e - 1] + 1) e++;
+                HIP_TRY(hipMemcpyAsync(d_counts + bidx[k], d_cnt + k, (e - k) * sizeof(uint64_t),
+                                       hipMemcpyDeviceToDevice, st),
+                        "scatter counts");
+            }
+        HIP_TRY(hipFreeAsync(m, st), "hipFreeAsync meta");
+    }
+    if (ws_max) {
+        void* ws = nullptr;
+        HIP_TRY(hipMallocAsync(&ws, ws_max, st), "hipMallocAsync long workspace");
+        for (uint32_t i = 0; i < n && rc == KCDC_OK; i++) {
+            if (!is_long[i]) continue;
+            const uint64_t cap = (i + 1 < n ? h_cut_base[i + 1] : cuts_cap) - h_cut_base[i];
+            rc = launch_split_long(*a, h_dptrs[i], h_lens[i], d_cuts + h_cut_base[i], cap, d_counts + i, ws, ws_max,
+                                   dev, stream);
+        }
+        (void)hipFreeAsync(ws, st);
+    }
+    return rc;
+}
+
 // =================================================================== data
 extern "C" int kcdc_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint32_t nstreams, uint64_t seed,
                               uint64_t first_sid, void* stream) {
@@ -438,4 +539,10 @@ extern "C" int kcdc_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_
     int rc = check_device(dev);
     if (rc) return rc;
     return launch_fill_prng(d_data, stride, stream_len, nstreams, seed, first_sid, stream);
+}
+
+extern "C" int kcdc_gorand_read(int64_t seed, uint8_t* out, uint64_t n) {
+    if (n && !out) return set_error(KCDC_EINVAL, "null buffer");
+    gorand_read(seed, out, n);
+    return KCDC_OK;
 }

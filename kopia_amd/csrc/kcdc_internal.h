@@ -15,7 +15,10 @@ struct Tables {
     int rk_shift = 0;       // deg(P) - 8
     uint64_t rk_out[256];   // b * x^(8*63) mod P
     uint64_t rk_mod[256];   // (b * x^deg mod P) | (b << deg)
+    uint64_t cooked[607];   // Go math/rand rngCooked (rng.go)
 };
+// rand.New(rand.NewSource(seed)).Read(p[:n]) (Go math/rand, 7 bytes per Int63).
+void gorand_read(int64_t seed, uint8_t* p, uint64_t n);
 const Tables& tables();
 
 enum Kind : int32_t { kFixed = 0, kBuzhash = 1, kRabinKarp = 2 };

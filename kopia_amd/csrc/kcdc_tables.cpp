@@ -112,8 +112,8 @@ struct GoRand {
         return x;
     }
     int64_t int63() { return static_cast<int64_t>(uint64() & 0x7FFFFFFFFFFFFFFFull); }
-    void read(uint8_t* p, int n) {  // rand.go read(): 7 bytes per Int63
-        for (int i = 0; i < n; i++) {
+    void read(uint8_t* p, uint64_t n) {  // rand.go read(): 7 bytes per Int63
+        for (uint64_t i = 0; i < n; i++) {
             if (pos == 0) { val = int63(); pos = 7; }
             p[i] = static_cast<uint8_t>(val);
             val >>= 8;
@@ -161,6 +161,7 @@ std::once_flag g_once;
 void build_tables() {
     std::vector<uint64_t> cooked(kLen);
     compute_rng_cooked(cooked.data());
+    std::memcpy(g_tables.cooked, cooked.data(), sizeof(g_tables.cooked));
     {  // buzhash32: GenerateHashes(1)
         GoRand r(1, cooked.data());
         std::set<uint32_t> used;
@@ -203,6 +204,11 @@ void build_tables() {
 const Tables& tables() {
     std::call_once(g_once, build_tables);
     return g_tables;
+}
+
+void gorand_read(int64_t seed, uint8_t* p, uint64_t n) {
+    GoRand r(seed, tables().cooked);
+    r.read(p, n);
 }
 
 }  // namespace kcdc
