@@ -124,9 +124,11 @@ int kcdc_split_batch_device(const char* name, const uint8_t* const* d_ptrs, cons
                             uint32_t nstreams, uint64_t* d_cuts, uint64_t cuts_cap, const uint64_t* d_cut_base,
                             uint64_t* d_counts, void* hip_stream);
 
-/* _host: host buffers in, host cut lists out (H2D + kernel + D2H through pinned
- * staging, overlapped).  Synchronous.  This is the path the Go cgo shim calls
- * (INTEGRATION.md). */
+/* _host: host buffers in, host cut lists out.  Streams are copied H2D in groups
+ * of <= 1 GiB (the HIP runtime stages pageable memory; buffers the caller
+ * allocated pinned are DMA'd directly), split by one launch per group, and the
+ * cut lists copied back.  Synchronous, PCIe-bound.  This is the
+ * path the Go cgo shim calls. */
 int kcdc_split_batch_host(const char* name, const uint8_t* const* h_ptrs, const uint64_t* lens, uint32_t nstreams,
                           uint64_t* cuts, uint64_t cuts_cap, const uint64_t* cut_base, uint64_t* counts, int device);
 

@@ -470,13 +470,17 @@ extern "C" int kcdc_split_files_device(const char* name, const uint8_t* const* h
             is_long[i] = 1;
             rest -= L;
         }
-    std::vector<const uint8_t*> bp;
-    std::vector<uint64_t> bl, bb;
+    std::vector<const uint8_t*> bp, lp;
+    std::vector<uint64_t> bl, bb, ll, lcap;
+    std::vector<uint64_t*> lcuts, lcnt;
     std::vector<uint32_t> bidx;
-    size_t ws_max = 0;
     for (uint32_t i = 0; i < n; i++) {
         if (is_long[i]) {
-            ws_max = std::max(ws_max, long_workspace_bytes(*a, h_lens[i]));
+            lp.push_back(h_dptrs[i]);
+            ll.push_back(h_lens[i]);
+            lcap.push_back((i + 1 < n ? h_cut_base[i + 1] : cuts_cap) - h_cut_base[i]);
+            lcuts.push_back(d_cuts + h_cut_base[i]);
+            lcnt.push_back(d_counts + i);
         } else {
             bidx.push_back(i);
             bp.push_back(h_dptrs[i]);
@@ -517,15 +521,13 @@ extern "C" int kcdc_split_files_device(const char* name, const uint8_t* const* h
             }
         HIP_TRY(hipFreeAsync(m, st), "hipFreeAsync meta");
     }
-    if (ws_max) {
+    if (!lp.empty()) {  // every long stream in one long-path launch
+        const uint32_t m = static_cast<uint32_t>(lp.size());
+        const size_t wsb = long_workspace_bytes_multi(*a, ll.data(), m);
         void* ws = nullptr;
-        HIP_TRY(hipMallocAsync(&ws, ws_max, st), "hipMallocAsync long workspace");
-        for (uint32_t i = 0; i < n && rc == KCDC_OK; i++) {
-            if (!is_long[i]) continue;
-            const uint64_t cap = (i + 1 < n ? h_cut_base[i + 1] : cuts_cap) - h_cut_base[i];
-            rc = launch_split_long(*a, h_dptrs[i], h_lens[i], d_cuts + h_cut_base[i], cap, d_counts + i, ws, ws_max,
-                                   dev, stream);
-        }
+        HIP_TRY(hipMallocAsync(&ws, wsb, st), "hipMallocAsync long workspace");
+        rc = launch_split_long_multi(*a, m, lp.data(), ll.data(), lcuts.data(), lcap.data(), lcnt.data(), ws, wsb,
+                                     dev, stream);
         (void)hipFreeAsync(ws, st);
     }
     return rc;

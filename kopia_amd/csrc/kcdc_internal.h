@@ -65,6 +65,12 @@ int launch_scan_first(const Algo& algo, const uint8_t* d_buf, uint64_t len, int6
 int launch_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint32_t nstreams, uint64_t seed,
                      uint64_t first_sid, void* stream);
 size_t long_workspace_bytes(const Algo& algo, uint64_t len);
+// Several long streams in one launch (segments of all streams scanned together, one
+// resolving wave per stream).
+size_t long_workspace_bytes_multi(const Algo& algo, const uint64_t* lens, uint32_t m);
+int launch_split_long_multi(const Algo& algo, uint32_t m, const uint8_t* const* d_data, const uint64_t* lens,
+                            uint64_t* const* d_cuts, const uint64_t* caps, uint64_t* const* d_counts, void* ws,
+                            size_t ws_bytes, int device, void* stream);
 int launch_split_long(const Algo& algo, const uint8_t* d_data, uint64_t len, uint64_t* d_cuts, uint64_t cuts_cap,
                       uint64_t* d_count, void* ws, size_t ws_bytes, int device, void* stream);
 

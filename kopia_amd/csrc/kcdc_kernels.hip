@@ -2357,20 +2357,40 @@ constexpr int64_t kSegBytes = kWave * kLaneMax;  // 128 KiB
 constexpr int kSegK = 4;
 constexpr uint64_t kTruncBit = 1ull << 63;
 
-struct LongArgs {
+// One stream of a long-path launch (several streams share one launch: their segments are
+// numbered consecutively, stream j owning global segments [seg0, seg0 + its segment count)).
+struct LongStream {
     const uint8_t* abase;
     int64_t off0;
     int64_t n;
-    int64_t nseg;
-    uint32_t* seg_cnt;   // stored count | (truncated << 31)
-    uint64_t* seg_cand;  // [nseg][kSegK] absolute positions
-    uint64_t* seg_off;   // exclusive prefix of stored counts
-    uint64_t* list;      // compacted candidates (kTruncBit marks the last stored of a truncated segment)
-    uint64_t* total;     // [1] number of list entries
+    int64_t seg0;
     uint64_t* cuts;
     uint64_t cuts_cap;
     uint64_t* count;
+    uint64_t pad;
 };
+struct LongArgs {
+    const LongStream* streams;
+    uint32_t nstreams;
+    int64_t nseg;        // all streams
+    uint32_t* seg_cnt;   // stored count | (truncated << 31)
+    uint64_t* seg_cand;  // [nseg][kSegK] positions (relative to the segment's stream)
+    uint64_t* seg_off;   // exclusive prefix of stored counts
+    uint64_t* list;      // compacted candidates (kTruncBit marks the last stored of a truncated segment)
+    uint64_t* total;     // [1] number of list entries
+};
+
+// The stream owning global segment `seg`: the last j with seg0 <= seg (wave-uniform).
+__device__ __forceinline__ uint32_t long_stream_of(const LongArgs& g, int64_t seg) {
+    uint32_t lo = 0, hi = g.nstreams - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        const int64_t s0 = static_cast<int64_t>(uni64(static_cast<uint64_t>(g.streams[mid].seg0)));
+        if (s0 <= seg) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
 
 template <int KIND>
 __global__ __launch_bounds__(kScanWaves * kWave, 2) void cand_scan_kernel(BatchArgs a, LongArgs g) {
@@ -2381,12 +2401,17 @@ __global__ __launch_bounds__(kScanWaves * kWave, 2) void cand_scan_kernel(BatchA
     const int64_t seg = static_cast<int64_t>(blockIdx.x) * kScanWaves + wave;
     if (seg >= g.nseg) return;
     auto hash = make_hash<KIND>(sm, a, lane);
+    const LongStream& S = g.streams[long_stream_of(g, seg)];
+    const int64_t off0 = static_cast<int64_t>(uni64(static_cast<uint64_t>(S.off0)));
+    const int64_t n = static_cast<int64_t>(uni64(static_cast<uint64_t>(S.n)));
+    const uint8_t* abase = reinterpret_cast<const uint8_t*>(uni64(reinterpret_cast<uint64_t>(S.abase)));
+    const int64_t seg0 = static_cast<int64_t>(uni64(static_cast<uint64_t>(S.seg0)));
     // Segments tile COORDINATES (position + off0) so every lane sub-range is 16-byte aligned.
-    const int64_t cs = seg * kSegBytes;
-    const int64_t lo = cs > g.off0 ? cs : g.off0;                                             // first tested
-    const int64_t hi = (cs + kSegBytes < g.off0 + g.n ? cs + kSegBytes : g.off0 + g.n) - 1;  // inclusive
+    const int64_t cs = (seg - seg0) * kSegBytes;
+    const int64_t lo = cs > off0 ? cs : off0;                                           // first tested
+    const int64_t hi = (cs + kSegBytes < off0 + n ? cs + kSegBytes : off0 + n) - 1;  // inclusive
     const int64_t tb = cs >= 64 ? cs - 64 : 0;
-    const Loader ld = make_loader(g.abase, g.off0, g.off0 + g.n, tb);
+    const Loader ld = make_loader(abase, off0, off0 + n, tb);
     const int64_t c0 = cs + lane * kLaneMax;
     uint32_t found[kSegK];
     int nf = 0;  // candidates found by this lane (kSegK + 1 means "more than kSegK")
@@ -2431,7 +2456,7 @@ __global__ __launch_bounds__(kScanWaves * kWave, 2) void cand_scan_kernel(BatchA
     const int tot = __shfl(incl, kWave - 1);
     const int pre = incl - nf;
     for (int j = 0; j < nf && j < kSegK; j++)
-        if (pre + j < kSegK) g.seg_cand[seg * kSegK + pre + j] = static_cast<uint64_t>(cs - g.off0) + found[j];
+        if (pre + j < kSegK) g.seg_cand[seg * kSegK + pre + j] = static_cast<uint64_t>(cs - off0) + found[j];
     if (lane == 0)
         g.seg_cnt[seg] = (tot > kSegK ? 0x80000000u : 0u) | static_cast<uint32_t>(tot < kSegK ? tot : kSegK);
 }
@@ -2493,6 +2518,7 @@ __global__ void compact_kernel(LongArgs g) {
 
 constexpr int kResolveWin = 4096;  // candidate-list entries staged in LDS
 
+// One wave per stream (blockIdx.x): walks the chunk rule over the stream's candidate list.
 template <int KIND>
 __global__ __launch_bounds__(kWave) void resolve_kernel(BatchArgs a, LongArgs g, int64_t mn, int64_t mx) {
     __shared__ HashSmem<KIND> sm;
@@ -2500,12 +2526,25 @@ __global__ __launch_bounds__(kWave) void resolve_kernel(BatchArgs a, LongArgs g,
     fill_tables<KIND>(sm, a);
     const int lane = threadIdx.x;
     const auto hash = make_hash<KIND>(sm, a, lane);
-    const int64_t total = static_cast<int64_t>(uni64(g.total[0]));
-    const int64_t n = g.n;
+    const LongStream& S = g.streams[blockIdx.x];
+    const int64_t n = static_cast<int64_t>(uni64(static_cast<uint64_t>(S.n)));
+    const int64_t off0 = static_cast<int64_t>(uni64(static_cast<uint64_t>(S.off0)));
+    const uint8_t* abase = reinterpret_cast<const uint8_t*>(uni64(reinterpret_cast<uint64_t>(S.abase)));
+    const int64_t seg0 = static_cast<int64_t>(uni64(static_cast<uint64_t>(S.seg0)));
+    const uint64_t cuts_cap = uni64(S.cuts_cap);
+    uint64_t* const cuts = reinterpret_cast<uint64_t*>(uni64(reinterpret_cast<uint64_t>(S.cuts)));
+    // this stream's slice of the compacted list
+    const int64_t lbeg = seg0 < g.nseg ? static_cast<int64_t>(uni64(g.seg_off[seg0])) : 0;
+    const int64_t lend = blockIdx.x + 1 < g.nstreams && uni64(static_cast<uint64_t>(g.streams[blockIdx.x + 1].seg0)) <
+                                                            static_cast<uint64_t>(g.nseg)
+                             ? static_cast<int64_t>(uni64(g.seg_off[g.streams[blockIdx.x + 1].seg0]))
+                             : static_cast<int64_t>(uni64(g.total[0]));
+    const uint64_t* const list = g.list + lbeg;
+    const int64_t total = n > 0 ? lend - lbeg : 0;
     int64_t wbase = 0;  // list index of win[0]
     auto load_win = [&](int64_t at) {
         __syncthreads();
-        for (int j = lane; j < kResolveWin; j += kWave) win[j] = at + j < total ? g.list[at + j] : ~0ull >> 1;
+        for (int j = lane; j < kResolveWin; j += kWave) win[j] = at + j < total ? list[at + j] : ~0ull >> 1;
         __syncthreads();
         wbase = at;
     };
@@ -2543,12 +2582,11 @@ __global__ __launch_bounds__(kWave) void resolve_kernel(BatchArgs a, LongArgs g,
                 if (e & kTruncBit) {  // its segment may hold unlisted candidates >= lo
                     // end (exclusive, in positions) of the coordinate segment holding entry e
                     const int64_t seg_end =
-                        ((static_cast<int64_t>(e & ~kTruncBit) + g.off0) / kSegBytes + 1) * kSegBytes - g.off0;
+                        ((static_cast<int64_t>(e & ~kTruncBit) + off0) / kSegBytes + 1) * kSegBytes - off0;
                     if (seg_end > lo) {
                         const int64_t rh = seg_end - 1 < hi ? seg_end - 1 : hi;
-                        const int64_t f =
-                            scan_region(hash, g.abase, g.off0, g.off0 + n, lo + g.off0, rh + g.off0, lane);
-                        if (f >= 0) c = f - g.off0;
+                        const int64_t f = scan_region(hash, abase, off0, off0 + n, lo + off0, rh + off0, lane);
+                        if (f >= 0) c = f - off0;
                     }
                 }
             }
@@ -2563,11 +2601,11 @@ __global__ __launch_bounds__(kWave) void resolve_kernel(BatchArgs a, LongArgs g,
             else
                 next = n;
         }
-        if (lane == 0 && cnt < g.cuts_cap) g.cuts[cnt] = static_cast<uint64_t>(next);
+        if (lane == 0 && cnt < cuts_cap) cuts[cnt] = static_cast<uint64_t>(next);
         cnt++;
         s = next;
     }
-    if (lane == 0) g.count[0] = cnt;
+    if (lane == 0) S.count[0] = cnt;
 }
 
 }  // namespace dev
@@ -2840,14 +2878,19 @@ int launch_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint
 namespace {
 struct LongLayout {
     int64_t nseg;
-    size_t off_cnt, off_cand, off_off, off_list, off_total, bytes;
+    size_t off_streams, off_cnt, off_cand, off_off, off_list, off_total, bytes;
 };
-LongLayout long_layout(uint64_t len) {
+int64_t long_nseg(uint64_t len, uint64_t off0) {  // segments tile coordinates (position + off0)
+    return len ? static_cast<int64_t>((len + off0 + dev::kSegBytes - 1) / dev::kSegBytes) : 0;
+}
+LongLayout long_layout(int64_t nseg, uint32_t nstreams) {
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
     LongLayout L{};
-    L.nseg = static_cast<int64_t>((len + 15 + dev::kSegBytes - 1) / dev::kSegBytes);  // coordinates: + off0 < 16
-    const size_t ns = static_cast<size_t>(L.nseg);
+    L.nseg = nseg;
+    const size_t ns = static_cast<size_t>(nseg);
     size_t o = 0;
+    L.off_streams = o;
+    o += al(nstreams * sizeof(dev::LongStream));
     L.off_cnt = o;
     o += al(ns * 4);
     L.off_cand = o;
@@ -2865,54 +2908,78 @@ LongLayout long_layout(uint64_t len) {
 
 size_t long_workspace_bytes(const Algo& algo, uint64_t len) {
     if (algo.kind == kFixed) return 0;
-    return long_layout(len).bytes;
+    return long_layout(long_nseg(len, 15), 1).bytes;  // any alignment: off0 < 16
 }
 
-int launch_split_long(const Algo& algo, const uint8_t* d_data, uint64_t len, uint64_t* d_cuts, uint64_t cuts_cap,
-                      uint64_t* d_count, void* ws, size_t ws_bytes, int device, void* stream) {
+size_t long_workspace_bytes_multi(const Algo& algo, const uint64_t* lens, uint32_t m) {
+    if (algo.kind == kFixed) return 0;
+    int64_t nseg = 0;
+    for (uint32_t j = 0; j < m; j++) nseg += long_nseg(lens[j], 15);
+    return long_layout(nseg, m).bytes;
+}
+
+int launch_split_long_multi(const Algo& algo, uint32_t m, const uint8_t* const* d_data, const uint64_t* lens,
+                            uint64_t* const* d_cuts, const uint64_t* caps, uint64_t* const* d_counts, void* ws,
+                            size_t ws_bytes, int device, void* stream) {
     int err = 0;
     const DeviceTables* t = device_tables(device, &err);
     if (!t) return err;
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (algo.kind == kFixed)  // reads no data; the batch entry point covers it
-        return set_error(-22, "kcdc_split_long_device: use kcdc_split_batch_device for FIXED splitters");
-    const LongLayout L = long_layout(len);
-    if (len == 0) {
-        const hipError_t e = hipMemsetAsync(d_count, 0, sizeof(uint64_t), st);
-        return e == hipSuccess ? 0 : hip_fail(e, "memset");
+        return set_error(-22, "long-stream path: use kcdc_split_batch_device for FIXED splitters");
+    if (m == 0) return 0;
+    std::vector<dev::LongStream> hs(m);
+    int64_t nseg = 0;
+    for (uint32_t j = 0; j < m; j++) {
+        const uint64_t p = reinterpret_cast<uint64_t>(d_data[j]);
+        dev::LongStream& S = hs[j];
+        S.off0 = static_cast<int64_t>(p & 15u);
+        S.abase = reinterpret_cast<const uint8_t*>(p - static_cast<uint64_t>(S.off0));
+        S.n = static_cast<int64_t>(lens[j]);
+        S.seg0 = nseg;
+        S.cuts = d_cuts[j];
+        S.cuts_cap = caps[j];
+        S.count = d_counts[j];
+        nseg += long_nseg(lens[j], static_cast<uint64_t>(S.off0));
     }
-    if (!ws || ws_bytes < L.bytes) return set_error(-22, "kcdc_split_long_device: workspace too small");
+    const LongLayout L = long_layout(nseg, m);
+    if (!ws || ws_bytes < L.bytes) return set_error(-22, "long-stream path: workspace too small");
     char* w = static_cast<char*>(ws);
     dev::LongArgs g{};
-    const uint64_t p = reinterpret_cast<uint64_t>(d_data);
-    g.off0 = static_cast<int64_t>(p & 15u);
-    g.abase = reinterpret_cast<const uint8_t*>(p - static_cast<uint64_t>(g.off0));
-    g.n = static_cast<int64_t>(len);
-    g.nseg = (g.off0 + g.n + dev::kSegBytes - 1) / dev::kSegBytes;  // <= L.nseg
+    g.streams = reinterpret_cast<const dev::LongStream*>(w + L.off_streams);
+    g.nstreams = m;
+    g.nseg = nseg;
     g.seg_cnt = reinterpret_cast<uint32_t*>(w + L.off_cnt);
     g.seg_cand = reinterpret_cast<uint64_t*>(w + L.off_cand);
     g.seg_off = reinterpret_cast<uint64_t*>(w + L.off_off);
     g.list = reinterpret_cast<uint64_t*>(w + L.off_list);
     g.total = reinterpret_cast<uint64_t*>(w + L.off_total);
-    g.cuts = d_cuts;
-    g.cuts_cap = cuts_cap;
-    g.count = d_count;
+    hipError_t e = hipMemcpyAsync(w + L.off_streams, hs.data(), m * sizeof(dev::LongStream), hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return hip_fail(e, "long-stream descriptors");
     dev::BatchArgs a = base_args(algo, *t);
-    const dim3 grid(static_cast<unsigned>((g.nseg + dev::kScanWaves - 1) / dev::kScanWaves));
-    const dim3 block(dev::kScanWaves * dev::kWave);
     const int64_t mn = static_cast<int64_t>(algo.min_size()), mx = static_cast<int64_t>(algo.max_size());
+    if (nseg > 0) {
+        const dim3 grid(static_cast<unsigned>((nseg + dev::kScanWaves - 1) / dev::kScanWaves));
+        const dim3 block(dev::kScanWaves * dev::kWave);
+        if (algo.kind == kBuzhash)
+            hipLaunchKernelGGL(dev::cand_scan_kernel<kBuzhash>, grid, block, 0, st, a, g);
+        else
+            hipLaunchKernelGGL(dev::cand_scan_kernel<kRabinKarp>, grid, block, 0, st, a, g);
+        hipLaunchKernelGGL(dev::seg_prefix_kernel, dim3(1), dim3(1024), 0, st, g);
+        hipLaunchKernelGGL(dev::compact_kernel, dim3(static_cast<unsigned>((nseg + 255) / 256)), dim3(256), 0, st, g);
+    }
     if (algo.kind == kBuzhash)
-        hipLaunchKernelGGL(dev::cand_scan_kernel<kBuzhash>, grid, block, 0, st, a, g);
+        hipLaunchKernelGGL(dev::resolve_kernel<kBuzhash>, dim3(m), dim3(dev::kWave), 0, st, a, g, mn, mx);
     else
-        hipLaunchKernelGGL(dev::cand_scan_kernel<kRabinKarp>, grid, block, 0, st, a, g);
-    hipLaunchKernelGGL(dev::seg_prefix_kernel, dim3(1), dim3(1024), 0, st, g);
-    hipLaunchKernelGGL(dev::compact_kernel, dim3(static_cast<unsigned>((g.nseg + 255) / 256)), dim3(256), 0, st, g);
-    if (algo.kind == kBuzhash)
-        hipLaunchKernelGGL(dev::resolve_kernel<kBuzhash>, dim3(1), dim3(dev::kWave), 0, st, a, g, mn, mx);
-    else
-        hipLaunchKernelGGL(dev::resolve_kernel<kRabinKarp>, dim3(1), dim3(dev::kWave), 0, st, a, g, mn, mx);
-    const hipError_t e = hipGetLastError();
+        hipLaunchKernelGGL(dev::resolve_kernel<kRabinKarp>, dim3(m), dim3(dev::kWave), 0, st, a, g, mn, mx);
+    e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "long-stream kernel launch");
+}
+
+int launch_split_long(const Algo& algo, const uint8_t* d_data, uint64_t len, uint64_t* d_cuts, uint64_t cuts_cap,
+                      uint64_t* d_count, void* ws, size_t ws_bytes, int device, void* stream) {
+    return launch_split_long_multi(algo, 1, &d_data, &len, &d_cuts, &cuts_cap, &d_count, ws, ws_bytes, device,
+                                   stream);
 }
 
 }  // namespace kcdc
