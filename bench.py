@@ -105,15 +105,19 @@ def main():
     ap.add_argument("--stream-mib", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-inclusive", action="store_true")
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4],
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
                     help="BASELINE.json config: 2 = 4096 x 4 MiB/GPU (default), 3 = one 64 GiB stream "
-                         "(exact tiled CDC), 4 = 8192 x 8 MiB/GPU")
+                         "(exact tiled CDC), 4 = 8192 x 8 MiB/GPU, 5 = Zipf-sized files, LPT over ranks")
     ap.add_argument("--long-gib", type=int, default=64, help="config 3 stream size")
+    ap.add_argument("--files-gib", type=int, default=32, help="config 5 bytes per GPU (256 GiB over 8 GPUs)")
+    ap.add_argument("--all-names", action="store_true", help="config 5: also time every registered name")
     args = ap.parse_args()
     if args.config == 4:
         args.streams, args.stream_mib = 8192, 8
     if args.config == 3:
         return bench_long(args)
+    if args.config == 5:
+        return bench_files(args)
 
     rank, world, local = kd.env_rank_world()
     torch.cuda.set_device(local)
@@ -248,6 +252,82 @@ def bench_long(args):
            "kernel_ms_events": round(ms, 3), "cuts": int(got.size),
            "identical_to_sequential_path": bool(np.array_equal(got, seq))}
     print(json.dumps(out), flush=True)
+
+
+def bench_files(args):
+    """Config 5: file sizes from a Zipf law over 19 classes 4 KiB..1 GiB
+    (s = 1.1, fixed seed), files_gib x world bytes in total, LPT-balanced over the ranks;
+    every rank splits its files with kcdc_split_files_device (each file through the batch
+    or the long path).  Weak scaling, no data-path collective.  FIXED names read no data."""
+    rank, world, local = kd.env_rank_world()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    sizes = kd.zipf_sizes(args.files_gib * world << 30)
+    mine = sorted(kd.lpt_plan(sizes, world)[rank], key=lambda i: int(sizes[i]))
+    lens = [int(sizes[i]) for i in mine]
+    total = sum(lens)
+    data = torch.empty(total, dtype=torch.uint8, device=dev)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64) if lens else np.zeros(0, np.int64)
+    # runs of equal sizes are contiguous (sorted): one fill per run, file ids = global indices
+    k = 0
+    while k < len(lens):
+        e = k
+        while e < len(lens) and lens[e] == lens[k] and mine[e] == mine[k] + (e - k):
+            e += 1
+        batch.fill_prng(data[int(offs[k]):], lens[k], e - k, lens[k], SEED, first_sid=int(mine[k]))
+        k = e
+    ptrs = [data.data_ptr() + int(o) for o in offs]
+    stream = torch.cuda.current_stream(dev)
+
+    def run(name, steps, warmup):
+        for _ in range(warmup):
+            batch.split_files_device(name, ptrs, lens, dev, stream)
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        t0 = time.perf_counter()
+        res = None
+        for _ in range(steps):
+            res = batch.split_files_device(name, ptrs, lens, dev, stream)
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        return kd.max_over_ranks(time.perf_counter() - t0, dev), res
+
+    name = args.splitter
+    steps = max(1, min(args.steps, 10))
+    elapsed, res = run(name, steps, max(1, min(args.warmup, 2)))
+    out = {"metric": METRIC, "value": round(total * world * steps / GiB / elapsed, 3), "unit": "GiB/s",
+           "n_gpus": world, "steps": steps, "warmup": max(1, min(args.warmup, 2)),
+           "ms_per_step": round(elapsed / steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+           "config": {"workload": f"config5: Zipf(s=1.1) file sizes over 4 KiB..1 GiB, {args.files_gib} GiB per GPU, "
+                                  f"LPT over {world} rank(s), {name}",
+                      "splitter": name, "files_this_rank": len(lens), "bytes_this_rank": total,
+                      "largest_file": max(lens) if lens else 0,
+                      "parallelism": f"LPT file sharding x{world}, no data-path collectives"}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # parity on a sample: the 64 smallest and the 2 largest files vs the oracle
+        from oracle import coracle  # oracle import confined to the checking leg
+        got = batch.read_files(*res)
+        pick = list(range(min(64, len(lens)))) + list(range(max(64, len(lens) - 2), len(lens)))
+        host = [data[int(offs[i]):int(offs[i]) + lens[i]].cpu().numpy() for i in pick]
+        want = coracle.split_batch(name, host, nthreads=min(16, os.cpu_count() or 1))
+        out["sample_parity_mismatches"] = sum(1 for j, i in enumerate(pick) if not np.array_equal(got[i], want[j]))
+        out["sample"] = f"{len(pick)} files (64 smallest, 2 largest) vs oracle/cdc_oracle.c"
+    if args.all_names:
+        out["per_name_gib_s"] = {}
+        for nm in ks.SupportedAlgorithms():
+            el, _ = run(nm, 2, 1)
+            out["per_name_gib_s"][nm] = round(total * world * 2 / GiB / el, 2)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
