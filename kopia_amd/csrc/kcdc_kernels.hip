@@ -2354,6 +2354,9 @@ __global__ void fill_prng_kernel(uint8_t* data, uint64_t stride, uint64_t len, u
 // candidate it needs, it rescans that range with the same scan_region() the
 // batch kernel uses.  The cut set is therefore exactly the sequential one.
 constexpr int64_t kSegBytes = kWave * kLaneMax;  // 128 KiB
+#ifndef KCDC_LONG_DMA
+#define KCDC_LONG_DMA 1  // buzhash candidate scan: cand_scan_dma_kernel (0: cand_scan_kernel)
+#endif
 constexpr int kSegK = 4;
 constexpr uint64_t kTruncBit = 1ull << 63;
 
@@ -2459,6 +2462,124 @@ __global__ __launch_bounds__(kScanWaves * kWave, 2) void cand_scan_kernel(BatchA
         if (pre + j < kSegK) g.seg_cand[seg * kSegK + pre + j] = static_cast<uint64_t>(cs - off0) + found[j];
     if (lane == 0)
         g.seg_cnt[seg] = (tot > kSegK ? 0x80000000u : 0u) | static_cast<uint32_t>(tot < kSegK ? tot : kSegK);
+}
+
+// Buzhash candidate scan of the long path on the batch kernel's feeding scheme: a segment
+// (128 KiB of coordinates) is exactly one tile of 64 lane segments, streamed by LDS-DMA in
+// 128-byte steps with the next segment's warm piece and first step prefetched during the
+// last step; persistent grid (one workgroup of kDmaWaves waves per CU), grid-stride over
+// the segments of every stream of the launch.  Records what cand_scan_kernel records.
+template <bool TOP>
+__global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void cand_scan_dma_kernel(BatchArgs a, LongArgs g) {
+    __shared__ BuzShared smtab;
+    __shared__ DmaSlots smslots;
+    __shared__ WarmSlots smwarm;
+    for (uint32_t i = threadIdx.x; i < 256u * 64u; i += blockDim.x) smtab.tab[i] = rotl_n(a.buz[i >> 6], a.buz_rot);
+    __syncthreads();
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    BuzRing hash;
+    hash.tab = reinterpret_cast<const char*>(smtab.tab);
+    hash.lane4 = static_cast<uint32_t>(lane) * 4u;
+    hash.mask = a.mask;
+    hash.h = 0;
+    uint8_t* sl = smslots.b[wave][0];
+    uint8_t* wl = smwarm.b[wave];
+    const uint32_t sl32 = lds_addr(sl), wl32 = lds_addr(wl);
+    const uint32_t lim = TOP ? a.buz_lim : 0u;
+    const int64_t nw = static_cast<int64_t>(gridDim.x) * kDmaWaves;
+    struct Seg {
+        const uint8_t* abase;
+        int64_t off0, n, cs, lo, hi;
+    };
+    auto seg_of = [&](int64_t seg) {
+        const LongStream& S = g.streams[long_stream_of(g, seg)];
+        Seg q;
+        q.off0 = static_cast<int64_t>(uni64(static_cast<uint64_t>(S.off0)));
+        q.n = static_cast<int64_t>(uni64(static_cast<uint64_t>(S.n)));
+        q.abase = reinterpret_cast<const uint8_t*>(uni64(reinterpret_cast<uint64_t>(S.abase)));
+        q.cs = (seg - static_cast<int64_t>(uni64(static_cast<uint64_t>(S.seg0)))) * kSegBytes;
+        q.lo = q.cs > q.off0 ? q.cs : q.off0;
+        q.hi = (q.cs + kSegBytes < q.off0 + q.n ? q.cs + kSegBytes : q.off0 + q.n) - 1;
+        return q;
+    };
+    auto issue = [&](const Seg& q) {
+        const TileGeom t = tile_geom(q.cs, q.hi, q.abase, q.off0, q.off0 + q.n);
+        dma_piece(t.ld, t.ld.tb, wl32, q.cs, t.L, -1, lane);
+        dma_step128(t.ld, t.ld.tb, sl32, q.cs, t.L, 0, lane);
+    };
+    int64_t seg = static_cast<int64_t>(blockIdx.x) * kDmaWaves + wave;
+    if (seg >= g.nseg) return;
+    Seg q = seg_of(seg);
+    issue(q);
+    for (;;) {
+        const int64_t nseg_next = seg + nw;
+        const bool has_next = nseg_next < g.nseg;
+        Seg qn = q;
+        if (has_next) qn = seg_of(nseg_next);
+        const TileGeom t = tile_geom(q.cs, q.hi, q.abase, q.off0, q.off0 + q.n);
+        const int64_t c0 = q.cs + lane * t.L;
+        {
+            uint32_t w16[16];
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            read_piece(wl, lane, c0 - 64, q.off0, w16);
+            hash.clear();
+            hash.template block<kWarm>(w16);
+        }
+        uint32_t found[kSegK];
+        int nf = 0;  // candidates of this lane (kSegK + 1: more than kSegK)
+        for (int nb = 0; nb < t.nb; nb++) {
+            const int64_t c = c0 + 128 * nb;
+            const typename BuzRing::State st0 = hash.save();
+            uint32_t dw[32];
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            read_step128(sl, lane, c, q.off0, dw);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot free: refill it
+            __builtin_amdgcn_sched_barrier(0);
+            if (nb + 1 < t.nb)
+                dma_step128(t.ld, t.ld.tb, sl32, q.cs, t.L, nb + 1, lane);
+            else if (has_next)
+                issue(qn);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t m = hash.template step128<TOP>(dw, 0u);
+            __builtin_amdgcn_sched_barrier(0);
+            if (m <= lim && c <= q.hi && nf <= kSegK) {  // rare: exact re-run from global memory
+                uint32_t prv[16], cur32[32];
+                t.ld.load(c - 64, prv);
+                t.ld.load(c, cur32);
+                const int64_t blo = q.lo - c, bhi = q.hi - c;
+                int from = blo < 0 ? 0 : static_cast<int>(blo);
+                const int to = bhi > 127 ? 127 : static_cast<int>(bhi);
+                while (from <= to && nf <= kSegK) {
+                    const uint32_t idx = hash.exact(st0, prv, cur32, from, to);
+                    if (idx >= 128u) break;
+                    if (nf < kSegK) found[nf] = static_cast<uint32_t>(c - q.cs) + idx;
+                    nf++;
+                    from = static_cast<int>(idx) + 1;
+                }
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), visible to the waitcnt pass
+            }
+        }
+        // exclusive prefix of per-lane counts (lane segments are in position order)
+        int incl = nf;
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const int v = __shfl_up(incl, d);
+            if (lane >= d) incl += v;
+        }
+        const int tot = __shfl(incl, kWave - 1);
+        const int pre = incl - nf;
+        for (int j = 0; j < nf && j < kSegK; j++)
+            if (pre + j < kSegK) g.seg_cand[seg * kSegK + pre + j] = static_cast<uint64_t>(q.cs - q.off0) + found[j];
+        if (lane == 0)
+            g.seg_cnt[seg] = (tot > kSegK ? 0x80000000u : 0u) | static_cast<uint32_t>(tot < kSegK ? tot : kSegK);
+        if (!has_next) break;
+        seg = nseg_next;
+        q = qn;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // Exclusive prefix sum of stored counts (one workgroup; the long path has at most
@@ -2961,10 +3082,18 @@ int launch_split_long_multi(const Algo& algo, uint32_t m, const uint8_t* const* 
     if (nseg > 0) {
         const dim3 grid(static_cast<unsigned>((nseg + dev::kScanWaves - 1) / dev::kScanWaves));
         const dim3 block(dev::kScanWaves * dev::kWave);
-        if (algo.kind == kBuzhash)
+        if (algo.kind == kBuzhash && KCDC_LONG_DMA) {  // LDS-DMA fed, persistent: one workgroup per CU
+            const dim3 pgrid(static_cast<unsigned>(
+                std::min<int64_t>(t->cus, (nseg + dev::kDmaWaves - 1) / dev::kDmaWaves)));
+            if (buz_frame(static_cast<uint32_t>(algo.mask())).top)
+                hipLaunchKernelGGL(dev::cand_scan_dma_kernel<true>, pgrid, dim3(dev::kDmaWaves * dev::kWave), 0, st, a, g);
+            else
+                hipLaunchKernelGGL(dev::cand_scan_dma_kernel<false>, pgrid, dim3(dev::kDmaWaves * dev::kWave), 0, st, a, g);
+        } else if (algo.kind == kBuzhash) {
             hipLaunchKernelGGL(dev::cand_scan_kernel<kBuzhash>, grid, block, 0, st, a, g);
-        else
+        } else {
             hipLaunchKernelGGL(dev::cand_scan_kernel<kRabinKarp>, grid, block, 0, st, a, g);
+        }
         hipLaunchKernelGGL(dev::seg_prefix_kernel, dim3(1), dim3(1024), 0, st, g);
         hipLaunchKernelGGL(dev::compact_kernel, dim3(static_cast<unsigned>((nseg + 255) / 256)), dim3(256), 0, st, g);
     }

@@ -21,12 +21,13 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "kopia_amd", "csrc", "kcdc_kernels.hip")
 HIPCC = "/opt/rocm/bin/hipcc"
-KERNEL = "_ZN4kcdc3dev23split_batch_pipe_kernelILb1EEEvNS0_9BatchArgsE"  # <TOP = true>, KCDC_SCHED 2
+KERNELS = ["_ZN4kcdc3dev23split_batch_pipe_kernelILb1EEEvNS0_9BatchArgsE",  # <TOP = true>, KCDC_SCHED 2
+           "_ZN4kcdc3dev20cand_scan_dma_kernelILb1EEEvNS0_9BatchArgsENS0_8LongArgsE"]  # long-path scan
 
 
-def _blocks(asm: str):
-    """Basic blocks of the DMA kernel: (label, [instructions])."""
-    m = re.search(rf"^{KERNEL}:(.*?)s_endpgm", asm, re.S | re.M)
+def _blocks(asm: str, kernel: str):
+    """Basic blocks of a DMA kernel: (label, [instructions])."""
+    m = re.search(rf"^{kernel}:(.*?)s_endpgm", asm, re.S | re.M)
     assert m, "DMA kernel not found in the device assembly"
     out, cur = [], ["entry", []]
     out.append(cur)
@@ -52,19 +53,21 @@ def dma_asm(tmp_path_factory):
     return open(out).read(), open(res).read()
 
 
-def test_dma_not_in_waterfall_loops(dma_asm):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_dma_not_in_waterfall_loops(dma_asm, kernel):
     asm, _ = dma_asm
-    for label, ins in _blocks(asm):
+    for label, ins in _blocks(asm, kernel):
         if any("buffer_load_dwordx4" in i and " lds" in i for i in ins):
             assert not any(i.startswith("s_cbranch_execnz " + label) for i in ins), \
                 f"LDS-DMA in a readfirstlane waterfall loop at {label}"
             assert not any(i.startswith("v_readfirstlane") for i in ins), f"readfirstlane next to LDS-DMA at {label}"
 
 
-def test_no_scratch_in_hash_or_dma_blocks(dma_asm):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_no_scratch_in_hash_or_dma_blocks(dma_asm, kernel):
     asm, _ = dma_asm
     hot = 0
-    for label, ins in _blocks(asm):
+    for label, ins in _blocks(asm, kernel):
         is_hash = sum(1 for i in ins if i.startswith("v_bitop3_b32")) >= 32
         is_dma = any("buffer_load_dwordx4" in i and " lds" in i for i in ins)
         hot += is_hash
@@ -73,18 +76,23 @@ def test_no_scratch_in_hash_or_dma_blocks(dma_asm):
     assert hot >= 1, "expected the unrolled hash step"
 
 
-def test_no_vgpr_spills(dma_asm):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_no_vgpr_spills(dma_asm, kernel):
     _, res = dma_asm
-    sect = res[res.index("Function Name: " + KERNEL):]
+    sect = res[res.index("Function Name: " + kernel):]
     m = re.search(r"VGPRs Spill: (\d+)", sect)
     assert m and int(m.group(1)) == 0, "VGPR spills in the DMA kernel"
 
 
-def test_hash_blocks_lean(dma_asm):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_hash_blocks_lean(dma_asm, kernel):
     asm, _ = dma_asm
-    for label, ins in _blocks(asm):
+    for label, ins in _blocks(asm, kernel):
         nb = sum(1 for i in ins if i.startswith("v_bitop3_b32"))
         if nb >= 32:
+            hk = [k for k, i in enumerate(ins) if i.startswith("v_bitop3_b32")]
+            assert not any(i.startswith("s_waitcnt") and "vmcnt" in i for i in ins[hk[0]:hk[-1]]), \
+                f"vmcnt wait among the hash instructions of {label} (drains the DMA prefetch)"
             nop = sum(1 for i in ins if i.startswith("s_nop"))
             vand = sum(1 for i in ins if i.startswith("v_and_b32"))
             assert nop <= nb // 16, f"{nop} s_nop for {nb} bytes in {label}"
