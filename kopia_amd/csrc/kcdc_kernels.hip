@@ -14,19 +14,19 @@
 // bytes are rolled) becomes "start scanning at s+min-64": bytes before that are
 // never read.
 //
-// Work decomposition — one wavefront per stream (batch path):
-//   persistent waves pull stream ids from an atomic queue; a wave walks its
-//   stream chunk by chunk, scanning the test region [s+min-1, s+max-1] in TILES
-//   of 64 lanes x L bytes.  Lane l owns the L-byte segment l of the tile and
-//   warms its hash up on the 64 bytes before it, so the 64 lanes hash
-//   independently.  Each lane streams its segment in kBlk-byte steps (whole
-//   128-byte lines, 16-byte buffer loads, one step prefetched).  Per byte: two
-//   v_perm (table addresses for the entering and the leaving byte), two LDS
-//   table reads (the 1 KiB buzhash table is replicated 64x so lane l always hits
-//   bank l%32: conflict-free), v_alignbit (rotl 1), two XOR and the candidate
-//   test folded into a running min (v_bitop3 + v_min3).  A step whose running
-//   min is 0 is re-run exactly (rolled loop) to find the first candidate; the
-//   earliest lane with a candidate (ballot + ffs) gives the tile's answer.
+// Kernels:
+//   split_batch_pipe_kernel  the batch hot path (buzhash): persistent waves, one stream per
+//       wave at a time through a ticketed ring queue; a stream is walked in TILES of 64
+//       lanes x L bytes of its test region [s+min-1, s+max-1], lane l hashing segment l
+//       after warming up on the 64 bytes before it.  Bytes arrive by LDS-DMA in 128-byte
+//       steps; per byte one v_perm (table address), one ds_read of the 64x replicated
+//       table (lane l hits bank l%32), a T-ring register for the leaving byte, v_alignbit
+//       and v_bitop3, and a running v_min3 candidate test in the rotated frame.  A step
+//       whose min passes is re-run exactly; the earliest lane's candidate is the cut.
+//   split_batch_kernel       the same walk with per-lane buffer loads (Rabin-Karp).
+//   cand_scan_dma_kernel / cand_scan_kernel, seg_prefix, compact, resolve   the long path.
+//   scan_first_kernel        one region's first candidate (streaming handle).
+//   split_fixed_kernel       FIXED names (reads no data).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -801,37 +801,15 @@ __global__ __launch_bounds__(kBatchWaves * kWave, kBatchWaves / 4) void split_ba
 // (8 x 3 slots 1.68, 6 x 4 1.81, 4 x 6 2.00).
 #define KCDC_DMA_WAVES 8
 #endif
-#ifndef KCDC_DMA_SLOTS
-#define KCDC_DMA_SLOTS 2
-#endif
 constexpr int kDmaWaves = KCDC_DMA_WAVES;  // waves per workgroup (one workgroup per CU)
-constexpr int kDmaSlots = KCDC_DMA_SLOTS;  // 4 KiB LDS-DMA slots per wave (pipeline depth)
-#ifndef KCDC_YIELD_BYTES
-// Scanned bytes per visit before a stream is yielded while others wait (0 = never).
-// A hand-off costs ~30 us of wave time under full HBM load (sc1 progress stores,
-// drained waits, contended head/tail atomics), so the quantum is coarse: measured on
-// MI355X (8 waves/CU), 4096 x 4 MiB: never 1.62 ms, 512 KiB 1.69, 768 KiB 1.53,
-// 1 MiB 1.57, 2 MiB 1.69; 8192 x 8 MiB: never 8.62 ms, 768 KiB 7.58, 1 MiB 7.63.
-#define KCDC_YIELD_BYTES (768 << 10)
-#endif
-constexpr int64_t kYieldBytes = KCDC_YIELD_BYTES;
-#ifndef KCDC_DMA_RUN
-#define KCDC_DMA_RUN 128
-#endif
-#ifndef KCDC_COLD
-#define KCDC_COLD 1  // cold tiles (carry + extension) instead of a warm-up per tile
-#endif
 #ifndef KCDC_DMA_AUX
 #define KCDC_DMA_AUX 2  // nt: once-read stream bytes (membench: 128-B runs 6.65 vs 6.38 TB/s)
 #endif
-// Bytes of each lane segment one DMA round fetches: 64 (two half-step pieces per step,
-// kDmaSlots-deep LDS pipeline) or 128 (one whole cache line per lane segment per step,
-// staged through ONE 8 KiB slot per wave: the step's bytes move to VGPRs at its start,
-// which frees the slot for the next step's DMA while the step is hashed).
-constexpr int kRun = KCDC_DMA_RUN;
-constexpr int kSlot = 64 * kWave;                            // 4 KiB: one 64-byte piece of every lane
-constexpr int kSlotBytes = kRun == 128 ? 128 * kWave : kSlot;  // LDS bytes per slot
-constexpr int kNSlots = kRun == 128 ? 1 : kDmaSlots;
+// Each step fetches 128 bytes (one whole cache line) of every lane segment, staged through
+// ONE 8 KiB slot per wave: the step's bytes move to VGPRs at its start, which frees the
+// slot for the next step's DMA while the step is hashed.
+constexpr int kSlot = 64 * kWave;          // 4 KiB: one 64-byte piece of every lane (warm slot)
+constexpr int kSlotBytes = 128 * kWave;    // 8 KiB: one 128-byte step of every lane
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 // The table and the DMA slots are SEPARATE __shared__ objects: LDS lowering then gives
@@ -839,14 +817,8 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // in-flight LDS-DMA into a slot.  In one struct every table read waited vmcnt(0) for the
 // DMA just issued, which serialised the prefetch with the hashing.
 struct DmaSlots {
-    __attribute__((aligned(16))) uint8_t b[kDmaWaves][kNSlots][kSlotBytes];
+    __attribute__((aligned(16))) uint8_t b[kDmaWaves][1][kSlotBytes];
 };
-// Each lane's segment head (first 64 bytes) for its predecessor's tile-end extension.
-struct HeadStash {
-    __attribute__((aligned(16))) uint32_t w[kDmaWaves][16][kWave];  // [wave][dword][lane]: conflict-free
-};
-static_assert(sizeof(DmaSlots) + sizeof(BuzShared) + (kRun == 128 ? sizeof(HeadStash) : 0) <= 160 * 1024,
-              "LDS-DMA slots + table + head stash exceed the CU's 160 KiB");
 
 // One LDS-DMA wave instruction (64 lanes x 16 B -> 1 KiB at LDS address m0), written as
 // inline asm so the waitcnt pass does not see an LDS-DMA: with several DMA sites and slots
@@ -959,223 +931,10 @@ __device__ __forceinline__ TileGeom tile_geom(int64_t ct, int64_t hi, const uint
     return g;
 }
 
-// scan_region() with LDS-DMA feeding; buzhash T-ring only.  Wave-uniform control
-// flow around every DMA (DMA lanes fetch for other lanes).
-// Resumable: tiles start at ct_io (tile-aligned; lo & ~127 on a fresh scan).  After
-// each candidate-free tile `budget` is charged the tile's bytes; once it is spent the
-// scan returns kYield with ct_io = next tile.  (The caller sets an unreachable budget
-// when the stream must not be yielded: a runtime flag tested here instead pushes the
-// tile state onto the VALU path and every LDS-DMA into a waterfall loop.)
-constexpr int64_t kYield = -2;
+// Scan budget meaning "never yield" (a visit's quantum when no stream waits).
 constexpr int64_t kNoYield = int64_t(1) << 62;
-template <bool TOP>
-__device__ int64_t scan_region_dma(BuzRing hash, uint32_t lim, uint8_t* sl, uint32_t* hs, const uint8_t* abase, int64_t off0,
-                                   int64_t nbytes_coord, int64_t lo, int64_t hi, int lane, int64_t& ct_io,
-                                   int64_t& budget) {
-    int64_t ct = ct_io;
-#if KCDC_DMA_RUN == 128
-    // Tiles of one visit are contiguous (tile t+1 starts where lane 63 of tile t ends).
-    // Only the first tile warms every lane on the 64 bytes before its segment (one 64-byte
-    // DMA piece); a later ("cold") tile carries lane 63's state into lane 0 and lets every
-    // other lane keep its own old state as a stand-in history: its first 63 positions are
-    // masked, and at the tile end its predecessor rolls 63 positions on into that head
-    // (extend64, the head bytes read from an LDS stash).  No warm-up bytes are
-    // read after the first tile, and the next tile's first step is prefetched during the
-    // last step of the current one, so a visit is one continuous DMA pipeline.
-    if (ct > hi) return -1;
-    TileGeom g = tile_geom(ct, hi, abase, off0, nbytes_coord);
-    bool cold = false;
-    for (;;) {
-        if (!cold) {  // first tile of the visit: warm-up piece (64 bytes before each lane segment)
-            uint32_t w16[16];
-            dma_piece(g.ld, g.ld.tb, lds_addr(sl), ct, g.L, -1, lane);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            read_piece(sl, lane, ct + lane * g.L - 64, off0, w16);
-            hash.clear();
-            hash.template block<kWarm>(w16);  // consumes w16: the slot reads have completed
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            dma_step128(g.ld, g.ld.tb, lds_addr(sl), ct, g.L, 0, lane);
-        }
-        const int64_t c0 = ct + lane * g.L;
-        const int64_t ct_next = ct + kWave * g.L;
-        const bool more = ct_next <= hi && budget - kWave * g.L > 0;  // another tile follows
-        TileGeom gn = g;
-        if (more) gn = tile_geom(ct_next, hi, abase, off0, nbytes_coord);
-        if (cold) hash.carry_from_last_lane(lane == 0);
-        const uint32_t hmask = lane == 0 ? 0u : 0xFFFFFFFFu;
-        int64_t found = -1;
-        for (int n = 0; n < g.nb; n++) {
-            const int64_t c = c0 + 128 * n;
-            const typename BuzRing::State st0 = hash.save();
-            uint32_t dw[32];
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            read_step128(sl, lane, c, off0, dw);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot free: refill it
-            __builtin_amdgcn_sched_barrier(0);
-            if (n + 1 < g.nb)
-                dma_step128(g.ld, g.ld.tb, lds_addr(sl), ct, g.L, n + 1, lane);
-            else if (KCDC_COLD && more)
-                dma_step128(gn.ld, gn.ld.tb, lds_addr(sl), ct_next, gn.L, 0, lane);
-            __builtin_amdgcn_sched_barrier(0);
-            if (n == 0) {
-#pragma unroll
-                for (int i = 0; i < 16; i++) hs[kWave * i + lane] = dw[i];
-            }
-#ifdef KCDC_EXP_MEMONLY
-            uint32_t m = 0;
-#pragma unroll
-            for (int i = 0; i < 32; i++) m |= dw[i];
-            asm volatile("" : "+v"(m));
-#else
-            const uint32_t m = hash.template step128<TOP>(dw, n == 0 && cold ? hmask : 0u);
-#endif
-            __builtin_amdgcn_sched_barrier(0);
-            if (m <= lim && found < 0 && c <= hi) {  // rare: exact re-run from global memory
-                uint32_t prv[16], cur[32];
-                g.ld.load(c - 64, prv);
-                g.ld.load(c, cur);
-                const int64_t blo = lo - c, bhi = hi - c;
-                const int ilo = blo < 0 ? 0 : static_cast<int>(blo), ihi = bhi > 127 ? 127 : static_cast<int>(bhi);
-                const uint32_t idx = n == 0 ? hash.exact_cold(prv, cur, ilo, ihi) : hash.exact(st0, prv, cur, ilo, ihi);
-                if (idx < 128u) found = c + idx;
-            }
-        }
-        if (cold) {  // lanes 0..62: the successor's first 63 positions
-            uint32_t nx[16];
-#pragma unroll
-            for (int i = 0; i < 16; i++) nx[i] = hs[kWave * i + ((lane + 1) & (kWave - 1))];
-            if (lane != kWave - 1) {
-                const uint32_t m = hash.template extend64<TOP>(nx);
-                const int64_t c = c0 + g.L;  // successor's segment start
-                if (m <= lim && found < 0 && c <= hi) {
-                    uint32_t prv[16], cur[16];
-                    g.ld.load(c - 64, prv);
-                    g.ld.load(c, cur);
-                    const int64_t blo = lo - c, bhi = hi - c;
-                    const uint32_t idx = hash.exact_cold(prv, cur, blo < 0 ? 0 : static_cast<int>(blo),
-                                                         bhi > 63 ? 63 : static_cast<int>(bhi));
-                    if (idx < 64u) found = c + idx;
-                }
-            }
-        }
-        const uint64_t hit = __ballot(found >= 0);
-        if (hit) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // a prefetched step may be in flight
-            const int first = __builtin_ctzll(hit);
-            return static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, first))));
-        }
-        budget -= kWave * g.L;
-        ct = ct_next;
-        if (!more) break;
-        g = gn;
-        cold = KCDC_COLD;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (ct <= hi) {  // budget spent: yield with the next tile
-        ct_io = ct;
-        return kYield;
-    }
-    return -1;
-#endif
-    while (ct <= hi) {
-        const int64_t rem = hi - ct + 1;
-        int64_t per = (rem + kWave - 1) / kWave;
-        per = (per + 127) & ~int64_t(127);
-        const int64_t L = per < kLaneMax ? per : kLaneMax;
-        const int64_t tb = ct >= 64 ? ct - 64 : 0;
-        const Loader ld = make_loader(abase, off0, nbytes_coord, tb);
-        const int64_t c0 = ct + lane * L;
-        const int nb = static_cast<int>(L / 128);
-        int64_t found = -1;
 
-        // Pipeline of kDmaSlots 4 KiB slots: piece q (q = 0 is the 64-byte warm-up piece
-        // before each lane segment, q = 1.. the segment's pieces) lands in slot q % S and
-        // is fetched S - 1 pieces ahead of its use.  Explicit counted waits: hipcc does not
-        // track these LDS-DMAs across the loop (it emitted no vmcnt before the slot reads),
-        // so every slot read is preceded by vmcnt(4 (S-1)) (the S-1 younger pieces may stay
-        // in flight) or, in the last S-1 pieces of the tile, vmcnt(0).
-        constexpr int S = kDmaSlots;
-        const int Q = 2 * nb + 1;  // pieces in this tile
-#pragma unroll
-        for (int j = 0; j < S; j++)
-            if (j < Q) dma_piece(ld, tb, lds_addr(sl + kSlot * j), ct, L, j - 1, lane);
-        uint32_t dw[16], loc[64];
-        __builtin_amdgcn_sched_barrier(0);
-        if (S - 1 <= Q - 1)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (S - 1)) : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        read_piece(sl, lane, c0 - 64, off0, dw);
-        hash.clear();
-        hash.template block<kWarm>(dw);
-        __builtin_amdgcn_sched_barrier(0);
-        if (S < Q) dma_piece(ld, tb, lds_addr(sl), ct, L, S - 1, lane);
-        int qs = 1 % S;  // slot of piece q
-        for (int n = 0; n < nb; n++) {
-            const int64_t c = c0 + 128 * n;
-            const typename BuzRing::State st0 = hash.save();
-            uint32_t m = 0xFFFFFFFFu;
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int q = 2 * n + 1 + h;
-                uint8_t* slot = sl + kSlot * qs;
-                __builtin_amdgcn_sched_barrier(0);
-                if (q + S - 1 <= Q - 1)
-                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (S - 1)) : "memory");
-                else
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                read_piece(slot, lane, c + 64 * h, off0, dw);
-#ifdef KCDC_EXP_MEMONLY
-#pragma unroll
-                for (int i = 0; i < 16; i++) m |= dw[i];
-                asm volatile("" : "+v"(m));
-#else
-                m = h == 0 ? hash.template half<0, TOP>(dw, loc, m) : hash.template half<1, TOP>(dw, loc, m);
-#endif
-                __builtin_amdgcn_sched_barrier(0);
-                if (q + S < Q) dma_piece(ld, tb, lds_addr(slot), ct, L, q + S - 1, lane);
-                qs = qs + 1 == S ? 0 : qs + 1;
-            }
-            if (m <= lim && found < 0 && c <= hi) {  // rare: exact re-run from global memory
-                uint32_t prv[16], cur[32];
-                ld.load(c - 64, prv);
-                ld.load(c, cur);
-                const int64_t blo = lo - c, bhi = hi - c;
-                const uint32_t idx = hash.exact(st0, prv, cur, blo < 0 ? 0 : static_cast<int>(blo),
-                                                bhi > 127 ? 127 : static_cast<int>(bhi));
-                if (idx < 128u) found = c + idx;
-            }
-        }
-        // drain this tile's DMAs before the slots are reused
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint64_t hit = __ballot(found >= 0);
-        if (hit) {
-            const int first = __builtin_ctzll(hit);
-            return static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, first))));
-        }
-        ct += kWave * L;
-        budget -= kWave * L;
-        if (ct <= hi && budget <= 0) {
-            ct_io = ct;
-            return kYield;
-        }
-    }
-    return -1;
-}
-
-// ---------------------------------------------------- time-sliced stream queue
-// A persistent wave owns one stream at a time.  While streams are waiting for a wave
-// (the queue has a backlog) an owner yields its stream after kYieldBytes of scanning:
-// the stream's progress {s, ct, cnt} is published and the stream re-queued, so every
-// stream advances at the chip's shared rate instead of the last streams starting only
-// when the first ones finish (a measured 0.65 busy fraction for 4096 streams on 3072
-// waves, tools/trace_sched.py).  Hand-off follows cdna_hip_programming.md Guideline 16
-// R1/R2: progress words stored sc1 (relaxed agent atomics) and drained before the ring
-// entry {tag = push number + 1, sid} is stored; the taker polls its entry's tag and
-// loads the progress sc1.  Ring size P > nstreams + grid waves (host), so two live
-// tickets never share a slot; a pusher waits for its slot to be empty (reset on take).
+// ------------------------------------------- agent-scope atomics, queue header
 typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef __attribute__((address_space(1))) uint64_t gu64;
 __device__ __forceinline__ uint32_t ld_agent(uint32_t* p) {
@@ -1197,348 +956,11 @@ __device__ __forceinline__ uint64_t bcast64(uint64_t v) {
 // Header words (uint32 offsets) 2 KiB apart: hammered counters do not share DRAM pages.
 constexpr int kQHead = 0, kQDone = 512, kQTail = 1024, kQErr = 1536;
 constexpr size_t kQHeaderBytes = 8192;
-// KCDC_TRACE builds also count, in header words 1792..: [+0] yields, [+1] (unused),
-// [+2] entry-wait spins, [+3] slot-wait spins; 64-bit s_memrealtime (100 MHz) sums over
-// waves: [+4..5] in take_stream, [+6..7] in yield_stream, [+8..9] in run_stream.
+// Header words 1792.. : debug-build failure record (pcheck, KCDC_DEBUG_CHECKS).
 constexpr int kQStat = 1792;
-#if KCDC_TRACE
-#define KCDC_QSTAT(w, v) \
-    do { if (lane == 0) atomicAdd(a.queue + (w), (v)); } while (0)
-#define KCDC_QSTAT64(w, v) \
-    do { if (lane == 0) atomicAdd(reinterpret_cast<unsigned long long*>(a.queue + (w)), (v)); } while (0)
-#else
-#define KCDC_QSTAT(w, v) do {} while (0)
-#define KCDC_QSTAT64(w, v) do {} while (0)
-#endif
 constexpr uint32_t kSpinCap = 1u << 22;                          // give up (error word) after ~seconds
 
-struct Progress {
-    int64_t s;     // current chunk start
-    int64_t ct;    // next tile coordinate of the chunk's candidate scan (< 0: not started)
-    uint64_t cnt;  // cuts emitted
-};
-
-// Take the next stream; returns its id (progress in pr) or -1 when no stream is waiting.
-// No wave ever waits for work: when tickets taken >= initial + yielded streams, every
-// queued stream already has a taker (each yielder takes a ticket right after its push),
-// so the wave exits.  `more` reports whether streams were still waiting after this take
-// (the owner then yields after kYieldBytes; no polling while scanning).
-__device__ int64_t take_stream(const BatchArgs& a, int lane, Progress& pr, bool& more) {
-    uint32_t* q = a.queue;
-    const uint32_t n = a.nstreams;
-    uint32_t tail = 0, t = 0;
-    if (lane == 0) {
-        tail = ld_agent(q + kQTail);
-        t = n + tail > ld_agent(q + kQHead) ? add_agent(q + kQHead, 1u) : 0xFFFFFFFFu;
-    }
-    t = bcast(t);
-    if (t == 0xFFFFFFFFu) return -1;
-    tail = bcast(tail);
-    more = n + tail > t + 1;
-    if (t < n) {  // initial ticket: stream t from its start
-        pr.s = 0;
-        pr.ct = -1;
-        pr.cnt = 0;
-        return t;
-    }
-    const uint32_t e = t - n;  // the push this ticket takes
-    uint64_t* slot = reinterpret_cast<uint64_t*>(a.ring) + (e & a.ring_mask);
-    uint64_t v = 0;
-    for (uint32_t spin = 0;; spin++) {
-        uint32_t st = 0;  // 0 wait, 1 got it, 2 exit
-        if (lane == 0) {
-            v = ld_agent64(slot);
-            if (static_cast<uint32_t>(v >> 32) == e + 1u) {
-                st = 1;
-            } else if (ld_agent(q + kQDone) >= n) {
-                st = 2;
-            } else if (spin >= kSpinCap) {
-                add_agent(q + kQErr, 1u);
-                st = 2;
-            }
-        }
-        st = bcast(st);
-        if (st == 2) return -1;
-        if (st == 1) break;
-        KCDC_QSTAT(kQStat + 2, 1u);
-        __builtin_amdgcn_s_sleep(64);
-    }
-    const uint32_t sid = bcast(static_cast<uint32_t>(v));
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // progress loads stay behind the poll
-    uint64_t w0 = 0, w1 = 0, w2 = 0;
-    if (lane == 0) {
-        w0 = ld_agent64(a.states + 3ull * sid + 0);
-        w1 = ld_agent64(a.states + 3ull * sid + 1);
-        w2 = ld_agent64(a.states + 3ull * sid + 2);
-        st_agent64(slot, 0);  // free the slot for push e + P
-    }
-    pr.s = static_cast<int64_t>(bcast64(w0));
-    pr.ct = static_cast<int64_t>(bcast64(w1));
-    pr.cnt = bcast64(w2);
-    return sid;
-}
-
-// Re-queue a yielded stream with its progress.
-__device__ void yield_stream(const BatchArgs& a, int lane, uint32_t sid, const Progress& pr) {
-    uint32_t* q = a.queue;
-    KCDC_QSTAT(kQStat + 0, 1u);
-    if (lane == 0) {
-        st_agent64(a.states + 3ull * sid + 0, static_cast<uint64_t>(pr.s));
-        st_agent64(a.states + 3ull * sid + 1, static_cast<uint64_t>(pr.ct));
-        st_agent64(a.states + 3ull * sid + 2, pr.cnt);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // progress visible before the entry
-    uint32_t e = 0;
-    if (lane == 0) e = add_agent(q + kQTail, 1u);
-    e = bcast(e);
-    uint64_t* slot = reinterpret_cast<uint64_t*>(a.ring) + (e & a.ring_mask);
-    for (uint32_t spin = 0;; spin++) {
-        uint32_t st = 0;
-        if (lane == 0) {
-            if (ld_agent64(slot) == 0) {
-                st_agent64(slot, (static_cast<uint64_t>(e + 1u) << 32) | sid);
-                st = 1;
-            } else if (spin >= kSpinCap) {
-                add_agent(q + kQErr, 1u);
-                st = 1;
-            }
-        }
-        if (bcast(st)) break;
-        KCDC_QSTAT(kQStat + 3, 1u);
-        __builtin_amdgcn_s_sleep(4);
-    }
-}
-
-// ------------------------------------------------ packed-entry stream queue (KCDC_SCHED 1)
-// Fewer round trips per hand-off than take_stream/yield_stream: a take is one atomic
-// (with the pushed count read beside it) and a yielded stream's progress travels inside
-// its 64-byte ring entry: three 16-byte sc1 stores, each
-// carrying the entry tag (push number + 1), so the taker needs no separate progress
-// loads and the pusher no drain before its flag (MI355X_MICROARCH.md: a tagged 16-byte
-// sc1 granule is read untorn).  Ticket t < n is stream t from its start; ticket t >= n is
-// ring entry e = t - n, polled until its tag matches or every stream is done.  A
-// ticket's holder always polls it, so every pushed entry has a taker (no deadlock);
-// waves exit only once kQDone reaches n.
-#ifndef KCDC_SCHED
-#define KCDC_SCHED 2
-#endif
-constexpr int kEntryBytes = 64;
-__device__ __forceinline__ uint32_t reserve_ticket(const BatchArgs& a, int lane) {
-    uint32_t t = 0;
-    if (lane == 0) t = add_agent(a.queue + kQHead, 1u);
-    return bcast(t);
-}
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t ring_rsrc(const BatchArgs& a) {
-    return __builtin_amdgcn_make_buffer_rsrc(a.ring, static_cast<short>(0),
-                                             static_cast<int>((a.ring_mask + 1u) * kEntryBytes), 0x00020000);
-}
-// Resolve ticket t into (sid, progress); false when every stream is done (wave exits).
-__device__ bool resolve_ticket(const BatchArgs& a, int lane, uint32_t t, uint32_t& sid, Progress& pr) {
-    const uint32_t n = a.nstreams;
-    if (t < n) {
-        sid = t;
-        pr.s = 0;
-        pr.ct = -1;
-        pr.cnt = 0;
-        return true;
-    }
-    const uint32_t e = t - n;
-    const __amdgpu_buffer_rsrc_t r = ring_rsrc(a);
-    const int off = static_cast<int>((e & a.ring_mask) * kEntryBytes) + 16 * (lane & 3);
-    for (uint32_t spin = 0;; spin++) {
-        u32x4 v = {0, 0, 0, 0};
-        if (lane < 3) v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16 /* sc1 */);
-        const bool ok = lane >= 3 || v.x == e + 1u;
-        if (__ballot(!ok) == 0) {
-            sid = __builtin_amdgcn_readlane(v.y, 0);
-            pr.cnt = __builtin_amdgcn_readlane(v.z, 0);
-            pr.s = static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(v.z, 1))) << 32) |
-                                        static_cast<uint32_t>(__builtin_amdgcn_readlane(v.y, 1)));
-            pr.ct = static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(v.z, 2))) << 32) |
-                                         static_cast<uint32_t>(__builtin_amdgcn_readlane(v.y, 2)));
-            return true;
-        }
-        uint32_t st = 0;  // 0 wait, 2 exit
-        if (lane == 0) {
-            if (ld_agent(a.queue + kQDone) >= n) {
-                st = 2;
-            } else if (spin >= kSpinCap) {
-                add_agent(a.queue + kQErr, 1u);
-                st = 2;
-            }
-        }
-        if (bcast(st) == 2) return false;
-        __builtin_amdgcn_s_sleep(32);
-    }
-}
-// Re-queue stream sid with its progress (one atomic for the entry number, one store).
-__device__ void push_stream(const BatchArgs& a, int lane, uint32_t sid, const Progress& pr) {
-    uint32_t e = 0;
-    if (lane == 0) e = add_agent(a.queue + kQTail, 1u);
-    e = bcast(e);
-    const uint64_t s = static_cast<uint64_t>(pr.s), ct = static_cast<uint64_t>(pr.ct);
-    u32x4 v;
-    v.x = e + 1u;
-    v.y = lane == 0 ? sid : lane == 1 ? static_cast<uint32_t>(s) : static_cast<uint32_t>(ct);
-    v.z = lane == 0 ? static_cast<uint32_t>(pr.cnt) : lane == 1 ? static_cast<uint32_t>(s >> 32)
-                                                                : static_cast<uint32_t>(ct >> 32);
-    v.w = 0;
-    if (lane < 3)
-        __builtin_amdgcn_raw_buffer_store_b128(v, ring_rsrc(a), static_cast<int>((e & a.ring_mask) * kEntryBytes) + 16 * lane,
-                                               0, 16 /* sc1 */);
-}
-
-// Advance stream sid from pr: returns true when it is finished, false when yielded.
-template <bool TOP>
-__device__ __forceinline__ bool run_stream(const BatchArgs& a, const BuzRing& hash, uint8_t* sl, uint32_t* hs,
-                                           uint32_t sid, Progress& pr, bool more, int lane) {
-    const uint64_t p = uni64(reinterpret_cast<uint64_t>(a.ptrs[sid]));
-    const int64_t n = static_cast<int64_t>(uni64(a.lens[sid]));
-    const uint64_t cb = uni64(a.cut_base[sid]);
-    const uint64_t cend = sid + 1 < a.nstreams ? uni64(a.cut_base[sid + 1]) : a.cuts_cap;
-    const uint64_t cap = cend > cb ? cend - cb : 0;
-    const int64_t off0 = static_cast<int64_t>(p & 15u);
-    const uint8_t* abase = reinterpret_cast<const uint8_t*>(p - static_cast<uint64_t>(off0));
-    const int64_t mn = static_cast<int64_t>(a.min_size), mx = static_cast<int64_t>(a.max_size);
-    int64_t budget = more && kYieldBytes > 0 ? kYieldBytes : kNoYield;
-    while (pr.s < n) {
-        const int64_t s = pr.s;
-        const int64_t pf = s + mn - 1;
-        int64_t next;
-        if (pf >= n) {
-            next = n;
-        } else {
-            const int64_t pl = s + mx - 1 < n - 1 ? s + mx - 1 : n - 1;
-            if (pr.ct < 0) pr.ct = (pf + off0) & ~int64_t(127);
-            const int64_t f = scan_region_dma<TOP>(hash, TOP ? a.buz_lim : 0u, sl, hs, abase, off0, off0 + n, pf + off0, pl + off0, lane, pr.ct,
-                                              budget);
-            if (f == kYield) return false;
-            if (f >= 0)
-                next = f - off0 + 1;
-            else if (s + mx - 1 <= n - 1)
-                next = s + mx;  // forced cut at max size (splitter_buzhash32.go:60-64)
-            else
-                next = n;
-        }
-        if (lane == 0 && pr.cnt < cap) a.cuts[cb + pr.cnt] = static_cast<uint64_t>(next);
-        pr.cnt++;
-        pr.s = next;
-        pr.ct = -1;
-    }
-    if (lane == 0) a.counts[sid] = pr.cnt;
-    return true;
-}
-
-template <bool TOP>
-__global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_dma_kernel(BatchArgs a) {
-    __shared__ BuzShared smtab;
-    __shared__ DmaSlots smslots;
-#if KCDC_DMA_RUN == 128
-    __shared__ HeadStash smheads;
-#endif
-    for (uint32_t i = threadIdx.x; i < 256u * 64u; i += blockDim.x) smtab.tab[i] = rotl_n(a.buz[i >> 6], a.buz_rot);
-    __syncthreads();
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    BuzRing hash;
-    hash.tab = reinterpret_cast<const char*>(smtab.tab);
-    hash.lane4 = static_cast<uint32_t>(lane) * 4u;
-    hash.mask = a.mask;
-    hash.h = 0;
-    uint8_t* sl = smslots.b[wave][0];
-#if KCDC_DMA_RUN == 128
-    uint32_t* hs = &smheads.w[wave][0][0];
-#else
-    uint32_t* hs = nullptr;
-#endif
-#ifdef KCDC_EXP_COMPONLY
-    for (int i = lane; i < kNSlots * kSlotBytes / 4; i += kWave)
-        reinterpret_cast<uint32_t*>(sl)[i] = static_cast<uint32_t>((i + 1) * 2654435761u) ^ (wave * 0x9E3779B9u);
-#endif
-#if KCDC_SCHED == 1
-    for (;;) {
-        Progress pr;
-        uint32_t sid;
-#if KCDC_TRACE
-        uint64_t tc = __builtin_amdgcn_s_memrealtime();
-#endif
-        // take a ticket; in the same round trip read how many streams were pushed
-        uint32_t t = 0, tail = 0;
-        if (lane == 0) t = add_agent(a.queue + kQHead, 1u);
-        if (lane == 1) tail = ld_agent(a.queue + kQTail);
-        t = __builtin_amdgcn_readlane(t, 0);
-        tail = __builtin_amdgcn_readlane(tail, 1);
-        if (!resolve_ticket(a, lane, t, sid, pr)) break;
-        // streams are waiting beyond this ticket => time-slice this one
-        const bool more = t + 1 < a.nstreams + tail;
-#if KCDC_TRACE
-        KCDC_QSTAT64(kQStat + 4, __builtin_amdgcn_s_memrealtime() - tc);
-        tc = __builtin_amdgcn_s_memrealtime();
-        if (lane == 0 && pr.s == 0 && pr.ct < 0) a.trace[3 * sid + 0] = tc;
-#endif
-        const bool fin = run_stream<TOP>(a, hash, sl, hs, sid, pr, more, lane);
-#if KCDC_TRACE
-        KCDC_QSTAT64(kQStat + 8, __builtin_amdgcn_s_memrealtime() - tc);
-        tc = __builtin_amdgcn_s_memrealtime();
-#endif
-        if (fin) {
-#if KCDC_TRACE
-            if (lane == 0) {
-                a.trace[3 * sid + 1] = __builtin_amdgcn_s_memrealtime();
-                a.trace[3 * sid + 2] = blockIdx.x | (wave << 16);
-            }
-#endif
-            if (lane == 0) add_agent(a.queue + kQDone, 1u);
-        } else {
-            push_stream(a, lane, sid, pr);
-#if KCDC_TRACE
-            KCDC_QSTAT(kQStat + 0, 1u);
-            KCDC_QSTAT64(kQStat + 6, __builtin_amdgcn_s_memrealtime() - tc);
-#endif
-        }
-    }
-#else
-    for (;;) {
-        Progress pr;
-#if KCDC_TRACE
-        uint64_t tc = __builtin_amdgcn_s_memrealtime();
-#endif
-        bool more = false;
-        const int64_t got = take_stream(a, lane, pr, more);
-#if KCDC_TRACE
-        KCDC_QSTAT64(kQStat + 4, __builtin_amdgcn_s_memrealtime() - tc);
-        tc = __builtin_amdgcn_s_memrealtime();
-#endif
-        if (got < 0) break;
-        const uint32_t sid = static_cast<uint32_t>(got);
-#if KCDC_TRACE
-        if (lane == 0 && pr.s == 0 && pr.ct < 0) a.trace[3 * sid + 0] = __builtin_amdgcn_s_memrealtime();
-#endif
-        const bool fin = run_stream<TOP>(a, hash, sl, hs, sid, pr, more, lane);
-#if KCDC_TRACE
-        KCDC_QSTAT64(kQStat + 8, __builtin_amdgcn_s_memrealtime() - tc);
-        tc = __builtin_amdgcn_s_memrealtime();
-#endif
-        if (fin) {
-#if KCDC_TRACE
-            if (lane == 0) {
-                a.trace[3 * sid + 1] = __builtin_amdgcn_s_memrealtime();
-                a.trace[3 * sid + 2] = blockIdx.x | (wave << 16);
-            }
-#endif
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // cuts/counts stored before done
-            if (lane == 0) add_agent(a.queue + kQDone, 1u);
-        } else {
-            yield_stream(a, lane, sid, pr);
-#if KCDC_TRACE
-            KCDC_QSTAT64(kQStat + 6, __builtin_amdgcn_s_memrealtime() - tc);
-#endif
-        }
-    }
-#endif
-}
-
-// ========================================= pipelined persistent kernel (KCDC_SCHED 2)
+// ======================================================= pipelined persistent kernel
 // One per-wave state machine over tiles.  Every tile warms its 64 lanes on the 64 bytes
 // before their segments (a 4 KiB piece in the wave's warm slot) and hashes 16 steps of
 // 128-byte runs (8 KiB step slot).  The warm piece and first step of the NEXT tile are
@@ -1593,6 +1015,8 @@ constexpr int kPEntryStride = 128;
 struct WarmSlots {
     __attribute__((aligned(16))) uint8_t b[kDmaWaves][kSlot];  // 4 KiB: the 64 bytes before each lane segment
 };
+static_assert(sizeof(DmaSlots) + sizeof(WarmSlots) + sizeof(BuzShared) <= 160 * 1024,
+              "step slots + warm slots + table exceed the CU's 160 KiB of LDS");
 
 struct PStream {
     uint32_t sid;    // | kProbeBit for a probe
@@ -2885,11 +2309,11 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         const unsigned need = (s.nstreams + wg_waves - 1) / wg_waves;
         const unsigned grid = need < cus ? need : cus;
         uint64_t ring = 1;
-        // KCDC_SCHED 1: a reserved ticket may be polled up to a quantum after it was taken,
-        // while the other waves keep pushing: size the ring with ample margin
-        const uint64_t live = static_cast<uint64_t>(s.nstreams) + (KCDC_SCHED >= 1 ? 8ull : 1ull) * grid * wg_waves;
+        // every push (yields, probes, tombstones) takes a fresh slot; a launch pushes at most
+        // a few entries per wave beyond the initial n: size the ring with ample margin
+        const uint64_t live = static_cast<uint64_t>(s.nstreams) + 8ull * grid * wg_waves;
         while (ring <= live) ring <<= 1;
-        const size_t ring_bytes = dma ? (KCDC_SCHED == 2 ? 128 : KCDC_SCHED == 1 ? 64 : 8) * ring : 0;
+        const size_t ring_bytes = dma ? static_cast<size_t>(dev::kPEntryStride) * ring : 0;
         const size_t hdr = dev::kQHeaderBytes;
         const size_t bytes = hdr + ring_bytes + (dma ? 24ull * s.nstreams : 0);
         char* ws = nullptr;
@@ -2924,36 +2348,24 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         a.trace = g_trace;
 #endif
         // header + ring zeroed per launch (the ring is also left empty by every finished launch)
-#if KCDC_SCHED == 2
         if (dma) {
             const uint32_t slots = static_cast<uint32_t>(ring);
             const uint64_t threads = std::max<uint64_t>(8ull * slots, dev::kQHeaderBytes / 4);
             hipLaunchKernelGGL(dev::init_ring_kernel, dim3(static_cast<unsigned>((threads + 255) / 256)), dim3(256), 0, st, a,
                                slots, grid * wg_waves);
-        } else
-#endif
-        {
+        } else {
             hipError_t e = hipMemsetAsync(ws, 0, hdr + ring_bytes, st);
             if (e != hipSuccess) return hip_fail(e, "queue reset");
         }
         // persistent grid: one workgroup per CU, never more workgroups than the streams need
         if (dma) {
             const bool top = buz_frame(static_cast<uint32_t>(algo.mask())).top;
-#if KCDC_SCHED == 2
             if (top)
                 hipLaunchKernelGGL(dev::split_batch_pipe_kernel<true>, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0,
                                    st, a);
             else
                 hipLaunchKernelGGL(dev::split_batch_pipe_kernel<false>, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0,
                                    st, a);
-#else
-            if (top)
-                hipLaunchKernelGGL(dev::split_batch_dma_kernel<true>, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0,
-                                   st, a);
-            else
-                hipLaunchKernelGGL(dev::split_batch_dma_kernel<false>, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0,
-                                   st, a);
-#endif
         } else {
             const dim3 block(dev::kBatchWaves * dev::kWave);
             if (algo.kind == kBuzhash)

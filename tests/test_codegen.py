@@ -1,6 +1,6 @@
 """Codegen guards for the LDS-DMA batch kernel (CPU: hipcc cross-compiles gfx950).
 
-Two silent performance cliffs were hit while developing split_batch_dma_kernel
+Two silent performance cliffs were hit while developing the LDS-DMA batch kernel
 (kopia_amd/csrc/kcdc_kernels.hip) and are pinned here:
 * a runtime flag tested inside the tile loop made hipcc treat the tile state as
   divergent: every LDS-DMA (buffer_load ... lds, which needs SGPR operands) was
@@ -21,7 +21,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "kopia_amd", "csrc", "kcdc_kernels.hip")
 HIPCC = "/opt/rocm/bin/hipcc"
-KERNELS = ["_ZN4kcdc3dev23split_batch_pipe_kernelILb1EEEvNS0_9BatchArgsE",  # <TOP = true>, KCDC_SCHED 2
+KERNELS = ["_ZN4kcdc3dev23split_batch_pipe_kernelILb1EEEvNS0_9BatchArgsE",  # <TOP = true>
            "_ZN4kcdc3dev20cand_scan_dma_kernelILb1EEEvNS0_9BatchArgsENS0_8LongArgsE"]  # long-path scan
 
 

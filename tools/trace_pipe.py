@@ -1,5 +1,5 @@
 """Per-wave start/end trace of the pipelined batch kernel (library built with
--DKCDC_TRACE=1, KCDC_SCHED 2): how much of the kernel's span the waves are alive, and
+-DKCDC_TRACE=1): how much of the kernel's span the waves are alive, and
 the spread of their end times (the scheduling tail).  usage: trace_pipe.py LIB [ns mib]"""
 import ctypes as C
 import json
