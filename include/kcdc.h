@@ -104,6 +104,22 @@ void kcdc_splitter_reset(kcdc_splitter* s);
  * names) or free.  The handle must not be used afterwards. */
 void kcdc_splitter_close(kcdc_splitter* s);
 
+/* ------------------------------------------------ grouped streaming handles
+ * Kopia runs many object writers at once (snapshot/upload/upload.go:769-782),
+ * each with its own Splitter fed 64 KiB slices (upload.go:394-407).  A group
+ * batches the GPU work of all its handles' concurrent NextSplitPoint calls into
+ * one launch: each call stages its slice into pinned memory from its own thread
+ * and blocks until the group's launch returns its answer (same semantics and
+ * results as kcdc_splitter_next on a private handle).  The group thread waits up
+ * to `max_wait_us` for more calls (0: ship whatever is there) and takes at most
+ * `max_batch` calls per launch (0: 256).  One name per group (a repository uses
+ * one splitter).  Handles come from kcdc_group_splitter and are released with
+ * kcdc_splitter_close; free the group after its handles. */
+typedef struct kcdc_group kcdc_group;
+kcdc_group* kcdc_group_new(const char* name, int device, uint32_t max_batch, uint32_t max_wait_us);
+kcdc_splitter* kcdc_group_splitter(kcdc_group* g);
+void kcdc_group_free(kcdc_group* g);
+
 /* ------------------------------------------------------ batch (hot path)
  * Split `nstreams` independent streams in one launch; every stream starts from
  * a fresh splitter (the pool's Reset-on-Close, splitter_pool.go:18-22).

@@ -59,6 +59,9 @@ _SIGS = {
     "kcdc_fill_prng": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, _P]),
     "kcdc_split_files_device": (C.c_int, [C.c_char_p, _P, _P, C.c_uint32, _P, C.c_uint64, _P, _P, _P]),
     "kcdc_gorand_read": (C.c_int, [C.c_int64, _P, C.c_uint64]),
+    "kcdc_group_new": (_P, [C.c_char_p, C.c_int, C.c_uint32, C.c_uint32]),
+    "kcdc_group_splitter": (_P, [_P]),
+    "kcdc_group_free": (None, [_P]),
 }
 
 

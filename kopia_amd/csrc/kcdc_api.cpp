@@ -4,8 +4,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -131,6 +134,7 @@ struct kcdc_splitter {
     size_t stage_cap = 0;
     int64_t* d_out = nullptr;
     int64_t* h_out = nullptr;
+    kcdc_group* group = nullptr;  // set: GPU scans are batched with the group's other handles
 };
 
 namespace {
@@ -177,8 +181,14 @@ int ensure_stage(kcdc_splitter* s, size_t need) {
     return KCDC_OK;
 }
 
+int64_t group_first_candidate(kcdc_splitter* s, const uint8_t* b, size_t n);
+
 // First candidate index in slice b[0..n) given the 64-byte history, on the GPU.
 int64_t gpu_first_candidate(kcdc_splitter* s, const uint8_t* b, size_t n) {
+    if (s->group) {
+        const int64_t f = group_first_candidate(s, b, n);
+        if (f != KCDC_EOVERFLOW) return f;  // too big for the group's staging: scan it alone
+    }
     const size_t total = kWindow + n;
     int rc = ensure_stage(s, total);
     if (rc) return rc;
@@ -295,13 +305,203 @@ extern "C" void kcdc_splitter_reset(kcdc_splitter* s) {
 extern "C" void kcdc_splitter_close(kcdc_splitter* s) {
     if (!s) return;
     kcdc_splitter_reset(s);  // recyclableSplitter.Close: Reset, then pool.Put
-    if (s->algo->pooled && algo_index(s->algo) >= 0) {
+    if (s->algo->pooled && algo_index(s->algo) >= 0 && !s->group) {
         Pool& p = g_pools[algo_index(s->algo)];
         std::lock_guard<std::mutex> lk(p.mu);
         p.free.push_back(s);
         return;
     }
     destroy(s);
+}
+
+// ============================================== grouped streaming handles
+// Many object writers run at once (snapshot/upload/upload.go:769-782), each calling
+// NextSplitPoint on its own splitter with a 64 KiB slice.  Alone, each call is one GPU
+// round trip.  A group gathers the calls of all its handles that arrive together into one
+// launch (one wave per call): writers copy "history ‖ slice" into the open pinned staging
+// buffer in parallel, the group thread seals it, ships it (H2D, kernel, D2H) while the
+// writers fill the other buffer, and hands every writer its answer.
+struct kcdc_group {
+    const Algo* algo = nullptr;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t max_batch = 0;
+    std::chrono::microseconds wait{0};
+    struct Buf {
+        uint8_t* h = nullptr;  // pinned staging
+        uint8_t* d = nullptr;
+        ScanReq* h_req = nullptr;
+        ScanReq* d_req = nullptr;
+        int64_t* h_out = nullptr;
+        int64_t* d_out = nullptr;
+        std::vector<int64_t*> result;  // each request's answer slot (the writer's stack)
+        size_t used = 0;
+        uint32_t n = 0, writing = 0;
+        uint64_t seq = 0;
+    };
+    static constexpr size_t kCap = size_t(32) << 20;  // staging bytes per buffer
+    Buf buf[2];
+    int open = 0;
+    uint64_t seq_next = 1, completed = 0;
+    int error = 0;
+    std::mutex mu;
+    std::condition_variable cv_work, cv_done;
+    bool stop = false;
+    std::thread th;
+};
+
+namespace {
+
+void group_release(kcdc_group* g) {
+    DeviceGuard dg(g->device);
+    for (auto& b : g->buf) {
+        if (b.h) (void)hipHostFree(b.h);
+        if (b.d) (void)hipFree(b.d);
+        if (b.h_req) (void)hipHostFree(b.h_req);
+        if (b.d_req) (void)hipFree(b.d_req);
+        if (b.h_out) (void)hipHostFree(b.h_out);
+        if (b.d_out) (void)hipFree(b.d_out);
+    }
+    if (g->stream) (void)hipStreamDestroy(g->stream);
+    delete g;
+}
+
+void group_loop(kcdc_group* g) {
+    (void)hipSetDevice(g->device);
+    std::unique_lock<std::mutex> lk(g->mu);
+    for (;;) {
+        g->cv_work.wait(lk, [&] { return g->stop || g->buf[g->open].n > 0; });
+        if (g->stop && g->buf[g->open].n == 0) return;
+        // let the writers that are arriving join this launch
+        const auto deadline = std::chrono::steady_clock::now() + g->wait;
+        g->cv_work.wait_until(lk, deadline, [&] { return g->stop || g->buf[g->open].n >= g->max_batch; });
+        kcdc_group::Buf& B = g->buf[g->open];
+        g->open ^= 1;  // later writers fill the other buffer (idle: launches complete in order)
+        g->buf[g->open].seq = g->seq_next++;
+        g->cv_work.wait(lk, [&] { return B.writing == 0; });
+        const uint32_t n = B.n;
+        const size_t used = B.used;
+        lk.unlock();
+        int rc = KCDC_OK;
+        hipError_t e = hipMemcpyAsync(B.d, B.h, used, hipMemcpyHostToDevice, g->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(B.d_req, B.h_req, n * sizeof(ScanReq), hipMemcpyHostToDevice, g->stream);
+        if (e == hipSuccess) {
+            rc = launch_scan_first_batch(*g->algo, B.d, B.d_req, n, B.d_out, g->device, g->stream);
+            if (rc == KCDC_OK) e = hipMemcpyAsync(B.h_out, B.d_out, n * sizeof(int64_t), hipMemcpyDeviceToHost, g->stream);
+        }
+        if (e == hipSuccess && rc == KCDC_OK) e = hipStreamSynchronize(g->stream);
+        if (e != hipSuccess && rc == KCDC_OK) rc = KCDC_EIO;
+        lk.lock();
+        for (uint32_t k = 0; k < n; k++) *B.result[k] = rc == KCDC_OK ? B.h_out[k] : rc;
+        B.n = 0;
+        B.used = 0;
+        g->completed = B.seq;
+        g->cv_done.notify_all();
+        g->cv_work.notify_all();  // writers waiting for room
+    }
+}
+
+int64_t group_first_candidate(kcdc_splitter* s, const uint8_t* b, size_t n) {
+    kcdc_group* g = s->group;
+    const size_t total = kWindow + n;
+    const size_t need = (total + 255) & ~size_t(255);
+    if (need > kcdc_group::kCap) return KCDC_EOVERFLOW;
+    int64_t result = KCDC_EIO;
+    std::unique_lock<std::mutex> lk(g->mu);
+    g->cv_work.wait(lk, [&] {
+        const kcdc_group::Buf& B = g->buf[g->open];
+        return B.n < g->max_batch && B.used + need <= kcdc_group::kCap;
+    });
+    kcdc_group::Buf& B = g->buf[g->open];
+    const uint32_t slot = B.n++;
+    const size_t off = B.used;
+    B.used += need;
+    B.writing++;
+    B.result[slot] = &result;
+    const uint64_t seq = B.seq;
+    lk.unlock();
+    std::memcpy(B.h + off, s->hist, kWindow);  // staged by the writer's own thread
+    std::memcpy(B.h + off + kWindow, b, n);
+    B.h_req[slot] = ScanReq{off, static_cast<int64_t>(total), kWindow, static_cast<int64_t>(total) - 1};
+    lk.lock();
+    B.writing--;
+    g->cv_work.notify_all();
+    g->cv_done.wait(lk, [&] { return g->completed >= seq; });
+    lk.unlock();
+    if (result < -1) return set_error(static_cast<int>(result), "grouped scan failed");
+    return result < 0 ? -1 : result - kWindow;
+}
+
+}  // namespace
+
+extern "C" kcdc_group* kcdc_group_new(const char* name, int device, uint32_t max_batch, uint32_t max_wait_us) {
+    const Algo* a = find_algo(name);
+    if (!a) {
+        set_error(KCDC_ENOENT, std::string("unknown splitter: ") + (name ? name : "(null)"));
+        return nullptr;
+    }
+    if (a->kind == kFixed) {
+        set_error(KCDC_EINVAL, "FIXED splitters read no data: use kcdc_splitter_new");
+        return nullptr;
+    }
+    if (check_device(device) != KCDC_OK) return nullptr;
+    DeviceGuard dg(device);
+    int err = 0;
+    if (!device_tables(device, &err)) return nullptr;
+    kcdc_group* g = new kcdc_group();
+    g->algo = a;
+    g->device = device;
+    g->max_batch = std::max<uint32_t>(1, std::min<uint32_t>(max_batch ? max_batch : 256, 4096));
+    g->wait = std::chrono::microseconds(max_wait_us);
+    bool ok = hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) == hipSuccess;
+    for (auto& b : g->buf) {
+        ok = ok && hipHostMalloc(&b.h, kcdc_group::kCap, hipHostMallocDefault) == hipSuccess &&
+             hipMalloc(&b.d, kcdc_group::kCap) == hipSuccess &&
+             hipHostMalloc(&b.h_req, g->max_batch * sizeof(ScanReq), hipHostMallocDefault) == hipSuccess &&
+             hipMalloc(&b.d_req, g->max_batch * sizeof(ScanReq)) == hipSuccess &&
+             hipHostMalloc(&b.h_out, g->max_batch * sizeof(int64_t), hipHostMallocDefault) == hipSuccess &&
+             hipMalloc(&b.d_out, g->max_batch * sizeof(int64_t)) == hipSuccess;
+        if (ok) b.result.resize(g->max_batch);
+    }
+    if (!ok) {
+        set_error(KCDC_ENOMEM, "failed to allocate splitter group resources");
+        group_release(g);
+        return nullptr;
+    }
+    g->buf[0].seq = g->seq_next++;
+    g->th = std::thread(group_loop, g);
+    return g;
+}
+
+extern "C" kcdc_splitter* kcdc_group_splitter(kcdc_group* g) {
+    if (!g) {
+        set_error(KCDC_EINVAL, "null group");
+        return nullptr;
+    }
+    DeviceGuard dg(g->device);
+    kcdc_splitter* s = new kcdc_splitter();
+    s->algo = g->algo;
+    s->device = g->device;
+    s->group = g;
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&s->d_out, sizeof(int64_t)) != hipSuccess ||
+        hipHostMalloc(&s->h_out, sizeof(int64_t), hipHostMallocDefault) != hipSuccess) {
+        set_error(KCDC_EIO, "failed to allocate splitter device resources");
+        destroy(s);
+        return nullptr;
+    }
+    return s;
+}
+
+extern "C" void kcdc_group_free(kcdc_group* g) {
+    if (!g) return;
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        g->stop = true;
+    }
+    g->cv_work.notify_all();
+    if (g->th.joinable()) g->th.join();
+    group_release(g);
 }
 
 // ==================================================================== batch

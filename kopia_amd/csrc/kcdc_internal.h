@@ -64,6 +64,13 @@ int launch_scan_first(const Algo& algo, const uint8_t* d_buf, uint64_t len, int6
                       int device, void* stream);
 int launch_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint32_t nstreams, uint64_t seed,
                      uint64_t first_sid, void* stream);
+// Grouped streaming handles: request r scans [lo, hi] of the `len` bytes at base + off.
+struct ScanReq {
+    uint64_t off;
+    int64_t len, lo, hi;
+};
+int launch_scan_first_batch(const Algo& algo, const uint8_t* d_base, const ScanReq* d_reqs, uint32_t n, int64_t* d_out,
+                            int device, void* stream);
 size_t long_workspace_bytes(const Algo& algo, uint64_t len);
 // Several long streams in one launch (segments of all streams scanned together, one
 // resolving wave per stream).

@@ -1742,6 +1742,24 @@ __global__ __launch_bounds__(kWave) void scan_first_kernel(BatchArgs a, const ui
     if (lane == 0) out[0] = f;
 }
 
+// Grouped streaming handles: one wave per request, request r = first candidate in [lo, hi]
+// of the buffer at base + off (256-byte aligned, `len` bytes, 64 bytes of history first).
+template <int KIND>
+__global__ __launch_bounds__(kWave) void scan_first_batch_kernel(BatchArgs a, const uint8_t* base,
+                                                                 const ScanReq* reqs, int64_t* out) {
+    __shared__ HashSmem<KIND> sm;
+    fill_tables<KIND>(sm, a);
+    const int lane = threadIdx.x & (kWave - 1);
+    const auto hash = make_hash<KIND>(sm, a, lane);
+    const ScanReq& r = reqs[blockIdx.x];
+    const uint64_t off = uni64(r.off);
+    const int64_t len = static_cast<int64_t>(uni64(static_cast<uint64_t>(r.len)));
+    const int64_t lo = static_cast<int64_t>(uni64(static_cast<uint64_t>(r.lo)));
+    const int64_t hi = static_cast<int64_t>(uni64(static_cast<uint64_t>(r.hi)));
+    const int64_t f = scan_region(hash, base + off, 0, len, lo, hi, lane);
+    if (lane == 0) out[blockIdx.x] = f;
+}
+
 // ------------------------------------------------------ synthetic streams
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -2391,6 +2409,26 @@ int launch_scan_first(const Algo& algo, const uint8_t* d_buf, uint64_t len, int6
     else if (algo.kind == kRabinKarp)
         hipLaunchKernelGGL(dev::scan_first_kernel<kRabinKarp>, dim3(1), dim3(dev::kWave), 0, st, a, d_buf,
                            static_cast<int64_t>(len), lo, hi, d_out);
+    else
+        return set_error(-22, "scan_first: FIXED splitters read no data");
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : hip_fail(e, "scan kernel launch");
+}
+
+int launch_scan_first_batch(const Algo& algo, const uint8_t* d_base, const ScanReq* d_reqs, uint32_t n, int64_t* d_out,
+                            int device, void* stream) {
+    int err = 0;
+    const DeviceTables* t = device_tables(device, &err);
+    if (!t) return err;
+    if (n == 0) return 0;
+    dev::BatchArgs a = base_args(algo, *t);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (algo.kind == kBuzhash)
+        hipLaunchKernelGGL(dev::scan_first_batch_kernel<kBuzhash>, dim3(n), dim3(dev::kWave), 0, st, a, d_base, d_reqs,
+                           d_out);
+    else if (algo.kind == kRabinKarp)
+        hipLaunchKernelGGL(dev::scan_first_batch_kernel<kRabinKarp>, dim3(n), dim3(dev::kWave), 0, st, a, d_base,
+                           d_reqs, d_out);
     else
         return set_error(-22, "scan_first: FIXED splitters read no data");
     const hipError_t e = hipGetLastError();

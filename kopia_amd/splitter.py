@@ -96,6 +96,34 @@ class Splitter:
             pass
 
 
+class SplitterGroup:
+    """kcdc_group: handles for concurrent object writers whose GPU scans share launches
+    (one wave per pending NextSplitPoint call).  Each handle is used by one thread at a
+    time, like any Splitter; different handles may be called from different threads."""
+
+    def __init__(self, name: str, device: int = 0, max_batch: int = 0, max_wait_us: int = 0):
+        g = _lib.lib().kcdc_group_new(name.encode(), device, max_batch, max_wait_us)
+        if not g:
+            raise _lib.KcdcError(_lib.KCDC_EINVAL, _lib.last_error())
+        self._g = g
+        self.name = name
+
+    def splitter(self) -> Splitter:
+        h = _lib.lib().kcdc_group_splitter(self._g)
+        if not h:
+            raise _lib.KcdcError(_lib.KCDC_EINVAL, _lib.last_error())
+        s = Splitter.__new__(Splitter)
+        s._h = h
+        s.name = self.name
+        return s
+
+    def close(self) -> None:
+        """Free the group (close its splitters first)."""
+        if self._g:
+            _lib.lib().kcdc_group_free(self._g)
+            self._g = None
+
+
 Factory = Callable[[], Splitter]
 
 

@@ -114,3 +114,14 @@ def test_fixed_streaming_handle_needs_no_device():
     assert s.NextSplitPoint(data[:100000]) == -1
     assert s.NextSplitPoint(data[100000:]) == (128 << 10) - 100000
     s.Close()
+
+
+def test_group_needs_device_and_rolling_name():
+    """kcdc_group_new: unknown names and FIXED are refused; without a gfx950 device it fails
+    loudly (no CPU fallback)."""
+    L = _lib.lib()
+    assert not L.kcdc_group_new(b"NO-SUCH-SPLITTER", 0, 0, 0)
+    assert not L.kcdc_group_new(b"FIXED-4M", 0, 0, 0)
+    if L.kcdc_device_count() == 0:
+        with pytest.raises(_lib.KcdcError):
+            ks.SplitterGroup("DYNAMIC-4M-BUZHASH")
