@@ -1823,6 +1823,12 @@ struct LongArgs {
     uint64_t* seg_off;   // exclusive prefix of stored counts
     uint64_t* list;      // compacted candidates (kTruncBit marks the last stored of a truncated segment)
     uint64_t* total;     // [1] number of list entries
+    // parallel resolver (resolve_par_kernel); serial == nullptr: every stream resolves serially
+    uint32_t* serial;    // [nstreams] 1: this stream needs the serial resolver
+    uint32_t* jump;      // [levels][node_cap] successor tables, node k of stream j at lbeg + 2j + k
+    uint32_t* forced;    // [node_cap] non-candidate cuts between a node's cut and its successor's
+    uint64_t node_cap;
+    uint32_t levels;
 };
 
 // The stream owning global segment `seg`: the last j with seg0 <= seg (wave-uniform).
@@ -2084,6 +2090,7 @@ constexpr int kResolveWin = 4096;  // candidate-list entries staged in LDS
 // One wave per stream (blockIdx.x): walks the chunk rule over the stream's candidate list.
 template <int KIND>
 __global__ __launch_bounds__(kWave) void resolve_kernel(BatchArgs a, LongArgs g, int64_t mn, int64_t mx) {
+    if (g.serial && g.serial[blockIdx.x] == 0) return;  // resolved by resolve_par_kernel
     __shared__ HashSmem<KIND> sm;
     __shared__ uint64_t win[kResolveWin];
     fill_tables<KIND>(sm, a);
@@ -2169,6 +2176,148 @@ __global__ __launch_bounds__(kWave) void resolve_kernel(BatchArgs a, LongArgs g,
         s = next;
     }
     if (lane == 0) S.count[0] = cnt;
+}
+
+// Parallel chunk resolution of one stream per workgroup (1024 threads), for streams whose
+// candidate list is complete (no truncated segment) and fits the node tables.  Nodes: the
+// list entries 0..M-1 ("a chunk ends after p_k"), START = M (the stream start) and END.
+//  A. succ(k): the node whose candidate ends the chunk after node k's cut, walking the
+//     chunk rule from s = p_k + 1 (forced cuts at max size / the stream end in between are
+//     counted in forced[k]; they are arithmetic in s).  Candidates are sorted: binary search.
+//  B. jump tables: jump_t(k) = succ^(2^t)(k).
+//  C. the chain START -> ... -> END: node d of the chain by binary lifting on d, its cut
+//     index by a block prefix sum of (1 + forced), then every node writes its own cuts.
+// The cut list equals the serial walk's (resolve_kernel) cut for cut.
+__device__ __forceinline__ uint32_t lower_bound_pos(const uint64_t* list, uint32_t m, int64_t v) {
+    uint32_t lo = 0, hi = m;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (static_cast<int64_t>(list[mid]) < v) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(1024) void resolve_par_kernel(LongArgs g, int64_t mn, int64_t mx) {
+    __shared__ uint32_t s_flag;
+    __shared__ uint64_t s_wsum[16];
+    __shared__ uint64_t s_carry;
+    __shared__ uint64_t s_depth;
+    const uint32_t j = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const LongStream& S = g.streams[j];
+    const int64_t n = S.n;
+    const int64_t seg0 = S.seg0;
+    const int64_t lbeg = seg0 < g.nseg ? static_cast<int64_t>(g.seg_off[seg0]) : 0;
+    const int64_t lend = j + 1 < g.nstreams && static_cast<uint64_t>(g.streams[j + 1].seg0) < static_cast<uint64_t>(g.nseg)
+                             ? static_cast<int64_t>(g.seg_off[g.streams[j + 1].seg0])
+                             : static_cast<int64_t>(g.total[0]);
+    const uint32_t M = n > 0 ? static_cast<uint32_t>(lend - lbeg) : 0u;
+    const uint64_t nb = static_cast<uint64_t>(lbeg) + 2ull * j;  // this stream's node base
+    const uint64_t* list = g.list + lbeg;
+    if (tid == 0) s_flag = nb + M + 2 > g.node_cap ? 1u : 0u;
+    __syncthreads();
+    for (uint32_t k = tid; k < M && !s_flag; k += 1024)
+        if (list[k] & kTruncBit) s_flag = 1u;  // benign race: any writer stores 1
+    __syncthreads();
+    if (s_flag) {
+        if (tid == 0) g.serial[j] = 1u;
+        return;
+    }
+    if (tid == 0) g.serial[j] = 0u;
+    const uint32_t START = M, END = M + 1;
+    uint32_t* J0 = g.jump + nb;
+    uint32_t* F = g.forced + nb;
+    for (uint32_t k = tid; k <= END; k += 1024) {  // A
+        uint32_t sc = END, f = 0;
+        if (k != END) {
+            int64_t s = k == START ? 0 : static_cast<int64_t>(list[k]) + 1;
+            while (s < n) {
+                const int64_t lo = s + mn - 1;
+                if (lo >= n) {  // the last chunk [s, n)
+                    f++;
+                    break;
+                }
+                const int64_t hi = s + mx - 1 < n - 1 ? s + mx - 1 : n - 1;
+                const uint32_t q = lower_bound_pos(list, M, lo);
+                if (q < M && static_cast<int64_t>(list[q]) <= hi) {
+                    sc = q;
+                    break;
+                }
+                f++;  // forced cut at s + mx, or at the stream end
+                if (s + mx - 1 <= n - 1) s += mx;
+                else break;
+            }
+        }
+        J0[k] = sc;
+        F[k] = f;
+    }
+    __syncthreads();
+    const uint64_t stride = g.node_cap;
+    for (uint32_t t = 1; t < g.levels; t++) {  // B
+        const uint32_t* Jp = g.jump + (t - 1) * stride + nb;
+        uint32_t* Jt = g.jump + t * stride + nb;
+        for (uint32_t k = tid; k <= END; k += 1024) Jt[k] = Jp[Jp[k]];
+        __syncthreads();
+    }
+    if (tid == 0) {  // chain length: START's depth (number of candidate nodes on the chain)
+        uint32_t cur = START;
+        uint64_t d = 0;
+        for (int t = static_cast<int>(g.levels) - 1; t >= 0; t--) {
+            const uint32_t nx = g.jump[static_cast<uint64_t>(t) * stride + nb + cur];
+            if (nx != END) {
+                cur = nx;
+                d += 1ull << t;
+            }
+        }
+        s_depth = d;
+        s_carry = 0;
+    }
+    __syncthreads();
+    const uint64_t D = s_depth;  // chain nodes d = 0 (START) .. D
+    uint64_t* const cuts = S.cuts;
+    const uint64_t cap = S.cuts_cap;
+    for (uint64_t base = 0; base <= D; base += 1024) {  // C
+        const uint64_t d = base + static_cast<uint64_t>(tid);
+        const bool valid = d <= D;
+        uint32_t node = START;
+        if (valid)
+            for (uint32_t t = 0; t < g.levels; t++)
+                if ((d >> t) & 1) node = g.jump[static_cast<uint64_t>(t) * stride + nb + node];
+        const uint64_t wgt = valid ? F[node] + (d > 0 ? 1u : 0u) : 0u;
+        uint64_t incl = wgt;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t v = __shfl_up(incl, o);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) s_wsum[w] = incl;
+        __syncthreads();
+        uint64_t pre = s_carry;
+        for (int k = 0; k < w; k++) pre += s_wsum[k];
+        uint64_t idx = pre + incl - wgt;
+        if (valid) {
+            int64_t s = 0;
+            if (d > 0) {
+                s = static_cast<int64_t>(list[node]) + 1;
+                if (idx < cap) cuts[idx] = static_cast<uint64_t>(s);
+                idx++;
+            }
+            for (uint32_t r = 0; r < F[node]; r++) {
+                const int64_t next = s + mn - 1 >= n ? n : (s + mx - 1 <= n - 1 ? s + mx : n);
+                if (idx < cap) cuts[idx] = static_cast<uint64_t>(next);
+                idx++;
+                s = next;
+            }
+        }
+        __syncthreads();
+        if (tid == 1023) {
+            uint64_t tot = s_carry;
+            for (int k = 0; k < 16; k++) tot += s_wsum[k];
+            s_carry = tot;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) S.count[0] = s_carry;
 }
 
 }  // namespace dev
@@ -2447,9 +2596,15 @@ int launch_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint
 }
 
 namespace {
+#ifndef KCDC_PAR_RESOLVE
+#define KCDC_PAR_RESOLVE 1  // resolve_par_kernel for streams with complete candidate lists
+#endif
+constexpr uint64_t kParNodeCap = uint64_t(1) << 22;  // parallel-resolver nodes per launch
 struct LongLayout {
     int64_t nseg;
-    size_t off_streams, off_cnt, off_cand, off_off, off_list, off_total, bytes;
+    uint64_t node_cap;
+    uint32_t levels;
+    size_t off_streams, off_cnt, off_cand, off_off, off_list, off_total, off_serial, off_forced, off_jump, bytes;
 };
 int64_t long_nseg(uint64_t len, uint64_t off0) {  // segments tile coordinates (position + off0)
     return len ? static_cast<int64_t>((len + off0 + dev::kSegBytes - 1) / dev::kSegBytes) : 0;
@@ -2472,6 +2627,20 @@ LongLayout long_layout(int64_t nseg, uint32_t nstreams) {
     o += al(ns * dev::kSegK * 8);
     L.off_total = o;
     o += 256;
+    L.node_cap = 0;
+    L.levels = 0;
+    L.off_serial = L.off_forced = L.off_jump = o;
+    if (KCDC_PAR_RESOLVE) {
+        L.node_cap = std::min<uint64_t>(static_cast<uint64_t>(ns) * dev::kSegK + 2ull * nstreams, kParNodeCap);
+        L.levels = 1;
+        while ((uint64_t(1) << L.levels) <= L.node_cap) L.levels++;
+        L.off_serial = o;
+        o += al(nstreams * 4);
+        L.off_forced = o;
+        o += al(L.node_cap * 4);
+        L.off_jump = o;
+        o += al(static_cast<size_t>(L.levels) * L.node_cap * 4);
+    }
     L.bytes = o;
     return L;
 }
@@ -2525,6 +2694,13 @@ int launch_split_long_multi(const Algo& algo, uint32_t m, const uint8_t* const* 
     g.seg_off = reinterpret_cast<uint64_t*>(w + L.off_off);
     g.list = reinterpret_cast<uint64_t*>(w + L.off_list);
     g.total = reinterpret_cast<uint64_t*>(w + L.off_total);
+    if (KCDC_PAR_RESOLVE) {
+        g.serial = reinterpret_cast<uint32_t*>(w + L.off_serial);
+        g.forced = reinterpret_cast<uint32_t*>(w + L.off_forced);
+        g.jump = reinterpret_cast<uint32_t*>(w + L.off_jump);
+        g.node_cap = L.node_cap;
+        g.levels = L.levels;
+    }
     hipError_t e = hipMemcpyAsync(w + L.off_streams, hs.data(), m * sizeof(dev::LongStream), hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return hip_fail(e, "long-stream descriptors");
     dev::BatchArgs a = base_args(algo, *t);
@@ -2546,6 +2722,13 @@ int launch_split_long_multi(const Algo& algo, uint32_t m, const uint8_t* const* 
         }
         hipLaunchKernelGGL(dev::seg_prefix_kernel, dim3(1), dim3(1024), 0, st, g);
         hipLaunchKernelGGL(dev::compact_kernel, dim3(static_cast<unsigned>((nseg + 255) / 256)), dim3(256), 0, st, g);
+    }
+    if (g.serial) {  // streams it cannot take (truncated segments) stay flagged for resolve_kernel
+        if (nseg == 0) {
+            e = hipMemsetAsync(w + L.off_total, 0, sizeof(uint64_t), st);
+            if (e != hipSuccess) return hip_fail(e, "long-stream total");
+        }
+        hipLaunchKernelGGL(dev::resolve_par_kernel, dim3(m), dim3(1024), 0, st, g, mn, mx);
     }
     if (algo.kind == kBuzhash)
         hipLaunchKernelGGL(dev::resolve_kernel<kBuzhash>, dim3(m), dim3(dev::kWave), 0, st, a, g, mn, mx);
