@@ -1799,7 +1799,7 @@ constexpr int64_t kSegBytes = kWave * kLaneMax;  // 128 KiB
 #ifndef KCDC_LONG_DMA
 #define KCDC_LONG_DMA 1  // buzhash candidate scan: cand_scan_dma_kernel (0: cand_scan_kernel)
 #endif
-constexpr int kSegK = 4;
+constexpr int kSegK = 8;
 constexpr uint64_t kTruncBit = 1ull << 63;
 
 // One stream of a long-path launch (several streams share one launch: their segments are
