@@ -802,6 +802,9 @@ __global__ __launch_bounds__(kBatchWaves * kWave, kBatchWaves / 4) void split_ba
 #define KCDC_DMA_WAVES 8
 #endif
 constexpr int kDmaWaves = KCDC_DMA_WAVES;  // waves per workgroup (one workgroup per CU)
+#ifndef KCDC_STEP_PRIO
+#define KCDC_STEP_PRIO 0  // raise the wave priority from the step's slot read to its refill DMA
+#endif
 #ifndef KCDC_DMA_AUX
 #define KCDC_DMA_AUX 2  // nt: once-read stream bytes (membench: 128-B runs 6.65 vs 6.38 TB/s)
 #endif
@@ -1482,6 +1485,9 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             uint32_t dw[32];
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if KCDC_STEP_PRIO
+            __builtin_amdgcn_s_setprio(3);  // win the SIMD for the slot read + refill
+#endif
             read_step128(sl, lane, c, cur.off0, dw);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot free: refill it
             __builtin_amdgcn_sched_barrier(0);
@@ -1503,6 +1509,9 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                     next_issued = true;
                 }
             }
+#if KCDC_STEP_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
             __builtin_amdgcn_sched_barrier(0);
 #ifdef KCDC_EXP_MEMONLY
             uint32_t m = 0;
