@@ -33,6 +33,11 @@ clean:
 	rm -rf build $(LIB)
 	$(MAKE) -s -C oracle clean
 
+# C ABI driver: concurrent writers through grouped vs private streaming handles
+build/group_bench: tools/group_bench.cpp include/kcdc.h $(LIB)
+	@mkdir -p build
+	g++ -O2 -std=c++17 -pthread -Iinclude $< -Lkopia_amd -lkcdc -Wl,-rpath,'$$ORIGIN/../kopia_amd' -o $@
+
 .PHONY: all oracle clean asm
 
 # ---- experiment builds (A/B of compile-time tunables; not used by the product)
