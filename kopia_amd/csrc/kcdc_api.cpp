@@ -182,6 +182,7 @@ int ensure_stage(kcdc_splitter* s, size_t need) {
 }
 
 int64_t group_first_candidate(kcdc_splitter* s, const uint8_t* b, size_t n);
+void group_handle_closed(kcdc_group* g);
 
 // First candidate index in slice b[0..n) given the 64-byte history, on the GPU.
 int64_t gpu_first_candidate(kcdc_splitter* s, const uint8_t* b, size_t n) {
@@ -305,7 +306,12 @@ extern "C" void kcdc_splitter_reset(kcdc_splitter* s) {
 extern "C" void kcdc_splitter_close(kcdc_splitter* s) {
     if (!s) return;
     kcdc_splitter_reset(s);  // recyclableSplitter.Close: Reset, then pool.Put
-    if (s->algo->pooled && algo_index(s->algo) >= 0 && !s->group) {
+    if (s->group) {  // grouped handles are never pooled
+        group_handle_closed(s->group);
+        destroy(s);
+        return;
+    }
+    if (s->algo->pooled && algo_index(s->algo) >= 0) {
         Pool& p = g_pools[algo_index(s->algo)];
         std::lock_guard<std::mutex> lk(p.mu);
         p.free.push_back(s);
@@ -321,6 +327,9 @@ extern "C" void kcdc_splitter_close(kcdc_splitter* s) {
 // launch (one wave per call): writers copy "history ‖ slice" into the open pinned staging
 // buffer in parallel, the group thread seals it, ships it (H2D, kernel, D2H) while the
 // writers fill the other buffer, and hands every writer its answer.
+#ifndef KCDC_GROUP_ZC
+#define KCDC_GROUP_ZC 1  // the scan reads the pinned staging in place (mapped), answers land in host memory
+#endif
 struct kcdc_group {
     const Algo* algo = nullptr;
     int device = 0;
@@ -329,7 +338,7 @@ struct kcdc_group {
     std::chrono::microseconds wait{0};
     struct Buf {
         uint8_t* h = nullptr;  // pinned staging
-        uint8_t* d = nullptr;
+        uint8_t* d = nullptr;  // its device copy, or (KCDC_GROUP_ZC) its device mapping
         ScanReq* h_req = nullptr;
         ScanReq* d_req = nullptr;
         int64_t* h_out = nullptr;
@@ -343,6 +352,7 @@ struct kcdc_group {
     Buf buf[2];
     int open = 0;
     uint64_t seq_next = 1, completed = 0;
+    uint32_t live = 0;  // open handles: a launch is sealed at once when every one of them waits
     int error = 0;
     std::mutex mu;
     std::condition_variable cv_work, cv_done;
@@ -356,11 +366,13 @@ void group_release(kcdc_group* g) {
     DeviceGuard dg(g->device);
     for (auto& b : g->buf) {
         if (b.h) (void)hipHostFree(b.h);
-        if (b.d) (void)hipFree(b.d);
         if (b.h_req) (void)hipHostFree(b.h_req);
-        if (b.d_req) (void)hipFree(b.d_req);
         if (b.h_out) (void)hipHostFree(b.h_out);
-        if (b.d_out) (void)hipFree(b.d_out);
+        if (!KCDC_GROUP_ZC) {  // device copies (zero-copy: mappings of the host buffers)
+            if (b.d) (void)hipFree(b.d);
+            if (b.d_req) (void)hipFree(b.d_req);
+            if (b.d_out) (void)hipFree(b.d_out);
+        }
     }
     if (g->stream) (void)hipStreamDestroy(g->stream);
     delete g;
@@ -374,7 +386,10 @@ void group_loop(kcdc_group* g) {
         if (g->stop && g->buf[g->open].n == 0) return;
         // let the writers that are arriving join this launch
         const auto deadline = std::chrono::steady_clock::now() + g->wait;
-        g->cv_work.wait_until(lk, deadline, [&] { return g->stop || g->buf[g->open].n >= g->max_batch; });
+        g->cv_work.wait_until(lk, deadline, [&] {
+            const uint32_t n = g->buf[g->open].n;
+            return g->stop || n >= g->max_batch || n >= g->live;
+        });
         kcdc_group::Buf& B = g->buf[g->open];
         g->open ^= 1;  // later writers fill the other buffer (idle: launches complete in order)
         g->buf[g->open].seq = g->seq_next++;
@@ -383,11 +398,18 @@ void group_loop(kcdc_group* g) {
         const size_t used = B.used;
         lk.unlock();
         int rc = KCDC_OK;
-        hipError_t e = hipMemcpyAsync(B.d, B.h, used, hipMemcpyHostToDevice, g->stream);
-        if (e == hipSuccess) e = hipMemcpyAsync(B.d_req, B.h_req, n * sizeof(ScanReq), hipMemcpyHostToDevice, g->stream);
-        if (e == hipSuccess) {
+        hipError_t e = hipSuccess;
+        if (KCDC_GROUP_ZC) {  // the kernel reads the staging and writes the answers over PCIe
             rc = launch_scan_first_batch(*g->algo, B.d, B.d_req, n, B.d_out, g->device, g->stream);
-            if (rc == KCDC_OK) e = hipMemcpyAsync(B.h_out, B.d_out, n * sizeof(int64_t), hipMemcpyDeviceToHost, g->stream);
+        } else {
+            e = hipMemcpyAsync(B.d, B.h, used, hipMemcpyHostToDevice, g->stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(B.d_req, B.h_req, n * sizeof(ScanReq), hipMemcpyHostToDevice, g->stream);
+            if (e == hipSuccess) {
+                rc = launch_scan_first_batch(*g->algo, B.d, B.d_req, n, B.d_out, g->device, g->stream);
+                if (rc == KCDC_OK)
+                    e = hipMemcpyAsync(B.h_out, B.d_out, n * sizeof(int64_t), hipMemcpyDeviceToHost, g->stream);
+            }
         }
         if (e == hipSuccess && rc == KCDC_OK) e = hipStreamSynchronize(g->stream);
         if (e != hipSuccess && rc == KCDC_OK) rc = KCDC_EIO;
@@ -399,6 +421,14 @@ void group_loop(kcdc_group* g) {
         g->cv_done.notify_all();
         g->cv_work.notify_all();  // writers waiting for room
     }
+}
+
+void group_handle_closed(kcdc_group* g) {
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        g->live--;
+    }
+    g->cv_work.notify_all();  // a pending launch may now hold every live handle
 }
 
 int64_t group_first_candidate(kcdc_splitter* s, const uint8_t* b, size_t n) {
@@ -454,13 +484,24 @@ extern "C" kcdc_group* kcdc_group_new(const char* name, int device, uint32_t max
     g->max_batch = std::max<uint32_t>(1, std::min<uint32_t>(max_batch ? max_batch : 256, 4096));
     g->wait = std::chrono::microseconds(max_wait_us);
     bool ok = hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) == hipSuccess;
+    const unsigned hflags = KCDC_GROUP_ZC ? hipHostMallocMapped : hipHostMallocDefault;
     for (auto& b : g->buf) {
-        ok = ok && hipHostMalloc(&b.h, kcdc_group::kCap, hipHostMallocDefault) == hipSuccess &&
-             hipMalloc(&b.d, kcdc_group::kCap) == hipSuccess &&
-             hipHostMalloc(&b.h_req, g->max_batch * sizeof(ScanReq), hipHostMallocDefault) == hipSuccess &&
-             hipMalloc(&b.d_req, g->max_batch * sizeof(ScanReq)) == hipSuccess &&
-             hipHostMalloc(&b.h_out, g->max_batch * sizeof(int64_t), hipHostMallocDefault) == hipSuccess &&
-             hipMalloc(&b.d_out, g->max_batch * sizeof(int64_t)) == hipSuccess;
+        ok = ok && hipHostMalloc(&b.h, kcdc_group::kCap, hflags) == hipSuccess &&
+             hipHostMalloc(&b.h_req, g->max_batch * sizeof(ScanReq), hflags) == hipSuccess &&
+             hipHostMalloc(&b.h_out, g->max_batch * sizeof(int64_t), hflags) == hipSuccess;
+        if (ok && KCDC_GROUP_ZC) {
+            void *pd = nullptr, *pr = nullptr, *po = nullptr;
+            ok = hipHostGetDevicePointer(&pd, b.h, 0) == hipSuccess &&
+                 hipHostGetDevicePointer(&pr, b.h_req, 0) == hipSuccess &&
+                 hipHostGetDevicePointer(&po, b.h_out, 0) == hipSuccess;
+            b.d = static_cast<uint8_t*>(pd);
+            b.d_req = static_cast<ScanReq*>(pr);
+            b.d_out = static_cast<int64_t*>(po);
+        } else if (ok) {
+            ok = hipMalloc(&b.d, kcdc_group::kCap) == hipSuccess &&
+                 hipMalloc(&b.d_req, g->max_batch * sizeof(ScanReq)) == hipSuccess &&
+                 hipMalloc(&b.d_out, g->max_batch * sizeof(int64_t)) == hipSuccess;
+        }
         if (ok) b.result.resize(g->max_batch);
     }
     if (!ok) {
@@ -482,7 +523,6 @@ extern "C" kcdc_splitter* kcdc_group_splitter(kcdc_group* g) {
     kcdc_splitter* s = new kcdc_splitter();
     s->algo = g->algo;
     s->device = g->device;
-    s->group = g;
     if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&s->d_out, sizeof(int64_t)) != hipSuccess ||
         hipHostMalloc(&s->h_out, sizeof(int64_t), hipHostMallocDefault) != hipSuccess) {
@@ -490,6 +530,9 @@ extern "C" kcdc_splitter* kcdc_group_splitter(kcdc_group* g) {
         destroy(s);
         return nullptr;
     }
+    std::lock_guard<std::mutex> lk(g->mu);
+    s->group = g;
+    g->live++;
     return s;
 }
 
