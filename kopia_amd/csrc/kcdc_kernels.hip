@@ -2608,7 +2608,7 @@ namespace {
 #ifndef KCDC_PAR_RESOLVE
 #define KCDC_PAR_RESOLVE 1  // resolve_par_kernel for streams with complete candidate lists
 #endif
-constexpr uint64_t kParNodeCap = uint64_t(1) << 22;  // parallel-resolver nodes per launch
+constexpr uint64_t kParNodeCap = uint64_t(1) << 20;  // parallel-resolver nodes per launch (<= 88 MB of tables)
 struct LongLayout {
     int64_t nseg;
     uint64_t node_cap;
