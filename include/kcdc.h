@@ -142,7 +142,8 @@ int kcdc_split_batch_device(const char* name, const uint8_t* const* d_ptrs, cons
 
 /* _host: host buffers in, host cut lists out.  Streams are copied H2D in groups
  * of <= 1 GiB (the HIP runtime stages pageable memory; buffers the caller
- * allocated pinned are DMA'd directly), split by one launch per group, and the
+ * allocated pinned are DMA'd directly), each group split like
+ * kcdc_split_files_device (large streams through the long-stream path), and the
  * cut lists copied back.  Synchronous, PCIe-bound.  This is the
  * path the Go cgo shim calls. */
 int kcdc_split_batch_host(const char* name, const uint8_t* const* h_ptrs, const uint64_t* lens, uint32_t nstreams,

@@ -615,7 +615,7 @@ extern "C" int kcdc_split_batch_host(const char* name, const uint8_t* const* h_p
         uint64_t gcap = (i1 < nstreams ? cut_base[i1] : cuts_cap) - cut_base[i0];
         rc = grow(reinterpret_cast<void**>(&C.d_data), &C.d_data_cap, std::max<size_t>(bytes, 256));
         if (rc) return rc;
-        const size_t meta = ng * (sizeof(void*) + 3 * sizeof(uint64_t)) + gcap * sizeof(uint64_t) + 64;
+        const size_t meta = ng * sizeof(uint64_t) + gcap * sizeof(uint64_t) + 64;
         rc = grow(&C.d_meta, &C.d_meta_cap, meta);
         if (rc) return rc;
         std::vector<const uint8_t*> dptr(ng);
@@ -629,17 +629,10 @@ extern "C" int kcdc_split_batch_host(const char* name, const uint8_t* const* h_p
                         "H2D stream");
             off += (lens[i0 + k] + 255) & ~size_t(255);
         }
-        char* m = static_cast<char*>(C.d_meta);
-        auto* d_ptrs = reinterpret_cast<const uint8_t**>(m);
-        auto* d_lens = reinterpret_cast<uint64_t*>(m + ng * sizeof(void*));
-        auto* d_base = d_lens + ng;
-        auto* d_cnt = d_base + ng;
+        auto* d_cnt = static_cast<uint64_t*>(C.d_meta);
         auto* d_cuts = d_cnt + ng;
-        HIP_TRY(hipMemcpyAsync(d_ptrs, dptr.data(), ng * sizeof(void*), hipMemcpyHostToDevice, C.stream), "H2D meta");
-        HIP_TRY(hipMemcpyAsync(d_lens, lens + i0, ng * sizeof(uint64_t), hipMemcpyHostToDevice, C.stream), "H2D meta");
-        HIP_TRY(hipMemcpyAsync(d_base, base.data(), ng * sizeof(uint64_t), hipMemcpyHostToDevice, C.stream), "H2D meta");
-        SplitArgs s{d_ptrs, d_lens, ng, d_cuts, gcap, d_base, d_cnt};
-        rc = launch_split_batch(*a, s, device, C.stream);
+        // each stream through the batch kernel or, if it would be the batch's tail, the long path
+        rc = kcdc_split_files_device(name, dptr.data(), lens + i0, ng, d_cuts, gcap, base.data(), d_cnt, C.stream);
         if (rc) return rc;
         HIP_TRY(hipMemcpyAsync(counts + i0, d_cnt, ng * sizeof(uint64_t), hipMemcpyDeviceToHost, C.stream), "D2H");
         if (gcap)

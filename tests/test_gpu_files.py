@@ -75,3 +75,15 @@ def test_benchmark_splitter_stats_match_golden(key):
         got = {k: r[k] for k in want}
         assert got == want, r["splitter"]
         assert r["bytes_per_second"] > 0
+
+
+def test_host_batch_routes_large_streams():
+    """kcdc_split_batch_host goes through the same router: a 100 MiB stream next to small ones
+    (the long path) and a batch of mid-size ones, all equal to the oracle."""
+    name = "DYNAMIC-1M-BUZHASH"
+    sizes = [100 << 20, 1024, 3 << 20, 0, 5 << 20 | 3]
+    streams = [coracle.gen_stream(SEED, 700 + i, L) for i, L in enumerate(sizes)]
+    got = batch.split_batch_host(name, streams)
+    want = coracle.split_batch(name, streams, nthreads=8)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert np.array_equal(g, np.asarray(w, dtype=np.int64)), (i, sizes[i])
