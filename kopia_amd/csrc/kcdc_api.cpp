@@ -137,6 +137,10 @@ struct kcdc_splitter {
     kcdc_group* group = nullptr;  // set: GPU scans are batched with the group's other handles
 };
 
+#ifndef KCDC_HANDLE_ZC
+#define KCDC_HANDLE_ZC 1  // private handles: the scan reads the pinned staging in place (mapped)
+#endif
+
 namespace {
 
 struct Pool {
@@ -157,12 +161,26 @@ void push_hist(kcdc_splitter* s, const uint8_t* b, size_t n) {
 void destroy(kcdc_splitter* s) {
     if (!s) return;
     DeviceGuard g(s->device);
-    if (s->d_stage) (void)hipFree(s->d_stage);
+    if (s->d_stage && !KCDC_HANDLE_ZC) (void)hipFree(s->d_stage);  // zero-copy: a mapping of h_stage
     if (s->h_stage) (void)hipHostFree(s->h_stage);
-    if (s->d_out) (void)hipFree(s->d_out);
+    if (s->d_out && !KCDC_HANDLE_ZC) (void)hipFree(s->d_out);
     if (s->h_out) (void)hipHostFree(s->h_out);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
+}
+
+// The one-word answer of a private scan (zero-copy: written by the kernel into mapped host memory).
+hipError_t alloc_out(kcdc_splitter* s) {
+    if (KCDC_HANDLE_ZC) {
+        hipError_t e = hipHostMalloc(&s->h_out, sizeof(int64_t), hipHostMallocMapped);
+        void* pd = nullptr;
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&pd, s->h_out, 0);
+        s->d_out = static_cast<int64_t*>(pd);
+        return e;
+    }
+    hipError_t e = hipMalloc(&s->d_out, sizeof(int64_t));
+    if (e == hipSuccess) e = hipHostMalloc(&s->h_out, sizeof(int64_t), hipHostMallocDefault);
+    return e;
 }
 
 int ensure_stage(kcdc_splitter* s, size_t need) {
@@ -170,13 +188,20 @@ int ensure_stage(kcdc_splitter* s, size_t need) {
     size_t cap = std::max<size_t>(need, 1 << 20);
     cap = std::min<size_t>(std::max(cap, s->stage_cap * 2), s->algo->max_size() + 2 * kWindow);
     cap = std::max(cap, need);
-    if (s->d_stage) (void)hipFree(s->d_stage);
+    if (s->d_stage && !KCDC_HANDLE_ZC) (void)hipFree(s->d_stage);
     if (s->h_stage) (void)hipHostFree(s->h_stage);
     s->d_stage = nullptr;
     s->h_stage = nullptr;
     s->stage_cap = 0;
-    HIP_TRY(hipMalloc(&s->d_stage, cap), "hipMalloc stage");
-    HIP_TRY(hipHostMalloc(&s->h_stage, cap, hipHostMallocDefault), "hipHostMalloc stage");
+    if (KCDC_HANDLE_ZC) {
+        HIP_TRY(hipHostMalloc(&s->h_stage, cap, hipHostMallocMapped), "hipHostMalloc stage");
+        void* pd = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(&pd, s->h_stage, 0), "stage mapping");
+        s->d_stage = static_cast<uint8_t*>(pd);
+    } else {
+        HIP_TRY(hipMalloc(&s->d_stage, cap), "hipMalloc stage");
+        HIP_TRY(hipHostMalloc(&s->h_stage, cap, hipHostMallocDefault), "hipHostMalloc stage");
+    }
     s->stage_cap = cap;
     return KCDC_OK;
 }
@@ -195,11 +220,13 @@ int64_t gpu_first_candidate(kcdc_splitter* s, const uint8_t* b, size_t n) {
     if (rc) return rc;
     std::memcpy(s->h_stage, s->hist, kWindow);
     std::memcpy(s->h_stage + kWindow, b, n);
-    HIP_TRY(hipMemcpyAsync(s->d_stage, s->h_stage, total, hipMemcpyHostToDevice, s->stream), "H2D slice");
+    if (!KCDC_HANDLE_ZC)
+        HIP_TRY(hipMemcpyAsync(s->d_stage, s->h_stage, total, hipMemcpyHostToDevice, s->stream), "H2D slice");
     rc = launch_scan_first(*s->algo, s->d_stage, total, kWindow, static_cast<int64_t>(total) - 1, s->d_out, s->device,
                            s->stream);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(s->h_out, s->d_out, sizeof(int64_t), hipMemcpyDeviceToHost, s->stream), "D2H result");
+    if (!KCDC_HANDLE_ZC)
+        HIP_TRY(hipMemcpyAsync(s->h_out, s->d_out, sizeof(int64_t), hipMemcpyDeviceToHost, s->stream), "D2H result");
     HIP_TRY(hipStreamSynchronize(s->stream), "scan sync");
     const int64_t f = s->h_out[0];
     return f < 0 ? -1 : f - kWindow;
@@ -233,8 +260,7 @@ extern "C" kcdc_splitter* kcdc_splitter_new(const char* name, int device) {
         DeviceGuard g(device);
         int err = 0;
         if (!device_tables(device, &err) || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
-            hipMalloc(&s->d_out, sizeof(int64_t)) != hipSuccess ||
-            hipHostMalloc(&s->h_out, sizeof(int64_t), hipHostMallocDefault) != hipSuccess) {
+            alloc_out(s) != hipSuccess) {
             if (!err) set_error(KCDC_EIO, "failed to allocate splitter device resources");
             destroy(s);
             return nullptr;
@@ -524,8 +550,7 @@ extern "C" kcdc_splitter* kcdc_group_splitter(kcdc_group* g) {
     s->algo = g->algo;
     s->device = g->device;
     if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&s->d_out, sizeof(int64_t)) != hipSuccess ||
-        hipHostMalloc(&s->h_out, sizeof(int64_t), hipHostMallocDefault) != hipSuccess) {
+        alloc_out(s) != hipSuccess) {
         set_error(KCDC_EIO, "failed to allocate splitter device resources");
         destroy(s);
         return nullptr;
