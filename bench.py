@@ -311,14 +311,22 @@ def bench_files(args):
                       "largest_file": max(lens) if lens else 0,
                       "parallelism": f"LPT file sharding x{world}, no data-path collectives"}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # parity on a sample: the 64 smallest and the 2 largest files vs the oracle
-        from oracle import coracle  # oracle import confined to the checking leg
+        # cpu_baseline leg: the oracle's C restatement timed on a sample of this rank's files
+        # (the 64 smallest and the 2 largest), which also checks the GPU cuts of the sample
+        from oracle import coracle  # oracle import confined to this leg
         got = batch.read_files(*res)
         pick = list(range(min(64, len(lens)))) + list(range(max(64, len(lens) - 2), len(lens)))
         host = [data[int(offs[i]):int(offs[i]) + lens[i]].cpu().numpy() for i in pick]
-        want = coracle.split_batch(name, host, nthreads=min(16, os.cpu_count() or 1))
-        out["sample_parity_mismatches"] = sum(1 for j, i in enumerate(pick) if not np.array_equal(got[i], want[j]))
-        out["sample"] = f"{len(pick)} files (64 smallest, 2 largest) vs oracle/cdc_oracle.c"
+        nthreads = min(16, os.cpu_count() or 1)
+        t0 = time.perf_counter()
+        want = coracle.split_batch(name, host, nthreads=nthreads)
+        dt = time.perf_counter() - t0
+        sb = sum(lens[i] for i in pick)
+        out["cpu_baseline"] = {
+            "value": round(sb / GiB / dt, 3), "unit": "GiB/s", "cores": nthreads, "kind": "port",
+            "sample": f"{len(pick)} files of this rank (64 smallest, 2 largest; {sb >> 20} MiB), {name}, "
+                      f"oracle/cdc_oracle.c, {nthreads} threads, {dt:.2f}s wall",
+            "sample_parity_mismatches": sum(1 for j, i in enumerate(pick) if not np.array_equal(got[i], want[j]))}
     if args.all_names:
         out["per_name_gib_s"] = {}
         for nm in ks.SupportedAlgorithms():
