@@ -315,7 +315,8 @@ def bench_files(args):
         # (the 64 smallest and the 2 largest), which also checks the GPU cuts of the sample
         from oracle import coracle  # oracle import confined to this leg
         got = batch.read_files(*res)
-        pick = list(range(min(64, len(lens)))) + list(range(max(64, len(lens) - 2), len(lens)))
+        pick = sorted(set(range(min(64, len(lens)))) | set(range(0, len(lens), 8)) |
+                      set(range(max(0, len(lens) - 2), len(lens))))
         host = [data[int(offs[i]):int(offs[i]) + lens[i]].cpu().numpy() for i in pick]
         nthreads = min(16, os.cpu_count() or 1)
         t0 = time.perf_counter()
@@ -324,7 +325,7 @@ def bench_files(args):
         sb = sum(lens[i] for i in pick)
         out["cpu_baseline"] = {
             "value": round(sb / GiB / dt, 3), "unit": "GiB/s", "cores": nthreads, "kind": "port",
-            "sample": f"{len(pick)} files of this rank (64 smallest, 2 largest; {sb >> 20} MiB), {name}, "
+            "sample": f"{len(pick)} files of this rank (64 smallest, every 8th, 2 largest; {sb >> 20} MiB), {name}, "
                       f"oracle/cdc_oracle.c, {nthreads} threads, {dt:.2f}s wall",
             "sample_parity_mismatches": sum(1 for j, i in enumerate(pick) if not np.array_equal(got[i], want[j]))}
     if args.all_names:
