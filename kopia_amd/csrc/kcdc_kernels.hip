@@ -2039,46 +2039,70 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void cand_scan_dm
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// Exclusive prefix sum of stored counts (one workgroup; the long path has at most
-// a few hundred thousand segments).
-__global__ __launch_bounds__(1024) void seg_prefix_kernel(LongArgs g) {
-    __shared__ uint64_t wsum[16];
-    __shared__ uint64_t carry;
+// Exclusive prefix sum of the stored counts over all segments, in three launches:
+// per-block sums of kPrefixItems segments, a scan of the block sums (one thread: a few
+// hundred blocks at most), then every block scans its items from its offset.
+constexpr int kPrefixItems = 1024 * 8;
+__global__ __launch_bounds__(1024) void seg_blocksum_kernel(LongArgs g, uint64_t* block_sum) {
+    __shared__ uint32_t wsum[16];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    if (t == 0) carry = 0;
-    __syncthreads();
-    constexpr int kItems = 8;
-    for (int64_t base = 0; base < g.nseg; base += 1024 * kItems) {
-        uint32_t v[kItems];
-        uint32_t sum = 0;
-#pragma unroll
-        for (int j = 0; j < kItems; j++) {
-            const int64_t i = base + static_cast<int64_t>(t) * kItems + j;
-            v[j] = i < g.nseg ? (g.seg_cnt[i] & 0x7FFFFFFFu) : 0u;
-            sum += v[j];
-        }
-        uint32_t incl = sum;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t x = __shfl_up(incl, d);
-            if (lane >= d) incl += x;
-        }
-        if (lane == 63) wsum[w] = incl;
-        __syncthreads();
-        uint64_t wpre = 0;
-        for (int k = 0; k < w; k++) wpre += wsum[k];
-        uint64_t run = carry + wpre + incl - sum;
-#pragma unroll
-        for (int j = 0; j < kItems; j++) {
-            const int64_t i = base + static_cast<int64_t>(t) * kItems + j;
-            if (i < g.nseg) g.seg_off[i] = run;
-            run += v[j];
-        }
-        __syncthreads();
-        if (t == 1023) carry = run;
-        __syncthreads();
+    const int64_t base = static_cast<int64_t>(blockIdx.x) * kPrefixItems;
+    uint32_t sum = 0;
+    for (int j = 0; j < 8; j++) {
+        const int64_t i = base + static_cast<int64_t>(t) * 8 + j;
+        sum += i < g.nseg ? (g.seg_cnt[i] & 0x7FFFFFFFu) : 0u;
     }
-    if (t == 0) g.total[0] = carry;
+    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_down(sum, d);
+    if (lane == 0) wsum[w] = sum;
+    __syncthreads();
+    if (t == 0) {
+        uint64_t tot = 0;
+        for (int k = 0; k < 16; k++) tot += wsum[k];
+        block_sum[blockIdx.x] = tot;
+    }
+}
+
+__global__ void block_offsets_kernel(LongArgs g, uint64_t* block_sum, uint32_t nblocks) {
+    if (threadIdx.x != 0) return;
+    uint64_t run = 0;
+    for (uint32_t b = 0; b < nblocks; b++) {  // in place: block_sum[b] becomes its exclusive offset
+        const uint64_t v = block_sum[b];
+        block_sum[b] = run;
+        run += v;
+    }
+    g.total[0] = run;
+}
+
+__global__ __launch_bounds__(1024) void seg_prefix_kernel(LongArgs g, const uint64_t* block_off) {
+    __shared__ uint64_t wsum[16];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    constexpr int kItems = 8;
+    const int64_t base = static_cast<int64_t>(blockIdx.x) * kPrefixItems;
+    uint32_t v[kItems];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        const int64_t i = base + static_cast<int64_t>(t) * kItems + j;
+        v[j] = i < g.nseg ? (g.seg_cnt[i] & 0x7FFFFFFFu) : 0u;
+        sum += v[j];
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t x = __shfl_up(incl, d);
+        if (lane >= d) incl += x;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint64_t run = block_off[blockIdx.x];
+    for (int k = 0; k < w; k++) run += wsum[k];
+    run += incl - sum;
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+        const int64_t i = base + static_cast<int64_t>(t) * kItems + j;
+        if (i < g.nseg) g.seg_off[i] = run;
+        run += v[j];
+    }
 }
 
 __global__ void compact_kernel(LongArgs g) {
@@ -2613,7 +2637,7 @@ struct LongLayout {
     int64_t nseg;
     uint64_t node_cap;
     uint32_t levels;
-    size_t off_streams, off_cnt, off_cand, off_off, off_list, off_total, off_serial, off_forced, off_jump, bytes;
+    size_t off_streams, off_cnt, off_cand, off_off, off_list, off_total, off_bsum, off_serial, off_forced, off_jump, bytes;
 };
 int64_t long_nseg(uint64_t len, uint64_t off0) {  // segments tile coordinates (position + off0)
     return len ? static_cast<int64_t>((len + off0 + dev::kSegBytes - 1) / dev::kSegBytes) : 0;
@@ -2636,6 +2660,8 @@ LongLayout long_layout(int64_t nseg, uint32_t nstreams) {
     o += al(ns * dev::kSegK * 8);
     L.off_total = o;
     o += 256;
+    L.off_bsum = o;
+    o += al((static_cast<size_t>(nseg) + dev::kPrefixItems - 1) / dev::kPrefixItems * 8 + 8);
     L.node_cap = 0;
     L.levels = 0;
     L.off_serial = L.off_forced = L.off_jump = o;
@@ -2729,7 +2755,11 @@ int launch_split_long_multi(const Algo& algo, uint32_t m, const uint8_t* const* 
         } else {
             hipLaunchKernelGGL(dev::cand_scan_kernel<kRabinKarp>, grid, block, 0, st, a, g);
         }
-        hipLaunchKernelGGL(dev::seg_prefix_kernel, dim3(1), dim3(1024), 0, st, g);
+        const unsigned nblk = static_cast<unsigned>((nseg + dev::kPrefixItems - 1) / dev::kPrefixItems);
+        uint64_t* bsum = reinterpret_cast<uint64_t*>(w + L.off_bsum);
+        hipLaunchKernelGGL(dev::seg_blocksum_kernel, dim3(nblk), dim3(1024), 0, st, g, bsum);
+        hipLaunchKernelGGL(dev::block_offsets_kernel, dim3(1), dim3(64), 0, st, g, bsum, nblk);
+        hipLaunchKernelGGL(dev::seg_prefix_kernel, dim3(nblk), dim3(1024), 0, st, g, bsum);
         hipLaunchKernelGGL(dev::compact_kernel, dim3(static_cast<unsigned>((nseg + 255) / 256)), dim3(256), 0, st, g);
     }
     if (g.serial) {  // streams it cannot take (truncated segments) stay flagged for resolve_kernel
