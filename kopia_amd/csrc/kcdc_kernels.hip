@@ -489,6 +489,121 @@ struct BuzRing {
     }
 };
 
+// buzhash32 without the T-ring: the leaving byte's table value is read from LDS again (a
+// second v_perm + ds_read_b32 per byte), and the raw bytes of the 64 positions before the
+// step (16 VGPRs) stand in for the 64 ring registers.  Those bytes also feed the rare exact
+// re-run, so it needs no global loads.  One more VALU per byte for the registers a third
+// wave per SIMD would need (DESIGN.md §5, round-2 plan).  Off (KCDC_REREAD 0): at 8 waves/CU
+// it is bit-exact but 15 % slower (1.58 vs 1.38 ms).
+#ifndef KCDC_REREAD
+#define KCDC_REREAD 0
+#endif
+#ifndef KCDC_RR_W
+#define KCDC_RR_W 8  // bytes per lookahead window (2 table reads each)
+#endif
+struct BuzRe {
+    const char* tab;
+    uint32_t lane4;
+    uint32_t mask;
+    uint32_t h;
+    uint32_t prev[16];  // raw bytes of the 64 positions before the current step
+    using State = uint32_t;
+    __device__ __forceinline__ State save() const { return h; }
+    __device__ __forceinline__ uint32_t look(uint32_t dwv, int k) const {
+        const uint32_t a = __builtin_amdgcn_perm(dwv, lane4, 0x0c0c0000u | ((4u + k) << 8));
+        return *reinterpret_cast<const uint32_t*>(tab + a);
+    }
+    // hash of the 64 bytes w (the window before the first step), from a zero history
+    __device__ __forceinline__ void warm(const uint32_t (&w)[16]) {
+        h = 0;
+        uint32_t t[16];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 16; i++) t[i] = look(w[(16 * q + i) >> 2], i & 3);
+#pragma unroll
+            for (int i = 0; i < 16; i++) h = rotl1(h) ^ t[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) prev[i] = w[i];
+    }
+    // One 128-byte step; returns min over positions 63..127 of the (rotated-frame) hash and,
+    // or-ed with hmask, over positions 0..62.  prev is left for the caller (advance()).
+    template <bool TOP>
+    __device__ __forceinline__ uint32_t step128(const uint32_t (&dw)[32], uint32_t hmask) {
+        constexpr int W = KCDC_RR_W;
+        uint32_t m = 0xFFFFFFFFu, m0 = 0xFFFFFFFFu;
+        uint32_t ti[W], to[W], ni[W], no[W];
+        auto leave = [&](int b) -> uint32_t { return b < 64 ? prev[b >> 2] : dw[(b - 64) >> 2]; };
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+            ti[i] = look(dw[i >> 2], i & 3);
+            to[i] = look(leave(i), i & 3);
+        }
+#pragma unroll
+        for (int w = 0; w < 128 / W; w++) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (w < 128 / W - 1) {
+#pragma unroll
+                for (int i = 0; i < W; i++) {
+                    const int b = W * (w + 1) + i;
+                    ni[i] = look(dw[b >> 2], b & 3);
+                    no[i] = look(leave(b), b & 3);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < W; i++) {
+                const int b = W * w + i;
+                h = roll3(h, to[i], ti[i]);
+                const uint32_t t = TOP ? h : h & mask;
+                if (b < 63) {
+                    m0 = min(m0, t);
+                    if ((b & 3) == 3) asm volatile("" : "+v"(m0));
+                } else {
+                    m = min(m, t);
+                    if ((b & 3) == 3) asm volatile("" : "+v"(m));
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < W; i++) {
+                ti[i] = ni[i];
+                to[i] = no[i];
+            }
+        }
+        return min(m, m0 | hmask);
+    }
+    __device__ __forceinline__ void advance(const uint32_t (&dw)[32]) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) prev[i] = dw[16 + i];
+    }
+    // index of the first i in [lo, hi] of the step with (h & mask) == 0, else 128
+    __device__ __forceinline__ uint32_t exact(State st0, const uint32_t (&dw)[32], int lo, int hi) const {
+        uint32_t e[32], o[32];
+#pragma unroll
+        for (int j = 0; j < 32; j++) {
+            e[j] = dw[j];
+            o[j] = j < 16 ? prev[j] : dw[j - 16];
+        }
+        uint32_t hh = st0, first = 128;
+#pragma unroll 1
+        for (int j = 0; j < 32; j++) {
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                hh = rotl1(hh) ^ look(o[0], b) ^ look(e[0], b);
+                const int i = 4 * j + b;
+                if (first == 128 && (hh & mask) == 0 && i >= lo && i <= hi) first = static_cast<uint32_t>(i);
+            }
+#pragma unroll
+            for (int k = 0; k < 31; k++) {
+                e[k] = e[k + 1];
+                o[k] = o[k + 1];
+            }
+        }
+        return first;
+    }
+};
+
 // rabinkarp64: v ^= out[b[p-64]]; idx = v >> shift; v = (v << 8 | b[p]) ^ mod[idx].
 struct RabinShared {
     uint64_t out[256];
@@ -1330,7 +1445,12 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
     __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    BuzRing hash;
+#if KCDC_REREAD
+    using Hash = BuzRe;
+#else
+    using Hash = BuzRing;
+#endif
+    Hash hash;
     hash.tab = reinterpret_cast<const char*>(smtab.tab);
     hash.lane4 = static_cast<uint32_t>(lane) * 4u;
     hash.mask = a.mask;
@@ -1452,8 +1572,12 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                          : "+v"(ht_lo), "+v"(ht_hi), "+v"(qc_lo), "+v"(qc_hi), "+v"(pr.x), "+v"(pr.y), "+v"(pr.z),
                            "+v"(pr.w)::"memory");
             read_piece(wl, lane, c0 - 64, cur.off0, w16);
+#if KCDC_REREAD
+            hash.warm(w16);
+#else
             hash.clear();
             hash.template block<kWarm>(w16);
+#endif
         }
         uint32_t tk = 0, pe = 0;
         int64_t nbacklog = 0;
@@ -1481,7 +1605,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         const int poll_step = g.nb > 1 ? g.nb / 2 : 0;
         for (int n = 0; n < (probe_dead ? 0 : g.nb); n++) {
             const int64_t c = c0 + 128 * n;
-            const typename BuzRing::State st0 = hash.save();
+            const typename Hash::State st0 = hash.save();
             uint32_t dw[32];
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1522,6 +1646,15 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             const uint32_t m = hash.template step128<TOP>(dw, 0u);
 #endif
             __builtin_amdgcn_sched_barrier(0);
+#if KCDC_REREAD
+            if (m <= lim && found < 0 && c <= hi) {  // rare: exact re-run from the step's registers
+                const int64_t blo = lo - c, bhi = hi - c;
+                const uint32_t idx = hash.exact(st0, dw, blo < 0 ? 0 : static_cast<int>(blo),
+                                                bhi > 127 ? 127 : static_cast<int>(bhi));
+                if (idx < 128u) found = c + idx;
+            }
+            hash.advance(dw);
+#else
             if (m <= lim && found < 0 && c <= hi) {  // rare: exact re-run from global memory
                 uint32_t prv[16], cur32[32];
                 g.ld.load(c - 64, prv);
@@ -1534,6 +1667,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                 // pending around the loop and waits for them in the hash loop (draining DMAs)
                 __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
             }
+#endif
         }
         // ---- end of tile
         if (probe_dead) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's DMAs, unused
