@@ -308,66 +308,10 @@ struct BuzRing {
             return m;
         }
     }
-    // Half-steps of a 128-byte step for the LDS-DMA path (the two 64-byte pieces arrive
-    // separately): HALF 0 consumes the ring and fills loc, HALF 1 consumes loc and
-    // refills the ring.  Returns the running min of (h & mask) over the half.
-    // TOP (mask rotated to the top bits): the running min is over the raw hash and the
-    // caller tests m <= buz_lim; otherwise over h & mask and the caller tests m == 0.
-    template <int HALF, bool TOP>
-    __device__ __forceinline__ uint32_t half(const uint32_t (&dw)[16], uint32_t (&loc)[64], uint32_t m) {
-#if KCDC_LOOKAHEAD
-        // Table reads software-pipelined one 16-byte window ahead: window w+1's 16
-        // ds_reads are issued before window w is rolled, so their LDS latency hides
-        // under window w's arithmetic (one exposed latency per 64 bytes, not per 16).
-        uint32_t tw[16], tn[16];
-#pragma unroll
-        for (int i = 0; i < 16; i++) tw[i] = look(dw[i >> 2], i & 3);
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-            __builtin_amdgcn_sched_barrier(0);
-            if (w < 3) {
-#pragma unroll
-                for (int i = 0; i < 16; i++) tn[i] = look(dw[(16 * (w + 1) + i) >> 2], i & 3);
-            }
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const int b = 16 * w + i;
-                if (HALF == 0) {
-                    h = roll3(h, ring[b], tw[i]);
-                    loc[b] = tw[i];
-                } else {
-                    h = roll3(h, loc[b], tw[i]);
-                    ring[b] = tw[i];
-                }
-                m = min(m, TOP ? h : h & mask);
-                if ((i & 3) == 3) asm volatile("" : "+v"(m));
-            }
-#pragma unroll
-            for (int i = 0; i < 16; i++) tw[i] = tn[i];
-        }
-        return m;
-#endif
-#pragma unroll
-        for (int i = 0; i < 64; i++) {
-            if (kSchedWindow && i % kSchedWindow == 0) __builtin_amdgcn_sched_barrier(0);
-            const uint32_t t = look(dw[i >> 2], i & 3);
-            if (HALF == 0) {
-                h = roll3(h, ring[i], t);
-                loc[i] = t;
-            } else {
-                h = roll3(h, loc[i], t);
-                ring[i] = t;
-            }
-            m = min(m, TOP ? h : h & mask);
-            if ((i & 3) == 3) asm volatile("" : "+v"(m));
-        }
-        return m;
-    }
     // A whole 128-byte step (the 128-byte-run DMA path): bytes 0..63 consume the ring and
     // fill loc, bytes 64..127 consume loc and refill the ring (loc[b] can take ring[b]'s
     // register).  Table reads run one 16-byte window ahead of the arithmetic.
-    // Positions 0..62 keep their own running min m0, or-ed with hmask at the end (a lane
-    // whose state has a stand-in history passes all ones: its predecessor tests them).
+    // Positions 0..62 keep their own running min m0, or-ed with hmask at the end.
     template <bool TOP>
     __device__ __forceinline__ uint32_t step128(const uint32_t (&dw)[32], uint32_t hmask) {
         constexpr int W = KCDC_LA_W;  // bytes per lookahead window
@@ -406,60 +350,6 @@ struct BuzRing {
             for (int i = 0; i < W; i++) tw[i] = tn[i];
         }
         return min(m, m0 | hmask);
-    }
-    // Tile-end extension: continue into the successor lane's segment head nx (its first
-    // 64 bytes), whose first 63 positions that lane tested only against a stand-in
-    // history.  All 64 bytes are rolled (position 63 is tested twice, harmlessly) so the
-    // ring keeps its phase: ring[0] is again the oldest byte, a consistent state.
-    template <bool TOP>
-    __device__ __forceinline__ uint32_t extend64(const uint32_t (&nx)[16]) {
-        uint32_t m = 0xFFFFFFFFu;
-        uint32_t t[16];
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int i = 0; i < 16; i++) t[i] = look(nx[(16 * w + i) >> 2], i & 3);
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const int b = 16 * w + i;
-                h = roll3(h, ring[b], t[i]);
-                ring[b] = t[i];
-                m = min(m, TOP ? h : h & mask);
-                if ((i & 3) == 3) asm volatile("" : "+v"(m));
-            }
-        }
-        return m;
-    }
-    // Lane 0 takes lane 63's state (readlane/writelane); the other lanes keep theirs.
-    // Lane 0 so continues from the true state at the end of the previous tile; every other
-    // lane holds SOME consistent state (a real 64-byte history), which makes its hash
-    // exact from its 64th byte on.
-    __device__ __forceinline__ void carry_from_last_lane(bool lane0) {
-        const uint32_t hl = __builtin_amdgcn_readlane(h, kWave - 1);
-        h = lane0 ? hl : h;
-#pragma unroll
-        for (int i = 0; i < 64; i++) {
-            const uint32_t v = __builtin_amdgcn_readlane(ring[i], kWave - 1);
-            ring[i] = lane0 ? v : ring[i];
-        }
-    }
-    // Exact first candidate among positions [lo, hi] of cur (4N bytes) from a zero state
-    // warmed on the true previous 64 bytes prv (rare path; independent of the ring).
-    template <int N>
-    __device__ __forceinline__ uint32_t exact_cold(const uint32_t (&prv)[16], const uint32_t (&cur)[N], int lo,
-                                                   int hi) const {
-        uint32_t hh = 0, o[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) o[j] = prv[j];
-#pragma unroll 1
-        for (int j = 0; j < 16; j++) {
-#pragma unroll
-            for (int b = 0; b < 4; b++) hh = rotl1(hh) ^ look(o[0], b);
-#pragma unroll
-            for (int k = 0; k < 15; k++) o[k] = o[k + 1];
-        }
-        return exact(hh, prv, cur, lo, hi);
     }
     template <int N>
     __device__ __forceinline__ uint32_t exact(State st0, const uint32_t (&prv)[16], const uint32_t (&dw)[N], int lo,
@@ -1072,10 +962,11 @@ __device__ __forceinline__ uint64_t bcast64(uint64_t v) {
     return (static_cast<uint64_t>(bcast(static_cast<uint32_t>(v >> 32))) << 32) | bcast(static_cast<uint32_t>(v));
 }
 // Header words (uint32 offsets) 2 KiB apart: hammered counters do not share DRAM pages.
-constexpr int kQHead = 0, kQDone = 512, kQTail = 1024, kQErr = 1536;
+// Word 0 holds the 64-bit {head, tail} ticket counter (kQHT, below).
+constexpr int kQDone = 512, kQErr = 1536;
 constexpr size_t kQHeaderBytes = 8192;
 // Header words 1792.. : debug-build failure record (pcheck, KCDC_DEBUG_CHECKS).
-constexpr int kQStat = 1792;
+[[maybe_unused]] constexpr int kQStat = 1792;
 constexpr uint32_t kSpinCap = 1u << 22;                          // give up (error word) after ~seconds
 
 // ======================================================= pipelined persistent kernel
