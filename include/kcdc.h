@@ -135,7 +135,9 @@ void kcdc_group_free(kcdc_group* g);
  * _device: every pointer (the array of stream pointers, lens, cuts, cut_base,
  * counts) is device memory on the current device; the call is asynchronous on
  * `hip_stream` (NULL = legacy default stream) except for error checking of
- * the launch.  Stream bytes may have any alignment.  */
+ * the launch.  Stream bytes may have any alignment.  Each launch takes one of 64
+ * per-device queue workspaces in turn: launches on one stream are ordered, but
+ * at most 64 launches may be in flight at once across different streams. */
 int kcdc_split_batch_device(const char* name, const uint8_t* const* d_ptrs, const uint64_t* d_lens,
                             uint32_t nstreams, uint64_t* d_cuts, uint64_t cuts_cap, const uint64_t* d_cut_base,
                             uint64_t* d_counts, void* hip_stream);
