@@ -136,8 +136,8 @@ void kcdc_group_free(kcdc_group* g);
  * counts) is device memory on the current device; the call is asynchronous on
  * `hip_stream` (NULL = legacy default stream) except for error checking of
  * the launch.  Stream bytes may have any alignment.  Each launch takes one of 64
- * per-device queue workspaces in turn: launches on one stream are ordered, but
- * at most 64 launches may be in flight at once across different streams. */
+ * per-device queue workspaces in turn; a launch that reuses a workspace still in
+ * use by another stream waits for it (an event), so any number may be in flight. */
 int kcdc_split_batch_device(const char* name, const uint8_t* const* d_ptrs, const uint64_t* d_lens,
                             uint32_t nstreams, uint64_t* d_cuts, uint64_t cuts_cap, const uint64_t* d_cut_base,
                             uint64_t* d_counts, void* hip_stream);

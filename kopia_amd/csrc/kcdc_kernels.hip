@@ -2398,6 +2398,8 @@ DeviceTables g_dev_tables[kMaxDevices];
 struct QueueWs {
     char* base = nullptr;
     size_t bytes = 0;
+    hipEvent_t done = nullptr;  // recorded after the slot's last launch: a reuse from another
+                                // stream waits for it (more than kQueueSlots launches in flight)
 };
 QueueWs g_qws[kMaxDevices][kQueueSlots];
 std::vector<char*> g_retired;
@@ -2542,10 +2544,12 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         const size_t hdr = dev::kQHeaderBytes;
         const size_t bytes = hdr + ring_bytes + (dma ? 24ull * s.nstreams : 0);
         char* ws = nullptr;
+        // The slot stays locked from its selection to its event record, so a later user of the
+        // same slot always waits for this launch.
+        std::lock_guard<std::mutex> lk(g_dev_mu);
+        const unsigned slot = g_queue_next[device]++ % kQueueSlots;
+        QueueWs& q = g_qws[device][slot];
         {
-            std::lock_guard<std::mutex> lk(g_dev_mu);
-            const unsigned slot = g_queue_next[device]++ % kQueueSlots;
-            QueueWs& q = g_qws[device][slot];
             if (q.bytes < bytes) {
                 int prev = 0;
                 (void)hipGetDevice(&prev);
@@ -2560,6 +2564,17 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
                 q.bytes = nbytes;
             }
             ws = q.base;
+            if (!q.done) {
+                int prev = 0;
+                (void)hipGetDevice(&prev);
+                (void)hipSetDevice(device);
+                const hipError_t e = hipEventCreateWithFlags(&q.done, hipEventDisableTiming);
+                (void)hipSetDevice(prev);
+                if (e != hipSuccess) return hip_fail(e, "queue workspace event");
+            } else {
+                const hipError_t e = hipStreamWaitEvent(st, q.done, 0);
+                if (e != hipSuccess) return hip_fail(e, "queue workspace wait");
+            }
         }
         a.queue = reinterpret_cast<uint32_t*>(ws);
 #if KCDC_TRACE || KCDC_DEBUG_CHECKS
@@ -2598,6 +2613,8 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
             else
                 hipLaunchKernelGGL(dev::split_batch_kernel<kRabinKarp>, dim3(grid), block, 0, st, a);
         }
+        const hipError_t er = hipEventRecord(q.done, st);
+        if (er != hipSuccess) return hip_fail(er, "queue workspace record");
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : hip_fail(e, "split kernel launch");
