@@ -33,3 +33,22 @@ def test_more_launches_than_queue_slots_across_streams():
         got = batch.read_cuts(b)
         for j, i in enumerate(order):
             assert np.array_equal(got[j], np.asarray(want[i], dtype=np.int64)), (k, j)
+
+
+def test_many_tiny_streams_one_launch():
+    """200,000 streams of 0..4096 bytes in one batch launch (n >> waves: every ticket, ring
+    entry and tombstone path of the queue at scale); all below min size, so each stream is
+    one chunk ending at its length (empty streams: none)."""
+    name, n = "DYNAMIC-128K-BUZHASH", 200_000
+    rng = np.random.default_rng(5)
+    lens = rng.integers(0, 4097, n)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    dev = torch.device("cuda", 0)
+    data = torch.zeros(int(lens.sum()) + 64, dtype=torch.uint8, device=dev)
+    b = batch.make_device_batch(name, [data.data_ptr() + int(o) for o in offs], lens.tolist(), dev)
+    batch.split_batch_device(name, b)
+    torch.cuda.synchronize(dev)
+    got = batch.read_cuts(b)
+    for i in range(n):
+        want = [int(lens[i])] if lens[i] else []
+        assert got[i].tolist() == want, (i, int(lens[i]))
