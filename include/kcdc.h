@@ -114,7 +114,8 @@ void kcdc_splitter_close(kcdc_splitter* s);
  * to `max_wait_us` for more calls (0: ship whatever is there) and takes at most
  * `max_batch` calls per launch (0: 256).  One name per group (a repository uses
  * one splitter).  Handles come from kcdc_group_splitter and are released with
- * kcdc_splitter_close; free the group after its handles. */
+ * kcdc_splitter_close.  kcdc_group_free may come first: the group then lives on
+ * until its last handle is closed (no handle may be created after it). */
 typedef struct kcdc_group kcdc_group;
 kcdc_group* kcdc_group_new(const char* name, int device, uint32_t max_batch, uint32_t max_wait_us);
 kcdc_splitter* kcdc_group_splitter(kcdc_group* g);

@@ -379,6 +379,7 @@ struct kcdc_group {
     int open = 0;
     uint64_t seq_next = 1, completed = 0;
     uint32_t live = 0;  // open handles: a launch is sealed at once when every one of them waits
+    bool closing = false;  // kcdc_group_free was called with handles still open
     int error = 0;
     std::mutex mu;
     std::condition_variable cv_work, cv_done;
@@ -449,12 +450,25 @@ void group_loop(kcdc_group* g) {
     }
 }
 
+void group_shutdown(kcdc_group* g) {
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        g->stop = true;
+    }
+    g->cv_work.notify_all();
+    if (g->th.joinable()) g->th.join();
+    group_release(g);
+}
+
 void group_handle_closed(kcdc_group* g) {
+    bool last = false;
     {
         std::lock_guard<std::mutex> lk(g->mu);
         g->live--;
+        last = g->closing && g->live == 0;
     }
     g->cv_work.notify_all();  // a pending launch may now hold every live handle
+    if (last) group_shutdown(g);  // kcdc_group_free came first: the last handle frees the group
 }
 
 int64_t group_first_candidate(kcdc_splitter* s, const uint8_t* b, size_t n) {
@@ -565,11 +579,12 @@ extern "C" void kcdc_group_free(kcdc_group* g) {
     if (!g) return;
     {
         std::lock_guard<std::mutex> lk(g->mu);
-        g->stop = true;
+        if (g->live > 0) {  // handles still open: the last kcdc_splitter_close frees the group
+            g->closing = true;
+            return;
+        }
     }
-    g->cv_work.notify_all();
-    if (g->th.joinable()) g->th.join();
-    group_release(g);
+    group_shutdown(g);
 }
 
 // ==================================================================== batch

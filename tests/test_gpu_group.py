@@ -106,3 +106,16 @@ def test_group_throughput_vs_private_handles():
     assert rg == rp
     print(f"\n{nw} writers x {L >> 20} MiB in 64 KiB slices: grouped {nw * L / tg / 1e9:.2f} GB/s, "
           f"private handles {nw * L / tp / 1e9:.2f} GB/s")
+
+
+def test_group_freed_before_its_handles():
+    """kcdc_group_free with a handle still open defers to that handle's Close; the handle keeps
+    working in the meantime."""
+    name = "DYNAMIC-128K-BUZHASH"
+    data = coracle.gen_stream(SEED, 77, 3 << 20)
+    g = ks.SplitterGroup(name, 0)
+    s = g.splitter()
+    g.close()
+    assert write_object(s, data, slice_plan(np.random.default_rng(3), len(data), "64k")) == \
+        coracle.split_stream(name, data).tolist()
+    s.Close()
