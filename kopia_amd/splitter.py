@@ -118,10 +118,17 @@ class SplitterGroup:
         return s
 
     def close(self) -> None:
-        """Free the group (close its splitters first)."""
+        """Free the group; splitters still open keep working, and the last one to close
+        releases it."""
         if self._g:
             _lib.lib().kcdc_group_free(self._g)
             self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 Factory = Callable[[], Splitter]
