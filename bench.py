@@ -6,45 +6,125 @@ counter-PRNG bytes resident in HBM, split with the default algorithm
 DYNAMIC-4M-BUZHASH (repo/splitter/splitter.go:89).  One *step* = one launch of
 the batch splitter over all 4096 streams (the whole 16 GiB shard); cut lists stay
 in HBM.  For N > 1 GPUs every rank splits its own shard (stream ids offset by
-rank): weak scaling, no collective on the data path (the only collectives are
-the timing barrier and the max-over-ranks of the elapsed time).
+rank): weak scaling, no collective on the data path.  The only inter-process
+traffic is the timing barrier and the max/gather of per-rank timings, over gloo
+(CPU) -- no RCCL.
+
+Launch: under torch.distributed.run (RANK/WORLD_SIZE/LOCAL_RANK set) each process
+is one rank; without RANK, `--gpus N` spawns N fresh rank processes itself (before
+anything touches a GPU in this process), the way `kopia benchmark splitter
+--parallel` runs N splitters at once (cli/command_benchmark.go:67-82).
 
 Prints ONE JSON line on rank 0 (the driver's contract).  Extra keys:
-  roofline     — dominant kernel's algorithmic bytes / kernel time vs HBM peak
-  cpu_baseline — the oracle's C restatement of the reference Go loop timed on
-                 this host (rank 0, N=1 only)
-  host_inclusive_gib_s — H2D + kernel + D2H rate through kcdc_split_batch_host
+  roofline     — the dominant kernel: rolled (algorithmic) bytes / kernel time vs
+                 HBM peak, plus the rocprofv3-measured physical HBM rate
+  cpu_baseline — the oracle's C restatement of the reference Go loop on this host's
+                 cores, 1 thread and all usable threads (rank 0, N=1 only)
+  host_inclusive_gib_s — host buffers -> H2D -> kernel -> D2H (kcdc_split_batch_host)
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 
 import numpy as np
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from kopia_amd import _lib, batch  # noqa: E402
-from kopia_amd import dist as kd  # noqa: E402
-from kopia_amd import splitter as ks  # noqa: E402
-
 METRIC = "splitter throughput GiB/s (device-resident) at 1/2/4/8 GPU; boundaries bit-exact"
 SEED = 0x6B6F706961
-# dominant kernel per splitter kind (kcdc_kernels.hip launch_split_batch)
+# the pipelined launch: init_ring_kernel, the splitter kernel, check_queue_kernel
 BATCH_KERNEL = {0: "kcdc::dev::split_fixed_kernel", 1: "kcdc::dev::split_batch_pipe_kernel<true>",
                 2: "kcdc::dev::split_batch_kernel<rabinkarp>"}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 GiB = float(1 << 30)
 
 
+# ----------------------------------------------------------------- ranks
+def env_rank_world() -> tuple[int, int, int]:
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+class Comm:
+    """Timing barrier and scalar/object reductions over gloo (CPU): no RCCL anywhere."""
+
+    def __init__(self, rank: int, world: int):
+        self.rank, self.world = rank, world
+        self.dist = None
+        if world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def gather(self, obj) -> list:
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _child(rank: int, world: int, port: int, argv: list, entry: str):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    mod = sys.modules[__name__]
+    getattr(mod, entry)(argv)
+
+
+def spawn_ranks(world: int, argv: list, entry: str = "main") -> None:
+    """Run `entry(argv)` in `world` fresh processes (spawn start method, so nothing of this
+    process -- which has not touched a GPU -- is inherited); returns when all exit."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_child, args=(world, _free_port(), argv, entry), nprocs=world, join=True,
+                       start_method="spawn")
+
+
+def aggregate(per_rank: list, steps: int) -> dict:
+    """Whole-job numbers from every rank's {bytes_per_step, elapsed_s}: value = all ranks'
+    bytes / the slowest rank's time (weak scaling), plus each rank's own rate."""
+    elapsed = max(r["elapsed_s"] for r in per_rank)
+    total = sum(r["bytes_per_step"] for r in per_rank) * steps
+    return {"value": round(total / GiB / elapsed, 3), "elapsed_s": elapsed,
+            "ms_per_step": round(elapsed / steps * 1e3, 4),
+            "per_gpu_gib_s": [round(r["bytes_per_step"] * steps / GiB / r["own_s"], 3) for r in per_rank]}
+
+
+# ------------------------------------------------------------- roofline
 def rolled_bytes(cuts: np.ndarray, min_size: int) -> int:
-    """Bytes the reference loop must read for one stream:
-    per chunk [s,e): (e-s) - max(min(min-1, e-s) - 64, 0)."""
+    """Bytes the reference loop must roll for one stream:
+    per chunk [s,e): (e-s) - max(min(min-1, e-s) - 64, 0).  The reference's fast path
+    (splitter_buzhash32.go:29-40) never reads the rest, and neither does the kernel."""
     if cuts.size == 0:
         return 0
     lens = np.diff(np.concatenate(([0], cuts)))
@@ -52,81 +132,133 @@ def rolled_bytes(cuts: np.ndarray, min_size: int) -> int:
     return int(np.sum(lens - np.maximum(fastp - 64, 0)))
 
 
-def load_pmc_traffic(kernel_prefix: str):
-    """Measured HBM bytes per launch from a committed rocprofv3 --pmc summary
-    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None."""
+def load_pmc_traffic(kernel: str, config: str):
+    """Measured HBM bytes per launch of `kernel` on `config` from a committed rocprofv3
+    --pmc FETCH_SIZE summary (profiles/pmc_traffic.json, tools/pmc_traffic.py), or None."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
-        return None
     try:
         d = json.load(open(p))
-        return d.get(kernel_prefix, {}).get("hbm_bytes_per_launch")
-    except Exception:
+    except (OSError, ValueError):
         return None
+    e = d.get(f"{kernel}|{config}")
+    return e.get("hbm_bytes_per_launch") if e else None
 
 
-def cpu_baseline(name: str, ns: int, L: int, gpu_cuts: list, nthreads: int, min_seconds: float = 10.0):
-    """Rank 0, N=1: the C restatement of the reference Go loop (oracle/, "port"),
-    timed on host cores over a sample of the same workload; also checks that the
-    GPU cut lists of the sample are bit-identical."""
+def roofline(kernel: str, config: str, kern_ms: float, rolled: int, stream_bytes: int) -> dict:
+    kern_s = kern_ms * 1e-3
+    achieved = rolled / kern_s / 1e9
+    traffic = load_pmc_traffic(kernel, config)
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kernel,
+            "kernel_ms": round(kern_ms, 4), "algorithmic_bytes_per_launch": rolled,
+            "algorithmic_bytes_def": "rolled bytes R: the bytes the reference loop reads, per chunk [s,e) "
+                                     "(e-s) - max(min(min-1,e-s) - 64, 0) (SURVEY.md §8d), summed over the "
+                                     "launch's cut lists",
+            "hbm_gbs_measured": round(traffic / kern_s / 1e9, 1) if traffic else None,
+            "hbm_frac_measured": round(traffic / kern_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+            "traffic_source": "profiles/pmc_traffic.json[" + f"{kernel}|{config}" + "] (FETCH_SIZE x 1024 x 2)",
+            "stream_bytes_per_launch": stream_bytes,
+            "stream_gbs": round(stream_bytes / kern_s / 1e9, 1)}
+
+
+# --------------------------------------------------------- CPU baseline
+def host_cpu_info() -> dict:
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    logical = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = logical
+    quota = None
+    try:  # cgroup v2 CPU quota ("max 100000" = unlimited)
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    threads = usable if quota is None else max(1, min(usable, int(quota + 0.5)))
+    return {"cpu_model": model, "logical_cores": logical, "affinity_cpus": usable, "cgroup_cpu_quota": quota,
+            "threads_all": threads}
+
+
+def _time_passes(fn, min_seconds: float) -> tuple[int, float]:
+    t0 = time.perf_counter()
+    fn()
+    passes = 1
+    while time.perf_counter() - t0 < min_seconds:
+        fn()
+        passes += 1
+    return passes, time.perf_counter() - t0
+
+
+def cpu_baseline(name: str, ns: int, L: int, gpu_cuts: list) -> dict:
+    """Rank 0, N=1: the C restatement of the reference Go loop (oracle/cdc_oracle.c, "port")
+    timed on this host with 1 thread and with every usable thread, on disjoint streams of
+    the same workload (`--parallel`, cli/command_benchmark.go:67-82); also checks the GPU
+    cut lists of the whole sample bit-for-bit."""
     from oracle import coracle  # oracle import confined to this leg
+    import concurrent.futures as cf
+    info = host_cpu_info()
+    nt = info["threads_all"]
     t0 = time.time()
     streams = [None] * ns
-    # generate the sample (not timed), then time only the split
-    import concurrent.futures as cf
-    with cf.ThreadPoolExecutor(nthreads) as ex:
+    with cf.ThreadPoolExecutor(nt) as ex:
         for i, s in enumerate(ex.map(lambda i: coracle.gen_stream(SEED, i, L), range(ns))):
             streams[i] = s
     gen_s = time.time() - t0
-    coracle.split_batch(name, streams[:8], nthreads=nthreads)  # warm
-    # repeat whole passes over the sample until >= min_seconds of wall time
-    t0 = time.perf_counter()
-    want = coracle.split_batch(name, streams, nthreads=nthreads)
-    passes = 1
-    while time.perf_counter() - t0 < min_seconds:
-        coracle.split_batch(name, streams, nthreads=nthreads)
-        passes += 1
-    dt = time.perf_counter() - t0
+    want = coracle.split_batch(name, streams, nthreads=nt)  # parity reference (untimed)
     mism = sum(1 for i in range(ns) if not np.array_equal(want[i], gpu_cuts[i]))
-    return {"value": round(passes * ns * L / GiB / dt, 3), "unit": "GiB/s", "cores": nthreads, "kind": "port",
-            "sample": f"{ns} x {L >> 20} MiB counter-PRNG streams (stream ids 0..{ns - 1}, same bytes as GPU rank 0), "
-                      f"{name}, C restatement of repo/splitter/splitter_buzhash32.go:26-67 (oracle/cdc_oracle.c), "
-                      f"{nthreads} threads, {passes} passes, {dt:.2f}s wall",
-            "sample_parity_mismatches": mism, "gen_seconds": round(gen_s, 2)}, streams
+    one = streams[: max(1, min(ns, (512 << 20) // L))]
+    p1, d1 = _time_passes(lambda: coracle.split_batch(name, one, nthreads=1), 8.0)
+    pa, da = _time_passes(lambda: coracle.split_batch(name, streams, nthreads=nt), 8.0)
+    r1 = p1 * len(one) * L / GiB / d1
+    ra = pa * ns * L / GiB / da
+    return {"value": round(ra, 3), "unit": "GiB/s", "cores": info["logical_cores"], "kind": "port",
+            "threads_1": round(r1, 3), "threads_all": round(ra, 3), "threads_all_n": nt,
+            "cpu_model": info["cpu_model"], "affinity_cpus": info["affinity_cpus"],
+            "cgroup_cpu_quota": info["cgroup_cpu_quota"],
+            "sample": f"{ns} x {L >> 20} MiB counter-PRNG streams (ids 0..{ns - 1}, the GPU's bytes), {name}; "
+                      f"C restatement of repo/splitter/splitter_buzhash32.go:26-67 (oracle/cdc_oracle.c); "
+                      f"1 thread: {len(one)} streams x {p1} passes in {d1:.1f}s; {nt} threads (every usable CPU of "
+                      f"this process): {pa} passes in {da:.1f}s",
+            "sample_parity_mismatches": mism, "gen_seconds": round(gen_s, 2)}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--splitter", default="DYNAMIC-4M-BUZHASH")
-    ap.add_argument("--streams", type=int, default=4096)
-    ap.add_argument("--stream-mib", type=int, default=4)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-host-inclusive", action="store_true")
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
-                    help="BASELINE.json config: 2 = 4096 x 4 MiB/GPU (default), 3 = one 64 GiB stream "
-                         "(exact tiled CDC), 4 = 8192 x 8 MiB/GPU, 5 = Zipf-sized files, LPT over ranks")
-    ap.add_argument("--long-gib", type=int, default=64, help="config 3 stream size")
-    ap.add_argument("--files-gib", type=int, default=32, help="config 5 bytes per GPU (256 GiB over 8 GPUs)")
-    ap.add_argument("--all-names", action="store_true", help="config 5: also time every registered name")
-    args = ap.parse_args()
-    if args.config == 4:
-        args.streams, args.stream_mib = 8192, 8
-    if args.config == 3:
-        return bench_long(args)
-    if args.config == 5:
-        return bench_files(args)
+def cpu_config1(seconds_cap: float = 12.0) -> dict:
+    """Config 1 on the host: `kopia benchmark splitter --data-size 256MiB --block-count 1
+    --rand-seed 42` (cli/command_benchmark_splitters.go:64-131) through the oracle, one
+    thread, every registered name, GB/s base-10 as the command prints them."""
+    from oracle import coracle
+    from kopia_amd import splitter as ks
+    buf = coracle.gorand_read(42, 256 << 20)
+    out, t_all = {}, time.perf_counter()
+    for nm in ks.SupportedAlgorithms():
+        t0 = time.perf_counter()
+        coracle.split_stream(nm, buf)
+        out[nm] = round(buf.size / 1e9 / (time.perf_counter() - t0), 3)
+        if time.perf_counter() - t_all > seconds_cap:
+            out["_truncated"] = True
+            break
+    return out
 
-    rank, world, local = kd.env_rank_world()
+
+# ------------------------------------------------------------- configs
+def bench_batch(args, comm: Comm):
+    """Configs 2 and 4: `streams` x `stream_mib` per GPU, one batch launch per step."""
+    import torch
+    from kopia_amd import batch
+    from kopia_amd import splitter as ks
+    rank, world = comm.rank, comm.world
+    local = env_rank_world()[2]
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
-
     name, ns, L = args.splitter, args.streams, args.stream_mib << 20
     info = ks.lookup(name)
     assert info is not None, name
@@ -135,14 +267,12 @@ def main():
     b = batch.make_device_batch(name, [data.data_ptr() + i * L for i in range(ns)], [L] * ns, dev)
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize(dev)
-
     for _ in range(args.warmup):
         batch.split_batch_device(name, b, stream)
     torch.cuda.synchronize(dev)
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if dist:
-        dist.barrier()
+    comm.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for e0, e1 in evs:
@@ -150,44 +280,29 @@ def main():
         batch.split_batch_device(name, b, stream)
         e1.record(stream)
     torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    elapsed = kd.max_over_ranks(time.perf_counter() - t0, dev)
+    own = time.perf_counter() - t0
+    comm.barrier()
+    elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
 
     cuts = batch.read_cuts(b)
-    alg_bytes = sum(rolled_bytes(c, int(info.min_size)) for c in cuts)  # per launch, this rank
-    total_bytes = ns * L * world * args.steps
-    value = total_bytes / GiB / elapsed
-
+    rolled = sum(rolled_bytes(c, int(info.min_size)) for c in cuts)
+    per = comm.gather({"bytes_per_step": ns * L, "elapsed_s": elapsed, "own_s": own, "kernel_ms": kern_ms,
+                       "rolled": rolled})
+    agg = aggregate(per, args.steps)
+    cfg = f"config{args.config}"
     out = {
-        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "metric": METRIC, "value": agg["value"], "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": agg["ms_per_step"], "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": f"config{args.config}: {ns} x {args.stream_mib} MiB independent streams per GPU "
+        "config": {"workload": f"{cfg}: {ns} x {args.stream_mib} MiB independent streams per GPU "
                                f"(counter-PRNG bytes, HBM-resident), {name}",
                    "splitter": name, "streams_per_gpu": ns, "stream_bytes": L, "global_streams": ns * world,
-                   "parallelism": f"stream-sharded x{world}, no data-path collectives"},
+                   "parallelism": f"stream-sharded x{world}, no data-path collectives (gloo timing only)"},
+        "per_gpu_gib_s": agg["per_gpu_gib_s"],
     }
-    # Roofline: algorithmic bytes = 1 byte per ingested stream byte, so
-    # `achieved` = stream bytes / kernel time.  A skip-aware kernel reads only the bytes the
-    # reference loop rolls (min-size fast path), so `frac` can exceed 1; the physical HBM
-    # figure is `traffic` (rocprofv3 FETCH_SIZE, calibrated) / kernel time.
-    traffic = load_pmc_traffic("split_batch")  # key written by tools/pmc_traffic.py
-    kern_s = kern_ms * 1e-3
-    achieved = ns * L / kern_s / 1e9
-    out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                       "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                       "kernel": BATCH_KERNEL[int(info.kind)], "kernel_ms": round(kern_ms, 4),
-                       "algorithmic_bytes_per_launch": ns * L,
-                       "algorithmic_bytes_def": "1 byte per ingested stream byte (SURVEY.md §8d): "
-                                                f"{ns} streams x {L} B per launch",
-                       "hbm_gbs_measured": round(traffic / kern_s / 1e9, 1) if traffic else None,
-                       "hbm_frac_measured": round(traffic / kern_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
-                       "rolled_bytes_per_launch": alg_bytes,
-                       "rolled_gbs": round(alg_bytes / kern_s / 1e9, 1)}
-    out["cut_stats"] = {"chunks": int(sum(c.size for c in cuts)),
-                        "rolled_fraction": round(alg_bytes / (ns * L), 4)}
+    out["roofline"] = roofline(BATCH_KERNEL[int(info.kind)], cfg, kern_ms, rolled, ns * L)
+    out["cut_stats"] = {"chunks": int(sum(c.size for c in cuts)), "rolled_fraction": round(rolled / (ns * L), 4)}
 
     if rank == 0 and world == 1 and not args.no_host_inclusive:
         # host-inclusive: pageable host buffers -> H2D -> kernel -> D2H (kcdc_split_batch_host)
@@ -203,78 +318,89 @@ def main():
         del host, views
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        nthreads = min(16, os.cpu_count() or 1)
-        sample = min(ns, max(1, (16 << 30) // L))  # bounded host sample (<= 16 GiB)
-        base, _ = cpu_baseline(name, sample, L, cuts, nthreads)
-        out["cpu_baseline"] = base
-
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if dist:
-        dist.destroy_process_group()
+        out["cpu_baseline"] = cpu_baseline(name, ns, L, cuts)
+        if args.config == 2:
+            out["cpu_baseline"]["config1_gb_s_1thread"] = cpu_config1()
+    return out
 
 
-def bench_long(args):
+def bench_long(args, comm: Comm):
     """Config 3: ONE long stream (default 64 GiB) split exactly by the tiled candidate
-    scan + device resolver; cut set checked against the per-wave sequential path.
-    Single GPU (the stream does not shard across ranks in this mode)."""
-    rank, world, local = kd.env_rank_world()
-    assert world == 1, "config 3 is a single-GPU configuration"
+    scan + device resolver.  Single GPU (on N ranks each splits its own stream)."""
+    import torch
+    from kopia_amd import batch
+    from kopia_amd import splitter as ks
+    local = env_rank_world()[2]
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     name, L = args.splitter, args.long_gib << 30
+    info = ks.lookup(name)
     data = torch.empty(L, dtype=torch.uint8, device=dev)
-    batch.fill_prng(data, L, 1, L, SEED, first_sid=0)
+    batch.fill_prng(data, L, 1, L, SEED, first_sid=comm.rank)
     stream = torch.cuda.current_stream(dev)
     cuts, count, ws = batch.split_long_device(name, data.data_ptr(), L, dev, stream)
     torch.cuda.synchronize(dev)
     steps = max(1, min(args.steps, 10))
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    comm.barrier()
     t0 = time.perf_counter()
     for e0, e1 in evs:
         e0.record(stream)
         _c, _n, _w = batch.split_long_device(name, data.data_ptr(), L, dev, stream)
         e1.record(stream)
     torch.cuda.synchronize(dev)
+    own = time.perf_counter() - t0
+    comm.barrier()
     elapsed = time.perf_counter() - t0
     ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     got = batch.read_long(cuts, count)
-    # independent check: the per-wave sequential batch path on the same bytes
-    b = batch.make_device_batch(name, [data.data_ptr()], [L], dev)
-    batch.split_batch_device(name, b, stream)
-    torch.cuda.synchronize(dev)
-    seq = batch.read_cuts(b)[0]
-    out = {"metric": METRIC, "value": round(L * steps / GiB / elapsed, 3), "unit": "GiB/s", "n_gpus": 1,
-           "steps": steps, "warmup": 1, "ms_per_step": round(elapsed / steps * 1e3, 3), "higher_is_better": True,
-           "scaling": "strong", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-           "config": {"workload": f"config3: one {args.long_gib} GiB stream, exact intra-stream tiled CDC, {name}",
-                      "splitter": name, "stream_bytes": L, "parallelism": "single GPU, 128 KiB segments/wave"},
-           "kernel_ms_events": round(ms, 3), "cuts": int(got.size),
-           "identical_to_sequential_path": bool(np.array_equal(got, seq))}
-    print(json.dumps(out), flush=True)
+    per = comm.gather({"bytes_per_step": L, "elapsed_s": elapsed, "own_s": own})
+    agg = aggregate(per, steps)
+    out = {"metric": METRIC, "value": agg["value"], "unit": "GiB/s", "n_gpus": comm.world, "steps": steps,
+           "warmup": 1, "ms_per_step": agg["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+           "config": {"workload": f"config3: one {args.long_gib} GiB stream per GPU, exact intra-stream tiled CDC, "
+                                  f"{name}", "splitter": name, "stream_bytes": L,
+                      "parallelism": "128 KiB segments per wave; one stream per GPU"},
+           "per_gpu_gib_s": agg["per_gpu_gib_s"], "kernel_ms_events": round(ms, 3), "cuts": int(got.size)}
+    # the long path scans every byte: its algorithmic bytes are the stream bytes
+    out["roofline"] = roofline("kcdc::dev::cand_scan_dma_kernel<true>", "config3", ms, L, L)
+    out["roofline"]["algorithmic_bytes_def"] = "every stream byte (the full-scan candidate pass reads each once)"
+    if comm.rank == 0 and comm.world == 1 and not args.no_cpu_baseline:
+        # the oracle's single sequential pass over the same bytes (generated on the fly)
+        from oracle import coracle
+        t0 = time.perf_counter()
+        want, cnt = coracle.split_prng_streams(name, SEED, [0], L, nthreads=1)
+        dt = time.perf_counter() - t0
+        out["oracle_parity"] = bool(np.array_equal(got, want[0, :cnt[0]]))
+        out["cpu_baseline"] = {"value": round(L / GiB / dt, 3), "unit": "GiB/s", "cores": host_cpu_info()["logical_cores"],
+                               "kind": "port", "threads_1": round(L / GiB / dt, 3),
+                               "sample": f"the whole {args.long_gib} GiB stream, one sequential pass of "
+                                         f"oracle/cdc_oracle.c (bytes generated on the fly), {name}"}
+    return out
 
 
-def bench_files(args):
+def bench_files(args, comm: Comm):
     """Config 5: file sizes from a Zipf law over 19 classes 4 KiB..1 GiB
     (s = 1.1, fixed seed), files_gib x world bytes in total, LPT-balanced over the ranks;
     every rank splits its files with kcdc_split_files_device (each file through the batch
     or the long path).  Weak scaling, no data-path collective.  FIXED names read no data."""
-    rank, world, local = kd.env_rank_world()
+    import torch
+    from kopia_amd import batch
+    from kopia_amd import dist as kd
+    from kopia_amd import splitter as ks
+    rank, world = comm.rank, comm.world
+    local = env_rank_world()[2]
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
     sizes = kd.zipf_sizes(args.files_gib * world << 30)
     mine = sorted(kd.lpt_plan(sizes, world)[rank], key=lambda i: int(sizes[i]))
     lens = [int(sizes[i]) for i in mine]
     total = sum(lens)
     data = torch.empty(total, dtype=torch.uint8, device=dev)
     offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64) if lens else np.zeros(0, np.int64)
-    # runs of equal sizes are contiguous (sorted): one fill per run, file ids = global indices
     k = 0
-    while k < len(lens):
+    while k < len(lens):  # runs of equal sizes are contiguous (sorted): one fill per run
         e = k
         while e < len(lens) and lens[e] == lens[k] and mine[e] == mine[k] + (e - k):
             e += 1
@@ -287,56 +413,108 @@ def bench_files(args):
         for _ in range(warmup):
             batch.split_files_device(name, ptrs, lens, dev, stream)
         torch.cuda.synchronize(dev)
-        if dist:
-            dist.barrier()
+        comm.barrier()
         t0 = time.perf_counter()
         res = None
         for _ in range(steps):
             res = batch.split_files_device(name, ptrs, lens, dev, stream)
         torch.cuda.synchronize(dev)
-        if dist:
-            dist.barrier()
-        return kd.max_over_ranks(time.perf_counter() - t0, dev), res
+        own = time.perf_counter() - t0
+        comm.barrier()
+        return time.perf_counter() - t0, own, res
 
     name = args.splitter
     steps = max(1, min(args.steps, 10))
-    elapsed, res = run(name, steps, max(1, min(args.warmup, 2)))
-    out = {"metric": METRIC, "value": round(total * world * steps / GiB / elapsed, 3), "unit": "GiB/s",
-           "n_gpus": world, "steps": steps, "warmup": max(1, min(args.warmup, 2)),
-           "ms_per_step": round(elapsed / steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-           "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+    elapsed, own, res = run(name, steps, max(1, min(args.warmup, 2)))
+    agg = aggregate(comm.gather({"bytes_per_step": total, "elapsed_s": elapsed, "own_s": own}), steps)
+    out = {"metric": METRIC, "value": agg["value"], "unit": "GiB/s", "n_gpus": world, "steps": steps,
+           "warmup": max(1, min(args.warmup, 2)), "ms_per_step": agg["ms_per_step"], "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
            "config": {"workload": f"config5: Zipf(s=1.1) file sizes over 4 KiB..1 GiB, {args.files_gib} GiB per GPU, "
                                   f"LPT over {world} rank(s), {name}",
                       "splitter": name, "files_this_rank": len(lens), "bytes_this_rank": total,
                       "largest_file": max(lens) if lens else 0,
-                      "parallelism": f"LPT file sharding x{world}, no data-path collectives"}}
+                      "parallelism": f"LPT file sharding x{world}, no data-path collectives"},
+           "per_gpu_gib_s": agg["per_gpu_gib_s"]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # cpu_baseline leg: the oracle's C restatement timed on a sample of this rank's files
-        # (the 64 smallest and the 2 largest), which also checks the GPU cuts of the sample
-        from oracle import coracle  # oracle import confined to this leg
+        # cpu_baseline leg: the oracle's C restatement on a sample of this rank's files
+        # (the 64 smallest, every 8th and the 2 largest), which also checks their GPU cuts
+        from oracle import coracle
         got = batch.read_files(*res)
         pick = sorted(set(range(min(64, len(lens)))) | set(range(0, len(lens), 8)) |
                       set(range(max(0, len(lens) - 2), len(lens))))
         host = [data[int(offs[i]):int(offs[i]) + lens[i]].cpu().numpy() for i in pick]
-        nthreads = min(16, os.cpu_count() or 1)
+        nt = host_cpu_info()["threads_all"]
         t0 = time.perf_counter()
-        want = coracle.split_batch(name, host, nthreads=nthreads)
+        want = coracle.split_batch(name, host, nthreads=nt)
         dt = time.perf_counter() - t0
         sb = sum(lens[i] for i in pick)
         out["cpu_baseline"] = {
-            "value": round(sb / GiB / dt, 3), "unit": "GiB/s", "cores": nthreads, "kind": "port",
+            "value": round(sb / GiB / dt, 3), "unit": "GiB/s", "cores": host_cpu_info()["logical_cores"],
+            "kind": "port", "threads_all_n": nt,
             "sample": f"{len(pick)} files of this rank (64 smallest, every 8th, 2 largest; {sb >> 20} MiB), {name}, "
-                      f"oracle/cdc_oracle.c, {nthreads} threads, {dt:.2f}s wall",
+                      f"oracle/cdc_oracle.c, {nt} threads, {dt:.2f}s wall",
             "sample_parity_mismatches": sum(1 for j, i in enumerate(pick) if not np.array_equal(got[i], want[j]))}
     if args.all_names:
         out["per_name_gib_s"] = {}
         for nm in ks.SupportedAlgorithms():
-            el, _ = run(nm, 2, 1)
+            el, _own, _ = run(nm, 2, 1)
             out["per_name_gib_s"][nm] = round(total * world * 2 / GiB / el, 2)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    return out
+
+
+def launcher_selftest(argv):
+    """Spawn + gloo timing/aggregation without a GPU (tests/test_bench_launcher.py): every
+    rank reports made-up timings, rank 0 writes the aggregate to argv[0]."""
+    rank, world, _ = env_rank_world()
+    comm = Comm(rank, world)
+    try:
+        comm.barrier()
+        per = comm.gather({"bytes_per_step": (rank + 1) << 30, "elapsed_s": 1.0 + rank, "own_s": 0.5 + rank})
+        mx = comm.max(float(rank))
+        if rank == 0:
+            with open(argv[0], "w") as f:
+                json.dump({"agg": aggregate(per, 2), "max": mx, "world": world}, f)
+    finally:
+        comm.close()
+
+
+def parse(argv):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--splitter", default="DYNAMIC-4M-BUZHASH")
+    ap.add_argument("--streams", type=int, default=4096)
+    ap.add_argument("--stream-mib", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-inclusive", action="store_true")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
+                    help="BASELINE.json config: 2 = 4096 x 4 MiB/GPU (default), 3 = one 64 GiB stream "
+                         "(exact tiled CDC), 4 = 8192 x 8 MiB/GPU, 5 = Zipf-sized files, LPT over ranks")
+    ap.add_argument("--long-gib", type=int, default=64, help="config 3 stream size")
+    ap.add_argument("--files-gib", type=int, default=32, help="config 5 bytes per GPU (256 GiB over 8 GPUs)")
+    ap.add_argument("--all-names", action="store_true", help="config 5: also time every registered name")
+    args = ap.parse_args(argv)
+    if args.config == 4:
+        args.streams, args.stream_mib = 8192, 8
+    return args
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    rank, world, _local = env_rank_world()
+    if "RANK" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus, argv)  # this process never touches a GPU
+    comm = Comm(rank, world)
+    try:
+        fn = {2: bench_batch, 4: bench_batch, 3: bench_long, 5: bench_files}[args.config]
+        out = fn(args, comm)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+    finally:
+        comm.close()
 
 
 if __name__ == "__main__":

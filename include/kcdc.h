@@ -33,6 +33,11 @@ extern "C" {
 #define KCDC_ENODEV (-19)    /* no usable gfx950 device */
 #define KCDC_EOVERFLOW (-75) /* caller-provided cut capacity too small */
 
+/* counts[i] value of every stream of a batch launch that could not complete on the
+ * device (a wave gave up waiting in the work queue): the launch's cut lists are invalid.
+ * The _host entry points return KCDC_EIO instead. */
+#define KCDC_COUNT_FAILED UINT64_MAX
+
 #define KCDC_KIND_FIXED 0
 #define KCDC_KIND_BUZHASH 1
 #define KCDC_KIND_RABINKARP 2
@@ -136,7 +141,8 @@ void kcdc_group_free(kcdc_group* g);
  * _device: every pointer (the array of stream pointers, lens, cuts, cut_base,
  * counts) is device memory on the current device; the call is asynchronous on
  * `hip_stream` (NULL = legacy default stream) except for error checking of
- * the launch.  Stream bytes may have any alignment.  Each launch takes one of 64
+ * the launch.  A launch that fails on the device sets every counts[i] to
+ * KCDC_COUNT_FAILED (no partial results are ever reported as complete).  Stream bytes may have any alignment.  Each launch takes one of 64
  * per-device queue workspaces in turn; a launch that reuses a workspace still in
  * use by another stream waits for it (an event), so any number may be in flight. */
 int kcdc_split_batch_device(const char* name, const uint8_t* const* d_ptrs, const uint64_t* d_lens,
@@ -189,6 +195,20 @@ int kcdc_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint32
  * read block after block, so consecutive blocks are one continuous read).
  * Host-only (no GPU needed). */
 int kcdc_gorand_read(int64_t seed, uint8_t* out, uint64_t n);
+
+/* ------------------------------------------------------------- testing
+ * Hooks for the library's own tests (not part of the splitter surface).
+ * kcdc_test_set: process-wide knobs read by every later batch launch.
+ *   KCDC_TEST_SPIN_CAP    polls before a waiting wave gives up (0: default, ~seconds)
+ *   KCDC_TEST_NO_STEAL    1: waves never requeue the streams of workgroups that have not started
+ *   KCDC_TEST_FORCE_ERROR 1: every batch launch reports failure (KCDC_COUNT_FAILED)
+ * kcdc_test_occupy: occupy `nwg` CUs (one workgroup with all of the CU's LDS each) for
+ * `usec` microseconds on `hip_stream`, e.g. to run a batch beside a kernel that holds CUs. */
+#define KCDC_TEST_SPIN_CAP 1
+#define KCDC_TEST_NO_STEAL 2
+#define KCDC_TEST_FORCE_ERROR 3
+int kcdc_test_set(int32_t key, int64_t value);
+int kcdc_test_occupy(uint32_t nwg, uint32_t usec, void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -22,6 +22,8 @@ KCDC_EINVAL = -22
 KCDC_EOVERFLOW = -75
 
 KIND_FIXED, KIND_BUZHASH, KIND_RABINKARP = 0, 1, 2
+COUNT_FAILED = (1 << 64) - 1  # KCDC_COUNT_FAILED: the batch launch failed on the device
+TEST_SPIN_CAP, TEST_NO_STEAL, TEST_FORCE_ERROR = 1, 2, 3
 
 
 class KcdcError(RuntimeError):
@@ -62,6 +64,8 @@ _SIGS = {
     "kcdc_group_new": (_P, [C.c_char_p, C.c_int, C.c_uint32, C.c_uint32]),
     "kcdc_group_splitter": (_P, [_P]),
     "kcdc_group_free": (None, [_P]),
+    "kcdc_test_set": (C.c_int, [C.c_int32, C.c_int64]),
+    "kcdc_test_occupy": (C.c_int, [C.c_uint32, C.c_uint32, _P]),
 }
 
 

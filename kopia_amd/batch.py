@@ -47,11 +47,18 @@ def split_batch_device(name: str, b: DeviceBatch, stream=None) -> None:
         b.cut_base.data_ptr(), b.counts.data_ptr(), C.c_void_p(stream.cuda_stream)))
 
 
+def check_counts(counts: np.ndarray) -> None:
+    """Raise if the launch that produced `counts` failed on the device (KCDC_COUNT_FAILED)."""
+    if counts.size and (counts.view(np.uint64) == np.uint64(_lib.COUNT_FAILED)).any():
+        raise _lib.KcdcError(_lib.KCDC_EIO, "batch launch failed on the device (KCDC_COUNT_FAILED)")
+
+
 def read_cuts(b: DeviceBatch) -> list[np.ndarray]:
     """Copy cut lists back (host); raises on capacity overflow."""
     cuts = b.cuts.cpu().numpy()
     counts = b.counts.cpu().numpy()[:b.n]
     base = b.cut_base.cpu().numpy()
+    check_counts(counts)
     out = []
     for i in range(b.n):
         capi = (base[i + 1] if i + 1 < b.n else b.cap) - base[i]
@@ -142,6 +149,7 @@ def read_files(cuts, counts, base, cap) -> list[np.ndarray]:
     """Cut lists of split_files_device (host); raises on capacity overflow."""
     c = cuts.cpu().numpy()
     k = counts.cpu().numpy()[:len(base)]
+    check_counts(k)
     out = []
     for i in range(len(base)):
         capi = (base[i + 1] if i + 1 < len(base) else cap) - base[i]

@@ -466,8 +466,10 @@ void group_handle_closed(kcdc_group* g) {
         std::lock_guard<std::mutex> lk(g->mu);
         g->live--;
         last = g->closing && g->live == 0;
+        // Notify while holding the mutex: once it is released, the thread that shuts the
+        // group down (the last closer, or kcdc_group_free seeing live == 0) may delete g.
+        g->cv_work.notify_all();  // a pending launch may now hold every live handle
     }
-    g->cv_work.notify_all();  // a pending launch may now hold every live handle
     if (last) group_shutdown(g);  // kcdc_group_free came first: the last handle frees the group
 }
 
@@ -559,6 +561,13 @@ extern "C" kcdc_splitter* kcdc_group_splitter(kcdc_group* g) {
         set_error(KCDC_EINVAL, "null group");
         return nullptr;
     }
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        if (g->closing) {  // kcdc_group_free was called: no new handles (kcdc.h)
+            set_error(KCDC_EINVAL, "splitter group is being freed");
+            return nullptr;
+        }
+    }
     DeviceGuard dg(g->device);
     kcdc_splitter* s = new kcdc_splitter();
     s->algo = g->algo;
@@ -570,6 +579,11 @@ extern "C" kcdc_splitter* kcdc_group_splitter(kcdc_group* g) {
         return nullptr;
     }
     std::lock_guard<std::mutex> lk(g->mu);
+    if (g->closing) {  // freed while the handle's resources were allocated
+        set_error(KCDC_EINVAL, "splitter group is being freed");
+        destroy(s);
+        return nullptr;
+    }
     s->group = g;
     g->live++;
     return s;
@@ -681,6 +695,7 @@ extern "C" int kcdc_split_batch_host(const char* name, const uint8_t* const* h_p
                     "D2H cuts");
         HIP_TRY(hipStreamSynchronize(C.stream), "sync");
         for (uint32_t k = i0; k < i1; k++) {
+            if (counts[k] == KCDC_COUNT_FAILED) return set_error(KCDC_EIO, "batch launch failed on the device");
             const uint64_t capk = (k + 1 < nstreams ? cut_base[k + 1] : cuts_cap) - cut_base[k];
             if (counts[k] > capk) return set_error(KCDC_EOVERFLOW, "cut capacity too small for a stream");
         }

@@ -680,6 +680,12 @@ struct BatchArgs {
     // "candidate" becomes h <= buz_lim (= ~mask): the hot loop's test is a bare v_min3.
     uint32_t buz_rot;
     uint32_t buz_lim;  // ~mask when mask is a top-bits mask (else unused)
+    // Persistent queue without a co-residency assumption: wg_flags[b] is 0 until workgroup b
+    // starts (1) or a waiting wave steals its preassigned streams (2) and requeues them.
+    uint32_t* wg_flags;
+    uint32_t nwg;
+    uint32_t spin_cap;     // polls before a waiting wave gives up (error word; ~seconds)
+    uint32_t steal_spins;  // polls between scans for workgroups that never started (0: off)
 };
 
 template <int KIND>
@@ -963,11 +969,15 @@ __device__ __forceinline__ uint64_t bcast64(uint64_t v) {
 }
 // Header words (uint32 offsets) 2 KiB apart: hammered counters do not share DRAM pages.
 // Word 0 holds the 64-bit {head, tail} ticket counter (kQHT, below).
-constexpr int kQDone = 512, kQErr = 1536;
+constexpr int kQDone = 512, kQErr = 1536, kQSteal = 1024;
 constexpr size_t kQHeaderBytes = 8192;
 // Header words 1792.. : debug-build failure record (pcheck, KCDC_DEBUG_CHECKS).
 [[maybe_unused]] constexpr int kQStat = 1792;
-constexpr uint32_t kSpinCap = 1u << 22;                          // give up (error word) after ~seconds
+// A waiting wave gives up (error word, the launch reports failure) only after this many polls
+// without progress of the queue (streams done, entries reserved): a bug guard that keeps the
+// kernel bounded, ~100 s; no correct launch waits that long (one wave scans >= 6 GB/s).
+constexpr uint32_t kSpinCap = 1u << 26;
+constexpr uint32_t kStealSpins = 256;                            // ~0.5 ms of polling between steal scans
 
 // ======================================================= pipelined persistent kernel
 // One per-wave state machine over tiles.  Every tile warms its 64 lanes on the 64 bytes
@@ -1218,10 +1228,61 @@ __device__ __forceinline__ uint64_t qht_take(const BatchArgs& a, int lane, uint6
     return qht_value(static_cast<uint32_t>(raw), static_cast<uint32_t>(raw >> 32));
 }
 
+__device__ __forceinline__ void pwrite(const BatchArgs& a, int lane, uint32_t e, const PStream& st, bool tomb);
+
+// Forward progress without co-residency.  Each wave's first ticket is preassigned (its global
+// wave index, init_ring_kernel), so a workgroup that is not resident -- another kernel holds
+// its CU -- would keep its streams while the resident waves wait for them.  A wave that has
+// waited kStealSpins polls scans the workgroup flags; for a workgroup that has not started it
+// swaps the flag 0 -> 2 and requeues that workgroup's preassigned streams as fresh ring
+// entries (their initial states, rebuilt from the batch arrays).  A workgroup that starts
+// later finds its flag at 2 and takes its tickets from the counter.  A waiting wave then
+// waits only on entries reserved by running waves (written without blocking) or on streams
+// held by running waves, so every wait ends.
+__device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
+    uint32_t found = 0xFFFFFFFFu;
+    for (uint32_t b0 = 0; b0 < a.nwg; b0 += kWave) {
+        const uint32_t b = b0 + static_cast<uint32_t>(lane);
+        const uint32_t f = b < a.nwg ? ld_agent(a.wg_flags + b) : 1u;
+        const uint64_t m = __ballot(f == 0u);
+        if (m) {
+            found = b0 + static_cast<uint32_t>(__builtin_ctzll(m));
+            break;
+        }
+    }
+    found = __builtin_amdgcn_readfirstlane(found);
+    if (found == 0xFFFFFFFFu) return false;
+    uint32_t old = 1u;
+    if (lane == 0) {
+        old = 0u;
+        __hip_atomic_compare_exchange_strong((gu32*)(a.wg_flags + found), &old, 2u, __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (bcast(old) != 0u) return false;  // it started (or another wave stole it) meanwhile
+    const uint32_t first = found * wg_waves;
+    const uint32_t k = first >= a.nstreams ? 0u : min(wg_waves, a.nstreams - first);
+    if (k == 0) return true;
+    const uint64_t ht = qht_take(a, lane, static_cast<uint64_t>(k) << 32);  // reserve k entries
+    const uint32_t e0 = static_cast<uint32_t>(ht >> 32);
+    for (uint32_t i = 0; i < k; i++) {
+        const uint32_t sid = first + i;
+        PStream st;
+        const uint64_t cb = uni64(a.cut_base[sid]);
+        pstream_fresh(st, sid, uni64(reinterpret_cast<uint64_t>(a.ptrs[sid])), uni64(a.lens[sid]), cb,
+                      sid + 1 < a.nstreams ? uni64(a.cut_base[sid + 1]) : a.cuts_cap);
+        uniformize(st);
+        pwrite(a, lane, e0 + i, st, false);
+    }
+    if (lane == 0) add_agent(a.queue + kQSteal, 1u);
+    return true;
+}
+
 // Blocking resolution of ticket t (its ring entry, polled): 1 resolved, 2 tombstone (take
-// another ticket), 0 every stream is done (the wave exits).
-__device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st) {
+// another ticket), 0 every stream is done, or the wave gave up (error word) -- it exits.
+__device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, uint32_t wg_waves) {
     const uint32_t n = a.nstreams;
+    uint32_t idle = 0;            // polls since the queue last moved
+    uint64_t seen = ~0ull;        // lane 0: {done, tail} at the last poll
     for (uint32_t spin = 0;; spin++) {
         const u32x4 v = pentry_load(a, lane, t);
         if (pentry_ok(v, lane, t)) {
@@ -1231,14 +1292,24 @@ __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st) {
         }
         uint32_t stop = 0;
         if (lane == 0) {
-            if (ld_agent(a.queue + kQDone) >= n) {
+            const uint32_t done = ld_agent(a.queue + kQDone);
+            const uint32_t tail = static_cast<uint32_t>(ld_agent64(reinterpret_cast<uint64_t*>(a.queue + kQHT)) >> 32);
+            const uint64_t now = (static_cast<uint64_t>(done) << 32) | tail;
+            idle = now == seen ? idle + 1 : 0;
+            seen = now;
+            if (done >= n) {
                 stop = 1;
-            } else if (spin >= kSpinCap) {
+            } else if (idle >= a.spin_cap) {
                 add_agent(a.queue + kQErr, 1u);
                 stop = 1;
             }
         }
         if (bcast(stop)) return 0;
+        if (a.steal_spins && spin % a.steal_spins == a.steal_spins - 1) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA is in flight here either
+            try_steal(a, lane, wg_waves);
+            continue;  // poll the entry again at once
+        }
         __builtin_amdgcn_s_sleep(16);
     }
 }
@@ -1393,7 +1464,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                 backlog = static_cast<int64_t>(ht >> 32) - static_cast<int64_t>(t) - 1;
             }
             const uint32_t held = t;
-            const int r = presolve(a, lane, held, cur);
+            const int r = presolve(a, lane, held, cur, kDmaWaves);
             if (r == 0) return false;
             t = 0xFFFFFFFFu;
             if (r == 2) continue;  // tombstone
@@ -1409,9 +1480,19 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         }
     };
     {
-        const uint32_t gw0 = blockIdx.x * kDmaWaves + wave;  // first ticket: preassigned (see init_ring_kernel)
+        // First ticket: preassigned (see init_ring_kernel), unless a waiting wave has stolen
+        // this workgroup's streams before it started (try_steal): then take one from the counter.
+        uint32_t f0 = 1u;
+        if (lane == 0) {
+            f0 = 0u;
+            __hip_atomic_compare_exchange_strong((gu32*)(a.wg_flags + blockIdx.x), &f0, 1u, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const bool stolen = bcast(f0) == 2u;
+        const uint32_t gw0 = blockIdx.x * kDmaWaves + wave;
         const int64_t nw = static_cast<int64_t>(gridDim.x) * kDmaWaves;
-        if (!take_blocking(gw0 < a.nstreams ? gw0 : 0xFFFFFFFFu, static_cast<int64_t>(a.nstreams) - nw)) KCDC_PRET;
+        if (!take_blocking(!stolen && gw0 < a.nstreams ? gw0 : 0xFFFFFFFFu, static_cast<int64_t>(a.nstreams) - nw))
+            KCDC_PRET;
     }
     bool issued = false;  // this tile's warm piece + step 0 are in flight
     for (;;) {
@@ -1747,6 +1828,17 @@ __global__ void init_ring_kernel(BatchArgs a, uint32_t nslots, uint32_t nwaves) 
         const u32x4 z = {0, 0, 0, 0};
         *reinterpret_cast<u32x4*>(reinterpret_cast<uint32_t*>(a.states) + 4ull * e) = z;
     }
+    if (i < a.nwg) a.wg_flags[i] = 0u;  // no workgroup has started
+}
+
+// After each pipelined launch: a launch that did not finish every stream (a wave gave up
+// waiting, KCDC_DEBUG_CHECKS failure) marks every count of the batch as failed, so no caller
+// can read partial or stale cut lists as a result (kcdc.h, KCDC_COUNT_FAILED).
+__global__ void check_queue_kernel(BatchArgs a) {
+    const bool bad = a.queue[kQErr] != 0u || a.queue[kQDone] != a.nstreams;
+    if (!bad) return;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.nstreams; i += gridDim.x * blockDim.x)
+        a.counts[i] = ~0ull;
 }
 
 // FIXED-*: cuts every chunk length (splitter_fixed.go:15-26); reads no data.
@@ -2378,6 +2470,21 @@ __global__ __launch_bounds__(1024) void resolve_par_kernel(LongArgs g, int64_t m
     if (tid == 0) S.count[0] = s_carry;
 }
 
+// Test support (kcdc_test_occupy): hold `nwg` CUs -- one workgroup each, all of the CU's
+// LDS -- for `us` microseconds of the 100 MHz constant clock, then exit (bounded).
+__global__ __launch_bounds__(64) void occupy_kernel(uint64_t ticks, uint32_t* sink) {
+    extern __shared__ uint32_t hold[];
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t x = threadIdx.x;
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+        __builtin_amdgcn_s_sleep(127);
+        x = x * 1664525u + 1013904223u;
+    }
+    hold[threadIdx.x] = x;
+    __syncthreads();
+    if (hold[(threadIdx.x + 1) & 63] == 0x12345678u) sink[0] = x;  // keeps the loop and the LDS live
+}
+
 }  // namespace dev
 
 // ================================================================== host
@@ -2408,6 +2515,14 @@ unsigned g_queue_next[kMaxDevices];
 std::mutex g_dev_mu;
 
 int hip_fail(hipError_t e, const char* what) { return set_error(-5, std::string(what) + ": " + hipGetErrorString(e)); }
+
+// Test hooks (kcdc_test_set, include/kcdc.h "testing"): read by every later launch.
+struct TestKnobs {
+    uint32_t spin_cap = 0;     // 0: dev::kSpinCap
+    bool no_steal = false;     // disable try_steal
+    bool force_error = false;  // mark every pipelined launch as failed
+};
+TestKnobs g_test;
 
 // Rotated buzhash frame for a reference mask (avg - 1).  A contiguous low mask of k bits
 // (avg a power of two, the registered splitters) rotates to the top k bits: rot = 32 - k,
@@ -2542,7 +2657,8 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         while (ring <= live) ring <<= 1;
         const size_t ring_bytes = dma ? static_cast<size_t>(dev::kPEntryStride) * ring : 0;
         const size_t hdr = dev::kQHeaderBytes;
-        const size_t bytes = hdr + ring_bytes + (dma ? 24ull * s.nstreams : 0);
+        const size_t states_bytes = dma ? ((24ull * s.nstreams + 255) & ~size_t(255)) : 0;
+        const size_t bytes = hdr + ring_bytes + states_bytes + (dma ? 4ull * grid : 0);
         char* ws = nullptr;
         // The slot stays locked from its selection to its event record, so a later user of the
         // same slot always waits for this launch.
@@ -2583,6 +2699,10 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         a.ring = reinterpret_cast<uint32_t*>(ws + hdr);
         a.states = reinterpret_cast<uint64_t*>(ws + hdr + ring_bytes);
         a.ring_mask = static_cast<uint32_t>(ring - 1);
+        a.wg_flags = reinterpret_cast<uint32_t*>(ws + hdr + ring_bytes + states_bytes);
+        a.nwg = grid;
+        a.spin_cap = g_test.spin_cap ? g_test.spin_cap : dev::kSpinCap;
+        a.steal_spins = g_test.no_steal ? 0u : dev::kStealSpins;
 #if KCDC_TRACE
         if (trace_reserve(std::max<uint64_t>(s.nstreams, 2ull * grid * wg_waves)) != 0) return set_error(-12, "trace buffer");
         a.trace = g_trace;
@@ -2590,7 +2710,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         // header + ring zeroed per launch (the ring is also left empty by every finished launch)
         if (dma) {
             const uint32_t slots = static_cast<uint32_t>(ring);
-            const uint64_t threads = std::max<uint64_t>(8ull * slots, dev::kQHeaderBytes / 4);
+            const uint64_t threads = std::max<uint64_t>(std::max<uint64_t>(8ull * slots, dev::kQHeaderBytes / 4), grid);
             hipLaunchKernelGGL(dev::init_ring_kernel, dim3(static_cast<unsigned>((threads + 255) / 256)), dim3(256), 0, st, a,
                                slots, grid * wg_waves);
         } else {
@@ -2606,6 +2726,12 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
             else
                 hipLaunchKernelGGL(dev::split_batch_pipe_kernel<false>, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0,
                                    st, a);
+            if (g_test.force_error) {  // test hook: report a failed launch (kcdc_test_set)
+                const hipError_t e = hipMemsetAsync(ws + 4 * dev::kQErr, 0xFF, 4, st);
+                if (e != hipSuccess) return hip_fail(e, "test hook");
+            }
+            hipLaunchKernelGGL(dev::check_queue_kernel, dim3(std::min<unsigned>((s.nstreams + 255) / 256, 256u)), dim3(256),
+                               0, st, a);
         } else {
             const dim3 block(dev::kBatchWaves * dev::kWave);
             if (algo.kind == kBuzhash)
@@ -2823,6 +2949,32 @@ int launch_split_long(const Algo& algo, const uint8_t* d_data, uint64_t len, uin
                       uint64_t* d_count, void* ws, size_t ws_bytes, int device, void* stream) {
     return launch_split_long_multi(algo, 1, &d_data, &len, &d_cuts, &cuts_cap, &d_count, ws, ws_bytes, device,
                                    stream);
+}
+
+// ------------------------------------------------------------------ testing
+extern "C" int kcdc_test_set(int32_t key, int64_t value) {
+    switch (key) {
+        case 1: g_test.spin_cap = static_cast<uint32_t>(value); return 0;   // KCDC_TEST_SPIN_CAP
+        case 2: g_test.no_steal = value != 0; return 0;                     // KCDC_TEST_NO_STEAL
+        case 3: g_test.force_error = value != 0; return 0;                  // KCDC_TEST_FORCE_ERROR
+        default: return set_error(-22, "unknown test knob");
+    }
+}
+
+extern "C" int kcdc_test_occupy(uint32_t nwg, uint32_t usec, void* stream) {
+    if (nwg == 0) return 0;
+    if (usec > 10u * 1000u * 1000u) return set_error(-22, "occupy: at most 10 s");
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(dev::occupy_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return hip_fail(e, "occupy attribute");
+    uint32_t* sink = nullptr;
+    e = hipMallocAsync(reinterpret_cast<void**>(&sink), 4, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "occupy sink");
+    hipLaunchKernelGGL(dev::occupy_kernel, dim3(nwg), dim3(64), 160 * 1024, static_cast<hipStream_t>(stream),
+                       static_cast<uint64_t>(usec) * 100u, sink);
+    e = hipGetLastError();
+    (void)hipFreeAsync(sink, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : hip_fail(e, "occupy launch");
 }
 
 }  // namespace kcdc

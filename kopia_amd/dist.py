@@ -1,6 +1,6 @@
 """Multi-GPU host logic: one process per GPU, streams sharded with no data-path
 collective.  The only collectives are the timing barrier and the
-max-over-ranks of elapsed time.
+max-over-ranks of elapsed time, over gloo (CPU); no RCCL.
 
 * Static sharding (configs 2 and 4): rank r owns stream ids [r*per, (r+1)*per).
 * LPT balancing (config 5, Zipf file sizes): streams sorted by size descending,
@@ -56,11 +56,12 @@ def zipf_sizes(total_bytes: int, seed: int = 0x5A1F, s: float = 1.1, classes: in
 
 
 def max_over_ranks(value: float, device=None) -> float:
-    """All-reduce MAX of a scalar (the bench's elapsed time); identity when not distributed."""
+    """All-reduce MAX of a scalar (the bench's elapsed time) over the CPU (gloo) process
+    group; identity when not distributed.  `device` is unused (kept for callers)."""
     import torch
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

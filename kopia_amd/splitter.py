@@ -15,6 +15,7 @@ read like repo/splitter/splitter_test.go.
 from __future__ import annotations
 
 import ctypes as C
+import threading
 from typing import Callable, Optional
 
 from . import _lib
@@ -107,6 +108,7 @@ class SplitterGroup:
             raise _lib.KcdcError(_lib.KCDC_EINVAL, _lib.last_error())
         self._g = g
         self.name = name
+        self._close_mu = threading.Lock()
 
     def splitter(self) -> Splitter:
         h = _lib.lib().kcdc_group_splitter(self._g)
@@ -119,10 +121,12 @@ class SplitterGroup:
 
     def close(self) -> None:
         """Free the group; splitters still open keep working, and the last one to close
-        releases it."""
-        if self._g:
-            _lib.lib().kcdc_group_free(self._g)
-            self._g = None
+        releases it.  Safe to call from several threads (the handle is swapped out under a
+        lock, so it is freed once); close() must not race splitter()."""
+        with self._close_mu:
+            g, self._g = self._g, None
+        if g:
+            _lib.lib().kcdc_group_free(g)
 
     def __del__(self):
         try:

@@ -1,0 +1,147 @@
+"""The batch kernel's persistent work queue: failures are loud, and progress does not
+depend on every workgroup of the persistent grid being resident at once.
+
+Reference contract: NextSplitPoint has no error channel (repo/splitter/splitter.go:25),
+so the library must never hand back a cut list it did not finish (kcdc.h,
+KCDC_COUNT_FAILED)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from kopia_amd import _lib, batch
+from oracle import coracle
+
+pytestmark = pytest.mark.gpu
+SEED = 0x6B6F706961
+NAME = "DYNAMIC-4M-BUZHASH"
+
+
+class knob:
+    def __init__(self, key, value):
+        self.key, self.value = key, value
+
+    def __enter__(self):
+        assert _lib.lib().kcdc_test_set(self.key, self.value) == 0
+
+    def __exit__(self, *exc):
+        _lib.lib().kcdc_test_set(self.key, 0)
+
+
+def _streams(gpu, ns, L, first_sid=0):
+    import torch
+    data = torch.empty(ns * L, dtype=torch.uint8, device=gpu)
+    batch.fill_prng(data, L, ns, L, SEED, first_sid=first_sid)
+    return data, batch.make_device_batch(NAME, [data.data_ptr() + i * L for i in range(ns)], [L] * ns, gpu)
+
+
+def _oracle(ns, L, first_sid=0):
+    cuts, counts = coracle.split_prng_streams(NAME, SEED, np.arange(first_sid, first_sid + ns), L, nthreads=16)
+    return [cuts[i, :counts[i]] for i in range(ns)]
+
+
+def test_failed_launch_is_reported(gpu):
+    """A launch marked failed on the device (test hook) sets every count to
+    KCDC_COUNT_FAILED: the device path raises on read, the host path returns EIO."""
+    import torch
+    ns, L = 64, 1 << 20
+    data, b = _streams(gpu, ns, L)
+    with knob(_lib.TEST_FORCE_ERROR, 1):
+        batch.split_batch_device(NAME, b)
+        torch.cuda.synchronize()
+        counts = b.counts.cpu().numpy()[:ns].view(np.uint64)
+        assert (counts == np.uint64(_lib.COUNT_FAILED)).all()
+        with pytest.raises(_lib.KcdcError) as e:
+            batch.read_cuts(b)
+        assert e.value.code == _lib.KCDC_EIO
+        host = data[: 4 * L].cpu().numpy()
+        with pytest.raises(_lib.KcdcError) as e:
+            batch.split_batch_host(NAME, [host[i * L:(i + 1) * L] for i in range(4)])
+        assert e.value.code == _lib.KCDC_EIO
+    # the next launch is clean again
+    batch.split_batch_device(NAME, b)
+    torch.cuda.synchronize()
+    got = batch.read_cuts(b)
+    want = _oracle(ns, L)
+    assert all(np.array_equal(got[i], want[i]) for i in range(ns))
+
+
+def test_waiting_wave_give_up_is_reported(gpu):
+    """With a one-poll cap, waves that wait for work give up: the error word must turn
+    into KCDC_COUNT_FAILED, never into a silently partial result."""
+    import torch
+    ns, L = 4096, 1 << 20
+    _data, b = _streams(gpu, ns, L)
+    with knob(_lib.TEST_SPIN_CAP, 1), knob(_lib.TEST_NO_STEAL, 1):
+        batch.split_batch_device(NAME, b)
+        torch.cuda.synchronize()
+        with pytest.raises(_lib.KcdcError) as e:
+            batch.read_cuts(b)
+        assert e.value.code == _lib.KCDC_EIO
+
+
+def _beside_occupier(gpu, nwg, usec):
+    """Run a 4096 x 4 MiB launch on one stream while a kernel on another stream holds
+    `nwg` CUs for `usec`; returns (cut lists, batch end, occupier end) in ms after start."""
+    import time
+
+    import torch
+    ns, L = 4096, 4 << 20
+    _data, b = _streams(gpu, ns, L)
+    batch.split_batch_device(NAME, b)  # warm (tables, workspaces)
+    torch.cuda.synchronize()
+    sa, sb = torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)
+    t0 = torch.cuda.Event(enable_timing=True)
+    ea = torch.cuda.Event(enable_timing=True)
+    eb = torch.cuda.Event(enable_timing=True)
+    t0.record(sa)
+    sb.wait_event(t0)
+    _lib.check(_lib.lib().kcdc_test_occupy(nwg, usec, C.c_void_p(sa.cuda_stream)))
+    ea.record(sa)
+    time.sleep(0.005)  # the occupier is resident before the batch is dispatched
+    batch.split_batch_device(NAME, b, sb)
+    eb.record(sb)
+    torch.cuda.synchronize()
+    return batch.read_cuts(b), t0.elapsed_time(eb), t0.elapsed_time(ea)
+
+
+def test_batch_beside_occupying_kernel_steals(gpu):
+    """Half the CUs are held for 300 ms: the batch's workgroups there cannot start, their
+    preassigned streams are requeued by waiting waves, and the launch finishes (with
+    every stream bit-exact) long before the occupier does."""
+    got, t_batch, t_occ = _beside_occupier(gpu, 128, 300_000)
+    want = _oracle(4096, 4 << 20)
+    bad = [i for i in range(4096) if not np.array_equal(got[i], want[i])]
+    assert not bad, f"{len(bad)} streams differ, first {bad[:5]}"
+    assert t_occ > 250.0, t_occ
+    assert t_batch < 0.5 * t_occ, (t_batch, t_occ)
+
+
+def test_batch_beside_occupying_kernel_no_steal(gpu):
+    """Without stealing the same launch waits for the occupied CUs (no deadlock, no
+    give-up) and is still exact."""
+    with knob(_lib.TEST_NO_STEAL, 1):
+        got, t_batch, t_occ = _beside_occupier(gpu, 128, 100_000)
+    want = _oracle(4096, 4 << 20)
+    assert all(np.array_equal(got[i], want[i]) for i in range(4096))
+    assert t_batch >= 0.9 * t_occ, (t_batch, t_occ)
+
+
+def test_highest_device_index(gpu):
+    """Per-device state (tables, queue workspaces, host staging) on the highest visible
+    device; with several devices, device 0 and the last one in the same process agree."""
+    import torch
+    ndev = torch.cuda.device_count()
+    ns, L = 256, 4 << 20
+    want = _oracle(ns, L, first_sid=7)
+    for d in sorted({0, ndev - 1}):
+        dev = torch.device("cuda", d)
+        with torch.cuda.device(dev):
+            _data, b = _streams(dev, ns, L, first_sid=7)
+            batch.split_batch_device(NAME, b)
+            torch.cuda.synchronize(dev)
+            got = batch.read_cuts(b)
+        assert all(np.array_equal(got[i], want[i]) for i in range(ns)), f"device {d}"
+        host = [coracle.gen_stream(SEED, 7 + i, L) for i in range(4)]
+        hc = batch.split_batch_host(NAME, host, device=d)
+        assert all(np.array_equal(hc[i], want[i]) for i in range(4)), f"device {d} host path"

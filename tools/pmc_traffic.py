@@ -1,6 +1,9 @@
 """Turn a rocprofv3 `--pmc FETCH_SIZE` pass into per-launch HBM read bytes.
 
-usage: python tools/pmc_traffic.py <run_counter_collection.csv> <kernel substring> [out.json]
+usage: python tools/pmc_traffic.py <run_counter_collection.csv> <kernel> <config> [out.json]
+
+The entry is keyed "<kernel>|<config>" (e.g. "kcdc::dev::split_batch_pipe_kernel<true>|config2"),
+which is what bench.py looks up for that configuration's roofline.
 
 FETCH_SIZE is reported in KiB and derives from TCC_EA0_RDREQ x 64 B; on gfx950 a
 wide (16 B/lane) read is tallied at half its bytes (/opt/skills/guides/
@@ -16,12 +19,13 @@ import sys
 
 
 def main():
-    path, key = sys.argv[1], sys.argv[2]
-    out = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_traffic.json"
+    path, kernel, config = sys.argv[1], sys.argv[2], sys.argv[3]
+    out = sys.argv[4] if len(sys.argv) > 4 else "profiles/pmc_traffic.json"
+    key = f"{kernel}|{config}"
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if key in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE"]
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE"]
     if not vals:
-        sys.exit(f"no FETCH_SIZE rows for kernels matching {key!r}")
+        sys.exit(f"no FETCH_SIZE rows for kernels matching {kernel!r}")
     kib = statistics.median(vals)
     try:
         d = json.load(open(out))
