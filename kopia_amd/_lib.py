@@ -11,7 +11,8 @@ import os
 from functools import lru_cache
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libkcdc.so")
+# KCDC_LIB: an alternative build of the same library (A/B experiments, tools/gpu_ab.sh)
+LIB_PATH = os.environ.get("KCDC_LIB") or os.path.join(HERE, "libkcdc.so")
 
 KCDC_OK = 0
 KCDC_ENOENT = -2

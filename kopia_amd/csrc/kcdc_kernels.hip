@@ -680,12 +680,6 @@ struct BatchArgs {
     // "candidate" becomes h <= buz_lim (= ~mask): the hot loop's test is a bare v_min3.
     uint32_t buz_rot;
     uint32_t buz_lim;  // ~mask when mask is a top-bits mask (else unused)
-    // Persistent queue without a co-residency assumption: wg_flags[b] is 0 until workgroup b
-    // starts (1) or a waiting wave steals its preassigned streams (2) and requeues them.
-    uint32_t* wg_flags;
-    uint32_t nwg;
-    uint32_t spin_cap;     // polls before a waiting wave gives up (error word; ~seconds)
-    uint32_t steal_spins;  // polls between scans for workgroups that never started (0: off)
 };
 
 template <int KIND>
@@ -970,6 +964,11 @@ __device__ __forceinline__ uint64_t bcast64(uint64_t v) {
 // Header words (uint32 offsets) 2 KiB apart: hammered counters do not share DRAM pages.
 // Word 0 holds the 64-bit {head, tail} ticket counter (kQHT, below).
 constexpr int kQDone = 512, kQErr = 1536, kQSteal = 1024;
+// Rarely read words (kept out of the kernel arguments, whose SGPRs the hot loop needs):
+// kQCfg+0 spin cap, kQCfg+1 steal period; kQFlags.. one flag per workgroup (grid <= 256):
+// 0 until workgroup b starts (1) or a waiting wave requeues its preassigned streams (2).
+constexpr int kQCfg = 1040, kQFlags = 1088;
+constexpr uint32_t kMaxPipeGrid = 256;
 constexpr size_t kQHeaderBytes = 8192;
 // Header words 1792.. : debug-build failure record (pcheck, KCDC_DEBUG_CHECKS).
 [[maybe_unused]] constexpr int kQStat = 1792;
@@ -1229,6 +1228,9 @@ __device__ __forceinline__ uint64_t qht_take(const BatchArgs& a, int lane, uint6
 }
 
 __device__ __forceinline__ void pwrite(const BatchArgs& a, int lane, uint32_t e, const PStream& st, bool tomb);
+#ifndef KCDC_STEAL
+#define KCDC_STEAL 1
+#endif
 
 // Forward progress without co-residency.  Each wave's first ticket is preassigned (its global
 // wave index, init_ring_kernel), so a workgroup that is not resident -- another kernel holds
@@ -1241,9 +1243,11 @@ __device__ __forceinline__ void pwrite(const BatchArgs& a, int lane, uint32_t e,
 // held by running waves, so every wait ends.
 __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
     uint32_t found = 0xFFFFFFFFu;
-    for (uint32_t b0 = 0; b0 < a.nwg; b0 += kWave) {
+    uint32_t* const flags = a.queue + kQFlags;
+    const uint32_t nwg = gridDim.x;
+    for (uint32_t b0 = 0; b0 < nwg; b0 += kWave) {
         const uint32_t b = b0 + static_cast<uint32_t>(lane);
-        const uint32_t f = b < a.nwg ? ld_agent(a.wg_flags + b) : 1u;
+        const uint32_t f = b < nwg ? ld_agent(flags + b) : 1u;
         const uint64_t m = __ballot(f == 0u);
         if (m) {
             found = b0 + static_cast<uint32_t>(__builtin_ctzll(m));
@@ -1255,7 +1259,7 @@ __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
     uint32_t old = 1u;
     if (lane == 0) {
         old = 0u;
-        __hip_atomic_compare_exchange_strong((gu32*)(a.wg_flags + found), &old, 2u, __ATOMIC_RELAXED,
+        __hip_atomic_compare_exchange_strong((gu32*)(flags + found), &old, 2u, __ATOMIC_RELAXED,
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (bcast(old) != 0u) return false;  // it started (or another wave stole it) meanwhile
@@ -1281,6 +1285,7 @@ __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
 // another ticket), 0 every stream is done, or the wave gave up (error word) -- it exits.
 __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, uint32_t wg_waves) {
     const uint32_t n = a.nstreams;
+    const uint32_t spin_cap = ld_agent(a.queue + kQCfg), steal_spins = ld_agent(a.queue + kQCfg + 1);
     uint32_t idle = 0;            // polls since the queue last moved
     uint64_t seen = ~0ull;        // lane 0: {done, tail} at the last poll
     for (uint32_t spin = 0;; spin++) {
@@ -1299,13 +1304,13 @@ __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, u
             seen = now;
             if (done >= n) {
                 stop = 1;
-            } else if (idle >= a.spin_cap) {
+            } else if (idle >= spin_cap) {
                 add_agent(a.queue + kQErr, 1u);
                 stop = 1;
             }
         }
         if (bcast(stop)) return 0;
-        if (a.steal_spins && spin % a.steal_spins == a.steal_spins - 1) {
+        if (KCDC_STEAL && steal_spins && spin % steal_spins == steal_spins - 1) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA is in flight here either
             try_steal(a, lane, wg_waves);
             continue;  // poll the entry again at once
@@ -1442,6 +1447,11 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
     PStream cur;
     int64_t budget = kNoYield;
     bool dry = false;  // the queue was (nearly) dry when this stream was taken: probes may pay
+    // Claim of this workgroup's preassigned tickets: lane 0's CAS result (0 or 1: ours, 2: the
+    // streams were requeued by try_steal).  Issued before the first resolve and checked after
+    // it, so its round trip overlaps the entry load; nothing is changed before the check.
+    uint32_t claim = 1u;
+    bool check_claim = false;
     // Blocking take of the next stream with a region to scan (t: a ticket already held,
     // or ~0u to take one); false when every stream is done.  No LDS-DMA may be in flight.
     auto take_blocking = [&](uint32_t t, int64_t backlog_hint) -> bool {
@@ -1467,6 +1477,10 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             const int r = presolve(a, lane, held, cur, kDmaWaves);
             if (r == 0) return false;
             t = 0xFFFFFFFFu;
+            if (check_claim) {
+                check_claim = false;
+                if (bcast(claim) == 2u) continue;  // requeued by another wave: take a fresh ticket
+            }
             if (r == 2) continue;  // tombstone
             uniformize(cur);
             if (!pcheck(a, lane, cur, held, 1)) return false;
@@ -1480,19 +1494,17 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         }
     };
     {
-        // First ticket: preassigned (see init_ring_kernel), unless a waiting wave has stolen
+        // First ticket: preassigned (see init_ring_kernel), unless a waiting wave has requeued
         // this workgroup's streams before it started (try_steal): then take one from the counter.
-        uint32_t f0 = 1u;
         if (lane == 0) {
-            f0 = 0u;
-            __hip_atomic_compare_exchange_strong((gu32*)(a.wg_flags + blockIdx.x), &f0, 1u, __ATOMIC_RELAXED,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            claim = 0u;
+            __hip_atomic_compare_exchange_strong((gu32*)(a.queue + kQFlags + blockIdx.x), &claim, 1u,
+                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        const bool stolen = bcast(f0) == 2u;
         const uint32_t gw0 = blockIdx.x * kDmaWaves + wave;
         const int64_t nw = static_cast<int64_t>(gridDim.x) * kDmaWaves;
-        if (!take_blocking(!stolen && gw0 < a.nstreams ? gw0 : 0xFFFFFFFFu, static_cast<int64_t>(a.nstreams) - nw))
-            KCDC_PRET;
+        check_claim = gw0 < a.nstreams;
+        if (!take_blocking(gw0 < a.nstreams ? gw0 : 0xFFFFFFFFu, static_cast<int64_t>(a.nstreams) - nw)) KCDC_PRET;
     }
     bool issued = false;  // this tile's warm piece + step 0 are in flight
     for (;;) {
@@ -1800,12 +1812,18 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
 // 0..n-1 = every stream's initial state; later entries get tag 0 (never a valid tag).
 // Head starts at min(n, launch waves): wave w's first ticket is w, taken without an atomic
 // (2048 waves hitting one counter at launch serialised for ~100 us).
-__global__ void init_ring_kernel(BatchArgs a, uint32_t nslots, uint32_t nwaves) {
+__global__ void init_ring_kernel(BatchArgs a, uint32_t nslots, uint32_t nwaves, uint32_t spin_cap,
+                                 uint32_t steal_spins) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < kQHeaderBytes / 4)
+    if (i < kQHeaderBytes / 4)  // (workgroup flags kQFlags.. start at 0: none has started)
         a.queue[i] = i == static_cast<uint32_t>(kQHT) + 1u ? a.nstreams  // tail = n
                    : i == static_cast<uint32_t>(kQHT) ? (nwaves < a.nstreams ? nwaves : a.nstreams)
+                   : i == static_cast<uint32_t>(kQCfg) ? spin_cap
+                   : i == static_cast<uint32_t>(kQCfg) + 1u ? steal_spins
                                                       : 0u;
+    // Every count starts as KCDC_COUNT_FAILED and is overwritten when its stream finishes: a
+    // launch that loses a stream (a wave gave up waiting) can never report it as split.
+    if (i < a.nstreams) a.counts[i] = ~0ull;
     if (i >= nslots * 8u) return;
     const uint32_t e = i >> 3, g = i & 7u;
     u32x4 v = {0, 0, 0, 0};
@@ -1828,15 +1846,10 @@ __global__ void init_ring_kernel(BatchArgs a, uint32_t nslots, uint32_t nwaves) 
         const u32x4 z = {0, 0, 0, 0};
         *reinterpret_cast<u32x4*>(reinterpret_cast<uint32_t*>(a.states) + 4ull * e) = z;
     }
-    if (i < a.nwg) a.wg_flags[i] = 0u;  // no workgroup has started
 }
 
-// After each pipelined launch: a launch that did not finish every stream (a wave gave up
-// waiting, KCDC_DEBUG_CHECKS failure) marks every count of the batch as failed, so no caller
-// can read partial or stale cut lists as a result (kcdc.h, KCDC_COUNT_FAILED).
-__global__ void check_queue_kernel(BatchArgs a) {
-    const bool bad = a.queue[kQErr] != 0u || a.queue[kQDone] != a.nstreams;
-    if (!bad) return;
+// Test hook (KCDC_TEST_FORCE_ERROR): mark a finished launch as failed.
+__global__ void poison_counts_kernel(BatchArgs a) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.nstreams; i += gridDim.x * blockDim.x)
         a.counts[i] = ~0ull;
 }
@@ -2649,7 +2662,8 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         const bool dma = algo.kind == kBuzhash && KCDC_DMA;
         const unsigned wg_waves = dma ? dev::kDmaWaves : dev::kBatchWaves;
         const unsigned need = (s.nstreams + wg_waves - 1) / wg_waves;
-        const unsigned grid = need < cus ? need : cus;
+        unsigned grid = need < cus ? need : cus;
+        if (dma && grid > dev::kMaxPipeGrid) grid = dev::kMaxPipeGrid;  // one claim flag per workgroup
         uint64_t ring = 1;
         // every push (yields, probes, tombstones) takes a fresh slot; a launch pushes at most
         // a few entries per wave beyond the initial n: size the ring with ample margin
@@ -2657,8 +2671,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         while (ring <= live) ring <<= 1;
         const size_t ring_bytes = dma ? static_cast<size_t>(dev::kPEntryStride) * ring : 0;
         const size_t hdr = dev::kQHeaderBytes;
-        const size_t states_bytes = dma ? ((24ull * s.nstreams + 255) & ~size_t(255)) : 0;
-        const size_t bytes = hdr + ring_bytes + states_bytes + (dma ? 4ull * grid : 0);
+        const size_t bytes = hdr + ring_bytes + (dma ? 24ull * s.nstreams : 0);
         char* ws = nullptr;
         // The slot stays locked from its selection to its event record, so a later user of the
         // same slot always waits for this launch.
@@ -2699,10 +2712,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         a.ring = reinterpret_cast<uint32_t*>(ws + hdr);
         a.states = reinterpret_cast<uint64_t*>(ws + hdr + ring_bytes);
         a.ring_mask = static_cast<uint32_t>(ring - 1);
-        a.wg_flags = reinterpret_cast<uint32_t*>(ws + hdr + ring_bytes + states_bytes);
-        a.nwg = grid;
-        a.spin_cap = g_test.spin_cap ? g_test.spin_cap : dev::kSpinCap;
-        a.steal_spins = g_test.no_steal ? 0u : dev::kStealSpins;
+
 #if KCDC_TRACE
         if (trace_reserve(std::max<uint64_t>(s.nstreams, 2ull * grid * wg_waves)) != 0) return set_error(-12, "trace buffer");
         a.trace = g_trace;
@@ -2710,9 +2720,10 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         // header + ring zeroed per launch (the ring is also left empty by every finished launch)
         if (dma) {
             const uint32_t slots = static_cast<uint32_t>(ring);
-            const uint64_t threads = std::max<uint64_t>(std::max<uint64_t>(8ull * slots, dev::kQHeaderBytes / 4), grid);
+            const uint64_t threads = std::max<uint64_t>(8ull * slots, dev::kQHeaderBytes / 4);  // >= nstreams
             hipLaunchKernelGGL(dev::init_ring_kernel, dim3(static_cast<unsigned>((threads + 255) / 256)), dim3(256), 0, st, a,
-                               slots, grid * wg_waves);
+                               slots, grid * wg_waves, g_test.spin_cap ? g_test.spin_cap : dev::kSpinCap,
+                               g_test.no_steal ? 0u : dev::kStealSpins);
         } else {
             hipError_t e = hipMemsetAsync(ws, 0, hdr + ring_bytes, st);
             if (e != hipSuccess) return hip_fail(e, "queue reset");
@@ -2726,12 +2737,9 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
             else
                 hipLaunchKernelGGL(dev::split_batch_pipe_kernel<false>, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0,
                                    st, a);
-            if (g_test.force_error) {  // test hook: report a failed launch (kcdc_test_set)
-                const hipError_t e = hipMemsetAsync(ws + 4 * dev::kQErr, 0xFF, 4, st);
-                if (e != hipSuccess) return hip_fail(e, "test hook");
-            }
-            hipLaunchKernelGGL(dev::check_queue_kernel, dim3(std::min<unsigned>((s.nstreams + 255) / 256, 256u)), dim3(256),
-                               0, st, a);
+            if (g_test.force_error)  // test hook: report a failed launch (kcdc_test_set)
+                hipLaunchKernelGGL(dev::poison_counts_kernel, dim3(std::min<unsigned>((s.nstreams + 255) / 256, 256u)),
+                                   dim3(256), 0, st, a);
         } else {
             const dim3 block(dev::kBatchWaves * dev::kWave);
             if (algo.kind == kBuzhash)

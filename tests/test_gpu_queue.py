@@ -54,9 +54,11 @@ def test_failed_launch_is_reported(gpu):
         with pytest.raises(_lib.KcdcError) as e:
             batch.read_cuts(b)
         assert e.value.code == _lib.KCDC_EIO
+        # sub-MiB streams: the host path routes them through the batch kernel (larger ones
+        # that would be a batch's tail take the long path, which has no work queue)
         host = data[: 4 * L].cpu().numpy()
         with pytest.raises(_lib.KcdcError) as e:
-            batch.split_batch_host(NAME, [host[i * L:(i + 1) * L] for i in range(4)])
+            batch.split_batch_host(NAME, [host[i * (L // 4):(i + 1) * (L // 4)] for i in range(16)])
         assert e.value.code == _lib.KCDC_EIO
     # the next launch is clean again
     batch.split_batch_device(NAME, b)
@@ -67,17 +69,29 @@ def test_failed_launch_is_reported(gpu):
 
 
 def test_waiting_wave_give_up_is_reported(gpu):
-    """With a one-poll cap, waves that wait for work give up: the error word must turn
-    into KCDC_COUNT_FAILED, never into a silently partial result."""
+    """One 1 GiB stream among 2047 tiny ones: one wave scans it for tens of ms while every
+    other wave waits on a queue that does not move.  With a 1000-poll cap they give up;
+    that must surface as KCDC_COUNT_FAILED, never as a silently partial result -- and the
+    same launch with the default cap is exact."""
     import torch
-    ns, L = 4096, 1 << 20
-    _data, b = _streams(gpu, ns, L)
-    with knob(_lib.TEST_SPIN_CAP, 1), knob(_lib.TEST_NO_STEAL, 1):
+    big, small, ns = 1 << 30, 64 << 10, 2048
+    data = torch.empty(big + (ns - 1) * small, dtype=torch.uint8, device=gpu)
+    batch.fill_prng(data, big, 1, big, SEED, first_sid=0)
+    batch.fill_prng(data[big:], small, ns - 1, small, SEED, first_sid=1)
+    ptrs = [data.data_ptr()] + [data.data_ptr() + big + i * small for i in range(ns - 1)]
+    b = batch.make_device_batch(NAME, ptrs, [big] + [small] * (ns - 1), gpu)
+    with knob(_lib.TEST_SPIN_CAP, 1000), knob(_lib.TEST_NO_STEAL, 1):
         batch.split_batch_device(NAME, b)
         torch.cuda.synchronize()
         with pytest.raises(_lib.KcdcError) as e:
             batch.read_cuts(b)
         assert e.value.code == _lib.KCDC_EIO
+    batch.split_batch_device(NAME, b)
+    torch.cuda.synchronize()
+    got = batch.read_cuts(b)
+    cuts, counts = coracle.split_prng_streams(NAME, SEED, [0], big, nthreads=1)
+    np.testing.assert_array_equal(got[0], cuts[0, :counts[0]])
+    assert all(g.tolist() == [small] for g in got[1:])  # shorter than min: one chunk
 
 
 def _beside_occupier(gpu, nwg, usec):
