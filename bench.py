@@ -40,7 +40,7 @@ METRIC = "splitter throughput GiB/s (device-resident) at 1/2/4/8 GPU; boundaries
 SEED = 0x6B6F706961
 # the pipelined launch: init_ring_kernel, the splitter kernel, check_queue_kernel
 BATCH_KERNEL = {0: "kcdc::dev::split_fixed_kernel", 1: "kcdc::dev::split_batch_pipe_kernel<true>",
-                2: "kcdc::dev::split_batch_kernel<rabinkarp>"}
+                2: "kcdc::dev::split_batch_kernel<2>"}  # rocprofv3 names
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 GiB = float(1 << 30)
 
@@ -290,7 +290,7 @@ def bench_batch(args, comm: Comm):
     per = comm.gather({"bytes_per_step": ns * L, "elapsed_s": elapsed, "own_s": own, "kernel_ms": kern_ms,
                        "rolled": rolled})
     agg = aggregate(per, args.steps)
-    cfg = f"config{args.config}"
+    cfg = f"config{args.config}" + ("-rk" if int(info.kind) == 2 else "")
     out = {
         "metric": METRIC, "value": agg["value"], "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": agg["ms_per_step"], "higher_is_better": True,

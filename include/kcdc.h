@@ -199,16 +199,26 @@ int kcdc_gorand_read(int64_t seed, uint8_t* out, uint64_t n);
 /* ------------------------------------------------------------- testing
  * Hooks for the library's own tests (not part of the splitter surface).
  * kcdc_test_set: process-wide knobs read by every later batch launch.
- *   KCDC_TEST_SPIN_CAP    polls before a waiting wave gives up (0: default, ~seconds)
+ *   KCDC_TEST_SPIN_CAP    polls without queue progress before a waiting wave gives up, the
+ *                         current poll included (0: default, ~seconds; 1: at the first
+ *                         unready poll)
  *   KCDC_TEST_NO_STEAL    1: waves never requeue the streams of workgroups that have not started
  *   KCDC_TEST_FORCE_ERROR 1: every batch launch reports failure (KCDC_COUNT_FAILED)
  * kcdc_test_occupy: occupy `nwg` CUs (one workgroup with all of the CU's LDS each) for
- * `usec` microseconds on `hip_stream`, e.g. to run a batch beside a kernel that holds CUs. */
+ * `usec` microseconds on `hip_stream`, e.g. to run a batch beside a kernel that holds CUs.
+ * kcdc_test_queue_stat: after the last pipelined batch launch has finished (synchronise
+ * first), read one word of its queue header: KCDC_TEST_STAT_GIVEUPS (waves that gave up
+ * waiting), KCDC_TEST_STAT_DONE (streams finished), KCDC_TEST_STAT_STEALS (requeued
+ * workgroups).  Synchronous copy; returns the word, or a negative KCDC_E* code. */
 #define KCDC_TEST_SPIN_CAP 1
 #define KCDC_TEST_NO_STEAL 2
 #define KCDC_TEST_FORCE_ERROR 3
 int kcdc_test_set(int32_t key, int64_t value);
 int kcdc_test_occupy(uint32_t nwg, uint32_t usec, void* hip_stream);
+#define KCDC_TEST_STAT_GIVEUPS 1
+#define KCDC_TEST_STAT_DONE 2
+#define KCDC_TEST_STAT_STEALS 3
+int64_t kcdc_test_queue_stat(int32_t key);
 
 #ifdef __cplusplus
 }

@@ -25,6 +25,7 @@ KCDC_EOVERFLOW = -75
 KIND_FIXED, KIND_BUZHASH, KIND_RABINKARP = 0, 1, 2
 COUNT_FAILED = (1 << 64) - 1  # KCDC_COUNT_FAILED: the batch launch failed on the device
 TEST_SPIN_CAP, TEST_NO_STEAL, TEST_FORCE_ERROR = 1, 2, 3
+STAT_GIVEUPS, STAT_DONE, STAT_STEALS = 1, 2, 3
 
 
 class KcdcError(RuntimeError):
@@ -67,6 +68,7 @@ _SIGS = {
     "kcdc_group_free": (None, [_P]),
     "kcdc_test_set": (C.c_int, [C.c_int32, C.c_int64]),
     "kcdc_test_occupy": (C.c_int, [C.c_uint32, C.c_uint32, _P]),
+    "kcdc_test_queue_stat": (C.c_int64, [C.c_int32]),
 }
 
 

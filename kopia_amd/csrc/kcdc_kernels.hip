@@ -1304,7 +1304,7 @@ __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, u
             seen = now;
             if (done >= n) {
                 stop = 1;
-            } else if (idle >= spin_cap) {
+            } else if (idle + 1u >= spin_cap) {  // this poll included: a cap of 1 gives up at once (test knob)
                 add_agent(a.queue + kQErr, 1u);
                 stop = 1;
             }
@@ -2534,6 +2534,8 @@ struct TestKnobs {
     uint32_t spin_cap = 0;     // 0: dev::kSpinCap
     bool no_steal = false;     // disable try_steal
     bool force_error = false;  // mark every pipelined launch as failed
+    char* last_ws = nullptr;   // queue header of the last pipelined launch (kcdc_test_queue_stat)
+    int last_dev = 0;
 };
 TestKnobs g_test;
 
@@ -2706,6 +2708,8 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
             }
         }
         a.queue = reinterpret_cast<uint32_t*>(ws);
+        g_test.last_ws = ws;
+        g_test.last_dev = device;
 #if KCDC_TRACE || KCDC_DEBUG_CHECKS
         g_last_ws = ws;
 #endif
@@ -2967,6 +2971,19 @@ extern "C" int kcdc_test_set(int32_t key, int64_t value) {
         case 3: g_test.force_error = value != 0; return 0;                  // KCDC_TEST_FORCE_ERROR
         default: return set_error(-22, "unknown test knob");
     }
+}
+
+extern "C" int64_t kcdc_test_queue_stat(int32_t key) {
+    const int word = key == 1 ? dev::kQErr : key == 2 ? dev::kQDone : key == 3 ? dev::kQSteal : -1;
+    if (word < 0) return set_error(-22, "unknown queue statistic");
+    if (!g_test.last_ws) return set_error(-22, "no pipelined batch launch yet");
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(g_test.last_dev);
+    uint32_t v = 0;
+    const hipError_t e = hipMemcpy(&v, g_test.last_ws + 4 * word, 4, hipMemcpyDeviceToHost);
+    (void)hipSetDevice(prev);
+    return e == hipSuccess ? static_cast<int64_t>(v) : hip_fail(e, "queue statistic");
 }
 
 extern "C" int kcdc_test_occupy(uint32_t nwg, uint32_t usec, void* stream) {

@@ -68,11 +68,11 @@ def test_failed_launch_is_reported(gpu):
     assert all(np.array_equal(got[i], want[i]) for i in range(ns))
 
 
-def test_waiting_wave_give_up_is_reported(gpu):
+def test_waiting_wave_give_up_loses_nothing(gpu):
     """One 1 GiB stream among 2047 tiny ones: one wave scans it for tens of ms while every
-    other wave waits on a queue that does not move.  With a 1000-poll cap they give up;
-    that must surface as KCDC_COUNT_FAILED, never as a silently partial result -- and the
-    same launch with the default cap is exact."""
+    other wave waits on a queue that does not move.  With a 1000-poll cap the waiting waves
+    give up (the queue header counts them); they hold no stream, so the result is still
+    exact -- a give-up can only ever cost a stream that a waiting wave held a ticket for."""
     import torch
     big, small, ns = 1 << 30, 64 << 10, 2048
     data = torch.empty(big + (ns - 1) * small, dtype=torch.uint8, device=gpu)
@@ -80,18 +80,55 @@ def test_waiting_wave_give_up_is_reported(gpu):
     batch.fill_prng(data[big:], small, ns - 1, small, SEED, first_sid=1)
     ptrs = [data.data_ptr()] + [data.data_ptr() + big + i * small for i in range(ns - 1)]
     b = batch.make_device_batch(NAME, ptrs, [big] + [small] * (ns - 1), gpu)
-    with knob(_lib.TEST_SPIN_CAP, 1000), knob(_lib.TEST_NO_STEAL, 1):
-        batch.split_batch_device(NAME, b)
-        torch.cuda.synchronize()
-        with pytest.raises(_lib.KcdcError) as e:
-            batch.read_cuts(b)
-        assert e.value.code == _lib.KCDC_EIO
-    batch.split_batch_device(NAME, b)
-    torch.cuda.synchronize()
-    got = batch.read_cuts(b)
     cuts, counts = coracle.split_prng_streams(NAME, SEED, [0], big, nthreads=1)
-    np.testing.assert_array_equal(got[0], cuts[0, :counts[0]])
-    assert all(g.tolist() == [small] for g in got[1:])  # shorter than min: one chunk
+    for cap in (1000, 0):
+        with knob(_lib.TEST_SPIN_CAP, cap), knob(_lib.TEST_NO_STEAL, 1):
+            batch.split_batch_device(NAME, b)
+            torch.cuda.synchronize()
+            giveups = _lib.check(_lib.lib().kcdc_test_queue_stat(_lib.STAT_GIVEUPS))
+            assert _lib.check(_lib.lib().kcdc_test_queue_stat(_lib.STAT_DONE)) == ns
+        assert (giveups > 0) == (cap != 0), (cap, giveups)
+        got = batch.read_cuts(b)
+        np.testing.assert_array_equal(got[0], cuts[0, :counts[0]])
+        assert all(g.tolist() == [small] for g in got[1:])  # shorter than min: one chunk
+
+
+def test_give_up_holding_a_ticket_is_reported(gpu):
+    """A 1-poll cap: waves give up as soon as the entry behind their ticket is not yet
+    written, which loses the stream a yielding wave then writes there.  Every launch must
+    then be exact or raise KCDC_EIO (its lost streams' counts stay KCDC_COUNT_FAILED) --
+    never a silently partial cut list.  At least one launch must lose a stream."""
+    import torch
+    ns, L = 4096, 4 << 20  # (min size is 2 MiB: shorter streams never queue a yield)
+    _data, b = _streams(gpu, ns, L)
+    want = _oracle(ns, L)
+    failed = 0
+    for _ in range(4):
+        with knob(_lib.TEST_SPIN_CAP, 1), knob(_lib.TEST_NO_STEAL, 1):
+            batch.split_batch_device(NAME, b)
+            torch.cuda.synchronize()
+            giveups = _lib.check(_lib.lib().kcdc_test_queue_stat(_lib.STAT_GIVEUPS))
+            done = _lib.check(_lib.lib().kcdc_test_queue_stat(_lib.STAT_DONE))
+        counts = b.counts.cpu().numpy()[:ns].view(np.uint64)
+        lost = int((counts == np.uint64(_lib.COUNT_FAILED)).sum())
+        assert lost == ns - done, (lost, done)
+        if lost:
+            failed += 1
+            assert giveups > 0
+            with pytest.raises(_lib.KcdcError) as e:
+                batch.read_cuts(b)
+            assert e.value.code == _lib.KCDC_EIO
+        else:
+            got = batch.read_cuts(b)
+            assert all(np.array_equal(got[i], want[i]) for i in range(ns))
+        # streams that did finish are exact either way
+        ok = np.nonzero(counts != np.uint64(_lib.COUNT_FAILED))[0]
+        cuts = b.cuts.cpu().numpy().view(np.uint64)
+        base = b.cut_base.cpu().numpy().view(np.uint64)
+        for i in ok[:: max(1, len(ok) // 64)]:
+            c = int(counts[i])
+            assert np.array_equal(cuts[int(base[i]):int(base[i]) + c], want[i])
+    assert failed > 0, "a 1-poll cap never lost a stream: the test does not exercise the failure path"
 
 
 def _beside_occupier(gpu, nwg, usec):
