@@ -164,6 +164,51 @@ def split_prng_streams(name: str, seed: int, sids, stream_len: int, nthreads: in
     return cuts.reshape(ns, cap), counts
 
 
+def split_prng_stream_blocks(name: str, seed: int, sid: int, stream_len: int, block: int = 256 << 20,
+                             gen_threads: int = 8) -> tuple[np.ndarray, float]:
+    """One (arbitrarily long) counter-PRNG stream split through the STREAMING oracle
+    (NextSplitPoint over successive `block`-byte slices, repo/object/object_writer.go:
+    120-136): host memory stays at a few blocks (a 64 GiB stream needs no 64 GiB buffer).
+    Blocks are generated ahead on `gen_threads` threads.  Returns (cut end offsets, the
+    seconds spent inside NextSplitPoint -- the single-thread split time)."""
+    import concurrent.futures as cf
+    import time
+    k, size = params(name)
+    L = lib()
+    nxt = L["orc_next"]  # a fresh function object: raw pointer arguments, no bytes copy
+    nxt.restype = C.c_int64
+    nxt.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+    h = L.orc_new(k, size)
+    cuts, split_s = [], 0.0
+    try:
+        nblk = (stream_len + block - 1) // block
+        depth = 2 * gen_threads
+        with cf.ThreadPoolExecutor(gen_threads) as ex:
+            def gen(j):
+                return gen_stream(seed, sid, min(block, stream_len - j * block), offset=j * block)
+            futs = {j: ex.submit(gen, j) for j in range(min(depth, nblk))}
+            for j in range(nblk):
+                buf = futs.pop(j).result()
+                if j + depth < nblk:
+                    futs[j + depth] = ex.submit(gen, j + depth)
+                base, pos, n = j * block, 0, buf.size
+                t0 = time.perf_counter()
+                while pos < n:
+                    r = nxt(h, buf.ctypes.data + pos, n - pos)
+                    if r < 0:
+                        break
+                    pos += r
+                    cuts.append(base + pos)
+                split_s += time.perf_counter() - t0
+    finally:
+        L.orc_free(h)
+    if not cuts or cuts[-1] < stream_len:
+        cuts.append(stream_len)  # the trailing chunk (objectWriter.Result)
+    if stream_len == 0:
+        cuts = []
+    return np.asarray(cuts, dtype=np.int64), split_s
+
+
 def gen_stream(seed: int, sid: int, n: int, offset: int = 0) -> np.ndarray:
     out = np.empty(n, dtype=np.uint8)
     lib().orc_gen_stream(seed, sid, offset, out.ctypes.data, n)

@@ -119,3 +119,36 @@ def test_group_freed_before_its_handles():
     assert write_object(s, data, slice_plan(np.random.default_rng(3), len(data), "64k")) == \
         coracle.split_stream(name, data).tolist()
     s.Close()
+
+
+def test_group_freed_then_many_handles_close_concurrently():
+    """kcdc_group_free with 16 handles open, then 16 threads each write an object through
+    their handle and Close it at the same time: the last closer tears the group down while
+    the others are still closing (the release path must not touch the group after its
+    unlock).  Every writer's cuts equal the oracle's."""
+    name, nw = "DYNAMIC-128K-BUZHASH", 16
+    streams = [coracle.gen_stream(SEED, 1200 + i, (1 << 20) + 4099 * i) for i in range(nw)]
+    want = [coracle.split_stream(name, d).tolist() for d in streams]
+    for rep in range(3):
+        g = ks.SplitterGroup(name, 0, max_batch=64, max_wait_us=100)
+        hs = [g.splitter() for _ in range(nw)]
+        g.close()
+        got, errs = [None] * nw, []
+        go = threading.Barrier(nw)
+
+        def run(i):
+            try:
+                got[i] = write_object(hs[i], streams[i], slice_plan(np.random.default_rng(rep * 100 + i),
+                                                                    len(streams[i]), "64k"))
+                go.wait(timeout=60)  # every writer done: close all at once
+                hs[i].Close()
+            except Exception as e:  # surfaced below
+                errs.append(e)
+
+        th = [threading.Thread(target=run, args=(i,)) for i in range(nw)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert not errs, errs
+        assert got == want
