@@ -199,7 +199,7 @@ int kcdc_gorand_read(int64_t seed, uint8_t* out, uint64_t n);
 /* ------------------------------------------------------------- testing
  * Hooks for the library's own tests (not part of the splitter surface).
  * kcdc_test_set: process-wide knobs read by every later batch launch.
- *   KCDC_TEST_SPIN_CAP    polls without queue progress before a waiting wave gives up, the
+ *   KCDC_TEST_SPIN_CAP    polls with no stream finishing before a waiting wave gives up, the
  *                         current poll included (0: default, ~seconds; 1: at the first
  *                         unready poll)
  *   KCDC_TEST_NO_STEAL    1: waves never requeue the streams of workgroups that have not started

@@ -972,9 +972,9 @@ constexpr uint32_t kMaxPipeGrid = 256;
 constexpr size_t kQHeaderBytes = 8192;
 // Header words 1792.. : debug-build failure record (pcheck, KCDC_DEBUG_CHECKS).
 [[maybe_unused]] constexpr int kQStat = 1792;
-// A waiting wave gives up (error word, the launch reports failure) only after this many polls
-// without progress of the queue (streams done, entries reserved): a bug guard that keeps the
-// kernel bounded, ~100 s; no correct launch waits that long (one wave scans >= 6 GB/s).
+// A waiting wave gives up (error word; a stream it held a ticket for is then reported failed)
+// only after this many polls with no stream finishing: a bug guard that keeps the kernel
+// bounded, >= 60 s; no correct launch waits that long (one wave scans >= 6 GB/s).
 constexpr uint32_t kSpinCap = 1u << 26;
 constexpr uint32_t kStealSpins = 256;                            // ~0.5 ms of polling between steal scans
 
@@ -1286,8 +1286,8 @@ __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
 __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, uint32_t wg_waves) {
     const uint32_t n = a.nstreams;
     const uint32_t spin_cap = ld_agent(a.queue + kQCfg), steal_spins = ld_agent(a.queue + kQCfg + 1);
-    uint32_t idle = 0;            // polls since the queue last moved
-    uint64_t seen = ~0ull;        // lane 0: {done, tail} at the last poll
+    uint32_t idle = 0;            // polls since a stream last finished
+    uint32_t seen = ~0u;          // lane 0: streams done at the last poll
     for (uint32_t spin = 0;; spin++) {
         const u32x4 v = pentry_load(a, lane, t);
         if (pentry_ok(v, lane, t)) {
@@ -1297,11 +1297,11 @@ __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, u
         }
         uint32_t stop = 0;
         if (lane == 0) {
+            // Progress = streams finishing.  Not the {head, tail} word: every ticket take and
+            // yield is an atomic on it, and waiting waves polling it slowed those by ~7%.
             const uint32_t done = ld_agent(a.queue + kQDone);
-            const uint32_t tail = static_cast<uint32_t>(ld_agent64(reinterpret_cast<uint64_t*>(a.queue + kQHT)) >> 32);
-            const uint64_t now = (static_cast<uint64_t>(done) << 32) | tail;
-            idle = now == seen ? idle + 1 : 0;
-            seen = now;
+            idle = done == seen ? idle + 1 : 0;
+            seen = done;
             if (done >= n) {
                 stop = 1;
             } else if (idle + 1u >= spin_cap) {  // this poll included: a cap of 1 gives up at once (test knob)
@@ -1447,14 +1447,13 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
     PStream cur;
     int64_t budget = kNoYield;
     bool dry = false;  // the queue was (nearly) dry when this stream was taken: probes may pay
-    // Claim of this workgroup's preassigned tickets: lane 0's CAS result (0 or 1: ours, 2: the
-    // streams were requeued by try_steal).  Issued before the first resolve and checked after
-    // it, so its round trip overlaps the entry load; nothing is changed before the check.
-    uint32_t claim = 1u;
-    bool check_claim = false;
     // Blocking take of the next stream with a region to scan (t: a ticket already held,
     // or ~0u to take one); false when every stream is done.  No LDS-DMA may be in flight.
-    auto take_blocking = [&](uint32_t t, int64_t backlog_hint) -> bool {
+    // claim: the first take's claim of this workgroup's preassigned tickets (lane 0's CAS
+    // result: 0 or 1 ours, 2 the streams were requeued by try_steal), issued before the first
+    // resolve and checked after it so its round trip overlaps the entry load; ~0u elsewhere
+    // (a constant at those call sites: no claim state stays live across the main loop).
+    auto take_blocking = [&](uint32_t t, int64_t backlog_hint, uint32_t claim) -> bool {
 #if KCDC_TRACE
         const uint64_t tb0 = __builtin_amdgcn_s_memrealtime();
         tr_last = tb0;
@@ -1477,9 +1476,10 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             const int r = presolve(a, lane, held, cur, kDmaWaves);
             if (r == 0) return false;
             t = 0xFFFFFFFFu;
-            if (check_claim) {
-                check_claim = false;
-                if (bcast(claim) == 2u) continue;  // requeued by another wave: take a fresh ticket
+            if (claim != 0xFFFFFFFFu) {
+                const bool requeued = bcast(claim) == 2u;
+                claim = 0xFFFFFFFFu;
+                if (requeued) continue;  // requeued by another wave: take a fresh ticket
             }
             if (r == 2) continue;  // tombstone
             uniformize(cur);
@@ -1493,9 +1493,15 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             }
         }
     };
+    // Pending blocking take (set right before jumping to the loop top, so none of it is live
+    // across the hash loop).
+    bool need_take = true;
+    uint32_t take_t = 0xFFFFFFFFu, take_claim = 0xFFFFFFFFu;
+    int64_t take_backlog = 0;
     {
         // First ticket: preassigned (see init_ring_kernel), unless a waiting wave has requeued
         // this workgroup's streams before it started (try_steal): then take one from the counter.
+        uint32_t claim = 1u;
         if (lane == 0) {
             claim = 0u;
             __hip_atomic_compare_exchange_strong((gu32*)(a.queue + kQFlags + blockIdx.x), &claim, 1u,
@@ -1503,11 +1509,18 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         }
         const uint32_t gw0 = blockIdx.x * kDmaWaves + wave;
         const int64_t nw = static_cast<int64_t>(gridDim.x) * kDmaWaves;
-        check_claim = gw0 < a.nstreams;
-        if (!take_blocking(gw0 < a.nstreams ? gw0 : 0xFFFFFFFFu, static_cast<int64_t>(a.nstreams) - nw)) KCDC_PRET;
+        take_t = gw0 < a.nstreams ? gw0 : 0xFFFFFFFFu;
+        take_backlog = static_cast<int64_t>(a.nstreams) - nw;
+        take_claim = gw0 < a.nstreams ? (claim & 3u) : 0xFFFFFFFFu;
     }
     bool issued = false;  // this tile's warm piece + step 0 are in flight
     for (;;) {
+        // The one blocking take site (inlined once: presolve and try_steal are large).
+        if (need_take) {
+            if (!take_blocking(take_t, take_backlog, take_claim)) KCDC_PRET;
+            need_take = false;
+            issued = false;
+        }
         uniformize(cur);
         if (!pcheck(a, lane, cur, 0xFFFFFFFFu, 5)) return;
         int64_t lo, hi;
@@ -1798,13 +1811,17 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                 a.counts[cur.sid] = cur.cnt;
                 add_agent(a.queue + kQDone, 1u);
             }
-            if (!take_blocking(0xFFFFFFFFu, 0)) KCDC_PRET;
-            issued = false;
+            need_take = true;
+            take_t = 0xFFFFFFFFu;
+            take_backlog = 0;
+            take_claim = 0xFFFFFFFFu;
             continue;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no prefetch may remain in flight
-        if (!take_blocking(switching ? tk : 0xFFFFFFFFu, nbacklog)) KCDC_PRET;
-        issued = false;
+        need_take = true;
+        take_t = switching ? tk : 0xFFFFFFFFu;
+        take_backlog = nbacklog;
+        take_claim = 0xFFFFFFFFu;
     }
 }
 
