@@ -797,6 +797,9 @@ __global__ __launch_bounds__(kBatchWaves * kWave, kBatchWaves / 4) void split_ba
 #ifndef KCDC_DMA
 #define KCDC_DMA 1
 #endif
+#ifndef KCDC_RK_PIPE
+#define KCDC_RK_PIPE 1  // Rabin-Karp batches through split_batch_rk_kernel (two chains per lane)
+#endif
 #ifndef KCDC_TRACE
 #define KCDC_TRACE 0  // timing-trace builds only (tools/trace_sched.py)
 #endif
@@ -1825,6 +1828,532 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
     }
 }
 
+// ================================================= Rabin-Karp pipelined kernel
+// rabinkarp64 (splitter_rabinkarp64.go:26-67, rollinghash Roll):
+//   u = v ^ out[leave];  v = (u << 8 | enter) ^ mod[u >> 45]
+// Per byte the chain waits on one table read indexed by the hash itself (mod[]), so one
+// chain per lane is LDS-latency bound (round 1: 4.07 ms on config 2).  Here each lane runs
+// TWO independent chains, A over the first half of its lane segment and B over the second,
+// interleaved byte by byte so two mod[] reads are in flight per lane (four per SIMD).
+//
+// Feeding keeps whole 128-byte lines (64-byte runs cap the DMA at 4.4 vs 6.6 TB/s,
+// tools/membench.hip rk): the wave's one 8 KiB step slot receives, per lane, a line of
+// chain A and a line of chain B alternately; a chain consumes 64 bytes per step, the
+// first half of its line when it arrives and the second half (kept in VGPRs) one step
+// later.  A tile (64 lanes x L bytes, L a multiple of 256) is:
+//   W     the warm fill [A: 64 B before its half | B: 64 B before its half] (both chains
+//         warm from a zero history);
+//   2K    line fills (A line 0, B line 0, A line 1, ...), K = L/256 lines per chain;
+//   D     drain: B's last 64 bytes (no fill: the slot takes the next tile's warm fill, or
+//         the next stream's queue entry).
+// Tables (96 KiB, conflict-free or nearly): out[] with 32 replicas at a 256-byte stride
+// (lane l reads replica l % 32, bank pair 2(l % 32); address = one v_perm of the leaving
+// byte), mod[] with 16 replicas at a 128-byte stride (lanes l and l+16 share a bank pair
+// only for indices of equal parity).  8 waves x 8 KiB slots + 96 KiB = 160 KiB.
+#ifndef KCDC_RK_MODREP
+#define KCDC_RK_MODREP 16  // mod[] replicas: 16 = 2-way conflicts, perm-addressed out[]; 32 = conflict-free mod[]
+                           // but a 2-op out[] address: 3.01 vs 2.80 ms on config 2 (issue-bound)
+#endif
+constexpr int kRkModRep = KCDC_RK_MODREP;
+constexpr int kRkOutRep = 48 - kRkModRep;  // out[] gets the rest of the 96 KiB
+struct RkTables {
+    uint64_t mod[256 * kRkModRep];  // mod[i*R + r]: first, so its addresses fit the 16-bit ds offset
+    uint64_t out[256 * kRkOutRep];  // outx[b*R' + r] (rk_roll: out[] pre-shifted and pre-reduced)
+};
+static_assert(sizeof(RkTables) + sizeof(DmaSlots) <= 160 * 1024, "Rabin-Karp tables + step slots exceed LDS");
+constexpr uint32_t kRkIdxBit = 13;  // u >> 45 = bits 13..20 of the high word (deg P = 53, host-checked)
+
+struct RkCtx {
+    const char* modb;  // LDS byte address of RkTables::mod
+    const char* outb;  // LDS byte address of RkTables::out
+    uint32_t lane8o;   // (lane % out replicas) * 8
+    uint32_t lane8m;   // (lane % mod replicas) * 8
+    uint32_t mask;     // avg - 1
+};
+
+__device__ __forceinline__ uint64_t rk_out(const RkCtx& k, uint32_t w, int b) {
+    uint32_t a;
+    if constexpr (kRkOutRep == 32) {  // (byte b of w) << 8 | lane8o: the replica address in one v_perm
+        a = __builtin_amdgcn_perm(w, k.lane8o, 0x0c0c0000u | ((4u + b) << 8));
+    } else {  // 16 replicas, 128-byte stride: (byte b of w) << 7 | lane8o
+        a = ((b == 0 ? (w << 7) : (w >> (8 * b - 7))) & 0x7F80u) | k.lane8o;
+    }
+#if KCDC_RK_ABL == 1
+    return static_cast<uint64_t>(a);
+#else
+    return *reinterpret_cast<const uint64_t*>(k.outb + a);
+#endif
+}
+// One roll with the leaving byte's out[] value already read: returns nothing, updates (hi, lo).
+// Linearity folds the leaving byte's removal into one table read that is off the chain:
+// mod[] is GF(2)-linear in its index and idx(v ^ o) = idx(v) ^ idx(o), so
+//   ((v ^ o) << 8 | c) ^ mod[idx(v ^ o)] = ((v << 8) | c) ^ mod[idx(v)] ^ outx[l],
+//   outx[l] = (out[l] << 8) ^ mod[idx(out[l])]   (bits 53..60 cancel on both sides).
+// The chain is then v -> address (2 VALU) -> mod[] read -> one v_bitop3, and a roll costs
+// ~8.5 VALU instead of 10.5 (the u = v ^ out xors are gone).
+#ifndef KCDC_RK_ABL
+#define KCDC_RK_ABL 0  // ablations (timing only, wrong cuts): 1 no out[] reads, 2 mod[] off the chain,
+                       // 3 no wait for the line fills
+#endif
+__device__ __forceinline__ void rk_roll(const RkCtx& k, uint32_t& hi, uint32_t& lo, uint64_t ox, uint32_t w, int b) {
+#if KCDC_RK_ABL == 2
+    const uint32_t am = (__builtin_amdgcn_ubfe(w, 8 * b, 8) << (kRkModRep == 32 ? 8 : 7)) | k.lane8m;
+#else
+    const uint32_t am = (__builtin_amdgcn_ubfe(hi, kRkIdxBit, 8) << (kRkModRep == 32 ? 8 : 7)) | k.lane8m;
+#endif
+    const uint64_t m = *reinterpret_cast<const uint64_t*>(k.modb + am);
+    const uint32_t th = __builtin_amdgcn_alignbit(hi, lo, 24);                          // v << 8, high word
+    const uint32_t tl = __builtin_amdgcn_perm(w, lo, 0x02010000u | (4u + b));           // v << 8 | enter
+    hi = __builtin_amdgcn_bitop3_b32(th, static_cast<uint32_t>(m >> 32), static_cast<uint32_t>(ox >> 32), 0x96);
+    lo = __builtin_amdgcn_bitop3_b32(tl, static_cast<uint32_t>(m), static_cast<uint32_t>(ox), 0x96);
+}
+// Warm roll (leaving byte 0: out[0] = 0).
+__device__ __forceinline__ void rk_roll0(const RkCtx& k, uint32_t& hi, uint32_t& lo, uint32_t w, int b) {
+    const uint32_t am = (__builtin_amdgcn_ubfe(hi, kRkIdxBit, 8) << (kRkModRep == 32 ? 8 : 7)) | k.lane8m;
+    const uint64_t m = *reinterpret_cast<const uint64_t*>(k.modb + am);
+    const uint32_t th = __builtin_amdgcn_alignbit(hi, lo, 24);
+    const uint32_t tl = __builtin_amdgcn_perm(w, lo, 0x02010000u | (4u + b));
+    hi = th ^ static_cast<uint32_t>(m >> 32);
+    lo = tl ^ static_cast<uint32_t>(m);
+}
+
+#ifndef KCDC_RK_W
+#define KCDC_RK_W 2  // bytes per lookahead window: outx[] reads of both chains issued one window ahead (2: 2.58 ms, 4: 2.65)
+#endif
+// 64 bytes of chain A (in a / leaving pa) and of chain B (in b / leaving pb), interleaved;
+// returns the running min of (lo & mask) per chain.  ACT_A/ACT_B: whether that chain's
+// bytes are real (an idle chain is not rolled at all).
+template <bool ACT_A, bool ACT_B>
+__device__ __forceinline__ void rk_step64(const RkCtx& k, uint32_t& ha, uint32_t& la, const uint32_t (&a)[16],
+                                          const uint32_t (&pa)[16], uint32_t& hb, uint32_t& lb,
+                                          const uint32_t (&b)[16], const uint32_t (&pb)[16], uint32_t& ma,
+                                          uint32_t& mb) {
+    constexpr int W = KCDC_RK_W;
+    uint64_t oa[W], ob[W], na[W], nb[W];
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+        if (ACT_A) oa[i] = rk_out(k, pa[i >> 2], i & 3);
+        if (ACT_B) ob[i] = rk_out(k, pb[i >> 2], i & 3);
+    }
+#pragma unroll
+    for (int w = 0; w < 64 / W; w++) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (w < 64 / W - 1) {
+#pragma unroll
+            for (int i = 0; i < W; i++) {
+                const int x = W * (w + 1) + i;
+                if (ACT_A) na[i] = rk_out(k, pa[x >> 2], x & 3);
+                if (ACT_B) nb[i] = rk_out(k, pb[x >> 2], x & 3);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+            const int x = W * w + i;
+            if (ACT_A) {
+                rk_roll(k, ha, la, oa[i], a[x >> 2], x & 3);
+                ma = min(ma, la & k.mask);
+            }
+            if (ACT_B) {
+                rk_roll(k, hb, lb, ob[i], b[x >> 2], x & 3);
+                mb = min(mb, lb & k.mask);
+            }
+            if ((x & 3) == 3) {
+                if (ACT_A) asm volatile("" : "+v"(ma));
+                if (ACT_B) asm volatile("" : "+v"(mb));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+            if (ACT_A) oa[i] = na[i];
+            if (ACT_B) ob[i] = nb[i];
+        }
+    }
+}
+
+// Exact re-run of one chain's 64 bytes from (hi, lo) (rare): first index in [lo_i, hi_i]
+// with (lo & mask) == 0, else 64.
+__device__ uint32_t rk_exact64(const RkCtx& k, uint32_t hi, uint32_t lo, const uint32_t (&in)[16],
+                                            const uint32_t (&prv)[16], int lo_i, int hi_i) {
+    uint32_t e[16], o[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        e[j] = in[j];
+        o[j] = prv[j];
+    }
+    uint32_t first = 64;
+#pragma unroll 1
+    for (int j = 0; j < 16; j++) {
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            rk_roll(k, hi, lo, rk_out(k, o[0], b), e[0], b);
+            const int i = 4 * j + b;
+            if (first == 64 && (lo & k.mask) == 0 && i >= lo_i && i <= hi_i) first = static_cast<uint32_t>(i);
+        }
+#pragma unroll
+        for (int q = 0; q < 15; q++) {
+            e[q] = e[q + 1];
+            o[q] = o[q + 1];
+        }
+    }
+    return first;
+}
+
+// Geometry of a Rabin-Karp tile at ct: L bytes per lane (a multiple of 256: two chains of
+// whole 128-byte lines), K lines per chain.
+struct RkGeom {
+    int64_t L;
+    int K;
+    Loader ld;
+};
+__device__ __forceinline__ RkGeom rk_geom(int64_t ct, int64_t hi, const uint8_t* abase, int64_t off0,
+                                          int64_t nbytes_coord) {
+    const int64_t rem = hi - ct + 1;
+    int64_t per = (rem + kWave - 1) / kWave;
+    per = (per + 255) & ~int64_t(255);
+    RkGeom g;
+    g.L = per < kLaneMax ? per : kLaneMax;
+    g.K = static_cast<int>(g.L / 256);
+    g.ld = make_loader(abase, off0, nbytes_coord, ct >= 64 ? ct - 64 : 0);
+    return g;
+}
+// Warm fill: lane l's slot line = [64 B before c0 | 64 B before c0 + L/2] (16-byte granule j
+// of lane l at j ^ sw(l), as dma_step128).
+__device__ __forceinline__ void rk_dma_warm(const Loader& ld, uint32_t slot, int64_t ct, int64_t L, int lane) {
+#ifdef KCDC_EXP_COMPONLY
+    return;
+#endif
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int l = 8 * i + (lane >> 3);
+        const int jj = (lane & 7) ^ ((l >> 1) & 7);
+        const int64_t c0 = ct + l * L + (jj < 4 ? 0 : L / 2);
+        const int64_t coord = c0 - 64 + 16 * (jj & 3);
+        dma_lds16(ld.d, slot + 1024u * i, static_cast<int32_t>(coord - ld.tb));
+    }
+}
+// Line fill f (1..2K): odd f = line (f-1)/2 of chain A, even f = line f/2 - 1 of chain B.
+__device__ __forceinline__ void rk_dma_line(const Loader& ld, uint32_t slot, int64_t ct, int64_t L, int f, int lane) {
+    const int64_t half = (f & 1) ? 0 : L / 2;
+    const int64_t line = (f & 1) ? (f - 1) / 2 : f / 2 - 1;
+    dma_step128(ld, ld.tb, slot, ct + half, L, line, lane);
+}
+__device__ __forceinline__ void rk_mask_head(uint32_t (&dw)[16], int64_t c, int64_t off0) {
+    if (c == 0 && off0) {  // bytes before the stream start are virtual zeros
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            const int64_t keep_from = off0 - 4 * d;
+            const uint32_t m = keep_from <= 0 ? 0xFFFFFFFFu : (keep_from >= 4 ? 0u : (0xFFFFFFFFu << (8 * keep_from)));
+            dw[d] &= m;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_rk_kernel(BatchArgs a) {
+    __shared__ RkTables smt;
+    __shared__ DmaSlots smslots;
+    for (uint32_t i = threadIdx.x; i < 256u * kRkModRep; i += blockDim.x) smt.mod[i] = a.rk_mod[i / kRkModRep];
+    for (uint32_t i = threadIdx.x; i < 256u * kRkOutRep; i += blockDim.x) {  // outx[] (rk_roll)
+        const uint64_t o = a.rk_out[i / kRkOutRep];
+        smt.out[i] = (o << 8) ^ a.rk_mod[(o >> 45) & 0xFFu];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    RkCtx kx;
+    kx.modb = reinterpret_cast<const char*>(smt.mod);
+    kx.outb = reinterpret_cast<const char*>(smt.out);
+    kx.lane8o = static_cast<uint32_t>(lane & (kRkOutRep - 1)) * 8u;
+    kx.lane8m = static_cast<uint32_t>(lane & (kRkModRep - 1)) * 8u;
+    kx.mask = a.mask;
+    uint8_t* sl = smslots.b[wave][0];
+    const uint32_t sl32 = lds_addr(sl);
+    const int64_t mx = static_cast<int64_t>(a.max_size);
+
+    PStream cur;
+    int64_t budget = kNoYield;
+    auto take_blocking = [&](uint32_t t, int64_t backlog_hint, uint32_t claim) -> bool {
+        for (;;) {
+            int64_t backlog = backlog_hint;
+            if (t == 0xFFFFFFFFu) {
+                const uint64_t ht = qht_take(a, lane, 1);
+                t = static_cast<uint32_t>(ht);
+                backlog = static_cast<int64_t>(ht >> 32) - static_cast<int64_t>(t) - 1;
+            }
+            const uint32_t held = t;
+            const int r = presolve(a, lane, held, cur, kDmaWaves);
+            if (r == 0) return false;
+            t = 0xFFFFFFFFu;
+            if (claim != 0xFFFFFFFFu) {
+                const bool requeued = bcast(claim) == 2u;
+                claim = 0xFFFFFFFFu;
+                if (requeued) continue;
+            }
+            if (r == 2) continue;  // tombstone
+            uniformize(cur);
+            if (!pcheck(a, lane, cur, held, 1)) return false;
+            budget = pipe_quantum(backlog);
+            if (pstream_region(a, cur, lane)) return true;
+            if (lane == 0) {
+                a.counts[cur.sid] = cur.cnt;
+                add_agent(a.queue + kQDone, 1u);
+            }
+        }
+    };
+    bool need_take = true;
+    uint32_t take_t = 0xFFFFFFFFu, take_claim = 0xFFFFFFFFu;
+    int64_t take_backlog = 0;
+    {
+        uint32_t claim = 1u;
+        if (lane == 0) {
+            claim = 0u;
+            __hip_atomic_compare_exchange_strong((gu32*)(a.queue + kQFlags + blockIdx.x), &claim, 1u,
+                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const uint32_t gw0 = blockIdx.x * kDmaWaves + wave;
+        const int64_t nw = static_cast<int64_t>(gridDim.x) * kDmaWaves;
+        take_t = gw0 < a.nstreams ? gw0 : 0xFFFFFFFFu;
+        take_backlog = static_cast<int64_t>(a.nstreams) - nw;
+        take_claim = gw0 < a.nstreams ? (claim & 3u) : 0xFFFFFFFFu;
+    }
+    bool issued = false;  // this tile's warm fill is in flight
+    for (;;) {
+        if (need_take) {
+            if (!take_blocking(take_t, take_backlog, take_claim)) return;
+            need_take = false;
+            issued = false;
+        }
+        uniformize(cur);
+        if (!pcheck(a, lane, cur, 0xFFFFFFFFu, 5)) return;
+        int64_t lo, hi;
+        pregion(a, cur, lo, hi);
+        const RkGeom g = rk_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n);
+        const int64_t ct = cur.ct, ct_next = ct + kWave * g.L;
+        const bool last_of_region = ct_next > hi;
+        const bool budget_out = budget - kWave * g.L <= 0;
+        bool ends_nocand = false;
+        if (last_of_region) {
+            const int64_t s2 = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;
+            ends_nocand = s2 >= cur.n || s2 + static_cast<int64_t>(a.min_size) - 1 >= cur.n;
+        }
+        const bool switching = budget_out || ends_nocand;
+        const bool reserve = budget_out && !ends_nocand;
+        uint64_t ht_raw = 0;
+        if (switching) ht_raw = qht_add(a, lane, 1);  // the next stream's ticket
+        if (!issued) rk_dma_warm(g.ld, sl32, ct, g.L, lane);
+        const int64_t c0 = ct + lane * g.L, c0b = c0 + g.L / 2;
+        uint32_t ht_lo = static_cast<uint32_t>(ht_raw), ht_hi = static_cast<uint32_t>(ht_raw >> 32);
+        uint32_t ha = 0, la = 0, hb = 0, lb = 0;
+        uint32_t pa[16], pb[16];
+        // ---- W: warm fill -> both chains' 64-byte histories; line 1 (A line 0) goes out
+        {
+            uint32_t dw[32];
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(ht_lo), "+v"(ht_hi)::"memory");
+            read_step128(sl, lane, -1, cur.off0, dw);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            rk_dma_line(g.ld, sl32, ct, g.L, 1, lane);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                pa[i] = dw[i];
+                pb[i] = dw[16 + i];
+            }
+#pragma unroll
+            for (int x = 0; x < 64; x++) {
+                if (x % 16 == 0) __builtin_amdgcn_sched_barrier(0);
+                rk_roll0(kx, ha, la, pa[x >> 2], x & 3);
+                rk_roll0(kx, hb, lb, pb[x >> 2], x & 3);
+            }
+        }
+        uint32_t tk = 0;
+        int64_t nbacklog = 0;
+        if (switching) {
+            const uint64_t ht = qht_value(ht_lo, ht_hi);
+            tk = static_cast<uint32_t>(ht);
+            nbacklog = static_cast<int64_t>(ht >> 32) + (reserve ? 1 : 0) - static_cast<int64_t>(tk) - 1;
+        }
+        uint64_t pe_raw = 0;
+        bool res_issued = false, next_issued = false, entry_issued = false;
+        int64_t found_a = -1, found_b = -1;
+        uint32_t bf[16];  // the second half of the line that arrived last step
+#pragma unroll
+        for (int i = 0; i < 16; i++) bf[i] = 0;
+        // After line fill f is read: issue what the slot takes next (fill f+1, or after the
+        // last fill the next tile's warm fill / the next stream's queue entry).
+        auto refill = [&](int f) {
+            if (f < 2 * g.K) {
+                rk_dma_line(g.ld, sl32, ct, g.L, f + 1, lane);
+            } else {
+                if (reserve && !res_issued) {  // this stream's ring entry, reserved late
+                    pe_raw = qht_add(a, lane, 1ull << 32);
+                    res_issued = true;
+                }
+                if (switching) {
+                    pentry_dma(a, lane, tk, sl32);
+                    entry_issued = true;
+                } else if (!last_of_region) {  // the next tile has its own geometry
+                    const RkGeom gn = rk_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n);
+                    rk_dma_warm(gn.ld, sl32, ct_next, gn.L, lane);
+                    next_issued = true;
+                }
+            }
+        };
+        // Hit check of one chain's 64 bytes at coordinate c (state before: h0/l0).
+        auto check = [&](uint32_t mm, int64_t& found, int64_t c, uint32_t h0, uint32_t l0, const uint32_t (&in)[16],
+                         const uint32_t (&prv)[16]) {
+            if (mm == 0 && found < 0 && c <= hi) {
+                const int64_t blo = lo - c, bhi = hi - c;
+                const uint32_t idx = rk_exact64(kx, h0, l0, in, prv, blo < 0 ? 0 : static_cast<int>(blo),
+                                                bhi > 63 ? 63 : static_cast<int>(bhi));
+                if (idx < 64u) found = c + idx;
+            }
+        };
+        for (int j = 0; j < g.K; j++) {
+            // ---- odd fill 2j+1: A line j (A: its first half; B: the second half of its line j-1)
+            {
+                uint32_t dw[32], na[16];
+                __builtin_amdgcn_sched_barrier(0);
+#if KCDC_RK_ABL != 3
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+                read_step128(sl, lane, c0 + 128 * j, cur.off0, dw);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                refill(2 * j + 1);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < 16; i++) na[i] = dw[i];
+                const uint32_t ha0 = ha, la0 = la, hb0 = hb, lb0 = lb;
+                uint32_t ma = 0xFFFFFFFFu, mb = 0xFFFFFFFFu;
+                if (j == 0) {
+                    rk_step64<true, false>(kx, ha, la, na, pa, hb, lb, bf, pb, ma, mb);
+                } else {
+                    rk_step64<true, true>(kx, ha, la, na, pa, hb, lb, bf, pb, ma, mb);
+                    check(mb, found_b, c0b + 128 * (j - 1) + 64, hb0, lb0, bf, pb);
+#pragma unroll
+                    for (int i = 0; i < 16; i++) pb[i] = bf[i];
+                }
+                check(ma, found_a, c0 + 128 * j, ha0, la0, na, pa);
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    pa[i] = na[i];
+                    bf[i] = dw[16 + i];  // A's second half, next step
+                }
+            }
+            // ---- even fill 2j+2: B line j (A: the second half of its line j; B: its first half)
+            {
+                uint32_t dw[32], nb[16];
+                __builtin_amdgcn_sched_barrier(0);
+#if KCDC_RK_ABL != 3
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+                read_step128(sl, lane, c0b + 128 * j, cur.off0, dw);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                refill(2 * j + 2);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < 16; i++) nb[i] = dw[i];
+                const uint32_t ha0 = ha, la0 = la, hb0 = hb, lb0 = lb;
+                uint32_t ma = 0xFFFFFFFFu, mb = 0xFFFFFFFFu;
+                rk_step64<true, true>(kx, ha, la, bf, pa, hb, lb, nb, pb, ma, mb);
+                check(ma, found_a, c0 + 128 * j + 64, ha0, la0, bf, pa);
+                check(mb, found_b, c0b + 128 * j, hb0, lb0, nb, pb);
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    pa[i] = bf[i];
+                    pb[i] = nb[i];
+                    bf[i] = dw[16 + i];  // B's second half, next step
+                }
+            }
+        }
+        // ---- D: B's last 64 bytes (the slot meanwhile takes the next warm fill / entry)
+        {
+            const uint32_t hb0 = hb, lb0 = lb;
+            uint32_t ma = 0xFFFFFFFFu, mb = 0xFFFFFFFFu;
+            rk_step64<false, true>(kx, ha, la, bf, pa, hb, lb, bf, pb, ma, mb);
+            check(mb, found_b, c0b + 128 * (g.K - 1) + 64, hb0, lb0, bf, pb);
+        }
+        // ---- end of tile
+        if (reserve && !res_issued) {
+            pe_raw = qht_add(a, lane, 1ull << 32);
+            res_issued = true;
+        }
+        const int64_t found = found_a >= 0 ? found_a : found_b;
+        const uint64_t hit = __ballot(found >= 0);
+        bool region_changed = true;
+        bool live;
+        const int64_t forced = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;
+        if (hit) {
+            const int first = __builtin_ctzll(hit);
+            const int64_t f = static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, first))));
+            const int64_t next = f - cur.off0 + 1;
+            emit_cut(a, cur, lane, next);
+            cur.s = next;
+            cur.ct = -1;
+        } else if (last_of_region) {  // forced cut at max size (splitter_rabinkarp64.go:60-64) or the end
+            emit_cut(a, cur, lane, forced);
+            cur.s = forced;
+            cur.ct = -1;
+        } else {
+            cur.ct = ct_next;
+            budget -= kWave * g.L;
+            region_changed = false;
+        }
+        live = pstream_region(a, cur, lane);
+        if (!live && lane == 0) {
+            a.counts[cur.sid] = cur.cnt;
+            add_agent(a.queue + kQDone, 1u);
+        }
+        if (!switching && live) {  // same stream, next tile
+            issued = next_issued && !region_changed;
+            if (next_issued && region_changed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stale prefetch
+            continue;
+        }
+        if (reserve) {
+            const uint32_t pe = static_cast<uint32_t>(
+                qht_value(static_cast<uint32_t>(pe_raw), static_cast<uint32_t>(pe_raw >> 32)) >> 32);
+            pwrite(a, lane, pe, cur, !live);
+        } else if (live) {  // a candidate kept the stream alive past its predicted last tile
+            const uint64_t ht = qht_take(a, lane, 1ull << 32);
+            pwrite(a, lane, static_cast<uint32_t>(ht >> 32), cur, false);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the entry DMA (or a stale prefetch) has landed
+        bool took = false;
+        if (switching && entry_issued) {
+            const u32x4 ev = *reinterpret_cast<const u32x4*>(sl + 16 * (lane & 7));
+            if (pentry_ok(ev, lane, tk) && static_cast<uint32_t>(__builtin_amdgcn_readlane(ev.w, 0)) != kTombstone) {
+                PStream nx;
+                pentry_decode(nx, ev);
+                uniformize(nx);
+                if (!pcheck(a, lane, nx, tk, 2)) return;
+                cur = nx;
+                budget = pipe_quantum(nbacklog);
+                took = true;
+                issued = false;
+                if (!pstream_region(a, cur, lane)) {
+                    if (lane == 0) {
+                        a.counts[cur.sid] = cur.cnt;
+                        add_agent(a.queue + kQDone, 1u);
+                    }
+                    need_take = true;
+                    take_t = 0xFFFFFFFFu;
+                    take_backlog = 0;
+                    take_claim = 0xFFFFFFFFu;
+                }
+                continue;
+            }
+        }
+        if (!took) {
+            need_take = true;
+            take_t = switching ? tk : 0xFFFFFFFFu;
+            take_backlog = nbacklog;
+            take_claim = 0xFFFFFFFFu;
+        }
+    }
+}
+
 // Before each pipelined launch: zero the queue header (tail := n) and write ring entries
 // 0..n-1 = every stream's initial state; later entries get tag 0 (never a valid tag).
 // Head starts at min(n, launch waves): wave w's first ticket is w, taken without an atomic
@@ -2678,7 +3207,9 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         hipLaunchKernelGGL(dev::split_fixed_kernel, dim3(s.nstreams), dim3(256), 0, st, a);
     } else {
         const unsigned cus = static_cast<unsigned>(t->cus);
-        const bool dma = algo.kind == kBuzhash && KCDC_DMA;
+        const bool dma = (algo.kind == kBuzhash || (algo.kind == kRabinKarp && KCDC_RK_PIPE)) && KCDC_DMA;
+        if (algo.kind == kRabinKarp && dma && tables().rk_shift != 45)
+            return set_error(-22, "Rabin-Karp kernel: the polynomial must have degree 53");
         const unsigned wg_waves = dma ? dev::kDmaWaves : dev::kBatchWaves;
         const unsigned need = (s.nstreams + wg_waves - 1) / wg_waves;
         unsigned grid = need < cus ? need : cus;
@@ -2750,7 +3281,12 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
             if (e != hipSuccess) return hip_fail(e, "queue reset");
         }
         // persistent grid: one workgroup per CU, never more workgroups than the streams need
-        if (dma) {
+        if (dma && algo.kind == kRabinKarp) {
+            hipLaunchKernelGGL(dev::split_batch_rk_kernel, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0, st, a);
+            if (g_test.force_error)
+                hipLaunchKernelGGL(dev::poison_counts_kernel, dim3(std::min<unsigned>((s.nstreams + 255) / 256, 256u)),
+                                   dim3(256), 0, st, a);
+        } else if (dma) {
             const bool top = buz_frame(static_cast<uint32_t>(algo.mask())).top;
             if (top)
                 hipLaunchKernelGGL(dev::split_batch_pipe_kernel<true>, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0,

@@ -185,11 +185,13 @@ def test_zero_runs_and_dense_candidates(gpu):
 
 
 # ------------------------------------------------ config 2 (bench workload)
-def test_config2_full_parity(gpu):
-    """BASELINE configs[1]: 4096 x 4 MiB counter-PRNG streams, DYNAMIC-4M-BUZHASH,
-    every stream's cut list bit-exact vs the oracle (threaded C restatement)."""
+@pytest.mark.parametrize("name", ["DYNAMIC-4M-BUZHASH", "DYNAMIC-4M-RABINKARP", "DYNAMIC-128K-RABINKARP"])
+def test_config2_full_parity(gpu, name):
+    """BASELINE configs[1]: 4096 x 4 MiB counter-PRNG streams (the default splitter, and the
+    Rabin-Karp kernel at two averages), every stream's cut list bit-exact vs the oracle
+    (threaded C restatement)."""
     import torch
-    name, ns, L = "DYNAMIC-4M-BUZHASH", 4096, 4 << 20
+    ns, L = 4096, 4 << 20
     data = torch.empty(ns * L, dtype=torch.uint8, device=gpu)
     batch.fill_prng(data, L, ns, L, SEED, 0)
     b = batch.make_device_batch(name, [data.data_ptr() + i * L for i in range(ns)], [L] * ns, gpu)

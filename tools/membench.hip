@@ -149,8 +149,14 @@ int main(int argc, char** argv) {
     if (occ)
         cfgs = {CFGD(128, 1, 8, 2, 250), CFGD(64, 1, 8, 2, 125), CFGD(64, 1, 12, 2, 125), CFGD(64, 1, 16, 2, 125),
                 CFGD(128, 1, 12, 2, 250), CFGD(64, 2, 12, 2, 125), CFGD(128, 1, 8, 2, 300), CFGD(64, 1, 12, 2, 150)};
+    // Rabin-Karp plan: 64-B runs (two chains per lane, 64 B each per step) vs 128-B runs,
+    // 8 waves/CU, emulated hashing of ~10.5 VALU per byte (D = 2 ops per unit)
+    const bool rk = argc > 1 && std::string(argv[1]) == "rk";
+    if (rk)
+        cfgs = {CFGD(128, 1, 8, 2, 672), CFGD(64, 2, 8, 2, 336), CFGD(64, 1, 8, 2, 336), CFGD(128, 1, 8, 2, 0),
+                CFGD(64, 2, 8, 2, 0), CFGD(64, 2, 8, 0, 336), CFGD(128, 1, 8, 2, 336), CFGD(64, 2, 8, 2, 168)};
     for (int rep = 0; rep < (calib ? 1 : 2); rep++) {
-      for (int layout = (depth || occ ? 1 : 0); layout < (calib ? 1 : depth || occ ? 2 : 3); layout++) {
+      for (int layout = (depth || occ || rk ? 1 : 0); layout < (calib ? 1 : depth || occ || rk ? 2 : 3); layout++) {
         for (auto& c : cfgs) {
             const size_t lds = static_cast<size_t>(c.w) * c.s * 64 * c.run;
             if (lds > 160 * 1024) {
