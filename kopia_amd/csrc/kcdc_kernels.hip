@@ -1970,6 +1970,56 @@ __device__ __forceinline__ void rk_step64(const RkCtx& k, uint32_t& ha, uint32_t
     }
 }
 
+#ifndef KCDC_RK_ORDER
+#define KCDC_RK_ORDER 1  // 1: per byte, the two mod[] reads issue BEFORE the outx[] prefetches of byte
+                         // x + W, so the in-order LDS return of the chain's read is not queued
+                         // behind them (0: prefetch the next window first): 2.57 vs 2.72 ms
+#endif
+template <bool ACT_A, bool ACT_B>
+__device__ __forceinline__ void rk_step64_ord(const RkCtx& k, uint32_t& ha, uint32_t& la, const uint32_t (&a)[16],
+                                              const uint32_t (&pa)[16], uint32_t& hb, uint32_t& lb,
+                                              const uint32_t (&b)[16], const uint32_t (&pb)[16], uint32_t& ma,
+                                              uint32_t& mb) {
+    constexpr int W = KCDC_RK_W;
+    uint64_t oa[64], ob[64];  // only W live at a time (unrolled: register renaming)
+#pragma unroll
+    for (int i = 0; i < W; i++) {
+        if (ACT_A) oa[i] = rk_out(k, pa[i >> 2], i & 3);
+        if (ACT_B) ob[i] = rk_out(k, pb[i >> 2], i & 3);
+    }
+#pragma unroll
+    for (int x = 0; x < 64; x++) {
+        const int sh = kRkModRep == 32 ? 8 : 7;
+        uint64_t mA = 0, mB = 0;
+        __builtin_amdgcn_sched_barrier(0);
+        if (ACT_A) mA = *reinterpret_cast<const uint64_t*>(k.modb + ((__builtin_amdgcn_ubfe(ha, kRkIdxBit, 8) << sh) | k.lane8m));
+        if (ACT_B) mB = *reinterpret_cast<const uint64_t*>(k.modb + ((__builtin_amdgcn_ubfe(hb, kRkIdxBit, 8) << sh) | k.lane8m));
+        if (x + W < 64) {
+            if (ACT_A) oa[x + W] = rk_out(k, pa[(x + W) >> 2], (x + W) & 3);
+            if (ACT_B) ob[x + W] = rk_out(k, pb[(x + W) >> 2], (x + W) & 3);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (ACT_A) {
+            const uint32_t th = __builtin_amdgcn_alignbit(ha, la, 24);
+            const uint32_t tl = __builtin_amdgcn_perm(a[x >> 2], la, 0x02010000u | (4u + (x & 3)));
+            ha = __builtin_amdgcn_bitop3_b32(th, static_cast<uint32_t>(mA >> 32), static_cast<uint32_t>(oa[x] >> 32), 0x96);
+            la = __builtin_amdgcn_bitop3_b32(tl, static_cast<uint32_t>(mA), static_cast<uint32_t>(oa[x]), 0x96);
+            ma = min(ma, la & k.mask);
+        }
+        if (ACT_B) {
+            const uint32_t th = __builtin_amdgcn_alignbit(hb, lb, 24);
+            const uint32_t tl = __builtin_amdgcn_perm(b[x >> 2], lb, 0x02010000u | (4u + (x & 3)));
+            hb = __builtin_amdgcn_bitop3_b32(th, static_cast<uint32_t>(mB >> 32), static_cast<uint32_t>(ob[x] >> 32), 0x96);
+            lb = __builtin_amdgcn_bitop3_b32(tl, static_cast<uint32_t>(mB), static_cast<uint32_t>(ob[x]), 0x96);
+            mb = min(mb, lb & k.mask);
+        }
+        if ((x & 3) == 3) {
+            if (ACT_A) asm volatile("" : "+v"(ma));
+            if (ACT_B) asm volatile("" : "+v"(mb));
+        }
+    }
+}
+
 // Exact re-run of one chain's 64 bytes from (hi, lo) (rare): first index in [lo_i, hi_i]
 // with (lo & mask) == 0, else 64.
 __device__ uint32_t rk_exact64(const RkCtx& k, uint32_t hi, uint32_t lo, const uint32_t (&in)[16],
@@ -2048,6 +2098,11 @@ __device__ __forceinline__ void rk_mask_head(uint32_t (&dw)[16], int64_t c, int6
     }
 }
 
+#if KCDC_RK_ORDER
+#define RK_STEP rk_step64_ord
+#else
+#define RK_STEP rk_step64
+#endif
 __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_rk_kernel(BatchArgs a) {
     __shared__ RkTables smt;
     __shared__ DmaSlots smslots;
@@ -2227,9 +2282,9 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                 const uint32_t ha0 = ha, la0 = la, hb0 = hb, lb0 = lb;
                 uint32_t ma = 0xFFFFFFFFu, mb = 0xFFFFFFFFu;
                 if (j == 0) {
-                    rk_step64<true, false>(kx, ha, la, na, pa, hb, lb, bf, pb, ma, mb);
+                    RK_STEP<true, false>(kx, ha, la, na, pa, hb, lb, bf, pb, ma, mb);
                 } else {
-                    rk_step64<true, true>(kx, ha, la, na, pa, hb, lb, bf, pb, ma, mb);
+                    RK_STEP<true, true>(kx, ha, la, na, pa, hb, lb, bf, pb, ma, mb);
                     check(mb, found_b, c0b + 128 * (j - 1) + 64, hb0, lb0, bf, pb);
 #pragma unroll
                     for (int i = 0; i < 16; i++) pb[i] = bf[i];
@@ -2257,7 +2312,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                 for (int i = 0; i < 16; i++) nb[i] = dw[i];
                 const uint32_t ha0 = ha, la0 = la, hb0 = hb, lb0 = lb;
                 uint32_t ma = 0xFFFFFFFFu, mb = 0xFFFFFFFFu;
-                rk_step64<true, true>(kx, ha, la, bf, pa, hb, lb, nb, pb, ma, mb);
+                RK_STEP<true, true>(kx, ha, la, bf, pa, hb, lb, nb, pb, ma, mb);
                 check(ma, found_a, c0 + 128 * j + 64, ha0, la0, bf, pa);
                 check(mb, found_b, c0b + 128 * j, hb0, lb0, nb, pb);
 #pragma unroll
@@ -2272,7 +2327,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         {
             const uint32_t hb0 = hb, lb0 = lb;
             uint32_t ma = 0xFFFFFFFFu, mb = 0xFFFFFFFFu;
-            rk_step64<false, true>(kx, ha, la, bf, pa, hb, lb, bf, pb, ma, mb);
+            RK_STEP<false, true>(kx, ha, la, bf, pa, hb, lb, bf, pb, ma, mb);
             check(mb, found_b, c0b + 128 * (g.K - 1) + 64, hb0, lb0, bf, pb);
         }
         // ---- end of tile
