@@ -161,6 +161,29 @@ def roofline(kernel: str, config: str, kern_ms: float, rolled: int, stream_bytes
             "stream_gbs": round(stream_bytes / kern_s / 1e9, 1)}
 
 
+def h2d_rates(host: np.ndarray, dev) -> dict:
+    """The PCIe H2D ceiling of the host-inclusive path, measured on this box: plain copies of
+    the same host bytes (pageable, as kcdc_split_batch_host receives them) and of a pinned
+    buffer, 1 GiB at a time."""
+    import torch
+    n = min(host.size, 1 << 30)
+    src = torch.from_numpy(host[:n])
+    dst = torch.empty(n, dtype=torch.uint8, device=dev)
+    pinned = torch.empty(n, dtype=torch.uint8).pin_memory()
+    pinned.copy_(src)
+    res = {}
+    for key, t in (("pageable", src), ("pinned", pinned)):
+        dst.copy_(t)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            dst.copy_(t, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        res[key] = round(3 * n / GiB / (time.perf_counter() - t0), 3)
+    del pinned, dst
+    return res
+
+
 # --------------------------------------------------------- CPU baseline
 def host_cpu_info() -> dict:
     model = None
@@ -315,6 +338,8 @@ def bench_batch(args, comm: Comm):
         dt = time.perf_counter() - t0
         assert all(np.array_equal(hc[i], cuts[i]) for i in range(nh))
         out["host_inclusive_gib_s"] = round(nh * L / GiB / dt, 3)
+        out["h2d_gib_s"] = h2d_rates(host, dev)
+        out["host_inclusive_vs_pageable_h2d"] = round(out["host_inclusive_gib_s"] / out["h2d_gib_s"]["pageable"], 3)
         del host, views
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

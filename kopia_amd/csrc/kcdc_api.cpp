@@ -618,13 +618,23 @@ extern "C" int kcdc_split_batch_device(const char* name, const uint8_t* const* d
 }
 
 namespace {
-struct HostCtx {
-    std::mutex mu;
+// One slot of the host batch path: a device arena for a group's bytes, its cut lists, and
+// pinned host copies of the answers (so the D2H never blocks the host thread).
+struct HostSlot {
     uint8_t* d_data = nullptr;
     size_t d_data_cap = 0;
     void* d_meta = nullptr;
     size_t d_meta_cap = 0;
+    uint64_t* h_meta = nullptr;  // pinned: counts then cuts of the group
+    size_t h_meta_cap = 0;
     hipStream_t stream = nullptr;
+    bool busy = false;
+    uint32_t i0 = 0, i1 = 0;
+    uint64_t gcap = 0;
+};
+struct HostCtx {
+    std::mutex mu;
+    HostSlot slot[2];
 };
 HostCtx g_host[64];
 
@@ -637,8 +647,38 @@ int grow(void** p, size_t* cap, size_t need) {
     *cap = need;
     return KCDC_OK;
 }
+int grow_pinned(uint64_t** p, size_t* cap, size_t need) {
+    if (need <= *cap) return KCDC_OK;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(p), need, hipHostMallocDefault), "hipHostMalloc");
+    *cap = need;
+    return KCDC_OK;
+}
+// Wait for a slot's group and hand its answers to the caller's arrays.
+int host_slot_finish(HostSlot& S, uint32_t nstreams, uint64_t* cuts, uint64_t cuts_cap, const uint64_t* cut_base,
+                     uint64_t* counts) {
+    if (!S.busy) return KCDC_OK;
+    S.busy = false;
+    HIP_TRY(hipStreamSynchronize(S.stream), "sync");
+    const uint32_t ng = S.i1 - S.i0;
+    std::memcpy(counts + S.i0, S.h_meta, ng * sizeof(uint64_t));
+    if (S.gcap) std::memcpy(cuts + cut_base[S.i0], S.h_meta + ng, S.gcap * sizeof(uint64_t));
+    for (uint32_t k = S.i0; k < S.i1; k++) {
+        if (counts[k] == KCDC_COUNT_FAILED) return set_error(KCDC_EIO, "batch launch failed on the device");
+        const uint64_t capk = (k + 1 < nstreams ? cut_base[k + 1] : cuts_cap) - cut_base[k];
+        if (counts[k] > capk) return set_error(KCDC_EOVERFLOW, "cut capacity too small for a stream");
+    }
+    return KCDC_OK;
+}
 }  // namespace
 
+// Host buffers in, cut lists out (snapshot/upload/upload.go:393-435 feeds the splitter from
+// files in host memory).  Streams go in groups of at most kArena bytes through two slots on
+// two HIP streams: while group k splits and its answers come back on one stream, group k+1's
+// bytes go up on the other, so the PCIe H2D copy -- the bound of this path -- never waits for
+// the GPU (the split of a 256 MiB group takes ~25 us against ~5 ms of transfer).
 extern "C" int kcdc_split_batch_host(const char* name, const uint8_t* const* h_ptrs, const uint64_t* lens,
                                      uint32_t nstreams, uint64_t* cuts, uint64_t cuts_cap, const uint64_t* cut_base,
                                      uint64_t* counts, int device) {
@@ -651,11 +691,11 @@ extern "C" int kcdc_split_batch_host(const char* name, const uint8_t* const* h_p
     DeviceGuard g(device);
     HostCtx& C = g_host[device];
     std::lock_guard<std::mutex> lk(C.mu);
-    if (!C.stream) HIP_TRY(hipStreamCreateWithFlags(&C.stream, hipStreamNonBlocking), "hipStreamCreate");
-    // Groups of streams whose bytes fit a 1 GiB device arena (a stream larger than
-    // that gets an arena of its own size).
-    const size_t kArena = size_t(1) << 30;
-    uint32_t i0 = 0;
+    for (HostSlot& S : C.slot)
+        if (!S.stream) HIP_TRY(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking), "hipStreamCreate");
+    // Groups of streams whose bytes fit one arena (a larger stream gets an arena of its own size).
+    const size_t kArena = size_t(256) << 20;
+    uint32_t i0 = 0, k = 0;
     while (i0 < nstreams) {
         uint32_t i1 = i0;
         size_t bytes = 0;
@@ -665,43 +705,62 @@ extern "C" int kcdc_split_batch_host(const char* name, const uint8_t* const* h_p
             bytes += sz;
             i1++;
         }
+        HostSlot& S = C.slot[k++ & 1];
+        rc = host_slot_finish(S, nstreams, cuts, cuts_cap, cut_base, counts);  // the group before last
+        if (rc) break;
         const uint32_t ng = i1 - i0;
-        uint64_t gcap = (i1 < nstreams ? cut_base[i1] : cuts_cap) - cut_base[i0];
-        rc = grow(reinterpret_cast<void**>(&C.d_data), &C.d_data_cap, std::max<size_t>(bytes, 256));
-        if (rc) return rc;
-        const size_t meta = ng * sizeof(uint64_t) + gcap * sizeof(uint64_t) + 64;
-        rc = grow(&C.d_meta, &C.d_meta_cap, meta);
-        if (rc) return rc;
+        const uint64_t gcap = (i1 < nstreams ? cut_base[i1] : cuts_cap) - cut_base[i0];
+        rc = grow(reinterpret_cast<void**>(&S.d_data), &S.d_data_cap, std::max<size_t>(bytes, 256));
+        if (!rc) rc = grow(&S.d_meta, &S.d_meta_cap, (ng + gcap) * sizeof(uint64_t) + 64);
+        if (!rc) rc = grow_pinned(&S.h_meta, &S.h_meta_cap, (ng + gcap) * sizeof(uint64_t) + 64);
+        if (rc) break;
         std::vector<const uint8_t*> dptr(ng);
         std::vector<uint64_t> base(ng);
+        // Runs of streams that are adjacent in host memory go up as ONE copy (each pageable
+        // copy call costs ~15 us of runtime staging: 1024 x 4 MiB copies lost 15% of the link);
+        // inside a run the device keeps the host layout, each run starts 256-byte aligned.
         size_t off = 0;
-        for (uint32_t k = 0; k < ng; k++) {
-            dptr[k] = C.d_data + off;
-            base[k] = cut_base[i0 + k] - cut_base[i0];
-            if (lens[i0 + k])
-                HIP_TRY(hipMemcpyAsync(C.d_data + off, h_ptrs[i0 + k], lens[i0 + k], hipMemcpyHostToDevice, C.stream),
-                        "H2D stream");
-            off += (lens[i0 + k] + 255) & ~size_t(255);
+        for (uint32_t j = 0; j < ng;) {
+            uint32_t e = j + 1;
+            size_t run = lens[i0 + j];
+            while (e < ng && h_ptrs[i0 + e] == h_ptrs[i0 + e - 1] + lens[i0 + e - 1]) run += lens[i0 + e++];
+            for (uint32_t q = j; q < e; q++) {
+                dptr[q] = S.d_data + off + (h_ptrs[i0 + q] - h_ptrs[i0 + j]);
+                base[q] = cut_base[i0 + q] - cut_base[i0];
+            }
+            if (run) {
+                const hipError_t err = hipMemcpyAsync(S.d_data + off, h_ptrs[i0 + j], run, hipMemcpyHostToDevice, S.stream);
+                if (err != hipSuccess) {
+                    rc = set_error(KCDC_EIO, std::string("H2D stream: ") + hipGetErrorString(err));
+                    break;
+                }
+            }
+            off += (run + 255) & ~size_t(255);
+            j = e;
         }
-        auto* d_cnt = static_cast<uint64_t*>(C.d_meta);
+        if (rc) break;
+        auto* d_cnt = static_cast<uint64_t*>(S.d_meta);
         auto* d_cuts = d_cnt + ng;
         // each stream through the batch kernel or, if it would be the batch's tail, the long path
-        rc = kcdc_split_files_device(name, dptr.data(), lens + i0, ng, d_cuts, gcap, base.data(), d_cnt, C.stream);
-        if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(counts + i0, d_cnt, ng * sizeof(uint64_t), hipMemcpyDeviceToHost, C.stream), "D2H");
-        if (gcap)
-            HIP_TRY(hipMemcpyAsync(cuts + cut_base[i0], d_cuts, gcap * sizeof(uint64_t), hipMemcpyDeviceToHost,
-                                   C.stream),
-                    "D2H cuts");
-        HIP_TRY(hipStreamSynchronize(C.stream), "sync");
-        for (uint32_t k = i0; k < i1; k++) {
-            if (counts[k] == KCDC_COUNT_FAILED) return set_error(KCDC_EIO, "batch launch failed on the device");
-            const uint64_t capk = (k + 1 < nstreams ? cut_base[k + 1] : cuts_cap) - cut_base[k];
-            if (counts[k] > capk) return set_error(KCDC_EOVERFLOW, "cut capacity too small for a stream");
+        rc = kcdc_split_files_device(name, dptr.data(), lens + i0, ng, d_cuts, gcap, base.data(), d_cnt, S.stream);
+        if (rc) break;
+        const hipError_t e = hipMemcpyAsync(S.h_meta, S.d_meta, (ng + gcap) * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                            S.stream);
+        if (e != hipSuccess) {
+            rc = set_error(KCDC_EIO, std::string("D2H: ") + hipGetErrorString(e));
+            break;
         }
+        S.busy = true;
+        S.i0 = i0;
+        S.i1 = i1;
+        S.gcap = gcap;
         i0 = i1;
     }
-    return KCDC_OK;
+    for (HostSlot& S : C.slot) {  // drain both slots, also after an error (no work left in flight)
+        const int r2 = host_slot_finish(S, nstreams, cuts, cuts_cap, cut_base, counts);
+        if (!rc) rc = r2;
+    }
+    return rc;
 }
 
 // ================================================================ long stream

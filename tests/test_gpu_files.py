@@ -87,3 +87,21 @@ def test_host_batch_routes_large_streams():
     want = coracle.split_batch(name, streams, nthreads=8)
     for i, (g, w) in enumerate(zip(got, want)):
         assert np.array_equal(g, np.asarray(w, dtype=np.int64)), (i, sizes[i])
+
+
+def test_host_batch_adjacent_runs():
+    """kcdc_split_batch_host copies streams that are adjacent in host memory as one run (the
+    device keeps their relative layout, so odd offsets inside a run): views of one buffer
+    with and without gaps, empty views among them, groups larger than one 256 MiB arena."""
+    name = "DYNAMIC-1M-BUZHASH"
+    rng = np.random.default_rng(5)
+    buf = coracle.gen_stream(SEED, 4242, 600 << 20)
+    views, pos = [], 0
+    while pos < buf.size - (8 << 20):
+        n = int(rng.integers(0, 6 << 20))
+        views.append(buf[pos:pos + n])
+        pos += n + (int(rng.integers(1, 4096)) if rng.random() < 0.3 else 0)  # sometimes a gap
+    got = batch.split_batch_host(name, views)
+    want = coracle.split_batch(name, views, nthreads=8)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert np.array_equal(g, np.asarray(w, dtype=np.int64)), (i, views[i].size)
