@@ -327,6 +327,9 @@ def bench_batch(args, comm: Comm):
     out["roofline"] = roofline(BATCH_KERNEL[int(info.kind)], cfg, kern_ms, rolled, ns * L)
     out["cut_stats"] = {"chunks": int(sum(c.size for c in cuts)), "rolled_fraction": round(rolled / (ns * L), 4)}
 
+    if args.hash and rank == 0:
+        out["hash"] = bench_hash(args, data, ns, L, cuts, dev)
+
     if rank == 0 and world == 1 and not args.no_host_inclusive:
         # host-inclusive: pageable host buffers -> H2D -> kernel -> D2H (kcdc_split_batch_host)
         nh = min(ns, 1024)
@@ -347,6 +350,56 @@ def bench_batch(args, comm: Comm):
         if args.config == 2:
             out["cpu_baseline"]["config1_gb_s_1thread"] = cpu_config1()
     return out
+
+
+def bench_hash(args, data, ns: int, L: int, cuts: list, dev) -> dict:
+    """§8f #2: keyed BLAKE2 content hash of every chunk the split produced
+    (repo/content/content_manager.go:812, repo/hashing/hashing.go:78-101), on the device.
+    A chunk is one sequential BLAKE2 chain (one lane), so two figures: the batch alone (its
+    5,7xx chunks: bounded by the longest chunk) and `--hash-inflight` batches' chunk tables
+    in one launch (the pipelined upload case: many chunks in flight; the same bytes are
+    re-read and re-hashed per table, 16 GiB each).  CPU baseline: hashlib, one thread."""
+    import hashlib
+    import torch
+    from kopia_amd import hashing as kh
+    name, key = args.hash, bytes(range(32))
+    offs, lens = kh.chunk_table([i * L for i in range(ns)], cuts)
+    total = int(lens.sum())
+
+    def timed(o, ln, reps):
+        kh.hash_chunks_device(name, data.data_ptr(), o, ln, key, dev)
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            out = kh.hash_chunks_device(name, data.data_ptr(), o, ln, key, dev)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) / reps, out
+
+    ms1, out = timed(offs, lens, 3)
+    # parity of a sample against the oracle (hashlib, RFC 7693; tests/test_hash_oracle.py)
+    host = None
+    bad = 0
+    pick = list(range(0, len(offs), max(1, len(offs) // 48)))
+    got = out.cpu().numpy()
+    fn, nn, keep = {"BLAKE2B-256-128": (hashlib.blake2b, 32, 16), "BLAKE2B-256": (hashlib.blake2b, 32, 32),
+                    "BLAKE2S-128": (hashlib.blake2s, 16, 16), "BLAKE2S-256": (hashlib.blake2s, 32, 32)}[name]
+    for i in pick:
+        chunk = data[int(offs[i]):int(offs[i] + lens[i])].cpu().numpy().tobytes()
+        bad += fn(chunk, key=key, digest_size=nn).digest()[:keep] != got[i].tobytes()
+    R = args.hash_inflight
+    msR, _ = timed(np.tile(offs, R), np.tile(lens, R), 1)
+    sample = data[: 256 << 20].cpu().numpy().tobytes()
+    t0 = time.perf_counter()
+    fn(sample, key=key, digest_size=nn).digest()
+    cpu = len(sample) / GiB / (time.perf_counter() - t0)
+    return {"algo": name, "batch_chunks": int(len(offs)), "batch_bytes": total, "largest_chunk": int(lens.max()),
+            "batch_ms": round(ms1, 3), "batch_gib_s": round(total / GiB / (ms1 * 1e-3), 2),
+            "inflight_tables": R, "inflight_chunks": int(R * len(offs)), "inflight_ms": round(msR, 3),
+            "inflight_gib_s": round(R * total / GiB / (msR * 1e-3), 2),
+            "sample_parity_mismatches": int(bad), "sample_chunks": len(pick),
+            "cpu_hashlib_1thread_gib_s": round(cpu, 3)}
 
 
 def bench_long(args, comm: Comm):
@@ -521,6 +574,9 @@ def parse(argv):
     ap.add_argument("--long-gib", type=int, default=64, help="config 3 stream size")
     ap.add_argument("--files-gib", type=int, default=32, help="config 5 bytes per GPU (256 GiB over 8 GPUs)")
     ap.add_argument("--all-names", action="store_true", help="config 5: also time every registered name")
+    ap.add_argument("--hash", default=None, help="configs 2/4: also hash every chunk on the device with this "
+                    "content hash (e.g. BLAKE2B-256-128)")
+    ap.add_argument("--hash-inflight", type=int, default=24, help="--hash: chunk tables per launch, throughput figure")
     args = ap.parse_args(argv)
     if args.config == 4:
         args.streams, args.stream_mib = 8192, 8

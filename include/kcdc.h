@@ -196,6 +196,26 @@ int kcdc_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint32
  * Host-only (no GPU needed). */
 int kcdc_gorand_read(int64_t seed, uint8_t* out, uint64_t n);
 
+/* ------------------------------------------------------------- content hashes
+ * Keyed BLAKE2 of many chunks of device-resident bytes: the content hash Kopia computes
+ * for every chunk the splitter cuts (repo/content/content_manager.go:812 ->
+ * repo/hashing/hashing.go:78-101, truncatedKeyedHashFuncFactory).  Names as registered in
+ * repo/hashing/blake_hashes.go:8-13: "BLAKE2B-256-128" (the default, hashing.go:51),
+ * "BLAKE2B-256", "BLAKE2S-128", "BLAKE2S-256".
+ * kcdc_hash_algorithms: fills names[0..cap) and returns the count.
+ * kcdc_hash_size: output bytes per chunk (16 or 32), or KCDC_ENOENT.
+ * kcdc_hash_chunks_device: chunk i is bytes [d_offsets[i], d_offsets[i] + d_lens[i]) of
+ *   d_data (any alignment); its hash goes to d_out + i * out_stride (out_stride >= the hash
+ *   size, a multiple of 4).  key: the repository's HMAC secret (<= 64 bytes for BLAKE2B,
+ *   <= 32 for BLAKE2S; BLAKE2S-128 needs one, as blake2s.New128 does).  d_order: optional
+ *   processing order (e.g. chunk indices by descending length: a wave runs until its
+ *   longest chunk is done), NULL = as given.  Asynchronous on hip_stream. */
+int kcdc_hash_algorithms(const char** names, int cap);
+int kcdc_hash_size(const char* hash_name);
+int kcdc_hash_chunks_device(const char* hash_name, const uint8_t* d_data, const uint64_t* d_offsets,
+                            const uint64_t* d_lens, const uint32_t* d_order, uint32_t nchunks, const uint8_t* key,
+                            uint32_t key_len, uint8_t* d_out, uint32_t out_stride, void* hip_stream);
+
 /* ------------------------------------------------------------- testing
  * Hooks for the library's own tests (not part of the splitter surface).
  * kcdc_test_set: process-wide knobs read by every later batch launch.

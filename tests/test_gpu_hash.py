@@ -1,0 +1,82 @@
+"""GPU: keyed BLAKE2 content hashes of many chunks (kcdc_hash_chunks_device) bit-exact
+against the oracle (hashlib, pinned by tests/test_hash_oracle.py): random chunk lengths and
+misaligned offsets, every registered name and key length class, the chunks the splitter
+cuts on config-2 streams, and the error contract."""
+import concurrent.futures as cf
+
+import numpy as np
+import pytest
+
+from kopia_amd import _lib, batch
+from kopia_amd import hashing as kh
+from oracle import coracle
+from test_hash_oracle import kopia_hash
+
+pytestmark = pytest.mark.gpu
+SEED = 0x6B6F706961
+
+
+def _hash_all(name, key, host, offs, lens):
+    import torch
+    dev = torch.device("cuda", 0)
+    d = torch.from_numpy(host).to(dev)
+    out = kh.hash_chunks_device(name, d.data_ptr(), offs, lens, key, dev)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", ["BLAKE2B-256-128", "BLAKE2B-256", "BLAKE2S-128", "BLAKE2S-256"])
+def test_random_chunks(gpu, name):
+    rng = np.random.default_rng(len(name))
+    host = coracle.gen_stream(SEED, 31, 4 << 20)
+    n = 700
+    lens = rng.integers(0, 20000, n)
+    lens[:12] = [0, 1, 3, 4, 63, 64, 65, 127, 128, 129, 255, 256]
+    offs = np.array([int(rng.integers(0, host.size - int(L))) for L in lens], dtype=np.int64)
+    maxk = 64 if name.startswith("BLAKE2B") else 32
+    for klen in sorted({0, 1, 17, 32, maxk}):
+        if name == "BLAKE2S-128" and klen == 0:
+            continue
+        key = bytes(rng.integers(0, 256, klen, dtype=np.uint8))
+        got = _hash_all(name, key, host, offs, lens)
+        for i in range(n):
+            want = kopia_hash(name, key, host[offs[i]:offs[i] + lens[i]].tobytes())
+            assert got[i].tobytes() == want, (name, klen, i, int(lens[i]), int(offs[i]))
+
+
+def test_config2_chunks(gpu):
+    """The chunks the batch splitter cuts from 256 x 4 MiB counter-PRNG streams, hashed with
+    the default algorithm and a 32-byte secret, equal the oracle's digests."""
+    import torch
+    name, ns, L = "DYNAMIC-4M-BUZHASH", 256, 4 << 20
+    dev = torch.device("cuda", 0)
+    data = torch.empty(ns * L, dtype=torch.uint8, device=dev)
+    batch.fill_prng(data, L, ns, L, SEED, 0)
+    b = batch.make_device_batch(name, [data.data_ptr() + i * L for i in range(ns)], [L] * ns, dev)
+    batch.split_batch_device(name, b)
+    cuts = batch.read_cuts(b)
+    offs, lens = kh.chunk_table([i * L for i in range(ns)], cuts)
+    key = bytes(range(32))
+    out = kh.hash_chunks_device(kh.DefaultAlgorithm, data.data_ptr(), offs, lens, key, dev)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    host = data.cpu().numpy()
+    with cf.ThreadPoolExecutor(16) as ex:
+        want = list(ex.map(lambda i: kopia_hash(kh.DefaultAlgorithm, key, host[offs[i]:offs[i] + lens[i]].tobytes()),
+                           range(len(offs))))
+    bad = [i for i in range(len(offs)) if got[i].tobytes() != want[i]]
+    assert not bad, f"{len(bad)} of {len(offs)} chunks differ"
+
+
+def test_errors(gpu):
+    import torch
+    dev = torch.device("cuda", 0)
+    d = torch.zeros(64, dtype=torch.uint8, device=dev)
+    with pytest.raises(_lib.KcdcError):
+        kh.hash_chunks_device("BLAKE2B-256", d.data_ptr(), [0], [10], b"x" * 65, dev)
+    with pytest.raises(_lib.KcdcError):
+        kh.hash_chunks_device("BLAKE2S-256", d.data_ptr(), [0], [10], b"x" * 33, dev)
+    with pytest.raises(_lib.KcdcError):
+        kh.hash_chunks_device("BLAKE2S-128", d.data_ptr(), [0], [10], b"", dev)
+    with pytest.raises(_lib.KcdcError):
+        kh.hash_chunks_device("SHA256", d.data_ptr(), [0], [10], b"k", dev)
