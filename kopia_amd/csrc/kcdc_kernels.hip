@@ -2103,6 +2103,102 @@ __device__ __forceinline__ void rk_mask_head(uint32_t (&dw)[16], int64_t c, int6
 #else
 #define RK_STEP rk_step64
 #endif
+// The line fills and drain of one tile (after its warm fill, which left both chains' states
+// and histories in ha/la, hb/lb, pa, pb): refill(f) is called right after fill f has been
+// read out of the slot (the slot is free), check(min, chain, coordinate, state before,
+// bytes, history) after each chain's 64 bytes.
+template <class Refill, class Check>
+__device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int lane, int64_t c0, int64_t c0b,
+                                        int64_t off0, int K, uint32_t& ha, uint32_t& la, uint32_t& hb, uint32_t& lb,
+                                        uint32_t (&pa)[16], uint32_t (&pb)[16], Refill&& refill, Check&& check) {
+    uint32_t bf[16];  // the second half of the line that arrived last step
+#pragma unroll
+    for (int i = 0; i < 16; i++) bf[i] = 0;
+    for (int j = 0; j < K; j++) {
+        // ---- odd fill 2j+1: A line j (A: its first half; B: the second half of its line j-1)
+        {
+            uint32_t dw[32], na[16];
+            __builtin_amdgcn_sched_barrier(0);
+#if KCDC_RK_ABL != 3
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+            read_step128(sl, lane, c0 + 128 * j, off0, dw);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            refill(2 * j + 1);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 16; i++) na[i] = dw[i];
+            const uint32_t ha0 = ha, la0 = la, hb0 = hb, lb0 = lb;
+            uint32_t ma = 0xFFFFFFFFu, mb = 0xFFFFFFFFu;
+            if (j == 0) {
+                RK_STEP<true, false>(kx, ha, la, na, pa, hb, lb, bf, pb, ma, mb);
+            } else {
+                RK_STEP<true, true>(kx, ha, la, na, pa, hb, lb, bf, pb, ma, mb);
+                check(mb, 1, c0b + 128 * (j - 1) + 64, hb0, lb0, bf, pb);
+#pragma unroll
+                for (int i = 0; i < 16; i++) pb[i] = bf[i];
+            }
+            check(ma, 0, c0 + 128 * j, ha0, la0, na, pa);
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                pa[i] = na[i];
+                bf[i] = dw[16 + i];  // A's second half, next step
+            }
+        }
+        // ---- even fill 2j+2: B line j (A: the second half of its line j; B: its first half)
+        {
+            uint32_t dw[32], nb[16];
+            __builtin_amdgcn_sched_barrier(0);
+#if KCDC_RK_ABL != 3
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+            read_step128(sl, lane, c0b + 128 * j, off0, dw);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            refill(2 * j + 2);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 16; i++) nb[i] = dw[i];
+            const uint32_t ha0 = ha, la0 = la, hb0 = hb, lb0 = lb;
+            uint32_t ma = 0xFFFFFFFFu, mb = 0xFFFFFFFFu;
+            RK_STEP<true, true>(kx, ha, la, bf, pa, hb, lb, nb, pb, ma, mb);
+            check(ma, 0, c0 + 128 * j + 64, ha0, la0, bf, pa);
+            check(mb, 1, c0b + 128 * j, hb0, lb0, nb, pb);
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                pa[i] = bf[i];
+                pb[i] = nb[i];
+                bf[i] = dw[16 + i];  // B's second half, next step
+            }
+        }
+    }
+    // ---- D: B's last 64 bytes (the slot meanwhile takes the next warm fill / entry)
+    {
+        const uint32_t hb0 = hb, lb0 = lb;
+        uint32_t ma = 0xFFFFFFFFu, mb = 0xFFFFFFFFu;
+        RK_STEP<false, true>(kx, ha, la, bf, pa, hb, lb, bf, pb, ma, mb);
+        check(mb, 1, c0b + 128 * (K - 1) + 64, hb0, lb0, bf, pb);
+    }
+}
+
+// Warm fill of a tile -> both chains' 64-byte histories (pa, pb) and states.
+__device__ __forceinline__ void rk_warm(const RkCtx& kx, const uint32_t (&dw)[32], uint32_t& ha, uint32_t& la,
+                                        uint32_t& hb, uint32_t& lb, uint32_t (&pa)[16], uint32_t (&pb)[16]) {
+    ha = la = hb = lb = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        pa[i] = dw[i];
+        pb[i] = dw[16 + i];
+    }
+#pragma unroll
+    for (int x = 0; x < 64; x++) {
+        if (x % 16 == 0) __builtin_amdgcn_sched_barrier(0);
+        rk_roll0(kx, ha, la, pa[x >> 2], x & 3);
+        rk_roll0(kx, hb, lb, pb[x >> 2], x & 3);
+    }
+}
+
 __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_rk_kernel(BatchArgs a) {
     __shared__ RkTables smt;
     __shared__ DmaSlots smslots;
@@ -2209,17 +2305,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             __builtin_amdgcn_sched_barrier(0);
             rk_dma_line(g.ld, sl32, ct, g.L, 1, lane);
             __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                pa[i] = dw[i];
-                pb[i] = dw[16 + i];
-            }
-#pragma unroll
-            for (int x = 0; x < 64; x++) {
-                if (x % 16 == 0) __builtin_amdgcn_sched_barrier(0);
-                rk_roll0(kx, ha, la, pa[x >> 2], x & 3);
-                rk_roll0(kx, hb, lb, pb[x >> 2], x & 3);
-            }
+            rk_warm(kx, dw, ha, la, hb, lb, pa, pb);
         }
         uint32_t tk = 0;
         int64_t nbacklog = 0;
@@ -2231,9 +2317,6 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         uint64_t pe_raw = 0;
         bool res_issued = false, next_issued = false, entry_issued = false;
         int64_t found_a = -1, found_b = -1;
-        uint32_t bf[16];  // the second half of the line that arrived last step
-#pragma unroll
-        for (int i = 0; i < 16; i++) bf[i] = 0;
         // After line fill f is read: issue what the slot takes next (fill f+1, or after the
         // last fill the next tile's warm fill / the next stream's queue entry).
         auto refill = [&](int f) {
@@ -2254,9 +2337,11 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                 }
             }
         };
-        // Hit check of one chain's 64 bytes at coordinate c (state before: h0/l0).
-        auto check = [&](uint32_t mm, int64_t& found, int64_t c, uint32_t h0, uint32_t l0, const uint32_t (&in)[16],
+        // Hit check of one chain's 64 bytes at coordinate c (state before: h0/l0): the
+        // chain's first candidate in [lo, hi].
+        auto check = [&](uint32_t mm, int chain, int64_t c, uint32_t h0, uint32_t l0, const uint32_t (&in)[16],
                          const uint32_t (&prv)[16]) {
+            int64_t& found = chain ? found_b : found_a;
             if (mm == 0 && found < 0 && c <= hi) {
                 const int64_t blo = lo - c, bhi = hi - c;
                 const uint32_t idx = rk_exact64(kx, h0, l0, in, prv, blo < 0 ? 0 : static_cast<int>(blo),
@@ -2264,72 +2349,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                 if (idx < 64u) found = c + idx;
             }
         };
-        for (int j = 0; j < g.K; j++) {
-            // ---- odd fill 2j+1: A line j (A: its first half; B: the second half of its line j-1)
-            {
-                uint32_t dw[32], na[16];
-                __builtin_amdgcn_sched_barrier(0);
-#if KCDC_RK_ABL != 3
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-                read_step128(sl, lane, c0 + 128 * j, cur.off0, dw);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
-                refill(2 * j + 1);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int i = 0; i < 16; i++) na[i] = dw[i];
-                const uint32_t ha0 = ha, la0 = la, hb0 = hb, lb0 = lb;
-                uint32_t ma = 0xFFFFFFFFu, mb = 0xFFFFFFFFu;
-                if (j == 0) {
-                    RK_STEP<true, false>(kx, ha, la, na, pa, hb, lb, bf, pb, ma, mb);
-                } else {
-                    RK_STEP<true, true>(kx, ha, la, na, pa, hb, lb, bf, pb, ma, mb);
-                    check(mb, found_b, c0b + 128 * (j - 1) + 64, hb0, lb0, bf, pb);
-#pragma unroll
-                    for (int i = 0; i < 16; i++) pb[i] = bf[i];
-                }
-                check(ma, found_a, c0 + 128 * j, ha0, la0, na, pa);
-#pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    pa[i] = na[i];
-                    bf[i] = dw[16 + i];  // A's second half, next step
-                }
-            }
-            // ---- even fill 2j+2: B line j (A: the second half of its line j; B: its first half)
-            {
-                uint32_t dw[32], nb[16];
-                __builtin_amdgcn_sched_barrier(0);
-#if KCDC_RK_ABL != 3
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-                read_step128(sl, lane, c0b + 128 * j, cur.off0, dw);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
-                refill(2 * j + 2);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int i = 0; i < 16; i++) nb[i] = dw[i];
-                const uint32_t ha0 = ha, la0 = la, hb0 = hb, lb0 = lb;
-                uint32_t ma = 0xFFFFFFFFu, mb = 0xFFFFFFFFu;
-                RK_STEP<true, true>(kx, ha, la, bf, pa, hb, lb, nb, pb, ma, mb);
-                check(ma, found_a, c0 + 128 * j + 64, ha0, la0, bf, pa);
-                check(mb, found_b, c0b + 128 * j, hb0, lb0, nb, pb);
-#pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    pa[i] = bf[i];
-                    pb[i] = nb[i];
-                    bf[i] = dw[16 + i];  // B's second half, next step
-                }
-            }
-        }
-        // ---- D: B's last 64 bytes (the slot meanwhile takes the next warm fill / entry)
-        {
-            const uint32_t hb0 = hb, lb0 = lb;
-            uint32_t ma = 0xFFFFFFFFu, mb = 0xFFFFFFFFu;
-            RK_STEP<false, true>(kx, ha, la, bf, pa, hb, lb, bf, pb, ma, mb);
-            check(mb, found_b, c0b + 128 * (g.K - 1) + 64, hb0, lb0, bf, pb);
-        }
+        rk_walk(kx, sl, lane, c0, c0b, cur.off0, g.K, ha, la, hb, lb, pa, pb, refill, check);
         // ---- end of tile
         if (reserve && !res_issued) {
             pe_raw = qht_add(a, lane, 1ull << 32);
@@ -2650,6 +2670,130 @@ __global__ __launch_bounds__(kScanWaves * kWave, 2) void cand_scan_kernel(BatchA
         if (pre + j < kSegK) g.seg_cand[seg * kSegK + pre + j] = static_cast<uint64_t>(cs - off0) + found[j];
     if (lane == 0)
         g.seg_cnt[seg] = (tot > kSegK ? 0x80000000u : 0u) | static_cast<uint32_t>(tot < kSegK ? tot : kSegK);
+}
+
+// Rabin-Karp candidate scan of the long path on split_batch_rk_kernel's tile walk (two
+// chains per lane, alternating 128-byte line fills, outx[] folding): one 128 KiB segment per
+// tile, persistent grid-stride over the segments of every stream of the launch, the next
+// segment's warm fill issued during the drain step.  Records what cand_scan_kernel records.
+__global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void cand_scan_rk_kernel(BatchArgs a, LongArgs g) {
+    __shared__ RkTables smt;
+    __shared__ DmaSlots smslots;
+    for (uint32_t i = threadIdx.x; i < 256u * kRkModRep; i += blockDim.x) smt.mod[i] = a.rk_mod[i / kRkModRep];
+    for (uint32_t i = threadIdx.x; i < 256u * kRkOutRep; i += blockDim.x) {
+        const uint64_t o = a.rk_out[i / kRkOutRep];
+        smt.out[i] = (o << 8) ^ a.rk_mod[(o >> 45) & 0xFFu];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & (kWave - 1);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    RkCtx kx;
+    kx.modb = reinterpret_cast<const char*>(smt.mod);
+    kx.outb = reinterpret_cast<const char*>(smt.out);
+    kx.lane8o = static_cast<uint32_t>(lane & (kRkOutRep - 1)) * 8u;
+    kx.lane8m = static_cast<uint32_t>(lane & (kRkModRep - 1)) * 8u;
+    kx.mask = a.mask;
+    uint8_t* sl = smslots.b[wave][0];
+    const uint32_t sl32 = lds_addr(sl);
+    const int64_t nw = static_cast<int64_t>(gridDim.x) * kDmaWaves;
+    struct Seg {
+        const uint8_t* abase;
+        int64_t off0, n, cs, lo, hi;
+    };
+    auto seg_of = [&](int64_t seg) {
+        const LongStream& S = g.streams[long_stream_of(g, seg)];
+        Seg q;
+        q.off0 = static_cast<int64_t>(uni64(static_cast<uint64_t>(S.off0)));
+        q.n = static_cast<int64_t>(uni64(static_cast<uint64_t>(S.n)));
+        q.abase = reinterpret_cast<const uint8_t*>(uni64(reinterpret_cast<uint64_t>(S.abase)));
+        q.cs = (seg - static_cast<int64_t>(uni64(static_cast<uint64_t>(S.seg0)))) * kSegBytes;
+        q.lo = q.cs > q.off0 ? q.cs : q.off0;
+        q.hi = (q.cs + kSegBytes < q.off0 + q.n ? q.cs + kSegBytes : q.off0 + q.n) - 1;
+        return q;
+    };
+    auto issue = [&](const Seg& q) {
+        const RkGeom t = rk_geom(q.cs, q.hi, q.abase, q.off0, q.off0 + q.n);
+        rk_dma_warm(t.ld, sl32, q.cs, t.L, lane);
+    };
+    int64_t seg = static_cast<int64_t>(blockIdx.x) * kDmaWaves + wave;
+    if (seg >= g.nseg) return;
+    Seg q = seg_of(seg);
+    issue(q);
+    for (;;) {
+        const int64_t nseg_next = seg + nw;
+        const bool has_next = nseg_next < g.nseg;
+        Seg qn = q;
+        if (has_next) qn = seg_of(nseg_next);
+        const RkGeom t = rk_geom(q.cs, q.hi, q.abase, q.off0, q.off0 + q.n);
+        const int64_t c0 = q.cs + lane * t.L, c0b = c0 + t.L / 2;
+        uint32_t ha, la, hb, lb, pa[16], pb[16];
+        {
+            uint32_t dw[32];
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            read_step128(sl, lane, -1, q.off0, dw);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            rk_dma_line(t.ld, sl32, q.cs, t.L, 1, lane);
+            __builtin_amdgcn_sched_barrier(0);
+            rk_warm(kx, dw, ha, la, hb, lb, pa, pb);
+        }
+        uint32_t fa[kSegK], fb[kSegK];
+        int na = 0, nb = 0;  // candidates per chain (kSegK + 1: more than kSegK)
+        auto refill = [&](int f) {
+            if (f < 2 * t.K)
+                rk_dma_line(t.ld, sl32, q.cs, t.L, f + 1, lane);
+            else if (has_next)
+                issue(qn);
+        };
+        auto check = [&](uint32_t mm, int chain, int64_t c, uint32_t h0, uint32_t l0, const uint32_t (&in)[16],
+                         const uint32_t (&prv)[16]) {
+            int& nf = chain ? nb : na;
+            uint32_t(&fnd)[kSegK] = chain ? fb : fa;
+            if (mm == 0 && c <= q.hi && nf <= kSegK) {  // rare: enumerate the piece's candidates exactly
+                const int64_t blo = q.lo - c, bhi = q.hi - c;
+                int from = blo < 0 ? 0 : static_cast<int>(blo);
+                const int to = bhi > 63 ? 63 : static_cast<int>(bhi);
+                while (from <= to && nf <= kSegK) {
+                    const uint32_t idx = rk_exact64(kx, h0, l0, in, prv, from, to);
+                    if (idx >= 64u) break;
+#pragma unroll
+                    for (int k = 0; k < kSegK; k++)  // fnd[nf] = ..., kept in registers (no scratch)
+                        if (k == nf) fnd[k] = static_cast<uint32_t>(c - q.cs) + idx;
+                    nf++;
+                    from = static_cast<int>(idx) + 1;
+                }
+            }
+        };
+        rk_walk(kx, sl, lane, c0, c0b, q.off0, t.K, ha, la, hb, lb, pa, pb, refill, check);
+        // this lane's candidates in position order: chain A's, then chain B's
+        const int nas = na < kSegK ? na : kSegK;
+        const int nf = na + nb > kSegK ? kSegK + 1 : na + nb;
+        uint32_t found[kSegK];
+#pragma unroll
+        for (int j = 0; j < kSegK; j++) {
+            uint32_t v = fa[j];
+#pragma unroll
+            for (int k = 0; k < kSegK; k++)
+                if (j >= nas && k == j - nas) v = fb[k];
+            found[j] = v;
+        }
+        int incl = nf;
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const int v = __shfl_up(incl, d);
+            if (lane >= d) incl += v;
+        }
+        const int tot = __shfl(incl, kWave - 1);
+        const int pre = incl - nf;
+        for (int j = 0; j < nf && j < kSegK; j++)
+            if (pre + j < kSegK) g.seg_cand[seg * kSegK + pre + j] = static_cast<uint64_t>(q.cs - q.off0) + found[j];
+        if (lane == 0)
+            g.seg_cnt[seg] = (tot > kSegK ? 0x80000000u : 0u) | static_cast<uint32_t>(tot < kSegK ? tot : kSegK);
+        if (!has_next) break;
+        seg = nseg_next;
+        q = qn;
+    }
 }
 
 // Buzhash candidate scan of the long path on the batch kernel's feeding scheme: a segment
@@ -3538,6 +3682,10 @@ int launch_split_long_multi(const Algo& algo, uint32_t m, const uint8_t* const* 
                 hipLaunchKernelGGL(dev::cand_scan_dma_kernel<true>, pgrid, dim3(dev::kDmaWaves * dev::kWave), 0, st, a, g);
             else
                 hipLaunchKernelGGL(dev::cand_scan_dma_kernel<false>, pgrid, dim3(dev::kDmaWaves * dev::kWave), 0, st, a, g);
+        } else if (algo.kind == kRabinKarp && KCDC_RK_PIPE) {  // two-chain LDS-DMA tiles, persistent
+            const dim3 pgrid(static_cast<unsigned>(
+                std::min<int64_t>(t->cus, (nseg + dev::kDmaWaves - 1) / dev::kDmaWaves)));
+            hipLaunchKernelGGL(dev::cand_scan_rk_kernel, pgrid, dim3(dev::kDmaWaves * dev::kWave), 0, st, a, g);
         } else if (algo.kind == kBuzhash) {
             hipLaunchKernelGGL(dev::cand_scan_kernel<kBuzhash>, grid, block, 0, st, a, g);
         } else {
