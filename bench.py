@@ -40,7 +40,7 @@ METRIC = "splitter throughput GiB/s (device-resident) at 1/2/4/8 GPU; boundaries
 SEED = 0x6B6F706961
 # the pipelined launch: init_ring_kernel, the splitter kernel, check_queue_kernel
 BATCH_KERNEL = {0: "kcdc::dev::split_fixed_kernel", 1: "kcdc::dev::split_batch_pipe_kernel<true>",
-                2: "kcdc::dev::split_batch_kernel<2>"}  # rocprofv3 names
+                2: "kcdc::dev::split_batch_rk_kernel"}  # rocprofv3 names
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 GiB = float(1 << 30)
 
@@ -442,7 +442,9 @@ def bench_long(args, comm: Comm):
                       "parallelism": "128 KiB segments per wave; one stream per GPU"},
            "per_gpu_gib_s": agg["per_gpu_gib_s"], "kernel_ms_events": round(ms, 3), "cuts": int(got.size)}
     # the long path scans every byte: its algorithmic bytes are the stream bytes
-    out["roofline"] = roofline("kcdc::dev::cand_scan_dma_kernel<true>", "config3", ms, L, L)
+    rk = int(info.kind) == 2
+    out["roofline"] = roofline("kcdc::dev::cand_scan_rk_kernel" if rk else "kcdc::dev::cand_scan_dma_kernel<true>",
+                               "config3" + ("-rk" if rk else ""), ms, L, L)
     out["roofline"]["algorithmic_bytes_def"] = "every stream byte (the full-scan candidate pass reads each once)"
     if comm.rank == 0 and comm.world == 1 and not args.no_cpu_baseline:
         # the oracle's single sequential pass over the same bytes: the streaming splitter fed
