@@ -841,21 +841,24 @@ extern "C" int kcdc_split_files_device(const char* name, const uint8_t* const* h
     if (!bidx.empty()) {  // one batch launch over the small streams, each keeping its cut range
         // counts[] of the batch go to a scratch array and are scattered to d_counts
         const uint32_t nb = static_cast<uint32_t>(bidx.size());
-        const size_t meta = nb * (sizeof(void*) + 3 * sizeof(uint64_t));
+        const size_t meta = nb * (sizeof(void*) + 4 * sizeof(uint64_t));
         char* m = nullptr;
         HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&m), meta, st), "hipMallocAsync meta");
         auto* d_ptrs = reinterpret_cast<const uint8_t**>(m);
         auto* d_lens = reinterpret_cast<uint64_t*>(m + nb * sizeof(void*));
         auto* d_base = d_lens + nb;
         auto* d_cnt = d_base + nb;
-        // The batch kernel takes stream k's capacity as base[k+1]-base[k], which here spans the
-        // ranges of any long streams between them: a stream that overflows its own range (the
-        // caller sized it too small) can spill into theirs, but counts[i] still exceeds the
-        // capacity the caller computed, and the long streams' cuts are written afterwards.
+        auto* d_end = d_cnt + nb;
+        // Each batch stream's cut range ends where the caller's range for it ends (cut_end),
+        // not at the next batch stream's base: a stream that overflows its range never writes
+        // into the ranges of long streams placed between batch streams.
         HIP_TRY(hipMemcpyAsync(d_ptrs, bp.data(), nb * sizeof(void*), hipMemcpyHostToDevice, st), "H2D meta");
         HIP_TRY(hipMemcpyAsync(d_lens, bl.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st), "H2D meta");
         HIP_TRY(hipMemcpyAsync(d_base, bb.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st), "H2D meta");
-        SplitArgs sa{d_ptrs, d_lens, nb, d_cuts, cuts_cap, d_base, d_cnt};
+        std::vector<uint64_t> be(nb);
+        for (uint32_t k = 0; k < nb; k++) be[k] = bidx[k] + 1 < n ? h_cut_base[bidx[k] + 1] : cuts_cap;
+        HIP_TRY(hipMemcpyAsync(d_end, be.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st), "H2D meta");
+        SplitArgs sa{d_ptrs, d_lens, nb, d_cuts, cuts_cap, d_base, d_cnt, d_end};
         rc = launch_split_batch(*a, sa, dev, stream);
         if (rc) {
             (void)hipFreeAsync(m, st);

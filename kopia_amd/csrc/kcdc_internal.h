@@ -54,6 +54,7 @@ struct SplitArgs {
     uint64_t cuts_cap;
     const uint64_t* cut_base;
     uint64_t* counts;
+    const uint64_t* cut_end = nullptr;  // optional per-stream end of the cut range (device)
 };
 // Launch the batch splitter for `algo` on `stream` (hipStream_t as void*).
 int launch_split_batch(const Algo& algo, const SplitArgs& a, int device, void* stream);

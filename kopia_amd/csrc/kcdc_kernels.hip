@@ -667,6 +667,7 @@ struct BatchArgs {
     uint32_t ring_mask;
     uint64_t* trace;  // KCDC_TRACE builds: per stream {start, end, workgroup | wave << 16} (else null)
     uint64_t cuts_cap;
+    const uint64_t* cut_end;  // optional: stream i's cut range ends at cut_end[i] (else cut_base[i+1] / cuts_cap)
     uint64_t min_size, max_size;
     const uint32_t* buz;
     const uint64_t* rk_out;
@@ -681,6 +682,11 @@ struct BatchArgs {
     uint32_t buz_rot;
     uint32_t buz_lim;  // ~mask when mask is a top-bits mask (else unused)
 };
+
+// End of stream sid's cut range (exclusive).
+__device__ __forceinline__ uint64_t cut_end_of(const BatchArgs& a, uint32_t sid) {
+    return a.cut_end ? a.cut_end[sid] : sid + 1 < a.nstreams ? a.cut_base[sid + 1] : a.cuts_cap;
+}
 
 template <int KIND>
 struct HashSmem;
@@ -735,7 +741,7 @@ __device__ __forceinline__ void split_one(const BatchArgs& a, const H& hash, uin
     const uint64_t p = uni64(reinterpret_cast<uint64_t>(a.ptrs[sid]));
     const int64_t n = static_cast<int64_t>(uni64(a.lens[sid]));
     const uint64_t cb = uni64(a.cut_base[sid]);
-    const uint64_t cend = sid + 1 < a.nstreams ? uni64(a.cut_base[sid + 1]) : a.cuts_cap;
+    const uint64_t cend = uni64(cut_end_of(a, sid));
     const uint64_t cap = cend > cb ? cend - cb : 0;
     const int64_t off0 = static_cast<int64_t>(p & 15u);
     const uint8_t* abase = reinterpret_cast<const uint8_t*>(p - static_cast<uint64_t>(off0));
@@ -1178,7 +1184,7 @@ __device__ __forceinline__ bool pcheck(const BatchArgs& a, int lane, const PStre
         } else if (st.cnt > st.cap) {
             code = 5;
             detail = st.cnt;
-        } else if (st.cap != (sid + 1 < a.nstreams ? uni64(a.cut_base[sid + 1]) : a.cuts_cap) - cb) {
+        } else if (st.cap != uni64(cut_end_of(a, sid)) - cb) {
             code = 7;
             detail = st.cap;
         } else if (!(st.sid & kProbeBit) && (st.s < 0 || st.s > st.n)) {
@@ -1276,7 +1282,7 @@ __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
         PStream st;
         const uint64_t cb = uni64(a.cut_base[sid]);
         pstream_fresh(st, sid, uni64(reinterpret_cast<uint64_t>(a.ptrs[sid])), uni64(a.lens[sid]), cb,
-                      sid + 1 < a.nstreams ? uni64(a.cut_base[sid + 1]) : a.cuts_cap);
+                      uni64(cut_end_of(a, sid)));
         uniformize(st);
         pwrite(a, lane, e0 + i, st, false);
     }
@@ -2451,7 +2457,7 @@ __global__ void init_ring_kernel(BatchArgs a, uint32_t nslots, uint32_t nwaves, 
     if (e < a.nstreams && g < static_cast<uint32_t>(kPEntryLanes)) {
         const uint64_t p = reinterpret_cast<uint64_t>(a.ptrs[e]);
         const uint64_t cb = a.cut_base[e];
-        const uint64_t cend = e + 1 < a.nstreams ? a.cut_base[e + 1] : a.cuts_cap;
+        const uint64_t cend = cut_end_of(a, e);
         const uint64_t w = g == 0 ? 0ull                           // cnt
                          : g == 1 ? 0ull                           // s
                          : g == 2 ? ~0ull                          // ct = -1: region not set up
@@ -2481,7 +2487,7 @@ __global__ void split_fixed_kernel(BatchArgs a) {
     if (sid >= a.nstreams) return;
     const uint64_t n = a.lens[sid];
     const uint64_t cb = a.cut_base[sid];
-    const uint64_t cend = sid + 1 < a.nstreams ? a.cut_base[sid + 1] : a.cuts_cap;
+    const uint64_t cend = cut_end_of(a, sid);
     const uint64_t cap = cend > cb ? cend - cb : 0;
     const uint64_t L = a.min_size;
     const uint64_t full = n / L;
@@ -3400,6 +3406,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
     a.cuts = s.cuts;
     a.cuts_cap = s.cuts_cap;
     a.cut_base = s.cut_base;
+    a.cut_end = s.cut_end;
     a.counts = s.counts;
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (algo.kind == kFixed) {

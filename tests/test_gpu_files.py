@@ -105,3 +105,35 @@ def test_host_batch_adjacent_runs():
     want = coracle.split_batch(name, views, nthreads=8)
     for i, (g, w) in enumerate(zip(got, want)):
         assert np.array_equal(g, np.asarray(w, dtype=np.int64)), (i, views[i].size)
+
+
+def test_files_overflowing_batch_stream_stays_in_its_range():
+    """A batch stream whose caller-sized cut range is too small (1 slot for many chunks) sits
+    between two long-path streams: its overflow is reported (count > its capacity) and never
+    lands in the long streams' ranges (their cuts stay exact; a sentinel after them too)."""
+    import ctypes as C
+    from kopia_amd import _lib
+    name = "DYNAMIC-128K-BUZHASH"
+    sizes = [96 << 20, 3 << 20, 96 << 20]  # long, batch (about 20 chunks), long
+    host, offs = _arena(sizes, sid0=900)
+    dev = torch.device("cuda", 0)
+    d = torch.from_numpy(host).to(dev)
+    caps = [ks.cut_capacity(name, sizes[0]), 1, ks.cut_capacity(name, sizes[2])]
+    base = np.array([0, caps[0], caps[0] + 1], dtype=np.uint64)
+    cap = int(sum(caps))
+    cuts = torch.full((cap + 8,), -7, dtype=torch.int64, device=dev)
+    counts = torch.zeros(3, dtype=torch.int64, device=dev)
+    ptrs = np.array([d.data_ptr() + o for o in offs], dtype=np.uint64)
+    lens = np.array(sizes, dtype=np.uint64)
+    _lib.check(_lib.lib().kcdc_split_files_device(name.encode(), ptrs.ctypes.data, lens.ctypes.data, 3,
+                                                  cuts.data_ptr(), cap, base.ctypes.data, counts.data_ptr(),
+                                                  C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
+    torch.cuda.synchronize()
+    c, k = cuts.cpu().numpy(), counts.cpu().numpy()
+    want = coracle.split_batch(name, [host[o:o + L] for o, L in zip(offs, sizes)], nthreads=8)
+    assert k[1] == len(want[1]) > 1  # the true count: larger than its 1-slot range
+    assert c[base[1]] == want[1][0]
+    for i in (0, 2):
+        assert k[i] == len(want[i])
+        assert np.array_equal(c[int(base[i]):int(base[i]) + k[i]], want[i]), i
+    assert (c[cap:] == -7).all()
