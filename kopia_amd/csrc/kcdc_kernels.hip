@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 #include <string>
 
@@ -2205,6 +2206,244 @@ __device__ __forceinline__ void rk_warm(const RkCtx& kx, const uint32_t (&dw)[32
     }
 }
 
+// ---------------------------------------------------------------- four chains per lane
+// Each lane runs FOUR chains (its segment in quarters, one per chain): four mod[] reads in
+// flight per lane, eight per SIMD.  The step slot still receives one whole 128-byte line
+// per lane per step, for the chains in rotation (fill f = line f/4 of chain f%4); a chain
+// consumes 32 bytes per step, so it holds its current line (and the previous line's last
+// 64 bytes, the leaving bytes of its first two quarters) in VGPRs.  Chain X starts X steps
+// after chain 0 (its first line arrives then): a tile is 2 warm fills ([A | B] and
+// [C | D] 64-byte histories) and 4n line fills, 4n + 3 steps; a chain outside its range in
+// a step (the first and last three) rolls stale registers and is restored.  The steps are
+// unrolled four at a time so which registers hold which quarter is static.
+#ifndef KCDC_RK_CHAINS
+#define KCDC_RK_CHAINS 2  // 4: the four-chain walker (rk4_walk) -- it needs ~370 VGPRs and spills
+#endif
+struct Rk4Geom {
+    int64_t L;  // bytes per lane (a multiple of 512)
+    int n;      // 128-byte lines per chain
+    Loader ld;
+};
+__device__ __forceinline__ Rk4Geom rk4_geom(int64_t ct, int64_t hi, const uint8_t* abase, int64_t off0,
+                                            int64_t nbytes_coord) {
+    const int64_t rem = hi - ct + 1;
+    int64_t per = (rem + kWave - 1) / kWave;
+    per = (per + 511) & ~int64_t(511);
+    Rk4Geom g;
+    g.L = per < kLaneMax ? per : kLaneMax;
+    g.n = static_cast<int>(g.L / 512);
+    g.ld = make_loader(abase, off0, nbytes_coord, ct >= 64 ? ct - 64 : 0);
+    return g;
+}
+// DMA lane offsets of a tile, computed once per tile in two VGPRs (the per-instruction
+// offsets of four chains' fills, hoisted by the compiler, cost ~100 VGPRs and spills).
+// Instruction i, DMA lane d: lane segment l = 8i + d/8 and 16-byte chunk jj = (d&7) ^
+// ((l>>1)&7), which is j0 for even i and j0 ^ 4 for odd i (j0 = (d&7) ^ ((d>>4)&3)).
+struct Rk4Lane {
+    uint32_t pe, po;  // (d/8) * L + 16 * jj, even / odd instructions
+    uint32_t je;      // j0 (the warm fills need the chunk's chain half)
+};
+__device__ __forceinline__ Rk4Lane rk4_lane(int64_t L, int lane) {
+    Rk4Lane r;
+    const uint32_t lb = static_cast<uint32_t>(lane) >> 3;
+    r.je = (static_cast<uint32_t>(lane) & 7u) ^ ((lb >> 1) & 7u);
+    r.pe = lb * static_cast<uint32_t>(L) + 16u * r.je;
+    r.po = lb * static_cast<uint32_t>(L) + 16u * (r.je ^ 4u);
+    asm volatile("" : "+v"(r.pe), "+v"(r.po), "+v"(r.je));  // computed here, not hoisted as 16 values
+    return r;
+}
+// Line fill f: line f/4 of chain f%4 (16-byte chunks of 128-byte runs, as dma_step128).
+__device__ __forceinline__ void rk4_dma_line(const Loader& ld, uint32_t slot, int64_t ct, int64_t L, int f,
+                                             const Rk4Lane& ln) {
+#ifdef KCDC_EXP_COMPONLY
+    return;
+#endif
+    const int32_t base = static_cast<int32_t>(ct + (f & 3) * (L / 4) + 128 * (f >> 2) - ld.tb);
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        dma_lds16(ld.d, slot + 1024u * i, base + static_cast<int32_t>(8 * i * L) + static_cast<int32_t>(i & 1 ? ln.po : ln.pe));
+}
+// Warm fill `half` (0: chains 0,1; 1: chains 2,3): lane l's slot line = [64 B before chain
+// 2h's quarter | 64 B before chain 2h+1's].
+__device__ __forceinline__ void rk4_dma_warm(const Loader& ld, uint32_t slot, int64_t ct, int64_t L, int half,
+                                             const Rk4Lane& ln) {
+#ifdef KCDC_EXP_COMPONLY
+    return;
+#endif
+    const int64_t Q = L / 4;
+    const int32_t base = static_cast<int32_t>(ct + 2 * half * Q - 64 - ld.tb);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint32_t jj = i & 1 ? ln.je ^ 4u : ln.je;
+        // (d/8) * L + 16 * (jj & 3) + (jj >> 2) * Q
+        const uint32_t lanepart = (i & 1 ? ln.po : ln.pe) - 64u * (jj >> 2) + (jj >> 2) * static_cast<uint32_t>(Q);
+        dma_lds16(ld.d, slot + 1024u * i, base + static_cast<int32_t>(8 * i * L) + static_cast<int32_t>(lanepart));
+    }
+}
+
+// 32 bytes of each of the four chains, interleaved byte by byte, read straight from the
+// line buffers (chain X consumes quarter q = (R - X) & 3 of Lb[X]; its leaving bytes are
+// Tl[X] for quarters 0, 1 and Lb[X] itself for 2, 3: static indices, no copies);
+// mk[X]: running min of (lo & mask).  The four mod[] reads of a byte issue before the
+// outx[] reads of the next byte (in-order LDS returns).
+template <int R>
+__device__ __forceinline__ uint32_t rk4_in(const uint32_t (&Lb)[4][32], int X, int i) {
+    const int q = (R - X) & 3;
+    return Lb[X][8 * q + i];
+}
+template <int R>
+__device__ __forceinline__ uint32_t rk4_lv(const uint32_t (&Lb)[4][32], const uint32_t (&Tl)[4][16], int X, int i) {
+    const int q = (R - X) & 3;
+    return q < 2 ? Tl[X][8 * q + i] : Lb[X][8 * (q - 2) + i];
+}
+template <int R>
+__device__ __forceinline__ void rk4_step32(const RkCtx& k, uint32_t (&h)[4], uint32_t (&lw)[4],
+                                           const uint32_t (&Lb)[4][32], const uint32_t (&Tl)[4][16],
+                                           uint32_t (&mk)[4]) {
+    uint64_t ox[4], nx[4];
+#pragma unroll
+    for (int X = 0; X < 4; X++) ox[X] = rk_out(k, rk4_lv<R>(Lb, Tl, X, 0), 0);
+#pragma unroll
+    for (int x = 0; x < 32; x++) {
+        const int sh = kRkModRep == 32 ? 8 : 7;
+        uint64_t m[4];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int X = 0; X < 4; X++)
+            m[X] = *reinterpret_cast<const uint64_t*>(k.modb + ((__builtin_amdgcn_ubfe(h[X], kRkIdxBit, 8) << sh) | k.lane8m));
+        if (x + 1 < 32) {
+#pragma unroll
+            for (int X = 0; X < 4; X++) nx[X] = rk_out(k, rk4_lv<R>(Lb, Tl, X, (x + 1) >> 2), (x + 1) & 3);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int X = 0; X < 4; X++) {
+            const uint32_t th = __builtin_amdgcn_alignbit(h[X], lw[X], 24);
+            const uint32_t tl = __builtin_amdgcn_perm(rk4_in<R>(Lb, X, x >> 2), lw[X], 0x02010000u | (4u + (x & 3)));
+            h[X] = __builtin_amdgcn_bitop3_b32(th, static_cast<uint32_t>(m[X] >> 32), static_cast<uint32_t>(ox[X] >> 32),
+                                               0x96);
+            lw[X] = __builtin_amdgcn_bitop3_b32(tl, static_cast<uint32_t>(m[X]), static_cast<uint32_t>(ox[X]), 0x96);
+            mk[X] = min(mk[X], lw[X] & k.mask);
+            ox[X] = nx[X];
+        }
+        if ((x & 3) == 3) {
+#pragma unroll
+            for (int X = 0; X < 4; X++) asm volatile("" : "+v"(mk[X]));
+        }
+    }
+}
+
+// Exact re-run of one chain's 32 bytes (rare): first index in [lo_i, hi_i], else 32.
+__device__ uint32_t rk_exact32(const RkCtx& k, uint32_t hi, uint32_t lo, const uint32_t (&in)[8],
+                               const uint32_t (&lv)[8], int lo_i, int hi_i) {
+    uint32_t e[8], o[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        e[j] = in[j];
+        o[j] = lv[j];
+    }
+    uint32_t first = 32;
+#pragma unroll 1
+    for (int j = 0; j < 8; j++) {
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            rk_roll(k, hi, lo, rk_out(k, o[0], b), e[0], b);
+            const int i = 4 * j + b;
+            if (first == 32 && (lo & k.mask) == 0 && i >= lo_i && i <= hi_i) first = static_cast<uint32_t>(i);
+        }
+#pragma unroll
+        for (int q = 0; q < 7; q++) {
+            e[q] = e[q + 1];
+            o[q] = o[q + 1];
+        }
+    }
+    return first;
+}
+
+// A whole four-chain tile: both warm fills (the first already in flight or landed),
+// 4n line fills and the drain steps.  refill(f): f = -2 (take warm fill 1), -1 (take line
+// fill 0), 0..4n-1 (after line fill f was read: the next fill, or after the last one the
+// next tile's warm fill / a queue entry).  check(min, chain, coordinate, state before,
+// bytes, leaving bytes) after each active chain-piece.
+template <class Refill, class Check>
+__device__ __forceinline__ void rk4_walk(const RkCtx& kx, const uint8_t* sl, int lane, int64_t c0, int64_t Q,
+                                         int64_t off0, int n, Refill&& refill, Check&& check) {
+    uint32_t Lb[4][32], Tl[4][16], h[4], lw[4];
+#pragma unroll
+    for (int w = 0; w < 2; w++) {  // warm fills: chains 2w, 2w+1 roll their 64-byte histories
+        uint32_t dw[32];
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        read_step128(sl, lane, -1, off0, dw);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        refill(w - 2);
+        __builtin_amdgcn_sched_barrier(0);
+        const int A = 2 * w, B = 2 * w + 1;
+        h[A] = lw[A] = h[B] = lw[B] = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            Tl[A][i] = dw[i];
+            Tl[B][i] = dw[16 + i];
+        }
+#pragma unroll
+        for (int x = 0; x < 64; x++) {
+            if (x % 16 == 0) __builtin_amdgcn_sched_barrier(0);
+            rk_roll0(kx, h[A], lw[A], Tl[A][x >> 2], x & 3);
+            rk_roll0(kx, h[B], lw[B], Tl[B][x >> 2], x & 3);
+        }
+    }
+    const int steps = 4 * n + 3;
+    auto step = [&](auto rc, int s) {
+        constexpr int r = decltype(rc)::value;  // the chain whose line arrives in this step
+        if (s < 4 * n) {
+            if (s >= 4) {  // the old line's last half: leaving bytes of the new quarters 0, 1
+#pragma unroll
+                for (int i = 0; i < 16; i++) Tl[r][i] = Lb[r][16 + i];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            read_step128(sl, lane, c0 + r * Q + 128 * (s >> 2), off0, Lb[r]);  // straight into the buffer
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            refill(s);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        uint32_t h0[4], l0[4], mk[4];
+#pragma unroll
+        for (int X = 0; X < 4; X++) {
+            h0[X] = h[X];
+            l0[X] = lw[X];
+            mk[X] = 0xFFFFFFFFu;
+        }
+        rk4_step32<r>(kx, h, lw, Lb, Tl, mk);
+#pragma unroll
+        for (int X = 0; X < 4; X++) {
+            const int p = s - X;  // chain X's piece in this step
+            if (p >= 0 && p < 4 * n) {
+                if (mk[X] == 0) {  // rare: the exact re-run needs the piece's bytes as arrays
+                    uint32_t in[8], lv[8];
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        in[i] = rk4_in<r>(Lb, X, i);
+                        lv[i] = rk4_lv<r>(Lb, Tl, X, i);
+                    }
+                    check(mk[X], X, c0 + X * Q + 32 * p, h0[X], l0[X], in, lv);
+                }
+            } else {  // outside its range (ramp): undo the rolls over stale registers
+                h[X] = h0[X];
+                lw[X] = l0[X];
+            }
+        }
+    };
+    for (int s0 = 0; s0 < steps; s0 += 4) {
+        step(std::integral_constant<int, 0>{}, s0);
+        if (s0 + 1 < steps) step(std::integral_constant<int, 1>{}, s0 + 1);
+        if (s0 + 2 < steps) step(std::integral_constant<int, 2>{}, s0 + 2);
+        if (s0 + 3 < steps) step(std::integral_constant<int, 3>{}, s0 + 3);
+    }
+}
+
 __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_rk_kernel(BatchArgs a) {
     __shared__ RkTables smt;
     __shared__ DmaSlots smslots;
@@ -2283,7 +2522,11 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         if (!pcheck(a, lane, cur, 0xFFFFFFFFu, 5)) return;
         int64_t lo, hi;
         pregion(a, cur, lo, hi);
+#if KCDC_RK_CHAINS == 4
+        const Rk4Geom g = rk4_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n);
+#else
         const RkGeom g = rk_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n);
+#endif
         const int64_t ct = cur.ct, ct_next = ct + kWave * g.L;
         const bool last_of_region = ct_next > hi;
         const bool budget_out = budget - kWave * g.L <= 0;
@@ -2296,9 +2539,16 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         const bool reserve = budget_out && !ends_nocand;
         uint64_t ht_raw = 0;
         if (switching) ht_raw = qht_add(a, lane, 1);  // the next stream's ticket
-        if (!issued) rk_dma_warm(g.ld, sl32, ct, g.L, lane);
-        const int64_t c0 = ct + lane * g.L, c0b = c0 + g.L / 2;
+        const int64_t c0 = ct + lane * g.L;
         uint32_t ht_lo = static_cast<uint32_t>(ht_raw), ht_hi = static_cast<uint32_t>(ht_raw >> 32);
+#if KCDC_RK_CHAINS == 4
+        const Rk4Lane ln = rk4_lane(g.L, lane);
+        if (!issued) rk4_dma_warm(g.ld, sl32, ct, g.L, 0, ln);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(ht_lo), "+v"(ht_hi)::"memory");  // the ticket, warm fill 0
+#else
+        if (!issued) rk_dma_warm(g.ld, sl32, ct, g.L, lane);
+        const int64_t c0b = c0 + g.L / 2;
         uint32_t ha = 0, la = 0, hb = 0, lb = 0;
         uint32_t pa[16], pb[16];
         // ---- W: warm fill -> both chains' 64-byte histories; line 1 (A line 0) goes out
@@ -2313,6 +2563,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             __builtin_amdgcn_sched_barrier(0);
             rk_warm(kx, dw, ha, la, hb, lb, pa, pb);
         }
+#endif
         uint32_t tk = 0;
         int64_t nbacklog = 0;
         if (switching) {
@@ -2322,46 +2573,81 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         }
         uint64_t pe_raw = 0;
         bool res_issued = false, next_issued = false, entry_issued = false;
+        // After the tile's last fill: the next tile's warm fill, or the next stream's entry.
+        auto refill_last = [&]() {
+            if (reserve && !res_issued) {  // this stream's ring entry, reserved late
+                pe_raw = qht_add(a, lane, 1ull << 32);
+                res_issued = true;
+            }
+            if (switching) {
+                pentry_dma(a, lane, tk, sl32);
+                entry_issued = true;
+            } else if (!last_of_region) {  // the next tile has its own geometry
+#if KCDC_RK_CHAINS == 4
+                const Rk4Geom gn = rk4_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n);
+                rk4_dma_warm(gn.ld, sl32, ct_next, gn.L, 0, rk4_lane(gn.L, lane));
+#else
+                const RkGeom gn = rk_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n);
+                rk_dma_warm(gn.ld, sl32, ct_next, gn.L, lane);
+#endif
+                next_issued = true;
+            }
+        };
+#if KCDC_RK_CHAINS == 4
+        int64_t fq[4] = {-1, -1, -1, -1};  // each chain's first candidate
+        auto refill = [&](int f) {
+            if (f == -2)
+                rk4_dma_warm(g.ld, sl32, ct, g.L, 1, ln);
+            else if (f < 4 * g.n - 1)
+                rk4_dma_line(g.ld, sl32, ct, g.L, f + 1, ln);
+            else
+                refill_last();
+        };
+        auto check = [&](uint32_t mm, int chain, int64_t c, uint32_t h0, uint32_t l0, const uint32_t (&in)[8],
+                         const uint32_t (&lv)[8]) {
+            if (mm == 0 && fq[chain] < 0 && c <= hi) {
+                const int64_t blo = lo - c, bhi = hi - c;
+                const uint32_t idx = rk_exact32(kx, h0, l0, in, lv, blo < 0 ? 0 : static_cast<int>(blo),
+                                                bhi > 31 ? 31 : static_cast<int>(bhi));
+                if (idx < 32u) fq[chain] = c + idx;
+            }
+        };
+        rk4_walk(kx, sl, lane, c0, g.L / 4, cur.off0, g.n, refill, check);
+        const int64_t found = fq[0] >= 0 ? fq[0] : fq[1] >= 0 ? fq[1] : fq[2] >= 0 ? fq[2] : fq[3];
+#else
         int64_t found_a = -1, found_b = -1;
         // After line fill f is read: issue what the slot takes next (fill f+1, or after the
         // last fill the next tile's warm fill / the next stream's queue entry).
         auto refill = [&](int f) {
-            if (f < 2 * g.K) {
+            if (f < 2 * g.K)
                 rk_dma_line(g.ld, sl32, ct, g.L, f + 1, lane);
-            } else {
-                if (reserve && !res_issued) {  // this stream's ring entry, reserved late
-                    pe_raw = qht_add(a, lane, 1ull << 32);
-                    res_issued = true;
-                }
-                if (switching) {
-                    pentry_dma(a, lane, tk, sl32);
-                    entry_issued = true;
-                } else if (!last_of_region) {  // the next tile has its own geometry
-                    const RkGeom gn = rk_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n);
-                    rk_dma_warm(gn.ld, sl32, ct_next, gn.L, lane);
-                    next_issued = true;
-                }
-            }
+            else
+                refill_last();
         };
         // Hit check of one chain's 64 bytes at coordinate c (state before: h0/l0): the
         // chain's first candidate in [lo, hi].
         auto check = [&](uint32_t mm, int chain, int64_t c, uint32_t h0, uint32_t l0, const uint32_t (&in)[16],
                          const uint32_t (&prv)[16]) {
-            int64_t& found = chain ? found_b : found_a;
-            if (mm == 0 && found < 0 && c <= hi) {
+            if (mm == 0 && (chain ? found_b : found_a) < 0 && c <= hi) {
                 const int64_t blo = lo - c, bhi = hi - c;
                 const uint32_t idx = rk_exact64(kx, h0, l0, in, prv, blo < 0 ? 0 : static_cast<int>(blo),
                                                 bhi > 63 ? 63 : static_cast<int>(bhi));
-                if (idx < 64u) found = c + idx;
+                if (idx < 64u) {
+                    if (chain)
+                        found_b = c + idx;
+                    else
+                        found_a = c + idx;
+                }
             }
         };
         rk_walk(kx, sl, lane, c0, c0b, cur.off0, g.K, ha, la, hb, lb, pa, pb, refill, check);
+        const int64_t found = found_a >= 0 ? found_a : found_b;
+#endif
         // ---- end of tile
         if (reserve && !res_issued) {
             pe_raw = qht_add(a, lane, 1ull << 32);
             res_issued = true;
         }
-        const int64_t found = found_a >= 0 ? found_a : found_b;
         const uint64_t hit = __ballot(found >= 0);
         bool region_changed = true;
         bool live;
