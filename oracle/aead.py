@@ -1,0 +1,98 @@
+"""ORACLE / TEST INFRASTRUCTURE ONLY -- never imported by the product path.
+
+Restatement of the published algorithms behind Kopia's CHACHA20-POLY1305-HMAC-SHA256
+content encryption (repo/encryption/chacha20_poly1305_hmac_sha256_encryptor.go,
+aead_helpers.go, encryption.go:82-95), whose arithmetic lives in golang.org/x/crypto
+(chacha20poly1305, not vendored here) and the Go standard library (crypto/hkdf,
+crypto/hmac, crypto/sha256):
+* deriveKey: HKDF-SHA256(masterKey, salt = purpose ("encryption"), info = "", 32 bytes)
+  (RFC 5869; Go's hkdf.Key(h, secret, salt, info, n) -- encryption.go:82-95);
+* per content: key = HMAC-SHA256(derived, iv), iv = the last 16 bytes of the content hash
+  (repo/content/content_manager_lock_free.go:178-182);
+* Seal: output = nonce(12) || ChaCha20-Poly1305(key, nonce, plaintext, aad = iv)
+  (RFC 8439 §2.8; aead_helpers.go: random nonce prefix).
+Pinned by the RFC 8439 / RFC 5869 example vectors (tests/test_aead_oracle.py).
+"""
+from __future__ import annotations
+
+import hashlib
+import hmac
+import struct
+
+import numpy as np
+
+
+def hkdf_sha256(ikm: bytes, salt: bytes, info: bytes, n: int) -> bytes:
+    prk = hmac.new(salt, ikm, hashlib.sha256).digest()
+    out, t, i = b"", b"", 1
+    while len(out) < n:
+        t = hmac.new(prk, t + info + bytes([i]), hashlib.sha256).digest()
+        out += t
+        i += 1
+    return out[:n]
+
+
+def derive_key(master_key: bytes, purpose: bytes = b"encryption", n: int = 32) -> bytes:
+    """encryption.go deriveKey (hkdf.Key(sha256.New, masterKey, purpose, "", n))."""
+    return hkdf_sha256(master_key, purpose, b"", n)
+
+
+def _rotl(x, n):
+    return ((x << n) | (x >> (32 - n))) & 0xFFFFFFFF
+
+
+def chacha20_block(key: bytes, counter: int, nonce: bytes) -> bytes:
+    """RFC 8439 §2.3."""
+    c = [0x61707865, 0x3320646E, 0x79622D32, 0x6B206574]
+    st = c + list(struct.unpack("<8I", key)) + [counter & 0xFFFFFFFF] + list(struct.unpack("<3I", nonce))
+    x = st[:]
+
+    def qr(a, b, cc, d):
+        x[a] = (x[a] + x[b]) & 0xFFFFFFFF; x[d] = _rotl(x[d] ^ x[a], 16)
+        x[cc] = (x[cc] + x[d]) & 0xFFFFFFFF; x[b] = _rotl(x[b] ^ x[cc], 12)
+        x[a] = (x[a] + x[b]) & 0xFFFFFFFF; x[d] = _rotl(x[d] ^ x[a], 8)
+        x[cc] = (x[cc] + x[d]) & 0xFFFFFFFF; x[b] = _rotl(x[b] ^ x[cc], 7)
+
+    for _ in range(10):
+        qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15)
+        qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14)
+    return struct.pack("<16I", *[(x[i] + st[i]) & 0xFFFFFFFF for i in range(16)])
+
+
+def chacha20_xor(key: bytes, counter: int, nonce: bytes, data: bytes) -> bytes:
+    """RFC 8439 §2.4 (numpy XOR of the keystream)."""
+    n = len(data)
+    ks = b"".join(chacha20_block(key, counter + j, nonce) for j in range((n + 63) // 64))
+    return (np.frombuffer(data, np.uint8) ^ np.frombuffer(ks[:n], np.uint8)).tobytes()
+
+
+def poly1305(key: bytes, msg: bytes) -> bytes:
+    """RFC 8439 §2.5."""
+    r = int.from_bytes(key[:16], "little") & 0x0FFFFFFC0FFFFFFC0FFFFFFC0FFFFFFF
+    s = int.from_bytes(key[16:], "little")
+    p = (1 << 130) - 5
+    acc = 0
+    for i in range(0, len(msg), 16):
+        blk = msg[i:i + 16]
+        acc = (acc + int.from_bytes(blk + b"\x01", "little")) * r % p
+    return ((acc + s) & ((1 << 128) - 1)).to_bytes(16, "little")
+
+
+def _pad16(b: bytes) -> bytes:
+    return b"" if len(b) % 16 == 0 else bytes(16 - len(b) % 16)
+
+
+def chacha20poly1305_seal(key: bytes, nonce: bytes, plaintext: bytes, aad: bytes) -> bytes:
+    """RFC 8439 §2.8: ciphertext || tag."""
+    otk = chacha20_block(key, 0, nonce)[:32]
+    ct = chacha20_xor(key, 1, nonce, plaintext)
+    mac = aad + _pad16(aad) + ct + _pad16(ct) + struct.pack("<QQ", len(aad), len(ct))
+    return ct + poly1305(otk, mac)
+
+
+def kopia_encrypt(derived: bytes, content_hash: bytes, nonce: bytes, plaintext: bytes) -> bytes:
+    """chacha20poly1305hmacSha256Encryptor.Encrypt with a given nonce (the reference draws
+    it from crypto/rand): nonce || Seal(key = HMAC-SHA256(derived, iv), aad = iv)."""
+    iv = content_hash[-16:]
+    key = hmac.new(derived, iv, hashlib.sha256).digest()
+    return nonce + chacha20poly1305_seal(key, nonce, plaintext, iv)
