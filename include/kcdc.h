@@ -32,6 +32,8 @@ extern "C" {
 #define KCDC_EINVAL (-22)
 #define KCDC_ENODEV (-19)    /* no usable gfx950 device */
 #define KCDC_EOVERFLOW (-75) /* caller-provided cut capacity too small */
+#define KCDC_EFBIG (-27)     /* chunk too long to encrypt (>= 1 GiB) */
+#define KCDC_EBADMSG (-74)   /* sealed chunk failed authentication */
 
 /* counts[i] value of every stream of a batch launch that could not complete on the
  * device (a wave gave up waiting in the work queue): the launch's cut lists are invalid.
@@ -215,6 +217,44 @@ int kcdc_hash_size(const char* hash_name);
 int kcdc_hash_chunks_device(const char* hash_name, const uint8_t* d_data, const uint64_t* d_offsets,
                             const uint64_t* d_lens, const uint32_t* d_order, uint32_t nchunks, const uint8_t* key,
                             uint32_t key_len, uint8_t* d_out, uint32_t out_stride, void* hip_stream);
+
+/* ------------------------------------------------------------- content encryption
+ * Kopia's CHACHA20-POLY1305-HMAC-SHA256 (repo/encryption/chacha20_poly1305_hmac_sha256_encryptor.go:
+ * Encrypt/Decrypt/Overhead, 24-80; aead_helpers.go:12-75) for many chunks per call:
+ *   key_i  = HMAC-SHA256(secret, iv_i)      iv_i = the last 16 bytes of chunk i's content ID
+ *            (getPackedContentIV, repo/content/content_manager_lock_free.go:178-182)
+ *   sealed = nonce_i(12) || ChaCha20-Poly1305(key_i, nonce_i, plaintext, aad = iv_i) (RFC 8439)
+ * secret: the repository's derived key, HKDF-SHA256(masterKey, "encryption", "", 32)
+ *   (deriveKey, repo/encryption/encryption.go:80-92), 1..64 bytes.
+ * kcdc_encryption_algorithms / kcdc_encryption_overhead (28): the registry (Register, encryption.go:65).
+ * kcdc_crypt_workspace_size(n): bytes of device scratch a call over n chunks needs (~9 KiB
+ *   per chunk: its key, one-time Poly1305 key and a table of powers of r).
+ * kcdc_encrypt_chunks_device: plaintext i = [d_offsets[i], +d_lens[i]) of d_data (any
+ *   alignment, < 1 GiB); d_nonces: 12 bytes per chunk (the reference draws them from
+ *   crypto/rand; the caller does here); the sealed chunk (d_lens[i] + 28 bytes) is written at
+ *   d_out + d_out_offsets[i] (a multiple of 4).  d_status[i]: 0, or KCDC_EFBIG (too long).
+ * kcdc_decrypt_chunks_device: sealed chunk i = [d_offsets[i], +d_sealed_lens[i]) of
+ *   d_sealed; its plaintext (d_sealed_lens[i] - 28 bytes) goes to d_out + d_out_offsets[i]
+ *   (a multiple of 4; up to 3 zero bytes of padding after it are written too).
+ *   d_status[i]: 0, KCDC_EBADMSG (authentication failed: aeadOpenPrefixedWithNonce's "unable to
+ *   decrypt content"; the plaintext slot holds unauthenticated bytes), KCDC_EINVAL (shorter than
+ *   28 bytes: "ciphertext too short") or KCDC_EFBIG.
+ * d_ivs: 16 bytes per chunk at d_ivs + i * iv_stride (e.g. the hash output of
+ * kcdc_hash_chunks_device + hash size - 16).  Asynchronous on hip_stream; d_work must stay
+ * allocated until the work finishes. */
+int kcdc_encryption_algorithms(const char** names, int cap);
+int kcdc_encryption_overhead(const char* algorithm);
+uint64_t kcdc_crypt_workspace_size(uint32_t nchunks);
+int kcdc_encrypt_chunks_device(const char* algorithm, const uint8_t* secret, uint32_t secret_len, const uint8_t* d_data,
+                               const uint64_t* d_offsets, const uint64_t* d_lens, uint32_t nchunks,
+                               const uint8_t* d_ivs, uint32_t iv_stride, const uint8_t* d_nonces, uint8_t* d_out,
+                               const uint64_t* d_out_offsets, int32_t* d_status, void* d_work, uint64_t work_bytes,
+                               void* hip_stream);
+int kcdc_decrypt_chunks_device(const char* algorithm, const uint8_t* secret, uint32_t secret_len,
+                               const uint8_t* d_sealed, const uint64_t* d_offsets, const uint64_t* d_sealed_lens,
+                               uint32_t nchunks, const uint8_t* d_ivs, uint32_t iv_stride, uint8_t* d_out,
+                               const uint64_t* d_out_offsets, int32_t* d_status, void* d_work, uint64_t work_bytes,
+                               void* hip_stream);
 
 /* ------------------------------------------------------------- testing
  * Hooks for the library's own tests (not part of the splitter surface).

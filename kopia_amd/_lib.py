@@ -21,6 +21,8 @@ KCDC_ENOMEM = -12
 KCDC_ENODEV = -19
 KCDC_EINVAL = -22
 KCDC_EOVERFLOW = -75
+KCDC_EFBIG = -27
+KCDC_EBADMSG = -74
 
 KIND_FIXED, KIND_BUZHASH, KIND_RABINKARP = 0, 1, 2
 COUNT_FAILED = (1 << 64) - 1  # KCDC_COUNT_FAILED: the batch launch failed on the device
@@ -73,6 +75,13 @@ _SIGS = {
     "kcdc_hash_size": (C.c_int, [C.c_char_p]),
     "kcdc_hash_chunks_device": (C.c_int, [C.c_char_p, _P, _P, _P, _P, C.c_uint32, C.c_char_p, C.c_uint32, _P,
                                           C.c_uint32, _P]),
+    "kcdc_encryption_algorithms": (C.c_int, [C.POINTER(C.c_char_p), C.c_int]),
+    "kcdc_encryption_overhead": (C.c_int, [C.c_char_p]),
+    "kcdc_crypt_workspace_size": (C.c_uint64, [C.c_uint32]),
+    "kcdc_encrypt_chunks_device": (C.c_int, [C.c_char_p, C.c_char_p, C.c_uint32, _P, _P, _P, C.c_uint32, _P,
+                                             C.c_uint32, _P, _P, _P, _P, _P, C.c_uint64, _P]),
+    "kcdc_decrypt_chunks_device": (C.c_int, [C.c_char_p, C.c_char_p, C.c_uint32, _P, _P, _P, C.c_uint32, _P,
+                                             C.c_uint32, _P, _P, _P, _P, C.c_uint64, _P]),
 }
 
 

@@ -59,10 +59,35 @@ def chacha20_block(key: bytes, counter: int, nonce: bytes) -> bytes:
     return struct.pack("<16I", *[(x[i] + st[i]) & 0xFFFFFFFF for i in range(16)])
 
 
+def _chacha20_blocks_np(key: bytes, counter: int, nonce: bytes, nblocks: int) -> bytes:
+    """The keystream of blocks counter .. counter + nblocks - 1 (RFC 8439 §2.3), every block
+    at once as numpy uint32 lanes -- the same rounds as chacha20_block."""
+    st = [np.full(nblocks, w, np.uint32) for w in (0x61707865, 0x3320646E, 0x79622D32, 0x6B206574)]
+    st += [np.full(nblocks, w, np.uint32) for w in struct.unpack("<8I", key)]
+    st += [(np.arange(nblocks, dtype=np.uint64) + counter).astype(np.uint32)]
+    st += [np.full(nblocks, w, np.uint32) for w in struct.unpack("<3I", nonce)]
+    x = [a.copy() for a in st]
+
+    def rotl(v, n):
+        return (v << np.uint32(n)) | (v >> np.uint32(32 - n))
+
+    def qr(a, b, c, d):
+        x[a] += x[b]; x[d] = rotl(x[d] ^ x[a], 16)
+        x[c] += x[d]; x[b] = rotl(x[b] ^ x[c], 12)
+        x[a] += x[b]; x[d] = rotl(x[d] ^ x[a], 8)
+        x[c] += x[d]; x[b] = rotl(x[b] ^ x[c], 7)
+
+    for _ in range(10):
+        qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15)
+        qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14)
+    out = np.stack([x[i] + st[i] for i in range(16)], axis=1).astype("<u4")
+    return out.tobytes()
+
+
 def chacha20_xor(key: bytes, counter: int, nonce: bytes, data: bytes) -> bytes:
     """RFC 8439 §2.4 (numpy XOR of the keystream)."""
     n = len(data)
-    ks = b"".join(chacha20_block(key, counter + j, nonce) for j in range((n + 63) // 64))
+    ks = _chacha20_blocks_np(key, counter, nonce, (n + 63) // 64)
     return (np.frombuffer(data, np.uint8) ^ np.frombuffer(ks[:n], np.uint8)).tobytes()
 
 

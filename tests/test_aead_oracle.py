@@ -37,3 +37,21 @@ def test_hkdf():
     v = V["hkdf"]
     got = aead.hkdf_sha256(bytes.fromhex(v["ikm"]), bytes.fromhex(v["salt"]), bytes.fromhex(v["info"]), v["L"])
     assert got.hex() == v["okm"]
+
+
+def test_vectorized_keystream_matches_blocks():
+    key, nonce = bytes(range(32)), bytes(range(12))
+    ks = aead._chacha20_blocks_np(key, 7, nonce, 5)
+    assert ks == b"".join(aead.chacha20_block(key, 7 + j, nonce) for j in range(5))
+
+
+def test_host_mirror_and_registry():
+    """kopia_amd.encryption's host-side key derivation equals the oracle's HKDF, and the
+    library's registry and overhead match chacha20_poly1305_hmac_sha256_encryptor.go:16,67."""
+    from kopia_amd import encryption as ke
+    m = bytes(range(32))
+    assert ke.derive_key(m) == aead.derive_key(m)
+    assert ke.SupportedAlgorithms() == ["CHACHA20-POLY1305-HMAC-SHA256"]
+    assert ke.overhead("CHACHA20-POLY1305-HMAC-SHA256") == 28
+    offs, total = ke.sealed_layout([0, 1, 5, 100])
+    assert offs.tolist() == [0, 28, 60, 96] and total == 224

@@ -1,0 +1,180 @@
+"""GPU: CHACHA20-POLY1305-HMAC-SHA256 content encryption of many chunks
+(kcdc_encrypt/decrypt_chunks_device) bit-exact against the oracle (oracle/aead.py, pinned by
+RFC 8439 / RFC 5869 vectors in tests/test_aead_oracle.py): random lengths across the 16-byte,
+64-byte and 4 KiB unit boundaries, misaligned plaintext offsets, empty chunks, the chunks the
+splitter cuts and hashes on config-2 streams (IV = the content hash), round trips, and the
+authentication-failure / short-input / error contract."""
+import numpy as np
+import pytest
+
+from kopia_amd import _lib, batch
+from kopia_amd import encryption as ke
+from kopia_amd import hashing as kh
+from oracle import aead, coracle
+
+pytestmark = pytest.mark.gpu
+SEED = 0x6B6F706961
+ALG = ke.ChaCha20Poly1305
+MASTER = bytes(range(100, 132))
+
+
+def _seal(enc, host, offs, lens, ivs, nonces, dev):
+    import torch
+    d = torch.from_numpy(host).to(dev)
+    d_ivs = torch.from_numpy(np.frombuffer(b"".join(ivs), np.uint8).copy()).to(dev)
+    oo, total = ke.sealed_layout(lens)
+    out = torch.full((max(total, 1),), 0xAB, dtype=torch.uint8, device=dev)
+    st = enc.encrypt_chunks_device(d.data_ptr(), offs, lens, d_ivs, 16, out, oo, dev, nonces=nonces)
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), oo, st.cpu().numpy()
+
+
+def _open(enc, sealed, soffs, slens, ivs, dev):
+    import torch
+    d = torch.from_numpy(np.ascontiguousarray(sealed)).to(dev)
+    d_ivs = torch.from_numpy(np.frombuffer(b"".join(ivs), np.uint8).copy()).to(dev)
+    po, total = ke.plain_layout(slens)
+    out = torch.zeros(total, dtype=torch.uint8, device=dev)
+    st = enc.decrypt_chunks_device(d.data_ptr(), soffs, slens, d_ivs, 16, out, po, dev)
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), po, st.cpu().numpy()
+
+
+def test_rfc_shaped_single(gpu):
+    """One chunk, fixed secret / IV / nonce, equals the oracle's Encrypt."""
+    enc = ke.Encryptor(ALG, MASTER)
+    pt = b"Ladies and Gentlemen of the class of '99: If I could offer you only one tip for the future, sunscreen would be it."
+    host = np.frombuffer(pt, np.uint8).copy()
+    iv = bytes(range(16))
+    nonce = bytes(range(40, 52))
+    out, oo, st = _seal(enc, host, [0], [len(pt)], [iv], nonce, gpu)
+    assert st.tolist() == [0]
+    want = aead.kopia_encrypt(aead.derive_key(MASTER), iv, nonce, pt)
+    assert out[:len(want)].tobytes() == want
+
+
+def test_random_chunks(gpu):
+    rng = np.random.default_rng(7)
+    host = coracle.gen_stream(SEED, 3, 3 << 20)
+    lens = list(rng.integers(0, 70000, 300))
+    lens[:24] = [0, 1, 3, 4, 15, 16, 17, 63, 64, 65, 127, 1000, 4095, 4096, 4097, 8191, 8192, 8193,
+                 12287, 16400, 65536, 65536 + 3, 1 << 20, (1 << 20) + 13]
+    lens = np.array(lens, dtype=np.int64)
+    offs = np.array([int(rng.integers(0, host.size - int(L))) for L in lens], dtype=np.int64)
+    ivs = [bytes(rng.integers(0, 256, 16, dtype=np.uint8)) for _ in lens]
+    nonces = bytes(rng.integers(0, 256, 12 * len(lens), dtype=np.uint8))
+    enc = ke.Encryptor(ALG, MASTER)
+    secret = aead.derive_key(MASTER)
+    out, oo, st = _seal(enc, host, offs, lens, ivs, nonces, gpu)
+    assert not st.any()
+    bad = []
+    for i in range(len(lens)):
+        want = aead.kopia_encrypt(secret, ivs[i], nonces[12 * i:12 * i + 12], host[offs[i]:offs[i] + lens[i]].tobytes())
+        if out[oo[i]:oo[i] + len(want)].tobytes() != want:
+            bad.append((i, int(lens[i])))
+    assert not bad, bad[:10]
+    # round trip through the device decryptor, sealed chunks at odd offsets
+    slens = lens + 28
+    soffs = np.concatenate(([5], 5 + np.cumsum(slens)[:-1] + np.arange(1, len(slens)))).astype(np.int64)
+    sealed = np.zeros(int(soffs[-1] + slens[-1] + 8), np.uint8)
+    for i in range(len(lens)):
+        sealed[soffs[i]:soffs[i] + slens[i]] = out[oo[i]:oo[i] + slens[i]]
+    plain, po, st2 = _open(enc, sealed, soffs, slens, ivs, gpu)
+    assert not st2.any()
+    for i in range(len(lens)):
+        assert plain[po[i]:po[i] + lens[i]].tobytes() == host[offs[i]:offs[i] + lens[i]].tobytes(), i
+
+
+def test_open_rejects(gpu):
+    """A flipped ciphertext, tag or nonce byte, a wrong IV, and a too-short input fail
+    (aeadOpenPrefixedWithNonce: "unable to decrypt content" / "ciphertext too short"); the
+    untouched chunks of the same call still open."""
+    rng = np.random.default_rng(11)
+    n, L = 8, 5000
+    host = rng.integers(0, 256, n * L, dtype=np.uint8)
+    ivs = [bytes([i]) * 16 for i in range(n)]
+    enc = ke.Encryptor(ALG, MASTER)
+    out, oo, st = _seal(enc, host, np.arange(n) * L, [L] * n, ivs, None, gpu)
+    assert not st.any()
+    slens = np.full(n, L + 28, np.int64)
+    sealed = out.copy()
+    sealed[oo[1] + 100] ^= 1          # ciphertext
+    sealed[oo[2] + 12 + L + 5] ^= 0x80  # tag
+    sealed[oo[3] + 2] ^= 4             # nonce
+    ivs2 = list(ivs)
+    ivs2[4] = bytes(16)                # wrong content ID
+    slens[5] = 27                      # too short
+    plain, po, st2 = _open(enc, sealed, oo, slens, ivs2, gpu)
+    assert st2.tolist() == [0, _lib.KCDC_EBADMSG, _lib.KCDC_EBADMSG, _lib.KCDC_EBADMSG, _lib.KCDC_EBADMSG,
+                            _lib.KCDC_EINVAL, 0, 0]
+    for i in (0, 6, 7):
+        assert plain[po[i]:po[i] + L].tobytes() == host[i * L:(i + 1) * L].tobytes()
+
+
+def test_nonces_differ_by_default(gpu):
+    """Without caller nonces, two seals of the same chunk differ (random nonce prefix) and
+    both open."""
+    enc = ke.Encryptor(ALG, MASTER)
+    host = np.arange(3000, dtype=np.uint8)
+    a, oo, _ = _seal(enc, host, [0], [3000], [bytes(16)], None, gpu)
+    b, _, _ = _seal(enc, host, [0], [3000], [bytes(16)], None, gpu)
+    assert a[:12].tobytes() != b[:12].tobytes()
+    for s in (a, b):
+        plain, po, st = _open(enc, s[:3028], [0], [3028], [bytes(16)], gpu)
+        assert st.tolist() == [0] and plain[:3000].tobytes() == host.tobytes()
+
+
+def test_config2_pipeline(gpu):
+    """split -> hash (BLAKE2B-256-128, content ID) -> encrypt with IV = content ID, all on the
+    device, on 64 x 4 MiB config-2 streams; every sealed chunk equals the oracle's Encrypt of
+    the same bytes with the same nonce, and the device decryptor round-trips the batch."""
+    import torch
+    name, ns, L = "DYNAMIC-4M-BUZHASH", 64, 4 << 20
+    dev = gpu
+    data = torch.empty(ns * L, dtype=torch.uint8, device=dev)
+    batch.fill_prng(data, L, ns, L, SEED, 0)
+    b = batch.make_device_batch(name, [data.data_ptr() + i * L for i in range(ns)], [L] * ns, dev)
+    batch.split_batch_device(name, b)
+    offs, lens = kh.chunk_table([i * L for i in range(ns)], batch.read_cuts(b))
+    hkey = bytes(range(32))
+    ids = kh.hash_chunks_device(kh.DefaultAlgorithm, data.data_ptr(), offs, lens, hkey, dev)
+    ids = ids.contiguous()
+    n = len(offs)
+    nonces = bytes(np.random.default_rng(3).integers(0, 256, 12 * n, dtype=np.uint8))
+    enc = ke.Encryptor(ALG, MASTER)
+    oo, total = ke.sealed_layout(lens)
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    st = enc.encrypt_chunks_device(data.data_ptr(), offs, lens, ids, 16, out, oo, dev, nonces=nonces)
+    torch.cuda.synchronize()
+    assert not st.cpu().numpy().any()
+    host, got, idh = data.cpu().numpy(), out.cpu().numpy(), ids.cpu().numpy()
+    secret = aead.derive_key(MASTER)
+    for i in range(0, n, max(1, n // 24)):  # the oracle's ChaCha20 runs ~25 MB/s: a spread sample
+        want = aead.kopia_encrypt(secret, idh[i].tobytes(), nonces[12 * i:12 * i + 12],
+                                  host[offs[i]:offs[i] + lens[i]].tobytes())
+        assert got[oo[i]:oo[i] + lens[i] + 28].tobytes() == want, i
+    plain = torch.zeros(ke.plain_layout(lens + 28)[1], dtype=torch.uint8, device=dev)
+    po, _ = ke.plain_layout(lens + 28)
+    st2 = enc.decrypt_chunks_device(out.data_ptr(), oo, lens + 28, ids, 16, plain, po, dev)
+    torch.cuda.synchronize()
+    assert not st2.cpu().numpy().any()
+    p = plain.cpu().numpy()
+    assert all(p[po[i]:po[i] + lens[i]].tobytes() == host[offs[i]:offs[i] + lens[i]].tobytes() for i in range(n))
+
+
+def test_errors(gpu):
+    import torch
+    enc = ke.Encryptor(ALG, MASTER)
+    d = torch.zeros(64, dtype=torch.uint8, device=gpu)
+    with pytest.raises(_lib.KcdcError):
+        ke.Encryptor("AES128-GCM", MASTER)
+    L = _lib.lib()
+    rc = L.kcdc_encrypt_chunks_device(ALG.encode(), enc.secret, 65, d.data_ptr(), d.data_ptr(), d.data_ptr(), 1,
+                                      d.data_ptr(), 16, d.data_ptr(), d.data_ptr(), d.data_ptr(), d.data_ptr(),
+                                      d.data_ptr(), 64, None)
+    assert rc == _lib.KCDC_EINVAL  # secret > 64 bytes
+    rc = L.kcdc_encrypt_chunks_device(ALG.encode(), enc.secret, 32, d.data_ptr(), d.data_ptr(), d.data_ptr(), 1,
+                                      d.data_ptr(), 16, d.data_ptr(), d.data_ptr(), d.data_ptr(), d.data_ptr(),
+                                      d.data_ptr(), 64, None)
+    assert rc == _lib.KCDC_EINVAL  # workspace too small
+    assert ke.overhead(ALG) == 28
