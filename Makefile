@@ -56,6 +56,6 @@ variants:
 	@for v in $(VARIANTS); do \
 	  n=$${v%%:*}; f=$$(echo $${v#*:} | tr ',' ' '); \
 	  echo "variant $$n: $$f"; \
-	  $(HIPCC) $(HIPFLAGS) $$f -shared -o build/variants/libkcdc_$$n.so $(CSRC)/kcdc_kernels.hip -x hip $(CSRC)/kcdc_api.cpp $(CSRC)/kcdc_tables.cpp $(CSRC)/kcdc_registry.cpp || exit 1; \
+	  $(HIPCC) $(HIPFLAGS) $$f -shared -o build/variants/libkcdc_$$n.so $(CSRC)/kcdc_kernels.hip $(CSRC)/kcdc_hash.hip $(CSRC)/kcdc_crypt.hip -x hip $(CSRC)/kcdc_api.cpp $(CSRC)/kcdc_tables.cpp $(CSRC)/kcdc_registry.cpp || exit 1; \
 	done
 .PHONY: variants

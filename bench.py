@@ -329,6 +329,8 @@ def bench_batch(args, comm: Comm):
 
     if args.hash and rank == 0:
         out["hash"] = bench_hash(args, data, ns, L, cuts, dev)
+    if args.encrypt and rank == 0:
+        out["encrypt"] = bench_encrypt(args, data, ns, L, cuts, dev)
 
     if rank == 0 and world == 1 and not args.no_host_inclusive:
         # host-inclusive: pageable host buffers -> H2D -> kernel -> D2H (kcdc_split_batch_host)
@@ -400,6 +402,67 @@ def bench_hash(args, data, ns: int, L: int, cuts: list, dev) -> dict:
             "inflight_gib_s": round(R * total / GiB / (msR * 1e-3), 2),
             "sample_parity_mismatches": int(bad), "sample_chunks": len(pick),
             "cpu_hashlib_1thread_gib_s": round(cpu, 3)}
+
+
+def bench_encrypt(args, data, ns: int, L: int, cuts: list, dev) -> dict:
+    """§8f #4: CHACHA20-POLY1305-HMAC-SHA256 of every chunk the split produced, keyed by its
+    content ID (BLAKE2B-256-128 on the device), as content_manager_lock_free.go:178-182 does.
+    Times seal (and open) of the whole batch: 4 launches each (key/power table, unit scan,
+    byte pass, tag).  Algorithmic HBM bytes: every plaintext byte read once and every sealed
+    byte written once (open: the reverse).  Parity: a spread sample against oracle/aead.py."""
+    import torch
+    from kopia_amd import encryption as ke
+    from kopia_amd import hashing as kh
+    from oracle import aead
+    offs, lens = kh.chunk_table([i * L for i in range(ns)], cuts)
+    n, total = len(offs), int(lens.sum())
+    ids = kh.hash_chunks_device(kh.DefaultAlgorithm, data.data_ptr(), offs, lens, bytes(range(32)), dev).contiguous()
+    master = bytes(range(64, 96))
+    enc = ke.Encryptor(ke.ChaCha20Poly1305, master)
+    nonces = bytes(np.random.default_rng(5).integers(0, 256, 12 * n, dtype=np.uint8))
+    oo, sealed_total = ke.sealed_layout(lens)
+    out = torch.empty(sealed_total, dtype=torch.uint8, device=dev)
+    po, plain_total = ke.plain_layout(lens + 28)
+    plain = torch.empty(plain_total, dtype=torch.uint8, device=dev)
+    reps = 5
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            st = fn()
+        e1.record()
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) / reps, st
+
+    seal_ms, st = timed(lambda: enc.encrypt_chunks_device(data.data_ptr(), offs, lens, ids, 16, out, oo, dev,
+                                                          nonces=nonces))
+    assert not st.cpu().numpy().any()
+    open_ms, st2 = timed(lambda: enc.decrypt_chunks_device(out.data_ptr(), oo, lens + 28, ids, 16, plain, po, dev))
+    assert not st2.cpu().numpy().any()
+    secret, idh = aead.derive_key(master), ids.cpu().numpy()
+    pick = list(range(0, n, max(1, n // 8)))
+    bad = 0
+    t0 = time.perf_counter()
+    for i in pick:
+        chunk = data[int(offs[i]):int(offs[i] + lens[i])].cpu().numpy().tobytes()
+        want = aead.kopia_encrypt(secret, idh[i].tobytes(), nonces[12 * i:12 * i + 12], chunk)
+        bad += out[int(oo[i]):int(oo[i]) + len(want)].cpu().numpy().tobytes() != want
+        bad += plain[int(po[i]):int(po[i] + lens[i])].cpu().numpy().tobytes() != chunk
+    oracle_s = time.perf_counter() - t0
+    alg = 2 * total + 28 * n
+    return {"algo": ke.ChaCha20Poly1305, "chunks": n, "plaintext_bytes": total,
+            "seal_ms": round(seal_ms, 3), "seal_gib_s": round(total / GiB / (seal_ms * 1e-3), 1),
+            "open_ms": round(open_ms, 3), "open_gib_s": round(total / GiB / (open_ms * 1e-3), 1),
+            "roofline": {"bound": "hbm", "achieved": round(alg / (seal_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(alg / (seal_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3),
+                         "algorithmic_bytes": alg, "timed": "all 4 seal launches (rocprof splits them)"},
+            "sample_parity_mismatches": int(bad), "sample_chunks": len(pick),
+            "cpu_oracle_gib_s": round(sum(int(lens[i]) for i in pick) * 2 / GiB / oracle_s, 4),
+            "cpu_oracle_note": "numpy/pure-Python RFC 8439 restatement (seal + compare), not an optimized "
+                               "CPU implementation: no crypto library in this image"}
 
 
 def bench_long(args, comm: Comm):
@@ -578,6 +641,8 @@ def parse(argv):
     ap.add_argument("--all-names", action="store_true", help="config 5: also time every registered name")
     ap.add_argument("--hash", default=None, help="configs 2/4: also hash every chunk on the device with this "
                     "content hash (e.g. BLAKE2B-256-128)")
+    ap.add_argument("--encrypt", action="store_true",
+                    help="also seal/open every chunk with CHACHA20-POLY1305-HMAC-SHA256 (§8f #4)")
     ap.add_argument("--hash-inflight", type=int, default=24, help="--hash: chunk tables per launch, throughput figure")
     args = ap.parse_args(argv)
     if args.config == 4:

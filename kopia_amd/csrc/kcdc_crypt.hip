@@ -34,6 +34,9 @@ constexpr uint32_t kUnit = 4096;                      // bytes per wave step
 constexpr uint32_t kTabT = 0, kTabA = 256, kTabB = 320, kTabC = 384, kTabN = 448;  // r^a, r^256b, r^16384c, r^(2^20)d
 constexpr uint64_t kMaxLen = (1ull << 30) - 64;       // exponents stay below 2^26
 constexpr uint32_t kM26 = 0x3FFFFFFu;
+#ifndef KCDC_CRYPT_ABL
+#define KCDC_CRYPT_ABL 0  // ablations for measurement (bit 0: no ChaCha20, bit 1: no Poly1305); 0 in the product
+#endif
 
 struct Fe {  // element of GF(2^130 - 5), radix 2^26, limbs not fully reduced
     uint32_t v[5];
@@ -166,14 +169,6 @@ __device__ __forceinline__ Fe fe_mul(const Fe& a, const Fe& b) {
     r.v[4] = static_cast<uint32_t>(d4) & kM26;
     r.v[0] = static_cast<uint32_t>(t) & kM26;
     r.v[1] += static_cast<uint32_t>(t >> 26);
-    return r;
-}
-
-__device__ __forceinline__ uint32_t fe_limb(const Fe& a, uint32_t i) {  // register select, no scratch
-    uint32_t r = a.v[0];
-#pragma unroll
-    for (uint32_t j = 1; j < 5; j++)
-        if (i == j) r = a.v[j];
     return r;
 }
 
@@ -426,13 +421,46 @@ __device__ __forceinline__ uint32_t swz(uint32_t i) {
     return ((s ^ ((s >> 4) & 3u)) << 2) | (i & 3u);
 }
 
+// LDS-DMA (buffer_load_dwordx4 ... lds): 64 lanes x 16 bytes -> LDS bytes [m0, m0 + 1 KiB),
+// lane d at m0 + 16 d.  Inline asm, so the compiler's waitcnt pass never waits on it; every
+// read of a slot follows an explicit s_waitcnt.  nt: each source byte is read once.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return __builtin_amdgcn_readfirstlane(
+        static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr_t)(const_cast<void*>(p)))));
+}
+__device__ __forceinline__ void dma16(const u32x4& d, uint32_t m0, uint32_t voff) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds" ::"s"(m0), "v"(voff),
+                 "s"(d)
+                 : "memory");
+}
+
+// Slot layout (4 KiB + one 16-byte tail granule per unit): the unit's aligned 16-byte
+// granule g sits at position pos(g) = g with its low 2 bits XORed by (g >> 4) & 3, so lane
+// l's reads of granules 4l..4l+4 and the coalesced word view (swz) are both conflict free.
+constexpr uint32_t kSlotBytes = kUnit + 32;
+
 // The byte pass: persistent waves, each over a contiguous range of (chunk, unit) pairs.
+// Unit u+1 is fetched into the wave's other LDS slot by DMA while unit u's keystream is
+// computed, so the ~1,000 VALU of ChaCha20 per lane hide the HBM latency.
+// Poly1305 over a run of consecutive full units of one chunk stays per lane: lane l holds
+// blocks 4l..4l+3 of every unit, 253 blocks apart from one unit to the next, so it runs
+// Horner as acc = acc r^253 + m0, then acc r + m1..m3.  The run is folded into the chunk
+// sum (lane l scaled by r^(4(63-l)), reduced across the wave, scaled by r^Q) only when the
+// chunk or the wave's range ends, or at the chunk's partial last unit.
 template <bool kOpen>
-__global__ __launch_bounds__(256) void crypt_units_kernel(CryptArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[4][1024];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    uint32_t* L = lds[wv];
-    const uint32_t total = a.units[a.n];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void crypt_units_kernel(
+    CryptArgs a, const ChunkKey* __restrict__ keys, const uint32_t* __restrict__ units,
+    const uint64_t* __restrict__ in_offs, const uint64_t* __restrict__ out_offs, const Fe* __restrict__ tabs,
+    uint8_t* __restrict__ out, unsigned long long* __restrict__ acc) {
+    // The arrays come as separate __restrict__ arguments: the output stores then cannot
+    // clobber them, so their wave-uniform reads are scalar loads.  As vector loads every one
+    // carried a vmcnt wait that drained the in-flight prefetch and the previous stores.
+    __shared__ __attribute__((aligned(16))) uint8_t lds[4][2][kSlotBytes];
+    // wave index made visibly uniform: the unit walk, the chunk record and its key stay in SGPRs
+    const uint32_t lane = threadIdx.x & 63u, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t total = units[a.n];
     const uint64_t W = static_cast<uint64_t>(gridDim.x) * 4u, w = static_cast<uint64_t>(blockIdx.x) * 4u + wv;
     uint32_t u = static_cast<uint32_t>(total * w / W);
     const uint32_t u1 = static_cast<uint32_t>(total * (w + 1) / W);
@@ -440,85 +468,198 @@ __global__ __launch_bounds__(256) void crypt_units_kernel(CryptArgs a) {
     uint32_t lo = 0, hi = a.n;  // units[lo] <= u < units[hi]
     while (hi - lo > 1u) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (a.units[mid] <= u) lo = mid;
+        if (units[mid] <= u) lo = mid;
         else hi = mid;
     }
+    const uint32_t slot_addr[2] = {lds_addr(lds[wv][0]), lds_addr(lds[wv][1])};
+    const uint32_t hdr_in = kOpen ? 12u : 0u, hdr_out = kOpen ? 0u : 12u;
+
+    // DMA of unit uq of chunk cq into slot sl; returns the unit's start offset in its first granule.
+    auto issue = [&](uint32_t cq, uint32_t uq, uint32_t sl) -> uint32_t {
+        const ChunkKey& k = keys[cq];
+        const uint64_t lq = static_cast<uint64_t>(k.len_lo) | (static_cast<uint64_t>(k.len_hi) << 32);
+        const uintptr_t chunk = reinterpret_cast<uintptr_t>(a.in + in_offs[cq] + hdr_in);
+        const uintptr_t src = chunk + static_cast<uint64_t>(uq) * kUnit;
+        const uintptr_t b16 = src & ~uintptr_t(15);
+        uint64_t nrec = ((chunk + lq + 15u) & ~uintptr_t(15)) - b16;  // granules holding chunk bytes
+        if (nrec > kUnit + 16u) nrec = kUnit + 16u;
+        u32x4 d;
+        d.x = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(b16));
+        d.y = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(b16 >> 32) & 0xFFFFu);  // stride 0
+        d.z = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nrec));
+        d.w = 0x00020000u;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) {
+            const uint32_t p = 64u * i + lane;
+            dma16(d, slot_addr[sl] + 1024u * i, 16u * ((p & ~3u) | ((p & 3u) ^ ((p >> 4) & 3u))));
+        }
+        if (lane == 0) dma16(d, slot_addr[sl] + kUnit, 16u * 256u);  // tail granule -> position 256
+        return static_cast<uint32_t>(src & 15u);
+    };
+
     uint32_t c = lo;
-    Fe accum = fe_zero();
-    auto flush = [&](uint32_t cc) {
-        if (lane < 5u) atomicAdd(a.acc + 5ull * cc + lane, static_cast<unsigned long long>(fe_limb(accum, lane)));
+    uint64_t nct = 0;        // 16-byte blocks of chunk c
+    Fe accum = fe_zero();    // chunk c's share from this wave, scaled to the message end
+    Fe run = fe_zero();      // this lane's Horner value over the current run of full units
+    uint32_t run_end = ~0u;  // unit index (within chunk c) of the run's last unit; ~0u: no run
+
+    auto wave_sum = [&](Fe h) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            Fe o;
+#pragma unroll
+            for (int j = 0; j < 5; j++) o.v[j] = __shfl_xor(h.v[j], off, 64);
+            h = fe_carry(fe_add(h, o));
+        }
+        return h;
+    };
+    auto fold_run = [&]() {
+        if (run_end == ~0u) return;
+        const Fe* tab = tabs + static_cast<uint64_t>(c) * kTabN;
+        const Fe h = wave_sum(fe_mul(run, tab[kTabT + 4u * (63u - lane)]));
+        const uint32_t q = static_cast<uint32_t>(nct + 1u - (static_cast<uint64_t>(run_end) * 256u + 255u));
+        accum = fe_carry(fe_add(accum, fe_mul(h, fe_pow_tab(tab, q))));
+        run = fe_zero();
+        run_end = ~0u;
+    };
+    auto flush = [&]() {
+        unsigned long long* dst = acc + 5ull * c;
+#pragma unroll
+        for (uint32_t j = 0; j < 5; j++)
+            if (lane == j) atomicAdd(dst + j, static_cast<unsigned long long>(accum.v[j]));
         accum = fe_zero();
     };
-    for (; u < u1; u++) {
-        if (a.units[c + 1] <= u) {
-            flush(c);
+
+    uint32_t sl = 0;
+    uint32_t mis = issue(c, u - units[c], 0);
+    uint32_t cn = c;  // chunk of unit u + 1
+    bool prev_full = false;  // the previous iteration was a full unit (16 stores, no other vector memory op)
+    for (; u < u1; u++, sl ^= 1u) {
+        bool exact = prev_full;
+        if (units[c + 1] <= u) {
+            fold_run();
+            flush();
+            exact = false;
             do c++;
-            while (a.units[c + 1] <= u);
+            while (units[c + 1] <= u);
         }
-        const ChunkKey& ck = a.keys[c];
+        // 1. prefetch unit u + 1 into the other slot (its previous unit's reads are done)
+        const bool more = u + 1u < u1;
+        uint32_t mis_next = 0;
+        if (more) {
+            if (cn < c) cn = c;
+            while (units[cn + 1] <= u + 1u) cn++;
+            mis_next = issue(cn, u + 1u - units[cn], sl ^ 1u);
+        }
+        const ChunkKey& ck = keys[c];
         const uint64_t len = static_cast<uint64_t>(ck.len_lo) | (static_cast<uint64_t>(ck.len_hi) << 32);
-        const uint32_t uu = u - a.units[c];
+        nct = (len + 15u) >> 4;
+        const uint32_t uu = u - units[c];
         const uint64_t ub = static_cast<uint64_t>(uu) * kUnit;
         const uint32_t rem = static_cast<uint32_t>(len - ub < kUnit ? len - ub : kUnit);
-        const uint8_t* src = a.in + a.in_offs[c] + (kOpen ? 12u : 0u) + ub;
-        uint32_t* dst = reinterpret_cast<uint32_t*>(a.out + a.out_offs[c] + (kOpen ? 0u : 12u) + ub);
+        const bool full = rem == kUnit;
+        uint32_t* dst = reinterpret_cast<uint32_t*>(out + out_offs[c] + hdr_out + ub);
 
-        // 1. coalesced load (any byte alignment, never past the unit's last aligned word) -> LDS
-        {
-            const uintptr_t sa = reinterpret_cast<uintptr_t>(src);
-            const uint32_t mis = static_cast<uint32_t>(sa & 3u);
-            const __attribute__((address_space(1))) uint32_t* ws =
-                reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(sa - mis);
-            const uint32_t lw = (rem + mis - 1u) >> 2;
-            uint32_t x[16], y[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const uint32_t i = 64u * k + lane;
-                x[k] = ws[min(i, lw)];
-                y[k] = ws[min(i + 1u, lw)];
-            }
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const uint32_t i = 64u * k + lane;
-                const uint32_t v = mis ? __builtin_amdgcn_alignbit(y[k], x[k], 8u * mis) : x[k];
-                L[swz(i)] = v & keep_mask(static_cast<int64_t>(rem) - 4 * static_cast<int64_t>(i));
-            }
-        }
-        wave_lds_sync();
-
-        // 2. lane-own 64 bytes: keystream XOR
+        // 2. this lane's keystream block (counter 1 + byte offset / 64), under the DMAs
         uint32_t ks[16];
-        uint32_t kk[8], nc[3];
+        {
+            uint32_t kk[8], nc[3];
 #pragma unroll
-        for (int j = 0; j < 8; j++) kk[j] = ck.key[j];
+            for (int j = 0; j < 8; j++) kk[j] = ck.key[j];
 #pragma unroll
-        for (int j = 0; j < 3; j++) nc[j] = ck.nonce[j];
-        chacha20_block(kk, 1u + uu * 64u + lane, nc, ks);
+            for (int j = 0; j < 3; j++) nc[j] = ck.nonce[j];
+#if KCDC_CRYPT_ABL & 1  // measurement only: keystream replaced by a cheap stand-in
+#pragma unroll
+            for (int j = 0; j < 16; j++) ks[j] = (1u + uu * 64u + lane) * (j + 1u) ^ kk[j & 7];
+#else
+            chacha20_block(kk, 1u + uu * 64u + lane, nc, ks);
+#endif
+        }
+        // 3. wait for this unit's DMA (only the prefetch may stay in flight), read this lane's
+        //    bytes [64 lane + mis, +64) from granules 4 lane .. 4 lane + 4
+        //    In steady state exactly the previous unit's 16 stores and the 5 prefetch DMAs
+        //    were issued after this unit's DMA; otherwise wait for everything but the prefetch.
+        if (exact) {
+            if (more) asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        } else {
+            if (more) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        uint8_t* S = lds[wv][sl];
         const uint32_t sw = (lane >> 2) & 3u;
-        uint32_t d[16], res[16];
+        uint32_t q[20];
 #pragma unroll
         for (int t = 0; t < 4; t++) {
-            const uint4 q = *reinterpret_cast<const uint4*>(L + ((4u * lane + (t ^ sw)) << 2));
-            d[4 * t] = q.x;
-            d[4 * t + 1] = q.y;
-            d[4 * t + 2] = q.z;
-            d[4 * t + 3] = q.w;
+            const uint4 g = *reinterpret_cast<const uint4*>(S + 16u * (4u * lane + (t ^ sw)));
+            q[4 * t] = g.x;
+            q[4 * t + 1] = g.y;
+            q[4 * t + 2] = g.z;
+            q[4 * t + 3] = g.w;
+        }
+        {
+            const uint32_t l1 = lane + 1u;
+            const uint4 g = *reinterpret_cast<const uint4*>(S + 16u * (4u * l1 + ((l1 >> 2) & 3u)));
+            q[16] = g.x;
+            q[17] = g.y;
+            q[18] = g.z;
+            q[19] = g.w;
+        }
+        uint32_t d[16], res[16];
+        {
+            const uint32_t sh = 8u * (mis & 3u);
+            switch (mis >> 2) {  // wave-uniform word offset
+#define KCDC_FUNNEL(W0)                                                                         \
+    case W0:                                                                                    \
+        _Pragma("unroll") for (int j = 0; j < 16; j++) d[j] =                                   \
+            __builtin_amdgcn_alignbit(q[j + W0 + 1 < 20 ? j + W0 + 1 : 19], q[j + W0], sh); \
+        break;
+                KCDC_FUNNEL(0)
+                KCDC_FUNNEL(1)
+                KCDC_FUNNEL(2)
+                default:
+                    KCDC_FUNNEL(3)
+#undef KCDC_FUNNEL
+            }
+        }
+        if (!full) {  // zero past the chunk end (the granules hold whatever follows it)
+#pragma unroll
+            for (int j = 0; j < 16; j++) d[j] &= keep_mask(static_cast<int64_t>(rem) - 64 * static_cast<int64_t>(lane) - 4 * j);
         }
 #pragma unroll
-        for (int j = 0; j < 16; j++)
-            res[j] = (d[j] ^ ks[j]) & keep_mask(static_cast<int64_t>(rem) - 64 * static_cast<int64_t>(lane) - 4 * j);
+        for (int j = 0; j < 16; j++) {
+            res[j] = d[j] ^ ks[j];
+            if (!full) res[j] &= keep_mask(static_cast<int64_t>(rem) - 64 * static_cast<int64_t>(lane) - 4 * j);
+        }
+        // 4. result -> this slot in the lane-own layout (every lane has read its granules)
         wave_lds_sync();
 #pragma unroll
         for (int t = 0; t < 4; t++)
-            *reinterpret_cast<uint4*>(L + ((4u * lane + (t ^ sw)) << 2)) =
+            *reinterpret_cast<uint4*>(S + 16u * (4u * lane + (t ^ sw))) =
                 make_uint4(res[4 * t], res[4 * t + 1], res[4 * t + 2], res[4 * t + 3]);
 
-        // 3. Poly1305 over the ciphertext blocks of this unit (zero padded to 16 bytes)
-        {
-            const uint32_t* m = kOpen ? d : res;
-            Fe r;
+        // 5. Poly1305 over this unit's ciphertext blocks (zero padded to 16 bytes)
+        const uint32_t* m = kOpen ? d : res;
+        Fe r;
 #pragma unroll
-            for (int j = 0; j < 5; j++) r.v[j] = ck.r[j];
+        for (int j = 0; j < 5; j++) r.v[j] = ck.r[j];
+        const Fe* tab = tabs + static_cast<uint64_t>(c) * kTabN;
+#if KCDC_CRYPT_ABL & 2  // measurement only: no Poly1305 work on full units
+        if (full) {
+            run.v[0] ^= m[0] ^ m[5] ^ m[10] ^ m[15];
+            run_end = uu;
+        } else
+#endif
+        if (full) {
+            run = fe_add(fe_mul(run, tab[kTabT + 253u]), fe_block(m[0], m[1], m[2], m[3]));
+#pragma unroll
+            for (int t = 1; t < 4; t++)
+                run = fe_add(fe_mul(run, r), fe_block(m[4 * t], m[4 * t + 1], m[4 * t + 2], m[4 * t + 3]));
+            run_end = uu;
+        } else {
+            // the chunk's last unit: lanes past the end add nothing; the unit sum is relative
+            // to its last block j_end, whose exponent is Nct + 1 - j_end
+            fold_run();
             const uint32_t nreal = (rem + 15u) >> 4, j0 = 4u * lane;
             Fe hl = fe_zero();
 #pragma unroll
@@ -526,36 +667,28 @@ __global__ __launch_bounds__(256) void crypt_units_kernel(CryptArgs a) {
                 const Fe nx = fe_add(fe_mul(hl, r), fe_block(m[4 * t], m[4 * t + 1], m[4 * t + 2], m[4 * t + 3]));
                 if (j0 + t < nreal) hl = nx;
             }
-            const Fe* tab = a.tabs + static_cast<uint64_t>(c) * kTabN;
-            if (j0 < nreal) {
-                const uint32_t jl = min(j0 + 3u, nreal - 1u);
-                hl = fe_mul(hl, tab[kTabT + (nreal - 1u - jl)]);
-            }
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) {
-                Fe o;
-#pragma unroll
-                for (int j = 0; j < 5; j++) o.v[j] = __shfl_xor(hl.v[j], off, 64);
-                hl = fe_carry(fe_add(hl, o));
-            }
-            // unit sum is relative to its last block j_end; that block's exponent is Nct + 1 - j_end
-            const uint64_t nct = (len + 15u) >> 4;
-            const uint32_t q = static_cast<uint32_t>(nct + 1u - (static_cast<uint64_t>(uu) * 256u + nreal - 1u));
-            hl = fe_mul(hl, fe_pow_tab(tab, q));
-            accum = fe_carry(fe_add(accum, hl));
+            if (j0 < nreal) hl = fe_mul(hl, tab[kTabT + (nreal - 1u - min(j0 + 3u, nreal - 1u))]);
+            else hl = fe_zero();
+            hl = wave_sum(hl);
+            const uint32_t qe = static_cast<uint32_t>(nct + 1u - (static_cast<uint64_t>(uu) * 256u + nreal - 1u));
+            accum = fe_carry(fe_add(accum, fe_mul(hl, fe_pow_tab(tab, qe))));
         }
         wave_lds_sync();
 
-        // 4. coalesced store; the zero tail of a partial last word stays inside the tag
+        // 6. coalesced store; the zero tail of a partial last word stays inside the tag
         //    (seal) or the 4-byte padding of the plaintext slot (open)
+        const uint32_t* Sw = reinterpret_cast<const uint32_t*>(S);
 #pragma unroll
         for (int k = 0; k < 16; k++) {
             const uint32_t i = 64u * k + lane;
-            if (4u * i < rem) dst[i] = L[swz(i)];
+            if (full || 4u * i < rem) dst[i] = Sw[swz(i)];
         }
         wave_lds_sync();
+        mis = mis_next;
+        prev_full = full;
     }
-    flush(c);
+    fold_run();
+    flush();
 }
 
 // One lane per chunk: add the AAD and length blocks, finish the tag, write or check it.
@@ -717,7 +850,8 @@ int crypt_run(const char* name, const uint8_t* secret, uint32_t secret_len, cons
     hipStream_t st = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(cryptdev::crypt_prep_kernel<kOpen>, dim3((n + 3u) / 4u), dim3(256), 0, st, a);
     hipLaunchKernelGGL(cryptdev::unit_scan_kernel, dim3(1), dim3(1024), 0, st, n, a.units);
-    hipLaunchKernelGGL(cryptdev::crypt_units_kernel<kOpen>, dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(cryptdev::crypt_units_kernel<kOpen>, dim3(grid), dim3(256), 0, st, a, a.keys, a.units, a.in_offs,
+                       a.out_offs, a.tabs, a.out, a.acc);
     hipLaunchKernelGGL(cryptdev::crypt_finish_kernel<kOpen>, dim3((n + 255u) / 256u), dim3(256), 0, st, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : set_error(-5, std::string("encryption kernel launch: ") + hipGetErrorString(e));
