@@ -221,9 +221,10 @@ int kcdc_hash_chunks_device(const char* hash_name, const uint8_t* d_data, const 
 /* ------------------------------------------------------------- content encryption
  * Kopia's CHACHA20-POLY1305-HMAC-SHA256 (repo/encryption/chacha20_poly1305_hmac_sha256_encryptor.go:
  * Encrypt/Decrypt/Overhead, 24-80; aead_helpers.go:12-75) for many chunks per call:
- *   key_i  = HMAC-SHA256(secret, iv_i)      iv_i = the last 16 bytes of chunk i's content ID
- *            (getPackedContentIV, repo/content/content_manager_lock_free.go:178-182)
- *   sealed = nonce_i(12) || ChaCha20-Poly1305(key_i, nonce_i, plaintext, aad = iv_i) (RFC 8439)
+ *   key_i  = HMAC-SHA256(secret, id_i)      id_i = the content ID the Encryptor is given; the content
+ *            manager passes the last 16 bytes of the content hash (getPackedContentIV,
+ *            repo/content/content_manager_lock_free.go:178-182)
+ *   sealed = nonce_i(12) || ChaCha20-Poly1305(key_i, nonce_i, plaintext, aad = id_i) (RFC 8439)
  * secret: the repository's derived key, HKDF-SHA256(masterKey, "encryption", "", 32)
  *   (deriveKey, repo/encryption/encryption.go:80-92), 1..64 bytes.
  * kcdc_encryption_algorithms / kcdc_encryption_overhead (28): the registry (Register, encryption.go:65).
@@ -239,20 +240,22 @@ int kcdc_hash_chunks_device(const char* hash_name, const uint8_t* d_data, const 
  *   d_status[i]: 0, KCDC_EBADMSG (authentication failed: aeadOpenPrefixedWithNonce's "unable to
  *   decrypt content"; the plaintext slot holds unauthenticated bytes), KCDC_EINVAL (shorter than
  *   28 bytes: "ciphertext too short") or KCDC_EFBIG.
- * d_ivs: 16 bytes per chunk at d_ivs + i * iv_stride (e.g. the hash output of
- * kcdc_hash_chunks_device + hash size - 16).  Asynchronous on hip_stream; d_work must stay
+ * d_ivs: iv_len (1..64) bytes per chunk at d_ivs + i * iv_stride: the content IDs (e.g. the
+ * hash output of kcdc_hash_chunks_device + hash size - 16, iv_len 16).  Asynchronous on hip_stream; d_work must stay
  * allocated until the work finishes. */
 int kcdc_encryption_algorithms(const char** names, int cap);
 int kcdc_encryption_overhead(const char* algorithm);
 uint64_t kcdc_crypt_workspace_size(uint32_t nchunks);
 int kcdc_encrypt_chunks_device(const char* algorithm, const uint8_t* secret, uint32_t secret_len, const uint8_t* d_data,
                                const uint64_t* d_offsets, const uint64_t* d_lens, uint32_t nchunks,
-                               const uint8_t* d_ivs, uint32_t iv_stride, const uint8_t* d_nonces, uint8_t* d_out,
+                               const uint8_t* d_ivs, uint32_t iv_len, uint32_t iv_stride, const uint8_t* d_nonces,
+                               uint8_t* d_out,
                                const uint64_t* d_out_offsets, int32_t* d_status, void* d_work, uint64_t work_bytes,
                                void* hip_stream);
 int kcdc_decrypt_chunks_device(const char* algorithm, const uint8_t* secret, uint32_t secret_len,
                                const uint8_t* d_sealed, const uint64_t* d_offsets, const uint64_t* d_sealed_lens,
-                               uint32_t nchunks, const uint8_t* d_ivs, uint32_t iv_stride, uint8_t* d_out,
+                               uint32_t nchunks, const uint8_t* d_ivs, uint32_t iv_len, uint32_t iv_stride,
+                               uint8_t* d_out,
                                const uint64_t* d_out_offsets, int32_t* d_status, void* d_work, uint64_t work_bytes,
                                void* hip_stream);
 

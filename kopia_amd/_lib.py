@@ -79,9 +79,9 @@ _SIGS = {
     "kcdc_encryption_overhead": (C.c_int, [C.c_char_p]),
     "kcdc_crypt_workspace_size": (C.c_uint64, [C.c_uint32]),
     "kcdc_encrypt_chunks_device": (C.c_int, [C.c_char_p, C.c_char_p, C.c_uint32, _P, _P, _P, C.c_uint32, _P,
-                                             C.c_uint32, _P, _P, _P, _P, _P, C.c_uint64, _P]),
+                                             C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint64, _P]),
     "kcdc_decrypt_chunks_device": (C.c_int, [C.c_char_p, C.c_char_p, C.c_uint32, _P, _P, _P, C.c_uint32, _P,
-                                             C.c_uint32, _P, _P, _P, _P, C.c_uint64, _P]),
+                                             C.c_uint32, C.c_uint32, _P, _P, _P, _P, C.c_uint64, _P]),
 }
 
 

@@ -276,7 +276,8 @@ struct CryptArgs {
     const uint64_t* in_lens;    // seal: plaintext lengths; open: sealed lengths
     uint8_t* out;               // seal: sealed base; open: plaintext base
     const uint64_t* out_offs;   // multiples of 4
-    const uint8_t* ivs;         // 16 bytes per chunk at ivs + i * iv_stride
+    const uint8_t* ivs;         // iv_len bytes per chunk at ivs + i * iv_stride (the content ID)
+    uint32_t iv_len;            // 1..64
     uint32_t iv_stride;
     const uint8_t* nonces;      // seal: 12 bytes per chunk
     int32_t* status;            // per chunk: 0, or a negative errno
@@ -299,23 +300,40 @@ __global__ __launch_bounds__(256) void crypt_prep_kernel(CryptArgs a) {
     const uint64_t len = bad ? 0 : (kOpen ? in_len - 28u : in_len);
     const uint8_t* ivp = a.ivs + static_cast<uint64_t>(c) * a.iv_stride;
     const uint8_t* np = kOpen ? a.in + a.in_offs[c] : a.nonces + 12ull * c;
-    uint32_t blk[16];
-#pragma unroll
-    for (int j = 0; j < 4; j++) blk[j] = bswap32(load_le32_bytes(ivp + 4 * j));
     uint32_t nonce[3] = {0u, 0u, 0u};
     if (!(kOpen && bad)) {
 #pragma unroll
         for (int j = 0; j < 3; j++) nonce[j] = load_le32_bytes(np + 4 * j);
     }
-    // HMAC-SHA256(secret, iv): inner block = iv || pad (80 bytes hashed), outer = digest || pad (96 bytes).
-    blk[4] = 0x80000000u;
+    // HMAC-SHA256(secret, id): after the (key ^ ipad) block, id || 0x80 || 0.. || bit length
+    // fills one block (id <= 55 bytes) or two; the outer hash is digest || pad (96 bytes).
+    const uint32_t il = a.iv_len;
+    uint32_t blk[32];
 #pragma unroll
-    for (int j = 5; j < 15; j++) blk[j] = 0;
-    blk[15] = 80u * 8u;
+    for (int j = 0; j < 32; j++) blk[j] = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 65; i++) {
+        const uint32_t b = i < il ? static_cast<uint32_t>(ivp[i < 64 ? i : 63]) : (i == il ? 0x80u : 0u);
+        blk[i >> 2] |= b << (24 - 8 * (i & 3));
+    }
+    const bool two = il > 55u;
+    const uint32_t bits = (64u + il) * 8u;
+    if (two) blk[31] = bits;
+    else blk[15] = bits;
     uint32_t h[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) h[j] = a.mid.in[j];
-    sha256_compress(h, blk);
+    {
+        uint32_t b0[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) b0[j] = blk[j];
+        sha256_compress(h, b0);
+        if (two) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) b0[j] = blk[16 + j];
+            sha256_compress(h, b0);
+        }
+    }
 #pragma unroll
     for (int j = 0; j < 8; j++) blk[j] = h[j];
     blk[8] = 0x80000000u;
@@ -324,7 +342,12 @@ __global__ __launch_bounds__(256) void crypt_prep_kernel(CryptArgs a) {
     blk[15] = 96u * 8u;
 #pragma unroll
     for (int j = 0; j < 8; j++) h[j] = a.mid.out[j];
-    sha256_compress(h, blk);
+    {
+        uint32_t b0[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) b0[j] = blk[j];
+        sha256_compress(h, b0);
+    }
     uint32_t key[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) key[j] = bswap32(h[j]);
@@ -718,14 +741,27 @@ __global__ __launch_bounds__(256) void crypt_finish_kernel(CryptArgs a) {
         for (int j = 0; j < 5; j++) h.v[j] = static_cast<uint32_t>(l[j]);
         h = fe_carry(h);
     }
+    // AAD = the content ID, zero padded to 16-byte blocks: block i of na has exponent Nct + 1 + na - i
     const uint8_t* ivp = a.ivs + static_cast<uint64_t>(c) * a.iv_stride;
-    const Fe aad = fe_block(load_le32_bytes(ivp), load_le32_bytes(ivp + 4), load_le32_bytes(ivp + 8),
-                            load_le32_bytes(ivp + 12));
-    h = fe_carry(fe_add(h, fe_mul(aad, fe_pow_tab(tab, static_cast<uint32_t>(nct + 2u)))));
+    const uint32_t il = a.iv_len, na = (il + 15u) >> 4;
+    for (uint32_t i = 0; i < na; i++) {
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            w[j] = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const uint32_t at = 16u * i + 4u * j + b;
+                if (at < il) w[j] |= static_cast<uint32_t>(ivp[at]) << (8 * b);
+            }
+        }
+        const Fe m = fe_block(w[0], w[1], w[2], w[3]);
+        h = fe_carry(fe_add(h, fe_mul(m, fe_pow_tab(tab, static_cast<uint32_t>(nct + 1u + na - i)))));
+    }
     Fe r;
 #pragma unroll
     for (int j = 0; j < 5; j++) r.v[j] = ck.r[j];
-    const Fe lens = fe_block(16u, 0u, static_cast<uint32_t>(len), static_cast<uint32_t>(len >> 32));
+    const Fe lens = fe_block(il, 0u, static_cast<uint32_t>(len), static_cast<uint32_t>(len >> 32));
     h = fe_carry(fe_add(h, fe_mul(lens, r)));
     uint32_t s[4], tag[4];
 #pragma unroll
@@ -799,13 +835,15 @@ int units_grid(int* err) {
 
 template <bool kOpen>
 int crypt_run(const char* name, const uint8_t* secret, uint32_t secret_len, const uint8_t* d_in,
-              const uint64_t* d_in_offs, const uint64_t* d_in_lens, uint32_t n, const uint8_t* d_ivs, uint32_t iv_stride,
+              const uint64_t* d_in_offs, const uint64_t* d_in_lens, uint32_t n, const uint8_t* d_ivs, uint32_t iv_len,
+              uint32_t iv_stride,
               const uint8_t* d_nonces, uint8_t* d_out, const uint64_t* d_out_offs, int32_t* d_status, void* d_work,
               uint64_t work_bytes, void* stream) {
     if (!find_crypt(name)) return set_error(-2, std::string("unknown encryption algorithm: ") + (name ? name : "(null)"));
     if (!secret || secret_len == 0 || secret_len > 64)
         return set_error(-22, "secret must be 1..64 bytes (the HKDF-derived key is 32)");
-    if (iv_stride < 16 && n > 1) return set_error(-22, "iv_stride must be >= 16");
+    if (iv_len == 0 || iv_len > 64) return set_error(-22, "content ID (iv) must be 1..64 bytes");
+    if (iv_stride < iv_len && n > 1) return set_error(-22, "iv_stride must be >= iv_len");
     if (n == 0) return 0;
     if (!d_in || !d_in_offs || !d_in_lens || !d_ivs || !d_out || !d_out_offs || !d_status || !d_work ||
         (!kOpen && !d_nonces))
@@ -824,6 +862,7 @@ int crypt_run(const char* name, const uint8_t* secret, uint32_t secret_len, cons
     a.out = d_out;
     a.out_offs = d_out_offs;
     a.ivs = d_ivs;
+    a.iv_len = iv_len;
     a.iv_stride = iv_stride;
     a.nonces = d_nonces;
     a.status = d_status;
@@ -877,18 +916,19 @@ extern "C" uint64_t kcdc_crypt_workspace_size(uint32_t nchunks) { return ws_layo
 
 extern "C" int kcdc_encrypt_chunks_device(const char* name, const uint8_t* secret, uint32_t secret_len,
                                           const uint8_t* d_data, const uint64_t* d_offsets, const uint64_t* d_lens,
-                                          uint32_t nchunks, const uint8_t* d_ivs, uint32_t iv_stride,
+                                          uint32_t nchunks, const uint8_t* d_ivs, uint32_t iv_len, uint32_t iv_stride,
                                           const uint8_t* d_nonces, uint8_t* d_out, const uint64_t* d_out_offsets,
                                           int32_t* d_status, void* d_work, uint64_t work_bytes, void* stream) {
-    return crypt_run<false>(name, secret, secret_len, d_data, d_offsets, d_lens, nchunks, d_ivs, iv_stride, d_nonces,
-                            d_out, d_out_offsets, d_status, d_work, work_bytes, stream);
+    return crypt_run<false>(name, secret, secret_len, d_data, d_offsets, d_lens, nchunks, d_ivs, iv_len, iv_stride,
+                            d_nonces, d_out, d_out_offsets, d_status, d_work, work_bytes, stream);
 }
 
 extern "C" int kcdc_decrypt_chunks_device(const char* name, const uint8_t* secret, uint32_t secret_len,
                                           const uint8_t* d_sealed, const uint64_t* d_offsets,
                                           const uint64_t* d_sealed_lens, uint32_t nchunks, const uint8_t* d_ivs,
-                                          uint32_t iv_stride, uint8_t* d_out, const uint64_t* d_out_offsets,
+                                          uint32_t iv_len, uint32_t iv_stride, uint8_t* d_out,
+                                          const uint64_t* d_out_offsets,
                                           int32_t* d_status, void* d_work, uint64_t work_bytes, void* stream) {
-    return crypt_run<true>(name, secret, secret_len, d_sealed, d_offsets, d_sealed_lens, nchunks, d_ivs, iv_stride,
+    return crypt_run<true>(name, secret, secret_len, d_sealed, d_offsets, d_sealed_lens, nchunks, d_ivs, iv_len, iv_stride,
                            nullptr, d_out, d_out_offsets, d_status, d_work, work_bytes, stream);
 }

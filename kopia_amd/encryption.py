@@ -79,10 +79,11 @@ class Encryptor:
         return torch.empty(max(int(_lib.lib().kcdc_crypt_workspace_size(n)), 1), dtype=torch.uint8, device=device)
 
     def encrypt_chunks_device(self, data_ptr: int, offsets, lengths, d_ivs, iv_stride: int, d_out, out_offsets,
-                              device, nonces: bytes | None = None, stream=None):
+                              device, nonces: bytes | None = None, stream=None, iv_len: int = 16):
         """Seal chunk i = [offsets[i], +lengths[i]) of the device bytes at data_ptr into d_out
-        (a device uint8 tensor) at out_offsets[i].  d_ivs: device bytes, 16 per chunk at
-        stride iv_stride.  nonces: 12 bytes per chunk (default os.urandom, as crypto/rand).
+        (a device uint8 tensor) at out_offsets[i].  d_ivs: a device tensor holding the content
+        IDs, iv_len bytes each at stride iv_stride (the content manager's 16-byte packed IV).
+        nonces: 12 bytes per chunk (default os.urandom, as crypto/rand).
         Returns the device int32 status tensor (asynchronous on `stream`)."""
         import torch
         n = len(offsets)
@@ -102,13 +103,13 @@ class Encryptor:
             stream = torch.cuda.current_stream(device)
         _lib.check(_lib.lib().kcdc_encrypt_chunks_device(
             self.name.encode(), self.secret, len(self.secret), C.c_void_p(data_ptr), d_offs.data_ptr(),
-            d_lens.data_ptr(), n, C.c_void_p(d_ivs.data_ptr()), iv_stride, d_nonce.data_ptr(), d_out.data_ptr(),
+            d_lens.data_ptr(), n, C.c_void_p(d_ivs.data_ptr()), iv_len, iv_stride, d_nonce.data_ptr(), d_out.data_ptr(),
             d_oo.data_ptr(), status.data_ptr(), work.data_ptr(), work.numel(), C.c_void_p(stream.cuda_stream)))
         status._kcdc_keep = (d_offs, d_lens, d_oo, d_nonce, work, d_ivs)  # alive until the caller syncs
         return status[:n]
 
     def decrypt_chunks_device(self, sealed_ptr: int, offsets, sealed_lengths, d_ivs, iv_stride: int, d_out,
-                              out_offsets, device, stream=None):
+                              out_offsets, device, stream=None, iv_len: int = 16):
         """Open sealed chunk i = [offsets[i], +sealed_lengths[i]) into d_out at out_offsets[i].
         Returns the device int32 status tensor: 0, KCDC_EBADMSG, KCDC_EINVAL or KCDC_EFBIG."""
         import torch
@@ -124,7 +125,7 @@ class Encryptor:
             stream = torch.cuda.current_stream(device)
         _lib.check(_lib.lib().kcdc_decrypt_chunks_device(
             self.name.encode(), self.secret, len(self.secret), C.c_void_p(sealed_ptr), d_offs.data_ptr(),
-            d_lens.data_ptr(), n, C.c_void_p(d_ivs.data_ptr()), iv_stride, d_out.data_ptr(), d_oo.data_ptr(),
+            d_lens.data_ptr(), n, C.c_void_p(d_ivs.data_ptr()), iv_len, iv_stride, d_out.data_ptr(), d_oo.data_ptr(),
             status.data_ptr(), work.data_ptr(), work.numel(), C.c_void_p(stream.cuda_stream)))
         status._kcdc_keep = (d_offs, d_lens, d_oo, work, d_ivs)
         return status[:n]

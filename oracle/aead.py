@@ -7,11 +7,14 @@ aead_helpers.go, encryption.go:82-95), whose arithmetic lives in golang.org/x/cr
 crypto/hmac, crypto/sha256):
 * deriveKey: HKDF-SHA256(masterKey, salt = purpose ("encryption"), info = "", 32 bytes)
   (RFC 5869; Go's hkdf.Key(h, secret, salt, info, n) -- encryption.go:82-95);
-* per content: key = HMAC-SHA256(derived, iv), iv = the last 16 bytes of the content hash
-  (repo/content/content_manager_lock_free.go:178-182);
+* per content: key = HMAC-SHA256(derived, id), id = the content ID the Encryptor is given (the
+  content manager passes the last 16 bytes of the content hash,
+  repo/content/content_manager_lock_free.go:178-182);
 * Seal: output = nonce(12) || ChaCha20-Poly1305(key, nonce, plaintext, aad = iv)
   (RFC 8439 §2.8; aead_helpers.go: random nonce prefix).
-Pinned by the RFC 8439 / RFC 5869 example vectors (tests/test_aead_oracle.py).
+Pinned by the RFC 8439 / RFC 5869 example vectors and the reference's own ciphertext samples
+(repo/encryption/encryption_test.go:97-127, tests/golden/kopia_encryption_samples.json), which it
+re-seals byte for byte (tests/test_aead_oracle.py).
 """
 from __future__ import annotations
 
@@ -115,9 +118,23 @@ def chacha20poly1305_seal(key: bytes, nonce: bytes, plaintext: bytes, aad: bytes
     return ct + poly1305(otk, mac)
 
 
-def kopia_encrypt(derived: bytes, content_hash: bytes, nonce: bytes, plaintext: bytes) -> bytes:
-    """chacha20poly1305hmacSha256Encryptor.Encrypt with a given nonce (the reference draws
-    it from crypto/rand): nonce || Seal(key = HMAC-SHA256(derived, iv), aad = iv)."""
-    iv = content_hash[-16:]
-    key = hmac.new(derived, iv, hashlib.sha256).digest()
-    return nonce + chacha20poly1305_seal(key, nonce, plaintext, iv)
+def kopia_encrypt(derived: bytes, content_id: bytes, nonce: bytes, plaintext: bytes) -> bytes:
+    """chacha20poly1305hmacSha256Encryptor.Encrypt with a given nonce (the reference draws it
+    from crypto/rand): nonce || Seal(key = HMAC-SHA256(derived, content_id), aad = content_id).
+    The content manager passes the last 16 bytes of the content hash as content_id."""
+    key = hmac.new(derived, content_id, hashlib.sha256).digest()
+    return nonce + chacha20poly1305_seal(key, nonce, plaintext, content_id)
+
+
+def kopia_decrypt(derived: bytes, content_id: bytes, sealed: bytes) -> bytes | None:
+    """Decrypt (aeadOpenPrefixedWithNonce): None when authentication fails."""
+    if len(sealed) < 28:
+        return None
+    key = hmac.new(derived, content_id, hashlib.sha256).digest()
+    nonce, body = sealed[:12], sealed[12:]
+    otk = chacha20_block(key, 0, nonce)[:32]
+    ct, tag = body[:-16], body[-16:]
+    mac = content_id + _pad16(content_id) + ct + _pad16(ct) + struct.pack("<QQ", len(content_id), len(ct))
+    if not hmac.compare_digest(poly1305(otk, mac), tag):
+        return None
+    return chacha20_xor(key, 1, nonce, ct)

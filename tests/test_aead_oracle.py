@@ -55,3 +55,18 @@ def test_host_mirror_and_registry():
     assert ke.overhead("CHACHA20-POLY1305-HMAC-SHA256") == 28
     offs, total = ke.sealed_layout([0, 1, 5, 100])
     assert offs.tolist() == [0, 28, 60, 96] and total == 224
+
+
+def test_reference_ciphertext_samples():
+    """The reference's TestCiphertextSamples (encryption_test.go:97-127): the oracle opens every
+    CHACHA20-POLY1305-HMAC-SHA256 sample to its payload and, given the sample's nonce, re-seals
+    the payload to exactly the sample's bytes."""
+    for c in golden("kopia_encryption_samples.json")["cases"]:
+        secret = aead.derive_key(c["master_key"].encode())
+        cid, payload = c["content_id"].encode(), c["payload"].encode()
+        sample = bytes.fromhex(c["samples"]["CHACHA20-POLY1305-HMAC-SHA256"])
+        assert aead.kopia_decrypt(secret, cid, sample) == payload
+        assert aead.kopia_encrypt(secret, cid, sample[:12], payload) == sample
+        bad = bytearray(sample)
+        bad[15] ^= 1
+        assert aead.kopia_decrypt(secret, cid, bytes(bad)) is None

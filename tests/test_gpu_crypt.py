@@ -3,7 +3,8 @@
 RFC 8439 / RFC 5869 vectors in tests/test_aead_oracle.py): random lengths across the 16-byte,
 64-byte and 4 KiB unit boundaries, misaligned plaintext offsets, empty chunks, the chunks the
 splitter cuts and hashes on config-2 streams (IV = the content hash), round trips, and the
-authentication-failure / short-input / error contract."""
+authentication-failure / short-input / error contract; the reference's own ciphertext samples
+(encryption_test.go:97-127) open and re-seal byte for byte, with 32-byte content IDs."""
 import numpy as np
 import pytest
 
@@ -162,6 +163,61 @@ def test_config2_pipeline(gpu):
     assert all(p[po[i]:po[i] + lens[i]].tobytes() == host[offs[i]:offs[i] + lens[i]].tobytes() for i in range(n))
 
 
+def test_reference_samples(gpu):
+    """The reference's TestCiphertextSamples (encryption_test.go:97-127) on the device: each
+    CHACHA20-POLY1305-HMAC-SHA256 sample (32-byte content IDs) opens to its payload, and sealing
+    the payload with the sample's nonce reproduces the sample byte for byte."""
+    from conftest import golden
+    import torch
+    for c in golden("kopia_encryption_samples.json")["cases"]:
+        enc = ke.Encryptor(ALG, c["master_key"].encode())
+        cid, payload = c["content_id"].encode(), c["payload"].encode()
+        sample = bytes.fromhex(c["samples"][ALG])
+        d_id = torch.frombuffer(bytearray(cid), dtype=torch.uint8).to(gpu)
+        d_in = torch.frombuffer(bytearray(sample), dtype=torch.uint8).to(gpu)
+        plain = torch.zeros(len(payload) + 8, dtype=torch.uint8, device=gpu)
+        st = enc.decrypt_chunks_device(d_in.data_ptr(), [0], [len(sample)], d_id, len(cid), plain, [0], gpu,
+                                       iv_len=len(cid))
+        torch.cuda.synchronize()
+        assert st.cpu().tolist() == [0]
+        assert plain.cpu().numpy()[:len(payload)].tobytes() == payload
+        d_pl = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(gpu)
+        out = torch.zeros(len(sample) + 4, dtype=torch.uint8, device=gpu)
+        st = enc.encrypt_chunks_device(d_pl.data_ptr(), [0], [len(payload)], d_id, len(cid), out, [0], gpu,
+                                       nonces=sample[:12], iv_len=len(cid))
+        torch.cuda.synchronize()
+        assert st.cpu().tolist() == [0]
+        assert out.cpu().numpy()[:len(sample)].tobytes() == sample
+
+
+@pytest.mark.parametrize("iv_len", [1, 15, 17, 32, 55, 56, 63, 64])
+def test_content_id_lengths(gpu, iv_len):
+    """Content IDs of 1..64 bytes (HMAC message of one or two SHA-256 blocks, AAD of 1..4
+    Poly1305 blocks) against the oracle."""
+    import torch
+    rng = np.random.default_rng(iv_len)
+    n = 20
+    lens = rng.integers(0, 9000, n)
+    host = rng.integers(0, 256, int(lens.sum()) + 64, dtype=np.uint8)
+    offs = np.concatenate(([1], 1 + np.cumsum(lens)[:-1])).astype(np.int64)
+    ids = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+    nonces = bytes(rng.integers(0, 256, 12 * n, dtype=np.uint8))
+    enc = ke.Encryptor(ALG, MASTER)
+    d = torch.from_numpy(host).to(gpu)
+    d_ids = torch.from_numpy(ids).to(gpu)
+    oo, total = ke.sealed_layout(lens)
+    out = torch.zeros(total, dtype=torch.uint8, device=gpu)
+    st = enc.encrypt_chunks_device(d.data_ptr(), offs, lens, d_ids, 64, out, oo, gpu, nonces=nonces, iv_len=iv_len)
+    torch.cuda.synchronize()
+    assert not st.cpu().numpy().any()
+    got = out.cpu().numpy()
+    secret = aead.derive_key(MASTER)
+    for i in range(n):
+        want = aead.kopia_encrypt(secret, ids[i, :iv_len].tobytes(), nonces[12 * i:12 * i + 12],
+                                  host[offs[i]:offs[i] + lens[i]].tobytes())
+        assert got[oo[i]:oo[i] + lens[i] + 28].tobytes() == want, i
+
+
 def test_errors(gpu):
     import torch
     enc = ke.Encryptor(ALG, MASTER)
@@ -169,12 +225,12 @@ def test_errors(gpu):
     with pytest.raises(_lib.KcdcError):
         ke.Encryptor("AES128-GCM", MASTER)
     L = _lib.lib()
-    rc = L.kcdc_encrypt_chunks_device(ALG.encode(), enc.secret, 65, d.data_ptr(), d.data_ptr(), d.data_ptr(), 1,
-                                      d.data_ptr(), 16, d.data_ptr(), d.data_ptr(), d.data_ptr(), d.data_ptr(),
-                                      d.data_ptr(), 64, None)
-    assert rc == _lib.KCDC_EINVAL  # secret > 64 bytes
-    rc = L.kcdc_encrypt_chunks_device(ALG.encode(), enc.secret, 32, d.data_ptr(), d.data_ptr(), d.data_ptr(), 1,
-                                      d.data_ptr(), 16, d.data_ptr(), d.data_ptr(), d.data_ptr(), d.data_ptr(),
-                                      d.data_ptr(), 64, None)
-    assert rc == _lib.KCDC_EINVAL  # workspace too small
+    def call(secret_len, iv_len, work):
+        return L.kcdc_encrypt_chunks_device(ALG.encode(), enc.secret, secret_len, d.data_ptr(), d.data_ptr(),
+                                            d.data_ptr(), 1, d.data_ptr(), iv_len, 16, d.data_ptr(), d.data_ptr(),
+                                            d.data_ptr(), d.data_ptr(), d.data_ptr(), work, None)
+    assert call(65, 16, 1 << 20) == _lib.KCDC_EINVAL  # secret > 64 bytes
+    assert call(32, 16, 64) == _lib.KCDC_EINVAL       # workspace too small
+    assert call(32, 0, 1 << 20) == _lib.KCDC_EINVAL   # empty content ID
+    assert call(32, 65, 1 << 20) == _lib.KCDC_EINVAL  # content ID > 64 bytes
     assert ke.overhead(ALG) == 28
