@@ -357,12 +357,14 @@ def bench_batch(args, comm: Comm):
 def bench_hash(args, data, ns: int, L: int, cuts: list, dev) -> dict:
     """§8f #2: keyed BLAKE2 content hash of every chunk the split produced
     (repo/content/content_manager.go:812, repo/hashing/hashing.go:78-101), on the device.
-    A chunk is one sequential BLAKE2 chain (one lane), so two figures: the batch alone (its
-    5,7xx chunks: bounded by the longest chunk) and `--hash-inflight` batches' chunk tables
-    in one launch (the pipelined upload case: many chunks in flight; the same bytes are
-    re-read and re-hashed per table, 16 GiB each).  CPU baseline: hashlib, one thread."""
+    A chunk is one sequential BLAKE2 chain (a quad of lanes), so two figures: the batch alone
+    (its 5,7xx chunks: bounded by the longest chunk) and `--hash-inflight` batches' chunk
+    tables in one launch (the pipelined upload case: many chunks in flight; the same bytes are
+    re-read and re-hashed per table, 16 GiB each).  Each beside the one-lane-per-chunk kernel.
+    CPU baseline: hashlib, one thread."""
     import hashlib
     import torch
+    from kopia_amd import _lib
     from kopia_amd import hashing as kh
     name, key = args.hash, bytes(range(32))
     offs, lens = kh.chunk_table([i * L for i in range(ns)], cuts)
@@ -379,7 +381,11 @@ def bench_hash(args, data, ns: int, L: int, cuts: list, dev) -> dict:
         torch.cuda.synchronize(dev)
         return e0.elapsed_time(e1) / reps, out
 
-    ms1, out = timed(offs, lens, 3)
+    ms1, out = timed(offs, lens, 3)  # auto: a quad of lanes per chunk at this chunk count
+    L = _lib.lib()
+    L.kcdc_test_set(_lib.TEST_HASH_LANES, 1)
+    ms1_lane, _ = timed(offs, lens, 1)  # one lane per chunk, for comparison
+    L.kcdc_test_set(_lib.TEST_HASH_LANES, 0)
     # parity of a sample against the oracle (hashlib, RFC 7693; tests/test_hash_oracle.py)
     host = None
     bad = 0
@@ -392,14 +398,21 @@ def bench_hash(args, data, ns: int, L: int, cuts: list, dev) -> dict:
         bad += fn(chunk, key=key, digest_size=nn).digest()[:keep] != got[i].tobytes()
     R = args.hash_inflight
     msR, _ = timed(np.tile(offs, R), np.tile(lens, R), 1)
+    L.kcdc_test_set(_lib.TEST_HASH_LANES, 1)
+    msR1, _ = timed(np.tile(offs, R), np.tile(lens, R), 1)  # one lane per chunk, for comparison
+    L.kcdc_test_set(_lib.TEST_HASH_LANES, 0)
     sample = data[: 256 << 20].cpu().numpy().tobytes()
     t0 = time.perf_counter()
     fn(sample, key=key, digest_size=nn).digest()
     cpu = len(sample) / GiB / (time.perf_counter() - t0)
     return {"algo": name, "batch_chunks": int(len(offs)), "batch_bytes": total, "largest_chunk": int(lens.max()),
             "batch_ms": round(ms1, 3), "batch_gib_s": round(total / GiB / (ms1 * 1e-3), 2),
+            "batch_kernel": "4 lanes per chunk" if len(offs) <= (1 << 20) else "1 lane per chunk",
+            "batch_1lane_ms": round(ms1_lane, 3),
             "inflight_tables": R, "inflight_chunks": int(R * len(offs)), "inflight_ms": round(msR, 3),
             "inflight_gib_s": round(R * total / GiB / (msR * 1e-3), 2),
+            "inflight_kernel": "4 lanes per chunk" if R * len(offs) <= (1 << 20) else "1 lane per chunk",
+            "inflight_1lane_ms": round(msR1, 3),
             "sample_parity_mismatches": int(bad), "sample_chunks": len(pick),
             "cpu_hashlib_1thread_gib_s": round(cpu, 3)}
 

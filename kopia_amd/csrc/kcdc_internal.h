@@ -39,6 +39,9 @@ const Algo* custom_algo(int32_t kind, uint64_t avg);  // interned, nullptr if in
 int algo_index(const Algo* a);                         // registry index, -1 for custom
 const Algo& algo_at(int i);  // sorted by name
 
+// Test knob: lanes per chunk of the content-hash kernels (0 auto, 1, 4).
+int& test_hash_lanes();
+
 // Thread-local error reporting.
 int set_error(int code, const std::string& msg);
 

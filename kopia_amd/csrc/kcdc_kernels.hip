@@ -4018,6 +4018,7 @@ extern "C" int kcdc_test_set(int32_t key, int64_t value) {
         case 1: g_test.spin_cap = static_cast<uint32_t>(value); return 0;   // KCDC_TEST_SPIN_CAP
         case 2: g_test.no_steal = value != 0; return 0;                     // KCDC_TEST_NO_STEAL
         case 3: g_test.force_error = value != 0; return 0;                  // KCDC_TEST_FORCE_ERROR
+        case 4: test_hash_lanes() = static_cast<int>(value); return 0;     // KCDC_TEST_HASH_LANES
         default: return set_error(-22, "unknown test knob");
     }
 }

@@ -1,7 +1,8 @@
 """GPU: keyed BLAKE2 content hashes of many chunks (kcdc_hash_chunks_device) bit-exact
 against the oracle (hashlib, pinned by tests/test_hash_oracle.py): random chunk lengths and
 misaligned offsets, every registered name and key length class, the chunks the splitter
-cuts on config-2 streams, and the error contract."""
+cuts on config-2 streams, and the error contract -- through both kernels (one lane per chunk,
+and a quad of lanes per chunk)."""
 import concurrent.futures as cf
 
 import numpy as np
@@ -25,13 +26,23 @@ def _hash_all(name, key, host, offs, lens):
     return out.cpu().numpy()
 
 
+@pytest.fixture(params=[1, 4], ids=["lane", "quad"])
+def lanes(request):
+    """Both kernels: one lane per chunk, and a quad of lanes per chunk (KCDC_TEST_HASH_LANES)."""
+    L = _lib.lib()
+    L.kcdc_test_set(_lib.TEST_HASH_LANES, request.param)
+    yield request.param
+    L.kcdc_test_set(_lib.TEST_HASH_LANES, 0)
+
+
 @pytest.mark.parametrize("name", ["BLAKE2B-256-128", "BLAKE2B-256", "BLAKE2S-128", "BLAKE2S-256"])
-def test_random_chunks(gpu, name):
+def test_random_chunks(gpu, name, lanes):
     rng = np.random.default_rng(len(name))
     host = coracle.gen_stream(SEED, 31, 4 << 20)
     n = 700
     lens = rng.integers(0, 20000, n)
-    lens[:12] = [0, 1, 3, 4, 63, 64, 65, 127, 128, 129, 255, 256]
+    lens[:16] = [0, 1, 3, 4, 15, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 129]
+    lens[16:20] = [255, 256, 96, 97]
     offs = np.array([int(rng.integers(0, host.size - int(L))) for L in lens], dtype=np.int64)
     maxk = 64 if name.startswith("BLAKE2B") else 32
     for klen in sorted({0, 1, 17, 32, maxk}):
@@ -44,7 +55,7 @@ def test_random_chunks(gpu, name):
             assert got[i].tobytes() == want, (name, klen, i, int(lens[i]), int(offs[i]))
 
 
-def test_config2_chunks(gpu):
+def test_config2_chunks(gpu, lanes):
     """The chunks the batch splitter cuts from 256 x 4 MiB counter-PRNG streams, hashed with
     the default algorithm and a 32-byte secret, equal the oracle's digests."""
     import torch
