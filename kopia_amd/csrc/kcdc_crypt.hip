@@ -473,7 +473,10 @@ constexpr uint32_t kSlotBytes = kUnit + 32;
 // sum (lane l scaled by r^(4(63-l)), reduced across the wave, scaled by r^Q) only when the
 // chunk or the wave's range ends, or at the chunk's partial last unit.
 template <bool kOpen>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void crypt_units_kernel(
+#ifndef KCDC_CRYPT_WAVES
+#define KCDC_CRYPT_WAVES 4  // waves per SIMD: 127 VGPRs, no VGPR spills; seal 3.08-3.12 vs 3.17-3.20 ms at 3
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KCDC_CRYPT_WAVES, KCDC_CRYPT_WAVES))) void crypt_units_kernel(
     CryptArgs a, const ChunkKey* __restrict__ keys, const uint32_t* __restrict__ units,
     const uint64_t* __restrict__ in_offs, const uint64_t* __restrict__ out_offs, const Fe* __restrict__ tabs,
     uint8_t* __restrict__ out, unsigned long long* __restrict__ acc) {
