@@ -269,6 +269,8 @@ int kcdc_decrypt_chunks_device(const char* algorithm, const uint8_t* secret, uin
  *   KCDC_TEST_FORCE_ERROR 1: every batch launch reports failure (KCDC_COUNT_FAILED)
  *   KCDC_TEST_HASH_LANES  lanes per chunk of kcdc_hash_chunks_device: 0 auto (4 up to 2^20
  *                         chunks, else 1), 1 or 4
+ *   KCDC_TEST_NO_SERVER   1: private streaming handles launch one scan per call instead of using
+ *                         the device's resident scan server
  * kcdc_test_occupy: occupy `nwg` CUs (one workgroup with all of the CU's LDS each) for
  * `usec` microseconds on `hip_stream`, e.g. to run a batch beside a kernel that holds CUs.
  * kcdc_test_queue_stat: after the last pipelined batch launch has finished (synchronise
@@ -279,6 +281,7 @@ int kcdc_decrypt_chunks_device(const char* algorithm, const uint8_t* secret, uin
 #define KCDC_TEST_NO_STEAL 2
 #define KCDC_TEST_FORCE_ERROR 3
 #define KCDC_TEST_HASH_LANES 4
+#define KCDC_TEST_NO_SERVER 5
 int kcdc_test_set(int32_t key, int64_t value);
 int kcdc_test_occupy(uint32_t nwg, uint32_t usec, void* hip_stream);
 #define KCDC_TEST_STAT_GIVEUPS 1

@@ -194,7 +194,9 @@ int ensure_stage(kcdc_splitter* s, size_t need) {
     s->h_stage = nullptr;
     s->stage_cap = 0;
     if (KCDC_HANDLE_ZC) {
-        HIP_TRY(hipHostMalloc(&s->h_stage, cap, hipHostMallocMapped), "hipHostMalloc stage");
+        // fine-grained: the resident scan server reads it between requests without a kernel
+        // boundary, so no stale cached copy may survive
+        HIP_TRY(hipHostMalloc(&s->h_stage, cap, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc stage");
         void* pd = nullptr;
         HIP_TRY(hipHostGetDevicePointer(&pd, s->h_stage, 0), "stage mapping");
         s->d_stage = static_cast<uint8_t*>(pd);
@@ -220,6 +222,14 @@ int64_t gpu_first_candidate(kcdc_splitter* s, const uint8_t* b, size_t n) {
     if (rc) return rc;
     std::memcpy(s->h_stage, s->hist, kWindow);
     std::memcpy(s->h_stage + kWindow, b, n);
+    if (KCDC_HANDLE_ZC) {  // the resident scan server: no launch, tables already in LDS
+        int64_t f = -1;
+        const int rs = server_scan_first(*s->algo, s->d_stage, total, kWindow, static_cast<int64_t>(total) - 1,
+                                         s->device, &f);
+        if (rs < 0) return rs;
+        if (rs == 0) return f < 0 ? -1 : f - kWindow;
+        // busy (another handle holds it) or unavailable: a scan of our own
+    }
     if (!KCDC_HANDLE_ZC)
         HIP_TRY(hipMemcpyAsync(s->d_stage, s->h_stage, total, hipMemcpyHostToDevice, s->stream), "H2D slice");
     rc = launch_scan_first(*s->algo, s->d_stage, total, kWindow, static_cast<int64_t>(total) - 1, s->d_out, s->device,

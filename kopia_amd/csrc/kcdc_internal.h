@@ -66,6 +66,12 @@ int launch_split_batch(const Algo& algo, const SplitArgs& a, int device, void* s
 // d_out[0] the first candidate position in [lo, hi] or -1.
 int launch_scan_first(const Algo& algo, const uint8_t* d_buf, uint64_t len, int64_t lo, int64_t hi, int64_t* d_out,
                       int device, void* stream);
+// The same scan through the device's resident scan server (no launch): 0 and *out = the
+// first candidate in [lo, hi] (or -1); 1 = the server is unavailable or busy (launch
+// instead); < 0 = error.  d_stage: fine-grained mapped host memory, 256-byte aligned.
+int server_scan_first(const Algo& algo, const uint8_t* d_stage, uint64_t len, int64_t lo, int64_t hi, int device,
+                      int64_t* out);
+void set_scan_server_off(bool off);
 int launch_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint32_t nstreams, uint64_t seed,
                      uint64_t first_sid, void* stream);
 // Grouped streaming handles: request r scans [lo, hi] of the `len` bytes at base + off.

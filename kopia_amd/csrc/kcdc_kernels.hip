@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstring>
 #include <mutex>
 #include <type_traits>
 #include <vector>
@@ -2812,6 +2814,118 @@ __global__ __launch_bounds__(kWave) void scan_first_batch_kernel(BatchArgs a, co
     if (lane == 0) out[blockIdx.x] = f;
 }
 
+// Resident scan server for private streaming handles (kcdc_splitter_next): one workgroup
+// stays on the GPU while handles are busy and takes requests from a mailbox in fine-grained
+// (coherent) host memory, so a NextSplitPoint pays no kernel launch and no table fill.
+// Per request: all 512 threads copy the slice (mapped host staging) into device scratch
+// with every load in flight, then 8 waves scan 8 sub-ranges of [lo, hi] and the smallest
+// first candidate wins.  The kernel exits after kSrvIdle ticks without a request or
+// kSrvLife ticks in total (s_memrealtime, 100 MHz); the host relaunches it when needed.
+struct ServerMbox {
+    uint64_t req_seq;  // host: incremented after the fields below are written
+    uint64_t pad0[7];
+    uint64_t src;      // device-visible address of the slice (history || bytes)
+    int64_t len, lo, hi;
+    uint64_t pad1[4];
+    uint64_t done_seq;  // device: the request served, after `result`
+    int64_t result;
+    uint64_t pad2[6];
+};
+constexpr uint64_t kSrvIdle = 200000;     // 2 ms
+constexpr uint64_t kSrvLife = 20000000;   // 200 ms: every server kernel is bounded
+constexpr int kSrvWaves = 8;  // 2 per SIMD: scan_region needs up to 219 VGPRs (1,024 threads spilled)
+
+template <int KIND>
+__global__ __launch_bounds__(kSrvWaves * kWave) void scan_server_kernel(BatchArgs a, ServerMbox* mb, uint8_t* scratch,
+                                                                        uint64_t served) {
+    __shared__ HashSmem<KIND> sm;
+    __shared__ int64_t wave_first[kSrvWaves];
+    __shared__ uint64_t cmd[5];
+    fill_tables<KIND>(sm, a);
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    const auto hash0 = make_hash<KIND>(sm, a, lane);
+    const uint64_t t0 = wall_clock64();
+    uint64_t last = t0;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            uint64_t sq = served;
+            for (;;) {
+                // relaxed: an acquire at system scope invalidates the L2 on every poll.  The
+                // mailbox and the staging are fine-grained host memory (never cached), and the
+                // loads below issue only after this loop has exited.
+                sq = __hip_atomic_load(&mb->req_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (sq != served) break;
+                const uint64_t now = wall_clock64();
+                if (now - last > kSrvIdle || now - t0 > kSrvLife) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            cmd[0] = sq;
+            if (sq != served) {
+                cmd[1] = __hip_atomic_load(&mb->src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                cmd[2] = static_cast<uint64_t>(__hip_atomic_load(&mb->len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+                cmd[3] = static_cast<uint64_t>(__hip_atomic_load(&mb->lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+                cmd[4] = static_cast<uint64_t>(__hip_atomic_load(&mb->hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+            }
+        }
+        __syncthreads();
+        const uint64_t sq = cmd[0];
+        if (sq == served) break;  // idle or lifetime: every thread leaves together
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(cmd[1]);
+        const int64_t len = static_cast<int64_t>(cmd[2]), lo = static_cast<int64_t>(cmd[3]),
+                      hi = static_cast<int64_t>(cmd[4]);
+        // the slice -> device scratch (the staging is 256-byte aligned; len <= the scratch).
+        // One system-scope acquire per request (not per poll): no line of the staging, which
+        // the host rewrites between requests, may be served from a cache.
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        // 8 loads in flight per thread (64 KiB per round over PCIe), then their stores: a
+        // load-store loop left one 16-byte PCIe read per thread outstanding and cost ~2 us per 8 KiB
+        const int64_t n16 = len >> 4;
+        constexpr int kIn = 8;
+        constexpr int64_t kT = kSrvWaves * kWave;
+        const u32x4* s16 = reinterpret_cast<const u32x4*>(src);
+        u32x4* d16 = reinterpret_cast<u32x4*>(scratch);
+        for (int64_t base = 0; base < n16; base += kIn * kT) {
+            u32x4 v[kIn];
+#pragma unroll
+            for (int k = 0; k < kIn; k++) {
+                const int64_t i = base + k * kT + threadIdx.x;
+                if (i < n16) v[k] = __builtin_nontemporal_load(s16 + i);
+            }
+#pragma unroll
+            for (int k = 0; k < kIn; k++) {
+                const int64_t i = base + k * kT + threadIdx.x;
+                if (i < n16) d16[i] = v[k];
+            }
+        }
+        for (int64_t i = (n16 << 4) + threadIdx.x; i < len; i += kT) scratch[i] = src[i];
+        // Every reader of the scratch is a wave of this workgroup: after the barrier (which waits
+        // for the stores) only this CU's vector L1 may still hold the previous request's lines,
+        // so invalidate just that (an agent-scope fence would also write back and invalidate
+        // the L2 on every request).
+        __syncthreads();
+        asm volatile("buffer_inv sc0" ::: "memory");
+        const int64_t span = hi - lo + 1, per = ((span + kSrvWaves - 1) / kSrvWaves + 63) & ~int64_t(63);
+        const int64_t mlo = lo + per * w, mhi = mlo + per - 1 < hi ? mlo + per - 1 : hi;
+        int64_t f = -1;
+        if (mlo <= mhi) f = scan_region(hash0, scratch, 0, len, mlo, mhi, lane);
+        if (lane == 0) wave_first[w] = f;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t best = -1;
+            for (int k = 0; k < kSrvWaves; k++)
+                if (wave_first[k] >= 0 && (best < 0 || wave_first[k] < best)) best = wave_first[k];
+            // result, then (after it has completed) the sequence number the host waits for; a
+            // release at system scope would write back the whole L2 first
+            __hip_atomic_store(&mb->result, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&mb->done_seq, sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        served = sq;
+        last = wall_clock64();
+        __syncthreads();
+    }
+}
+
 // ------------------------------------------------------ synthetic streams
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -3822,6 +3936,108 @@ int launch_scan_first(const Algo& algo, const uint8_t* d_buf, uint64_t len, int6
     return e == hipSuccess ? 0 : hip_fail(e, "scan kernel launch");
 }
 
+// ---- resident scan server (host side): one per (device, hash kind)
+namespace {
+struct ScanServer {
+    std::mutex mu;
+    bool init = false;
+    hipStream_t st = nullptr;
+    dev::ServerMbox* h = nullptr;  // fine-grained, mapped
+    dev::ServerMbox* d = nullptr;
+    uint8_t* scratch = nullptr;
+    uint64_t cap = 0;
+    uint64_t seq = 0;
+    bool launched = false;
+    std::chrono::steady_clock::time_point last_answer{};  // the server was alive then
+};
+ScanServer g_srv[64][2];
+bool g_srv_off = false;  // kcdc_test_set(KCDC_TEST_NO_SERVER)
+
+int srv_launch(ScanServer& sv, const Algo& algo, const DeviceTables& t) {
+    dev::BatchArgs a = base_args(algo, t);
+    if (algo.kind == kBuzhash)
+        hipLaunchKernelGGL(dev::scan_server_kernel<kBuzhash>, dim3(1), dim3(dev::kSrvWaves * dev::kWave), 0, sv.st, a,
+                           sv.d, sv.scratch, sv.seq - 1);
+    else
+        hipLaunchKernelGGL(dev::scan_server_kernel<kRabinKarp>, dim3(1), dim3(dev::kSrvWaves * dev::kWave), 0, sv.st, a,
+                           sv.d, sv.scratch, sv.seq - 1);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "scan server launch");
+    sv.launched = true;
+    return 0;
+}
+}  // namespace
+
+void set_scan_server_off(bool off) { g_srv_off = off; }
+
+int server_scan_first(const Algo& algo, const uint8_t* d_stage, uint64_t len, int64_t lo, int64_t hi, int device,
+                      int64_t* out) {
+    if (g_srv_off || device < 0 || device >= 64 || (algo.kind != kBuzhash && algo.kind != kRabinKarp)) return 1;
+    ScanServer& sv = g_srv[device][algo.kind == kBuzhash ? 0 : 1];
+    std::unique_lock<std::mutex> lk(sv.mu, std::try_to_lock);
+    if (!lk.owns_lock()) return 1;  // another handle holds the server: the caller launches its own scan
+    int err = 0;
+    const DeviceTables* t = device_tables(device, &err);
+    if (!t) return err;
+    if (!sv.init) {
+        if (hipStreamCreateWithFlags(&sv.st, hipStreamNonBlocking) != hipSuccess) return 1;
+        void* p = nullptr;
+        if (hipHostMalloc(&p, sizeof(dev::ServerMbox), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return 1;
+        sv.h = static_cast<dev::ServerMbox*>(p);
+        std::memset(sv.h, 0, sizeof(dev::ServerMbox));
+        void* pd = nullptr;
+        if (hipHostGetDevicePointer(&pd, p, 0) != hipSuccess) return 1;
+        sv.d = static_cast<dev::ServerMbox*>(pd);
+        sv.init = true;
+    }
+    if (len > sv.cap) {  // grow the scratch: the previous server must be gone first
+        if (sv.launched) {
+            if (hipStreamSynchronize(sv.st) != hipSuccess) return hip_fail(hipGetLastError(), "scan server sync");
+            sv.launched = false;
+        }
+        if (sv.scratch) (void)hipFree(sv.scratch);
+        sv.scratch = nullptr;
+        sv.cap = 0;
+        const uint64_t cap = std::max<uint64_t>((len + 255) & ~uint64_t(255), 4ull << 20);
+        if (hipMalloc(&sv.scratch, cap) != hipSuccess) return 1;
+        sv.cap = cap;
+    }
+    sv.h->src = reinterpret_cast<uint64_t>(d_stage);
+    sv.h->len = static_cast<int64_t>(len);
+    sv.h->lo = lo;
+    sv.h->hi = hi;
+    const uint64_t sq = ++sv.seq;
+    __atomic_store_n(&sv.h->req_seq, sq, __ATOMIC_RELEASE);
+    using clk = std::chrono::steady_clock;
+    const auto t_start = clk::now();
+    // A server that answered within the last millisecond is still polling (it idles out after
+    // 2 ms): skip the runtime query, which costs microseconds.  Otherwise ask the stream.
+    if (!sv.launched || (t_start - sv.last_answer > std::chrono::milliseconds(1) && hipStreamQuery(sv.st) == hipSuccess)) {
+        const int rc = srv_launch(sv, algo, *t);
+        if (rc) return rc;
+    }
+    // Wait for the answer.  A server that timed out before seeing this request has finished
+    // its kernel (hipStreamQuery succeeds) without serving it: launch a new one.
+    auto next_check = t_start + std::chrono::microseconds(200);
+    uint32_t spins = 0;
+    while (__atomic_load_n(&sv.h->done_seq, __ATOMIC_ACQUIRE) != sq) {
+        if (++spins % 64 == 0) {
+            const auto now = clk::now();
+            if (now < next_check) continue;
+            next_check = now + std::chrono::microseconds(200);
+            if (hipStreamQuery(sv.st) == hipSuccess && __atomic_load_n(&sv.h->done_seq, __ATOMIC_ACQUIRE) != sq) {
+                const int rc = srv_launch(sv, algo, *t);
+                if (rc) return rc;
+            }
+            if (now - t_start > std::chrono::seconds(10)) return set_error(-5, "scan server did not answer");
+        }
+    }
+    *out = __atomic_load_n(&sv.h->result, __ATOMIC_ACQUIRE);
+    sv.last_answer = clk::now();
+    return 0;
+}
+
 int launch_scan_first_batch(const Algo& algo, const uint8_t* d_base, const ScanReq* d_reqs, uint32_t n, int64_t* d_out,
                             int device, void* stream) {
     int err = 0;
@@ -4019,6 +4235,7 @@ extern "C" int kcdc_test_set(int32_t key, int64_t value) {
         case 2: g_test.no_steal = value != 0; return 0;                     // KCDC_TEST_NO_STEAL
         case 3: g_test.force_error = value != 0; return 0;                  // KCDC_TEST_FORCE_ERROR
         case 4: test_hash_lanes() = static_cast<int>(value); return 0;     // KCDC_TEST_HASH_LANES
+        case 5: set_scan_server_off(value != 0); return 0;                 // KCDC_TEST_NO_SERVER
         default: return set_error(-22, "unknown test knob");
     }
 }

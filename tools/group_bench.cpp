@@ -5,7 +5,9 @@
 // with the aggregate rate of both modes and whether every writer's cuts agree.
 //   g++ -O2 -std=c++17 -pthread -Iinclude tools/group_bench.cpp -Lkopia_amd -lkcdc \
 //       -Wl,-rpath,'$ORIGIN/../kopia_amd' -o build/group_bench
-//   build/group_bench [writers=16] [MiB per writer=64] [slice KiB=64] [name] [wait_us=50]
+//   build/group_bench [writers=16] [MiB per writer=64] [slice KiB=64] [name] [wait_us=50] [no_server=0]
+// no_server=1: private handles launch one scan per call (KCDC_TEST_NO_SERVER) instead of using
+// the resident scan server.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -47,6 +49,8 @@ int main(int argc, char** argv) {
     const size_t S = (argc > 3 ? std::strtoull(argv[3], nullptr, 10) : 64) << 10;
     const std::string name = argc > 4 ? argv[4] : "DYNAMIC-4M-BUZHASH";
     const uint32_t wait_us = argc > 5 ? static_cast<uint32_t>(std::atoi(argv[5])) : 50;
+    const int no_server = argc > 6 ? std::atoi(argv[6]) : 0;
+    kcdc_test_set(KCDC_TEST_NO_SERVER, no_server);
     if (kcdc_device_count() < 1) {
         std::fprintf(stderr, "no gfx950 device: %s\n", kcdc_last_error());
         return 1;
