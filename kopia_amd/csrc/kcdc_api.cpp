@@ -131,6 +131,7 @@ struct kcdc_splitter {
     uint8_t hist[kWindow] = {0};    // last 64 stream bytes (zeros before the start)
     uint8_t* h_stage = nullptr;     // pinned: hist || slice
     uint8_t* d_stage = nullptr;
+    uint8_t* d_scratch = nullptr;   // zero-copy: device memory the fallback scan copies the staging into
     size_t stage_cap = 0;
     int64_t* d_out = nullptr;
     int64_t* h_out = nullptr;
@@ -163,6 +164,7 @@ void destroy(kcdc_splitter* s) {
     DeviceGuard g(s->device);
     if (s->d_stage && !KCDC_HANDLE_ZC) (void)hipFree(s->d_stage);  // zero-copy: a mapping of h_stage
     if (s->h_stage) (void)hipHostFree(s->h_stage);
+    if (s->d_scratch) (void)hipFree(s->d_scratch);
     if (s->d_out && !KCDC_HANDLE_ZC) (void)hipFree(s->d_out);
     if (s->h_out) (void)hipHostFree(s->h_out);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -190,8 +192,10 @@ int ensure_stage(kcdc_splitter* s, size_t need) {
     cap = std::max(cap, need);
     if (s->d_stage && !KCDC_HANDLE_ZC) (void)hipFree(s->d_stage);
     if (s->h_stage) (void)hipHostFree(s->h_stage);
+    if (s->d_scratch) (void)hipFree(s->d_scratch);
     s->d_stage = nullptr;
     s->h_stage = nullptr;
+    s->d_scratch = nullptr;
     s->stage_cap = 0;
     if (KCDC_HANDLE_ZC) {
         // fine-grained: the resident scan server reads it between requests without a kernel
@@ -200,6 +204,7 @@ int ensure_stage(kcdc_splitter* s, size_t need) {
         void* pd = nullptr;
         HIP_TRY(hipHostGetDevicePointer(&pd, s->h_stage, 0), "stage mapping");
         s->d_stage = static_cast<uint8_t*>(pd);
+        HIP_TRY(hipMalloc(&s->d_scratch, cap), "hipMalloc scan scratch");
     } else {
         HIP_TRY(hipMalloc(&s->d_stage, cap), "hipMalloc stage");
         HIP_TRY(hipHostMalloc(&s->h_stage, cap, hipHostMallocDefault), "hipHostMalloc stage");
@@ -233,7 +238,7 @@ int64_t gpu_first_candidate(kcdc_splitter* s, const uint8_t* b, size_t n) {
     if (!KCDC_HANDLE_ZC)
         HIP_TRY(hipMemcpyAsync(s->d_stage, s->h_stage, total, hipMemcpyHostToDevice, s->stream), "H2D slice");
     rc = launch_scan_first(*s->algo, s->d_stage, total, kWindow, static_cast<int64_t>(total) - 1, s->d_out, s->device,
-                           s->stream);
+                           s->stream, s->d_scratch);
     if (rc) return rc;
     if (!KCDC_HANDLE_ZC)
         HIP_TRY(hipMemcpyAsync(s->h_out, s->d_out, sizeof(int64_t), hipMemcpyDeviceToHost, s->stream), "D2H result");
@@ -375,6 +380,7 @@ struct kcdc_group {
     struct Buf {
         uint8_t* h = nullptr;  // pinned staging
         uint8_t* d = nullptr;  // its device copy, or (KCDC_GROUP_ZC) its device mapping
+        uint8_t* scratch = nullptr;  // (KCDC_GROUP_ZC) device scratch the scan copies the staging into
         ScanReq* h_req = nullptr;
         ScanReq* d_req = nullptr;
         int64_t* h_out = nullptr;
@@ -405,6 +411,7 @@ void group_release(kcdc_group* g) {
         if (b.h) (void)hipHostFree(b.h);
         if (b.h_req) (void)hipHostFree(b.h_req);
         if (b.h_out) (void)hipHostFree(b.h_out);
+        if (b.scratch) (void)hipFree(b.scratch);
         if (!KCDC_GROUP_ZC) {  // device copies (zero-copy: mappings of the host buffers)
             if (b.d) (void)hipFree(b.d);
             if (b.d_req) (void)hipFree(b.d_req);
@@ -437,7 +444,7 @@ void group_loop(kcdc_group* g) {
         int rc = KCDC_OK;
         hipError_t e = hipSuccess;
         if (KCDC_GROUP_ZC) {  // the kernel reads the staging and writes the answers over PCIe
-            rc = launch_scan_first_batch(*g->algo, B.d, B.d_req, n, B.d_out, g->device, g->stream);
+            rc = launch_scan_first_batch(*g->algo, B.d, B.d_req, n, B.d_out, g->device, g->stream, B.scratch);
         } else {
             e = hipMemcpyAsync(B.d, B.h, used, hipMemcpyHostToDevice, g->stream);
             if (e == hipSuccess)
@@ -549,6 +556,7 @@ extern "C" kcdc_group* kcdc_group_new(const char* name, int device, uint32_t max
             b.d = static_cast<uint8_t*>(pd);
             b.d_req = static_cast<ScanReq*>(pr);
             b.d_out = static_cast<int64_t*>(po);
+            ok = ok && hipMalloc(&b.scratch, kcdc_group::kCap) == hipSuccess;
         } else if (ok) {
             ok = hipMalloc(&b.d, kcdc_group::kCap) == hipSuccess &&
                  hipMalloc(&b.d_req, g->max_batch * sizeof(ScanReq)) == hipSuccess &&

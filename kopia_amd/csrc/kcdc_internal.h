@@ -64,8 +64,10 @@ int launch_split_batch(const Algo& algo, const SplitArgs& a, int device, void* s
 // Single-region first-candidate scan used by the streaming handle:
 // bytes [0, len) of `d_buf` are the stream, positions < 0 are zero; returns via
 // d_out[0] the first candidate position in [lo, hi] or -1.
+// d_scratch (optional, device memory of at least len bytes): copy the bytes there first with
+// a whole workgroup, then scan them with 4 waves (for d_buf in mapped host memory).
 int launch_scan_first(const Algo& algo, const uint8_t* d_buf, uint64_t len, int64_t lo, int64_t hi, int64_t* d_out,
-                      int device, void* stream);
+                      int device, void* stream, uint8_t* d_scratch = nullptr);
 // The same scan through the device's resident scan server (no launch): 0 and *out = the
 // first candidate in [lo, hi] (or -1); 1 = the server is unavailable or busy (launch
 // instead); < 0 = error.  d_stage: fine-grained mapped host memory, 256-byte aligned.
@@ -80,7 +82,7 @@ struct ScanReq {
     int64_t len, lo, hi;
 };
 int launch_scan_first_batch(const Algo& algo, const uint8_t* d_base, const ScanReq* d_reqs, uint32_t n, int64_t* d_out,
-                            int device, void* stream);
+                            int device, void* stream, uint8_t* d_scratch = nullptr);  // scratch: as base's extent
 size_t long_workspace_bytes(const Algo& algo, uint64_t len);
 // Several long streams in one launch (segments of all streams scanned together, one
 // resolving wave per stream).

@@ -2833,6 +2833,9 @@ struct ServerMbox {
 };
 constexpr uint64_t kSrvIdle = 200000;     // 2 ms
 constexpr uint64_t kSrvLife = 20000000;   // 200 ms: every server kernel is bounded
+#ifndef KCDC_SRV_IN
+#define KCDC_SRV_IN 8  // 16-byte PCIe reads in flight per thread while copying a request's slice
+#endif
 constexpr int kSrvWaves = 8;  // 2 per SIMD: scan_region needs up to 219 VGPRs (1,024 threads spilled)
 
 template <int KIND>
@@ -2880,7 +2883,7 @@ __global__ __launch_bounds__(kSrvWaves * kWave) void scan_server_kernel(BatchArg
         // 8 loads in flight per thread (64 KiB per round over PCIe), then their stores: a
         // load-store loop left one 16-byte PCIe read per thread outstanding and cost ~2 us per 8 KiB
         const int64_t n16 = len >> 4;
-        constexpr int kIn = 8;
+        constexpr int kIn = KCDC_SRV_IN;
         constexpr int64_t kT = kSrvWaves * kWave;
         const u32x4* s16 = reinterpret_cast<const u32x4*>(src);
         u32x4* d16 = reinterpret_cast<u32x4*>(scratch);
@@ -2924,6 +2927,74 @@ __global__ __launch_bounds__(kSrvWaves * kWave) void scan_server_kernel(BatchArg
         last = wall_clock64();
         __syncthreads();
     }
+}
+
+// Copy-then-scan form of the scans above, one 8-wave workgroup per request: the request's
+// bytes (mapped host staging) are copied into device scratch with 8 16-byte PCIe reads in
+// flight per thread, then 8 waves scan 8 sub-ranges of [lo, hi].  One wave reading 64 KiB of
+// host memory itself was PCIe-latency bound (41 us per private scan, 54 us per group launch).
+constexpr int kCpWaves = 8;  // 64 KiB of PCIe reads in flight; 2 waves per SIMD (scan_region <= 235 VGPRs)
+template <int KIND>
+__device__ __forceinline__ int64_t scan_request_cp(HashSmem<KIND>& sm, const BatchArgs& a, const uint8_t* src,
+                                                   uint8_t* scr, int64_t len, int64_t lo, int64_t hi) {
+    __shared__ int64_t wf[kCpWaves];
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    constexpr int kIn = 8;
+    constexpr int64_t kT = kCpWaves * kWave;
+    const int64_t n16 = len >> 4;
+    const u32x4* s16 = reinterpret_cast<const u32x4*>(src);
+    u32x4* d16 = reinterpret_cast<u32x4*>(scr);
+    for (int64_t b = 0; b < n16; b += kIn * kT) {
+        u32x4 v[kIn];
+#pragma unroll
+        for (int k = 0; k < kIn; k++) {
+            const int64_t i = b + k * kT + threadIdx.x;
+            if (i < n16) v[k] = __builtin_nontemporal_load(s16 + i);
+        }
+#pragma unroll
+        for (int k = 0; k < kIn; k++) {
+            const int64_t i = b + k * kT + threadIdx.x;
+            if (i < n16) d16[i] = v[k];
+        }
+    }
+    for (int64_t i = (n16 << 4) + threadIdx.x; i < len; i += kT) scr[i] = src[i];
+    __syncthreads();
+    asm volatile("buffer_inv sc0" ::: "memory");  // this CU's L1 may hold an earlier request's lines
+    const auto hash = make_hash<KIND>(sm, a, lane);
+    const int64_t span = hi - lo + 1, per = ((span + kCpWaves - 1) / kCpWaves + 63) & ~int64_t(63);
+    const int64_t mlo = lo + per * w, mhi = mlo + per - 1 < hi ? mlo + per - 1 : hi;
+    const int64_t f = mlo <= mhi ? scan_region(hash, scr, 0, len, mlo, mhi, lane) : -1;
+    if (lane == 0) wf[w] = f;
+    __syncthreads();
+    int64_t best = -1;
+    for (int k = 0; k < kCpWaves; k++)
+        if (wf[k] >= 0 && (best < 0 || wf[k] < best)) best = wf[k];
+    return best;
+}
+
+template <int KIND>
+__global__ __launch_bounds__(kCpWaves * kWave) void scan_first_cp_kernel(BatchArgs a, const uint8_t* buf, int64_t len,
+                                                                         int64_t lo, int64_t hi, int64_t* out,
+                                                                         uint8_t* scratch) {
+    __shared__ HashSmem<KIND> sm;
+    fill_tables<KIND>(sm, a);
+    const int64_t f = scan_request_cp<KIND>(sm, a, buf, scratch, len, lo, hi);
+    if (threadIdx.x == 0) out[0] = f;
+}
+
+template <int KIND>
+__global__ __launch_bounds__(kCpWaves * kWave) void scan_first_batch_cp_kernel(BatchArgs a, const uint8_t* base,
+                                                                               const ScanReq* reqs, int64_t* out,
+                                                                               uint8_t* scratch) {
+    __shared__ HashSmem<KIND> sm;
+    fill_tables<KIND>(sm, a);
+    const ScanReq& r = reqs[blockIdx.x];
+    const uint64_t off = uni64(r.off);
+    const int64_t len = static_cast<int64_t>(uni64(static_cast<uint64_t>(r.len)));
+    const int64_t lo = static_cast<int64_t>(uni64(static_cast<uint64_t>(r.lo)));
+    const int64_t hi = static_cast<int64_t>(uni64(static_cast<uint64_t>(r.hi)));
+    const int64_t f = scan_request_cp<KIND>(sm, a, base + off, scratch + off, len, lo, hi);
+    if (threadIdx.x == 0) out[blockIdx.x] = f;
 }
 
 // ------------------------------------------------------ synthetic streams
@@ -3918,12 +3989,22 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
 }
 
 int launch_scan_first(const Algo& algo, const uint8_t* d_buf, uint64_t len, int64_t lo, int64_t hi, int64_t* d_out,
-                      int device, void* stream) {
+                      int device, void* stream, uint8_t* d_scratch) {
     int err = 0;
     const DeviceTables* t = device_tables(device, &err);
     if (!t) return err;
     dev::BatchArgs a = base_args(algo, *t);
     hipStream_t st = static_cast<hipStream_t>(stream);
+    if (d_scratch && (algo.kind == kBuzhash || algo.kind == kRabinKarp)) {
+        if (algo.kind == kBuzhash)
+            hipLaunchKernelGGL(dev::scan_first_cp_kernel<kBuzhash>, dim3(1), dim3(dev::kCpWaves * dev::kWave), 0, st, a,
+                               d_buf, static_cast<int64_t>(len), lo, hi, d_out, d_scratch);
+        else
+            hipLaunchKernelGGL(dev::scan_first_cp_kernel<kRabinKarp>, dim3(1), dim3(dev::kCpWaves * dev::kWave), 0, st,
+                               a, d_buf, static_cast<int64_t>(len), lo, hi, d_out, d_scratch);
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : hip_fail(e, "scan kernel launch");
+    }
     if (algo.kind == kBuzhash)
         hipLaunchKernelGGL(dev::scan_first_kernel<kBuzhash>, dim3(1), dim3(dev::kWave), 0, st, a, d_buf,
                            static_cast<int64_t>(len), lo, hi, d_out);
@@ -4039,13 +4120,23 @@ int server_scan_first(const Algo& algo, const uint8_t* d_stage, uint64_t len, in
 }
 
 int launch_scan_first_batch(const Algo& algo, const uint8_t* d_base, const ScanReq* d_reqs, uint32_t n, int64_t* d_out,
-                            int device, void* stream) {
+                            int device, void* stream, uint8_t* d_scratch) {
     int err = 0;
     const DeviceTables* t = device_tables(device, &err);
     if (!t) return err;
     if (n == 0) return 0;
     dev::BatchArgs a = base_args(algo, *t);
     hipStream_t st = static_cast<hipStream_t>(stream);
+    if (d_scratch && (algo.kind == kBuzhash || algo.kind == kRabinKarp)) {
+        if (algo.kind == kBuzhash)
+            hipLaunchKernelGGL(dev::scan_first_batch_cp_kernel<kBuzhash>, dim3(n), dim3(dev::kCpWaves * dev::kWave), 0,
+                               st, a, d_base, d_reqs, d_out, d_scratch);
+        else
+            hipLaunchKernelGGL(dev::scan_first_batch_cp_kernel<kRabinKarp>, dim3(n), dim3(dev::kCpWaves * dev::kWave), 0,
+                               st, a, d_base, d_reqs, d_out, d_scratch);
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : hip_fail(e, "scan kernel launch");
+    }
     if (algo.kind == kBuzhash)
         hipLaunchKernelGGL(dev::scan_first_batch_kernel<kBuzhash>, dim3(n), dim3(dev::kWave), 0, st, a, d_base, d_reqs,
                            d_out);
