@@ -288,6 +288,9 @@ int kcdc_test_occupy(uint32_t nwg, uint32_t usec, void* hip_stream);
 #define KCDC_TEST_STAT_DONE 2
 #define KCDC_TEST_STAT_STEALS 3
 int64_t kcdc_test_queue_stat(int32_t key);
+/* Requests the resident scan server has answered in this process (private streaming handles use
+ * it while exactly one private handle is open). */
+int64_t kcdc_test_server_requests(void);
 
 #ifdef __cplusplus
 }

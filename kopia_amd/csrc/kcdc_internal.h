@@ -74,6 +74,7 @@ int launch_scan_first(const Algo& algo, const uint8_t* d_buf, uint64_t len, int6
 int server_scan_first(const Algo& algo, const uint8_t* d_stage, uint64_t len, int64_t lo, int64_t hi, int device,
                       int64_t* out);
 void set_scan_server_off(bool off);
+uint64_t scan_server_requests();
 int launch_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint32_t nstreams, uint64_t seed,
                      uint64_t first_sid, void* stream);
 // Grouped streaming handles: request r scans [lo, hi] of the `len` bytes at base + off.

@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstring>
 #include <mutex>
@@ -4033,6 +4034,7 @@ struct ScanServer {
 };
 ScanServer g_srv[64][2];
 bool g_srv_off = false;  // kcdc_test_set(KCDC_TEST_NO_SERVER)
+std::atomic<uint64_t> g_srv_served{0};  // requests answered by a server (kcdc_test_server_requests)
 
 int srv_launch(ScanServer& sv, const Algo& algo, const DeviceTables& t) {
     dev::BatchArgs a = base_args(algo, t);
@@ -4050,6 +4052,7 @@ int srv_launch(ScanServer& sv, const Algo& algo, const DeviceTables& t) {
 }  // namespace
 
 void set_scan_server_off(bool off) { g_srv_off = off; }
+uint64_t scan_server_requests() { return g_srv_served.load(std::memory_order_relaxed); }
 
 int server_scan_first(const Algo& algo, const uint8_t* d_stage, uint64_t len, int64_t lo, int64_t hi, int device,
                       int64_t* out) {
@@ -4116,6 +4119,7 @@ int server_scan_first(const Algo& algo, const uint8_t* d_stage, uint64_t len, in
     }
     *out = __atomic_load_n(&sv.h->result, __ATOMIC_ACQUIRE);
     sv.last_answer = clk::now();
+    g_srv_served.fetch_add(1, std::memory_order_relaxed);
     return 0;
 }
 
@@ -4320,6 +4324,8 @@ int launch_split_long(const Algo& algo, const uint8_t* d_data, uint64_t len, uin
 }
 
 // ------------------------------------------------------------------ testing
+extern "C" int64_t kcdc_test_server_requests(void) { return static_cast<int64_t>(scan_server_requests()); }
+
 extern "C" int kcdc_test_set(int32_t key, int64_t value) {
     switch (key) {
         case 1: g_test.spin_cap = static_cast<uint32_t>(value); return 0;   // KCDC_TEST_SPIN_CAP

@@ -49,7 +49,10 @@ def test_server_on_off_oracle(gpu, server, name):
     want = coracle.split_stream(name, np.frombuffer(data, np.uint8)).tolist()
     for off in (0, 1):
         server.kcdc_test_set(_lib.TEST_NO_SERVER, off)
+        before = server.kcdc_test_server_requests()
         assert _feed(name, data, [64 << 10, 1000, 300000, 7]) == want, ("no_server", off)
+        served = server.kcdc_test_server_requests() - before
+        assert (served > 0) if off == 0 else (served == 0), (off, served)  # the path under test ran
 
 
 def test_server_idle_relaunch(gpu, server):
@@ -73,6 +76,7 @@ def test_server_idle_relaunch(gpu, server):
     if not cuts or cuts[-1] != len(data):
         cuts.append(len(data))
     assert cuts == want
+    assert server.kcdc_test_server_requests() > 0
 
 
 def test_server_scratch_growth(gpu, server):
@@ -85,8 +89,9 @@ def test_server_scratch_growth(gpu, server):
 
 
 def test_server_concurrent_handles(gpu, server):
-    """Eight writers with private handles at once: whoever finds the server busy launches its
-    own scan; every writer's cuts equal the oracle's."""
+    """Eight writers with private handles at once: with more than one private handle open the
+    scans are launched side by side instead of queueing on the one-workgroup server; every
+    writer's cuts equal the oracle's."""
     name = "DYNAMIC-1M-BUZHASH"
     streams = [coracle.gen_stream(SEED, 20 + w, 12 << 20).tobytes() for w in range(8)]
     wants = [coracle.split_stream(name, np.frombuffer(d, np.uint8)).tolist() for d in streams]
