@@ -333,11 +333,20 @@ __global__ __launch_bounds__(256) void blake2_chunks_x4_kernel(const uint8_t* da
             if (q == 1) d ^= static_cast<W>(t >> 32);
         }
         if (q == 2 && last) d = ~d;
+        // the message words of round r + 1 are read from LDS during round r: the chain never
+        // waits for them (4 LDS reads per round were on the critical path)
+        W mx = mword(sidx[0] & 15u), my = mword((sidx[0] >> 4) & 15u);
+        W dx = mword((sidx[0] >> 8) & 15u), dy = mword(sidx[0] >> 12);
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            const uint32_t si = sidx[r];
-            const W mx = mword(si & 15u), my = mword((si >> 4) & 15u);
-            const W dx = mword((si >> 8) & 15u), dy = mword(si >> 12);
+            W nmx = mx, nmy = my, ndx = dx, ndy = dy;
+            if (r + 1 < R) {
+                const uint32_t sn = sidx[r + 1];
+                nmx = mword(sn & 15u);
+                nmy = mword((sn >> 4) & 15u);
+                ndx = mword((sn >> 8) & 15u);
+                ndy = mword(sn >> 12);
+            }
             g(a, b, cc, d, mx, my);
             b = qperm<kQRot1>(b);
             cc = qperm<kQRot2>(cc);
@@ -346,6 +355,10 @@ __global__ __launch_bounds__(256) void blake2_chunks_x4_kernel(const uint8_t* da
             b = qperm<kQRot3>(b);
             cc = qperm<kQRot2>(cc);
             d = qperm<kQRot1>(d);
+            mx = nmx;
+            my = nmy;
+            dx = ndx;
+            dy = ndy;
         }
         h0 ^= a ^ cc;
         h1 ^= b ^ d;
