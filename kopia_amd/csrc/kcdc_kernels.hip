@@ -3216,7 +3216,11 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void cand_scan_rk
             __builtin_amdgcn_sched_barrier(0);
             rk_warm(kx, dw, ha, la, hb, lb, pa, pb);
         }
-        uint32_t fa[kSegK], fb[kSegK];
+        // candidates per chain, two per register: 16-bit offsets from the chain's start (a lane
+        // covers at most 2 KiB of a 128 KiB segment tile); halves state live across the walk
+        uint32_t fa[kSegK / 2], fb[kSegK / 2];
+#pragma unroll
+        for (int k = 0; k < kSegK / 2; k++) fa[k] = fb[k] = 0;
         int na = 0, nb = 0;  // candidates per chain (kSegK + 1: more than kSegK)
         auto refill = [&](int f) {
             if (f < 2 * t.K)
@@ -3227,7 +3231,8 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void cand_scan_rk
         auto check = [&](uint32_t mm, int chain, int64_t c, uint32_t h0, uint32_t l0, const uint32_t (&in)[16],
                          const uint32_t (&prv)[16]) {
             int& nf = chain ? nb : na;
-            uint32_t(&fnd)[kSegK] = chain ? fb : fa;
+            uint32_t(&fnd)[kSegK / 2] = chain ? fb : fa;
+            const int64_t cstart = chain ? c0b : c0;
             if (mm == 0 && c <= q.hi && nf <= kSegK) {  // rare: enumerate the piece's candidates exactly
                 const int64_t blo = q.lo - c, bhi = q.hi - c;
                 int from = blo < 0 ? 0 : static_cast<int>(blo);
@@ -3235,9 +3240,10 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void cand_scan_rk
                 while (from <= to && nf <= kSegK) {
                     const uint32_t idx = rk_exact64(kx, h0, l0, in, prv, from, to);
                     if (idx >= 64u) break;
+                    const uint32_t rel = static_cast<uint32_t>(c - cstart) + idx;  // < 2^16
 #pragma unroll
-                    for (int k = 0; k < kSegK; k++)  // fnd[nf] = ..., kept in registers (no scratch)
-                        if (k == nf) fnd[k] = static_cast<uint32_t>(c - q.cs) + idx;
+                    for (int k = 0; k < kSegK; k++)  // entry nf = rel, kept in registers (no scratch)
+                        if (k == nf) fnd[k >> 1] |= rel << (16 * (k & 1));
                     nf++;
                     from = static_cast<int>(idx) + 1;
                 }
@@ -3247,13 +3253,14 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void cand_scan_rk
         // this lane's candidates in position order: chain A's, then chain B's
         const int nas = na < kSegK ? na : kSegK;
         const int nf = na + nb > kSegK ? kSegK + 1 : na + nb;
-        uint32_t found[kSegK];
+        uint32_t found[kSegK];  // offsets from the segment start
+        const uint32_t base_a = static_cast<uint32_t>(c0 - q.cs), base_b = static_cast<uint32_t>(c0b - q.cs);
 #pragma unroll
         for (int j = 0; j < kSegK; j++) {
-            uint32_t v = fa[j];
+            uint32_t v = base_a + ((fa[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
 #pragma unroll
             for (int k = 0; k < kSegK; k++)
-                if (j >= nas && k == j - nas) v = fb[k];
+                if (j >= nas && k == j - nas) v = base_b + ((fb[k >> 1] >> (16 * (k & 1))) & 0xFFFFu);
             found[j] = v;
         }
         int incl = nf;
