@@ -47,7 +47,24 @@ constexpr uint64_t kIV64[8] = {0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull, 0x3
 constexpr uint32_t kIV32[8] = {0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u, 0xA54FF53Au,
                                0x510E527Fu, 0x9B05688Cu, 0x1F83D9ABu, 0x5BE0CD19u};
 
-__device__ __forceinline__ uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotate right by a constant on the two 32-bit halves: two independent v_alignbit (a
+// rotate by 32 is a register swap); the shift-or form compiled to ~5 dependent instructions.
+template <int N>
+__device__ __forceinline__ uint64_t rotr64(uint64_t x) {
+    const uint32_t lo = static_cast<uint32_t>(x), hi = static_cast<uint32_t>(x >> 32);
+    uint32_t nlo, nhi;
+    if constexpr (N == 32) {
+        nlo = hi;
+        nhi = lo;
+    } else if constexpr (N < 32) {
+        nlo = __builtin_amdgcn_alignbit(hi, lo, N);
+        nhi = __builtin_amdgcn_alignbit(lo, hi, N);
+    } else {
+        nlo = __builtin_amdgcn_alignbit(lo, hi, N - 32);
+        nhi = __builtin_amdgcn_alignbit(hi, lo, N - 32);
+    }
+    return (static_cast<uint64_t>(nhi) << 32) | nlo;
+}
 __device__ __forceinline__ uint32_t rotr32(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
 
 // Words [0, nw) of the block at p (take valid bytes, the rest zero), from 4-byte-aligned
@@ -84,13 +101,13 @@ __device__ __forceinline__ void load_block(const uint8_t* p, uint32_t take, uint
 // ------------------------------------------------------------------ BLAKE2b
 __device__ __forceinline__ void g64(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, uint64_t x, uint64_t y) {
     a = a + b + x;
-    d = rotr64(d ^ a, 32);
+    d = rotr64<32>(d ^ a);
     c = c + d;
-    b = rotr64(b ^ c, 24);
+    b = rotr64<24>(b ^ c);
     a = a + b + y;
-    d = rotr64(d ^ a, 16);
+    d = rotr64<16>(d ^ a);
     c = c + d;
-    b = rotr64(b ^ c, 63);
+    b = rotr64<63>(b ^ c);
 }
 
 __device__ __forceinline__ void compress64(uint64_t (&h)[8], const uint32_t (&mw)[32], uint64_t t, bool last) {
