@@ -234,3 +234,41 @@ def test_errors(gpu):
     assert call(32, 0, 1 << 20) == _lib.KCDC_EINVAL   # empty content ID
     assert call(32, 65, 1 << 20) == _lib.KCDC_EINVAL  # content ID > 64 bytes
     assert ke.overhead(ALG) == 28
+
+
+def test_large_chunk_power_table(gpu):
+    """An 80 MiB chunk: 5.2 M Poly1305 blocks, so the unit exponents reach the table's top level
+    (r^(2^20 d)); sealed bytes and tag equal the oracle's, and the device opens it."""
+    import torch
+    n = 80 << 20
+    host = coracle.gen_stream(SEED, 40, n + 3)
+    iv = bytes(range(200, 216))
+    nonce = bytes(range(12))
+    enc = ke.Encryptor(ALG, MASTER)
+    out, oo, st = _seal(enc, host, [3], [n], [iv], nonce, gpu)
+    assert st.tolist() == [0]
+    want = aead.kopia_encrypt(aead.derive_key(MASTER), iv, nonce, host[3:3 + n].tobytes())
+    assert out[:n + 28].tobytes() == want
+    plain, po, st2 = _open(enc, out[:n + 28], [0], [n + 28], [iv], gpu)
+    assert st2.tolist() == [0] and plain[:n].tobytes() == host[3:3 + n].tobytes()
+    del torch
+
+
+def test_too_long_chunk_and_empty_call(gpu):
+    """A chunk of 1 GiB + 1 byte reports KCDC_EFBIG (exponents stay below 2^26) while its
+    neighbour seals normally; an empty call does nothing."""
+    import torch
+    enc = ke.Encryptor(ALG, MASTER)
+    big = (1 << 30) + 1
+    d = torch.zeros(big + 64, dtype=torch.uint8, device=gpu)
+    ids = torch.zeros((2, 16), dtype=torch.uint8, device=gpu)
+    lens = np.array([big, 100], np.int64)
+    oo = np.array([0, 256], np.int64)
+    out = torch.zeros(512, dtype=torch.uint8, device=gpu)
+    st = enc.encrypt_chunks_device(d.data_ptr(), [0, 64], lens, ids, 16, out, oo, gpu, nonces=bytes(24))
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [_lib.KCDC_EFBIG, 0]
+    want = aead.kopia_encrypt(aead.derive_key(MASTER), bytes(16), bytes(12), bytes(100))
+    assert out.cpu().numpy()[256:256 + 128].tobytes() == want
+    st0 = enc.encrypt_chunks_device(d.data_ptr(), [], [], ids, 16, out, [], gpu)
+    assert st0.numel() == 0
