@@ -91,3 +91,19 @@ def test_errors(gpu):
         kh.hash_chunks_device("BLAKE2S-128", d.data_ptr(), [0], [10], b"", dev)
     with pytest.raises(_lib.KcdcError):
         kh.hash_chunks_device("SHA256", d.data_ptr(), [0], [10], b"k", dev)
+
+
+@pytest.mark.parametrize("name", ["BLAKE2B-256-128", "BLAKE2S-256"])
+def test_large_chunks(gpu, name, lanes):
+    """Chunks of 64 MiB to 256 MiB + 5 at odd offsets (block counters past 2^21 blocks,
+    unaligned tails) through both kernels, against hashlib."""
+    import torch
+    sizes = [64 << 20, (128 << 20) + 1, (256 << 20) + 5]
+    offs = np.array([3, 3 + sizes[0] + 7, 3 + sizes[0] + 7 + sizes[1] + 1], dtype=np.int64)
+    total = int(offs[-1] + sizes[-1] + 16)
+    host = coracle.gen_stream(SEED, 41, total)
+    key = bytes(range(7, 39))
+    got = _hash_all(name, key, host, offs, np.array(sizes, np.int64))
+    for i, L in enumerate(sizes):
+        assert got[i].tobytes() == kopia_hash(name, key, host[offs[i]:offs[i] + L].tobytes()), (name, L)
+    del torch
