@@ -685,6 +685,10 @@ struct BatchArgs {
     // "candidate" becomes h <= buz_lim (= ~mask): the hot loop's test is a bare v_min3.
     uint32_t buz_rot;
     uint32_t buz_lim;  // ~mask when mask is a top-bits mask (else unused)
+    // Batch tiles: bytes per lane segment at most (a tile is 64 of them, ~avg/4): the scan of
+    // a chunk's region stops at the tile holding its first candidate, and a tile of avg bytes
+    // overshoots by ~58 % on average (exponential candidate gaps), one of avg/4 by ~13 %.
+    uint32_t lane_cap;
 };
 
 // End of stream sid's cut range (exclusive).
@@ -941,12 +945,12 @@ struct TileGeom {
     Loader ld;
 };
 __device__ __forceinline__ TileGeom tile_geom(int64_t ct, int64_t hi, const uint8_t* abase, int64_t off0,
-                                              int64_t nbytes_coord) {
+                                              int64_t nbytes_coord, int64_t lane_cap = kLaneMax) {
     const int64_t rem = hi - ct + 1;
     int64_t per = (rem + kWave - 1) / kWave;
     per = (per + 127) & ~int64_t(127);
     TileGeom g;
-    g.L = per < kLaneMax ? per : kLaneMax;
+    g.L = per < lane_cap ? per : lane_cap;
     g.nb = static_cast<int>(g.L / 128);
     g.ld = make_loader(abase, off0, nbytes_coord, ct >= 64 ? ct - 64 : 0);
     return g;
@@ -1410,8 +1414,9 @@ __device__ __forceinline__ uint64_t probe_poll(const BatchArgs& a, int lane, uin
     return lane == 0 ? ld_agent64(probe_word(a, sid)) : 0ull;
 }
 
-__device__ __forceinline__ void ptile_issue(const PStream& st, int64_t hi, uint32_t wl, uint32_t sl, int lane) {
-    const TileGeom g = tile_geom(st.ct, hi, st.abase, st.off0, st.off0 + st.n);
+__device__ __forceinline__ void ptile_issue(const PStream& st, int64_t hi, uint32_t wl, uint32_t sl, int lane,
+                                            int64_t lane_cap) {
+    const TileGeom g = tile_geom(st.ct, hi, st.abase, st.off0, st.off0 + st.n, lane_cap);
     dma_piece(g.ld, g.ld.tb, wl, st.ct, g.L, -1, lane);
     dma_step128(g.ld, g.ld.tb, sl, st.ct, g.L, 0, lane);
 }
@@ -1538,7 +1543,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         if (!pcheck(a, lane, cur, 0xFFFFFFFFu, 5)) return;
         int64_t lo, hi;
         pregion(a, cur, lo, hi);
-        const TileGeom g = tile_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n);
+        const TileGeom g = tile_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n, a.lane_cap);
         const int64_t ct = cur.ct, ct_next = ct + kWave * g.L;
         const bool last_of_region = ct_next > hi;
         const bool budget_out = budget - kWave * g.L <= 0;
@@ -1571,7 +1576,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         }
         uint64_t qc_raw = 0;
         if (may_split && lane == 0) qc_raw = ld_agent64(reinterpret_cast<uint64_t*>(a.queue + kQHT));
-        if (!issued) ptile_issue(cur, hi, wl32, sl32, lane);
+        if (!issued) ptile_issue(cur, hi, wl32, sl32, lane, a.lane_cap);
         const int64_t c0 = ct + lane * g.L;
         uint32_t ht_lo = static_cast<uint32_t>(ht_raw), ht_hi = static_cast<uint32_t>(ht_raw >> 32);
         uint32_t qc_lo = static_cast<uint32_t>(qc_raw), qc_hi = static_cast<uint32_t>(qc_raw >> 32);
@@ -1639,7 +1644,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                 if (!last_of_region) {
                     PStream t2 = cur;
                     t2.ct = ct_next;
-                    ptile_issue(t2, hi, wl32, sl32, lane);
+                    ptile_issue(t2, hi, wl32, sl32, lane, a.lane_cap);
                     next_issued = true;
                 }
             }
@@ -1809,7 +1814,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                     int64_t nlo, nhi;
                     pregion(a, nx, nlo, nhi);
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // entry read before the slot refill
-                    ptile_issue(nx, nhi, wl32, sl32, lane);
+                    ptile_issue(nx, nhi, wl32, sl32, lane, a.lane_cap);
                     nstate = 3;
                 }
             }
@@ -3803,6 +3808,11 @@ dev::BatchArgs base_args(const Algo& algo, const DeviceTables& t) {
     a.rk_out = t.rk_out;
     a.rk_mod = t.rk_mod;
     a.rk_shift = static_cast<uint32_t>(tables().rk_shift);
+    // largest power of two <= avg / 256, within [256, kLaneMax]: tiles of ~avg/4 (1 MiB and
+    // larger averages keep the full 2 KiB lane segments)
+    uint64_t cap = dev::kLaneMax;
+    while (cap > 256 && cap * 256 > algo.avg) cap >>= 1;
+    a.lane_cap = static_cast<uint32_t>(cap);
     return a;
 }
 #if KCDC_TRACE || KCDC_DEBUG_CHECKS
