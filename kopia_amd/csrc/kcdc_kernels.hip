@@ -67,6 +67,9 @@ constexpr int kNdw = kBlk / 4;          // dwords per lane per step
 #define KCDC_LANE_MAX 2048
 #endif
 constexpr int64_t kLaneMax = KCDC_LANE_MAX;  // max bytes per lane segment (tile = 64 x kLaneMax)
+#ifndef KCDC_TILE_DIV
+#define KCDC_TILE_DIV 256  // batch lane segments <= avg / KCDC_TILE_DIV (tiles ~ 64 avg / DIV), >= 256 B
+#endif
 #ifndef KCDC_BATCH_WAVES
 #define KCDC_BATCH_WAVES 8
 #endif
@@ -2071,12 +2074,12 @@ struct RkGeom {
     Loader ld;
 };
 __device__ __forceinline__ RkGeom rk_geom(int64_t ct, int64_t hi, const uint8_t* abase, int64_t off0,
-                                          int64_t nbytes_coord) {
+                                          int64_t nbytes_coord, int64_t lane_cap = kLaneMax) {
     const int64_t rem = hi - ct + 1;
     int64_t per = (rem + kWave - 1) / kWave;
     per = (per + 255) & ~int64_t(255);
     RkGeom g;
-    g.L = per < kLaneMax ? per : kLaneMax;
+    g.L = per < lane_cap ? per : lane_cap;  // lane_cap: a multiple of 256
     g.K = static_cast<int>(g.L / 256);
     g.ld = make_loader(abase, off0, nbytes_coord, ct >= 64 ? ct - 64 : 0);
     return g;
@@ -2533,7 +2536,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
 #if KCDC_RK_CHAINS == 4
         const Rk4Geom g = rk4_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n);
 #else
-        const RkGeom g = rk_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n);
+        const RkGeom g = rk_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n, a.lane_cap);
 #endif
         const int64_t ct = cur.ct, ct_next = ct + kWave * g.L;
         const bool last_of_region = ct_next > hi;
@@ -2595,7 +2598,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                 const Rk4Geom gn = rk4_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n);
                 rk4_dma_warm(gn.ld, sl32, ct_next, gn.L, 0, rk4_lane(gn.L, lane));
 #else
-                const RkGeom gn = rk_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n);
+                const RkGeom gn = rk_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n, a.lane_cap);
                 rk_dma_warm(gn.ld, sl32, ct_next, gn.L, lane);
 #endif
                 next_issued = true;
@@ -3811,7 +3814,7 @@ dev::BatchArgs base_args(const Algo& algo, const DeviceTables& t) {
     // largest power of two <= avg / 256, within [256, kLaneMax]: tiles of ~avg/4 (1 MiB and
     // larger averages keep the full 2 KiB lane segments)
     uint64_t cap = dev::kLaneMax;
-    while (cap > 256 && cap * 256 > algo.avg) cap >>= 1;
+    while (cap > 256 && cap * KCDC_TILE_DIV > algo.avg) cap >>= 1;
     a.lane_cap = static_cast<uint32_t>(cap);
     return a;
 }
