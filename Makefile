@@ -5,7 +5,7 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
 CSRC := kopia_amd/csrc
 OBJ := build/obj
-SRCS := $(CSRC)/kcdc_kernels.hip $(CSRC)/kcdc_hash.hip $(CSRC)/kcdc_crypt.hip $(CSRC)/kcdc_api.cpp $(CSRC)/kcdc_tables.cpp $(CSRC)/kcdc_registry.cpp
+SRCS := $(CSRC)/kcdc_kernels.hip $(CSRC)/kcdc_hash.hip $(CSRC)/kcdc_crypt.hip $(CSRC)/kcdc_compress.hip $(CSRC)/kcdc_api.cpp $(CSRC)/kcdc_tables.cpp $(CSRC)/kcdc_registry.cpp
 OBJS := $(patsubst $(CSRC)/%,$(OBJ)/%.o,$(SRCS))
 LIB := kopia_amd/libkcdc.so
 
@@ -56,6 +56,6 @@ variants:
 	@for v in $(VARIANTS); do \
 	  n=$${v%%:*}; f=$$(echo $${v#*:} | tr ',' ' '); \
 	  echo "variant $$n: $$f"; \
-	  $(HIPCC) $(HIPFLAGS) $$f -shared -o build/variants/libkcdc_$$n.so $(CSRC)/kcdc_kernels.hip $(CSRC)/kcdc_hash.hip $(CSRC)/kcdc_crypt.hip -x hip $(CSRC)/kcdc_api.cpp $(CSRC)/kcdc_tables.cpp $(CSRC)/kcdc_registry.cpp || exit 1; \
+	  $(HIPCC) $(HIPFLAGS) $$f -shared -o build/variants/libkcdc_$$n.so $(CSRC)/kcdc_kernels.hip $(CSRC)/kcdc_hash.hip $(CSRC)/kcdc_crypt.hip $(CSRC)/kcdc_compress.hip -x hip $(CSRC)/kcdc_api.cpp $(CSRC)/kcdc_tables.cpp $(CSRC)/kcdc_registry.cpp || exit 1; \
 	done
 .PHONY: variants

@@ -259,6 +259,32 @@ int kcdc_decrypt_chunks_device(const char* algorithm, const uint8_t* secret, uin
                                const uint64_t* d_out_offsets, int32_t* d_status, void* d_work, uint64_t work_bytes,
                                void* hip_stream);
 
+/* ------------------------------------------------------------- content compression
+ * Kopia's deflate compressors (repo/compression/compressor_deflate.go:14-62 Compress; header IDs
+ * compression_ids.go:28-30) for many chunks per call, with the content manager's keep-or-drop
+ * rule (maybeCompressAndEncryptDataForPacking, repo/content/content_manager_lock_free.go:42-73):
+ *   out_i = BE32(header ID) || raw DEFLATE stream (RFC 1951) of chunk i
+ *   id_i  = header ID if len(out_i) < len(chunk i), else 0 (NoCompression: store chunk i as is)
+ * Any RFC 1951 inflater (flate.NewReader in Decompress, compressor_deflate.go:64-78) reads out_i
+ * after its 4 header bytes; the bytes are this encoder's, not klauspost/compress's.
+ * kcdc_compression_algorithms: the names encoded on the device; kcdc_compression_header_id: a
+ *   name's header ID (or a negative error).
+ * kcdc_compress_bound(len): the largest out_i for a chunk of len bytes (6 + len + 5 per 512 bytes).
+ * kcdc_compress_workspace_size(total, n): device scratch for n chunks of `total` bytes in all
+ *   (~1.13 bytes per input byte).
+ * kcdc_compress_chunks_device: chunk i = [d_offsets[i], +d_lens[i]) of d_data (any alignment);
+ *   out_i goes to d_out + d_out_offsets[i] (room for kcdc_compress_bound bytes), its length to
+ *   d_out_lens[i] and id_i to d_header_ids[i].  A workspace too small for the chunks' spans
+ *   leaves every d_out_lens[i] = 0.  Asynchronous on hip_stream. */
+int kcdc_compression_algorithms(const char** names, int cap);
+int64_t kcdc_compression_header_id(const char* algorithm);
+uint64_t kcdc_compress_bound(uint64_t len);
+uint64_t kcdc_compress_workspace_size(uint64_t total_bytes, uint32_t nchunks);
+int kcdc_compress_chunks_device(const char* algorithm, const uint8_t* d_data, const uint64_t* d_offsets,
+                                const uint64_t* d_lens, uint32_t nchunks, uint8_t* d_out,
+                                const uint64_t* d_out_offsets, uint64_t* d_out_lens, uint32_t* d_header_ids,
+                                void* d_work, uint64_t work_bytes, void* hip_stream);
+
 /* ------------------------------------------------------------- testing
  * Hooks for the library's own tests (not part of the splitter surface).
  * kcdc_test_set: process-wide knobs read by every later batch launch.

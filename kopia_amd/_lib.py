@@ -83,6 +83,12 @@ _SIGS = {
                                              C.c_uint32, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint64, _P]),
     "kcdc_decrypt_chunks_device": (C.c_int, [C.c_char_p, C.c_char_p, C.c_uint32, _P, _P, _P, C.c_uint32, _P,
                                              C.c_uint32, C.c_uint32, _P, _P, _P, _P, C.c_uint64, _P]),
+    "kcdc_compression_algorithms": (C.c_int, [C.POINTER(C.c_char_p), C.c_int]),
+    "kcdc_compression_header_id": (C.c_int64, [C.c_char_p]),
+    "kcdc_compress_bound": (C.c_uint64, [C.c_uint64]),
+    "kcdc_compress_workspace_size": (C.c_uint64, [C.c_uint64, C.c_uint32]),
+    "kcdc_compress_chunks_device": (C.c_int, [C.c_char_p, _P, _P, _P, C.c_uint32, _P, _P, _P, _P, _P, C.c_uint64,
+                                              _P]),
 }
 
 

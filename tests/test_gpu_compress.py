@@ -1,0 +1,152 @@
+"""GPU: deflate content compression of many chunks (kcdc_compress_chunks_device) against the
+oracle (oracle/deflate.py: the reference's framing, zlib as the independent RFC 1951 inflater).
+Every chunk must inflate back to its bytes behind its 4-byte header ID, carry the content
+manager's keep-or-drop ID (content_manager_lock_free.go:64-73), and the reference's own test
+properties hold (compressor_test.go:15-87): all-zero data shrinks, random data does not, and
+another compressor's reader rejects the stream.  Edge cases: empty chunks, lengths across the
+512-byte segment and 32 KiB span boundaries, misaligned offsets, 8 MiB chunks, mixed data."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from kopia_amd import _lib
+from kopia_amd import compression as kc
+from oracle import coracle, deflate
+
+pytestmark = pytest.mark.gpu
+DEFLATE = ["deflate-best-compression", "deflate-best-speed", "deflate-default"]
+
+
+def _compress(name, host, offs, lens, dev):
+    import torch
+    d = torch.from_numpy(np.ascontiguousarray(host)).to(dev)
+    oo, total = kc.compressed_layout(lens)
+    out = torch.full((total,), 0xAB, dtype=torch.uint8, device=dev)
+    comp = kc.Compressor(name)
+    out_lens, ids = comp.compress_chunks_device(d.data_ptr(), offs, lens, out, oo, dev)
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), oo, out_lens.cpu().numpy(), ids.cpu().numpy()
+
+
+def _check(name, host, offs, lens, out, oo, out_lens, ids):
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        blob = out[oo[i]:oo[i] + out_lens[i]].tobytes()
+        assert 6 <= out_lens[i] <= kc.compress_bound(int(n)), (i, n, out_lens[i])
+        assert deflate.decompress(name, blob) == host[o:o + n].tobytes(), (i, n)
+        assert ids[i] == deflate.kept_header_id(name, int(n), int(out_lens[i])), i
+
+
+def _mixed(nbytes, seed):
+    """Random, zero, periodic and word-salad stretches (so segments hit every encoder path)."""
+    rng = np.random.default_rng(seed)
+    words = [b"kopia", b"snapshot", b"content", b"chunk", b"the", b"of", b"blob", b"index", b" ", b"\n"]
+    out, size = [], 0
+    while size < nbytes:
+        kind = int(rng.integers(0, 4))
+        n = int(rng.integers(1, 20000))
+        if kind == 0:
+            s = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        elif kind == 1:
+            s = bytes(n)
+        elif kind == 2:
+            p = rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8).tobytes()
+            s = (p * (n // len(p) + 1))[:n]
+        else:
+            s = b"".join(words[int(k)] for k in rng.integers(0, len(words), n // 4 + 1))[:n]
+        out.append(s)
+        size += len(s)
+    return np.frombuffer(b"".join(out)[:nbytes], np.uint8).copy()
+
+
+@pytest.mark.parametrize("name", DEFLATE)
+def test_reference_properties(name, gpu):
+    """compressor_test.go:21-84 through the device: 10000 zero bytes shrink (and keep the ID),
+    10000 random bytes do not (ID 0, NoCompression), both inflate back; the other deflate
+    compressors' readers reject the stream by its header."""
+    zeros = np.zeros(10000, np.uint8)
+    rnd = np.random.default_rng(5).integers(0, 256, 10000, dtype=np.uint8)
+    host = np.concatenate([zeros, rnd])
+    offs, lens = [0, 10000], [10000, 10000]
+    out, oo, ol, ids = _compress(name, host, offs, lens, gpu)
+    _check(name, host, offs, lens, out, oo, ol, ids)
+    assert ol[0] < 10000 and ids[0] == deflate.HEADER_IDS[name]
+    assert ol[1] >= 10000 and ids[1] == 0
+    blob = out[oo[0]:oo[0] + ol[0]].tobytes()
+    for other in DEFLATE:
+        if other != name:
+            with pytest.raises(ValueError):
+                deflate.decompress(other, blob)
+
+
+def test_ragged_misaligned_chunks(gpu):
+    host = _mixed(24 << 20, 11)
+    rng = np.random.default_rng(12)
+    edge = [0, 1, 2, 3, 4, 5, 7, 8, 255, 511, 512, 513, 1023, 1024, 1025, 4096, 32767, 32768, 32769,
+            65535, 65536, 65537, 100000, (1 << 20) + 3]
+    lens = edge + [int(x) for x in rng.integers(0, 300000, 200)]
+    offs = [int(rng.integers(0, host.size - L)) for L in lens]
+    out, oo, ol, ids = _compress("deflate-default", host, offs, lens, gpu)
+    _check("deflate-default", host, offs, lens, out, oo, ol, ids)
+    assert (ids != 0).sum() > len(lens) // 2  # mixed data mostly compresses
+
+
+@pytest.mark.parametrize("name", DEFLATE)
+def test_large_compressible_chunks(name, gpu):
+    """The reference benchmark's inputs (compressor_test.go:92-96): a repeated 1..10 pattern and
+    zeros, as 8 MiB + odd chunks; both must shrink far below the input."""
+    pat = np.tile(np.arange(1, 11, dtype=np.uint8), (8 << 20) // 10 + 2)[:(8 << 20) + 13]
+    host = np.concatenate([pat, np.zeros((8 << 20) + 13, np.uint8), _mixed(4 << 20, 3)])
+    offs = [0, pat.size, 2 * pat.size]
+    lens = [pat.size, pat.size, 4 << 20]
+    out, oo, ol, ids = _compress(name, host, offs, lens, gpu)
+    _check(name, host, offs, lens, out, oo, ol, ids)
+    assert ol[0] < 0.05 * lens[0] and ol[1] < 0.05 * lens[1]
+
+
+def test_splitter_chunks_of_mixed_stream(gpu):
+    """Chunks cut by the oracle's DYNAMIC-128K-BUZHASH over a mixed 32 MiB stream."""
+    host = _mixed(32 << 20, 21)
+    cuts = [int(c) for c in coracle.split_batch("DYNAMIC-128K-BUZHASH", [host])[0]]
+    bounds = [0] + cuts + ([] if cuts and cuts[-1] == host.size else [host.size])
+    offs = bounds[:-1]
+    lens = [b - a for a, b in zip(bounds[:-1], bounds[1:])]
+    assert sum(lens) == host.size and len(lens) > 100
+    out, oo, ol, ids = _compress("deflate-best-speed", host, offs, lens, gpu)
+    _check("deflate-best-speed", host, offs, lens, out, oo, ol, ids)
+
+
+def test_random_stream_is_stored(gpu):
+    """Config-2 bytes (uniform PRNG): every segment falls back to a stored block, the output is
+    the bound minus the unused trailer slack, and the ID is NoCompression."""
+    host = coracle.gen_stream(0x6B6F706961, 0, 8 << 20)
+    lens = [1 << 20] * 8
+    offs = [i << 20 for i in range(8)]
+    out, oo, ol, ids = _compress("deflate-default", host, offs, lens, gpu)
+    _check("deflate-default", host, offs, lens, out, oo, ol, ids)
+    assert not ids.any()
+    assert all(int(x) == kc.compress_bound(1 << 20) for x in ol)
+
+
+def test_workspace_too_small_writes_no_output(gpu):
+    import torch
+    host = torch.zeros(1 << 20, dtype=torch.uint8, device=gpu)
+    offs = torch.tensor([0], dtype=torch.int64, device=gpu)
+    lens = torch.tensor([1 << 20], dtype=torch.int64, device=gpu)
+    oo = torch.tensor([0], dtype=torch.int64, device=gpu)
+    out = torch.zeros(kc.compress_bound(1 << 20), dtype=torch.uint8, device=gpu)
+    ol = torch.full((1,), 7, dtype=torch.int64, device=gpu)
+    ids = torch.full((1,), 7, dtype=torch.int32, device=gpu)
+    need = int(_lib.lib().kcdc_compress_workspace_size(1 << 20, 1))
+    work = torch.empty(need // 4, dtype=torch.uint8, device=gpu)
+    rc = _lib.lib().kcdc_compress_chunks_device(b"deflate-default", C.c_void_p(host.data_ptr()), offs.data_ptr(),
+                                                lens.data_ptr(), 1, out.data_ptr(), oo.data_ptr(), ol.data_ptr(),
+                                                ids.data_ptr(), work.data_ptr(), work.numel(), None)
+    torch.cuda.synchronize()
+    assert rc == 0
+    assert ol.item() == 0 and ids.item() == 0
+    # Too small even for the per-chunk table: refused up front.
+    rc = _lib.lib().kcdc_compress_chunks_device(b"deflate-default", C.c_void_p(host.data_ptr()), offs.data_ptr(),
+                                                lens.data_ptr(), 1, out.data_ptr(), oo.data_ptr(), ol.data_ptr(),
+                                                ids.data_ptr(), work.data_ptr(), 4, None)
+    assert rc == _lib.KCDC_EINVAL
