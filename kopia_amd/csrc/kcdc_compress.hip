@@ -19,7 +19,9 @@
 // empty final fixed block (03 00).
 //
 // Kernels, in stream order: span_count (spans per chunk), span_scan (prefix), deflate_spans
-// (LZ77 + bits), deflate_finish (per chunk: scan of segment lengths, header, concatenation).
+// (LZ77 + bits; output bytes per span), span_pos (their prefix), deflate_copy (one wave per
+// span: segments to their places, dword stores), deflate_frame (per chunk: header ID, final
+// block, length, the ID kept).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -48,6 +50,8 @@ struct CompArgs {
     uint32_t* ids;
     uint32_t* spans;    // [n + 1]: spans per chunk, then their exclusive prefix
     uint32_t* seglen;   // [max_spans * 64]
+    uint32_t* span_bytes;  // [max_spans]: output bytes of each span's segments
+    uint64_t* span_pos;    // [max_spans + 1]: their exclusive prefix over all chunks
     uint8_t* slots;     // [max_spans * 64 * kSlot]
     uint32_t n;
     uint32_t max_spans;
@@ -189,10 +193,8 @@ __global__ __launch_bounds__(64) void deflate_spans_kernel(CompArgs a) {
 
     const uint32_t slot = b * 64u + lane;
     const uint32_t x0 = kSeg * lane;
-    if (x0 >= span_len) {
-        a.seglen[slot] = 0u;
-        return;
-    }
+    uint32_t word = 0;  // the segment's length word (0: past the span's end)
+    if (x0 < span_len) word = [&]() -> uint32_t {
     const uint32_t xe = span_len - x0 < kSeg ? span_len : x0 + kSeg;
     const uint32_t seg_len = xe - x0;
     uint32_t* base = reinterpret_cast<uint32_t*>(a.slots + static_cast<uint64_t>(slot) * kSlot);
@@ -243,6 +245,20 @@ __global__ __launch_bounds__(64) void deflate_spans_kernel(CompArgs a) {
             x += 1u + ((x - lit) >> a.skip);
         }
     }
+    if (!over) {
+        // The block's exact size with the pending literals, counted 4 bytes at a time (a fixed
+        // literal is 8 bits, 9 from 0x90): a segment that would not beat a stored copy (random
+        // data) is never emitted.
+        uint32_t a0 = lit, nine = 0;
+        for (; a0 < xe && ((a0 + d) & 3u); a0++) nine += byte(a0) >= 144u;
+        for (; a0 + 4u <= xe; a0 += 4u) {
+            const uint32_t v = L[pw((a0 + d) >> 2)];
+            nine += __builtin_popcount(v & 0x80808080u & ((v << 1) | (v << 2) | (v << 3)));
+        }
+        for (; a0 < xe; a0++) nine += byte(a0) >= 144u;
+        const uint32_t bits = 32u * static_cast<uint32_t>(w.op - base) + w.nb + 8u * (xe - lit) + nine + 10u;
+        if (((bits + 7u) >> 3) + 4u >= seg_len + 5u) over = true;
+    }
     if (!over) literals(xe);
     uint32_t bytes = 0;
     if (!over) {
@@ -255,75 +271,118 @@ __global__ __launch_bounds__(64) void deflate_spans_kernel(CompArgs a) {
         if (w.nb) *w.op = static_cast<uint32_t>(w.bb);
         if (bytes >= seg_len + 5u) over = true;
     }
-    a.seglen[slot] = over ? (kStored | seg_len) : bytes;
+    return over ? (kStored | seg_len) : bytes;
+    }();
+    a.seglen[slot] = word;
+    // The span's output bytes (stored segments: 5 + n).
+    uint32_t eff = (word & kStored) ? 5u + (word & ~kStored) : word;
+    for (uint32_t o = 32; o > 0; o >>= 1) eff += __shfl_xor(eff, o, 64);
+    if (lane == 0) a.span_bytes[b] = eff;
 }
 
-// One workgroup per chunk: concatenates its segments behind the header ID and ends the
-// stream with an empty final fixed block.
-__global__ __launch_bounds__(256) void deflate_finish_kernel(CompArgs a) {
-    __shared__ uint32_t pos[256];
-    __shared__ uint32_t wsum[4];
-    const uint32_t c = blockIdx.x, t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+// Exclusive prefix (64-bit) of span_bytes[0..total) into span_pos[0..total]; one workgroup.
+__global__ __launch_bounds__(1024) void span_pos_kernel(CompArgs a) {
+    __shared__ uint64_t part[1024];
+    const uint32_t total = a.spans[a.n];
+    if (total > a.max_spans) return;
+    const uint32_t t = threadIdx.x;
+    const uint64_t b = static_cast<uint64_t>(total) * t / 1024u, e = static_cast<uint64_t>(total) * (t + 1) / 1024u;
+    uint64_t s = 0;
+    for (uint64_t i = b; i < e; i++) s += a.span_bytes[i];
+    part[t] = s;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024u; d <<= 1) {
+        const uint64_t v = t >= d ? part[t - d] : 0ull;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint64_t run = part[t] - s;
+    for (uint64_t i = b; i < e; i++) {
+        a.span_pos[i] = run;
+        run += a.span_bytes[i];
+    }
+    if (t == 1023u) a.span_pos[total] = part[1023];
+}
+
+// n bytes from src to dst, both at any alignment, by one wave: byte stores for dst's partial
+// head and tail words, aligned dword stores (from two aligned loads + alignbit) in between.
+// Only aligned source words holding a byte of [src, src + n) are read.
+__device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint32_t n, uint32_t lane) {
+    const uint32_t head = min(n, static_cast<uint32_t>((4u - (reinterpret_cast<uintptr_t>(dst) & 3u)) & 3u));
+    if (lane < head) dst[lane] = src[lane];
+    const uint32_t m = (n - head) >> 2;
+    uint32_t* dw = reinterpret_cast<uint32_t*>(dst + head);
+    const uint8_t* s0 = src + head;
+    const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(s0) & 3u);
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(s0 - sh);
+    for (uint32_t i = lane; i < m; i += 64u) {
+        const uint32_t w0 = sw[i];
+        const uint32_t w1 = sh ? sw[i + 1] : 0u;
+        dw[i] = __builtin_amdgcn_alignbit(w1, w0, 8u * sh);
+    }
+    const uint32_t done = head + 4u * m;
+    if (lane < n - done) dst[done + lane] = src[done + lane];
+}
+
+// One wave per span: its segments' bytes to their places in the chunk's stream.
+__global__ __launch_bounds__(64) void deflate_copy_kernel(CompArgs a) {
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    const uint32_t total = a.spans[a.n];
+    if (total > a.max_spans || b >= total) return;
+    uint32_t lo = 0, hi = a.n;
+    while (hi - lo > 1u) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.spans[mid] <= b) lo = mid; else hi = mid;
+    }
+    const uint32_t c = lo;
+    const uint32_t u = b - a.spans[c];
+    uint8_t* dst = a.out + a.out_offs[c] + 4u + (a.span_pos[b] - a.span_pos[a.spans[c]]);
+    const uint8_t* in = a.in + a.in_offs[c] + static_cast<uint64_t>(u) * kSpan;
+    const uint32_t word = a.seglen[b * 64u + lane];
+    const uint32_t eff = (word & kStored) ? 5u + (word & ~kStored) : word;
+    uint32_t incl = eff;
+    for (uint32_t o = 1; o < 64u; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const uint32_t pos = incl - eff;
+    for (uint32_t j = 0; j < 64u; j++) {
+        const uint32_t wj = __shfl(word, j, 64), pj = __shfl(pos, j, 64);
+        if (wj == 0u) break;  // the rest of the span is past the chunk's end
+        uint8_t* o = dst + pj;
+        if (wj & kStored) {
+            const uint32_t m = wj & ~kStored;
+            if (lane < 5u) {
+                const uint32_t hdr = lane == 0 ? 0u : lane == 1 ? (m & 255u) : lane == 2 ? (m >> 8)
+                                   : lane == 3 ? (~m & 255u) : ((~m >> 8) & 255u);
+                o[lane] = static_cast<uint8_t>(hdr);  // stored block: BFINAL 0, BTYPE 00, LEN, NLEN
+            }
+            wave_copy(o + 5, in + j * kSeg, m, lane);
+        } else {
+            wave_copy(o, a.slots + (static_cast<uint64_t>(b) * 64u + j) * kSlot, wj, lane);
+        }
+    }
+}
+
+// One thread per chunk: header ID, the empty final block (03 00), the length and the ID kept.
+__global__ __launch_bounds__(256) void deflate_frame_kernel(CompArgs a) {
+    const uint32_t c = blockIdx.x * 256u + threadIdx.x;
+    if (c >= a.n) return;
     const uint32_t total = a.spans[a.n];
     if (total > a.max_spans) {  // workspace smaller than the chunks need: no output
-        if (t == 0) {
-            a.out_lens[c] = 0ull;
-            a.ids[c] = 0u;
-        }
+        a.out_lens[c] = 0ull;
+        a.ids[c] = 0u;
         return;
     }
-    const uint64_t s0 = static_cast<uint64_t>(a.spans[c]) * 64u;
-    const uint32_t ns = (a.spans[c + 1] - a.spans[c]) * 64u;
     uint8_t* dst = a.out + a.out_offs[c];
-    const uint8_t* src_in = a.in + a.in_offs[c];
-    uint64_t carry = 4;
-    for (uint32_t base = 0; base < ns; base += 256u) {
-        const uint32_t i = base + t;
-        const uint32_t Lr = i < ns ? a.seglen[s0 + i] : 0u;
-        const uint32_t eff = (Lr & kStored) ? 5u + (Lr & ~kStored) : Lr;
-        // Block exclusive scan of eff.
-        uint32_t incl = eff;
-        for (uint32_t o = 1; o < 64u; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += y;
-        }
-        if (lane == 63u) wsum[wv] = incl;
-        __syncthreads();
-        uint32_t before = 0, tot = 0;
-        for (uint32_t k = 0; k < 4u; k++) {
-            if (k < wv) before += wsum[k];
-            tot += wsum[k];
-        }
-        pos[t] = before + incl - eff;
-        __syncthreads();
-        for (uint32_t j = wv; j < 256u && base + j < ns; j += 4u) {
-            const uint32_t Lj = a.seglen[s0 + base + j];
-            uint8_t* o = dst + carry + pos[j];
-            if (Lj & kStored) {
-                const uint32_t m = Lj & ~kStored;
-                if (lane < 5u) {
-                    const uint32_t hdr = lane == 0 ? 0u : lane == 1 ? (m & 255u) : lane == 2 ? (m >> 8)
-                                       : lane == 3 ? (~m & 255u) : ((~m >> 8) & 255u);
-                    o[lane] = static_cast<uint8_t>(hdr);
-                }
-                const uint8_t* s = src_in + static_cast<uint64_t>(base + j) * kSeg;
-                for (uint32_t q = lane; q < m; q += 64u) o[5u + q] = s[q];
-            } else {
-                const uint8_t* s = a.slots + (s0 + base + j) * kSlot;
-                for (uint32_t q = lane; q < Lj; q += 64u) o[q] = s[q];
-            }
-        }
-        carry += tot;
-        __syncthreads();
-    }
-    if (t < 4u) dst[t] = static_cast<uint8_t>(a.header_id >> (8u * (3u - t)));
-    if (t == 4u) dst[carry] = 0x03u;  // BFINAL 1, BTYPE 01, end of block
-    if (t == 5u) dst[carry + 1] = 0x00u;
-    if (t == 0) {
-        const uint64_t out_len = carry + 2u;
-        a.out_lens[c] = out_len;
-        a.ids[c] = out_len < a.in_lens[c] ? a.header_id : 0u;  // content_manager_lock_free.go:64
-    }
+    const uint64_t body = a.span_pos[a.spans[c + 1]] - a.span_pos[a.spans[c]];
+    for (uint32_t t = 0; t < 4u; t++) dst[t] = static_cast<uint8_t>(a.header_id >> (8u * (3u - t)));
+    dst[4 + body] = 0x03u;  // BFINAL 1, BTYPE 01, end of block
+    dst[5 + body] = 0x00u;
+    const uint64_t out_len = body + 6u;
+    a.out_lens[c] = out_len;
+    a.ids[c] = out_len < a.in_lens[c] ? a.header_id : 0u;  // content_manager_lock_free.go:64
 }
 
 }  // namespace compdev
@@ -352,13 +411,16 @@ const CompAlgo* find_comp(const char* name) {
 uint64_t align256c(uint64_t x) { return (x + 255u) & ~uint64_t(255); }
 
 struct CompWs {
-    uint64_t spans, seglen, slots, total;
+    uint64_t spans, seglen, span_bytes, span_pos, slots, total;
 };
+constexpr uint64_t kPerSpan = 64u * (compdev::kSlot + 4u) + 4u + 8u;
 CompWs comp_ws(uint32_t n, uint64_t max_spans) {
     CompWs l{};
     l.spans = 0;
     l.seglen = align256c((uint64_t(n) + 1u) * 4u);
-    l.slots = align256c(l.seglen + max_spans * 64u * 4u);
+    l.span_bytes = align256c(l.seglen + max_spans * 64u * 4u);
+    l.span_pos = align256c(l.span_bytes + max_spans * 4u);
+    l.slots = align256c(l.span_pos + (max_spans + 1u) * 8u);
     l.total = align256c(l.slots + max_spans * 64u * compdev::kSlot);
     return l;
 }
@@ -400,7 +462,7 @@ extern "C" int kcdc_compress_chunks_device(const char* name, const uint8_t* d_da
     // The largest span count this workspace holds (the kernels check the real count against it).
     const uint64_t fixed = comp_ws(nchunks, 0).total;
     if (work_bytes < fixed) return set_error(-22, "workspace too small (kcdc_compress_workspace_size)");
-    uint64_t max_spans = (work_bytes - fixed) / (64u * (compdev::kSlot + 4u));
+    uint64_t max_spans = (work_bytes - fixed) / kPerSpan;
     while (max_spans > 0 && comp_ws(nchunks, max_spans).total > work_bytes) max_spans--;
     if (max_spans > 0x7fffffffull) max_spans = 0x7fffffffull;
     compdev::CompArgs a{};
@@ -415,6 +477,8 @@ extern "C" int kcdc_compress_chunks_device(const char* name, const uint8_t* d_da
     uint8_t* w = static_cast<uint8_t*>(d_work);
     a.spans = reinterpret_cast<uint32_t*>(w + l.spans);
     a.seglen = reinterpret_cast<uint32_t*>(w + l.seglen);
+    a.span_bytes = reinterpret_cast<uint32_t*>(w + l.span_bytes);
+    a.span_pos = reinterpret_cast<uint64_t*>(w + l.span_pos);
     a.slots = w + l.slots;
     a.n = nchunks;
     a.max_spans = static_cast<uint32_t>(max_spans);
@@ -423,9 +487,13 @@ extern "C" int kcdc_compress_chunks_device(const char* name, const uint8_t* d_da
     hipStream_t st = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(compdev::span_count_kernel, dim3((nchunks + 255u) / 256u), dim3(256), 0, st, a);
     hipLaunchKernelGGL(compdev::span_scan_kernel, dim3(1), dim3(1024), 0, st, nchunks, a.spans);
-    if (max_spans > 0)
-        hipLaunchKernelGGL(compdev::deflate_spans_kernel, dim3(static_cast<uint32_t>(max_spans)), dim3(64), 0, st, a);
-    hipLaunchKernelGGL(compdev::deflate_finish_kernel, dim3(nchunks), dim3(256), 0, st, a);
+    if (max_spans > 0) {
+        const dim3 grid(static_cast<uint32_t>(max_spans));
+        hipLaunchKernelGGL(compdev::deflate_spans_kernel, grid, dim3(64), 0, st, a);
+        hipLaunchKernelGGL(compdev::span_pos_kernel, dim3(1), dim3(1024), 0, st, a);
+        hipLaunchKernelGGL(compdev::deflate_copy_kernel, grid, dim3(64), 0, st, a);
+    }
+    hipLaunchKernelGGL(compdev::deflate_frame_kernel, dim3((nchunks + 255u) / 256u), dim3(256), 0, st, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : set_error(-5, std::string("compression kernel launch: ") + hipGetErrorString(e));
 }
