@@ -288,26 +288,12 @@ struct CryptArgs {
     HmacMid mid;
 };
 
-// One wave per chunk: key, one-time Poly1305 key, power table; every lane computes the
-// (wave-uniform) key schedule and then its own table entries.
-template <bool kOpen>
-__global__ __launch_bounds__(256) void crypt_prep_kernel(CryptArgs a) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t c = blockIdx.x * 4u + (threadIdx.x >> 6);
-    if (c >= a.n) return;
-    const uint64_t in_len = a.in_lens[c];
-    const bool bad = kOpen ? (in_len < 28u || in_len - 28u > kMaxLen) : in_len > kMaxLen;
-    const uint64_t len = bad ? 0 : (kOpen ? in_len - 28u : in_len);
-    const uint8_t* ivp = a.ivs + static_cast<uint64_t>(c) * a.iv_stride;
-    const uint8_t* np = kOpen ? a.in + a.in_offs[c] : a.nonces + 12ull * c;
-    uint32_t nonce[3] = {0u, 0u, 0u};
-    if (!(kOpen && bad)) {
-#pragma unroll
-        for (int j = 0; j < 3; j++) nonce[j] = load_le32_bytes(np + 4 * j);
-    }
+// HMAC-SHA256(secret, id) from the secret's midstates: the per-content key of both encryptors
+// (chacha20_poly1305_hmac_sha256_encryptor.go:24-48, aes256_gcm_hmac_sha256_encryptor.go:24-47).
+__device__ __forceinline__ void hmac_key(const HmacMid& mid, const uint8_t* ivp, uint32_t il, uint32_t (&key)[8]) {
     // HMAC-SHA256(secret, id): after the (key ^ ipad) block, id || 0x80 || 0.. || bit length
     // fills one block (id <= 55 bytes) or two; the outer hash is digest || pad (96 bytes).
-    const uint32_t il = a.iv_len;
+    
     uint32_t blk[32];
 #pragma unroll
     for (int j = 0; j < 32; j++) blk[j] = 0;
@@ -322,7 +308,7 @@ __global__ __launch_bounds__(256) void crypt_prep_kernel(CryptArgs a) {
     else blk[15] = bits;
     uint32_t h[8];
 #pragma unroll
-    for (int j = 0; j < 8; j++) h[j] = a.mid.in[j];
+    for (int j = 0; j < 8; j++) h[j] = mid.in[j];
     {
         uint32_t b0[16];
 #pragma unroll
@@ -341,16 +327,36 @@ __global__ __launch_bounds__(256) void crypt_prep_kernel(CryptArgs a) {
     for (int j = 9; j < 15; j++) blk[j] = 0;
     blk[15] = 96u * 8u;
 #pragma unroll
-    for (int j = 0; j < 8; j++) h[j] = a.mid.out[j];
+    for (int j = 0; j < 8; j++) h[j] = mid.out[j];
     {
         uint32_t b0[16];
 #pragma unroll
         for (int j = 0; j < 16; j++) b0[j] = blk[j];
         sha256_compress(h, b0);
     }
-    uint32_t key[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) key[j] = bswap32(h[j]);
+}
+
+// One wave per chunk: key, one-time Poly1305 key, power table; every lane computes the
+// (wave-uniform) key schedule and then its own table entries.
+template <bool kOpen>
+__global__ __launch_bounds__(256) void crypt_prep_kernel(CryptArgs a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t c = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (c >= a.n) return;
+    const uint64_t in_len = a.in_lens[c];
+    const bool bad = kOpen ? (in_len < 28u || in_len - 28u > kMaxLen) : in_len > kMaxLen;
+    const uint64_t len = bad ? 0 : (kOpen ? in_len - 28u : in_len);
+    const uint8_t* ivp = a.ivs + static_cast<uint64_t>(c) * a.iv_stride;
+    const uint8_t* np = kOpen ? a.in + a.in_offs[c] : a.nonces + 12ull * c;
+    uint32_t nonce[3] = {0u, 0u, 0u};
+    if (!(kOpen && bad)) {
+#pragma unroll
+        for (int j = 0; j < 3; j++) nonce[j] = load_le32_bytes(np + 4 * j);
+    }
+    uint32_t key[8];
+    hmac_key(a.mid, ivp, a.iv_len, key);
     uint32_t ks[16];
     chacha20_block(key, 0u, nonce, ks);  // block 0 -> Poly1305 one-time key (RFC 8439 §2.6)
     const uint32_t r0 = ks[0] & 0x0FFFFFFFu, r1 = ks[1] & 0x0FFFFFFCu, r2 = ks[2] & 0x0FFFFFFCu, r3 = ks[3] & 0x0FFFFFFCu;
@@ -783,6 +789,478 @@ __global__ __launch_bounds__(256) void crypt_finish_kernel(CryptArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ AES256-GCM-HMAC-SHA256
+// repo/encryption/aes256_gcm_hmac_sha256_encryptor.go:24-65 (key = HMAC-SHA256(secret, id);
+// AES-256-GCM from Go's crypto/cipher, 12-byte nonce, aad = id), aead_helpers.go:12-75.
+// NIST SP 800-38D: J0 = nonce || 1, block j of the text uses counter j + 2, the tag is
+// GHASH_H(aad, text) ^ E(J0).  AES is the big-endian T-table form (FIPS-197 §5.1 with
+// SubBytes/ShiftRows/MixColumns folded into four 256-word tables), the tables derived on the
+// device from GF(2^8) inverses.  GHASH elements are 4 big-endian words: bit 31 of w[0] is the
+// coefficient of x^0.
+//
+// Byte pass layout: a chunk of c 16-byte blocks is padded at the FRONT with pre zero blocks to
+// U whole 4 KiB units (256 blocks), so every unit is full and zero blocks before the text
+// leave GHASH unchanged.  A segment is 64 units counted back from the end (the first may be
+// shorter), one wave.  Lane l owns the blocks
+// v = l (mod 64): CTR + GHASH Horner with the one multiplier M = H^64 (4-bit tables per nibble
+// position in LDS); at the segment end lane l's sum is scaled by H^(63-l), the wave XORs the
+// lanes, scales by H^(16384 (segments after)), and XORs that into the chunk's accumulator.
+constexpr uint32_t kGcmSegUnits = 64;               // units per segment (one wave)
+constexpr uint32_t kGcmHp = 12;                     // H^(16384 * 2^i): chunks < 2^30 B
+
+struct GcmKey {  // per chunk, 1664 bytes
+    uint32_t rk[60];
+    uint32_t h[4], h64[4], ej0[4];
+    uint32_t nonce[3];  // big-endian words
+    uint32_t len_lo, len_hi;
+    uint32_t pre, nseg;
+    uint32_t pad[3];
+    uint32_t acc[4];           // XOR of the segments' scaled sums (atomic)
+    uint32_t hp[kGcmHp][4];    // H^(16384 * 2^i)
+    uint32_t hl[64][4];        // H^l
+    uint32_t pad2[26];
+};
+static_assert(sizeof(GcmKey) == 1664, "GcmKey layout");
+
+__device__ __forceinline__ uint32_t xt8(uint32_t a) { return ((a << 1) ^ ((a & 0x80u) ? 0x11Bu : 0u)) & 0xFFu; }
+__device__ __forceinline__ uint32_t gmul8(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        r ^= (b & 1u) ? a : 0u;
+        a = xt8(a);
+        b >>= 1;
+    }
+    return r;
+}
+// FIPS-197 §5.1.1: S(x) = affine(x^254).
+__device__ __forceinline__ uint32_t aes_sbox_entry(uint32_t x) {
+    uint32_t p = 1, b = x;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {  // x^254: bits 1..7 of 254
+        if ((254u >> i) & 1u) p = gmul8(p, b);
+        b = gmul8(b, b);
+    }
+    uint32_t out = 0x63u;
+#pragma unroll
+    for (int k = 0; k < 5; k++) out ^= ((p << k) | (p >> (8 - k))) & 0xFFu;
+    return out;
+}
+
+// Te0[x] = {2S, S, S, 3S} big-endian; Te1..Te3 are its byte rotations.  Sb[x] = S.
+struct AesTabs {
+    uint32_t te[4][256];
+    uint32_t sb[256];
+};
+__device__ __forceinline__ void aes_tabs_build(AesTabs& t, uint32_t tid, uint32_t nthreads) {
+    for (uint32_t x = tid; x < 256u; x += nthreads) {
+        const uint32_t s = aes_sbox_entry(x), s2 = xt8(s), s3 = s2 ^ s;
+        const uint32_t w = (s2 << 24) | (s << 16) | (s << 8) | s3;
+        t.te[0][x] = w;
+        t.te[1][x] = ror32(w, 8);
+        t.te[2][x] = ror32(w, 16);
+        t.te[3][x] = ror32(w, 24);
+        t.sb[x] = s;
+    }
+}
+
+__device__ __forceinline__ void aes256_expand(const AesTabs& t, const uint32_t (&key)[8], uint32_t (&rk)[60]) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) rk[i] = key[i];
+    uint32_t rcon = 1;
+#pragma unroll
+    for (int i = 8; i < 60; i++) {
+        uint32_t x = rk[i - 1];
+        if (i % 8 == 0) {
+            x = (t.sb[(x >> 16) & 255u] << 24) | (t.sb[(x >> 8) & 255u] << 16) | (t.sb[x & 255u] << 8) | t.sb[x >> 24];
+            x ^= rcon << 24;
+            rcon = xt8(rcon);
+        } else if (i % 8 == 4) {
+            x = (t.sb[x >> 24] << 24) | (t.sb[(x >> 16) & 255u] << 16) | (t.sb[(x >> 8) & 255u] << 8) | t.sb[x & 255u];
+        }
+        rk[i] = rk[i - 8] ^ x;
+    }
+}
+
+template <typename RK>
+__device__ __forceinline__ void aes256_block(const AesTabs& t, const RK& rk, uint32_t (&s)[4]) {
+    uint32_t s0 = s[0] ^ rk[0], s1 = s[1] ^ rk[1], s2 = s[2] ^ rk[2], s3 = s[3] ^ rk[3];
+#pragma unroll
+    for (int r = 1; r < 14; r++) {
+        const uint32_t t0 = t.te[0][s0 >> 24] ^ t.te[1][(s1 >> 16) & 255u] ^ t.te[2][(s2 >> 8) & 255u] ^ t.te[3][s3 & 255u] ^ rk[4 * r];
+        const uint32_t t1 = t.te[0][s1 >> 24] ^ t.te[1][(s2 >> 16) & 255u] ^ t.te[2][(s3 >> 8) & 255u] ^ t.te[3][s0 & 255u] ^ rk[4 * r + 1];
+        const uint32_t t2 = t.te[0][s2 >> 24] ^ t.te[1][(s3 >> 16) & 255u] ^ t.te[2][(s0 >> 8) & 255u] ^ t.te[3][s1 & 255u] ^ rk[4 * r + 2];
+        const uint32_t t3 = t.te[0][s3 >> 24] ^ t.te[1][(s0 >> 16) & 255u] ^ t.te[2][(s1 >> 8) & 255u] ^ t.te[3][s2 & 255u] ^ rk[4 * r + 3];
+        s0 = t0;
+        s1 = t1;
+        s2 = t2;
+        s3 = t3;
+    }
+    auto fin = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+        return ((t.sb[a >> 24] << 24) | (t.sb[(b >> 16) & 255u] << 16) | (t.sb[(c >> 8) & 255u] << 8) | t.sb[d & 255u]) ^ k;
+    };
+    s[0] = fin(s0, s1, s2, s3, rk[56]);
+    s[1] = fin(s1, s2, s3, s0, rk[57]);
+    s[2] = fin(s2, s3, s0, s1, rk[58]);
+    s[3] = fin(s3, s0, s1, s2, rk[59]);
+}
+
+// z = x * y in GCM's field (bit-serial, 128 steps).
+__device__ __forceinline__ void gf_mul(const uint32_t (&x)[4], const uint32_t (&y)[4], uint32_t (&z)[4]) {
+    uint32_t v0 = y[0], v1 = y[1], v2 = y[2], v3 = y[3];
+    uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const uint32_t xw = x[w];
+#pragma unroll 8
+        for (int b = 31; b >= 0; b--) {
+            const uint32_t m = 0u - ((xw >> b) & 1u);
+            z0 ^= v0 & m;
+            z1 ^= v1 & m;
+            z2 ^= v2 & m;
+            z3 ^= v3 & m;
+            const uint32_t red = 0xE1000000u & (0u - (v3 & 1u));
+            v3 = __builtin_amdgcn_alignbit(v2, v3, 1);
+            v2 = __builtin_amdgcn_alignbit(v1, v2, 1);
+            v1 = __builtin_amdgcn_alignbit(v0, v1, 1);
+            v0 = (v0 >> 1) ^ red;
+        }
+    }
+    z[0] = z0;
+    z[1] = z1;
+    z[2] = z2;
+    z[3] = z3;
+}
+__device__ __forceinline__ void gf_mul_in(uint32_t (&x)[4], const uint32_t (&y)[4]) {
+    uint32_t z[4];
+    gf_mul(x, y, z);
+#pragma unroll
+    for (int j = 0; j < 4; j++) x[j] = z[j];
+}
+__device__ __forceinline__ void gf_one(uint32_t (&x)[4]) {
+    x[0] = 0x80000000u;
+    x[1] = x[2] = x[3] = 0u;
+}
+// x = y^e (square and multiply, e < 2^bits)
+__device__ __forceinline__ void gf_pow(const uint32_t (&y)[4], uint64_t e, uint32_t (&x)[4]) {
+    gf_one(x);
+    uint32_t b[4] = {y[0], y[1], y[2], y[3]};
+    while (e) {
+        if (e & 1u) gf_mul_in(x, b);
+        e >>= 1;
+        if (e) gf_mul_in(b, b);
+    }
+}
+
+__device__ __forceinline__ void gcm_layout(uint64_t len, uint32_t& pre, uint32_t& nseg) {
+    const uint64_t c = (len + 15u) >> 4;
+    const uint64_t u = (c + 255u) >> 8;
+    pre = static_cast<uint32_t>(u * 256u - c);
+    nseg = static_cast<uint32_t>((u + kGcmSegUnits - 1u) / kGcmSegUnits);
+}
+
+// One wave per chunk: HMAC key, key schedule, H, E(J0), powers of H; the nonce for seal.
+template <bool kOpen>
+__global__ __launch_bounds__(256) void gcm_prep_kernel(CryptArgs a, GcmKey* keys) {
+    __shared__ AesTabs t;
+    aes_tabs_build(t, threadIdx.x, 256u);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t c = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (c >= a.n) return;
+    const uint64_t in_len = a.in_lens[c];
+    const bool bad = kOpen ? (in_len < 28u || in_len - 28u > kMaxLen) : in_len > kMaxLen;
+    const uint64_t len = bad ? 0 : (kOpen ? in_len - 28u : in_len);
+    const uint8_t* ivp = a.ivs + static_cast<uint64_t>(c) * a.iv_stride;
+    const uint8_t* np = kOpen ? a.in + a.in_offs[c] : a.nonces + 12ull * c;
+    uint32_t nonce[3] = {0u, 0u, 0u};  // little-endian words as stored
+    if (!(kOpen && bad)) {
+#pragma unroll
+        for (int j = 0; j < 3; j++) nonce[j] = load_le32_bytes(np + 4 * j);
+    }
+    uint32_t key[8];
+    hmac_key(a.mid, ivp, a.iv_len, key);  // big-endian words of the digest after bswap below
+#pragma unroll
+    for (int j = 0; j < 8; j++) key[j] = bswap32(key[j]);
+    uint32_t rk[60];
+    aes256_expand(t, key, rk);
+    uint32_t h[4] = {0u, 0u, 0u, 0u};
+    aes256_block(t, rk, h);
+    uint32_t ej0[4] = {bswap32(nonce[0]), bswap32(nonce[1]), bswap32(nonce[2]), 1u};
+    aes256_block(t, rk, ej0);
+    GcmKey& k = keys[c];
+    // Lane l: H^l, and for l < 12 H^(16384 * 2^l) = H^(2^(14 + l)); lane 0 also H^64.
+    uint32_t p[4];
+    gf_pow(h, lane, p);
+#pragma unroll
+    for (int j = 0; j < 4; j++) k.hl[lane][j] = p[j];
+    if (lane < kGcmHp) {
+        uint32_t q[4] = {h[0], h[1], h[2], h[3]};
+        for (uint32_t i = 0; i < 14u + lane; i++) gf_mul_in(q, q);
+#pragma unroll
+        for (int j = 0; j < 4; j++) k.hp[lane][j] = q[j];
+    }
+    uint32_t pre, nseg;
+    gcm_layout(len, pre, nseg);
+    if (lane == 0) {
+        uint32_t q[4] = {h[0], h[1], h[2], h[3]};
+        for (int i = 0; i < 6; i++) gf_mul_in(q, q);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            k.h[j] = h[j];
+            k.h64[j] = q[j];
+            k.ej0[j] = ej0[j];
+            k.acc[j] = 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < 3; j++) k.nonce[j] = bswap32(nonce[j]);
+        k.len_lo = static_cast<uint32_t>(len);
+        k.len_hi = static_cast<uint32_t>(len >> 32);
+        k.pre = pre;
+        k.nseg = nseg;
+        a.units[c] = nseg;
+        a.status[c] = bad ? (kOpen && in_len < 28u ? -22 : -27) : 0;  // EINVAL / EFBIG
+    }
+    uint32_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < 60; j++)
+        if (lane == static_cast<uint32_t>(j)) mine = rk[j];
+    if (lane < 60u) k.rk[lane] = mine;
+    if (!kOpen && lane < 3u) reinterpret_cast<uint32_t*>(a.out + a.out_offs[c])[lane] = nonce[lane];
+}
+
+// GHASH tables of one wave: tab[k][n] = (nibble n at position k) * M, position k = bits 4k..4k+3
+// of the big-endian 128-bit value (k = 0: the low bits of w[3]).
+struct GcmWave {
+    uint32_t tab[32][16][4];
+    uint32_t p[128][4];  // M * x^i
+};
+
+__device__ __forceinline__ void gcm_tab_build(GcmWave& g, const uint32_t (&m)[4], uint32_t lane) {
+    uint32_t v0 = m[0], v1 = m[1], v2 = m[2], v3 = m[3];
+    for (uint32_t i = 0; i < 128u; i++) {
+        if ((i & 63u) == lane) {
+            g.p[i][0] = v0;
+            g.p[i][1] = v1;
+            g.p[i][2] = v2;
+            g.p[i][3] = v3;
+        }
+        const uint32_t red = 0xE1000000u & (0u - (v3 & 1u));
+        v3 = __builtin_amdgcn_alignbit(v2, v3, 1);
+        v2 = __builtin_amdgcn_alignbit(v1, v2, 1);
+        v1 = __builtin_amdgcn_alignbit(v0, v1, 1);
+        v0 = (v0 >> 1) ^ red;
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (uint32_t q = 0; q < 8u; q++) {
+        const uint32_t e = lane + 64u * q, kk = e >> 4, n = e & 15u;
+        uint32_t z[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (uint32_t b = 0; b < 4u; b++)
+            if ((n >> b) & 1u) {
+                const uint32_t i = 127u - 4u * kk - b;
+#pragma unroll
+                for (int j = 0; j < 4; j++) z[j] ^= g.p[i][j];
+            }
+#pragma unroll
+        for (int j = 0; j < 4; j++) g.tab[kk][n][j] = z[j];
+    }
+    wave_lds_sync();
+}
+
+// x = x * M through the wave's tables.
+__device__ __forceinline__ void gcm_tab_mul(const GcmWave& g, uint32_t (&x)[4]) {
+    uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        const uint32_t xw = x[3 - w];  // positions 8w .. 8w+7 live in word 3 - w
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint4 e = *reinterpret_cast<const uint4*>(g.tab[8 * w + q][(xw >> (4 * q)) & 15u]);
+            z0 ^= e.x;
+            z1 ^= e.y;
+            z2 ^= e.z;
+            z3 ^= e.w;
+        }
+    }
+    x[0] = z0;
+    x[1] = z1;
+    x[2] = z2;
+    x[3] = z3;
+}
+
+template <bool kOpen>
+__global__ __launch_bounds__(256) void gcm_units_kernel(CryptArgs a, const GcmKey* __restrict__ keys,
+                                                         GcmKey* acc_keys, const uint32_t* __restrict__ segp) {
+    __shared__ AesTabs t;
+    __shared__ GcmWave gw[4];
+    aes_tabs_build(t, threadIdx.x, 256u);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    GcmWave& g = gw[wv];
+    const uint32_t total = segp[a.n];
+    const uint32_t nw = gridDim.x * 4u;
+    uint32_t cur = 0xFFFFFFFFu;
+    for (uint32_t s = blockIdx.x * 4u + wv; s < total; s += nw) {
+        uint32_t lo = 0, hi = a.n;  // segp[lo] <= s < segp[hi]
+        while (hi - lo > 1u) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (segp[mid] <= s) lo = mid;
+            else hi = mid;
+        }
+        const uint32_t c = lo;
+        const GcmKey& k = keys[c];
+        if (c != cur) {
+            wave_lds_sync();
+            const uint32_t m[4] = {k.h64[0], k.h64[1], k.h64[2], k.h64[3]};
+            gcm_tab_build(g, m, lane);
+            cur = c;
+        }
+        const uint64_t len = static_cast<uint64_t>(k.len_lo) | (static_cast<uint64_t>(k.len_hi) << 32);
+        const uint32_t pre = k.pre, nseg = k.nseg;
+        const uint64_t nblk = (len + 15u) >> 4;
+        const uint32_t units = static_cast<uint32_t>((nblk + pre) >> 8);
+        const uint32_t sl = s - segp[c];
+        // Segments end at 64-unit steps from the chunk's end: only the first is partial, so every
+        // segment after this one holds exactly 16384 blocks.
+        const uint32_t u1 = units - kGcmSegUnits * (nseg - 1u - sl);
+        const uint32_t u0 = u1 > kGcmSegUnits ? u1 - kGcmSegUnits : 0u;
+        const uint8_t* inb = a.in + a.in_offs[c] + (kOpen ? 12u : 0u);
+        uint8_t* outb = a.out + a.out_offs[c] + (kOpen ? 0u : 12u);
+        const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(inb) & 3u);
+        const uint32_t* inw = reinterpret_cast<const uint32_t*>(inb - mis);
+        uint32_t* outw = reinterpret_cast<uint32_t*>(outb);
+        uint32_t acc[4] = {0u, 0u, 0u, 0u};
+        for (uint32_t u = u0; u < u1; u++) {
+            uint32_t st[4][4];
+            int64_t jb[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int64_t j = static_cast<int64_t>(256u * u + 64u * r + lane) - pre;
+                jb[r] = j;
+                st[r][0] = k.nonce[0];
+                st[r][1] = k.nonce[1];
+                st[r][2] = k.nonce[2];
+                st[r][3] = static_cast<uint32_t>(j + 2);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; r++) aes256_block(t, k.rk, st[r]);
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const int64_t j = jb[r];
+                const int64_t rem = j >= 0 ? static_cast<int64_t>(len) - 16 * j : 0;
+                const uint32_t hiB = rem <= 0 ? 0u : rem >= 16 ? 16u : static_cast<uint32_t>(rem);
+                uint32_t d[4] = {0u, 0u, 0u, 0u};
+                if (hiB) {
+                    const uint64_t w0 = 4ull * static_cast<uint64_t>(j);  // word index of the block in inw
+                    uint32_t w[5];
+#pragma unroll
+                    for (uint32_t q = 0; q < 5u; q++) w[q] = (4u * q < mis + hiB) ? inw[w0 + q] : 0u;
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        d[q] = __builtin_amdgcn_alignbit(w[q + 1], w[q], 8u * mis) & keep_mask(static_cast<int64_t>(hiB) - 4 * q);
+                }
+                uint32_t o[4], gin[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    o[q] = (d[q] ^ bswap32(st[r][q])) & keep_mask(static_cast<int64_t>(hiB) - 4 * q);
+                    gin[q] = bswap32(kOpen ? d[q] : o[q]);
+                }
+                if (hiB) {
+                    uint32_t* ow = outw + 4ull * static_cast<uint64_t>(j);
+#pragma unroll
+                    for (uint32_t q = 0; q < 4u; q++) {
+                        if (4u * q + 4u <= hiB) ow[q] = o[q];
+                        else if (4u * q < hiB) {
+                            uint8_t* ob = reinterpret_cast<uint8_t*>(ow + q);
+                            for (uint32_t b = 0; b < hiB - 4u * q; b++) ob[b] = static_cast<uint8_t>(o[q] >> (8 * b));
+                        }
+                    }
+                }
+                gcm_tab_mul(g, acc);
+#pragma unroll
+                for (int q = 0; q < 4; q++) acc[q] ^= gin[q];
+            }
+        }
+        // Lane l's last block is 63 - l blocks before the segment's end.
+        {
+            const uint32_t hl[4] = {k.hl[63u - lane][0], k.hl[63u - lane][1], k.hl[63u - lane][2], k.hl[63u - lane][3]};
+            gf_mul_in(acc, hl);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) acc[q] ^= __shfl_xor(acc[q], off, 64);
+        }
+        uint32_t after = nseg - 1u - sl;  // whole segments after this one
+        for (uint32_t i = 0; after; i++, after >>= 1)
+            if (after & 1u) {
+                const uint32_t hp[4] = {k.hp[i][0], k.hp[i][1], k.hp[i][2], k.hp[i][3]};
+                gf_mul_in(acc, hp);
+            }
+        if (lane < 4u) {
+            uint32_t mine = acc[0];
+#pragma unroll
+            for (int q = 1; q < 4; q++)
+                if (lane == static_cast<uint32_t>(q)) mine = acc[q];
+            atomicXor(&acc_keys[c].acc[lane], mine);
+        }
+    }
+}
+
+// One lane per chunk: AAD, text sum, length block, tag.
+template <bool kOpen>
+__global__ __launch_bounds__(256) void gcm_finish_kernel(CryptArgs a, const GcmKey* keys) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.n || a.status[c] != 0) return;
+    const GcmKey& k = keys[c];
+    const uint64_t len = static_cast<uint64_t>(k.len_lo) | (static_cast<uint64_t>(k.len_hi) << 32);
+    const uint32_t h[4] = {k.h[0], k.h[1], k.h[2], k.h[3]};
+    const uint8_t* ivp = a.ivs + static_cast<uint64_t>(c) * a.iv_stride;
+    const uint32_t il = a.iv_len;
+    uint32_t x[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t i = 0; i < il; i += 16u) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const uint32_t at = i + 4u * q + b;
+                w = (w << 8) | (at < il ? static_cast<uint32_t>(ivp[at]) : 0u);
+            }
+            x[q] ^= w;
+        }
+        gf_mul_in(x, h);
+    }
+    uint32_t hc[4];
+    gf_pow(h, (len + 15u) >> 4, hc);
+    gf_mul_in(x, hc);
+    uint32_t sc[4] = {k.acc[0], k.acc[1], k.acc[2], k.acc[3]};
+    gf_mul_in(sc, h);
+    const uint64_t abits = 8ull * il, cbits = 8ull * len;
+    x[0] ^= sc[0] ^ static_cast<uint32_t>(abits >> 32);
+    x[1] ^= sc[1] ^ static_cast<uint32_t>(abits);
+    x[2] ^= sc[2] ^ static_cast<uint32_t>(cbits >> 32);
+    x[3] ^= sc[3] ^ static_cast<uint32_t>(cbits);
+    gf_mul_in(x, h);
+    uint32_t tag[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) tag[q] = bswap32(x[q] ^ k.ej0[q]);  // little-endian words of the tag bytes
+    if (kOpen) {
+        const uint8_t* tp = a.in + a.in_offs[c] + 12u + len;
+        uint32_t diff = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) diff |= load_le32_bytes(tp + 4 * j) ^ tag[j];
+        a.status[c] = diff ? -74 : 0;  // EBADMSG
+    } else {
+        uint8_t* tp = a.out + a.out_offs[c] + 12u + len;
+#pragma unroll
+        for (int j = 0; j < 16; j++) tp[j] = static_cast<uint8_t>(tag[j >> 2] >> (8 * (j & 3)));
+    }
+}
+
 }  // namespace cryptdev
 
 namespace {
@@ -795,7 +1273,8 @@ struct CryptAlgo {
     uint32_t overhead;
 };
 // repo/encryption/chacha20_poly1305_hmac_sha256_encryptor.go:16,67 (name, Overhead())
-constexpr CryptAlgo kCryptAlgos[] = {{"CHACHA20-POLY1305-HMAC-SHA256", 28}};
+// aes256_gcm_hmac_sha256_encryptor.go:15,67-69,72 (AES256-GCM-HMAC-SHA256, Overhead() = 28)
+constexpr CryptAlgo kCryptAlgos[] = {{"AES256-GCM-HMAC-SHA256", 28}, {"CHACHA20-POLY1305-HMAC-SHA256", 28}};
 
 const CryptAlgo* find_crypt(const char* name) {
     if (!name) return nullptr;
@@ -828,6 +1307,23 @@ int units_grid(int* err) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             return *err = set_error(-5, "device attribute query failed"), 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, cryptdev::crypt_units_kernel<false>, 256, 0) != hipSuccess ||
+            per <= 0)
+            per = 2;
+        cached_grid = cus * per;
+        cached_dev = dev;
+    }
+    return cached_grid;
+}
+
+int gcm_grid(int* err) {
+    static thread_local int cached_dev = -1, cached_grid = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return *err = set_error(-5, "hipGetDevice failed"), 0;
+    if (dev != cached_dev) {
+        int cus = 0, per = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            return *err = set_error(-5, "device attribute query failed"), 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, cryptdev::gcm_units_kernel<false>, 256, 0) != hipSuccess ||
             per <= 0)
             per = 2;
         cached_grid = cus * per;
@@ -890,6 +1386,18 @@ int crypt_run(const char* name, const uint8_t* secret, uint32_t secret_len, cons
         cryptdev::sha256_compress(a.mid.out, ob);
     }
     hipStream_t st = static_cast<hipStream_t>(stream);
+    if (std::strcmp(name, "AES256-GCM-HMAC-SHA256") == 0) {
+        static_assert(sizeof(cryptdev::GcmKey) <= sizeof(ChunkKey) + kTabN * sizeof(Fe), "GcmKey fits the ChaCha slots");
+        cryptdev::GcmKey* gk = reinterpret_cast<cryptdev::GcmKey*>(w + l.keys);
+        const int ggrid = gcm_grid(&err);
+        if (err) return err;
+        hipLaunchKernelGGL(cryptdev::gcm_prep_kernel<kOpen>, dim3((n + 3u) / 4u), dim3(256), 0, st, a, gk);
+        hipLaunchKernelGGL(cryptdev::unit_scan_kernel, dim3(1), dim3(1024), 0, st, n, a.units);
+        hipLaunchKernelGGL(cryptdev::gcm_units_kernel<kOpen>, dim3(ggrid), dim3(256), 0, st, a, gk, gk, a.units);
+        hipLaunchKernelGGL(cryptdev::gcm_finish_kernel<kOpen>, dim3((n + 255u) / 256u), dim3(256), 0, st, a, gk);
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : set_error(-5, std::string("encryption kernel launch: ") + hipGetErrorString(e));
+    }
     hipLaunchKernelGGL(cryptdev::crypt_prep_kernel<kOpen>, dim3((n + 3u) / 4u), dim3(256), 0, st, a);
     hipLaunchKernelGGL(cryptdev::unit_scan_kernel, dim3(1), dim3(1024), 0, st, n, a.units);
     hipLaunchKernelGGL(cryptdev::crypt_units_kernel<kOpen>, dim3(grid), dim3(256), 0, st, a, a.keys, a.units, a.in_offs,

@@ -1,6 +1,7 @@
 """Content encryption of chunks on the GPU (C ABI: include/kcdc.h, kcdc_encrypt/decrypt_*),
-mirroring Kopia's encryption package for CHACHA20-POLY1305-HMAC-SHA256
-(repo/encryption/encryption.go: Encryptor, CreateEncryptor, SupportedAlgorithms, deriveKey;
+mirroring Kopia's encryption package for AES256-GCM-HMAC-SHA256 (the default) and
+CHACHA20-POLY1305-HMAC-SHA256 (repo/encryption/encryption.go: Encryptor, CreateEncryptor,
+SupportedAlgorithms, deriveKey; aes256_gcm_hmac_sha256_encryptor.go;
 chacha20_poly1305_hmac_sha256_encryptor.go; aead_helpers.go).  Many chunks per launch; the
 content ID's last 16 bytes are the per-content IV (content_manager_lock_free.go:178-182).
 No CPU fallback for the byte path: the library must be loaded."""
@@ -16,6 +17,8 @@ import numpy as np
 from . import _lib
 
 ChaCha20Poly1305 = "CHACHA20-POLY1305-HMAC-SHA256"
+Aes256Gcm = "AES256-GCM-HMAC-SHA256"
+DefaultAlgorithm = Aes256Gcm  # encryption.go DefaultAlgorithm
 PurposeEncryptionKey = b"encryption"  # encryption.go purposeEncryptionKey
 KeyDerivationSecretSize = 32  # chacha20KeyDerivationSecretSize
 NonceSize = 12

@@ -51,8 +51,9 @@ def test_host_mirror_and_registry():
     from kopia_amd import encryption as ke
     m = bytes(range(32))
     assert ke.derive_key(m) == aead.derive_key(m)
-    assert ke.SupportedAlgorithms() == ["CHACHA20-POLY1305-HMAC-SHA256"]
+    assert ke.SupportedAlgorithms() == ["AES256-GCM-HMAC-SHA256", "CHACHA20-POLY1305-HMAC-SHA256"]
     assert ke.overhead("CHACHA20-POLY1305-HMAC-SHA256") == 28
+    assert ke.overhead("AES256-GCM-HMAC-SHA256") == 28  # aes256GCMHmacSha256Overhead
     offs, total = ke.sealed_layout([0, 1, 5, 100])
     assert offs.tolist() == [0, 28, 60, 96] and total == 224
 

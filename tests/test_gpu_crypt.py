@@ -1,6 +1,8 @@
-"""GPU: CHACHA20-POLY1305-HMAC-SHA256 content encryption of many chunks
-(kcdc_encrypt/decrypt_chunks_device) bit-exact against the oracle (oracle/aead.py, pinned by
-RFC 8439 / RFC 5869 vectors in tests/test_aead_oracle.py): random lengths across the 16-byte,
+"""GPU: content encryption of many chunks (kcdc_encrypt/decrypt_chunks_device) with both device
+encryptors, CHACHA20-POLY1305-HMAC-SHA256 and AES256-GCM-HMAC-SHA256 (Kopia's default), bit-exact
+against the oracles (oracle/aead.py, pinned by RFC 8439 / RFC 5869 vectors in
+tests/test_aead_oracle.py; oracle/aesgcm.py, pinned by FIPS-197 / GCM vectors in
+tests/test_aesgcm_oracle.py): random lengths across the 16-byte,
 64-byte and 4 KiB unit boundaries, misaligned plaintext offsets, empty chunks, the chunks the
 splitter cuts and hashes on config-2 streams (IV = the content hash), round trips, and the
 authentication-failure / short-input / error contract; the reference's own ciphertext samples
@@ -11,11 +13,17 @@ import pytest
 from kopia_amd import _lib, batch
 from kopia_amd import encryption as ke
 from kopia_amd import hashing as kh
-from oracle import aead, coracle
+from oracle import aead, aesgcm, coracle
 
 pytestmark = pytest.mark.gpu
 SEED = 0x6B6F706961
-ALG = ke.ChaCha20Poly1305
+ALGS = [ke.ChaCha20Poly1305, ke.Aes256Gcm]
+ORACLE = {ke.ChaCha20Poly1305: aead, ke.Aes256Gcm: aesgcm}
+
+
+@pytest.fixture(params=ALGS)
+def alg(request):
+    return request.param
 MASTER = bytes(range(100, 132))
 
 
@@ -41,20 +49,20 @@ def _open(enc, sealed, soffs, slens, ivs, dev):
     return out.cpu().numpy(), po, st.cpu().numpy()
 
 
-def test_rfc_shaped_single(gpu):
+def test_rfc_shaped_single(alg, gpu):
     """One chunk, fixed secret / IV / nonce, equals the oracle's Encrypt."""
-    enc = ke.Encryptor(ALG, MASTER)
+    enc = ke.Encryptor(alg, MASTER)
     pt = b"Ladies and Gentlemen of the class of '99: If I could offer you only one tip for the future, sunscreen would be it."
     host = np.frombuffer(pt, np.uint8).copy()
     iv = bytes(range(16))
     nonce = bytes(range(40, 52))
     out, oo, st = _seal(enc, host, [0], [len(pt)], [iv], nonce, gpu)
     assert st.tolist() == [0]
-    want = aead.kopia_encrypt(aead.derive_key(MASTER), iv, nonce, pt)
+    want = ORACLE[alg].kopia_encrypt(aead.derive_key(MASTER), iv, nonce, pt)
     assert out[:len(want)].tobytes() == want
 
 
-def test_random_chunks(gpu):
+def test_random_chunks(alg, gpu):
     rng = np.random.default_rng(7)
     host = coracle.gen_stream(SEED, 3, 3 << 20)
     lens = list(rng.integers(0, 70000, 300))
@@ -64,13 +72,13 @@ def test_random_chunks(gpu):
     offs = np.array([int(rng.integers(0, host.size - int(L))) for L in lens], dtype=np.int64)
     ivs = [bytes(rng.integers(0, 256, 16, dtype=np.uint8)) for _ in lens]
     nonces = bytes(rng.integers(0, 256, 12 * len(lens), dtype=np.uint8))
-    enc = ke.Encryptor(ALG, MASTER)
+    enc = ke.Encryptor(alg, MASTER)
     secret = aead.derive_key(MASTER)
     out, oo, st = _seal(enc, host, offs, lens, ivs, nonces, gpu)
     assert not st.any()
     bad = []
     for i in range(len(lens)):
-        want = aead.kopia_encrypt(secret, ivs[i], nonces[12 * i:12 * i + 12], host[offs[i]:offs[i] + lens[i]].tobytes())
+        want = ORACLE[alg].kopia_encrypt(secret, ivs[i], nonces[12 * i:12 * i + 12], host[offs[i]:offs[i] + lens[i]].tobytes())
         if out[oo[i]:oo[i] + len(want)].tobytes() != want:
             bad.append((i, int(lens[i])))
     assert not bad, bad[:10]
@@ -86,7 +94,7 @@ def test_random_chunks(gpu):
         assert plain[po[i]:po[i] + lens[i]].tobytes() == host[offs[i]:offs[i] + lens[i]].tobytes(), i
 
 
-def test_open_rejects(gpu):
+def test_open_rejects(alg, gpu):
     """A flipped ciphertext, tag or nonce byte, a wrong IV, and a too-short input fail
     (aeadOpenPrefixedWithNonce: "unable to decrypt content" / "ciphertext too short"); the
     untouched chunks of the same call still open."""
@@ -94,7 +102,7 @@ def test_open_rejects(gpu):
     n, L = 8, 5000
     host = rng.integers(0, 256, n * L, dtype=np.uint8)
     ivs = [bytes([i]) * 16 for i in range(n)]
-    enc = ke.Encryptor(ALG, MASTER)
+    enc = ke.Encryptor(alg, MASTER)
     out, oo, st = _seal(enc, host, np.arange(n) * L, [L] * n, ivs, None, gpu)
     assert not st.any()
     slens = np.full(n, L + 28, np.int64)
@@ -112,10 +120,10 @@ def test_open_rejects(gpu):
         assert plain[po[i]:po[i] + L].tobytes() == host[i * L:(i + 1) * L].tobytes()
 
 
-def test_nonces_differ_by_default(gpu):
+def test_nonces_differ_by_default(alg, gpu):
     """Without caller nonces, two seals of the same chunk differ (random nonce prefix) and
     both open."""
-    enc = ke.Encryptor(ALG, MASTER)
+    enc = ke.Encryptor(alg, MASTER)
     host = np.arange(3000, dtype=np.uint8)
     a, oo, _ = _seal(enc, host, [0], [3000], [bytes(16)], None, gpu)
     b, _, _ = _seal(enc, host, [0], [3000], [bytes(16)], None, gpu)
@@ -125,7 +133,7 @@ def test_nonces_differ_by_default(gpu):
         assert st.tolist() == [0] and plain[:3000].tobytes() == host.tobytes()
 
 
-def test_config2_pipeline(gpu):
+def test_config2_pipeline(alg, gpu):
     """split -> hash (BLAKE2B-256-128, content ID) -> encrypt with IV = content ID, all on the
     device, on 64 x 4 MiB config-2 streams; every sealed chunk equals the oracle's Encrypt of
     the same bytes with the same nonce, and the device decryptor round-trips the batch."""
@@ -142,7 +150,7 @@ def test_config2_pipeline(gpu):
     ids = ids.contiguous()
     n = len(offs)
     nonces = bytes(np.random.default_rng(3).integers(0, 256, 12 * n, dtype=np.uint8))
-    enc = ke.Encryptor(ALG, MASTER)
+    enc = ke.Encryptor(alg, MASTER)
     oo, total = ke.sealed_layout(lens)
     out = torch.empty(total, dtype=torch.uint8, device=dev)
     st = enc.encrypt_chunks_device(data.data_ptr(), offs, lens, ids, 16, out, oo, dev, nonces=nonces)
@@ -150,8 +158,8 @@ def test_config2_pipeline(gpu):
     assert not st.cpu().numpy().any()
     host, got, idh = data.cpu().numpy(), out.cpu().numpy(), ids.cpu().numpy()
     secret = aead.derive_key(MASTER)
-    for i in range(0, n, max(1, n // 24)):  # the oracle's ChaCha20 runs ~25 MB/s: a spread sample
-        want = aead.kopia_encrypt(secret, idh[i].tobytes(), nonces[12 * i:12 * i + 12],
+    for i in range(0, n, max(1, n // (24 if alg == ke.ChaCha20Poly1305 else 8))):  # oracles run ~3-25 MB/s: a spread sample
+        want = ORACLE[alg].kopia_encrypt(secret, idh[i].tobytes(), nonces[12 * i:12 * i + 12],
                                   host[offs[i]:offs[i] + lens[i]].tobytes())
         assert got[oo[i]:oo[i] + lens[i] + 28].tobytes() == want, i
     plain = torch.zeros(ke.plain_layout(lens + 28)[1], dtype=torch.uint8, device=dev)
@@ -163,16 +171,16 @@ def test_config2_pipeline(gpu):
     assert all(p[po[i]:po[i] + lens[i]].tobytes() == host[offs[i]:offs[i] + lens[i]].tobytes() for i in range(n))
 
 
-def test_reference_samples(gpu):
+def test_reference_samples(alg, gpu):
     """The reference's TestCiphertextSamples (encryption_test.go:97-127) on the device: each
     CHACHA20-POLY1305-HMAC-SHA256 sample (32-byte content IDs) opens to its payload, and sealing
     the payload with the sample's nonce reproduces the sample byte for byte."""
     from conftest import golden
     import torch
     for c in golden("kopia_encryption_samples.json")["cases"]:
-        enc = ke.Encryptor(ALG, c["master_key"].encode())
+        enc = ke.Encryptor(alg, c["master_key"].encode())
         cid, payload = c["content_id"].encode(), c["payload"].encode()
-        sample = bytes.fromhex(c["samples"][ALG])
+        sample = bytes.fromhex(c["samples"][alg])
         d_id = torch.frombuffer(bytearray(cid), dtype=torch.uint8).to(gpu)
         d_in = torch.frombuffer(bytearray(sample), dtype=torch.uint8).to(gpu)
         plain = torch.zeros(len(payload) + 8, dtype=torch.uint8, device=gpu)
@@ -191,7 +199,7 @@ def test_reference_samples(gpu):
 
 
 @pytest.mark.parametrize("iv_len", [1, 15, 17, 32, 55, 56, 63, 64])
-def test_content_id_lengths(gpu, iv_len):
+def test_content_id_lengths(alg, gpu, iv_len):
     """Content IDs of 1..64 bytes (HMAC message of one or two SHA-256 blocks, AAD of 1..4
     Poly1305 blocks) against the oracle."""
     import torch
@@ -202,7 +210,7 @@ def test_content_id_lengths(gpu, iv_len):
     offs = np.concatenate(([1], 1 + np.cumsum(lens)[:-1])).astype(np.int64)
     ids = rng.integers(0, 256, (n, 64), dtype=np.uint8)
     nonces = bytes(rng.integers(0, 256, 12 * n, dtype=np.uint8))
-    enc = ke.Encryptor(ALG, MASTER)
+    enc = ke.Encryptor(alg, MASTER)
     d = torch.from_numpy(host).to(gpu)
     d_ids = torch.from_numpy(ids).to(gpu)
     oo, total = ke.sealed_layout(lens)
@@ -213,52 +221,52 @@ def test_content_id_lengths(gpu, iv_len):
     got = out.cpu().numpy()
     secret = aead.derive_key(MASTER)
     for i in range(n):
-        want = aead.kopia_encrypt(secret, ids[i, :iv_len].tobytes(), nonces[12 * i:12 * i + 12],
+        want = ORACLE[alg].kopia_encrypt(secret, ids[i, :iv_len].tobytes(), nonces[12 * i:12 * i + 12],
                                   host[offs[i]:offs[i] + lens[i]].tobytes())
         assert got[oo[i]:oo[i] + lens[i] + 28].tobytes() == want, i
 
 
-def test_errors(gpu):
+def test_errors(alg, gpu):
     import torch
-    enc = ke.Encryptor(ALG, MASTER)
+    enc = ke.Encryptor(alg, MASTER)
     d = torch.zeros(64, dtype=torch.uint8, device=gpu)
     with pytest.raises(_lib.KcdcError):
         ke.Encryptor("AES128-GCM", MASTER)
     L = _lib.lib()
     def call(secret_len, iv_len, work):
-        return L.kcdc_encrypt_chunks_device(ALG.encode(), enc.secret, secret_len, d.data_ptr(), d.data_ptr(),
+        return L.kcdc_encrypt_chunks_device(alg.encode(), enc.secret, secret_len, d.data_ptr(), d.data_ptr(),
                                             d.data_ptr(), 1, d.data_ptr(), iv_len, 16, d.data_ptr(), d.data_ptr(),
                                             d.data_ptr(), d.data_ptr(), d.data_ptr(), work, None)
     assert call(65, 16, 1 << 20) == _lib.KCDC_EINVAL  # secret > 64 bytes
     assert call(32, 16, 64) == _lib.KCDC_EINVAL       # workspace too small
     assert call(32, 0, 1 << 20) == _lib.KCDC_EINVAL   # empty content ID
     assert call(32, 65, 1 << 20) == _lib.KCDC_EINVAL  # content ID > 64 bytes
-    assert ke.overhead(ALG) == 28
+    assert ke.overhead(alg) == 28
 
 
-def test_large_chunk_power_table(gpu):
+def test_large_chunk_power_table(alg, gpu):
     """An 80 MiB chunk: 5.2 M Poly1305 blocks, so the unit exponents reach the table's top level
     (r^(2^20 d)); sealed bytes and tag equal the oracle's, and the device opens it."""
     import torch
-    n = 80 << 20
+    n = 80 << 20 if alg == ke.ChaCha20Poly1305 else (24 << 20) + 5  # AES: 97 GHASH segments, numpy oracle
     host = coracle.gen_stream(SEED, 40, n + 3)
     iv = bytes(range(200, 216))
     nonce = bytes(range(12))
-    enc = ke.Encryptor(ALG, MASTER)
+    enc = ke.Encryptor(alg, MASTER)
     out, oo, st = _seal(enc, host, [3], [n], [iv], nonce, gpu)
     assert st.tolist() == [0]
-    want = aead.kopia_encrypt(aead.derive_key(MASTER), iv, nonce, host[3:3 + n].tobytes())
+    want = ORACLE[alg].kopia_encrypt(aead.derive_key(MASTER), iv, nonce, host[3:3 + n].tobytes())
     assert out[:n + 28].tobytes() == want
     plain, po, st2 = _open(enc, out[:n + 28], [0], [n + 28], [iv], gpu)
     assert st2.tolist() == [0] and plain[:n].tobytes() == host[3:3 + n].tobytes()
     del torch
 
 
-def test_too_long_chunk_and_empty_call(gpu):
+def test_too_long_chunk_and_empty_call(alg, gpu):
     """A chunk of 1 GiB + 1 byte reports KCDC_EFBIG (exponents stay below 2^26) while its
     neighbour seals normally; an empty call does nothing."""
     import torch
-    enc = ke.Encryptor(ALG, MASTER)
+    enc = ke.Encryptor(alg, MASTER)
     big = (1 << 30) + 1
     d = torch.zeros(big + 64, dtype=torch.uint8, device=gpu)
     ids = torch.zeros((2, 16), dtype=torch.uint8, device=gpu)
@@ -268,7 +276,7 @@ def test_too_long_chunk_and_empty_call(gpu):
     st = enc.encrypt_chunks_device(d.data_ptr(), [0, 64], lens, ids, 16, out, oo, gpu, nonces=bytes(24))
     torch.cuda.synchronize()
     assert st.cpu().tolist() == [_lib.KCDC_EFBIG, 0]
-    want = aead.kopia_encrypt(aead.derive_key(MASTER), bytes(16), bytes(12), bytes(100))
+    want = ORACLE[alg].kopia_encrypt(aead.derive_key(MASTER), bytes(16), bytes(12), bytes(100))
     assert out.cpu().numpy()[256:256 + 128].tobytes() == want
     st0 = enc.encrypt_chunks_device(d.data_ptr(), [], [], ids, 16, out, [], gpu)
     assert st0.numel() == 0

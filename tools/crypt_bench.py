@@ -1,4 +1,4 @@
-"""Seal/open timing of CHACHA20-POLY1305-HMAC-SHA256 over a synthetic chunk table (A/B of
+"""Seal/open timing of a device encryptor (--algo) over a synthetic chunk table (A/B of
 library builds via KCDC_LIB; not a parity test -- tests/test_gpu_crypt.py is)."""
 import argparse
 import json
@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--gib", type=float, default=4.0)
     ap.add_argument("--avg-mib", type=float, default=4.0)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--algo", default="CHACHA20-POLY1305-HMAC-SHA256")
     args = ap.parse_args()
     import torch
     from kopia_amd import encryption as ke
@@ -30,7 +31,7 @@ def main():
     offs = np.concatenate(([3], 3 + np.cumsum(lens)[:-1])).astype(np.int64)  # misaligned
     data = torch.randint(0, 256, (int(offs[-1] + lens[-1] + 8),), dtype=torch.uint8, device=dev)
     ids = torch.randint(0, 256, (len(lens), 16), dtype=torch.uint8, device=dev)
-    enc = ke.Encryptor(ke.ChaCha20Poly1305, bytes(range(32)))
+    enc = ke.Encryptor(args.algo, bytes(range(32)))
     oo, st_total = ke.sealed_layout(lens)
     out = torch.empty(st_total, dtype=torch.uint8, device=dev)
     po, pt_total = ke.plain_layout(lens + 28)
