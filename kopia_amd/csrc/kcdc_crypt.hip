@@ -847,22 +847,36 @@ __device__ __forceinline__ uint32_t aes_sbox_entry(uint32_t x) {
     return out;
 }
 
-// Te0[x] = {2S, S, S, 3S} big-endian; Te1..Te3 are its byte rotations.  Sb[x] = S.
-struct AesTabs {
-    uint32_t te[4][256];
+// Te0[x] = {2S, S, S, 3S} big-endian, Te1 = ror8(Te0); Te2 = ror16(Te0), Te3 = ror16(Te1) are one
+// v_alignbit each.  Row x (256 bytes) holds 32 copies of Te0[x] then 32 of Te1[x]: lane l reads
+// copy l & 31, so the 32 lanes of a ds_read_b32 group hit 32 distinct banks (one shared table
+// was 60 % bank-conflict cycles), and the byte address (x << 8) | lane offset is ONE v_perm of
+// the state word.  Kernels keep the table first in their LDS so the base folds
+// into the ds_read offset.  Sb[x] = S for the key schedule.
+struct alignas(256) AesTabs {
+    uint32_t te[256 * 64];
     uint32_t sb[256];
 };
 __device__ __forceinline__ void aes_tabs_build(AesTabs& t, uint32_t tid, uint32_t nthreads) {
     for (uint32_t x = tid; x < 256u; x += nthreads) {
-        const uint32_t s = aes_sbox_entry(x), s2 = xt8(s), s3 = s2 ^ s;
-        const uint32_t w = (s2 << 24) | (s << 16) | (s << 8) | s3;
-        t.te[0][x] = w;
-        t.te[1][x] = ror32(w, 8);
-        t.te[2][x] = ror32(w, 16);
-        t.te[3][x] = ror32(w, 24);
-        t.sb[x] = s;
+        const uint32_t sx = aes_sbox_entry(x), s2 = xt8(sx), s3 = s2 ^ sx;
+        const uint32_t w = (s2 << 24) | (sx << 16) | (sx << 8) | s3, w1 = ror32(w, 8);
+#pragma unroll 8
+        for (uint32_t c = 0; c < 64u; c++) {
+            const uint32_t cc = (c + x) & 63u;  // lanes start on different banks
+            t.te[64u * x + cc] = (cc & 32u) ? w1 : w;
+        }
+        t.sb[x] = sx;
     }
 }
+// LDS byte address of a table entry: byte k of s in address byte 1, the lane's copy offset
+// (in byte 0 of `off`: 4 (lane & 31), + 128 for Te1) in byte 0.
+template <int k>
+__device__ __forceinline__ uint32_t te_at(const AesTabs& t, uint32_t s, uint32_t off) {
+    const uint32_t byte = __builtin_amdgcn_perm(s, off, 0x0C0C0000u | ((4u + k) << 8));
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(t.te) + byte);
+}
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
 
 __device__ __forceinline__ void aes256_expand(const AesTabs& t, const uint32_t (&key)[8], uint32_t (&rk)[60]) {
 #pragma unroll
@@ -882,22 +896,30 @@ __device__ __forceinline__ void aes256_expand(const AesTabs& t, const uint32_t (
     }
 }
 
+// One block in place; o0 / o1 = the lane's Te0 / Te1 copy offsets (4 (lane & 31), + 128).
 template <typename RK>
-__device__ __forceinline__ void aes256_block(const AesTabs& t, const RK& rk, uint32_t (&s)[4]) {
+__device__ __forceinline__ void aes256_block(const AesTabs& t, uint32_t o0, uint32_t o1, const RK& rk, uint32_t (&s)[4]) {
     uint32_t s0 = s[0] ^ rk[0], s1 = s[1] ^ rk[1], s2 = s[2] ^ rk[2], s3 = s[3] ^ rk[3];
+    auto col = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+        const uint32_t t0 = te_at<3>(t, a, o0), t1 = te_at<2>(t, b, o1);
+        const uint32_t t2 = ror32(te_at<1>(t, c, o0), 16), t3 = ror32(te_at<0>(t, d, o1), 16);
+        return xor3(xor3(t0, t1, t2), t3, k);
+    };
 #pragma unroll
     for (int r = 1; r < 14; r++) {
-        const uint32_t t0 = t.te[0][s0 >> 24] ^ t.te[1][(s1 >> 16) & 255u] ^ t.te[2][(s2 >> 8) & 255u] ^ t.te[3][s3 & 255u] ^ rk[4 * r];
-        const uint32_t t1 = t.te[0][s1 >> 24] ^ t.te[1][(s2 >> 16) & 255u] ^ t.te[2][(s3 >> 8) & 255u] ^ t.te[3][s0 & 255u] ^ rk[4 * r + 1];
-        const uint32_t t2 = t.te[0][s2 >> 24] ^ t.te[1][(s3 >> 16) & 255u] ^ t.te[2][(s0 >> 8) & 255u] ^ t.te[3][s1 & 255u] ^ rk[4 * r + 2];
-        const uint32_t t3 = t.te[0][s3 >> 24] ^ t.te[1][(s0 >> 16) & 255u] ^ t.te[2][(s1 >> 8) & 255u] ^ t.te[3][s2 & 255u] ^ rk[4 * r + 3];
+        const uint32_t t0 = col(s0, s1, s2, s3, rk[4 * r]);
+        const uint32_t t1 = col(s1, s2, s3, s0, rk[4 * r + 1]);
+        const uint32_t t2 = col(s2, s3, s0, s1, rk[4 * r + 2]);
+        const uint32_t t3 = col(s3, s0, s1, s2, rk[4 * r + 3]);
         s0 = t0;
         s1 = t1;
         s2 = t2;
         s3 = t3;
     }
+    // Last round: S(x) is byte 2 and byte 1 of Te0[x]; two v_perm assemble the column.
     auto fin = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
-        return ((t.sb[a >> 24] << 24) | (t.sb[(b >> 16) & 255u] << 16) | (t.sb[(c >> 8) & 255u] << 8) | t.sb[d & 255u]) ^ k;
+        const uint32_t ea = te_at<3>(t, a, o0), eb = te_at<2>(t, b, o0), ec = te_at<1>(t, c, o0), ed = te_at<0>(t, d, o0);
+        return xor3(__builtin_amdgcn_perm(ea, eb, 0x06020C0Cu), __builtin_amdgcn_perm(ec, ed, 0x0C0C0501u), k);
     };
     s[0] = fin(s0, s1, s2, s3, rk[56]);
     s[1] = fin(s1, s2, s3, s0, rk[57]);
@@ -962,7 +984,7 @@ __device__ __forceinline__ void gcm_layout(uint64_t len, uint32_t& pre, uint32_t
 // One wave per chunk: HMAC key, key schedule, H, E(J0), powers of H; the nonce for seal.
 template <bool kOpen>
 __global__ __launch_bounds__(256) void gcm_prep_kernel(CryptArgs a, GcmKey* keys) {
-    __shared__ AesTabs t;
+    __shared__ AesTabs t;  // the kernel's only LDS object: at address 0
     aes_tabs_build(t, threadIdx.x, 256u);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
@@ -985,9 +1007,10 @@ __global__ __launch_bounds__(256) void gcm_prep_kernel(CryptArgs a, GcmKey* keys
     uint32_t rk[60];
     aes256_expand(t, key, rk);
     uint32_t h[4] = {0u, 0u, 0u, 0u};
-    aes256_block(t, rk, h);
+    const uint32_t o0 = 4u * (lane & 31u), o1 = o0 + 128u;
+    aes256_block(t, o0, o1, rk, h);
     uint32_t ej0[4] = {bswap32(nonce[0]), bswap32(nonce[1]), bswap32(nonce[2]), 1u};
-    aes256_block(t, rk, ej0);
+    aes256_block(t, o0, o1, rk, ej0);
     GcmKey& k = keys[c];
     // Lane l: H^l, and for l < 12 H^(16384 * 2^l) = H^(2^(14 + l)); lane 0 also H^64.
     uint32_t p[4];
@@ -1031,8 +1054,8 @@ __global__ __launch_bounds__(256) void gcm_prep_kernel(CryptArgs a, GcmKey* keys
 
 // GHASH tables of one wave: tab[k][n] = (nibble n at position k) * M, position k = bits 4k..4k+3
 // of the big-endian 128-bit value (k = 0: the low bits of w[3]).
-struct GcmWave {
-    uint32_t tab[32][16][4];
+struct alignas(256) GcmWave {
+    alignas(256) uint32_t tab[32][16][4];  // 16-byte aligned rows: ds_read_b128, banks mod 64
     uint32_t p[128][4];  // M * x^i
 };
 
@@ -1069,19 +1092,20 @@ __device__ __forceinline__ void gcm_tab_build(GcmWave& g, const uint32_t (&m)[4]
     wave_lds_sync();
 }
 
-// x = x * M through the wave's tables.
+// x = x * M through the wave's tables (two entries per 3-input XOR).
 __device__ __forceinline__ void gcm_tab_mul(const GcmWave& g, uint32_t (&x)[4]) {
     uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
 #pragma unroll
     for (int w = 0; w < 4; w++) {
         const uint32_t xw = x[3 - w];  // positions 8w .. 8w+7 live in word 3 - w
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
+        for (int q = 0; q < 8; q += 2) {
             const uint4 e = *reinterpret_cast<const uint4*>(g.tab[8 * w + q][(xw >> (4 * q)) & 15u]);
-            z0 ^= e.x;
-            z1 ^= e.y;
-            z2 ^= e.z;
-            z3 ^= e.w;
+            const uint4 f = *reinterpret_cast<const uint4*>(g.tab[8 * w + q + 1][(xw >> (4 * q + 4)) & 15u]);
+            z0 = xor3(z0, e.x, f.x);
+            z1 = xor3(z1, e.y, f.y);
+            z2 = xor3(z2, e.z, f.z);
+            z3 = xor3(z3, e.w, f.w);
         }
     }
     x[0] = z0;
@@ -1090,20 +1114,31 @@ __device__ __forceinline__ void gcm_tab_mul(const GcmWave& g, uint32_t (&x)[4]) 
     x[3] = z3;
 }
 
+#ifndef KCDC_GCM_WAVES
+#define KCDC_GCM_WAVES 2  // waves per SIMD the register budget is sized for
+#endif
+#ifndef KCDC_GCM_RB
+#define KCDC_GCM_RB 2  // AES blocks in flight per lane (rows of a unit per batch)
+#endif
+constexpr uint32_t kGcmWaves = 8;  // waves per workgroup: one 64 KiB table, 8 GHASH tables, 146 KiB
+struct GcmLds {
+    AesTabs t;  // first: at LDS address 0
+    GcmWave gw[kGcmWaves];
+};
 template <bool kOpen>
-__global__ __launch_bounds__(256) void gcm_units_kernel(CryptArgs a, const GcmKey* __restrict__ keys,
-                                                         GcmKey* acc_keys, const uint32_t* __restrict__ segp) {
-    __shared__ AesTabs t;
-    __shared__ GcmWave gw[4];
-    aes_tabs_build(t, threadIdx.x, 256u);
+__global__ __launch_bounds__(64 * kGcmWaves) __attribute__((amdgpu_waves_per_eu(KCDC_GCM_WAVES, KCDC_GCM_WAVES))) void gcm_units_kernel(
+    CryptArgs a, const GcmKey* __restrict__ keys, GcmKey* acc_keys, const uint32_t* __restrict__ segp) {
+    __shared__ GcmLds L;
+    aes_tabs_build(L.t, threadIdx.x, 64u * kGcmWaves);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t o0 = 4u * (lane & 31u), o1 = o0 + 128u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    GcmWave& g = gw[wv];
+    GcmWave& g = L.gw[wv];
     const uint32_t total = segp[a.n];
-    const uint32_t nw = gridDim.x * 4u;
+    const uint32_t nw = gridDim.x * kGcmWaves;
     uint32_t cur = 0xFFFFFFFFu;
-    for (uint32_t s = blockIdx.x * 4u + wv; s < total; s += nw) {
+    for (uint32_t s = blockIdx.x * kGcmWaves + wv; s < total; s += nw) {
         uint32_t lo = 0, hi = a.n;  // segp[lo] <= s < segp[hi]
         while (hi - lo > 1u) {
             const uint32_t mid = (lo + hi) >> 1;
@@ -1133,12 +1168,14 @@ __global__ __launch_bounds__(256) void gcm_units_kernel(CryptArgs a, const GcmKe
         const uint32_t* inw = reinterpret_cast<const uint32_t*>(inb - mis);
         uint32_t* outw = reinterpret_cast<uint32_t*>(outb);
         uint32_t acc[4] = {0u, 0u, 0u, 0u};
-        for (uint32_t u = u0; u < u1; u++) {
-            uint32_t st[4][4];
-            int64_t jb[4];
+        for (uint32_t u = u0; u < u1; u++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int64_t j = static_cast<int64_t>(256u * u + 64u * r + lane) - pre;
+        for (int rb = 0; rb < 4; rb += KCDC_GCM_RB) {
+            uint32_t st[KCDC_GCM_RB][4];
+            int64_t jb[KCDC_GCM_RB];
+#pragma unroll
+            for (int r = 0; r < KCDC_GCM_RB; r++) {
+                const int64_t j = static_cast<int64_t>(256u * u + 64u * (rb + r) + lane) - pre;
                 jb[r] = j;
                 st[r][0] = k.nonce[0];
                 st[r][1] = k.nonce[1];
@@ -1146,9 +1183,9 @@ __global__ __launch_bounds__(256) void gcm_units_kernel(CryptArgs a, const GcmKe
                 st[r][3] = static_cast<uint32_t>(j + 2);
             }
 #pragma unroll
-            for (int r = 0; r < 4; r++) aes256_block(t, k.rk, st[r]);
+            for (int r = 0; r < KCDC_GCM_RB; r++) aes256_block(L.t, o0, o1, k.rk, st[r]);
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
+            for (int r = 0; r < KCDC_GCM_RB; r++) {
                 const int64_t j = jb[r];
                 const int64_t rem = j >= 0 ? static_cast<int64_t>(len) - 16 * j : 0;
                 const uint32_t hiB = rem <= 0 ? 0u : rem >= 16 ? 16u : static_cast<uint32_t>(rem);
@@ -1323,7 +1360,7 @@ int gcm_grid(int* err) {
         int cus = 0, per = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             return *err = set_error(-5, "device attribute query failed"), 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, cryptdev::gcm_units_kernel<false>, 256, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, cryptdev::gcm_units_kernel<false>, 64 * cryptdev::kGcmWaves, 0) != hipSuccess ||
             per <= 0)
             per = 2;
         cached_grid = cus * per;
@@ -1393,7 +1430,7 @@ int crypt_run(const char* name, const uint8_t* secret, uint32_t secret_len, cons
         if (err) return err;
         hipLaunchKernelGGL(cryptdev::gcm_prep_kernel<kOpen>, dim3((n + 3u) / 4u), dim3(256), 0, st, a, gk);
         hipLaunchKernelGGL(cryptdev::unit_scan_kernel, dim3(1), dim3(1024), 0, st, n, a.units);
-        hipLaunchKernelGGL(cryptdev::gcm_units_kernel<kOpen>, dim3(ggrid), dim3(256), 0, st, a, gk, gk, a.units);
+        hipLaunchKernelGGL(cryptdev::gcm_units_kernel<kOpen>, dim3(ggrid), dim3(64 * cryptdev::kGcmWaves), 0, st, a, gk, gk, a.units);
         hipLaunchKernelGGL(cryptdev::gcm_finish_kernel<kOpen>, dim3((n + 255u) / 256u), dim3(256), 0, st, a, gk);
         const hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : set_error(-5, std::string("encryption kernel launch: ") + hipGetErrorString(e));
