@@ -46,6 +46,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICRO
 # 256 CUs x 4 SIMDs x 16 lanes per cycle at the ~2.0 GHz the chip holds under load (DVFS,
 # MI355X_MICROARCH.md) -> 2.0e9 x 16,384 x 64 / 990 = 2.12 TB/s of plaintext.
 CHACHA_VALU_CEILING_GBS = 2118.0
+# AES256-GCM's byte pass (T-table AES-256 + 4-bit-table GHASH): 716 VALU per 16-byte block per lane,
+# measured (SQ_INSTS_VALU of gcm_units_kernel, profiles/r02/aes/pmc_sq.csv: 1.2e10 over 4 seals of
+# 268 M blocks) -> 2.0e9 x 16,384 x 16 / 716 = 732 GB/s of plaintext.
+AES_VALU_CEILING_GBS = 732.0
 GiB = float(1 << 30)
 
 
@@ -335,6 +339,7 @@ def bench_batch(args, comm: Comm):
         out["hash"] = bench_hash(args, data, ns, L, cuts, dev)
     if args.encrypt and rank == 0 and world == 1:
         out["encrypt"] = bench_encrypt(args, data, ns, L, cuts, dev)
+        out["encrypt_aes"] = bench_encrypt(args, data, ns, L, cuts, dev, "AES256-GCM-HMAC-SHA256")
 
     if rank == 0 and world == 1 and not args.no_host_inclusive:
         # host-inclusive: pageable host buffers -> H2D -> kernel -> D2H (kcdc_split_batch_host)
@@ -421,8 +426,9 @@ def bench_hash(args, data, ns: int, L: int, cuts: list, dev) -> dict:
             "cpu_hashlib_1thread_gib_s": round(cpu, 3)}
 
 
-def bench_encrypt(args, data, ns: int, L: int, cuts: list, dev) -> dict:
-    """§8f #4: CHACHA20-POLY1305-HMAC-SHA256 of every chunk the split produced, keyed by its
+def bench_encrypt(args, data, ns: int, L: int, cuts: list, dev, algo: str = "CHACHA20-POLY1305-HMAC-SHA256") -> dict:
+    """§8f #4: `algo` (CHACHA20-POLY1305-HMAC-SHA256, or AES256-GCM-HMAC-SHA256, Kopia's default)
+    of every chunk the split produced, keyed by its
     content ID (BLAKE2B-256-128 on the device), as content_manager_lock_free.go:178-182 does.
     Times seal (and open) of the whole batch: 4 launches each (key/power table, unit scan,
     byte pass, tag).  Algorithmic HBM bytes: every plaintext byte read once and every sealed
@@ -430,12 +436,14 @@ def bench_encrypt(args, data, ns: int, L: int, cuts: list, dev) -> dict:
     import torch
     from kopia_amd import encryption as ke
     from kopia_amd import hashing as kh
-    from oracle import aead
+    from oracle import aead, aesgcm
+    oracle = aesgcm if algo == ke.Aes256Gcm else aead
+    ceiling = AES_VALU_CEILING_GBS if algo == ke.Aes256Gcm else CHACHA_VALU_CEILING_GBS
     offs, lens = kh.chunk_table([i * L for i in range(ns)], cuts)
     n, total = len(offs), int(lens.sum())
     ids = kh.hash_chunks_device(kh.DefaultAlgorithm, data.data_ptr(), offs, lens, bytes(range(32)), dev).contiguous()
     master = bytes(range(64, 96))
-    enc = ke.Encryptor(ke.ChaCha20Poly1305, master)
+    enc = ke.Encryptor(algo, master)
     nonces = bytes(np.random.default_rng(5).integers(0, 256, 12 * n, dtype=np.uint8))
     oo, sealed_total = ke.sealed_layout(lens)
     out = torch.empty(sealed_total, dtype=torch.uint8, device=dev)
@@ -460,31 +468,31 @@ def bench_encrypt(args, data, ns: int, L: int, cuts: list, dev) -> dict:
     open_ms, st2 = timed(lambda: enc.decrypt_chunks_device(out.data_ptr(), oo, lens + 28, ids, 16, plain, po, dev))
     assert not st2.cpu().numpy().any()
     secret, idh = aead.derive_key(master), ids.cpu().numpy()
-    pick = list(range(0, n, max(1, n // 8)))
+    pick = list(range(0, n, max(1, n // (8 if algo != ke.Aes256Gcm else 4))))
     bad = 0
     t0 = time.perf_counter()
     for i in pick:
         chunk = data[int(offs[i]):int(offs[i] + lens[i])].cpu().numpy().tobytes()
-        want = aead.kopia_encrypt(secret, idh[i].tobytes(), nonces[12 * i:12 * i + 12], chunk)
+        want = oracle.kopia_encrypt(secret, idh[i].tobytes(), nonces[12 * i:12 * i + 12], chunk)
         bad += out[int(oo[i]):int(oo[i]) + len(want)].cpu().numpy().tobytes() != want
         bad += plain[int(po[i]):int(po[i] + lens[i])].cpu().numpy().tobytes() != chunk
     oracle_s = time.perf_counter() - t0
     alg = 2 * total + 28 * n
-    return {"algo": ke.ChaCha20Poly1305, "chunks": n, "plaintext_bytes": total,
+    return {"algo": algo, "chunks": n, "plaintext_bytes": total,
             "seal_ms": round(seal_ms, 3), "seal_gib_s": round(total / GiB / (seal_ms * 1e-3), 1),
             "open_ms": round(open_ms, 3), "open_gib_s": round(total / GiB / (open_ms * 1e-3), 1),
             # VALU-bound: ChaCha20 alone is ~990 VALU per 64-byte lane block; 1,024 SIMDs x
             # 16 lanes x ~2.0 GHz under load -> ~2.1 TB/s of plaintext.  The HBM fraction stays beside it.
             "roofline": {"bound": "valu", "achieved": round(total / (seal_ms * 1e-3) / 1e9, 1),
-                         "peak": CHACHA_VALU_CEILING_GBS, "unit": "GB/s of plaintext",
-                         "frac": round(total / (seal_ms * 1e-3) / 1e9 / CHACHA_VALU_CEILING_GBS, 3),
+                         "peak": ceiling, "unit": "GB/s of plaintext",
+                         "frac": round(total / (seal_ms * 1e-3) / 1e9 / ceiling, 3),
                          "hbm_achieved": round(alg / (seal_ms * 1e-3) / 1e9, 1), "hbm_peak": HBM_PEAK_GBS,
                          "hbm_frac": round(alg / (seal_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3),
                          "algorithmic_bytes": alg, "timed": "all 4 seal launches (rocprof splits them)"},
             "sample_parity_mismatches": int(bad), "sample_chunks": len(pick),
             "cpu_oracle_gib_s": round(sum(int(lens[i]) for i in pick) * 2 / GiB / oracle_s, 4),
-            "cpu_oracle_note": "numpy/pure-Python RFC 8439 restatement (seal + compare), not an optimized "
-                               "CPU implementation: no crypto library in this image"}
+            "cpu_oracle_note": "numpy/pure-Python restatement (oracle/aead.py or oracle/aesgcm.py; seal + "
+                               "compare), not an optimized CPU implementation: no crypto library in this image"}
 
 
 def bench_long(args, comm: Comm):

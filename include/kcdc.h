@@ -219,17 +219,20 @@ int kcdc_hash_chunks_device(const char* hash_name, const uint8_t* d_data, const 
                             uint32_t key_len, uint8_t* d_out, uint32_t out_stride, void* hip_stream);
 
 /* ------------------------------------------------------------- content encryption
- * Kopia's CHACHA20-POLY1305-HMAC-SHA256 (repo/encryption/chacha20_poly1305_hmac_sha256_encryptor.go:
- * Encrypt/Decrypt/Overhead, 24-80; aead_helpers.go:12-75) for many chunks per call:
+ * Kopia's two encryptors, AES256-GCM-HMAC-SHA256 (the default; repo/encryption/
+ * aes256_gcm_hmac_sha256_encryptor.go:24-72) and CHACHA20-POLY1305-HMAC-SHA256
+ * (chacha20_poly1305_hmac_sha256_encryptor.go: Encrypt/Decrypt/Overhead, 24-80; both through
+ * aead_helpers.go:12-75), for many chunks per call, selected by `algorithm`:
  *   key_i  = HMAC-SHA256(secret, id_i)      id_i = the content ID the Encryptor is given; the content
  *            manager passes the last 16 bytes of the content hash (getPackedContentIV,
  *            repo/content/content_manager_lock_free.go:178-182)
- *   sealed = nonce_i(12) || ChaCha20-Poly1305(key_i, nonce_i, plaintext, aad = id_i) (RFC 8439)
+ *   sealed = nonce_i(12) || AEAD(key_i, nonce_i, plaintext, aad = id_i)
+ *            AEAD = AES-256-GCM (NIST SP 800-38D) or ChaCha20-Poly1305 (RFC 8439); 16-byte tag
  * secret: the repository's derived key, HKDF-SHA256(masterKey, "encryption", "", 32)
  *   (deriveKey, repo/encryption/encryption.go:80-92), 1..64 bytes.
  * kcdc_encryption_algorithms / kcdc_encryption_overhead (28): the registry (Register, encryption.go:65).
- * kcdc_crypt_workspace_size(n): bytes of device scratch a call over n chunks needs (~9 KiB
- *   per chunk: its key, one-time Poly1305 key and a table of powers of r).
+ * kcdc_crypt_workspace_size(n): bytes of device scratch a call over n chunks needs, for either
+ *   algorithm (~9 KiB per chunk: its key and a table of powers of r, or of H for GCM).
  * kcdc_encrypt_chunks_device: plaintext i = [d_offsets[i], +d_lens[i]) of d_data (any
  *   alignment, < 1 GiB); d_nonces: 12 bytes per chunk (the reference draws them from
  *   crypto/rand; the caller does here); the sealed chunk (d_lens[i] + 28 bytes) is written at
