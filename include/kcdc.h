@@ -272,7 +272,7 @@ int kcdc_decrypt_chunks_device(const char* algorithm, const uint8_t* secret, uin
  * after its 4 header bytes; the bytes are this encoder's, not klauspost/compress's.
  * kcdc_compression_algorithms: the names encoded on the device; kcdc_compression_header_id: a
  *   name's header ID (or a negative error).
- * kcdc_compress_bound(len): the largest out_i for a chunk of len bytes (6 + len + 5 per 512 bytes).
+ * kcdc_compress_bound(len): the largest out_i for a chunk of len bytes (24 + len + 5 per 512 bytes).
  * kcdc_compress_workspace_size(total, n): device scratch for n chunks of `total` bytes in all
  *   (~1.13 bytes per input byte).
  * kcdc_compress_chunks_device: chunk i = [d_offsets[i], +d_lens[i]) of d_data (any alignment);

@@ -57,11 +57,17 @@ struct CompArgs {
     uint32_t max_spans;
     uint32_t header_id;
     uint32_t skip;      // literal-run skip shift of the match search (level)
+    uint32_t gzip;      // 1: the stream sits in a gzip member (RFC 1952): gzip, pgzip
+    uint32_t* crc;      // [n]: per chunk, XOR of its spans' shifted raw CRC-32s (atomic)
+    uint32_t x2n[32];   // x^(2^k) mod P, CRC-32's reflected polynomial (zlib x2n_table)
 };
 
 __global__ __launch_bounds__(256) void span_count_kernel(CompArgs a) {
     const uint32_t c = blockIdx.x * 256u + threadIdx.x;
-    if (c < a.n) a.spans[c] = static_cast<uint32_t>((a.in_lens[c] + kSpan - 1) / kSpan);
+    if (c < a.n) {
+        a.spans[c] = static_cast<uint32_t>((a.in_lens[c] + kSpan - 1) / kSpan);
+        a.crc[c] = 0u;
+    }
 }
 
 // Exclusive prefix of spans[0..n) in place; spans[n] = total.  One workgroup.
@@ -305,6 +311,79 @@ __global__ __launch_bounds__(1024) void span_pos_kernel(CompArgs a) {
     if (t == 1023u) a.span_pos[total] = part[1023];
 }
 
+// ------------------------------------------------------------------ CRC-32 (gzip trailer)
+// crc32(A || B) = crc32(A) * x^(8|B|) ^ crc32(B) in GF(2)[x] / P (zlib's crc32_combine), and the
+// raw CRC (register 0, no final XOR) ignores leading zero bytes.  So a chunk is cut into 32 KiB
+// spans counted back from its END (bytes before the chunk read as zeros), one wave per span,
+// 512 bytes per lane; lanes combine in a 6-level tree with the constants x^(2^(12+j)), the span
+// is scaled by x^(8 * 32768 * spans after it), and the chunk's word takes the XOR (atomic, order
+// free).  The frame kernel adds crc32 of len zero bytes (the init / final-XOR terms).
+constexpr uint32_t kCrcPoly = 0xEDB88320u;
+__host__ __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {  // a * b mod P (reflected)
+    uint32_t p = 0;
+    for (int i = 31; i >= 0; i--) {
+        p ^= ((a >> i) & 1u) ? b : 0u;
+        b = (b >> 1) ^ (kCrcPoly & (0u - (b & 1u)));
+    }
+    return p;
+}
+
+constexpr uint32_t kCrcWaves = 4;
+__global__ __launch_bounds__(64 * kCrcWaves) void crc_spans_kernel(CompArgs a) {
+    __shared__ uint32_t tab[256 * 32];  // 32 copies: lane l reads copy l & 31 (conflict free)
+    for (uint32_t x = threadIdx.x; x < 256u; x += 64u * kCrcWaves) {
+        uint32_t r = x;
+        for (int k = 0; k < 8; k++) r = (r >> 1) ^ (kCrcPoly & (0u - (r & 1u)));
+        for (uint32_t c = 0; c < 32u; c++) tab[32u * x + ((c + x) & 31u)] = r;
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t b = blockIdx.x * kCrcWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t total = a.spans[a.n];
+    if (total > a.max_spans || b >= total) return;
+    uint32_t lo = 0, hi = a.n;
+    while (hi - lo > 1u) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.spans[mid] <= b) lo = mid; else hi = mid;
+    }
+    const uint32_t c = lo;
+    const uint32_t s = b - a.spans[c], ns = a.spans[c + 1] - a.spans[c];
+    const int64_t len = static_cast<int64_t>(a.in_lens[c]);
+    const int64_t p0 = len - static_cast<int64_t>(kSpan) * (ns - s) + static_cast<int64_t>(kSeg) * lane;
+    const uint8_t* in = a.in + a.in_offs[c];
+    const uint32_t m = static_cast<uint32_t>((reinterpret_cast<uintptr_t>(in) + static_cast<uint64_t>(p0 & 3)) & 3u);
+    // word k of the segment = bytes [p0 + 4k, +4); aligned source words from base, bytes < 0 read as 0
+    const uint8_t* wb = in + p0 - m;  // only dereferenced where it holds a chunk byte
+    const uint32_t sel = 4u * (lane & 31u);
+    uint32_t r = 0;
+    const int64_t first = p0 >= 0 ? 0 : (-p0) >> 2;  // words wholly before the chunk stay 0: skip
+    uint32_t w0 = 0;
+    for (int64_t k = first; k < static_cast<int64_t>(kSeg / 4u); k++) {
+        const int64_t q = p0 + 4 * k;  // first byte of the word
+        if (k == first) w0 = (q - static_cast<int64_t>(m) + 4 > 0) ? *reinterpret_cast<const uint32_t*>(wb + 4 * k) : 0u;
+        // the next aligned word (this word's tail when m > 0, the next word's body when m == 0)
+        const uint32_t w1 = (q - static_cast<int64_t>(m) + 4 < len) ? *reinterpret_cast<const uint32_t*>(wb + 4 * k + 4) : 0u;
+        uint32_t w = __builtin_amdgcn_alignbit(w1, w0, 8u * m);
+        if (q < 0) w &= 0xFFFFFFFFu << (8u * static_cast<uint32_t>(-q));  // bytes before the chunk are 0
+        w0 = w1;
+        r ^= w;
+#pragma unroll
+        for (int t = 0; t < 4; t++) r = (r >> 8) ^ tab[32u * (r & 255u) + (sel >> 2)];
+    }
+    // lanes 2i, 2i+1, ...: left * x^(8 * right bytes) ^ right, right = 512 * 2^j bytes
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        const uint32_t right = __shfl_down(r, 1u << j, 64);
+        if (((lane >> j) & 1u) == 0u) r = multmodp(r, a.x2n[12 + j]) ^ right;
+    }
+    if (lane == 0) {
+        uint32_t after = ns - 1u - s;  // whole spans after this one: x^(8 * 32768 * after)
+        for (int bit = 0; after; bit++, after >>= 1)
+            if (after & 1u) r = multmodp(r, a.x2n[18 + bit]);
+        atomicXor(&a.crc[c], r);
+    }
+}
+
 // n bytes from src to dst, both at any alignment, by one wave: byte stores for dst's partial
 // head and tail words, aligned dword stores (from two aligned loads + alignbit) in between.
 // Only aligned source words holding a byte of [src, src + n) are read.
@@ -337,7 +416,7 @@ __global__ __launch_bounds__(64) void deflate_copy_kernel(CompArgs a) {
     }
     const uint32_t c = lo;
     const uint32_t u = b - a.spans[c];
-    uint8_t* dst = a.out + a.out_offs[c] + 4u + (a.span_pos[b] - a.span_pos[a.spans[c]]);
+    uint8_t* dst = a.out + a.out_offs[c] + 4u + (a.gzip ? 10u : 0u) + (a.span_pos[b] - a.span_pos[a.spans[c]]);
     const uint8_t* in = a.in + a.in_offs[c] + static_cast<uint64_t>(u) * kSpan;
     const uint32_t word = a.seglen[b * 64u + lane];
     const uint32_t eff = (word & kStored) ? 5u + (word & ~kStored) : word;
@@ -378,9 +457,31 @@ __global__ __launch_bounds__(256) void deflate_frame_kernel(CompArgs a) {
     uint8_t* dst = a.out + a.out_offs[c];
     const uint64_t body = a.span_pos[a.spans[c + 1]] - a.span_pos[a.spans[c]];
     for (uint32_t t = 0; t < 4u; t++) dst[t] = static_cast<uint8_t>(a.header_id >> (8u * (3u - t)));
-    dst[4 + body] = 0x03u;  // BFINAL 1, BTYPE 01, end of block
-    dst[5 + body] = 0x00u;
-    const uint64_t out_len = body + 6u;
+    uint64_t out_len;
+    if (a.gzip) {
+        // RFC 1952 member: ID1 ID2 CM=8 FLG=0 MTIME=0 XFL=0 OS=255, the stream, CRC32, ISIZE
+        const uint8_t gz[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 0, 0xff};
+        for (uint32_t t = 0; t < 10u; t++) dst[4 + t] = gz[t];
+        uint8_t* e = dst + 14 + body;
+        e[0] = 0x03u;
+        e[1] = 0x00u;
+        const uint64_t len = a.in_lens[c];
+        uint32_t z = 0x80000000u;  // x^(8 len) mod P = product of x^(2^(3+bit)) over len's bits
+        uint64_t n = len;
+        for (int bit = 0; n; bit++, n >>= 1)
+            if (n & 1u) z = multmodp(z, a.x2n[(3 + bit) & 31]);
+        const uint32_t crc = a.crc[c] ^ multmodp(z, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+        const uint32_t isize = static_cast<uint32_t>(len);
+        for (uint32_t t = 0; t < 4u; t++) {
+            e[2 + t] = static_cast<uint8_t>(crc >> (8u * t));
+            e[6 + t] = static_cast<uint8_t>(isize >> (8u * t));
+        }
+        out_len = body + 24u;
+    } else {
+        dst[4 + body] = 0x03u;  // BFINAL 1, BTYPE 01, end of block
+        dst[5 + body] = 0x00u;
+        out_len = body + 6u;
+    }
     a.out_lens[c] = out_len;
     a.ids[c] = out_len < a.in_lens[c] ? a.header_id : 0u;  // content_manager_lock_free.go:64
 }
@@ -391,14 +492,23 @@ namespace {
 
 struct CompAlgo {
     const char* name;
-    uint32_t header_id;  // repo/compression/compression_ids.go:28-30
+    uint32_t header_id;  // repo/compression/compression_ids.go:8-10, 19-21, 28-30
     uint32_t skip;
+    uint32_t gzip;
 };
-// repo/compression/compressor_deflate.go:14-16
+// compressor_deflate.go:14-16, compressor_gzip.go:15-17, compressor_pgzip.go:16-18 (sorted names).
+// pgzip's writer splits its input into independently compressed blocks; gzip and pgzip readers
+// accept any valid member, so both families carry the same device stream.
 constexpr CompAlgo kCompAlgos[] = {
-    {"deflate-best-compression", 0x1502u, 7u},
-    {"deflate-best-speed", 0x1501u, 4u},
-    {"deflate-default", 0x1500u, 5u},
+    {"deflate-best-compression", 0x1502u, 7u, 0u},
+    {"deflate-best-speed", 0x1501u, 4u, 0u},
+    {"deflate-default", 0x1500u, 5u, 0u},
+    {"gzip", 0x1000u, 5u, 1u},
+    {"gzip-best-compression", 0x1002u, 7u, 1u},
+    {"gzip-best-speed", 0x1001u, 4u, 1u},
+    {"pgzip", 0x1300u, 5u, 1u},
+    {"pgzip-best-compression", 0x1302u, 7u, 1u},
+    {"pgzip-best-speed", 0x1301u, 4u, 1u},
 };
 
 const CompAlgo* find_comp(const char* name) {
@@ -411,13 +521,14 @@ const CompAlgo* find_comp(const char* name) {
 uint64_t align256c(uint64_t x) { return (x + 255u) & ~uint64_t(255); }
 
 struct CompWs {
-    uint64_t spans, seglen, span_bytes, span_pos, slots, total;
+    uint64_t spans, crc, seglen, span_bytes, span_pos, slots, total;
 };
 constexpr uint64_t kPerSpan = 64u * (compdev::kSlot + 4u) + 4u + 8u;
 CompWs comp_ws(uint32_t n, uint64_t max_spans) {
     CompWs l{};
     l.spans = 0;
-    l.seglen = align256c((uint64_t(n) + 1u) * 4u);
+    l.crc = align256c((uint64_t(n) + 1u) * 4u);
+    l.seglen = align256c(l.crc + uint64_t(n) * 4u);
     l.span_bytes = align256c(l.seglen + max_spans * 64u * 4u);
     l.span_pos = align256c(l.span_bytes + max_spans * 4u);
     l.slots = align256c(l.span_pos + (max_spans + 1u) * 8u);
@@ -442,8 +553,8 @@ extern "C" int64_t kcdc_compression_header_id(const char* name) {
              : set_error(-2, std::string("unknown compression algorithm: ") + (name ? name : "(null)"));
 }
 
-extern "C" uint64_t kcdc_compress_bound(uint64_t len) {
-    return 6u + len + 5u * ((len + compdev::kSeg - 1) / compdev::kSeg);
+extern "C" uint64_t kcdc_compress_bound(uint64_t len) {  // + 18: a gzip member's header and trailer
+    return 24u + len + 5u * ((len + compdev::kSeg - 1) / compdev::kSeg);
 }
 
 extern "C" uint64_t kcdc_compress_workspace_size(uint64_t total_bytes, uint32_t nchunks) {
@@ -484,6 +595,15 @@ extern "C" int kcdc_compress_chunks_device(const char* name, const uint8_t* d_da
     a.max_spans = static_cast<uint32_t>(max_spans);
     a.header_id = al->header_id;
     a.skip = al->skip;
+    a.gzip = al->gzip;
+    a.crc = reinterpret_cast<uint32_t*>(w + l.crc);
+    {
+        uint32_t p = 1u << 30;  // x^1
+        for (int k = 0; k < 32; k++) {
+            a.x2n[k] = p;
+            p = compdev::multmodp(p, p);
+        }
+    }
     hipStream_t st = static_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(compdev::span_count_kernel, dim3((nchunks + 255u) / 256u), dim3(256), 0, st, a);
     hipLaunchKernelGGL(compdev::span_scan_kernel, dim3(1), dim3(1024), 0, st, nchunks, a.spans);
@@ -492,6 +612,10 @@ extern "C" int kcdc_compress_chunks_device(const char* name, const uint8_t* d_da
         hipLaunchKernelGGL(compdev::deflate_spans_kernel, grid, dim3(64), 0, st, a);
         hipLaunchKernelGGL(compdev::span_pos_kernel, dim3(1), dim3(1024), 0, st, a);
         hipLaunchKernelGGL(compdev::deflate_copy_kernel, grid, dim3(64), 0, st, a);
+        if (a.gzip)
+            hipLaunchKernelGGL(compdev::crc_spans_kernel,
+                               dim3(static_cast<uint32_t>((max_spans + compdev::kCrcWaves - 1) / compdev::kCrcWaves)),
+                               dim3(64 * compdev::kCrcWaves), 0, st, a);
     }
     hipLaunchKernelGGL(compdev::deflate_frame_kernel, dim3((nchunks + 255u) / 256u), dim3(256), 0, st, a);
     const hipError_t e = hipGetLastError();

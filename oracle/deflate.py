@@ -12,7 +12,8 @@ The reference encodes with github.com/klauspost/compress/flate (not vendored, Go
 encoder bytes are not comparable; parity for a compressor is the round trip through an
 independent RFC 1951 inflater (zlib here, flate.NewReader in the reference), the header, and the
 reference's own test properties (compressor_test.go:15-87: all-zero input shrinks, random input
-does not, another compressor's reader rejects the stream).
+does not, another compressor's reader rejects the stream).  The gzip family (compressor_gzip.go,
+compressor_pgzip.go) is the same stream in an RFC 1952 member.
 """
 from __future__ import annotations
 
@@ -28,6 +29,15 @@ HEADER_IDS = {
     "deflate-default": 0x1500, "deflate-best-speed": 0x1501, "deflate-best-compression": 0x1502,
 }
 DEFLATE_LEVELS = {"deflate-best-speed": 1, "deflate-default": 6, "deflate-best-compression": 9}
+# compressor_gzip.go / compressor_pgzip.go: the same DEFLATE levels inside a gzip member (RFC 1952);
+# gzip.NewReader / pgzip.NewReader accept any valid member.
+GZIP_LEVELS = {"gzip": 6, "gzip-best-speed": 1, "gzip-best-compression": 9,
+               "pgzip": 6, "pgzip-best-speed": 1, "pgzip-best-compression": 9}
+LEVELS = {**DEFLATE_LEVELS, **GZIP_LEVELS}
+
+
+def _wbits(name: str) -> int:
+    return 31 if name in GZIP_LEVELS else -15
 
 
 def header(name: str) -> bytes:
@@ -36,16 +46,17 @@ def header(name: str) -> bytes:
 
 def compress(name: str, data: bytes) -> bytes:
     """A reference-format stream from zlib's deflater (for ratio comparison, not byte parity)."""
-    co = zlib.compressobj(DEFLATE_LEVELS[name], zlib.DEFLATED, -15)
+    co = zlib.compressobj(LEVELS[name], zlib.DEFLATED, _wbits(name))
     return header(name) + co.compress(data) + co.flush()
 
 
 def decompress(name: str, blob: bytes) -> bytes:
     """deflateCompressor.Decompress(withHeader=true): header check, then a raw inflate that must
-    consume the whole stream (flate.NewReader reads to the final block)."""
+    consume the whole stream (flate.NewReader reads to the final block).  gzip/pgzip names: the
+    member's header, CRC-32 and ISIZE are checked as gzip.NewReader does (zlib, wbits 31)."""
     if blob[:4] != header(name):
         raise ValueError(f"invalid compression header, expected {header(name).hex()} but got {blob[:4].hex()}")
-    d = zlib.decompressobj(-15)
+    d = zlib.decompressobj(_wbits(name))
     out = d.decompress(blob[4:]) + d.flush()
     if not d.eof:
         raise ValueError("truncated deflate stream")

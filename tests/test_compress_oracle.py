@@ -12,6 +12,8 @@ from kopia_amd import compression as kc
 from oracle import deflate
 
 DEFLATE = ["deflate-best-compression", "deflate-best-speed", "deflate-default"]
+GZIP = ["gzip", "gzip-best-compression", "gzip-best-speed", "pgzip", "pgzip-best-compression", "pgzip-best-speed"]
+DEVICE = DEFLATE + GZIP  # the library's registry order (sorted names)
 
 
 def test_header_ids_match_reference():
@@ -20,11 +22,13 @@ def test_header_ids_match_reference():
     assert deflate.HEADER_IDS["deflate-best-speed"] == 0x1501
     assert deflate.HEADER_IDS["deflate-best-compression"] == 0x1502
     assert len(set(deflate.HEADER_IDS.values())) == len(deflate.HEADER_IDS)
+    # compression_ids.go:8-10, 19-21 (gzip, pgzip)
+    assert [deflate.HEADER_IDS[n] for n in GZIP] == [0x1000, 0x1002, 0x1001, 0x1300, 0x1302, 0x1301]
 
 
 def test_library_registry():
-    assert kc.SupportedAlgorithms() == DEFLATE
-    for name in DEFLATE:
+    assert kc.SupportedAlgorithms() == DEVICE
+    for name in DEVICE:
         assert kc.HeaderID(name) == deflate.HEADER_IDS[name]
     with pytest.raises(_lib.KcdcError):
         kc.HeaderID("zstd-fastest")  # registered in the reference, not encoded on the device
@@ -33,21 +37,23 @@ def test_library_registry():
 
 
 def test_bound():
-    assert kc.compress_bound(0) == 6
-    assert kc.compress_bound(1) == 12
-    assert kc.compress_bound(512) == 6 + 512 + 5
-    assert kc.compress_bound(513) == 6 + 513 + 10
-    assert kc.compress_bound(1 << 20) == 6 + (1 << 20) + 5 * 2048
+    """4-byte header ID + final block (2) + a gzip member's header and trailer (18), plus the
+    input and 5 bytes per 512-byte segment (a stored block's header)."""
+    assert kc.compress_bound(0) == 24
+    assert kc.compress_bound(1) == 30
+    assert kc.compress_bound(512) == 24 + 512 + 5
+    assert kc.compress_bound(513) == 24 + 513 + 10
+    assert kc.compress_bound(1 << 20) == 24 + (1 << 20) + 5 * 2048
 
 
-@pytest.mark.parametrize("name", DEFLATE)
+@pytest.mark.parametrize("name", DEVICE)
 def test_oracle_round_trip_and_properties(name):
     """compressor_test.go:15-87 on the oracle: zeros shrink, random does not, other headers fail."""
     zeros = bytes(10000)
     blob = deflate.compress(name, zeros)
     assert len(blob) < len(zeros)
     assert deflate.decompress(name, blob) == zeros
-    for other in DEFLATE:
+    for other in DEVICE:
         if other != name:
             with pytest.raises(ValueError):
                 deflate.decompress(other, blob)

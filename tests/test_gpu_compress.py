@@ -1,4 +1,4 @@
-"""GPU: deflate content compression of many chunks (kcdc_compress_chunks_device) against the
+"""GPU: deflate / gzip / pgzip content compression of many chunks (kcdc_compress_chunks_device) against the
 oracle (oracle/deflate.py: the reference's framing, zlib as the independent RFC 1951 inflater).
 Every chunk must inflate back to its bytes behind its 4-byte header ID, carry the content
 manager's keep-or-drop ID (content_manager_lock_free.go:64-73), and the reference's own test
@@ -16,6 +16,7 @@ from oracle import coracle, deflate
 
 pytestmark = pytest.mark.gpu
 DEFLATE = ["deflate-best-compression", "deflate-best-speed", "deflate-default"]
+GZIP = ["gzip", "gzip-best-compression", "gzip-best-speed", "pgzip", "pgzip-best-compression", "pgzip-best-speed"]
 
 
 def _compress(name, host, offs, lens, dev):
@@ -59,7 +60,7 @@ def _mixed(nbytes, seed):
     return np.frombuffer(b"".join(out)[:nbytes], np.uint8).copy()
 
 
-@pytest.mark.parametrize("name", DEFLATE)
+@pytest.mark.parametrize("name", DEFLATE + GZIP)
 def test_reference_properties(name, gpu):
     """compressor_test.go:21-84 through the device: 10000 zero bytes shrink (and keep the ID),
     10000 random bytes do not (ID 0, NoCompression), both inflate back; the other deflate
@@ -73,25 +74,28 @@ def test_reference_properties(name, gpu):
     assert ol[0] < 10000 and ids[0] == deflate.HEADER_IDS[name]
     assert ol[1] >= 10000 and ids[1] == 0
     blob = out[oo[0]:oo[0] + ol[0]].tobytes()
-    for other in DEFLATE:
+    for other in DEFLATE + GZIP:
         if other != name:
             with pytest.raises(ValueError):
                 deflate.decompress(other, blob)
 
 
-def test_ragged_misaligned_chunks(gpu):
+@pytest.mark.parametrize("name", ["deflate-default", "gzip", "pgzip-best-speed"])
+def test_ragged_misaligned_chunks(name, gpu):
+    """Edge lengths around the 512-byte segments and 32 KiB spans at random offsets; for the gzip
+    family this exercises the device CRC-32 (end-aligned spans, partial first span)."""
     host = _mixed(24 << 20, 11)
     rng = np.random.default_rng(12)
     edge = [0, 1, 2, 3, 4, 5, 7, 8, 255, 511, 512, 513, 1023, 1024, 1025, 4096, 32767, 32768, 32769,
             65535, 65536, 65537, 100000, (1 << 20) + 3]
     lens = edge + [int(x) for x in rng.integers(0, 300000, 200)]
     offs = [int(rng.integers(0, host.size - L)) for L in lens]
-    out, oo, ol, ids = _compress("deflate-default", host, offs, lens, gpu)
-    _check("deflate-default", host, offs, lens, out, oo, ol, ids)
+    out, oo, ol, ids = _compress(name, host, offs, lens, gpu)
+    _check(name, host, offs, lens, out, oo, ol, ids)
     assert (ids != 0).sum() > len(lens) // 2  # mixed data mostly compresses
 
 
-@pytest.mark.parametrize("name", DEFLATE)
+@pytest.mark.parametrize("name", DEFLATE + ["gzip-best-compression"])
 def test_large_compressible_chunks(name, gpu):
     """The reference benchmark's inputs (compressor_test.go:92-96): a repeated 1..10 pattern and
     zeros, as 8 MiB + odd chunks; both must shrink far below the input."""
@@ -104,7 +108,8 @@ def test_large_compressible_chunks(name, gpu):
     assert ol[0] < 0.05 * lens[0] and ol[1] < 0.05 * lens[1]
 
 
-def test_splitter_chunks_of_mixed_stream(gpu):
+@pytest.mark.parametrize("name", ["deflate-best-speed", "pgzip"])
+def test_splitter_chunks_of_mixed_stream(name, gpu):
     """Chunks cut by the oracle's DYNAMIC-128K-BUZHASH over a mixed 32 MiB stream."""
     host = _mixed(32 << 20, 21)
     cuts = [int(c) for c in coracle.split_batch("DYNAMIC-128K-BUZHASH", [host])[0]]
@@ -112,20 +117,22 @@ def test_splitter_chunks_of_mixed_stream(gpu):
     offs = bounds[:-1]
     lens = [b - a for a, b in zip(bounds[:-1], bounds[1:])]
     assert sum(lens) == host.size and len(lens) > 100
-    out, oo, ol, ids = _compress("deflate-best-speed", host, offs, lens, gpu)
-    _check("deflate-best-speed", host, offs, lens, out, oo, ol, ids)
+    out, oo, ol, ids = _compress(name, host, offs, lens, gpu)
+    _check(name, host, offs, lens, out, oo, ol, ids)
 
 
-def test_random_stream_is_stored(gpu):
+@pytest.mark.parametrize("name", ["deflate-default", "gzip"])
+def test_random_stream_is_stored(name, gpu):
     """Config-2 bytes (uniform PRNG): every segment falls back to a stored block, the output is
     the bound minus the unused trailer slack, and the ID is NoCompression."""
     host = coracle.gen_stream(0x6B6F706961, 0, 8 << 20)
     lens = [1 << 20] * 8
     offs = [i << 20 for i in range(8)]
-    out, oo, ol, ids = _compress("deflate-default", host, offs, lens, gpu)
-    _check("deflate-default", host, offs, lens, out, oo, ol, ids)
+    out, oo, ol, ids = _compress(name, host, offs, lens, gpu)
+    _check(name, host, offs, lens, out, oo, ol, ids)
     assert not ids.any()
-    assert all(int(x) == kc.compress_bound(1 << 20) for x in ol)
+    frame = 0 if name in GZIP else 18  # the bound leaves room for a gzip member's header and trailer
+    assert all(int(x) == kc.compress_bound(1 << 20) - frame for x in ol)
 
 
 def test_workspace_too_small_writes_no_output(gpu):
