@@ -263,8 +263,9 @@ int kcdc_decrypt_chunks_device(const char* algorithm, const uint8_t* secret, uin
                                void* hip_stream);
 
 /* ------------------------------------------------------------- content compression
- * Kopia's deflate compressors (repo/compression/compressor_deflate.go:14-62 Compress; header IDs
- * compression_ids.go:28-30) for many chunks per call, with the content manager's keep-or-drop
+ * Kopia's deflate, gzip and pgzip compressors (repo/compression/compressor_deflate.go:14-62,
+ * compressor_gzip.go:15-17, compressor_pgzip.go:16-18; header IDs compression_ids.go:8-30) for many
+ * chunks per call (gzip names: the stream inside an RFC 1952 member with its CRC-32 and ISIZE), with the content manager's keep-or-drop
  * rule (maybeCompressAndEncryptDataForPacking, repo/content/content_manager_lock_free.go:42-73):
  *   out_i = BE32(header ID) || raw DEFLATE stream (RFC 1951) of chunk i
  *   id_i  = header ID if len(out_i) < len(chunk i), else 0 (NoCompression: store chunk i as is)
