@@ -853,19 +853,28 @@ __device__ __forceinline__ uint32_t aes_sbox_entry(uint32_t x) {
 // was 60 % bank-conflict cycles), and the byte address (x << 8) | lane offset is ONE v_perm of
 // the state word.  Kernels keep the table first in their LDS so the base folds
 // into the ds_read offset.  Sb[x] = S for the key schedule.
+#ifndef KCDC_GCM_WIDE
+#define KCDC_GCM_WIDE 1  // 1: Te0 + Te1 rows of 256 B (one v_perm address); 0: Te0 only, 128-B rows (32 KiB)
+#endif
 struct alignas(256) AesTabs {
-    uint32_t te[256 * 64];
+    uint32_t te[256 * (KCDC_GCM_WIDE ? 64 : 32)];
     uint32_t sb[256];
 };
 __device__ __forceinline__ void aes_tabs_build(AesTabs& t, uint32_t tid, uint32_t nthreads) {
     for (uint32_t x = tid; x < 256u; x += nthreads) {
         const uint32_t sx = aes_sbox_entry(x), s2 = xt8(sx), s3 = s2 ^ sx;
         const uint32_t w = (s2 << 24) | (sx << 16) | (sx << 8) | s3, w1 = ror32(w, 8);
+#if KCDC_GCM_WIDE
 #pragma unroll 8
         for (uint32_t c = 0; c < 64u; c++) {
             const uint32_t cc = (c + x) & 63u;  // lanes start on different banks
             t.te[64u * x + cc] = (cc & 32u) ? w1 : w;
         }
+#else
+        (void)w1;
+#pragma unroll 8
+        for (uint32_t c = 0; c < 32u; c++) t.te[32u * x + ((c + x) & 31u)] = w;
+#endif
         t.sb[x] = sx;
     }
 }
@@ -873,7 +882,11 @@ __device__ __forceinline__ void aes_tabs_build(AesTabs& t, uint32_t tid, uint32_
 // (in byte 0 of `off`: 4 (lane & 31), + 128 for Te1) in byte 0.
 template <int k>
 __device__ __forceinline__ uint32_t te_at(const AesTabs& t, uint32_t s, uint32_t off) {
+#if KCDC_GCM_WIDE
     const uint32_t byte = __builtin_amdgcn_perm(s, off, 0x0C0C0000u | ((4u + k) << 8));
+#else
+    const uint32_t byte = (__builtin_amdgcn_ubfe(s, 8u * k, 8u) << 7) | off;
+#endif
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(t.te) + byte);
 }
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
@@ -901,8 +914,13 @@ template <typename RK>
 __device__ __forceinline__ void aes256_block(const AesTabs& t, uint32_t o0, uint32_t o1, const RK& rk, uint32_t (&s)[4]) {
     uint32_t s0 = s[0] ^ rk[0], s1 = s[1] ^ rk[1], s2 = s[2] ^ rk[2], s3 = s[3] ^ rk[3];
     auto col = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+#if KCDC_GCM_WIDE
         const uint32_t t0 = te_at<3>(t, a, o0), t1 = te_at<2>(t, b, o1);
         const uint32_t t2 = ror32(te_at<1>(t, c, o0), 16), t3 = ror32(te_at<0>(t, d, o1), 16);
+#else
+        const uint32_t t0 = te_at<3>(t, a, o0), t1 = ror32(te_at<2>(t, b, o0), 8);
+        const uint32_t t2 = ror32(te_at<1>(t, c, o0), 16), t3 = ror32(te_at<0>(t, d, o0), 24);
+#endif
         return xor3(xor3(t0, t1, t2), t3, k);
     };
 #pragma unroll
@@ -1115,12 +1133,13 @@ __device__ __forceinline__ void gcm_tab_mul(const GcmWave& g, uint32_t (&x)[4]) 
 }
 
 #ifndef KCDC_GCM_WAVES
-#define KCDC_GCM_WAVES 2  // waves per SIMD the register budget is sized for
+#define KCDC_GCM_WAVES (KCDC_GCM_WIDE ? 2 : 3)  // waves per SIMD the register budget is sized for
 #endif
 #ifndef KCDC_GCM_RB
 #define KCDC_GCM_RB 2  // AES blocks in flight per lane (rows of a unit per batch)
 #endif
-constexpr uint32_t kGcmWaves = 8;  // waves per workgroup: one 64 KiB table, 8 GHASH tables, 146 KiB
+// waves per workgroup: 64 KiB table + 8 GHASH tables = 146 KiB, or 32 KiB + 12 = 153 KiB
+constexpr uint32_t kGcmWaves = KCDC_GCM_WIDE ? 8 : 12;
 struct GcmLds {
     AesTabs t;  // first: at LDS address 0
     GcmWave gw[kGcmWaves];
