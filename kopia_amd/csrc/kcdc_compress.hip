@@ -351,24 +351,46 @@ __global__ __launch_bounds__(64 * kCrcWaves) void crc_spans_kernel(CompArgs a) {
     const int64_t len = static_cast<int64_t>(a.in_lens[c]);
     const int64_t p0 = len - static_cast<int64_t>(kSpan) * (ns - s) + static_cast<int64_t>(kSeg) * lane;
     const uint8_t* in = a.in + a.in_offs[c];
-    const uint32_t m = static_cast<uint32_t>((reinterpret_cast<uintptr_t>(in) + static_cast<uint64_t>(p0 & 3)) & 3u);
-    // word k of the segment = bytes [p0 + 4k, +4); aligned source words from base, bytes < 0 read as 0
-    const uint8_t* wb = in + p0 - m;  // only dereferenced where it holds a chunk byte
-    const uint32_t sel = 4u * (lane & 31u);
+    // 16-byte granules from the aligned address below the segment; m16 is wave-uniform (lanes
+    // are 512 bytes apart).  A granule is read only when it holds a byte of the chunk.
+    const uint32_t m16 = static_cast<uint32_t>((reinterpret_cast<uintptr_t>(in) + static_cast<uint64_t>(p0 & 15)) & 15u);
+    const uint8_t* gb = in + p0 - m16;
+    auto granule = [&](int64_t g) -> uint4 {
+        const int64_t o = p0 - static_cast<int64_t>(m16) + 16 * g;
+        return (o + 16 > 0 && o < len) ? *reinterpret_cast<const uint4*>(gb + 16 * g) : make_uint4(0u, 0u, 0u, 0u);
+    };
+    const uint32_t q4 = m16 >> 2, sh = 8u * (m16 & 3u);
+    const uint32_t sel = lane & 31u;
     uint32_t r = 0;
-    const int64_t first = p0 >= 0 ? 0 : (-p0) >> 2;  // words wholly before the chunk stay 0: skip
-    uint32_t w0 = 0;
-    for (int64_t k = first; k < static_cast<int64_t>(kSeg / 4u); k++) {
-        const int64_t q = p0 + 4 * k;  // first byte of the word
-        if (k == first) w0 = (q - static_cast<int64_t>(m) + 4 > 0) ? *reinterpret_cast<const uint32_t*>(wb + 4 * k) : 0u;
-        // the next aligned word (this word's tail when m > 0, the next word's body when m == 0)
-        const uint32_t w1 = (q - static_cast<int64_t>(m) + 4 < len) ? *reinterpret_cast<const uint32_t*>(wb + 4 * k + 4) : 0u;
-        uint32_t w = __builtin_amdgcn_alignbit(w1, w0, 8u * m);
-        if (q < 0) w &= 0xFFFFFFFFu << (8u * static_cast<uint32_t>(-q));  // bytes before the chunk are 0
-        w0 = w1;
-        r ^= w;
+    uint4 cur = granule(0);
+    for (int j = 0; j < static_cast<int>(kSeg / 16u); j++) {
+        const uint4 nxt = granule(j + 1);
+        const uint32_t c8[8] = {cur.x, cur.y, cur.z, cur.w, nxt.x, nxt.y, nxt.z, nxt.w};
+        uint32_t w4[4];
+        // words q4 .. q4 + 4 of the pair, shifted by sh bits (q4 uniform: one branch)
+        if (q4 == 0) {
 #pragma unroll
-        for (int t = 0; t < 4; t++) r = (r >> 8) ^ tab[32u * (r & 255u) + (sel >> 2)];
+            for (int i = 0; i < 4; i++) w4[i] = __builtin_amdgcn_alignbit(c8[i + 1], c8[i], sh);
+        } else if (q4 == 1) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) w4[i] = __builtin_amdgcn_alignbit(c8[i + 2], c8[i + 1], sh);
+        } else if (q4 == 2) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) w4[i] = __builtin_amdgcn_alignbit(c8[i + 3], c8[i + 2], sh);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++) w4[i] = __builtin_amdgcn_alignbit(c8[i + 4], c8[i + 3], sh);
+        }
+        cur = nxt;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int64_t pos = p0 + 16 * j + 4 * i;  // bytes before the chunk read as 0
+            uint32_t w = w4[i];
+            if (pos < 0) w = pos <= -4 ? 0u : (w & (0xFFFFFFFFu << (8u * static_cast<uint32_t>(-pos))));
+            r ^= w;
+#pragma unroll
+            for (int t = 0; t < 4; t++) r = (r >> 8) ^ tab[32u * (r & 255u) + sel];
+        }
     }
     // lanes 2i, 2i+1, ...: left * x^(8 * right bytes) ^ right, right = 512 * 2^j bytes
 #pragma unroll
