@@ -37,7 +37,10 @@ constexpr uint32_t kSeg = 512;                  // bytes per lane segment
 constexpr uint32_t kSpan = 64 * kSeg;           // bytes per wave span (<= the 32 KiB window)
 constexpr uint32_t kSlot = kSeg + 64;           // scratch bytes per segment (the encoder stops at kSeg + 8)
 constexpr uint32_t kStored = 0x80000000u;       // segment length flag: emit a stored block
-constexpr uint32_t kHashBits = 7;
+#ifndef KCDC_DEFLATE_HASH_BITS
+#define KCDC_DEFLATE_HASH_BITS 7  // per-lane match table entries (log2); LDS = 33 KiB span + 128 B << bits
+#endif
+constexpr uint32_t kHashBits = KCDC_DEFLATE_HASH_BITS;
 constexpr uint32_t kLdsWords = 8320;            // >= (4 * 2049 + 1) + 65: the staged span + 1 word of read-ahead
 
 struct CompArgs {
