@@ -1,4 +1,6 @@
-// Kopia content encryption on gfx950: CHACHA20-POLY1305-HMAC-SHA256.
+// Kopia content encryption on gfx950: CHACHA20-POLY1305-HMAC-SHA256 (this
+// header) and AES256-GCM-HMAC-SHA256, Kopia's default (the section "AES256-GCM-HMAC-SHA256"
+// below: T-table AES-CTR and table-driven GHASH, same four-launch shape).
 //
 // What the reference does per content (repo/encryption/chacha20_poly1305_hmac_sha256_encryptor.go:24-80,
 // aead_helpers.go:12-45, encryption.go:80-92, repo/content/content_manager_lock_free.go:178-182):
