@@ -11,8 +11,13 @@ import os
 from functools import lru_cache
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# KCDC_LIB: an alternative build of the same library (A/B experiments, tools/gpu_ab.sh)
-LIB_PATH = os.environ.get("KCDC_LIB") or os.path.join(HERE, "libkcdc.so")
+# KCDC_LIB: an alternative build of the same library, for A/B timing experiments only
+# (tools/crypt_bench.py, tools/hash_bench.py).  It is honoured only together with
+# KCDC_ALLOW_VARIANT_LIB=1, so a stray environment variable can never swap the product library.
+_ALT = os.environ.get("KCDC_LIB")
+if _ALT and os.environ.get("KCDC_ALLOW_VARIANT_LIB") != "1":
+    raise RuntimeError("KCDC_LIB names a variant build; set KCDC_ALLOW_VARIANT_LIB=1 to load it (experiments only)")
+LIB_PATH = _ALT or os.path.join(HERE, "libkcdc.so")
 
 KCDC_OK = 0
 KCDC_ENOENT = -2

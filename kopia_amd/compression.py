@@ -58,18 +58,21 @@ class Compressor:
         Asynchronous on `stream`."""
         import torch
         n = len(offsets)
-        out_lens = torch.zeros(max(n, 1), dtype=torch.int64, device=device)
-        ids = torch.zeros(max(n, 1), dtype=torch.int32, device=device)
-        if n == 0:
-            return out_lens[:0], ids[:0]
-        lens = np.asarray(lengths, dtype=np.int64)
-        d_offs = torch.as_tensor(np.asarray(offsets, dtype=np.int64)).to(device)
-        d_lens = torch.as_tensor(lens).to(device)
-        d_oo = torch.as_tensor(np.asarray(out_offsets, dtype=np.int64)).to(device)
-        wb = int(_lib.lib().kcdc_compress_workspace_size(int(lens.sum()), n))
-        work = torch.empty(max(wb, 1), dtype=torch.uint8, device=device)
         if stream is None:
             stream = torch.cuda.current_stream(device)
+        lens = np.asarray(lengths, dtype=np.int64)
+        # Temporaries are allocated and filled on `stream` itself (the kernels run there), and
+        # out_lens / ids need no fill: the frame kernel writes every entry.
+        with torch.cuda.stream(stream):
+            out_lens = torch.empty(max(n, 1), dtype=torch.int64, device=device)
+            ids = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+            if n == 0:
+                return out_lens[:0], ids[:0]
+            d_offs = torch.as_tensor(np.asarray(offsets, dtype=np.int64)).to(device)
+            d_lens = torch.as_tensor(lens).to(device)
+            d_oo = torch.as_tensor(np.asarray(out_offsets, dtype=np.int64)).to(device)
+            wb = int(_lib.lib().kcdc_compress_workspace_size(int(lens.sum()), n))
+            work = torch.empty(max(wb, 1), dtype=torch.uint8, device=device)
         _lib.check(_lib.lib().kcdc_compress_chunks_device(
             self.name.encode(), C.c_void_p(data_ptr), d_offs.data_ptr(), d_lens.data_ptr(), n, d_out.data_ptr(),
             d_oo.data_ptr(), out_lens.data_ptr(), ids.data_ptr(), work.data_ptr(), work.numel(),

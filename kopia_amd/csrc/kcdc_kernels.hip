@@ -679,6 +679,8 @@ struct BatchArgs {
     const uint32_t* buz;
     const uint64_t* rk_out;
     const uint64_t* rk_mod;
+    const uint64_t* rk2_main;  // Tables::rk2_main (two-byte Rabin-Karp step)
+    const uint32_t* rk2_test;  // Tables::rk2_test
     uint32_t nstreams;
     uint32_t mask;     // buzhash: the candidate mask in the rotated frame (below); rabin: as is
     uint32_t rk_shift;
@@ -1864,6 +1866,230 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
 //   2K    line fills (A line 0, B line 0, A line 1, ...), K = L/256 lines per chain;
 //   D     drain: B's last 64 bytes (no fill: the slot takes the next tile's warm fill, or
 //         the next stream's queue entry).
+#ifndef KCDC_RK_2STEP
+#define KCDC_RK_2STEP 1  // 1: two bytes per chain hop (rk2_pair); 0: one byte per hop (round 2)
+#endif
+#if KCDC_RK_2STEP
+#ifndef KCDC_RK2_T
+#define KCDC_RK2_T true
+#endif
+// ---- two bytes per chain hop (round 3)
+// The roll is GF(2)-linear, so two rolls fold into one (v = the hash, a/b = its bits
+// 45..52 / 37..44, c1 c2 the entering and l1 l2 the leaving bytes):
+//   v2 = ((v << 16) | c1 << 8 | c2) ^ T_lo[b] ^ T_hi[a] ^ O16[l1] ^ outx[l2]
+// with T_lo[b] = b x^53 mod P | b << 53 (= mod[b]), T_hi[a] = a x^61 mod P | (a & 7) << 61
+// (both also clear the shifted-out bits 53..63), O16[l] = l x^520 mod P, outx[l] = l x^512
+// mod P (Tables::rk2_main).  All four reads depend on v or on data only, so the chain is one
+// LDS round trip per TWO bytes (round 2: one per byte).  The odd byte's hash is needed only
+// for its test, i.e. its low word: lo1 = (lo << 8 | c1) ^ (a x^53 mod P).lo ^ outx[l1].lo --
+// two 32-bit reads off the chain (Tables::rk2_test).
+//
+// Conflict-free without 32 replicas per table: every read's four results are only XORed
+// together, so WHICH table a lane reads in which instruction does not matter.  One 256-byte
+// row per index holds all four tables, 8 replicas each (slot 8 t + r); in read k lane l takes
+// table (g + k) & 3 (g = (l >> 3) & 3), replica l & 7 -- the 32 lanes of a ds_read_b64 group
+// hit 32 distinct 8-byte slots, whatever the indices.  The test family is the same idea with
+// 128-byte rows (two tables x 16 replicas, 32-bit entries, lanes 16..31 swap tables).
+// R4 = [b, a, l1, l2] (one v_perm of hi >> 5 and the leaving dword) holds the four row indices
+// in table order, so each address is ONE v_perm: [8 slot(l, k), R4 byte t, 0, 0].
+// LDS: 32 KiB test rows + 64 KiB main rows + 8 x 8 KiB step slots = 160 KiB.
+struct RkTables {
+    uint32_t q[256 * 32];  // test family: row i (128 B), slots 0..15 (a x^53).lo, 16..31 outx[i].lo
+    uint64_t m[256 * 32];  // main family: row i (256 B), slots 8t..8t+7 table t = T_lo, T_hi, O16, outx
+};
+static_assert(sizeof(RkTables) + sizeof(DmaSlots) <= 160 * 1024, "Rabin-Karp tables + step slots exceed LDS");
+
+struct RkCtx {
+    const char* qb;     // LDS byte address of RkTables::q
+    const char* mb;     // LDS byte address of RkTables::m
+    uint32_t selr[2];   // R4 selector for byte pairs at j = 0, 2: R4 rotated by g bytes, so
+                        // R4 byte k = the row index of table (g + k) & 3, g = (l >> 3) & 3
+    uint32_t off;       // byte k: 8 * slot of read k = 8 (8 ((g + k) & 3) + (l & 7))
+    uint32_t offq;      // byte k': 2 * 4 * (16 tq + (l & 15)), tq = ((l >> 4) & 1) ^ k'
+    uint32_t selq[2];   // test read k': [OFFQ byte k', R4 byte of table 1 + tq, 0, 0] (halved:
+                        // 128-byte rows)
+    uint32_t mask;      // avg - 1
+};
+// Read k's address: [OFF byte k, R4 byte k, 0, 0] (the same selector in every lane).
+constexpr uint32_t rk2_sel(int k) { return 0x0c0c0000u | (static_cast<uint32_t>(k) << 8) | (4u + k); }
+
+// Fill the LDS tables from the device copies of Tables::rk2_main / rk2_test and set up the
+// lane's selectors (all threads of the workgroup; ends with a barrier).
+__device__ __forceinline__ RkCtx rk_setup(RkTables& smt, const BatchArgs& a, int lane) {
+    for (uint32_t i = threadIdx.x; i < 256u * 32u; i += blockDim.x) {
+        const uint32_t row = i >> 5, s = i & 31u;
+        smt.m[i] = a.rk2_main[4 * row + (s >> 3)];
+        smt.q[i] = a.rk2_test[2 * row + (s >> 4)];
+    }
+    __syncthreads();
+    RkCtx k;
+    k.qb = reinterpret_cast<const char*>(smt.q);
+    k.mb = reinterpret_cast<const char*>(smt.m);
+    const uint32_t l = static_cast<uint32_t>(lane), g = (l >> 3) & 3u;
+    k.off = 0;
+    k.selr[0] = k.selr[1] = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < 4; r++) {
+        const uint32_t t = (g + r) & 3u;  // R4 (unrotated) = [b, a, l1, l2]: bytes 0, 1 of hi >> 5, then pl
+        k.off |= (8u * (8u * t + (l & 7u))) << (8 * r);
+        k.selr[0] |= (t < 2 ? t : 4u + (t - 2)) << (8 * r);
+        k.selr[1] |= (t < 2 ? t : 6u + (t - 2)) << (8 * r);
+    }
+    k.offq = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < 2; r++) {
+        const uint32_t tq = ((l >> 4) & 1u) ^ r;
+        k.offq |= (8u * (16u * tq + (l & 15u))) << (8 * r);
+        k.selq[r] = 0x0c0c0000u | (((1u + tq - g) & 3u) << 8) | (4u + r);
+    }
+    k.mask = a.mask;
+    return k;
+}
+
+// One chain's two-byte hop at byte pair (x, x + 1) of a 64-byte piece: `w` the entering
+// dword, `pl` the leaving dword (the same bytes 64 positions earlier), j = x & 3 (0 or 2).
+// Issues the six table reads (R4 = [b, a, l1, l2] rotated by g bytes); rk2_finish consumes them.
+struct Rk2Reads {
+    uint64_t m[4];
+    uint32_t q[2];
+};
+template <int J, bool TEST>
+__device__ __forceinline__ Rk2Reads rk2_issue(const RkCtx& k, uint32_t hi, uint32_t pl) {
+    Rk2Reads r;
+    const uint32_t t = hi >> 5;  // [b, a, 0, 0] (hi < 2^21)
+    const uint32_t r4 = __builtin_amdgcn_perm(pl, t, k.selr[J >> 1]);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        r.m[i] = *reinterpret_cast<const uint64_t*>(k.mb + __builtin_amdgcn_perm(k.off, r4, rk2_sel(i)));
+    if (TEST) {
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+            r.q[i] = *reinterpret_cast<const uint32_t*>(k.qb + (__builtin_amdgcn_perm(k.offq, r4, k.selq[i]) >> 1));
+    }
+    return r;
+}
+// The hop's new state; with TEST, mm = min(mm, lo1 & mask, lo2 & mask).
+template <int J, bool TEST>
+__device__ __forceinline__ void rk2_finish(const RkCtx& k, uint32_t& hi, uint32_t& lo, uint32_t w, const Rk2Reads& r,
+                                           uint32_t& mm) {
+    const uint32_t sh = __builtin_amdgcn_alignbit(hi, lo, 16);  // (v << 16), high word
+    // (v << 16) | c1 << 8 | c2, low word: [c2, c1, lo.b0, lo.b1]
+    const uint32_t sl = __builtin_amdgcn_perm(w, lo, 0x01000000u | (static_cast<uint32_t>(4 + J) << 8) | (5u + J));
+    uint32_t l1 = 0;
+    if (TEST)  // (v << 8) | c1, low word: [c1, lo.b0, lo.b1, lo.b2]
+        l1 = __builtin_amdgcn_perm(w, lo, 0x02010000u | (4u + J));
+    const uint32_t h2 = __builtin_amdgcn_bitop3_b32(sh, static_cast<uint32_t>(r.m[0] >> 32),
+                                                    static_cast<uint32_t>(r.m[1] >> 32), 0x96);
+    const uint32_t l2 = __builtin_amdgcn_bitop3_b32(sl, static_cast<uint32_t>(r.m[0]), static_cast<uint32_t>(r.m[1]), 0x96);
+    hi = __builtin_amdgcn_bitop3_b32(h2, static_cast<uint32_t>(r.m[2] >> 32), static_cast<uint32_t>(r.m[3] >> 32), 0x96);
+    lo = __builtin_amdgcn_bitop3_b32(l2, static_cast<uint32_t>(r.m[2]), static_cast<uint32_t>(r.m[3]), 0x96);
+    if (TEST) {
+        const uint32_t v1 = __builtin_amdgcn_bitop3_b32(l1, r.q[0], r.q[1], 0x96);
+        mm = min(mm, min(v1 & k.mask, lo & k.mask));
+    }
+}
+
+// 64 bytes of chain A (in a / leaving pa) and of chain B (in b / leaving pb), interleaved
+// hop by hop; ma/mb: running min of (lo & mask) over the piece's 64 positions.  ACT_A/ACT_B:
+// whether that chain's bytes are real (an idle chain is not rolled at all).
+template <bool ACT_A, bool ACT_B>
+__device__ __forceinline__ void rk2_step64(const RkCtx& k, uint32_t& ha, uint32_t& la, const uint32_t (&a)[16],
+                                           const uint32_t (&pa)[16], uint32_t& hb, uint32_t& lb,
+                                           const uint32_t (&b)[16], const uint32_t (&pb)[16], uint32_t& ma,
+                                           uint32_t& mb) {
+#pragma unroll
+    for (int x = 0; x < 64; x += 2) {
+        __builtin_amdgcn_sched_barrier(0);
+        Rk2Reads ra, rb;
+        if ((x & 3) == 0) {
+            if (ACT_A) ra = rk2_issue<0, KCDC_RK2_T>(k, ha, pa[x >> 2]);
+            if (ACT_B) rb = rk2_issue<0, KCDC_RK2_T>(k, hb, pb[x >> 2]);
+        } else {
+            if (ACT_A) ra = rk2_issue<2, KCDC_RK2_T>(k, ha, pa[x >> 2]);
+            if (ACT_B) rb = rk2_issue<2, KCDC_RK2_T>(k, hb, pb[x >> 2]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if ((x & 3) == 0) {
+            if (ACT_A) rk2_finish<0, KCDC_RK2_T>(k, ha, la, a[x >> 2], ra, ma);
+            if (ACT_B) rk2_finish<0, KCDC_RK2_T>(k, hb, lb, b[x >> 2], rb, mb);
+        } else {
+            if (ACT_A) rk2_finish<2, KCDC_RK2_T>(k, ha, la, a[x >> 2], ra, ma);
+            if (ACT_B) rk2_finish<2, KCDC_RK2_T>(k, hb, lb, b[x >> 2], rb, mb);
+        }
+        // keep the running mins sequential (reassociated into trees they hold ~2 x 64 values)
+        if (ACT_A) asm volatile("" : "+v"(ma));
+        if (ACT_B) asm volatile("" : "+v"(mb));
+    }
+}
+
+// Exact re-run of one chain's 64 bytes at coordinate c from (hi, lo) (rare): first index in
+// [lo_i, hi_i] with (lo & mask) == 0, else 64.  The bytes are re-read from global memory one
+// dword pair at a time (the walk's 32-register copies of them pushed the kernel into spills
+// whose reloads waited on the line DMA); plain per-lane table addressing (conflicts do not
+// matter here).  Bytes before the stream start read as zero, as in the walk.
+__device__ uint32_t rk_exact64(const RkCtx& k, uint32_t hi, uint32_t lo, const Loader& ld, int64_t c, int lo_i,
+                               int hi_i) {
+    const uint32_t l = static_cast<uint32_t>(__lane_id());
+    uint32_t first = 64;
+    auto dword_at = [&](int64_t cc) -> uint32_t {
+        uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(ld.rsrc, static_cast<int32_t>(cc - ld.tb), 0, 0);
+        const int64_t keep_from = ld.off0 - cc;  // first byte of the dword inside the stream
+        if (keep_from > 0) v = keep_from >= 4 ? 0u : v & (0xFFFFFFFFu << (8 * keep_from));
+        return v;
+    };
+#pragma unroll 1
+    for (int j = 0; j < 16; j++) {
+        const uint32_t w = dword_at(c + 4 * j), pl = c - 64 + 4 * j >= 0 ? dword_at(c - 64 + 4 * j) : 0u;
+#pragma unroll
+        for (int J = 0; J < 4; J += 2) {
+            const uint32_t ib = (hi >> 5) & 0xFFu, ia = (hi >> 13) & 0xFFu, i1 = (pl >> (8 * J)) & 0xFFu,
+                           i2 = (pl >> (8 * J + 8)) & 0xFFu;  // rows of T_lo, T_hi, O16, outx
+            auto ent = [&](uint32_t row, uint32_t t) {
+                return *reinterpret_cast<const uint64_t*>(k.mb + 256u * row + 8u * (8u * t + (l & 7u)));
+            };
+            const uint64_t m = ent(ib, 0) ^ ent(ia, 1) ^ ent(i1, 2) ^ ent(i2, 3);
+            const uint32_t q0 = *reinterpret_cast<const uint32_t*>(k.qb + 128u * ia + 4u * (l & 15u));
+            const uint32_t q1 = *reinterpret_cast<const uint32_t*>(k.qb + 128u * i1 + 4u * (16u + (l & 15u)));
+            const uint32_t c1 = (w >> (8 * J)) & 0xFFu, c2 = (w >> (8 * J + 8)) & 0xFFu;
+            const uint32_t lo1 = ((lo << 8) | c1) ^ q0 ^ q1;
+            const uint32_t nhi = ((hi << 16) | (lo >> 16)) ^ static_cast<uint32_t>(m >> 32);
+            lo = ((lo << 16) | (c1 << 8) | c2) ^ static_cast<uint32_t>(m);
+            hi = nhi;
+            const int i = 4 * j + J;
+            if (first == 64 && (lo1 & k.mask) == 0 && i >= lo_i && i <= hi_i) first = static_cast<uint32_t>(i);
+            if (first == 64 && (lo & k.mask) == 0 && i + 1 >= lo_i && i + 1 <= hi_i) first = static_cast<uint32_t>(i + 1);
+        }
+    }
+    return first;
+}
+
+// Warm fill of a tile -> both chains' 64-byte histories (pa, pb) and states (leaving bytes 0:
+// every leaving-table row 0 is zero).
+__device__ __forceinline__ void rk_warm(const RkCtx& kx, const uint32_t (&dw)[32], uint32_t& ha, uint32_t& la,
+                                        uint32_t& hb, uint32_t& lb, uint32_t (&pa)[16], uint32_t (&pb)[16]) {
+    ha = la = hb = lb = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        pa[i] = dw[i];
+        pb[i] = dw[16 + i];
+    }
+    uint32_t mm = 0;
+#pragma unroll
+    for (int x = 0; x < 64; x += 2) {
+        __builtin_amdgcn_sched_barrier(0);
+        if ((x & 3) == 0) {
+            const Rk2Reads ra = rk2_issue<0, false>(kx, ha, 0u), rb = rk2_issue<0, false>(kx, hb, 0u);
+            rk2_finish<0, false>(kx, ha, la, pa[x >> 2], ra, mm);
+            rk2_finish<0, false>(kx, hb, lb, pb[x >> 2], rb, mm);
+        } else {
+            const Rk2Reads ra = rk2_issue<2, false>(kx, ha, 0u), rb = rk2_issue<2, false>(kx, hb, 0u);
+            rk2_finish<2, false>(kx, ha, la, pa[x >> 2], ra, mm);
+            rk2_finish<2, false>(kx, hb, lb, pb[x >> 2], rb, mm);
+        }
+    }
+}
+#define RK_STEP rk2_step64
+#else  // KCDC_RK_2STEP == 0: one byte per chain hop (round 2)
 // Tables (96 KiB, conflict-free or nearly): out[] with 32 replicas at a 256-byte stride
 // (lane l reads replica l % 32, bank pair 2(l % 32); address = one v_perm of the leaving
 // byte), mod[] with 16 replicas at a 128-byte stride (lanes l and l+16 share a bank pair
@@ -2066,6 +2292,53 @@ __device__ uint32_t rk_exact64(const RkCtx& k, uint32_t hi, uint32_t lo, const u
     return first;
 }
 
+// Warm fill of a tile -> both chains' 64-byte histories (pa, pb) and states.
+__device__ __forceinline__ void rk_warm(const RkCtx& kx, const uint32_t (&dw)[32], uint32_t& ha, uint32_t& la,
+                                        uint32_t& hb, uint32_t& lb, uint32_t (&pa)[16], uint32_t (&pb)[16]) {
+    ha = la = hb = lb = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        pa[i] = dw[i];
+        pb[i] = dw[16 + i];
+    }
+#pragma unroll
+    for (int x = 0; x < 64; x++) {
+        if (x % 16 == 0) __builtin_amdgcn_sched_barrier(0);
+        rk_roll0(kx, ha, la, pa[x >> 2], x & 3);
+        rk_roll0(kx, hb, lb, pb[x >> 2], x & 3);
+    }
+}
+__device__ __forceinline__ RkCtx rk_setup(RkTables& smt, const BatchArgs& a, int lane) {
+    for (uint32_t i = threadIdx.x; i < 256u * kRkModRep; i += blockDim.x) smt.mod[i] = a.rk_mod[i / kRkModRep];
+    for (uint32_t i = threadIdx.x; i < 256u * kRkOutRep; i += blockDim.x) {  // outx[] (rk_roll)
+        const uint64_t o = a.rk_out[i / kRkOutRep];
+        smt.out[i] = (o << 8) ^ a.rk_mod[(o >> 45) & 0xFFu];
+    }
+    __syncthreads();
+    RkCtx kx;
+    kx.modb = reinterpret_cast<const char*>(smt.mod);
+    kx.outb = reinterpret_cast<const char*>(smt.out);
+    kx.lane8o = static_cast<uint32_t>(lane & (kRkOutRep - 1)) * 8u;
+    kx.lane8m = static_cast<uint32_t>(lane & (kRkModRep - 1)) * 8u;
+    kx.mask = a.mask;
+    return kx;
+}
+#if KCDC_RK_ORDER
+#define RK_STEP rk_step64_ord
+#else
+#define RK_STEP rk_step64
+#endif
+#endif  // KCDC_RK_2STEP
+// The rare exact re-run of a 64-byte piece at coordinate c whose running test passed.
+__device__ __forceinline__ uint32_t rk_exact(const RkCtx& k, uint32_t h0, uint32_t l0, const Loader& ld, int64_t c,
+                                            const uint32_t (&in)[16], const uint32_t (&prv)[16], int lo_i, int hi_i) {
+#if KCDC_RK_2STEP
+    return rk_exact64(k, h0, l0, ld, c, lo_i, hi_i);
+#else
+    return rk_exact64(k, h0, l0, in, prv, lo_i, hi_i);
+#endif
+}
+
 // Geometry of a Rabin-Karp tile at ct: L bytes per lane (a multiple of 256: two chains of
 // whole 128-byte lines), K lines per chain.
 struct RkGeom {
@@ -2116,17 +2389,14 @@ __device__ __forceinline__ void rk_mask_head(uint32_t (&dw)[16], int64_t c, int6
     }
 }
 
-#if KCDC_RK_ORDER
-#define RK_STEP rk_step64_ord
-#else
-#define RK_STEP rk_step64
-#endif
 // The line fills and drain of one tile (after its warm fill, which left both chains' states
 // and histories in ha/la, hb/lb, pa, pb): refill(f) is called right after fill f has been
-// read out of the slot (the slot is free), check(min, chain, coordinate, state before,
-// bytes, history) after each chain's 64 bytes.
+// read out of the slot (the slot is free), check(min, chain, offset from the chain's start,
+// state before, bytes, history) after each chain's 64 bytes.  Coordinates stay out of the
+// walk (64-bit per-lane values live across it spilled, and every reload's vmcnt wait drained
+// the line DMA): `head` says whether lane 0's chain A starts at coordinate 0.
 template <class Refill, class Check>
-__device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int lane, int64_t c0, int64_t c0b,
+__device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int lane, bool head,
                                         int64_t off0, int K, uint32_t& ha, uint32_t& la, uint32_t& hb, uint32_t& lb,
                                         uint32_t (&pa)[16], uint32_t (&pb)[16], Refill&& refill, Check&& check) {
     uint32_t bf[16];  // the second half of the line that arrived last step
@@ -2140,7 +2410,7 @@ __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int 
 #if KCDC_RK_ABL != 3
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
-            read_step128(sl, lane, c0 + 128 * j, off0, dw);
+            read_step128(sl, lane, head && j == 0 ? 0 : 1, off0, dw);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             refill(2 * j + 1);
@@ -2153,11 +2423,11 @@ __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int 
                 RK_STEP<true, false>(kx, ha, la, na, pa, hb, lb, bf, pb, ma, mb);
             } else {
                 RK_STEP<true, true>(kx, ha, la, na, pa, hb, lb, bf, pb, ma, mb);
-                check(mb, 1, c0b + 128 * (j - 1) + 64, hb0, lb0, bf, pb);
+                check(mb, 1, 128 * (j - 1) + 64, hb0, lb0, bf, pb);
 #pragma unroll
                 for (int i = 0; i < 16; i++) pb[i] = bf[i];
             }
-            check(ma, 0, c0 + 128 * j, ha0, la0, na, pa);
+            check(ma, 0, 128 * j, ha0, la0, na, pa);
 #pragma unroll
             for (int i = 0; i < 16; i++) {
                 pa[i] = na[i];
@@ -2171,7 +2441,7 @@ __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int 
 #if KCDC_RK_ABL != 3
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
-            read_step128(sl, lane, c0b + 128 * j, off0, dw);
+            read_step128(sl, lane, 1, off0, dw);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             refill(2 * j + 2);
@@ -2181,8 +2451,8 @@ __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int 
             const uint32_t ha0 = ha, la0 = la, hb0 = hb, lb0 = lb;
             uint32_t ma = 0xFFFFFFFFu, mb = 0xFFFFFFFFu;
             RK_STEP<true, true>(kx, ha, la, bf, pa, hb, lb, nb, pb, ma, mb);
-            check(ma, 0, c0 + 128 * j + 64, ha0, la0, bf, pa);
-            check(mb, 1, c0b + 128 * j, hb0, lb0, nb, pb);
+            check(ma, 0, 128 * j + 64, ha0, la0, bf, pa);
+            check(mb, 1, 128 * j, hb0, lb0, nb, pb);
 #pragma unroll
             for (int i = 0; i < 16; i++) {
                 pa[i] = bf[i];
@@ -2196,282 +2466,16 @@ __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int 
         const uint32_t hb0 = hb, lb0 = lb;
         uint32_t ma = 0xFFFFFFFFu, mb = 0xFFFFFFFFu;
         RK_STEP<false, true>(kx, ha, la, bf, pa, hb, lb, bf, pb, ma, mb);
-        check(mb, 1, c0b + 128 * (K - 1) + 64, hb0, lb0, bf, pb);
-    }
-}
-
-// Warm fill of a tile -> both chains' 64-byte histories (pa, pb) and states.
-__device__ __forceinline__ void rk_warm(const RkCtx& kx, const uint32_t (&dw)[32], uint32_t& ha, uint32_t& la,
-                                        uint32_t& hb, uint32_t& lb, uint32_t (&pa)[16], uint32_t (&pb)[16]) {
-    ha = la = hb = lb = 0;
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-        pa[i] = dw[i];
-        pb[i] = dw[16 + i];
-    }
-#pragma unroll
-    for (int x = 0; x < 64; x++) {
-        if (x % 16 == 0) __builtin_amdgcn_sched_barrier(0);
-        rk_roll0(kx, ha, la, pa[x >> 2], x & 3);
-        rk_roll0(kx, hb, lb, pb[x >> 2], x & 3);
-    }
-}
-
-// ---------------------------------------------------------------- four chains per lane
-// Each lane runs FOUR chains (its segment in quarters, one per chain): four mod[] reads in
-// flight per lane, eight per SIMD.  The step slot still receives one whole 128-byte line
-// per lane per step, for the chains in rotation (fill f = line f/4 of chain f%4); a chain
-// consumes 32 bytes per step, so it holds its current line (and the previous line's last
-// 64 bytes, the leaving bytes of its first two quarters) in VGPRs.  Chain X starts X steps
-// after chain 0 (its first line arrives then): a tile is 2 warm fills ([A | B] and
-// [C | D] 64-byte histories) and 4n line fills, 4n + 3 steps; a chain outside its range in
-// a step (the first and last three) rolls stale registers and is restored.  The steps are
-// unrolled four at a time so which registers hold which quarter is static.
-#ifndef KCDC_RK_CHAINS
-#define KCDC_RK_CHAINS 2  // 4: the four-chain walker (rk4_walk) -- it needs ~370 VGPRs and spills
-#endif
-struct Rk4Geom {
-    int64_t L;  // bytes per lane (a multiple of 512)
-    int n;      // 128-byte lines per chain
-    Loader ld;
-};
-__device__ __forceinline__ Rk4Geom rk4_geom(int64_t ct, int64_t hi, const uint8_t* abase, int64_t off0,
-                                            int64_t nbytes_coord) {
-    const int64_t rem = hi - ct + 1;
-    int64_t per = (rem + kWave - 1) / kWave;
-    per = (per + 511) & ~int64_t(511);
-    Rk4Geom g;
-    g.L = per < kLaneMax ? per : kLaneMax;
-    g.n = static_cast<int>(g.L / 512);
-    g.ld = make_loader(abase, off0, nbytes_coord, ct >= 64 ? ct - 64 : 0);
-    return g;
-}
-// DMA lane offsets of a tile, computed once per tile in two VGPRs (the per-instruction
-// offsets of four chains' fills, hoisted by the compiler, cost ~100 VGPRs and spills).
-// Instruction i, DMA lane d: lane segment l = 8i + d/8 and 16-byte chunk jj = (d&7) ^
-// ((l>>1)&7), which is j0 for even i and j0 ^ 4 for odd i (j0 = (d&7) ^ ((d>>4)&3)).
-struct Rk4Lane {
-    uint32_t pe, po;  // (d/8) * L + 16 * jj, even / odd instructions
-    uint32_t je;      // j0 (the warm fills need the chunk's chain half)
-};
-__device__ __forceinline__ Rk4Lane rk4_lane(int64_t L, int lane) {
-    Rk4Lane r;
-    const uint32_t lb = static_cast<uint32_t>(lane) >> 3;
-    r.je = (static_cast<uint32_t>(lane) & 7u) ^ ((lb >> 1) & 7u);
-    r.pe = lb * static_cast<uint32_t>(L) + 16u * r.je;
-    r.po = lb * static_cast<uint32_t>(L) + 16u * (r.je ^ 4u);
-    asm volatile("" : "+v"(r.pe), "+v"(r.po), "+v"(r.je));  // computed here, not hoisted as 16 values
-    return r;
-}
-// Line fill f: line f/4 of chain f%4 (16-byte chunks of 128-byte runs, as dma_step128).
-__device__ __forceinline__ void rk4_dma_line(const Loader& ld, uint32_t slot, int64_t ct, int64_t L, int f,
-                                             const Rk4Lane& ln) {
-#ifdef KCDC_EXP_COMPONLY
-    return;
-#endif
-    const int32_t base = static_cast<int32_t>(ct + (f & 3) * (L / 4) + 128 * (f >> 2) - ld.tb);
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-        dma_lds16(ld.d, slot + 1024u * i, base + static_cast<int32_t>(8 * i * L) + static_cast<int32_t>(i & 1 ? ln.po : ln.pe));
-}
-// Warm fill `half` (0: chains 0,1; 1: chains 2,3): lane l's slot line = [64 B before chain
-// 2h's quarter | 64 B before chain 2h+1's].
-__device__ __forceinline__ void rk4_dma_warm(const Loader& ld, uint32_t slot, int64_t ct, int64_t L, int half,
-                                             const Rk4Lane& ln) {
-#ifdef KCDC_EXP_COMPONLY
-    return;
-#endif
-    const int64_t Q = L / 4;
-    const int32_t base = static_cast<int32_t>(ct + 2 * half * Q - 64 - ld.tb);
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const uint32_t jj = i & 1 ? ln.je ^ 4u : ln.je;
-        // (d/8) * L + 16 * (jj & 3) + (jj >> 2) * Q
-        const uint32_t lanepart = (i & 1 ? ln.po : ln.pe) - 64u * (jj >> 2) + (jj >> 2) * static_cast<uint32_t>(Q);
-        dma_lds16(ld.d, slot + 1024u * i, base + static_cast<int32_t>(8 * i * L) + static_cast<int32_t>(lanepart));
-    }
-}
-
-// 32 bytes of each of the four chains, interleaved byte by byte, read straight from the
-// line buffers (chain X consumes quarter q = (R - X) & 3 of Lb[X]; its leaving bytes are
-// Tl[X] for quarters 0, 1 and Lb[X] itself for 2, 3: static indices, no copies);
-// mk[X]: running min of (lo & mask).  The four mod[] reads of a byte issue before the
-// outx[] reads of the next byte (in-order LDS returns).
-template <int R>
-__device__ __forceinline__ uint32_t rk4_in(const uint32_t (&Lb)[4][32], int X, int i) {
-    const int q = (R - X) & 3;
-    return Lb[X][8 * q + i];
-}
-template <int R>
-__device__ __forceinline__ uint32_t rk4_lv(const uint32_t (&Lb)[4][32], const uint32_t (&Tl)[4][16], int X, int i) {
-    const int q = (R - X) & 3;
-    return q < 2 ? Tl[X][8 * q + i] : Lb[X][8 * (q - 2) + i];
-}
-template <int R>
-__device__ __forceinline__ void rk4_step32(const RkCtx& k, uint32_t (&h)[4], uint32_t (&lw)[4],
-                                           const uint32_t (&Lb)[4][32], const uint32_t (&Tl)[4][16],
-                                           uint32_t (&mk)[4]) {
-    uint64_t ox[4], nx[4];
-#pragma unroll
-    for (int X = 0; X < 4; X++) ox[X] = rk_out(k, rk4_lv<R>(Lb, Tl, X, 0), 0);
-#pragma unroll
-    for (int x = 0; x < 32; x++) {
-        const int sh = kRkModRep == 32 ? 8 : 7;
-        uint64_t m[4];
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int X = 0; X < 4; X++)
-            m[X] = *reinterpret_cast<const uint64_t*>(k.modb + ((__builtin_amdgcn_ubfe(h[X], kRkIdxBit, 8) << sh) | k.lane8m));
-        if (x + 1 < 32) {
-#pragma unroll
-            for (int X = 0; X < 4; X++) nx[X] = rk_out(k, rk4_lv<R>(Lb, Tl, X, (x + 1) >> 2), (x + 1) & 3);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int X = 0; X < 4; X++) {
-            const uint32_t th = __builtin_amdgcn_alignbit(h[X], lw[X], 24);
-            const uint32_t tl = __builtin_amdgcn_perm(rk4_in<R>(Lb, X, x >> 2), lw[X], 0x02010000u | (4u + (x & 3)));
-            h[X] = __builtin_amdgcn_bitop3_b32(th, static_cast<uint32_t>(m[X] >> 32), static_cast<uint32_t>(ox[X] >> 32),
-                                               0x96);
-            lw[X] = __builtin_amdgcn_bitop3_b32(tl, static_cast<uint32_t>(m[X]), static_cast<uint32_t>(ox[X]), 0x96);
-            mk[X] = min(mk[X], lw[X] & k.mask);
-            ox[X] = nx[X];
-        }
-        if ((x & 3) == 3) {
-#pragma unroll
-            for (int X = 0; X < 4; X++) asm volatile("" : "+v"(mk[X]));
-        }
-    }
-}
-
-// Exact re-run of one chain's 32 bytes (rare): first index in [lo_i, hi_i], else 32.
-__device__ uint32_t rk_exact32(const RkCtx& k, uint32_t hi, uint32_t lo, const uint32_t (&in)[8],
-                               const uint32_t (&lv)[8], int lo_i, int hi_i) {
-    uint32_t e[8], o[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        e[j] = in[j];
-        o[j] = lv[j];
-    }
-    uint32_t first = 32;
-#pragma unroll 1
-    for (int j = 0; j < 8; j++) {
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            rk_roll(k, hi, lo, rk_out(k, o[0], b), e[0], b);
-            const int i = 4 * j + b;
-            if (first == 32 && (lo & k.mask) == 0 && i >= lo_i && i <= hi_i) first = static_cast<uint32_t>(i);
-        }
-#pragma unroll
-        for (int q = 0; q < 7; q++) {
-            e[q] = e[q + 1];
-            o[q] = o[q + 1];
-        }
-    }
-    return first;
-}
-
-// A whole four-chain tile: both warm fills (the first already in flight or landed),
-// 4n line fills and the drain steps.  refill(f): f = -2 (take warm fill 1), -1 (take line
-// fill 0), 0..4n-1 (after line fill f was read: the next fill, or after the last one the
-// next tile's warm fill / a queue entry).  check(min, chain, coordinate, state before,
-// bytes, leaving bytes) after each active chain-piece.
-template <class Refill, class Check>
-__device__ __forceinline__ void rk4_walk(const RkCtx& kx, const uint8_t* sl, int lane, int64_t c0, int64_t Q,
-                                         int64_t off0, int n, Refill&& refill, Check&& check) {
-    uint32_t Lb[4][32], Tl[4][16], h[4], lw[4];
-#pragma unroll
-    for (int w = 0; w < 2; w++) {  // warm fills: chains 2w, 2w+1 roll their 64-byte histories
-        uint32_t dw[32];
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        read_step128(sl, lane, -1, off0, dw);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        refill(w - 2);
-        __builtin_amdgcn_sched_barrier(0);
-        const int A = 2 * w, B = 2 * w + 1;
-        h[A] = lw[A] = h[B] = lw[B] = 0;
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-            Tl[A][i] = dw[i];
-            Tl[B][i] = dw[16 + i];
-        }
-#pragma unroll
-        for (int x = 0; x < 64; x++) {
-            if (x % 16 == 0) __builtin_amdgcn_sched_barrier(0);
-            rk_roll0(kx, h[A], lw[A], Tl[A][x >> 2], x & 3);
-            rk_roll0(kx, h[B], lw[B], Tl[B][x >> 2], x & 3);
-        }
-    }
-    const int steps = 4 * n + 3;
-    auto step = [&](auto rc, int s) {
-        constexpr int r = decltype(rc)::value;  // the chain whose line arrives in this step
-        if (s < 4 * n) {
-            if (s >= 4) {  // the old line's last half: leaving bytes of the new quarters 0, 1
-#pragma unroll
-                for (int i = 0; i < 16; i++) Tl[r][i] = Lb[r][16 + i];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            read_step128(sl, lane, c0 + r * Q + 128 * (s >> 2), off0, Lb[r]);  // straight into the buffer
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-            refill(s);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        uint32_t h0[4], l0[4], mk[4];
-#pragma unroll
-        for (int X = 0; X < 4; X++) {
-            h0[X] = h[X];
-            l0[X] = lw[X];
-            mk[X] = 0xFFFFFFFFu;
-        }
-        rk4_step32<r>(kx, h, lw, Lb, Tl, mk);
-#pragma unroll
-        for (int X = 0; X < 4; X++) {
-            const int p = s - X;  // chain X's piece in this step
-            if (p >= 0 && p < 4 * n) {
-                if (mk[X] == 0) {  // rare: the exact re-run needs the piece's bytes as arrays
-                    uint32_t in[8], lv[8];
-#pragma unroll
-                    for (int i = 0; i < 8; i++) {
-                        in[i] = rk4_in<r>(Lb, X, i);
-                        lv[i] = rk4_lv<r>(Lb, Tl, X, i);
-                    }
-                    check(mk[X], X, c0 + X * Q + 32 * p, h0[X], l0[X], in, lv);
-                }
-            } else {  // outside its range (ramp): undo the rolls over stale registers
-                h[X] = h0[X];
-                lw[X] = l0[X];
-            }
-        }
-    };
-    for (int s0 = 0; s0 < steps; s0 += 4) {
-        step(std::integral_constant<int, 0>{}, s0);
-        if (s0 + 1 < steps) step(std::integral_constant<int, 1>{}, s0 + 1);
-        if (s0 + 2 < steps) step(std::integral_constant<int, 2>{}, s0 + 2);
-        if (s0 + 3 < steps) step(std::integral_constant<int, 3>{}, s0 + 3);
+        check(mb, 1, 128 * (K - 1) + 64, hb0, lb0, bf, pb);
     }
 }
 
 __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_rk_kernel(BatchArgs a) {
     __shared__ RkTables smt;
     __shared__ DmaSlots smslots;
-    for (uint32_t i = threadIdx.x; i < 256u * kRkModRep; i += blockDim.x) smt.mod[i] = a.rk_mod[i / kRkModRep];
-    for (uint32_t i = threadIdx.x; i < 256u * kRkOutRep; i += blockDim.x) {  // outx[] (rk_roll)
-        const uint64_t o = a.rk_out[i / kRkOutRep];
-        smt.out[i] = (o << 8) ^ a.rk_mod[(o >> 45) & 0xFFu];
-    }
-    __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    RkCtx kx;
-    kx.modb = reinterpret_cast<const char*>(smt.mod);
-    kx.outb = reinterpret_cast<const char*>(smt.out);
-    kx.lane8o = static_cast<uint32_t>(lane & (kRkOutRep - 1)) * 8u;
-    kx.lane8m = static_cast<uint32_t>(lane & (kRkModRep - 1)) * 8u;
-    kx.mask = a.mask;
+    const RkCtx kx = rk_setup(smt, a, lane);
     uint8_t* sl = smslots.b[wave][0];
     const uint32_t sl32 = lds_addr(sl);
     const int64_t mx = static_cast<int64_t>(a.max_size);
@@ -2533,11 +2537,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         if (!pcheck(a, lane, cur, 0xFFFFFFFFu, 5)) return;
         int64_t lo, hi;
         pregion(a, cur, lo, hi);
-#if KCDC_RK_CHAINS == 4
-        const Rk4Geom g = rk4_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n);
-#else
         const RkGeom g = rk_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n, a.lane_cap);
-#endif
         const int64_t ct = cur.ct, ct_next = ct + kWave * g.L;
         const bool last_of_region = ct_next > hi;
         const bool budget_out = budget - kWave * g.L <= 0;
@@ -2550,16 +2550,8 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         const bool reserve = budget_out && !ends_nocand;
         uint64_t ht_raw = 0;
         if (switching) ht_raw = qht_add(a, lane, 1);  // the next stream's ticket
-        const int64_t c0 = ct + lane * g.L;
         uint32_t ht_lo = static_cast<uint32_t>(ht_raw), ht_hi = static_cast<uint32_t>(ht_raw >> 32);
-#if KCDC_RK_CHAINS == 4
-        const Rk4Lane ln = rk4_lane(g.L, lane);
-        if (!issued) rk4_dma_warm(g.ld, sl32, ct, g.L, 0, ln);
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(ht_lo), "+v"(ht_hi)::"memory");  // the ticket, warm fill 0
-#else
         if (!issued) rk_dma_warm(g.ld, sl32, ct, g.L, lane);
-        const int64_t c0b = c0 + g.L / 2;
         uint32_t ha = 0, la = 0, hb = 0, lb = 0;
         uint32_t pa[16], pb[16];
         // ---- W: warm fill -> both chains' 64-byte histories; line 1 (A line 0) goes out
@@ -2574,7 +2566,6 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             __builtin_amdgcn_sched_barrier(0);
             rk_warm(kx, dw, ha, la, hb, lb, pa, pb);
         }
-#endif
         uint32_t tk = 0;
         int64_t nbacklog = 0;
         if (switching) {
@@ -2594,39 +2585,12 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                 pentry_dma(a, lane, tk, sl32);
                 entry_issued = true;
             } else if (!last_of_region) {  // the next tile has its own geometry
-#if KCDC_RK_CHAINS == 4
-                const Rk4Geom gn = rk4_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n);
-                rk4_dma_warm(gn.ld, sl32, ct_next, gn.L, 0, rk4_lane(gn.L, lane));
-#else
                 const RkGeom gn = rk_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n, a.lane_cap);
                 rk_dma_warm(gn.ld, sl32, ct_next, gn.L, lane);
-#endif
                 next_issued = true;
             }
         };
-#if KCDC_RK_CHAINS == 4
-        int64_t fq[4] = {-1, -1, -1, -1};  // each chain's first candidate
-        auto refill = [&](int f) {
-            if (f == -2)
-                rk4_dma_warm(g.ld, sl32, ct, g.L, 1, ln);
-            else if (f < 4 * g.n - 1)
-                rk4_dma_line(g.ld, sl32, ct, g.L, f + 1, ln);
-            else
-                refill_last();
-        };
-        auto check = [&](uint32_t mm, int chain, int64_t c, uint32_t h0, uint32_t l0, const uint32_t (&in)[8],
-                         const uint32_t (&lv)[8]) {
-            if (mm == 0 && fq[chain] < 0 && c <= hi) {
-                const int64_t blo = lo - c, bhi = hi - c;
-                const uint32_t idx = rk_exact32(kx, h0, l0, in, lv, blo < 0 ? 0 : static_cast<int>(blo),
-                                                bhi > 31 ? 31 : static_cast<int>(bhi));
-                if (idx < 32u) fq[chain] = c + idx;
-            }
-        };
-        rk4_walk(kx, sl, lane, c0, g.L / 4, cur.off0, g.n, refill, check);
-        const int64_t found = fq[0] >= 0 ? fq[0] : fq[1] >= 0 ? fq[1] : fq[2] >= 0 ? fq[2] : fq[3];
-#else
-        int64_t found_a = -1, found_b = -1;
+        int32_t found_a = -1, found_b = -1;  // offsets from the chain's start
         // After line fill f is read: issue what the slot takes next (fill f+1, or after the
         // last fill the next tile's warm fill / the next stream's queue entry).
         auto refill = [&](int f) {
@@ -2635,25 +2599,31 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             else
                 refill_last();
         };
-        // Hit check of one chain's 64 bytes at coordinate c (state before: h0/l0): the
-        // chain's first candidate in [lo, hi].
-        auto check = [&](uint32_t mm, int chain, int64_t c, uint32_t h0, uint32_t l0, const uint32_t (&in)[16],
+        // Hit check of one chain's 64 bytes at `rel` from its start (state before: h0/l0):
+        // the chain's first candidate in [lo, hi].  The coordinate is formed only here, from
+        // wave-uniform values and an opaque lane id (nothing 64-bit per lane lives across the walk).
+        auto check = [&](uint32_t mm, int chain, int rel, uint32_t h0, uint32_t l0, const uint32_t (&in)[16],
                          const uint32_t (&prv)[16]) {
-            if (mm == 0 && (chain ? found_b : found_a) < 0 && c <= hi) {
-                const int64_t blo = lo - c, bhi = hi - c;
-                const uint32_t idx = rk_exact64(kx, h0, l0, in, prv, blo < 0 ? 0 : static_cast<int>(blo),
-                                                bhi > 63 ? 63 : static_cast<int>(bhi));
-                if (idx < 64u) {
-                    if (chain)
-                        found_b = c + idx;
-                    else
-                        found_a = c + idx;
+            if (mm == 0 && (chain ? found_b : found_a) < 0) {
+                int ln = lane;
+                asm volatile("" : "+v"(ln));
+                const int64_t c = ct + ln * g.L + (chain ? g.L / 2 : 0) + rel;
+                if (c <= hi) {
+                    const int64_t blo = lo - c, bhi = hi - c;
+                    const uint32_t idx = rk_exact(kx, h0, l0, g.ld, c, in, prv, blo < 0 ? 0 : static_cast<int>(blo),
+                                                  bhi > 63 ? 63 : static_cast<int>(bhi));
+                    if (idx < 64u) {
+                        if (chain)
+                            found_b = rel + static_cast<int32_t>(idx);
+                        else
+                            found_a = rel + static_cast<int32_t>(idx);
+                    }
                 }
             }
         };
-        rk_walk(kx, sl, lane, c0, c0b, cur.off0, g.K, ha, la, hb, lb, pa, pb, refill, check);
-        const int64_t found = found_a >= 0 ? found_a : found_b;
-#endif
+        rk_walk(kx, sl, lane, ct == 0 && lane == 0, cur.off0, g.K, ha, la, hb, lb, pa, pb, refill, check);
+        const int64_t c0 = ct + lane * g.L;
+        const int64_t found = found_a >= 0 ? c0 + found_a : found_b >= 0 ? c0 + g.L / 2 + found_b : -1;
         // ---- end of tile
         if (reserve && !res_issued) {
             pe_raw = qht_add(a, lane, 1ull << 32);
@@ -3165,20 +3135,9 @@ __global__ __launch_bounds__(kScanWaves * kWave, 2) void cand_scan_kernel(BatchA
 __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void cand_scan_rk_kernel(BatchArgs a, LongArgs g) {
     __shared__ RkTables smt;
     __shared__ DmaSlots smslots;
-    for (uint32_t i = threadIdx.x; i < 256u * kRkModRep; i += blockDim.x) smt.mod[i] = a.rk_mod[i / kRkModRep];
-    for (uint32_t i = threadIdx.x; i < 256u * kRkOutRep; i += blockDim.x) {
-        const uint64_t o = a.rk_out[i / kRkOutRep];
-        smt.out[i] = (o << 8) ^ a.rk_mod[(o >> 45) & 0xFFu];
-    }
-    __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    RkCtx kx;
-    kx.modb = reinterpret_cast<const char*>(smt.mod);
-    kx.outb = reinterpret_cast<const char*>(smt.out);
-    kx.lane8o = static_cast<uint32_t>(lane & (kRkOutRep - 1)) * 8u;
-    kx.lane8m = static_cast<uint32_t>(lane & (kRkModRep - 1)) * 8u;
-    kx.mask = a.mask;
+    const RkCtx kx = rk_setup(smt, a, lane);
     uint8_t* sl = smslots.b[wave][0];
     const uint32_t sl32 = lds_addr(sl);
     const int64_t nw = static_cast<int64_t>(gridDim.x) * kDmaWaves;
@@ -3211,7 +3170,6 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void cand_scan_rk
         Seg qn = q;
         if (has_next) qn = seg_of(nseg_next);
         const RkGeom t = rk_geom(q.cs, q.hi, q.abase, q.off0, q.off0 + q.n);
-        const int64_t c0 = q.cs + lane * t.L, c0b = c0 + t.L / 2;
         uint32_t ha, la, hb, lb, pa[16], pb[16];
         {
             uint32_t dw[32];
@@ -3236,19 +3194,21 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void cand_scan_rk
             else if (has_next)
                 issue(qn);
         };
-        auto check = [&](uint32_t mm, int chain, int64_t c, uint32_t h0, uint32_t l0, const uint32_t (&in)[16],
+        auto check = [&](uint32_t mm, int chain, int crel, uint32_t h0, uint32_t l0, const uint32_t (&in)[16],
                          const uint32_t (&prv)[16]) {
             int& nf = chain ? nb : na;
             uint32_t(&fnd)[kSegK / 2] = chain ? fb : fa;
-            const int64_t cstart = chain ? c0b : c0;
-            if (mm == 0 && c <= q.hi && nf <= kSegK) {  // rare: enumerate the piece's candidates exactly
+            if (mm == 0 && nf <= kSegK) {  // rare: enumerate the piece's candidates exactly
+                int ln = lane;
+                asm volatile("" : "+v"(ln));  // the coordinate is formed here only (rk_walk)
+                const int64_t c = q.cs + ln * t.L + (chain ? t.L / 2 : 0) + crel;
                 const int64_t blo = q.lo - c, bhi = q.hi - c;
                 int from = blo < 0 ? 0 : static_cast<int>(blo);
                 const int to = bhi > 63 ? 63 : static_cast<int>(bhi);
                 while (from <= to && nf <= kSegK) {
-                    const uint32_t idx = rk_exact64(kx, h0, l0, in, prv, from, to);
+                    const uint32_t idx = rk_exact(kx, h0, l0, t.ld, c, in, prv, from, to);
                     if (idx >= 64u) break;
-                    const uint32_t rel = static_cast<uint32_t>(c - cstart) + idx;  // < 2^16
+                    const uint32_t rel = static_cast<uint32_t>(crel) + idx;  // < 2^16
 #pragma unroll
                     for (int k = 0; k < kSegK; k++)  // entry nf = rel, kept in registers (no scratch)
                         if (k == nf) fnd[k >> 1] |= rel << (16 * (k & 1));
@@ -3257,7 +3217,8 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void cand_scan_rk
                 }
             }
         };
-        rk_walk(kx, sl, lane, c0, c0b, q.off0, t.K, ha, la, hb, lb, pa, pb, refill, check);
+        rk_walk(kx, sl, lane, q.cs == 0 && lane == 0, q.off0, t.K, ha, la, hb, lb, pa, pb, refill, check);
+        const int64_t c0 = q.cs + lane * t.L, c0b = c0 + t.L / 2;
         // this lane's candidates in position order: chain A's, then chain B's
         const int nas = na < kSegK ? na : kSegK;
         const int nf = na + nb > kSegK ? kSegK + 1 : na + nb;
@@ -3743,6 +3704,8 @@ struct DeviceTables {
     uint32_t* buz = nullptr;
     uint64_t* rk_out = nullptr;
     uint64_t* rk_mod = nullptr;
+    uint64_t* rk2_main = nullptr;
+    uint32_t* rk2_test = nullptr;
     int cus = 0;
 };
 
@@ -3810,6 +3773,8 @@ dev::BatchArgs base_args(const Algo& algo, const DeviceTables& t) {
     a.buz = t.buz;
     a.rk_out = t.rk_out;
     a.rk_mod = t.rk_mod;
+    a.rk2_main = t.rk2_main;
+    a.rk2_test = t.rk2_test;
     a.rk_shift = static_cast<uint32_t>(tables().rk_shift);
     // largest power of two <= avg / 256, within [256, kLaneMax]: tiles of ~avg/4 (1 MiB and
     // larger averages keep the full 2 KiB lane segments)
@@ -3876,6 +3841,10 @@ const DeviceTables* device_tables(int device, int* err) {
     if (e == hipSuccess) e = hipMemcpy(d.buz, T.buz, sizeof(T.buz), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d.rk_out, T.rk_out, sizeof(T.rk_out), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d.rk_mod, T.rk_mod, sizeof(T.rk_mod), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&d.rk2_main, sizeof(T.rk2_main));
+    if (e == hipSuccess) e = hipMalloc(&d.rk2_test, sizeof(T.rk2_test));
+    if (e == hipSuccess) e = hipMemcpy(d.rk2_main, T.rk2_main, sizeof(T.rk2_main), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d.rk2_test, T.rk2_test, sizeof(T.rk2_test), hipMemcpyHostToDevice);
     (void)hipSetDevice(prev);
     if (e != hipSuccess) {
         *err = hip_fail(e, "table upload");

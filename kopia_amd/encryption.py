@@ -90,20 +90,24 @@ class Encryptor:
         Returns the device int32 status tensor (asynchronous on `stream`)."""
         import torch
         n = len(offsets)
-        status = torch.zeros(max(n, 1), dtype=torch.int32, device=device)
-        if n == 0:
-            return status[:0]
+        if stream is None:
+            stream = torch.cuda.current_stream(device)
         if nonces is None:
             nonces = os.urandom(NonceSize * n)
         if len(nonces) != NonceSize * n:
             raise ValueError("need 12 nonce bytes per chunk")
-        d_offs = torch.as_tensor(np.asarray(offsets, dtype=np.int64)).to(device)
-        d_lens = torch.as_tensor(np.asarray(lengths, dtype=np.int64)).to(device)
-        d_oo = torch.as_tensor(np.asarray(out_offsets, dtype=np.int64)).to(device)
-        d_nonce = torch.frombuffer(bytearray(nonces), dtype=torch.uint8).to(device)
-        work = self._work(n, device)
-        if stream is None:
-            stream = torch.cuda.current_stream(device)
+        # Every temporary is allocated and filled on `stream` itself, so the kernels below are
+        # ordered after those fills whatever the caller's current stream is.  The status words
+        # need no fill: the prep kernel writes every status[i].
+        with torch.cuda.stream(stream):
+            status = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+            if n == 0:
+                return status[:0]
+            d_offs = torch.as_tensor(np.asarray(offsets, dtype=np.int64)).to(device)
+            d_lens = torch.as_tensor(np.asarray(lengths, dtype=np.int64)).to(device)
+            d_oo = torch.as_tensor(np.asarray(out_offsets, dtype=np.int64)).to(device)
+            d_nonce = torch.frombuffer(bytearray(nonces), dtype=torch.uint8).to(device)
+            work = self._work(n, device)
         _lib.check(_lib.lib().kcdc_encrypt_chunks_device(
             self.name.encode(), self.secret, len(self.secret), C.c_void_p(data_ptr), d_offs.data_ptr(),
             d_lens.data_ptr(), n, C.c_void_p(d_ivs.data_ptr()), iv_len, iv_stride, d_nonce.data_ptr(), d_out.data_ptr(),
@@ -114,21 +118,37 @@ class Encryptor:
     def decrypt_chunks_device(self, sealed_ptr: int, offsets, sealed_lengths, d_ivs, iv_stride: int, d_out,
                               out_offsets, device, stream=None, iv_len: int = 16):
         """Open sealed chunk i = [offsets[i], +sealed_lengths[i]) into d_out at out_offsets[i].
-        Returns the device int32 status tensor: 0, KCDC_EBADMSG, KCDC_EINVAL or KCDC_EFBIG."""
+        Returns the device int32 status tensor: 0, KCDC_EBADMSG, KCDC_EINVAL or KCDC_EFBIG.
+
+        The plaintext is written before its tag is checked: d_out's slot of a chunk whose
+        status is not 0 holds unauthenticated bytes and must not be used (Go's AEAD.Open
+        returns no plaintext on failure).  raise_on_status(status) syncs and raises on any
+        failed chunk."""
         import torch
         n = len(offsets)
-        status = torch.zeros(max(n, 1), dtype=torch.int32, device=device)
-        if n == 0:
-            return status[:0]
-        d_offs = torch.as_tensor(np.asarray(offsets, dtype=np.int64)).to(device)
-        d_lens = torch.as_tensor(np.asarray(sealed_lengths, dtype=np.int64)).to(device)
-        d_oo = torch.as_tensor(np.asarray(out_offsets, dtype=np.int64)).to(device)
-        work = self._work(n, device)
         if stream is None:
             stream = torch.cuda.current_stream(device)
+        with torch.cuda.stream(stream):  # temporaries ordered on the kernels' stream (encrypt_chunks_device)
+            status = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+            if n == 0:
+                return status[:0]
+            d_offs = torch.as_tensor(np.asarray(offsets, dtype=np.int64)).to(device)
+            d_lens = torch.as_tensor(np.asarray(sealed_lengths, dtype=np.int64)).to(device)
+            d_oo = torch.as_tensor(np.asarray(out_offsets, dtype=np.int64)).to(device)
+            work = self._work(n, device)
         _lib.check(_lib.lib().kcdc_decrypt_chunks_device(
             self.name.encode(), self.secret, len(self.secret), C.c_void_p(sealed_ptr), d_offs.data_ptr(),
             d_lens.data_ptr(), n, C.c_void_p(d_ivs.data_ptr()), iv_len, iv_stride, d_out.data_ptr(), d_oo.data_ptr(),
             status.data_ptr(), work.data_ptr(), work.numel(), C.c_void_p(stream.cuda_stream)))
         status._kcdc_keep = (d_offs, d_lens, d_oo, work, d_ivs)
         return status[:n]
+
+
+def raise_on_status(status) -> None:
+    """Synchronise on a seal/open status tensor and raise KcdcError for the first chunk that
+    failed (KCDC_EBADMSG: authentication failed; its output slot must not be used)."""
+    st = status.cpu().numpy()
+    bad = np.nonzero(st)[0]
+    if len(bad):
+        i = int(bad[0])
+        raise _lib.KcdcError(int(st[i]), f"chunk {i} of {len(st)} failed ({len(bad)} failed in all)")

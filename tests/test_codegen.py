@@ -97,3 +97,82 @@ def test_hash_blocks_lean(dma_asm, kernel):
             vand = sum(1 for i in ins if i.startswith("v_and_b32"))
             assert nop <= nb // 16, f"{nop} s_nop for {nb} bytes in {label}"
             assert vand <= max(4, nb // 16), f"{vand} v_and_b32 for {nb} bytes in {label} (TOP test should be min-only)"
+
+
+# ---- Rabin-Karp batch and long-path kernels (two-byte hop, round 3)
+RK_KERNELS = ["_ZN4kcdc3dev21split_batch_rk_kernelENS0_9BatchArgsE",
+              "_ZN4kcdc3dev19cand_scan_rk_kernelENS0_9BatchArgsENS0_8LongArgsE"]
+
+
+@pytest.mark.parametrize("kernel", RK_KERNELS)
+def test_rk_no_vgpr_spills(dma_asm, kernel):
+    """The running candidate mins reassociated into trees (no asm barrier) and 64-bit per-lane
+    coordinates live across the walk each pushed the kernel past 256 VGPRs; the spill reloads
+    at every 64-byte check waited vmcnt and drained the line DMA."""
+    _, res = dma_asm
+    sect = res[res.index("Function Name: " + kernel):]
+    m = re.search(r"VGPRs Spill: (\d+)", sect)
+    assert m and int(m.group(1)) == 0, "VGPR spills in the Rabin-Karp kernel"
+
+
+@pytest.mark.parametrize("kernel", RK_KERNELS)
+def test_rk_hop_blocks_clean(dma_asm, kernel):
+    """No scratch and no vmcnt wait among a block's table reads (the hops of the walk)."""
+    asm, _ = dma_asm
+    hot = 0
+    for label, ins in _blocks(asm, kernel):
+        rd = [k for k, i in enumerate(ins) if i.startswith("ds_read_b64")]
+        if len(rd) < 16:
+            continue
+        hot += 1
+        assert not any(i.startswith("scratch_") for i in ins[rd[0]:rd[-1]]), f"scratch among the hops of {label}"
+        assert not any(i.startswith("s_waitcnt") and "vmcnt" in i for i in ins[rd[0]:rd[-1]]), \
+            f"vmcnt wait among the hops of {label} (drains the line DMA)"
+    assert hot >= 1, "expected the unrolled two-chain walk"
+
+
+# ---- content encryption / hash / compression kernels: LDS tables are read with ds_read only
+# A work-in-progress AES-GCM byte pass (round 2, before c909f3c) formed a T-table address as a
+# generic pointer and faulted the GPU (hipErrorIllegalAddress in test_rfc_shaped_single[AES]).
+# Every table read in these kernels must stay in the LDS address space, and none may spill.
+XSRC = {"crypt": "kcdc_crypt.hip", "hash": "kcdc_hash.hip", "compress": "kcdc_compress.hip"}
+
+
+@pytest.fixture(scope="module", params=sorted(XSRC))
+def xasm(request, tmp_path_factory):
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not available")
+    src = os.path.join(ROOT, "kopia_amd", "csrc", XSRC[request.param])
+    out = tmp_path_factory.mktemp("xasm") / "k.s"
+    subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S", src,
+                    "-o", str(out)], check=True, stderr=subprocess.DEVNULL)
+    return request.param, open(out).read()
+
+
+def _kernel_bodies(asm: str):
+    for m in re.finditer(r"^(_Z[^ :]*):", asm, re.M):
+        body = re.search(rf"^{re.escape(m.group(1))}:(.*?)^\.Lfunc_end", asm, re.S | re.M)
+        yield m.group(1), body.group(1)
+
+
+def test_no_flat_or_scratch_access(xasm):
+    what, asm = xasm
+    n = 0
+    for name, body in _kernel_bodies(asm):
+        n += 1
+        flat = re.findall(r"^\s*(flat_\w+)", body, re.M)
+        assert not flat, f"{name}: generic (flat) memory access {flat[:3]}"
+        assert not re.search(r"^\s*scratch_", body, re.M), f"{name}: scratch access (spill or stack array)"
+    assert n >= 1, f"no kernels found in {what}"
+
+
+def test_gcm_tables_read_from_lds(xasm):
+    what, asm = xasm
+    if what != "crypt":
+        pytest.skip("AES-GCM kernels live in kcdc_crypt.hip")
+    seen = 0
+    for name, body in _kernel_bodies(asm):
+        if "gcm_units_kernel" in name or "gcm_prep_kernel" in name:
+            seen += 1
+            assert len(re.findall(r"^\s*ds_read", body, re.M)) >= 256, f"{name}: table lookups not in LDS"
+    assert seen == 4

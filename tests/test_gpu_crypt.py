@@ -280,3 +280,37 @@ def test_too_long_chunk_and_empty_call(alg, gpu):
     assert out.cpu().numpy()[256:256 + 128].tobytes() == want
     st0 = enc.encrypt_chunks_device(d.data_ptr(), [], [], ids, 16, out, [], gpu)
     assert st0.numel() == 0
+
+
+def test_side_stream_status(alg, gpu):
+    """A caller's non-current stream (advisor, round 2): every temporary and the status words are
+    ordered on that stream, so a tampered chunk's KCDC_EBADMSG survives and a good one reads 0;
+    raise_on_status names the failed chunk."""
+    import torch
+    enc = ke.Encryptor(alg, MASTER)
+    host = coracle.gen_stream(SEED, 5, 1 << 16)
+    lens, offs = [1000, 5000, 77], [0, 2000, 9000]
+    ivs = [bytes([i]) * 16 for i in range(3)]
+    nonces = bytes(range(36))
+    side = torch.cuda.Stream(device=gpu)
+    d = torch.from_numpy(host).to(gpu)
+    d_ivs = torch.from_numpy(np.frombuffer(b"".join(ivs), np.uint8).copy()).to(gpu)
+    oo, total = ke.sealed_layout(lens)
+    sealed = torch.zeros(total, dtype=torch.uint8, device=gpu)
+    torch.cuda.synchronize()
+    st = enc.encrypt_chunks_device(d.data_ptr(), offs, lens, d_ivs, 16, sealed, oo, gpu, nonces=nonces, stream=side)
+    side.synchronize()
+    assert st.cpu().tolist() == [0, 0, 0]
+    with torch.cuda.stream(side):
+        sealed[int(oo[1]) + 20] ^= 1  # tamper chunk 1's ciphertext, on the side stream
+    slens = [L + ke.overhead(alg) for L in lens]
+    po, ptotal = ke.plain_layout(slens, alg)
+    out = torch.zeros(ptotal, dtype=torch.uint8, device=gpu)
+    st = enc.decrypt_chunks_device(sealed.data_ptr(), oo, slens, d_ivs, 16, out, po, gpu, stream=side)
+    side.synchronize()
+    assert st.cpu().tolist() == [0, _lib.KCDC_EBADMSG, 0]
+    with pytest.raises(_lib.KcdcError, match="chunk 1 of 3"):
+        ke.raise_on_status(st)
+    got = out.cpu().numpy()
+    assert got[po[0]:po[0] + lens[0]].tobytes() == host[0:1000].tobytes()
+    assert got[po[2]:po[2] + lens[2]].tobytes() == host[9000:9077].tobytes()
