@@ -5,7 +5,7 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function
 CSRC := kopia_amd/csrc
 OBJ := build/obj
-SRCS := $(CSRC)/kcdc_kernels.hip $(CSRC)/kcdc_hash.hip $(CSRC)/kcdc_crypt.hip $(CSRC)/kcdc_compress.hip $(CSRC)/kcdc_api.cpp $(CSRC)/kcdc_tables.cpp $(CSRC)/kcdc_registry.cpp
+SRCS := $(CSRC)/kcdc_kernels.hip $(CSRC)/kcdc_hash.hip $(CSRC)/kcdc_crypt.hip $(CSRC)/kcdc_compress.hip $(CSRC)/kcdc_api.cpp $(CSRC)/kcdc_writer.cpp $(CSRC)/kcdc_tables.cpp $(CSRC)/kcdc_registry.cpp
 OBJS := $(patsubst $(CSRC)/%,$(OBJ)/%.o,$(SRCS))
 LIB := kopia_amd/libkcdc.so
 

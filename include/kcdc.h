@@ -128,6 +128,32 @@ kcdc_group* kcdc_group_new(const char* name, int device, uint32_t max_batch, uin
 kcdc_splitter* kcdc_group_splitter(kcdc_group* g);
 void kcdc_group_free(kcdc_group* g);
 
+/* ------------------------------------------------ batching object writers
+ * The writer-level form of the streaming handle: objectWriter.Write
+ * (repo/object/object_writer.go:113-139) hands each 64 KiB slice (snapshot/upload/
+ * upload.go:394-407) to kcdc_bw_write, which only copies it into pinned staging.  A batcher
+ * thread ships every writer's staged bytes in one round (H2D, one batch-splitter launch over
+ * all writers, cut lists back) once `round_bytes` are staged (0: 256 MiB) or `max_wait_us`
+ * after the first staged byte (0: 2000).  Cut decisions therefore arrive later than the
+ * bytes: kcdc_bw_cuts returns the FINAL cut offsets found so far (absolute offsets in the
+ * object, strictly increasing, each a chunk end), and after kcdc_bw_finish (the object's
+ * Close/Result: blocks until every byte is split) the remaining ones including the trailing
+ * chunk's end.  The sequence is exactly the cuts of one NextSplitPoint pass over the whole
+ * object, however it was sliced.  The writer must keep the bytes of its unflushed chunks
+ * (objectWriter already buffers them in gather.WriteBuffer) and flush each chunk when its cut
+ * arrives.  Calls on one writer are serialised by the caller; writers are independent.
+ * kcdc_bw_write blocks while half a round of the writer's bytes is still unshipped. */
+typedef struct kcdc_bw_batcher kcdc_bw_batcher;
+typedef struct kcdc_bw kcdc_bw;
+kcdc_bw_batcher* kcdc_bw_batcher_new(const char* name, int device, uint64_t round_bytes, uint32_t max_wait_us);
+void kcdc_bw_batcher_free(kcdc_bw_batcher* b);  /* after every writer is freed */
+kcdc_bw* kcdc_bw_open(kcdc_bw_batcher* b);        /* Factory() for one object */
+int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len);
+int64_t kcdc_bw_cuts(kcdc_bw* w, uint64_t* out, uint64_t cap); /* final cuts taken (<= cap), or KCDC_E* */
+int kcdc_bw_finish(kcdc_bw* w);
+void kcdc_bw_free(kcdc_bw* w);
+int64_t kcdc_bw_rounds(const kcdc_bw_batcher* b); /* rounds shipped so far (test hook) */
+
 /* ------------------------------------------------------ batch (hot path)
  * Split `nstreams` independent streams in one launch; every stream starts from
  * a fresh splitter (the pool's Reset-on-Close, splitter_pool.go:18-22).

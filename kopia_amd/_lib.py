@@ -73,6 +73,14 @@ _SIGS = {
     "kcdc_group_new": (_P, [C.c_char_p, C.c_int, C.c_uint32, C.c_uint32]),
     "kcdc_group_splitter": (_P, [_P]),
     "kcdc_group_free": (None, [_P]),
+    "kcdc_bw_batcher_new": (_P, [C.c_char_p, C.c_int, C.c_uint64, C.c_uint32]),
+    "kcdc_bw_batcher_free": (None, [_P]),
+    "kcdc_bw_open": (_P, [_P]),
+    "kcdc_bw_write": (C.c_int, [_P, _P, C.c_size_t]),
+    "kcdc_bw_cuts": (C.c_int64, [_P, _P, C.c_uint64]),
+    "kcdc_bw_finish": (C.c_int, [_P]),
+    "kcdc_bw_free": (None, [_P]),
+    "kcdc_bw_rounds": (C.c_int64, [_P]),
     "kcdc_test_set": (C.c_int, [C.c_int32, C.c_int64]),
     "kcdc_test_occupy": (C.c_int, [C.c_uint32, C.c_uint32, _P]),
     "kcdc_test_queue_stat": (C.c_int64, [C.c_int32]),

@@ -62,6 +62,7 @@ struct SplitArgs {
     const uint64_t* cut_base;
     uint64_t* counts;
     const uint64_t* cut_end = nullptr;  // optional per-stream end of the cut range (device)
+    const uint64_t* starts = nullptr;   // optional per-stream first chunk start (device; bytes before = history)
 };
 // Launch the batch splitter for `algo` on `stream` (hipStream_t as void*).
 int launch_split_batch(const Algo& algo, const SplitArgs& a, int device, void* stream);

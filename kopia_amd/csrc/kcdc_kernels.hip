@@ -675,6 +675,8 @@ struct BatchArgs {
     uint64_t* trace;  // KCDC_TRACE builds: per stream {start, end, workgroup | wave << 16} (else null)
     uint64_t cuts_cap;
     const uint64_t* cut_end;  // optional: stream i's cut range ends at cut_end[i] (else cut_base[i+1] / cuts_cap)
+    const uint64_t* starts;   // optional: stream i's first chunk starts at starts[i] (else 0); the bytes before
+                              // it are the window history of a continued stream (kcdc_bw_*)
     uint64_t min_size, max_size;
     const uint32_t* buz;
     const uint64_t* rk_out;
@@ -1296,6 +1298,7 @@ __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
         const uint64_t cb = uni64(a.cut_base[sid]);
         pstream_fresh(st, sid, uni64(reinterpret_cast<uint64_t>(a.ptrs[sid])), uni64(a.lens[sid]), cb,
                       uni64(cut_end_of(a, sid)));
+        if (a.starts) st.s = static_cast<int64_t>(uni64(a.starts[sid]));
         uniformize(st);
         pwrite(a, lane, e0 + i, st, false);
     }
@@ -2726,7 +2729,7 @@ __global__ void init_ring_kernel(BatchArgs a, uint32_t nslots, uint32_t nwaves, 
         const uint64_t cb = a.cut_base[e];
         const uint64_t cend = cut_end_of(a, e);
         const uint64_t w = g == 0 ? 0ull                           // cnt
-                         : g == 1 ? 0ull                           // s
+                         : g == 1 ? (a.starts ? a.starts[e] : 0ull)  // s
                          : g == 2 ? ~0ull                          // ct = -1: region not set up
                          : g == 3 ? p
                          : g == 4 ? a.lens[e]
@@ -3715,7 +3718,7 @@ constexpr int kQueueSlots = 64;  // per-launch queue workspaces, chosen round-ro
 DeviceTables g_dev_tables[kMaxDevices];
 // Queue workspace of one launch slot: header (256 B: head, tail, done, error words 64 B
 // apart) | ring (P x 8 B, P = pow2 > nstreams + grid waves) | progress (nstreams x 24 B).
-// Grow-only; a replaced buffer is retired, not freed (an earlier launch may still use it).
+// Grow-only; a replaced buffer is freed once the slot's last launch (its `done` event) finished.
 struct QueueWs {
     char* base = nullptr;
     size_t bytes = 0;
@@ -3723,7 +3726,6 @@ struct QueueWs {
                                 // stream waits for it (more than kQueueSlots launches in flight)
 };
 QueueWs g_qws[kMaxDevices][kQueueSlots];
-std::vector<char*> g_retired;
 bool g_dev_ready[kMaxDevices];
 unsigned g_queue_next[kMaxDevices];
 std::mutex g_dev_mu;
@@ -3868,8 +3870,11 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
     a.cuts_cap = s.cuts_cap;
     a.cut_base = s.cut_base;
     a.cut_end = s.cut_end;
+    a.starts = s.starts;
     a.counts = s.counts;
     hipStream_t st = static_cast<hipStream_t>(stream);
+    if (s.starts && (algo.kind == kFixed || !KCDC_DMA || (algo.kind == kRabinKarp && !KCDC_RK_PIPE)))
+        return set_error(-22, "per-stream starts need the pipelined batch kernels");
     if (algo.kind == kFixed) {
         hipLaunchKernelGGL(dev::split_fixed_kernel, dim3(s.nstreams), dim3(256), 0, st, a);
     } else {
@@ -3905,7 +3910,10 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
                 hipError_t e = hipMalloc(&nb, nbytes);
                 (void)hipSetDevice(prev);
                 if (e != hipSuccess) return hip_fail(e, "queue workspace");
-                if (q.base) g_retired.push_back(q.base);
+                if (q.base) {  // the slot's previous launches are the only users of the old buffer
+                    if (q.done) (void)hipEventSynchronize(q.done);
+                    (void)hipFree(q.base);
+                }
                 q.base = nb;
                 q.bytes = nbytes;
             }

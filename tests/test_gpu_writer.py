@@ -1,0 +1,116 @@
+"""GPU: batching object writers (kcdc_bw_*) against the oracle.
+
+Concurrent writers feed their objects in 64 KiB slices (snapshot/upload/upload.go:394-407),
+random 1-1000 B slices, or whole; the final cuts they collect while writing plus the ones
+finish() returns must equal one sequential pass of the reference splitter over each object
+(oracle/cdc_oracle.c restates repo/splitter/splitter_buzhash32.go:26-67 and
+splitter_rabinkarp64.go:26-67, pinned by TestSplitterStability)."""
+import threading
+
+import numpy as np
+import pytest
+
+from kopia_amd import _lib
+from kopia_amd import splitter as ks
+from kopia_amd.writer import WriterBatcher
+from oracle import coracle
+
+pytestmark = pytest.mark.gpu
+SEED = 0x6B6F706961
+
+
+def _feed(w, data, mode, rng):
+    got = []
+    pos = 0
+    while pos < data.size:
+        if mode == "64k":
+            k = 64 << 10
+        elif mode == "rand":
+            k = int(rng.integers(1, 1001))
+        else:
+            k = data.size
+        w.write(data[pos:pos + k])
+        pos += k
+        if rng.random() < 0.05:
+            got.extend(w.cuts())
+    got.extend(w.finish())
+    return got
+
+
+def _run(name, sizes, modes, round_bytes=0, wait_us=0, sid0=0):
+    b = WriterBatcher(name, round_bytes=round_bytes, max_wait_us=wait_us)
+    datas = [coracle.gen_stream(SEED, sid0 + i, int(n)) for i, n in enumerate(sizes)]
+    got = [None] * len(sizes)
+    errs = []
+
+    def work(i):
+        try:
+            w = b.open()
+            got[i] = _feed(w, datas[i], modes[i % len(modes)], np.random.default_rng(i))
+            w.close()
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(sizes))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    rounds = b.rounds()
+    b.close()
+    assert not errs, errs
+    for i, d in enumerate(datas):
+        want = coracle.split_stream(name, d).tolist()
+        assert got[i] == want, f"writer {i} ({modes[i % len(modes)]}, {d.size} B): {len(got[i])} vs {len(want)} cuts"
+    return rounds
+
+
+@pytest.mark.parametrize("name", ["DYNAMIC-4M-BUZHASH", "DYNAMIC-128K-BUZHASH", "DYNAMIC-1M-RABINKARP",
+                                  "DYNAMIC-128K-RABINKARP"])
+def test_concurrent_writers_parity(gpu, name):
+    rng = np.random.default_rng(11)
+    avg = ks.GetFactory(name)().MaxSegmentSize() // 2
+    sizes = [int(rng.integers(0, 6 * avg)) for _ in range(12)] + [0, 1, 63, 64, avg // 2 - 1, avg // 2, 2 * avg]
+    _run(name, sizes, ["64k", "rand", "whole"])
+
+
+def test_sixty_four_writers_64k_slices(gpu):
+    """The uploader's shape: 64 concurrent writers, 64 KiB slices, several rounds."""
+    rounds = _run("DYNAMIC-4M-BUZHASH", [12 << 20] * 48 + [int(x) for x in range(1 << 20, 17 << 20, 1 << 20)],
+                  ["64k", "64k", "64k", "rand"], round_bytes=64 << 20)
+    assert rounds >= 4
+
+
+def test_tiny_rounds_carry_the_tail(gpu):
+    """1 MiB rounds force every chunk to span many rounds (device tail carried over)."""
+    rounds = _run("DYNAMIC-4M-BUZHASH", [20 << 20, 9 << 20, 3 << 20], ["64k", "rand"], round_bytes=1 << 20,
+                  wait_us=50)
+    assert rounds >= 20
+
+
+def test_kat_rows_through_writers(gpu):
+    """TestSplitterStability parameterisations (splitter_test.go:30-39) with random slicing."""
+    kat = coracle.gorand_read(5, 5_000_000)
+    for kind, avg, want in [(1, 32, (124235, 16, 64)), (1, 2048, (1924, 1024, 4096)), (2, 1024, (3771, 512, 2048))]:
+        name = _lib.lib().kcdc_custom_algorithm(kind, avg).decode()
+        b = WriterBatcher(name, round_bytes=1 << 20, max_wait_us=100)
+        w = b.open()
+        got = _feed(w, kat, "rand" if avg == 2048 else "64k", np.random.default_rng(avg))
+        w.close()
+        b.close()
+        assert got == coracle.split_stream(name, kat).tolist()
+        sizes = np.diff([0] + got)
+        assert (len(got), int(sizes[:-1].min()), int(sizes.max())) == want
+
+
+def test_errors(gpu):
+    b = WriterBatcher("DYNAMIC-4M-BUZHASH")
+    w = b.open()
+    w.write(bytes(1000))
+    assert w.finish() == [1000]
+    with pytest.raises(_lib.KcdcError):
+        w.write(b"x")
+    w.close()
+    b.close()
+    with pytest.raises(_lib.KcdcError):
+        WriterBatcher("NO-SUCH-SPLITTER")

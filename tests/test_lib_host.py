@@ -125,3 +125,23 @@ def test_group_needs_device_and_rolling_name():
     if L.kcdc_device_count() == 0:
         with pytest.raises(_lib.KcdcError):
             ks.SplitterGroup("DYNAMIC-4M-BUZHASH")
+
+
+def test_fixed_batched_writer_needs_no_device():
+    """kcdc_bw_* with a FIXED name: cuts every chunkLength (splitter_fixed.go:15-26), the trailing
+    chunk at finish, whatever the slicing; no device involved."""
+    from kopia_amd.writer import WriterBatcher
+    b = WriterBatcher("FIXED-128K")
+    w = b.open()
+    rng = np.random.default_rng(3)
+    n, got = 0, []
+    while n < 1_000_000:
+        k = int(rng.integers(1, 70000))
+        w.write(bytes(k))
+        n += k
+        got.extend(w.cuts())
+    got.extend(w.finish())
+    w.close()
+    b.close()
+    step = 128 << 10
+    assert got == list(range(step, n + 1, step)) + ([n] if n % step else [])
