@@ -9,7 +9,7 @@ SRCS := $(CSRC)/kcdc_kernels.hip $(CSRC)/kcdc_hash.hip $(CSRC)/kcdc_crypt.hip $(
 OBJS := $(patsubst $(CSRC)/%,$(OBJ)/%.o,$(SRCS))
 LIB := kopia_amd/libkcdc.so
 
-all: $(LIB) oracle
+all: $(LIB) oracle build/writer_bench
 
 $(OBJ)/%.hip.o: $(CSRC)/%.hip $(CSRC)/kcdc_internal.h include/kcdc.h
 	@mkdir -p $(OBJ)
@@ -59,3 +59,8 @@ variants:
 	  $(HIPCC) $(HIPFLAGS) $$f -shared -o build/variants/libkcdc_$$n.so $(CSRC)/kcdc_kernels.hip $(CSRC)/kcdc_hash.hip $(CSRC)/kcdc_crypt.hip $(CSRC)/kcdc_compress.hip -x hip $(CSRC)/kcdc_api.cpp $(CSRC)/kcdc_tables.cpp $(CSRC)/kcdc_registry.cpp || exit 1; \
 	done
 .PHONY: variants
+
+# C ABI driver: batching object writers (kcdc_bw_*), aggregate host-to-cuts rate
+build/writer_bench: tools/writer_bench.cpp include/kcdc.h $(LIB)
+	@mkdir -p build
+	g++ -O2 -std=c++17 -pthread -Iinclude $< -Lkopia_amd -lkcdc -Wl,-rpath,'$$ORIGIN/../kopia_amd' -o $@

@@ -61,7 +61,14 @@ int check_device(int dev) {
 
 // ======================================================= diagnostics / registry
 extern "C" const char* kcdc_last_error(void) { return kcdc::last_error_cstr(); }
-extern "C" const char* kcdc_version(void) { return "kcdc 0.1 (gfx950)"; }
+extern "C" const char* kcdc_version(void) {
+    static const std::string v = [] {
+        std::string a = std::string(ablations_kernels()) + ablations_crypt();
+        if (!a.empty()) a.pop_back();
+        return std::string("kcdc 0.3 (gfx950) ablations=") + (a.empty() ? "none" : a);
+    }();
+    return v.c_str();
+}
 
 extern "C" int kcdc_device_count(void) {
     int n = 0;

@@ -46,6 +46,11 @@ const Algo& algo_at(int i);  // sorted by name
 // Test knob: lanes per chunk of the content-hash kernels (0 auto, 1, 4).
 int& test_hash_lanes();
 
+// Wrong-output experiment switches compiled into this build (comma-terminated names; "" in
+// the product): kcdc_kernels.hip, kcdc_crypt.hip.
+const char* ablations_kernels();
+const char* ablations_crypt();
+
 // Thread-local error reporting.
 int set_error(int code, const std::string& msg);
 

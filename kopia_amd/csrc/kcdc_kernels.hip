@@ -3817,6 +3817,22 @@ extern "C" int kcdc_debug_trace_copy(uint64_t* host, uint64_t nstreams) {
 }
 #endif
 
+// Experiment switches that make the batch kernels cut WRONG (timing ablations only); the
+// product build has none of them (kcdc_version, tests/test_lib_host.py).
+const char* ablations_kernels() {
+    return ""
+#ifdef KCDC_EXP_COMPONLY
+           "KCDC_EXP_COMPONLY,"
+#endif
+#ifdef KCDC_EXP_MEMONLY
+           "KCDC_EXP_MEMONLY,"
+#endif
+#if defined(KCDC_RK_ABL) && KCDC_RK_ABL
+           "KCDC_RK_ABL,"
+#endif
+        ;
+}
+
 const DeviceTables* device_tables(int device, int* err) {
     *err = 0;
     if (device < 0 || device >= kMaxDevices) {

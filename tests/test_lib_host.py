@@ -145,3 +145,10 @@ def test_fixed_batched_writer_needs_no_device():
     b.close()
     step = 128 << 10
     assert got == list(range(step, n + 1, step)) + ([n] if n % step else [])
+
+
+def test_product_build_has_no_wrong_output_ablations():
+    """The timing ablations (KCDC_EXP_COMPONLY / _MEMONLY, KCDC_RK_ABL, KCDC_CRYPT_ABL) make the
+    kernels cut or encrypt wrongly; the shipped library must have none compiled in."""
+    v = _lib.lib().kcdc_version().decode()
+    assert v.endswith("ablations=none"), v

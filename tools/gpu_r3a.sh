@@ -12,3 +12,7 @@ timeout -k 10 300 python -u tools/kbench.py --name DYNAMIC-128K-RABINKARP --roun
 grep -A12 '^{' $OUT/kbench_rk128k.log | head -14
 timeout -k 10 400 python -u -m pytest tests/test_gpu_writer.py tests/test_gpu_crypt.py -x -v --timeout 200 --timeout-method thread > $OUT/writer_crypt.log 2>&1 || { tail -40 $OUT/writer_crypt.log; exit 1; }
 tail -2 $OUT/writer_crypt.log
+for w in 64 16 1; do
+  timeout -k 10 200 build/writer_bench $w $((4096 / w > 256 ? 256 : 4096 / w)) 64 DYNAMIC-4M-BUZHASH 256 3 >> $OUT/writer_bench.jsonl 2> $OUT/writer_bench.err || { cat $OUT/writer_bench.err; exit 1; }
+done
+cat $OUT/writer_bench.jsonl

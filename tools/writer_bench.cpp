@@ -1,0 +1,117 @@
+// Batching object writers through the C ABI (kcdc_bw_*): W writer threads
+// each feed their own object in S-byte slices, the way the uploader drives objectWriter.Write
+// (snapshot/upload/upload.go:394-407, repo/object/object_writer.go:113-139), poll the final
+// cuts as they arrive and finish.  The aggregate rate counts every byte from host memory to
+// final cut lists (PCIe included).  The cuts are checked against kcdc_split_batch_host on the
+// same objects (the whole-stream path, itself checked against the oracle by the GPU tests).
+// Prints one JSON line.
+//   build/writer_bench [writers=64] [MiB per writer=64] [slice KiB=64] [name] [round MiB=256] [reps=3]
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kcdc.h"
+
+int main(int argc, char** argv) {
+    const int W = argc > 1 ? std::atoi(argv[1]) : 64;
+    const size_t L = (argc > 2 ? std::strtoull(argv[2], nullptr, 10) : 64) << 20;
+    const size_t S = (argc > 3 ? std::strtoull(argv[3], nullptr, 10) : 64) << 10;
+    const std::string name = argc > 4 ? argv[4] : "DYNAMIC-4M-BUZHASH";
+    const uint64_t round = (argc > 5 ? std::strtoull(argv[5], nullptr, 10) : 256) << 20;
+    const int reps = argc > 6 ? std::atoi(argv[6]) : 3;
+    if (kcdc_device_count() < 1) {
+        std::fprintf(stderr, "no gfx950 device: %s\n", kcdc_last_error());
+        return 1;
+    }
+    std::vector<std::vector<uint8_t>> data(W, std::vector<uint8_t>(L));
+    {
+        std::vector<std::thread> th;
+        for (int i = 0; i < W; i++)
+            th.emplace_back([&, i] {
+                uint64_t x = 0x9E3779B97F4A7C15ull * (i + 1);
+                uint64_t* p = reinterpret_cast<uint64_t*>(data[i].data());
+                for (size_t k = 0; k < L / 8; k++) {
+                    x ^= x << 13;
+                    x ^= x >> 7;
+                    x ^= x << 17;
+                    p[k] = x;
+                }
+            });
+        for (auto& t : th) t.join();
+    }
+    // reference cuts: the whole-stream host path
+    std::vector<const uint8_t*> ptrs(W);
+    std::vector<uint64_t> lens(W, L), base(W), counts(W);
+    uint64_t cap = 0;
+    for (int i = 0; i < W; i++) {
+        ptrs[i] = data[i].data();
+        base[i] = cap;
+        cap += kcdc_cut_capacity(name.c_str(), L);
+    }
+    std::vector<uint64_t> ref(cap);
+    if (kcdc_split_batch_host(name.c_str(), ptrs.data(), lens.data(), W, ref.data(), cap, base.data(), counts.data(), 0)) {
+        std::fprintf(stderr, "kcdc_split_batch_host: %s\n", kcdc_last_error());
+        return 1;
+    }
+    kcdc_bw_batcher* b = kcdc_bw_batcher_new(name.c_str(), 0, round, 2000);
+    if (!b) {
+        std::fprintf(stderr, "kcdc_bw_batcher_new: %s\n", kcdc_last_error());
+        return 1;
+    }
+    std::vector<double> rates;
+    bool ok = true;
+    for (int r = 0; r < reps + 1; r++) {  // rep 0 warms the pinned pool and device buffers
+        std::vector<std::vector<uint64_t>> got(W);
+        std::atomic<int> ready{0};
+        std::atomic<bool> go{false};
+        std::vector<std::thread> th;
+        for (int i = 0; i < W; i++)
+            th.emplace_back([&, i] {
+                kcdc_bw* w = kcdc_bw_open(b);
+                uint64_t buf[256];
+                ready++;
+                while (!go.load()) std::this_thread::yield();
+                size_t pos = 0, calls = 0;
+                while (pos < L) {
+                    const size_t k = S < L - pos ? S : L - pos;
+                    if (kcdc_bw_write(w, data[i].data() + pos, k)) {
+                        std::fprintf(stderr, "kcdc_bw_write: %s\n", kcdc_last_error());
+                        std::exit(1);
+                    }
+                    pos += k;
+                    if (++calls % 16 == 0)
+                        for (int64_t n; (n = kcdc_bw_cuts(w, buf, 256)) > 0;) got[i].insert(got[i].end(), buf, buf + n);
+                }
+                if (kcdc_bw_finish(w)) {
+                    std::fprintf(stderr, "kcdc_bw_finish: %s\n", kcdc_last_error());
+                    std::exit(1);
+                }
+                for (int64_t n; (n = kcdc_bw_cuts(w, buf, 256)) > 0;) got[i].insert(got[i].end(), buf, buf + n);
+                kcdc_bw_free(w);
+            });
+        while (ready.load() < W) std::this_thread::yield();
+        const auto t0 = std::chrono::steady_clock::now();
+        go = true;
+        for (auto& t : th) t.join();
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (r > 0) rates.push_back(static_cast<double>(W) * L / s / (1ull << 30));
+        for (int i = 0; i < W; i++)
+            ok = ok && got[i] == std::vector<uint64_t>(ref.begin() + base[i], ref.begin() + base[i] + counts[i]);
+    }
+    const int64_t rounds = kcdc_bw_rounds(b);
+    kcdc_bw_batcher_free(b);
+    double best = 0, sum = 0;
+    for (double x : rates) {
+        best = x > best ? x : best;
+        sum += x;
+    }
+    std::printf("{\"writers\": %d, \"mib_per_writer\": %zu, \"slice_kib\": %zu, \"name\": \"%s\", \"round_mib\": %llu, "
+                "\"gib_s_mean\": %.2f, \"gib_s_best\": %.2f, \"rounds\": %lld, \"parity_ok\": %s}\n",
+                W, L >> 20, S >> 10, name.c_str(), static_cast<unsigned long long>(round >> 20),
+                rates.empty() ? 0.0 : sum / rates.size(), best, static_cast<long long>(rounds), ok ? "true" : "false");
+    return ok ? 0 : 2;
+}
