@@ -42,14 +42,10 @@ SEED = 0x6B6F706961
 BATCH_KERNEL = {0: "kcdc::dev::split_fixed_kernel", 1: "kcdc::dev::split_batch_pipe_kernel<true>",
                 2: "kcdc::dev::split_batch_rk_kernel"}  # rocprofv3 names
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
-# ChaCha20's VALU ceiling: 80 quarter-rounds x 12 ops + ~30 = ~990 VALU per 64-byte block per lane;
-# 256 CUs x 4 SIMDs x 16 lanes per cycle at the ~2.0 GHz the chip holds under load (DVFS,
-# MI355X_MICROARCH.md) -> 2.0e9 x 16,384 x 64 / 990 = 2.12 TB/s of plaintext.
-CHACHA_VALU_CEILING_GBS = 2118.0
-# AES256-GCM's byte pass (T-table AES-256 + 4-bit-table GHASH): 716 VALU per 16-byte block per lane,
-# measured (SQ_INSTS_VALU of gcm_units_kernel, profiles/r02/aes/pmc_sq.csv: 1.2e10 over 4 seals of
-# 268 M blocks) -> 2.0e9 x 16,384 x 16 / 716 = 732 GB/s of plaintext.
-AES_VALU_CEILING_GBS = 732.0
+# SIMD VALU-busy fraction of the byte-pass kernels, measured with rocprofv3 SQ counters
+# (profiles/r02/aes/pmc_sq.csv, profiles/r02/crypt/pmc_sq.csv): the reason the legs sit below HBM.
+AES_VALU_BUSY = 0.60
+CHACHA_VALU_BUSY = 0.83
 GiB = float(1 << 30)
 
 
@@ -438,7 +434,6 @@ def bench_encrypt(args, data, ns: int, L: int, cuts: list, dev, algo: str = "CHA
     from kopia_amd import hashing as kh
     from oracle import aead, aesgcm
     oracle = aesgcm if algo == ke.Aes256Gcm else aead
-    ceiling = AES_VALU_CEILING_GBS if algo == ke.Aes256Gcm else CHACHA_VALU_CEILING_GBS
     offs, lens = kh.chunk_table([i * L for i in range(ns)], cuts)
     n, total = len(offs), int(lens.sum())
     ids = kh.hash_chunks_device(kh.DefaultAlgorithm, data.data_ptr(), offs, lens, bytes(range(32)), dev).contiguous()
@@ -478,21 +473,46 @@ def bench_encrypt(args, data, ns: int, L: int, cuts: list, dev, algo: str = "CHA
         bad += plain[int(po[i]):int(po[i] + lens[i])].cpu().numpy().tobytes() != chunk
     oracle_s = time.perf_counter() - t0
     alg = 2 * total + 28 * n
+    valu_busy = AES_VALU_BUSY if algo == ke.Aes256Gcm else CHACHA_VALU_BUSY
     return {"algo": algo, "chunks": n, "plaintext_bytes": total,
             "seal_ms": round(seal_ms, 3), "seal_gib_s": round(total / GiB / (seal_ms * 1e-3), 1),
             "open_ms": round(open_ms, 3), "open_gib_s": round(total / GiB / (open_ms * 1e-3), 1),
-            # VALU-bound: ChaCha20 alone is ~990 VALU per 64-byte lane block; 1,024 SIMDs x
-            # 16 lanes x ~2.0 GHz under load -> ~2.1 TB/s of plaintext.  The HBM fraction stays beside it.
-            "roofline": {"bound": "valu", "achieved": round(total / (seal_ms * 1e-3) / 1e9, 1),
-                         "peak": ceiling, "unit": "GB/s of plaintext",
-                         "frac": round(total / (seal_ms * 1e-3) / 1e9 / ceiling, 3),
-                         "hbm_achieved": round(alg / (seal_ms * 1e-3) / 1e9, 1), "hbm_peak": HBM_PEAK_GBS,
-                         "hbm_frac": round(alg / (seal_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3),
-                         "algorithmic_bytes": alg, "timed": "all 4 seal launches (rocprof splits them)"},
+            # Against HBM: the algorithmic bytes are the plaintext read plus the sealed output
+            # written.  The bound that holds the kernel below it is vector ALU work (no AES or
+            # carry-less multiply instructions on gfx950; ChaCha20 is ~990 VALU per 64-byte lane
+            # block): the SIMDs' measured VALU-busy fraction is the explanation.
+            "roofline": {"bound": "hbm", "achieved": round(alg / (seal_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(alg / (seal_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3),
+                         "traffic": None, "algorithmic_bytes": alg,
+                         "limited_by": "VALU", "valu_busy_measured": valu_busy,
+                         "timed": "all 4 seal launches (rocprof splits them)"},
             "sample_parity_mismatches": int(bad), "sample_chunks": len(pick),
-            "cpu_oracle_gib_s": round(sum(int(lens[i]) for i in pick) * 2 / GiB / oracle_s, 4),
-            "cpu_oracle_note": "numpy/pure-Python restatement (oracle/aead.py or oracle/aesgcm.py; seal + "
-                               "compare), not an optimized CPU implementation: no crypto library in this image"}
+            "cpu_baseline": cpu_aead_baseline(algo, secret, data, offs, lens, idh, nonces)}
+
+
+def cpu_aead_baseline(algo, secret, data, offs, lens, idh, nonces) -> dict:
+    """The same seal (HMAC-SHA256 key per content + AEAD) by OpenSSL's EVP through ctypes, the
+    C-speed stand-in for the reference's Go crypto (oracle/openssl_aead.py; it re-seals the
+    reference's ciphertext samples byte for byte, tests/test_aead_oracle.py), on the chunks of
+    the batch's first 2 GiB, 1 thread and every usable thread."""
+    from oracle import openssl_aead as osl  # oracle import confined to this leg
+    if not osl.available():
+        return {"value": None, "note": "libcrypto.so.3 not loadable on this host"}
+    info = host_cpu_info()
+    lim = 2 << 30
+    sel = [i for i in range(len(offs)) if int(offs[i] + lens[i]) <= lim]
+    host = data[:lim].cpu().numpy()
+    so, sl = offs[sel], lens[sel]
+    sid = [idh[i].tobytes() for i in sel]
+    sn = b"".join(nonces[12 * i:12 * i + 12] for i in sel)
+    r1 = osl.seal_rate(algo, secret, host, so[: max(1, len(sel) // 4)], sl[: max(1, len(sel) // 4)], sid, sn, 1)
+    ra = osl.seal_rate(algo, secret, host, so, sl, sid, sn, info["threads_all"])
+    g1, ga = r1["bytes"] / GiB / r1["seconds"], ra["bytes"] / GiB / ra["seconds"]
+    return {"value": round(ga, 2), "unit": "GiB/s", "cores": info["threads_all"], "kind": "library",
+            "threads_1": round(g1, 2), "threads_all": round(ga, 2), "threads_all_n": info["threads_all"],
+            "cpu_model": info["cpu_model"],
+            "sample": f"{len(sel)} chunks ({ra['bytes'] / GiB:.2f} GiB) of this batch sealed by OpenSSL {algo} "
+                      f"(EVP + HMAC-SHA256 key per content); 1 thread on a quarter of them"}
 
 
 def bench_long(args, comm: Comm):
@@ -635,6 +655,44 @@ def bench_files(args, comm: Comm):
             el, _own, _ = run(nm, 2, 1)
             out["per_name_gib_s"][nm] = round(total * world * 2 / GiB / el, 2)
     return out
+
+
+def multirank_check(argv):
+    """tests/test_gpu_multirank.py: the N>1 path on the device.  Every rank (its GPU: LOCAL_RANK
+    modulo the visible devices, so two ranks may share the one GPU of a test box) splits its
+    disjoint static shard of config-2-shaped streams through libkcdc and computes the config-5
+    LPT plan on its own; rank 0 writes what the ranks gathered over gloo to argv[0].
+    argv: out_path, streams per rank, MiB per stream, splitter name."""
+    import hashlib
+
+    import torch
+
+    from kopia_amd import batch
+    from kopia_amd import dist as kd
+    out_path, per, mib, name = argv[0], int(argv[1]), int(argv[2]), argv[3]
+    rank, world, local = env_rank_world()
+    dev = torch.device("cuda", local % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    comm = Comm(rank, world)
+    try:
+        L = mib << 20
+        ids = kd.static_shard(rank, world, per)
+        data = torch.empty(per * L, dtype=torch.uint8, device=dev)
+        batch.fill_prng(data, L, per, L, SEED, int(ids[0]))
+        b = batch.make_device_batch(name, [data.data_ptr() + i * L for i in range(per)], [L] * per, dev)
+        batch.split_batch_device(name, b)
+        torch.cuda.synchronize(dev)
+        cuts = batch.read_cuts(b)
+        plan = kd.lpt_plan(kd.zipf_sizes(1 << 36), world)
+        digest = hashlib.sha256(json.dumps(plan).encode()).hexdigest()
+        comm.barrier()
+        got = comm.gather({"rank": rank, "device": str(dev), "ids": [int(i) for i in ids],
+                           "cuts": [c.tolist() for c in cuts], "plan": digest, "mine": len(plan[rank])})
+        if rank == 0:
+            with open(out_path, "w") as f:
+                json.dump(got, f)
+    finally:
+        comm.close()
 
 
 def launcher_selftest(argv):

@@ -1,5 +1,6 @@
 """The encryption oracle (oracle/aead.py) pinned by the published RFC 8439 and RFC 5869
 example vectors (tests/golden/aead_kat.json).  CPU only."""
+import numpy as np
 import pytest
 
 from conftest import golden
@@ -71,3 +72,25 @@ def test_reference_ciphertext_samples():
         bad = bytearray(sample)
         bad[15] ^= 1
         assert aead.kopia_decrypt(secret, cid, bytes(bad)) is None
+
+
+def test_openssl_cpu_baseline_reproduces_reference_samples():
+    """bench.py's CPU baseline for the encryption legs (OpenSSL EVP through ctypes, the C-speed
+    stand-in for Go's crypto) seals the reference's TestCiphertextSamples payloads
+    (encryption_test.go:97-127) to exactly the samples' bytes, for both encryptors, and agrees with
+    the oracles on a 1 MiB chunk."""
+    from oracle import aesgcm, openssl_aead as osl
+    if not osl.available():
+        pytest.skip("libcrypto.so.3 not loadable")
+    for c in golden("kopia_encryption_samples.json")["cases"]:
+        secret = aead.derive_key(c["master_key"].encode())
+        cid, payload = c["content_id"].encode(), c["payload"].encode()
+        for algo in (osl.AES, osl.CHACHA):
+            sample = bytes.fromhex(c["samples"][algo])
+            assert osl.Sealer(algo).kopia_encrypt(secret, cid, sample[:12], payload) == sample
+    rng = np.random.default_rng(9)
+    pt = rng.integers(0, 256, 1 << 20, dtype=np.uint8).tobytes()
+    secret, cid, nonce = bytes(range(32)), bytes(range(16)), bytes(range(12))
+    assert osl.Sealer(osl.CHACHA).kopia_encrypt(secret, cid, nonce, pt) == aead.kopia_encrypt(secret, cid, nonce, pt)
+    assert osl.Sealer(osl.AES).kopia_encrypt(secret, cid, nonce, pt[:4096]) == \
+        aesgcm.kopia_encrypt(secret, cid, nonce, pt[:4096])
