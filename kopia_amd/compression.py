@@ -1,7 +1,7 @@
 """Content compression of chunks on the GPU (C ABI: include/kcdc.h, kcdc_compress_*),
-mirroring Kopia's compression package for the deflate compressors
-(repo/compression/compressor.go: Compressor, HeaderID, ByName; compressor_deflate.go;
-compression_ids.go) and the content manager's keep-or-drop rule
+mirroring Kopia's compression package for the deflate, gzip, pgzip and s2 compressors
+(repo/compression/compressor.go: Compressor, HeaderID, ByName; compressor_deflate.go,
+compressor_gzip.go, compressor_pgzip.go, compressor_s2.go; compression_ids.go) and the content manager's keep-or-drop rule
 (repo/content/content_manager_lock_free.go:42-73: the compressed form is kept only when it is
 shorter than the content, else the header ID is NoCompression = 0).
 No CPU fallback for the byte path: the library must be loaded."""
@@ -18,8 +18,8 @@ compressionHeaderSize = 4  # compressor.go:15
 
 
 def SupportedAlgorithms() -> list[str]:
-    arr = (C.c_char_p * 16)()
-    n = _lib.lib().kcdc_compression_algorithms(arr, 16)
+    arr = (C.c_char_p * 64)()
+    n = _lib.lib().kcdc_compression_algorithms(arr, 64)
     return [arr[i].decode() for i in range(n)]
 
 

@@ -37,10 +37,21 @@ constexpr uint32_t kSeg = 512;                  // bytes per lane segment
 constexpr uint32_t kSpan = 64 * kSeg;           // bytes per wave span (<= the 32 KiB window)
 constexpr uint32_t kSlot = kSeg + 64;           // scratch bytes per segment (the encoder stops at kSeg + 8)
 constexpr uint32_t kStored = 0x80000000u;       // segment length flag: emit a stored block
+constexpr int kFmtDeflate = 0;                  // RFC 1951 (deflate, gzip, pgzip)
+constexpr int kFmtS2 = 1;                       // S2 / Snappy block elements in the S2 framing format
+constexpr uint32_t kS2StoredHdr = 3;            // a stored S2 segment: one literal, tag 61 + 2-byte length
+constexpr uint32_t kS2ChunkHdr = 8;             // framing chunk: type 0x00, 3-byte length, masked CRC-32C
+constexpr uint32_t kS2StreamId = 10;            // ff 06 00 00 "S2sTwO" (s2.NewWriter's stream identifier)
 #ifndef KCDC_DEFLATE_HASH_BITS
-#define KCDC_DEFLATE_HASH_BITS 7  // per-lane match table entries (log2); LDS = 33 KiB span + 128 B << bits
+#define KCDC_DEFLATE_HASH_BITS 6  // per-lane match table entries (log2); LDS = 33 KiB span + 128 B << bits
 #endif
 constexpr uint32_t kHashBits = KCDC_DEFLATE_HASH_BITS;
+// Span-wide table: for every 11-bit hash, the FIRST position of the span with that hash (an LDS
+// atomic min over all lanes before the parse).  A lane's own table only sees its 512-byte segment;
+// this one offers a match anywhere earlier in the span (<= 32 KiB back, inside the window).
+// Simulated on the mixed data (tools/compress_bench.py): ratio 0.362 -> 0.339 against zlib-6 0.270.
+// LDS: 33 KiB span + 8 KiB lane tables + 8 KiB span table = 49.7 KiB: three waves per CU, as before.
+constexpr uint32_t kFirstBits = 11;
 constexpr uint32_t kLdsWords = 8320;            // >= (4 * 2049 + 1) + 65: the staged span + 1 word of read-ahead
 
 struct CompArgs {
@@ -60,9 +71,14 @@ struct CompArgs {
     uint32_t max_spans;
     uint32_t header_id;
     uint32_t skip;      // literal-run skip shift of the match search (level)
+    uint32_t effort;    // 0: the lane's own table only; 1: + the span-wide first-occurrence table;
+                        // 2: + one-step lazy matching (compression levels)
     uint32_t gzip;      // 1: the stream sits in a gzip member (RFC 1952): gzip, pgzip
+    uint32_t fmt;       // kFmtDeflate or kFmtS2
     uint32_t* crc;      // [n]: per chunk, XOR of its spans' shifted raw CRC-32s (atomic)
+    uint32_t* span_crc; // [max_spans]: S2, each span's raw CRC-32C
     uint32_t x2n[32];   // x^(2^k) mod P, CRC-32's reflected polynomial (zlib x2n_table)
+    uint32_t x2nc[32];  // the same for CRC-32C (Castagnoli, S2 framing)
 };
 
 __global__ __launch_bounds__(256) void span_count_kernel(CompArgs a) {
@@ -154,10 +170,17 @@ __device__ __forceinline__ void put_match(Bits& w, uint32_t len, uint32_t dist) 
     if (deb) w.put(dev, deb);
 }
 
-// One wave per span: blockIdx.x = global span index.
-__global__ __launch_bounds__(64) void deflate_spans_kernel(CompArgs a) {
+// S2 framing header of span b: 0x00, 3-byte LE length of (CRC + block), then the masked CRC
+// (written by the copy kernel) and the block's uvarint uncompressed length.
+__device__ __forceinline__ uint32_t uvarint_len(uint32_t v) { return v < 128u ? 1u : v < 16384u ? 2u : 3u; }
+
+// One wave per span: blockIdx.x = global span index.  FMT: kFmtDeflate or kFmtS2 (the parse is
+// shared; the emitters differ: fixed-Huffman bits closed by a sync flush, or Snappy tags).
+template <int FMT>
+__global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
     __shared__ uint32_t L[kLdsWords];
     __shared__ uint16_t tab[(1u << kHashBits) * 64u];
+    __shared__ uint32_t ftab[1u << kFirstBits];
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
     const uint32_t total = a.spans[a.n];
     if (total > a.max_spans || b >= total) return;
@@ -188,6 +211,7 @@ __global__ __launch_bounds__(64) void deflate_spans_kernel(CompArgs a) {
     {
         uint64_t* t64 = reinterpret_cast<uint64_t*>(tab);
         for (uint32_t i = lane; i < (1u << kHashBits) * 16u; i += 64u) t64[i] = ~0ull;
+        for (uint32_t i = lane; i < (1u << kFirstBits); i += 64u) ftab[i] = ~0u;
     }
     __syncthreads();
     const uint8_t* Lb = reinterpret_cast<const uint8_t*>(L);
@@ -202,48 +226,118 @@ __global__ __launch_bounds__(64) void deflate_spans_kernel(CompArgs a) {
 
     const uint32_t slot = b * 64u + lane;
     const uint32_t x0 = kSeg * lane;
+    constexpr uint32_t kMul = 0x1E35A7BDu;
+    if (a.effort >= 1u) {  // every position's 4-byte hash: the span's first occurrence (LDS atomic min)
+        const uint32_t e = span_len >= 3u ? span_len - 3u : 0u;
+        for (uint32_t x = x0; x < x0 + kSeg && x < e; x++)
+            atomicMin(&ftab[(ld32(x) * kMul) >> (32u - kFirstBits)], x);
+        __syncthreads();
+    }
     uint32_t word = 0;  // the segment's length word (0: past the span's end)
     if (x0 < span_len) word = [&]() -> uint32_t {
     const uint32_t xe = span_len - x0 < kSeg ? span_len : x0 + kSeg;
     const uint32_t seg_len = xe - x0;
     uint32_t* base = reinterpret_cast<uint32_t*>(a.slots + static_cast<uint64_t>(slot) * kSlot);
-    const uint32_t limit = seg_len + 8u;  // bytes flushed before giving up on the fixed block
+    const uint32_t limit = seg_len + 8u;  // bytes flushed before giving up on the segment
     Bits w{0ull, 0u, base};
     bool over = false;
-    w.put(2u, 3);  // BFINAL 0, BTYPE 01
+    if constexpr (FMT == kFmtDeflate) w.put(2u, 3);  // BFINAL 0, BTYPE 01
     uint32_t x = x0, lit = x0;
     auto literals = [&](uint32_t e) {
+        if constexpr (FMT == kFmtS2) {  // one literal element: tag (n-1) << 2 | 0, 60: +1 byte, 61: +2
+            if (e == lit) return;
+            const uint32_t m = e - lit - 1u;
+            if (m < 60u) {
+                w.put(m << 2, 8);
+            } else if (m < 256u) {
+                w.put(60u << 2, 8);
+                w.put(m, 8);
+            } else {
+                w.put(61u << 2, 8);
+                w.put(m, 16);
+            }
+        }
         for (uint32_t q = lit; q < e; q++) {
-            put_lit(w, byte(q));
+            if constexpr (FMT == kFmtS2)
+                w.put(byte(q), 8);
+            else
+                put_lit(w, byte(q));
             if (4u * static_cast<uint32_t>(w.op - base) > limit) {
                 over = true;
                 break;
             }
         }
     };
-    while (!over && x + 4u <= xe) {
-        const uint32_t v = ld32(x);
-        const uint32_t h = (v * 0x1E35A7BDu) >> (32u - kHashBits);
-        const uint32_t cand = tab[h * 64u + lane];
-        tab[h * 64u + lane] = static_cast<uint16_t>(x);
-        if (cand >= x0 && cand < x && ld32(cand) == v) {
-            const uint32_t maxlen = xe - x < 258u ? xe - x : 258u;
-            uint32_t n = 4;
-            bool done = false;
-            while (n + 4u <= maxlen) {
-                const uint32_t diff = ld32(x + n) ^ ld32(cand + n);
-                if (diff) {
-                    n += static_cast<uint32_t>(__builtin_ctz(diff)) >> 3;
-                    done = true;
-                    break;
-                }
-                n += 4u;
+    // S2 copies (Snappy tags, no S2 repeat codes): copy1 for lengths 4..11 at offsets < 2048,
+    // else copy2 (lengths 1..64, 16-bit offsets: a span is 32 KiB); longer matches are split.
+    auto s2_copy = [&](uint32_t n, uint32_t off) {
+        while (n > 0u) {
+            const uint32_t k = n > 64u ? (n - 64u < 4u ? 60u : 64u) : n;  // keep the rest >= 4
+            if (k >= 4u && k <= 11u && off < 2048u) {
+                w.put(1u | ((k - 4u) << 2) | ((off >> 8) << 5), 8);
+                w.put(off & 255u, 8);
+            } else {
+                w.put(2u | ((k - 1u) << 2), 8);
+                w.put(off, 16);
             }
-            if (!done)
-                while (n < maxlen && byte(x + n) == byte(cand + n)) n++;
+            n -= k;
+        }
+    };
+    // Length of the match of x against an earlier q (>= 4 when the first 4 bytes agree), <= maxlen.
+    auto match_len = [&](uint32_t q, uint32_t xx, uint32_t v) -> uint32_t {
+        if (q >= xx || ld32(q) != v) return 0u;
+        const uint32_t cap = FMT == kFmtDeflate ? 258u : kSeg;  // S2 copies have no length limit
+        const uint32_t maxlen = xe - xx < cap ? xe - xx : cap;
+        uint32_t n = 4;
+        while (n + 4u <= maxlen) {
+            const uint32_t diff = ld32(xx + n) ^ ld32(q + n);
+            if (diff) return n + (static_cast<uint32_t>(__builtin_ctz(diff)) >> 3);
+            n += 4u;
+        }
+        while (n < maxlen && byte(xx + n) == byte(q + n)) n++;
+        return n;
+    };
+    // Best match at xx: the lane table's latest candidate (inside the segment) and, with effort
+    // >= 1, the span's first occurrence (anywhere earlier in the span).  Updates the lane table.
+    auto best_at = [&](uint32_t xx, uint32_t& q) -> uint32_t {
+        const uint32_t v = ld32(xx);
+        const uint32_t hv = v * kMul;
+        const uint32_t h = hv >> (32u - kHashBits);
+        const uint32_t c1 = tab[h * 64u + lane];
+        tab[h * 64u + lane] = static_cast<uint16_t>(xx);
+        uint32_t n = c1 >= x0 ? match_len(c1, xx, v) : 0u;
+        q = c1;
+        if (a.effort >= 1u) {
+            const uint32_t c2 = ftab[hv >> (32u - kFirstBits)];
+            if (c2 != c1) {
+                const uint32_t n2 = match_len(c2, xx, v);
+                if (n2 > n) {
+                    n = n2;
+                    q = c2;
+                }
+            }
+        }
+        return n;
+    };
+    while (!over && x + 4u <= xe) {
+        uint32_t cand;
+        uint32_t n = best_at(x, cand);
+        if (n && a.effort >= 2u && n < 32u && x + 5u <= xe) {  // lazy: a longer match one byte later wins
+            uint32_t c2;
+            const uint32_t n2 = best_at(x + 1u, c2);
+            if (n2 > n + 1u) {
+                x += 1u;
+                n = n2;
+                cand = c2;
+            }
+        }
+        if (n) {
             literals(x);
             if (over) break;
-            put_match(w, n, x - cand);
+            if constexpr (FMT == kFmtS2)
+                s2_copy(n, x - cand);
+            else
+                put_match(w, n, x - cand);
             if (4u * static_cast<uint32_t>(w.op - base) > limit) {
                 over = true;
                 break;
@@ -253,6 +347,22 @@ __global__ __launch_bounds__(64) void deflate_spans_kernel(CompArgs a) {
         } else {
             x += 1u + ((x - lit) >> a.skip);
         }
+    }
+    if constexpr (FMT == kFmtS2) {
+        if (!over) {  // exact size with the pending literal: worse than one stored literal -> stored
+            const uint32_t m = xe - lit;
+            const uint32_t bytes = 4u * static_cast<uint32_t>(w.op - base) + (w.nb >> 3) + m +
+                                   (m == 0u ? 0u : m <= 60u ? 1u : m <= 256u ? 2u : 3u);
+            if (bytes >= seg_len + kS2StoredHdr) over = true;
+        }
+        if (!over) literals(xe);
+        uint32_t bytes = 0;
+        if (!over) {
+            bytes = 4u * static_cast<uint32_t>(w.op - base) + (w.nb >> 3);
+            if (w.nb) *w.op = static_cast<uint32_t>(w.bb);
+            if (bytes >= seg_len + kS2StoredHdr) over = true;
+        }
+        return over ? (kStored | seg_len) : bytes;
     }
     if (!over) {
         // The block's exact size with the pending literals, counted 4 bytes at a time (a fixed
@@ -283,9 +393,11 @@ __global__ __launch_bounds__(64) void deflate_spans_kernel(CompArgs a) {
     return over ? (kStored | seg_len) : bytes;
     }();
     a.seglen[slot] = word;
-    // The span's output bytes (stored segments: 5 + n).
-    uint32_t eff = (word & kStored) ? 5u + (word & ~kStored) : word;
+    // The span's output bytes (stored segments: 5 + n, S2: 3 + n; S2 adds the framing header).
+    const uint32_t shdr = FMT == kFmtS2 ? kS2StoredHdr : 5u;
+    uint32_t eff = (word & kStored) ? shdr + (word & ~kStored) : word;
     for (uint32_t o = 32; o > 0; o >>= 1) eff += __shfl_xor(eff, o, 64);
+    if (FMT == kFmtS2) eff += kS2ChunkHdr + uvarint_len(span_len);
     if (lane == 0) a.span_bytes[b] = eff;
 }
 
@@ -321,22 +433,28 @@ __global__ __launch_bounds__(1024) void span_pos_kernel(CompArgs a) {
 // 512 bytes per lane; lanes combine in a 6-level tree with the constants x^(2^(12+j)), the span
 // is scaled by x^(8 * 32768 * spans after it), and the chunk's word takes the XOR (atomic, order
 // free).  The frame kernel adds crc32 of len zero bytes (the init / final-XOR terms).
-constexpr uint32_t kCrcPoly = 0xEDB88320u;
-__host__ __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {  // a * b mod P (reflected)
-    uint32_t p = 0;
+constexpr uint32_t kCrcPoly = 0xEDB88320u;   // CRC-32 (gzip), reflected
+constexpr uint32_t kCrc32cPoly = 0x82F63B78u; // CRC-32C (Castagnoli: the S2 / Snappy framing), reflected
+__host__ __device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b, uint32_t poly = kCrcPoly) {
+    uint32_t p = 0;  // a * b mod P (reflected)
     for (int i = 31; i >= 0; i--) {
         p ^= ((a >> i) & 1u) ? b : 0u;
-        b = (b >> 1) ^ (kCrcPoly & (0u - (b & 1u)));
+        b = (b >> 1) ^ (poly & (0u - (b & 1u)));
     }
     return p;
 }
 
+// S2 = false: gzip's CRC-32 of each chunk, its 32 KiB spans counted back from the chunk's end.
+// S2 = true: the CRC-32C of each S2 span on its own (a framing chunk's checksum), lanes counted
+// back from the span's end; raw register value to span_crc[b].
 constexpr uint32_t kCrcWaves = 4;
+template <bool S2>
 __global__ __launch_bounds__(64 * kCrcWaves) void crc_spans_kernel(CompArgs a) {
+    constexpr uint32_t poly = S2 ? kCrc32cPoly : kCrcPoly;
     __shared__ uint32_t tab[256 * 32];  // 32 copies: lane l reads copy l & 31 (conflict free)
     for (uint32_t x = threadIdx.x; x < 256u; x += 64u * kCrcWaves) {
         uint32_t r = x;
-        for (int k = 0; k < 8; k++) r = (r >> 1) ^ (kCrcPoly & (0u - (r & 1u)));
+        for (int k = 0; k < 8; k++) r = (r >> 1) ^ (poly & (0u - (r & 1u)));
         for (uint32_t c = 0; c < 32u; c++) tab[32u * x + ((c + x) & 31u)] = r;
     }
     __syncthreads();
@@ -351,9 +469,15 @@ __global__ __launch_bounds__(64 * kCrcWaves) void crc_spans_kernel(CompArgs a) {
     }
     const uint32_t c = lo;
     const uint32_t s = b - a.spans[c], ns = a.spans[c + 1] - a.spans[c];
-    const int64_t len = static_cast<int64_t>(a.in_lens[c]);
-    const int64_t p0 = len - static_cast<int64_t>(kSpan) * (ns - s) + static_cast<int64_t>(kSeg) * lane;
+    int64_t len = static_cast<int64_t>(a.in_lens[c]);
+    int64_t p0 = len - static_cast<int64_t>(kSpan) * (ns - s) + static_cast<int64_t>(kSeg) * lane;
     const uint8_t* in = a.in + a.in_offs[c];
+    if (S2) {  // the span alone: [s kSpan, s kSpan + span_len) as a message of its own
+        const int64_t sb = static_cast<int64_t>(s) * kSpan;
+        len = len - sb < static_cast<int64_t>(kSpan) ? len - sb : static_cast<int64_t>(kSpan);
+        in += sb;
+        p0 = len - static_cast<int64_t>(kSpan) + static_cast<int64_t>(kSeg) * lane;
+    }
     // 16-byte granules from the aligned address below the segment; m16 is wave-uniform (lanes
     // are 512 bytes apart).  A granule is read only when it holds a byte of the chunk.
     const uint32_t m16 = static_cast<uint32_t>((reinterpret_cast<uintptr_t>(in) + static_cast<uint64_t>(p0 & 15)) & 15u);
@@ -399,7 +523,11 @@ __global__ __launch_bounds__(64 * kCrcWaves) void crc_spans_kernel(CompArgs a) {
 #pragma unroll
     for (int j = 0; j < 6; j++) {
         const uint32_t right = __shfl_down(r, 1u << j, 64);
-        if (((lane >> j) & 1u) == 0u) r = multmodp(r, a.x2n[12 + j]) ^ right;
+        if (((lane >> j) & 1u) == 0u) r = multmodp(r, S2 ? a.x2nc[12 + j] : a.x2n[12 + j], poly) ^ right;
+    }
+    if (S2) {
+        if (lane == 0) a.span_crc[b] = r;
+        return;
     }
     if (lane == 0) {
         uint32_t after = ns - 1u - s;  // whole spans after this one: x^(8 * 32768 * after)
@@ -441,10 +569,33 @@ __global__ __launch_bounds__(64) void deflate_copy_kernel(CompArgs a) {
     }
     const uint32_t c = lo;
     const uint32_t u = b - a.spans[c];
-    uint8_t* dst = a.out + a.out_offs[c] + 4u + (a.gzip ? 10u : 0u) + (a.span_pos[b] - a.span_pos[a.spans[c]]);
+    uint8_t* dst = a.out + a.out_offs[c] + 4u + (a.gzip ? 10u : 0u) + (a.fmt == kFmtS2 ? kS2StreamId : 0u) +
+                   (a.span_pos[b] - a.span_pos[a.spans[c]]);
     const uint8_t* in = a.in + a.in_offs[c] + static_cast<uint64_t>(u) * kSpan;
     const uint32_t word = a.seglen[b * 64u + lane];
-    const uint32_t eff = (word & kStored) ? 5u + (word & ~kStored) : word;
+    const bool s2 = a.fmt == kFmtS2;
+    const uint32_t eff = (word & kStored) ? (s2 ? kS2StoredHdr : 5u) + (word & ~kStored) : word;
+    if (s2) {  // framing chunk header: 0x00, length, masked CRC-32C of the span, uvarint(span length)
+        const uint64_t len = a.in_lens[c], sb = static_cast<uint64_t>(u) * kSpan;
+        const uint32_t span_len = static_cast<uint32_t>(len - sb < kSpan ? len - sb : kSpan);
+        const uint32_t vl = uvarint_len(span_len);
+        if (lane == 0) {
+            const uint32_t clen = a.span_bytes[b] - 4u;  // CRC + block
+            uint32_t z = 0x80000000u;  // standard CRC-32C = raw ^ (~0 x^(8 n) mod P) ^ ~0
+            for (uint32_t n = span_len, bit = 0; n; bit++, n >>= 1)
+                if (n & 1u) z = multmodp(z, a.x2nc[(3 + bit) & 31], kCrc32cPoly);
+            const uint32_t crc = a.span_crc[b] ^ multmodp(z, 0xFFFFFFFFu, kCrc32cPoly) ^ 0xFFFFFFFFu;
+            const uint32_t masked = ((crc >> 15) | (crc << 17)) + 0xa282ead8u;
+            uint8_t h[11] = {0x00u, static_cast<uint8_t>(clen), static_cast<uint8_t>(clen >> 8),
+                             static_cast<uint8_t>(clen >> 16), static_cast<uint8_t>(masked),
+                             static_cast<uint8_t>(masked >> 8), static_cast<uint8_t>(masked >> 16),
+                             static_cast<uint8_t>(masked >> 24), 0u, 0u, 0u};
+            uint32_t v = span_len;
+            for (uint32_t i = 0; i < vl; i++, v >>= 7) h[8 + i] = static_cast<uint8_t>((v & 127u) | (i + 1 < vl ? 128u : 0u));
+            for (uint32_t i = 0; i < 8u + vl; i++) dst[i] = h[i];
+        }
+        dst += kS2ChunkHdr + vl;
+    }
     uint32_t incl = eff;
     for (uint32_t o = 1; o < 64u; o <<= 1) {
         const uint32_t y = __shfl_up(incl, o, 64);
@@ -455,7 +606,12 @@ __global__ __launch_bounds__(64) void deflate_copy_kernel(CompArgs a) {
         const uint32_t wj = __shfl(word, j, 64), pj = __shfl(pos, j, 64);
         if (wj == 0u) break;  // the rest of the span is past the chunk's end
         uint8_t* o = dst + pj;
-        if (wj & kStored) {
+        if ((wj & kStored) && s2) {  // one literal: tag 61 (length - 1 in 2 bytes)
+            const uint32_t m = wj & ~kStored;
+            if (lane < kS2StoredHdr)
+                o[lane] = static_cast<uint8_t>(lane == 0 ? 61u << 2 : lane == 1 ? ((m - 1u) & 255u) : ((m - 1u) >> 8));
+            wave_copy(o + kS2StoredHdr, in + j * kSeg, m, lane);
+        } else if (wj & kStored) {
             const uint32_t m = wj & ~kStored;
             if (lane < 5u) {
                 const uint32_t hdr = lane == 0 ? 0u : lane == 1 ? (m & 255u) : lane == 2 ? (m >> 8)
@@ -483,7 +639,11 @@ __global__ __launch_bounds__(256) void deflate_frame_kernel(CompArgs a) {
     const uint64_t body = a.span_pos[a.spans[c + 1]] - a.span_pos[a.spans[c]];
     for (uint32_t t = 0; t < 4u; t++) dst[t] = static_cast<uint8_t>(a.header_id >> (8u * (3u - t)));
     uint64_t out_len;
-    if (a.gzip) {
+    if (a.fmt == kFmtS2) {  // the stream identifier chunk, then the spans' framing chunks
+        const uint8_t id[kS2StreamId] = {0xffu, 6u, 0u, 0u, 'S', '2', 's', 'T', 'w', 'O'};
+        for (uint32_t t = 0; t < kS2StreamId; t++) dst[4 + t] = id[t];
+        out_len = 4u + kS2StreamId + body;
+    } else if (a.gzip) {
         // RFC 1952 member: ID1 ID2 CM=8 FLG=0 MTIME=0 XFL=0 OS=255, the stream, CRC32, ISIZE
         const uint8_t gz[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 0, 0xff};
         for (uint32_t t = 0; t < 10u; t++) dst[4 + t] = gz[t];
@@ -518,22 +678,32 @@ namespace {
 struct CompAlgo {
     const char* name;
     uint32_t header_id;  // repo/compression/compression_ids.go:8-10, 19-21, 28-30
-    uint32_t skip;
+    uint32_t skip;       // literal-run skip shift: larger = fewer positions skipped
+    uint32_t effort;     // match search (CompArgs::effort)
     uint32_t gzip;
+    uint32_t fmt = compdev::kFmtDeflate;
 };
 // compressor_deflate.go:14-16, compressor_gzip.go:15-17, compressor_pgzip.go:16-18 (sorted names).
 // pgzip's writer splits its input into independently compressed blocks; gzip and pgzip readers
-// accept any valid member, so both families carry the same device stream.
+// accept any valid member, so both families carry the same device stream.  The levels differ in
+// search effort: best-speed = the lane's own table, default = + the span's first occurrences,
+// best-compression = + lazy matching and no literal-run skipping to speak of.
 constexpr CompAlgo kCompAlgos[] = {
-    {"deflate-best-compression", 0x1502u, 7u, 0u},
-    {"deflate-best-speed", 0x1501u, 4u, 0u},
-    {"deflate-default", 0x1500u, 5u, 0u},
-    {"gzip", 0x1000u, 5u, 1u},
-    {"gzip-best-compression", 0x1002u, 7u, 1u},
-    {"gzip-best-speed", 0x1001u, 4u, 1u},
-    {"pgzip", 0x1300u, 5u, 1u},
-    {"pgzip-best-compression", 0x1302u, 7u, 1u},
-    {"pgzip-best-speed", 0x1301u, 4u, 1u},
+    {"deflate-best-compression", 0x1502u, 8u, 2u, 0u},
+    {"deflate-best-speed", 0x1501u, 4u, 0u, 0u},
+    {"deflate-default", 0x1500u, 5u, 1u, 0u},
+    {"gzip", 0x1000u, 5u, 1u, 1u},
+    {"gzip-best-compression", 0x1002u, 8u, 2u, 1u},
+    {"gzip-best-speed", 0x1001u, 4u, 0u, 1u},
+    {"pgzip", 0x1300u, 5u, 1u, 1u},
+    {"pgzip-best-compression", 0x1302u, 8u, 2u, 1u},
+    {"pgzip-best-speed", 0x1301u, 4u, 0u, 1u},
+    // compressor_s2.go:20-23: s2.NewWriter's stream (framing chunks of Snappy-compatible blocks, which
+    // s2.NewReader decodes); the parallel variants differ only in the writer's goroutines.
+    {"s2-better", 0x1201u, 8u, 2u, 0u, compdev::kFmtS2},
+    {"s2-default", 0x1200u, 5u, 1u, 0u, compdev::kFmtS2},
+    {"s2-parallel-4", 0x1202u, 5u, 1u, 0u, compdev::kFmtS2},
+    {"s2-parallel-8", 0x1203u, 5u, 1u, 0u, compdev::kFmtS2},
 };
 
 const CompAlgo* find_comp(const char* name) {
@@ -546,14 +716,15 @@ const CompAlgo* find_comp(const char* name) {
 uint64_t align256c(uint64_t x) { return (x + 255u) & ~uint64_t(255); }
 
 struct CompWs {
-    uint64_t spans, crc, seglen, span_bytes, span_pos, slots, total;
+    uint64_t spans, crc, span_crc, seglen, span_bytes, span_pos, slots, total;
 };
-constexpr uint64_t kPerSpan = 64u * (compdev::kSlot + 4u) + 4u + 8u;
+constexpr uint64_t kPerSpan = 64u * (compdev::kSlot + 4u) + 4u + 4u + 8u;
 CompWs comp_ws(uint32_t n, uint64_t max_spans) {
     CompWs l{};
     l.spans = 0;
     l.crc = align256c((uint64_t(n) + 1u) * 4u);
-    l.seglen = align256c(l.crc + uint64_t(n) * 4u);
+    l.span_crc = align256c(l.crc + uint64_t(n) * 4u);
+    l.seglen = align256c(l.span_crc + max_spans * 4u);
     l.span_bytes = align256c(l.seglen + max_spans * 64u * 4u);
     l.span_pos = align256c(l.span_bytes + max_spans * 4u);
     l.slots = align256c(l.span_pos + (max_spans + 1u) * 8u);
@@ -620,13 +791,18 @@ extern "C" int kcdc_compress_chunks_device(const char* name, const uint8_t* d_da
     a.max_spans = static_cast<uint32_t>(max_spans);
     a.header_id = al->header_id;
     a.skip = al->skip;
+    a.effort = al->effort;
     a.gzip = al->gzip;
+    a.fmt = al->fmt;
     a.crc = reinterpret_cast<uint32_t*>(w + l.crc);
+    a.span_crc = reinterpret_cast<uint32_t*>(w + l.span_crc);
     {
-        uint32_t p = 1u << 30;  // x^1
+        uint32_t p = 1u << 30, q = 1u << 30;  // x^1
         for (int k = 0; k < 32; k++) {
             a.x2n[k] = p;
+            a.x2nc[k] = q;
             p = compdev::multmodp(p, p);
+            q = compdev::multmodp(q, q, compdev::kCrc32cPoly);
         }
     }
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -634,13 +810,17 @@ extern "C" int kcdc_compress_chunks_device(const char* name, const uint8_t* d_da
     hipLaunchKernelGGL(compdev::span_scan_kernel, dim3(1), dim3(1024), 0, st, nchunks, a.spans);
     if (max_spans > 0) {
         const dim3 grid(static_cast<uint32_t>(max_spans));
-        hipLaunchKernelGGL(compdev::deflate_spans_kernel, grid, dim3(64), 0, st, a);
+        const dim3 cgrid(static_cast<uint32_t>((max_spans + compdev::kCrcWaves - 1) / compdev::kCrcWaves));
+        if (a.fmt == compdev::kFmtS2) {
+            hipLaunchKernelGGL(compdev::lz_spans_kernel<compdev::kFmtS2>, grid, dim3(64), 0, st, a);
+            hipLaunchKernelGGL(compdev::crc_spans_kernel<true>, cgrid, dim3(64 * compdev::kCrcWaves), 0, st, a);
+        } else {
+            hipLaunchKernelGGL(compdev::lz_spans_kernel<compdev::kFmtDeflate>, grid, dim3(64), 0, st, a);
+        }
         hipLaunchKernelGGL(compdev::span_pos_kernel, dim3(1), dim3(1024), 0, st, a);
         hipLaunchKernelGGL(compdev::deflate_copy_kernel, grid, dim3(64), 0, st, a);
         if (a.gzip)
-            hipLaunchKernelGGL(compdev::crc_spans_kernel,
-                               dim3(static_cast<uint32_t>((max_spans + compdev::kCrcWaves - 1) / compdev::kCrcWaves)),
-                               dim3(64 * compdev::kCrcWaves), 0, st, a);
+            hipLaunchKernelGGL(compdev::crc_spans_kernel<false>, cgrid, dim3(64 * compdev::kCrcWaves), 0, st, a);
     }
     hipLaunchKernelGGL(compdev::deflate_frame_kernel, dim3((nchunks + 255u) / 256u), dim3(256), 0, st, a);
     const hipError_t e = hipGetLastError();

@@ -34,6 +34,88 @@ DEFLATE_LEVELS = {"deflate-best-speed": 1, "deflate-default": 6, "deflate-best-c
 GZIP_LEVELS = {"gzip": 6, "gzip-best-speed": 1, "gzip-best-compression": 9,
                "pgzip": 6, "pgzip-best-speed": 1, "pgzip-best-compression": 9}
 LEVELS = {**DEFLATE_LEVELS, **GZIP_LEVELS}
+# compressor_s2.go:20-23: s2.NewWriter streams; the decoder is oracle/s2_oracle.c (restated from the
+# Snappy framing + block formats; klauspost/compress is not vendored), format parity only.
+S2_NAMES = ("s2-better", "s2-default", "s2-parallel-4", "s2-parallel-8")
+
+
+def s2_decode(stream: bytes) -> bytes:
+    """s2.NewReader over a framed stream: stream identifier, CRC-32C of every chunk checked."""
+    import ctypes as C
+
+    from oracle import coracle
+    L = coracle.lib()
+    L.orc_s2_decode.restype = C.c_int64
+    L.orc_s2_decode.argtypes = [C.c_char_p, C.c_int64, C.c_void_p, C.c_int64]
+    cap = 4 * len(stream) + (1 << 16)
+    while True:
+        out = C.create_string_buffer(cap)
+        n = L.orc_s2_decode(stream, len(stream), out, cap)
+        if n == -11 or n == -6:  # a block larger than the room left: retry bigger
+            cap *= 8
+            continue
+        if n < 0:
+            raise ValueError(f"invalid S2 stream (oracle error {n})")
+        return out.raw[:n]
+
+
+def s2_encode(data: bytes) -> bytes:
+    """A plain S2 stream writer (for the oracle's own round-trip properties, not byte parity with
+    s2.NewWriter): stream identifier, 64 KiB framing chunks, greedy 4-byte-hash LZ77 emitting
+    Snappy literal / copy-2 elements (the subset the device emits too)."""
+    import struct
+    out = [b"\xff\x06\x00\x00S2sTwO"]
+    for c0 in range(0, len(data), 1 << 16):
+        blk = data[c0:c0 + (1 << 16)]
+        n = len(blk)
+        body = bytearray()
+        v = n
+        while True:
+            body.append((v & 127) | (128 if v >= 128 else 0))
+            v >>= 7
+            if not v:
+                break
+        tab, i, lit = {}, 0, 0
+
+        def literal(a, b):
+            while a < b:
+                k = min(b - a, 65536)
+                body.extend(bytes([61 << 2]) + struct.pack("<H", k - 1) + blk[a:a + k])
+                a += k
+        while i + 4 <= n:
+            key = blk[i:i + 4]
+            q = tab.get(key, -1)
+            tab[key] = i
+            if q >= 0:
+                m = 4
+                while i + m < n and blk[q + m] == blk[i + m]:
+                    m += 1
+                literal(lit, i)
+                left = m
+                while left:
+                    k = min(left, 64)
+                    body.extend(bytes([2 | ((k - 1) << 2)]) + struct.pack("<H", i - q))
+                    left -= k
+                i += m
+                lit = i
+            else:
+                i += 1
+        literal(lit, n)
+        c = crc32c(blk)
+        masked = (((c >> 15) | (c << 17)) + 0xa282ead8) & 0xFFFFFFFF
+        payload = struct.pack("<I", masked) + bytes(body)
+        out.append(b"\x00" + struct.pack("<I", len(payload))[:3] + payload)
+    return b"".join(out)
+
+
+def crc32c(data: bytes) -> int:
+    import ctypes as C
+
+    from oracle import coracle
+    L = coracle.lib()
+    L.orc_crc32c.restype = C.c_uint32
+    L.orc_crc32c.argtypes = [C.c_char_p, C.c_int64]
+    return int(L.orc_crc32c(data, len(data)))
 
 
 def _wbits(name: str) -> int:
@@ -45,7 +127,10 @@ def header(name: str) -> bytes:
 
 
 def compress(name: str, data: bytes) -> bytes:
-    """A reference-format stream from zlib's deflater (for ratio comparison, not byte parity)."""
+    """A reference-format stream from zlib's deflater, or the oracle's S2 writer (for ratio
+    comparison and the oracle's own properties, not byte parity)."""
+    if name in S2_NAMES:
+        return header(name) + s2_encode(data)
     co = zlib.compressobj(LEVELS[name], zlib.DEFLATED, _wbits(name))
     return header(name) + co.compress(data) + co.flush()
 
@@ -56,6 +141,8 @@ def decompress(name: str, blob: bytes) -> bytes:
     member's header, CRC-32 and ISIZE are checked as gzip.NewReader does (zlib, wbits 31)."""
     if blob[:4] != header(name):
         raise ValueError(f"invalid compression header, expected {header(name).hex()} but got {blob[:4].hex()}")
+    if name in S2_NAMES:
+        return s2_decode(blob[4:])
     d = zlib.decompressobj(_wbits(name))
     out = d.decompress(blob[4:]) + d.flush()
     if not d.eof:

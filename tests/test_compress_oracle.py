@@ -13,7 +13,8 @@ from oracle import deflate
 
 DEFLATE = ["deflate-best-compression", "deflate-best-speed", "deflate-default"]
 GZIP = ["gzip", "gzip-best-compression", "gzip-best-speed", "pgzip", "pgzip-best-compression", "pgzip-best-speed"]
-DEVICE = DEFLATE + GZIP  # the library's registry order (sorted names)
+S2 = list(deflate.S2_NAMES)
+DEVICE = DEFLATE + GZIP + S2  # the library's registry order (sorted within each family)
 
 
 def test_header_ids_match_reference():
@@ -84,3 +85,41 @@ def test_sync_flush_segments_concatenate():
         stream += seg
     stream += b"\x03\x00"
     assert deflate.decompress("deflate-default", deflate.header("deflate-default") + stream) == b"".join(parts)
+
+
+def _s2_chunk(block: bytes, data: bytes, kind: int = 0) -> bytes:
+    import struct
+    c = deflate.crc32c(data)
+    m = (((c >> 15) | (c << 17)) + 0xa282ead8) & 0xFFFFFFFF
+    body = struct.pack("<I", m) + (block if kind == 0 else data)
+    return bytes([kind]) + struct.pack("<I", len(body))[:3] + body
+
+
+def test_s2_oracle_decoder():
+    """oracle/s2_oracle.c (the S2 compressors' reader, restated from the Snappy framing and block
+    formats): CRC-32C check value, literals of every length form, copy-1/-2/-4, uncompressed and
+    padding chunks decode; a wrong CRC, a missing stream identifier and an S2 repeat code are
+    rejected."""
+    import struct
+    assert deflate.crc32c(b"123456789") == 0xE3069283  # CRC-32C (Castagnoli) check value
+    sid = b"\xff\x06\x00\x00S2sTwO"
+    lit = bytes(range(256)) * 2
+    block = bytes([0x80, 0x04])  # uvarint 512 + 15 + 64 = 591 -> filled below
+    data = lit[:300] + lit[:300][-4:] * 3 + lit[:64]
+    body = bytes([61 << 2]) + struct.pack("<H", 299) + lit[:300]       # literal, 2-byte length
+    body += bytes([1 | ((8 - 4) << 2) | (0 << 5), 4])                  # copy-1: len 8, offset 4
+    body += bytes([3 | ((4 - 1) << 2)]) + struct.pack("<I", 4)         # copy-4: len 4, offset 4
+    body += bytes([2 | ((64 - 1) << 2)]) + struct.pack("<H", 312)      # copy-2: len 64, offset 312
+    n = len(data)
+    block = bytes([n & 127 | 128, n >> 7]) + body
+    stream = sid + _s2_chunk(block, data) + b"\xfe\x02\x00\x00\x00\x00" + _s2_chunk(b"", b"raw!", 1)
+    assert deflate.s2_decode(stream) == data + b"raw!"
+    with pytest.raises(ValueError):
+        deflate.s2_decode(stream[10:])  # no stream identifier
+    bad = bytearray(stream)
+    bad[14] ^= 1  # the masked CRC of the first chunk
+    with pytest.raises(ValueError):
+        deflate.s2_decode(bytes(bad))
+    rep = bytes([8, 3 << 2]) + b"abcd" + bytes([1 | (0 << 2), 0])      # copy-1 offset 0 (S2 repeat)
+    with pytest.raises(ValueError):
+        deflate.s2_decode(sid + _s2_chunk(rep, b"abcdabcd"))
