@@ -42,6 +42,9 @@ constexpr int kFmtS2 = 1;                       // S2 / Snappy block elements in
 constexpr uint32_t kS2StoredHdr = 3;            // a stored S2 segment: one literal, tag 61 + 2-byte length
 constexpr uint32_t kS2ChunkHdr = 8;             // framing chunk: type 0x00, 3-byte length, masked CRC-32C
 constexpr uint32_t kS2StreamId = 10;            // ff 06 00 00 "S2sTwO" (s2.NewWriter's stream identifier)
+constexpr int kFmtZstd = 2;                     // Zstandard frame (RFC 8878): one compressed block per segment
+constexpr uint32_t kZOff = 3;                   // a zstd segment's bytes start at slot + 3 (see lz_spans_kernel)
+constexpr uint32_t kZStoredHdr = 3;             // a stored zstd segment: Raw_Block header
 #ifndef KCDC_DEFLATE_HASH_BITS
 #define KCDC_DEFLATE_HASH_BITS 6  // per-lane match table entries (log2); LDS = 33 KiB span + 128 B << bits
 #endif
@@ -115,6 +118,104 @@ __global__ __launch_bounds__(1024) void span_scan_kernel(uint32_t n, uint32_t* s
 
 // LDS dword index of staged word k: one pad dword per 128 words (a 512-byte segment).
 __device__ __forceinline__ uint32_t pw(uint32_t k) { return k + (k >> 7); }
+
+// ---------------------------------------------------------------- Zstandard sequences (RFC 8878)
+// The sequences of a block go through FSE with the predefined distributions (Symbol_Compression_Modes
+// = Predefined_Mode for literal lengths, offsets and match lengths, RFC 8878 §3.1.1.3.2.2).  The
+// decoding tables are built exactly as the RFC's FSE table construction (spread with step
+// (size >> 1) + (size >> 3) + 3, "less than 1" symbols at the top); the encoder uses, per symbol, the
+// cell whose [baseline, baseline + 2^bits) holds the next state (a symbol's cells cover every state
+// once).  All compile-time: no table upload.
+template <int NS, int AL>
+struct FseTab {
+    static constexpr int kSize = 1 << AL;
+    uint8_t sym[kSize], nb[kSize], base[kSize];
+    uint8_t enc[NS][kSize];  // enc[s][next state] = the cell of symbol s that reaches it
+    uint8_t first[NS];       // some cell of s (the last sequence's state is free)
+    constexpr FseTab(const int8_t (&norm)[NS]) : sym{}, nb{}, base{}, enc{}, first{} {
+        int next[NS] = {};
+        int high = kSize - 1;
+        for (int s = 0; s < NS; s++) {
+            if (norm[s] == -1) {
+                sym[high--] = static_cast<uint8_t>(s);
+                next[s] = 1;
+            } else {
+                next[s] = norm[s];
+            }
+        }
+        int pos = 0;
+        const int step = (kSize >> 1) + (kSize >> 3) + 3;
+        for (int s = 0; s < NS; s++)
+            for (int i = 0; i < norm[s]; i++) {
+                sym[pos] = static_cast<uint8_t>(s);
+                do pos = (pos + step) & (kSize - 1);
+                while (pos > high);
+            }
+        for (int u = 0; u < kSize; u++) {
+            const int s = sym[u];
+            const int ns = next[s]++;
+            int hb = 0;
+            while ((2 << hb) <= ns) hb++;
+            nb[u] = static_cast<uint8_t>(AL - hb);
+            base[u] = static_cast<uint8_t>((ns << (AL - hb)) - kSize);
+            first[s] = static_cast<uint8_t>(u);
+            for (int t = base[u]; t < base[u] + (1 << nb[u]); t++) enc[s][t] = static_cast<uint8_t>(u);
+        }
+    }
+};
+constexpr int8_t kLLNorm[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
+                                2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+constexpr int8_t kMLNorm[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+constexpr int8_t kOFNorm[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                -1, -1, -1, -1, -1};
+__device__ const FseTab<36, 6> kFseLL(kLLNorm);
+__device__ const FseTab<53, 6> kFseML(kMLNorm);
+__device__ const FseTab<29, 5> kFseOF(kOFNorm);
+
+// Literal length -> (code, extra bits, extra value); RFC 8878 Literals_Length_Code table.
+__device__ __forceinline__ void ll_code(uint32_t ll, uint32_t& code, uint32_t& nbx, uint32_t& x) {
+    constexpr uint8_t base[20] = {16, 18, 20, 22, 24, 28, 32, 40, 48, 64, 128, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    constexpr uint8_t bits[20] = {1, 1, 1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+    if (ll < 16u) {
+        code = ll;
+        nbx = 0;
+        x = 0;
+    } else if (ll < 64u) {
+        uint32_t c = 0;
+        while (c + 1u < 9u && base[c + 1] <= ll) c++;
+        code = 16u + c;
+        nbx = bits[c];
+        x = ll - base[c];
+    } else {
+        const uint32_t h = 31u - __builtin_clz(ll);  // 64 -> 6
+        code = h + 19u;
+        nbx = h;
+        x = ll - (1u << h);
+    }
+}
+// Match length (>= 3) -> (code, extra bits, extra value); Match_Length_Code table.
+__device__ __forceinline__ void ml_code(uint32_t ml, uint32_t& code, uint32_t& nbx, uint32_t& x) {
+    constexpr uint8_t base[11] = {35, 37, 39, 41, 43, 47, 51, 59, 67, 83, 99};
+    constexpr uint8_t bits[11] = {1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5};
+    const uint32_t m = ml - 3u;
+    if (m < 32u) {
+        code = m;
+        nbx = 0;
+        x = 0;
+    } else if (ml < 131u) {
+        uint32_t c = 0;
+        while (c + 1u < 11u && base[c + 1] <= ml) c++;
+        code = 32u + c;
+        nbx = bits[c];
+        x = ml - base[c];
+    } else {
+        const uint32_t h = 31u - __builtin_clz(m);  // 128 -> 7: code 43, baseline 131
+        code = h + 36u;
+        nbx = h;
+        x = m - (1u << h);
+    }
+}
 
 struct Bits {
     uint64_t bb;
@@ -239,8 +340,12 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
     const uint32_t seg_len = xe - x0;
     uint32_t* base = reinterpret_cast<uint32_t*>(a.slots + static_cast<uint64_t>(slot) * kSlot);
     const uint32_t limit = seg_len + 8u;  // bytes flushed before giving up on the segment
-    Bits w{0ull, 0u, base};
+    // zstd: block header at bytes 3..5, Raw literals header at 6..7, the literals from byte 8; the
+    // sequences (4 bytes each) are kept from the slot's end downwards (8 + literals + 4 sequences
+    // <= 8 + seg_len: a sequence covers >= 4 input bytes, so the two never meet).
+    Bits w{0ull, 0u, FMT == kFmtZstd ? base + 2 : base};
     bool over = false;
+    uint32_t nseq = 0;
     if constexpr (FMT == kFmtDeflate) w.put(2u, 3);  // BFINAL 0, BTYPE 01
     uint32_t x = x0, lit = x0;
     auto literals = [&](uint32_t e) {
@@ -258,7 +363,7 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
             }
         }
         for (uint32_t q = lit; q < e; q++) {
-            if constexpr (FMT == kFmtS2)
+            if constexpr (FMT != kFmtDeflate)
                 w.put(byte(q), 8);
             else
                 put_lit(w, byte(q));
@@ -286,7 +391,7 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
     // Length of the match of x against an earlier q (>= 4 when the first 4 bytes agree), <= maxlen.
     auto match_len = [&](uint32_t q, uint32_t xx, uint32_t v) -> uint32_t {
         if (q >= xx || ld32(q) != v) return 0u;
-        const uint32_t cap = FMT == kFmtDeflate ? 258u : kSeg;  // S2 copies have no length limit
+        const uint32_t cap = FMT == kFmtS2 ? kSeg : 258u;  // S2 copies have no length limit
         const uint32_t maxlen = xe - xx < cap ? xe - xx : cap;
         uint32_t n = 4;
         while (n + 4u <= maxlen) {
@@ -334,10 +439,14 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
         if (n) {
             literals(x);
             if (over) break;
-            if constexpr (FMT == kFmtS2)
+            if constexpr (FMT == kFmtS2) {
                 s2_copy(n, x - cand);
-            else
+            } else if constexpr (FMT == kFmtZstd) {  // (literal length, match length - 4, offset)
+                base[143u - nseq] = ((x - lit) << 23) | ((n - 4u) << 15) | (x - cand);
+                nseq++;
+            } else {
                 put_match(w, n, x - cand);
+            }
             if (4u * static_cast<uint32_t>(w.op - base) > limit) {
                 over = true;
                 break;
@@ -347,6 +456,84 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
         } else {
             x += 1u + ((x - lit) >> a.skip);
         }
+    }
+    if constexpr (FMT == kFmtZstd) {
+        if (!over) literals(xe);  // the block's last literals (no sequence)
+        if (over) return kStored | seg_len;
+        const uint32_t nlit = 4u * static_cast<uint32_t>(w.op - (base + 2)) + (w.nb >> 3);
+        if (w.nb) *w.op = static_cast<uint32_t>(w.bb);
+        uint8_t* sb8 = reinterpret_cast<uint8_t*>(base);
+        // Sequences section: Number_of_Sequences, Symbol_Compression_Modes = 0 (all Predefined), then
+        // the FSE bitstream written backwards from the last sequence (RFC 8878 §3.1.1.3.2;
+        // zstd's ZSTD_encodeSequences order), closed by the 1-bit end marker.
+        uint8_t* op = sb8 + 8 + nlit;
+        uint64_t bb = 0;
+        uint32_t nb = 0;
+        auto put = [&](uint32_t v, uint32_t n) {
+            bb |= static_cast<uint64_t>(v) << nb;
+            nb += n;
+            while (nb >= 8u) {
+                *op++ = static_cast<uint8_t>(bb);
+                bb >>= 8;
+                nb -= 8u;
+            }
+        };
+        if (nseq < 128u) {
+            put(nseq, 8);
+        } else {
+            put(128u + (nseq >> 8), 8);
+            put(nseq & 255u, 8);
+        }
+        if (nseq) {
+            put(0u, 8);  // Predefined_Mode x 3
+            uint32_t sLL = 0, sML = 0, sOF = 0;
+            for (int k = static_cast<int>(nseq) - 1; k >= 0; k--) {
+                // the writer must stay below the sequences not yet read (rare: costly sequences)
+                if (op + 8 > sb8 + 4u * (144u - static_cast<uint32_t>(k) - 1u) || op > sb8 + seg_len + 2u) {
+                    over = true;
+                    break;
+                }
+                const uint32_t v = base[143u - static_cast<uint32_t>(k)];
+                const uint32_t ll = v >> 23, ml = ((v >> 15) & 255u) + 4u, ov = (v & 0x7FFFu) + 3u;
+                uint32_t llc, llb, llx, mlc, mlb, mlx;
+                ll_code(ll, llc, llb, llx);
+                ml_code(ml, mlc, mlb, mlx);
+                const uint32_t ofc = 31u - __builtin_clz(ov), ofx = ov - (1u << ofc);
+                if (k == static_cast<int>(nseq) - 1) {
+                    sLL = kFseLL.first[llc];
+                    sML = kFseML.first[mlc];
+                    sOF = kFseOF.first[ofc];
+                } else {  // the decoder's updates after sequence k: LL, ML, OF -> written OF, ML, LL
+                    const uint32_t nOF = kFseOF.enc[ofc][sOF];
+                    put(sOF - kFseOF.base[nOF], kFseOF.nb[nOF]);
+                    sOF = nOF;
+                    const uint32_t nML = kFseML.enc[mlc][sML];
+                    put(sML - kFseML.base[nML], kFseML.nb[nML]);
+                    sML = nML;
+                    const uint32_t nLL = kFseLL.enc[llc][sLL];
+                    put(sLL - kFseLL.base[nLL], kFseLL.nb[nLL]);
+                    sLL = nLL;
+                }
+                put(llx, llb);  // the decoder reads offset, match length, literal length extras
+                put(mlx, mlb);
+                put(ofx, ofc);
+            }
+            put(sML, 6);  // initial states, read LL, OF, ML
+            put(sOF, 5);
+            put(sLL, 6);
+            put(1u, 1);  // end marker
+            if (nb) put(0u, 8u - nb);
+        }
+        if (over) return kStored | seg_len;
+        const uint32_t total = static_cast<uint32_t>(op - sb8) - kZOff;  // block header + content
+        if (total >= seg_len + kZStoredHdr) return kStored | seg_len;
+        const uint32_t hdr = ((total - 3u) << 3) | (2u << 1);  // Compressed_Block, not the last
+        sb8[3] = static_cast<uint8_t>(hdr);
+        sb8[4] = static_cast<uint8_t>(hdr >> 8);
+        sb8[5] = static_cast<uint8_t>(hdr >> 16);
+        sb8[6] = static_cast<uint8_t>(0x04u | ((nlit & 15u) << 4));  // Raw_Literals_Block, 2-byte size
+        sb8[7] = static_cast<uint8_t>(nlit >> 4);
+        return total;
     }
     if constexpr (FMT == kFmtS2) {
         if (!over) {  // exact size with the pending literal: worse than one stored literal -> stored
@@ -394,7 +581,7 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
     }();
     a.seglen[slot] = word;
     // The span's output bytes (stored segments: 5 + n, S2: 3 + n; S2 adds the framing header).
-    const uint32_t shdr = FMT == kFmtS2 ? kS2StoredHdr : 5u;
+    const uint32_t shdr = FMT == kFmtS2 ? kS2StoredHdr : FMT == kFmtZstd ? kZStoredHdr : 5u;
     uint32_t eff = (word & kStored) ? shdr + (word & ~kStored) : word;
     for (uint32_t o = 32; o > 0; o >>= 1) eff += __shfl_xor(eff, o, 64);
     if (FMT == kFmtS2) eff += kS2ChunkHdr + uvarint_len(span_len);
@@ -557,6 +744,22 @@ __device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint
     if (lane < n - done) dst[done + lane] = src[done + lane];
 }
 
+// Zstandard frame header of a chunk of `len` bytes (RFC 8878 §3.1.1.1): magic, Frame_Header_Descriptor
+// with Single_Segment_flag (the window is the content) and the smallest Frame_Content_Size field;
+// no checksum, no dictionary.  Returns its size; writes it when dst is set.
+__device__ __forceinline__ uint32_t zstd_frame_header(uint64_t len, uint8_t* dst) {
+    const uint32_t fcs = len < 256u ? 1u : len < 65536u + 256u ? 2u : len < (1ull << 32) ? 4u : 8u;
+    if (dst) {
+        const uint8_t magic[4] = {0x28u, 0xB5u, 0x2Fu, 0xFDu};
+        for (int i = 0; i < 4; i++) dst[i] = magic[i];
+        const uint32_t flag = fcs == 1u ? 0u : fcs == 2u ? 1u : fcs == 4u ? 2u : 3u;
+        dst[4] = static_cast<uint8_t>((flag << 6) | 0x20u);
+        const uint64_t v = fcs == 2u ? len - 256u : len;
+        for (uint32_t i = 0; i < fcs; i++) dst[5 + i] = static_cast<uint8_t>(v >> (8u * i));
+    }
+    return 5u + fcs;
+}
+
 // One wave per span: its segments' bytes to their places in the chunk's stream.
 __global__ __launch_bounds__(64) void deflate_copy_kernel(CompArgs a) {
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
@@ -570,11 +773,12 @@ __global__ __launch_bounds__(64) void deflate_copy_kernel(CompArgs a) {
     const uint32_t c = lo;
     const uint32_t u = b - a.spans[c];
     uint8_t* dst = a.out + a.out_offs[c] + 4u + (a.gzip ? 10u : 0u) + (a.fmt == kFmtS2 ? kS2StreamId : 0u) +
+                   (a.fmt == kFmtZstd ? zstd_frame_header(a.in_lens[c], nullptr) : 0u) +
                    (a.span_pos[b] - a.span_pos[a.spans[c]]);
     const uint8_t* in = a.in + a.in_offs[c] + static_cast<uint64_t>(u) * kSpan;
     const uint32_t word = a.seglen[b * 64u + lane];
-    const bool s2 = a.fmt == kFmtS2;
-    const uint32_t eff = (word & kStored) ? (s2 ? kS2StoredHdr : 5u) + (word & ~kStored) : word;
+    const bool s2 = a.fmt == kFmtS2, zs = a.fmt == kFmtZstd;
+    const uint32_t eff = (word & kStored) ? (s2 ? kS2StoredHdr : zs ? kZStoredHdr : 5u) + (word & ~kStored) : word;
     if (s2) {  // framing chunk header: 0x00, length, masked CRC-32C of the span, uvarint(span length)
         const uint64_t len = a.in_lens[c], sb = static_cast<uint64_t>(u) * kSpan;
         const uint32_t span_len = static_cast<uint32_t>(len - sb < kSpan ? len - sb : kSpan);
@@ -606,7 +810,11 @@ __global__ __launch_bounds__(64) void deflate_copy_kernel(CompArgs a) {
         const uint32_t wj = __shfl(word, j, 64), pj = __shfl(pos, j, 64);
         if (wj == 0u) break;  // the rest of the span is past the chunk's end
         uint8_t* o = dst + pj;
-        if ((wj & kStored) && s2) {  // one literal: tag 61 (length - 1 in 2 bytes)
+        if ((wj & kStored) && zs) {  // Raw_Block: header (size << 3 | 0), then the bytes
+            const uint32_t m = wj & ~kStored;
+            if (lane < kZStoredHdr) o[lane] = static_cast<uint8_t>((m << 3) >> (8u * lane));
+            wave_copy(o + kZStoredHdr, in + j * kSeg, m, lane);
+        } else if ((wj & kStored) && s2) {  // one literal: tag 61 (length - 1 in 2 bytes)
             const uint32_t m = wj & ~kStored;
             if (lane < kS2StoredHdr)
                 o[lane] = static_cast<uint8_t>(lane == 0 ? 61u << 2 : lane == 1 ? ((m - 1u) & 255u) : ((m - 1u) >> 8));
@@ -620,7 +828,7 @@ __global__ __launch_bounds__(64) void deflate_copy_kernel(CompArgs a) {
             }
             wave_copy(o + 5, in + j * kSeg, m, lane);
         } else {
-            wave_copy(o, a.slots + (static_cast<uint64_t>(b) * 64u + j) * kSlot, wj, lane);
+            wave_copy(o, a.slots + (static_cast<uint64_t>(b) * 64u + j) * kSlot + (zs ? kZOff : 0u), wj, lane);
         }
     }
 }
@@ -639,7 +847,14 @@ __global__ __launch_bounds__(256) void deflate_frame_kernel(CompArgs a) {
     const uint64_t body = a.span_pos[a.spans[c + 1]] - a.span_pos[a.spans[c]];
     for (uint32_t t = 0; t < 4u; t++) dst[t] = static_cast<uint8_t>(a.header_id >> (8u * (3u - t)));
     uint64_t out_len;
-    if (a.fmt == kFmtS2) {  // the stream identifier chunk, then the spans' framing chunks
+    if (a.fmt == kFmtZstd) {  // frame header, the segments' blocks, a last empty Raw_Block (01 00 00)
+        const uint32_t fh = zstd_frame_header(a.in_lens[c], dst + 4);
+        uint8_t* e = dst + 4 + fh + body;
+        e[0] = 0x01u;
+        e[1] = 0x00u;
+        e[2] = 0x00u;
+        out_len = 4u + fh + body + 3u;
+    } else if (a.fmt == kFmtS2) {  // the stream identifier chunk, then the spans' framing chunks
         const uint8_t id[kS2StreamId] = {0xffu, 6u, 0u, 0u, 'S', '2', 's', 'T', 'w', 'O'};
         for (uint32_t t = 0; t < kS2StreamId; t++) dst[4 + t] = id[t];
         out_len = 4u + kS2StreamId + body;
@@ -704,6 +919,12 @@ constexpr CompAlgo kCompAlgos[] = {
     {"s2-default", 0x1200u, 5u, 1u, 0u, compdev::kFmtS2},
     {"s2-parallel-4", 0x1202u, 5u, 1u, 0u, compdev::kFmtS2},
     {"s2-parallel-8", 0x1203u, 5u, 1u, 0u, compdev::kFmtS2},
+    // compressor_zstd.go:15-18: zstd.NewWriter frames (zstd.NewReader decodes any RFC 8878 frame);
+    // zstd-best-compression is registered deprecated (decompression of old data), still encodable.
+    {"zstd", 0x1100u, 5u, 1u, 0u, compdev::kFmtZstd},
+    {"zstd-best-compression", 0x1103u, 8u, 2u, 0u, compdev::kFmtZstd},
+    {"zstd-better-compression", 0x1102u, 8u, 2u, 0u, compdev::kFmtZstd},
+    {"zstd-fastest", 0x1101u, 4u, 0u, 0u, compdev::kFmtZstd},
 };
 
 const CompAlgo* find_comp(const char* name) {
@@ -749,7 +970,7 @@ extern "C" int64_t kcdc_compression_header_id(const char* name) {
              : set_error(-2, std::string("unknown compression algorithm: ") + (name ? name : "(null)"));
 }
 
-extern "C" uint64_t kcdc_compress_bound(uint64_t len) {  // + 18: a gzip member's header and trailer
+extern "C" uint64_t kcdc_compress_bound(uint64_t len) {  // + 18: a gzip member's header and trailer (>= zstd's 13 + 3)
     return 24u + len + 5u * ((len + compdev::kSeg - 1) / compdev::kSeg);
 }
 
@@ -814,6 +1035,8 @@ extern "C" int kcdc_compress_chunks_device(const char* name, const uint8_t* d_da
         if (a.fmt == compdev::kFmtS2) {
             hipLaunchKernelGGL(compdev::lz_spans_kernel<compdev::kFmtS2>, grid, dim3(64), 0, st, a);
             hipLaunchKernelGGL(compdev::crc_spans_kernel<true>, cgrid, dim3(64 * compdev::kCrcWaves), 0, st, a);
+        } else if (a.fmt == compdev::kFmtZstd) {
+            hipLaunchKernelGGL(compdev::lz_spans_kernel<compdev::kFmtZstd>, grid, dim3(64), 0, st, a);
         } else {
             hipLaunchKernelGGL(compdev::lz_spans_kernel<compdev::kFmtDeflate>, grid, dim3(64), 0, st, a);
         }

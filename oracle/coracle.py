@@ -124,10 +124,16 @@ def feed_kind(kind: str, size: int, data: bytes, mode: str, seed: int = 1) -> np
 
 def split_stream(name: str, data) -> np.ndarray:
     """Chunk end offsets of a whole stream, trailing chunk included (last == len)."""
-    k, size = params(name)
+    kind, size = REGISTRY[name]
+    return split_stream_kind(kind, size, data)
+
+
+def split_stream_kind(kind: str, size: int, data) -> np.ndarray:
+    """As split_stream() for an unregistered parameterisation (the KAT factories)."""
+    k = KIND[kind]
     buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
     n = buf.size
-    cap = cut_capacity(name, n)
+    cap = n // max(size if kind == "fixed" else size // 2, 1) + 1
     out = np.zeros(max(cap, 1), dtype=np.int64)
     cnt = lib().orc_split_stream(k, size, buf.ctypes.data, n, out, cap)
     assert cnt <= cap

@@ -37,6 +37,58 @@ LEVELS = {**DEFLATE_LEVELS, **GZIP_LEVELS}
 # compressor_s2.go:20-23: s2.NewWriter streams; the decoder is oracle/s2_oracle.c (restated from the
 # Snappy framing + block formats; klauspost/compress is not vendored), format parity only.
 S2_NAMES = ("s2-better", "s2-default", "s2-parallel-4", "s2-parallel-8")
+# compressor_zstd.go:15-18: klauspost zstd.NewWriter at SpeedFastest / SpeedDefault / SpeedBetterCompression /
+# SpeedBestCompression (roughly zstd levels 1 / 3 / 7 / 11); the reader is zstd.NewReader.  The oracle's
+# independent RFC 8878 decoder is the system libzstd (libzstd.so.1, the C reference implementation).
+ZSTD_LEVELS = {"zstd": 3, "zstd-best-compression": 11, "zstd-better-compression": 7, "zstd-fastest": 1}
+ZSTD_NAMES = tuple(ZSTD_LEVELS)
+_ZSTD = None
+
+
+def _zstd():
+    global _ZSTD
+    if _ZSTD is None:
+        import ctypes as C
+        L = C.CDLL("libzstd.so.1")
+        L.ZSTD_decompress.restype = C.c_size_t
+        L.ZSTD_decompress.argtypes = [C.c_void_p, C.c_size_t, C.c_char_p, C.c_size_t]
+        L.ZSTD_compress.restype = C.c_size_t
+        L.ZSTD_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_int]
+        L.ZSTD_compressBound.restype = C.c_size_t
+        L.ZSTD_compressBound.argtypes = [C.c_size_t]
+        L.ZSTD_isError.restype = C.c_uint
+        L.ZSTD_isError.argtypes = [C.c_size_t]
+        L.ZSTD_getErrorName.restype = C.c_char_p
+        L.ZSTD_getErrorName.argtypes = [C.c_size_t]
+        L.ZSTD_getFrameContentSize.restype = C.c_ulonglong
+        L.ZSTD_getFrameContentSize.argtypes = [C.c_char_p, C.c_size_t]
+        _ZSTD = L
+    return _ZSTD
+
+
+def zstd_decode(stream: bytes) -> bytes:
+    """zstd.NewReader over whole frames (every block checked; trailing bytes rejected)."""
+    import ctypes as C
+    L = _zstd()
+    cap = L.ZSTD_getFrameContentSize(stream, len(stream))
+    if cap >= (1 << 63):  # unknown (0xFF..FF) or error (0xFF..FE): the device always writes the size
+        raise ValueError("zstd frame without a content size")
+    out = C.create_string_buffer(max(int(cap), 1))
+    n = L.ZSTD_decompress(out, int(cap), stream, len(stream))
+    if L.ZSTD_isError(n):
+        raise ValueError(f"invalid zstd stream: {L.ZSTD_getErrorName(n).decode()}")
+    return out.raw[:n]
+
+
+def zstd_encode(data: bytes, level: int) -> bytes:
+    import ctypes as C
+    L = _zstd()
+    cap = L.ZSTD_compressBound(len(data))
+    out = C.create_string_buffer(cap)
+    n = L.ZSTD_compress(out, cap, data, len(data), level)
+    if L.ZSTD_isError(n):
+        raise ValueError(L.ZSTD_getErrorName(n).decode())
+    return out.raw[:n]
 
 
 def s2_decode(stream: bytes) -> bytes:
@@ -127,10 +179,12 @@ def header(name: str) -> bytes:
 
 
 def compress(name: str, data: bytes) -> bytes:
-    """A reference-format stream from zlib's deflater, or the oracle's S2 writer (for ratio
+    """A reference-format stream from zlib's deflater, libzstd, or the oracle's S2 writer (for ratio
     comparison and the oracle's own properties, not byte parity)."""
     if name in S2_NAMES:
         return header(name) + s2_encode(data)
+    if name in ZSTD_NAMES:
+        return header(name) + zstd_encode(data, ZSTD_LEVELS[name])
     co = zlib.compressobj(LEVELS[name], zlib.DEFLATED, _wbits(name))
     return header(name) + co.compress(data) + co.flush()
 
@@ -143,6 +197,8 @@ def decompress(name: str, blob: bytes) -> bytes:
         raise ValueError(f"invalid compression header, expected {header(name).hex()} but got {blob[:4].hex()}")
     if name in S2_NAMES:
         return s2_decode(blob[4:])
+    if name in ZSTD_NAMES:
+        return zstd_decode(blob[4:])
     d = zlib.decompressobj(_wbits(name))
     out = d.decompress(blob[4:]) + d.flush()
     if not d.eof:

@@ -150,7 +150,10 @@ def xasm(request, tmp_path_factory):
 
 
 def _kernel_bodies(asm: str):
+    funcs = set(re.findall(r"^\s*\.type\s+(_Z[^,\s]*),@function", asm, re.M))
     for m in re.finditer(r"^(_Z[^ :]*):", asm, re.M):
+        if m.group(1) not in funcs:  # a __device__ constant (e.g. the zstd FSE tables), not code
+            continue
         body = re.search(rf"^{re.escape(m.group(1))}:(.*?)^\.Lfunc_end", asm, re.S | re.M)
         yield m.group(1), body.group(1)
 

@@ -14,7 +14,8 @@ from oracle import deflate
 DEFLATE = ["deflate-best-compression", "deflate-best-speed", "deflate-default"]
 GZIP = ["gzip", "gzip-best-compression", "gzip-best-speed", "pgzip", "pgzip-best-compression", "pgzip-best-speed"]
 S2 = list(deflate.S2_NAMES)
-DEVICE = DEFLATE + GZIP + S2  # the library's registry order (sorted within each family)
+ZSTD = ["zstd", "zstd-best-compression", "zstd-better-compression", "zstd-fastest"]
+DEVICE = DEFLATE + GZIP + S2 + ZSTD  # the library's registry order (sorted within each family)
 
 
 def test_header_ids_match_reference():
@@ -32,7 +33,7 @@ def test_library_registry():
     for name in DEVICE:
         assert kc.HeaderID(name) == deflate.HEADER_IDS[name]
     with pytest.raises(_lib.KcdcError):
-        kc.HeaderID("zstd-fastest")  # registered in the reference, not encoded on the device
+        kc.HeaderID("lz4")  # registered in the reference (deprecated), not encoded on the device
     with pytest.raises(_lib.KcdcError):
         kc.Compressor("no-such-compressor")
 

@@ -18,6 +18,8 @@ pytestmark = pytest.mark.gpu
 DEFLATE = ["deflate-best-compression", "deflate-best-speed", "deflate-default"]
 GZIP = ["gzip", "gzip-best-compression", "gzip-best-speed", "pgzip", "pgzip-best-compression", "pgzip-best-speed"]
 S2 = list(deflate.S2_NAMES)  # compressor_s2.go:20-23; decoded by oracle/s2_oracle.c (CRC-32C checked)
+ZSTD = list(deflate.ZSTD_NAMES)  # compressor_zstd.go:15-18; decoded by libzstd (the RFC 8878 reference decoder)
+ALL = DEFLATE + GZIP + S2 + ZSTD
 
 
 def _compress(name, host, offs, lens, dev):
@@ -61,7 +63,7 @@ def _mixed(nbytes, seed):
     return np.frombuffer(b"".join(out)[:nbytes], np.uint8).copy()
 
 
-@pytest.mark.parametrize("name", DEFLATE + GZIP + S2)
+@pytest.mark.parametrize("name", ALL)
 def test_reference_properties(name, gpu):
     """compressor_test.go:21-84 through the device: 10000 zero bytes shrink (and keep the ID),
     10000 random bytes do not (ID 0, NoCompression), both inflate back; the other deflate
@@ -75,13 +77,14 @@ def test_reference_properties(name, gpu):
     assert ol[0] < 10000 and ids[0] == deflate.HEADER_IDS[name]
     assert ol[1] >= 10000 and ids[1] == 0
     blob = out[oo[0]:oo[0] + ol[0]].tobytes()
-    for other in DEFLATE + GZIP + S2:
+    for other in ALL:
         if other != name:
             with pytest.raises(ValueError):
                 deflate.decompress(other, blob)
 
 
-@pytest.mark.parametrize("name", ["deflate-default", "gzip", "pgzip-best-speed", "s2-default", "s2-better"])
+@pytest.mark.parametrize("name", ["deflate-default", "gzip", "pgzip-best-speed", "s2-default", "s2-better",
+                                  "zstd", "zstd-best-compression"])
 def test_ragged_misaligned_chunks(name, gpu):
     """Edge lengths around the 512-byte segments and 32 KiB spans at random offsets; for the gzip
     family this exercises the device CRC-32 (end-aligned spans, partial first span)."""
@@ -96,7 +99,8 @@ def test_ragged_misaligned_chunks(name, gpu):
     assert (ids != 0).sum() > len(lens) // 2  # mixed data mostly compresses
 
 
-@pytest.mark.parametrize("name", DEFLATE + ["gzip-best-compression", "s2-better", "s2-parallel-8"])
+@pytest.mark.parametrize("name", DEFLATE + ["gzip-best-compression", "s2-better", "s2-parallel-8", "zstd-fastest",
+                                            "zstd-better-compression"])
 def test_large_compressible_chunks(name, gpu):
     """The reference benchmark's inputs (compressor_test.go:92-96): a repeated 1..10 pattern and
     zeros, as 8 MiB + odd chunks; both must shrink far below the input."""
@@ -111,7 +115,7 @@ def test_large_compressible_chunks(name, gpu):
     assert ol[0] < lim * lens[0] and ol[1] < lim * lens[1]
 
 
-@pytest.mark.parametrize("name", ["deflate-best-speed", "pgzip", "s2-parallel-4"])
+@pytest.mark.parametrize("name", ["deflate-best-speed", "pgzip", "s2-parallel-4", "zstd"])
 def test_splitter_chunks_of_mixed_stream(name, gpu):
     """Chunks cut by the oracle's DYNAMIC-128K-BUZHASH over a mixed 32 MiB stream."""
     host = _mixed(32 << 20, 21)
@@ -172,3 +176,25 @@ def test_s2_random_stream_is_stored(gpu):
     _check("s2-default", host, offs, lens, out, oo, ol, ids)
     assert not ids.any()
     assert all(int(x) == 4 + 10 + 32 * (8 + 3) + (1 << 20) + 3 * 2048 for x in ol)
+
+
+def test_zstd_random_stream_is_stored(gpu):
+    """Config-2 bytes through zstd: one frame per chunk (magic, descriptor, 4-byte content size),
+    every 512-byte segment a Raw_Block (3-byte header), a final empty Raw_Block; ID NoCompression."""
+    host = coracle.gen_stream(0x6B6F706961, 0, 8 << 20)
+    lens = [1 << 20] * 8
+    offs = [i << 20 for i in range(8)]
+    out, oo, ol, ids = _compress("zstd", host, offs, lens, gpu)
+    _check("zstd", host, offs, lens, out, oo, ol, ids)
+    assert not ids.any()
+    assert all(int(x) == 4 + 9 + 2048 * (3 + 512) + 3 for x in ol)
+
+
+@pytest.mark.parametrize("name", ["s2-default", "zstd"])
+def test_tiny_chunks_frame(name, gpu):
+    """Empty and few-byte chunks: a frame with no data block (zstd: header + final empty block;
+    S2: the stream identifier alone) still decodes to the empty string."""
+    host = np.frombuffer(b"abcabcabcabcabcabcabc", np.uint8).copy()
+    offs, lens = [0, 0, 3, 0], [0, 1, 4, 21]
+    out, oo, ol, ids = _compress(name, host, offs, lens, gpu)
+    _check(name, host, offs, lens, out, oo, ol, ids)

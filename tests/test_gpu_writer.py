@@ -91,14 +91,16 @@ def test_tiny_rounds_carry_the_tail(gpu):
 def test_kat_rows_through_writers(gpu):
     """TestSplitterStability parameterisations (splitter_test.go:30-39) with random slicing."""
     kat = coracle.gorand_read(5, 5_000_000)
-    for kind, avg, want in [(1, 32, (124235, 16, 64)), (1, 2048, (1924, 1024, 4096)), (2, 1024, (3771, 512, 2048))]:
+    rows = [(1, "buzhash", 32, (124235, 16, 64)), (1, "buzhash", 2048, (1924, 1024, 4096)),
+            (2, "rabinkarp", 1024, (3771, 512, 2048))]
+    for kind, oname, avg, want in rows:
         name = _lib.lib().kcdc_custom_algorithm(kind, avg).decode()
         b = WriterBatcher(name, round_bytes=1 << 20, max_wait_us=100)
         w = b.open()
         got = _feed(w, kat, "rand" if avg == 2048 else "64k", np.random.default_rng(avg))
         w.close()
         b.close()
-        assert got == coracle.split_stream(name, kat).tolist()
+        assert got == coracle.split_stream_kind(oname, avg, kat).tolist()
         sizes = np.diff([0] + got)
         assert (len(got), int(sizes[:-1].min()), int(sizes.max())) == want
 

@@ -1,5 +1,5 @@
 """Seal/open timing of a device encryptor (--algo) over a synthetic chunk table (A/B of
-library builds via KCDC_LIB; not a parity test -- tests/test_gpu_crypt.py is)."""
+library builds via KCDC_LIB (with KCDC_ALLOW_VARIANT_LIB=1); not a parity test -- tests/test_gpu_crypt.py is)."""
 import argparse
 import json
 import os

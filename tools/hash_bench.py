@@ -1,5 +1,5 @@
 """Content-hash timing on a synthetic chunk table shaped like one config-2 batch (A/B of
-library builds via KCDC_LIB; parity is tests/test_gpu_hash.py)."""
+library builds via KCDC_LIB (with KCDC_ALLOW_VARIANT_LIB=1); parity is tests/test_gpu_hash.py)."""
 import json
 import os
 import sys
