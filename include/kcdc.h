@@ -153,6 +153,9 @@ int64_t kcdc_bw_cuts(kcdc_bw* w, uint64_t* out, uint64_t cap); /* final cuts tak
 int kcdc_bw_finish(kcdc_bw* w);
 void kcdc_bw_free(kcdc_bw* w);
 int64_t kcdc_bw_rounds(const kcdc_bw_batcher* b); /* rounds shipped so far (test hook) */
+/* Observability: out[0..n) = rounds, bytes shipped, seconds the round thread spent issuing copies
+ * and launches, seconds it waited for the device.  Returns the number of values (4). */
+int kcdc_bw_stats(kcdc_bw_batcher* b, double* out, int n);
 
 /* ------------------------------------------------------ batch (hot path)
  * Split `nstreams` independent streams in one launch; every stream starts from

@@ -81,6 +81,7 @@ _SIGS = {
     "kcdc_bw_finish": (C.c_int, [_P]),
     "kcdc_bw_free": (None, [_P]),
     "kcdc_bw_rounds": (C.c_int64, [_P]),
+    "kcdc_bw_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_int]),
     "kcdc_test_set": (C.c_int, [C.c_int32, C.c_int64]),
     "kcdc_test_occupy": (C.c_int, [C.c_uint32, C.c_uint32, _P]),
     "kcdc_test_queue_stat": (C.c_int64, [C.c_int32]),

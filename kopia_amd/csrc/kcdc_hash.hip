@@ -419,6 +419,446 @@ __global__ __launch_bounds__(256) void blake2_chunks_x4_kernel(const uint8_t* da
     }
 }
 
+// ------------------------------------------------------------------ HMAC-SHA256 / HMAC-SHA224
+// repo/hashing/sha_hashes.go:10-12: hmac.New(sha256.New | sha256.New224, secret), truncated.
+// HMAC(K, m) = H(K0 ^ opad || H(K0 ^ ipad || m)) (RFC 2104, FIPS 198-1): the host compresses the
+// two key blocks once (ShaMid), so a chunk costs its own blocks plus one outer block.  One lane
+// per chunk: SHA-256's 64 rounds are one dependent chain (FIPS 180-4), no intra-block width.
+constexpr uint32_t kK256[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+    0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+    0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+    0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+
+struct ShaMid {
+    uint32_t in[8];   // state after the K0 ^ ipad block
+    uint32_t out[8];  // state after the K0 ^ opad block
+};
+
+__host__ __device__ __forceinline__ uint32_t ror32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+// One SHA-256 block (big-endian words already assembled in w).
+__host__ __device__ __forceinline__ void sha256_block(uint32_t (&h)[8], uint32_t (&w)[16]) {
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+    for (int r = 0; r < 64; r++) {
+        if (r >= 16) {
+            const uint32_t x = w[(r - 15) & 15], y = w[(r - 2) & 15];
+            w[r & 15] += (ror32(x, 7) ^ ror32(x, 18) ^ (x >> 3)) + w[(r - 7) & 15] + (ror32(y, 17) ^ ror32(y, 19) ^ (y >> 10));
+        }
+        const uint32_t t1 = hh + (ror32(e, 6) ^ ror32(e, 11) ^ ror32(e, 25)) + ((e & f) ^ (~e & g)) + kK256[r] + w[r & 15];
+        const uint32_t t2 = (ror32(a, 2) ^ ror32(a, 13) ^ ror32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+        hh = g;
+        g = f;
+        f = e;
+        e = d + t1;
+        d = c;
+        c = b;
+        b = a;
+        a = t1 + t2;
+    }
+    h[0] += a;
+    h[1] += b;
+    h[2] += c;
+    h[3] += d;
+    h[4] += e;
+    h[5] += f;
+    h[6] += g;
+    h[7] += hh;
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x00010203u); }
+
+// DW = digest words of the inner hash (8: SHA-256, 7: SHA-224).
+template <int DW>
+__global__ __launch_bounds__(256) void hmac_sha256_kernel(const uint8_t* data, const uint64_t* offs, const uint64_t* lens,
+                                                          const uint32_t* order, uint32_t n, ShaMid mid, uint32_t out_len,
+                                                          uint32_t out_stride, uint8_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = order ? order[i] : i;
+    const uint64_t len = lens[c];
+    const uint8_t* p = data + offs[c];
+    uint32_t h[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) h[j] = mid.in[j];
+    const uint64_t nfull = len / 64;
+    const uint32_t rem = static_cast<uint32_t>(len % 64);
+    uint32_t cur[16], nxt[16];
+    load_block<16>(p, nfull ? 64u : rem, cur);
+    for (uint64_t b = 0; b < nfull; b++) {  // block b+1 (or the tail) in flight while b is compressed
+        load_block<16>(p + 64 * (b + 1), b + 1 < nfull ? 64u : rem, nxt);
+#pragma unroll
+        for (int j = 0; j < 16; j++) cur[j] = bswap32(cur[j]);
+        sha256_block(h, cur);
+#pragma unroll
+        for (int j = 0; j < 16; j++) cur[j] = nxt[j];
+    }
+    // tail: rem bytes, 0x80, zeros, the 64-bit bit length of ipad block + message
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        if (static_cast<uint32_t>(j) == (rem >> 2)) cur[j] |= 0x80u << (8 * (rem & 3u));
+        cur[j] = bswap32(cur[j]);
+    }
+    const uint64_t bits = (len + 64) * 8;
+    if (rem >= 56) {
+        sha256_block(h, cur);
+#pragma unroll
+        for (int j = 0; j < 16; j++) cur[j] = 0;
+    }
+    cur[14] = static_cast<uint32_t>(bits >> 32);
+    cur[15] = static_cast<uint32_t>(bits);
+    sha256_block(h, cur);
+    // outer: K0 ^ opad (in mid.out) then the inner digest, 0x80, length (64 + 4 DW) * 8
+    uint32_t w[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) w[j] = j < DW ? h[j] : j == DW ? 0x80000000u : 0u;
+    w[15] = (64u + 4u * DW) * 8u;
+    uint32_t o2[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) o2[j] = mid.out[j];
+    sha256_block(o2, w);
+    uint32_t* o = reinterpret_cast<uint32_t*>(out + static_cast<uint64_t>(c) * out_stride);
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+        if (4u * j < out_len) o[j] = bswap32(o2[j]);
+}
+
+// ------------------------------------------------------------------ HMAC-SHA3-224 / -256
+// repo/hashing/sha_hashes.go:13-14: hmac.New(sha3.New224 | sha3.New256, secret); the HMAC block
+// is the sponge rate (144 / 136 bytes, FIPS 202; Go's sha3 BlockSize()).  The host absorbs the two
+// key blocks (KeccakMid); one lane per chunk runs Keccak-f[1600] on 25 x 64-bit lanes held as
+// 50 VGPR halves (rotations by constants are v_alignbit pairs, chi is v_bitop3).
+struct KeccakMid {
+    uint64_t in[25];
+    uint64_t out[25];
+};
+
+constexpr uint64_t kKeccakRC[24] = {
+    0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808Aull, 0x8000000080008000ull, 0x000000000000808Bull,
+    0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull, 0x000000000000008Aull, 0x0000000000000088ull,
+    0x0000000080008009ull, 0x000000008000000Aull, 0x000000008000808Bull, 0x800000000000008Bull, 0x8000000000008089ull,
+    0x8000000000008003ull, 0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800Aull, 0x800000008000000Aull,
+    0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+// rho offsets and pi destinations by lane index x + 5 y (FIPS 202 §3.2.2-3.2.3)
+constexpr int kKeccakRho[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+// pi: B[y, 2x + 3y] = rot(A[x, y]) -> destination index of source lane x + 5 y
+// pi: B[y, 2x + 3y] = rot(A[x, y], rho[x, y]): source lane x + 5 y -> destination y + 5 ((2x + 3y) mod 5)
+constexpr int keccak_pi_dst(int s) { return (s / 5) + 5 * ((2 * (s % 5) + 3 * (s / 5)) % 5); }
+
+// rotate left by n (a constant once the rounds are unrolled): v_alignbit pairs
+__device__ __forceinline__ uint64_t rotl64n(uint64_t x, int n) {
+    const uint32_t lo = static_cast<uint32_t>(x), hi = static_cast<uint32_t>(x >> 32);
+    uint32_t nlo, nhi;
+    if (n == 0) return x;
+    if (n == 32) {
+        nlo = hi;
+        nhi = lo;
+    } else if (n < 32) {
+        nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - n);
+        nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - n);
+    } else {
+        nhi = __builtin_amdgcn_alignbit(lo, hi, 64 - n);
+        nlo = __builtin_amdgcn_alignbit(hi, lo, 64 - n);
+    }
+    return (static_cast<uint64_t>(nhi) << 32) | nlo;
+}
+
+__device__ __forceinline__ void keccak_f(uint64_t (&s)[25]) {
+#pragma unroll
+    for (int r = 0; r < 24; r++) {
+        uint64_t C[5], D[5], B[25];
+#pragma unroll
+        for (int x = 0; x < 5; x++) C[x] = s[x] ^ s[x + 5] ^ s[x + 10] ^ s[x + 15] ^ s[x + 20];
+#pragma unroll
+        for (int x = 0; x < 5; x++) D[x] = C[(x + 4) % 5] ^ rotl64n(C[(x + 1) % 5], 1);
+#pragma unroll
+        for (int k = 0; k < 25; k++) B[keccak_pi_dst(k)] = rotl64n(s[k] ^ D[k % 5], kKeccakRho[k]);
+#pragma unroll
+        for (int y = 0; y < 25; y += 5) {
+#pragma unroll
+            for (int x = 0; x < 5; x++) s[y + x] = B[y + x] ^ (~B[y + (x + 1) % 5] & B[y + (x + 2) % 5]);
+        }
+        s[0] ^= kKeccakRC[r];
+    }
+}
+
+// RATE: sponge rate in bytes; DB: digest bytes of the inner hash.
+template <int RATE, int DB>
+__global__ __launch_bounds__(256) void hmac_sha3_kernel(const uint8_t* data, const uint64_t* offs, const uint64_t* lens,
+                                                        const uint32_t* order, uint32_t n, KeccakMid mid, uint32_t out_len,
+                                                        uint32_t out_stride, uint8_t* out) {
+    constexpr int NW = RATE / 4;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = order ? order[i] : i;
+    const uint64_t len = lens[c];
+    const uint8_t* p = data + offs[c];
+    uint64_t s[25];
+#pragma unroll
+    for (int j = 0; j < 25; j++) s[j] = mid.in[j];
+    const uint64_t nfull = len / RATE;
+    const uint32_t rem = static_cast<uint32_t>(len % RATE);
+    uint32_t cur[NW], nxt[NW];
+    load_block<NW>(p, nfull ? static_cast<uint32_t>(RATE) : rem, cur);
+    auto absorb = [&](const uint32_t (&w)[NW]) {
+#pragma unroll
+        for (int j = 0; j < NW / 2; j++) s[j] ^= static_cast<uint64_t>(w[2 * j]) | (static_cast<uint64_t>(w[2 * j + 1]) << 32);
+        keccak_f(s);
+    };
+    for (uint64_t b = 0; b < nfull; b++) {
+        load_block<NW>(p + static_cast<uint64_t>(RATE) * (b + 1), b + 1 < nfull ? static_cast<uint32_t>(RATE) : rem, nxt);
+        absorb(cur);
+#pragma unroll
+        for (int j = 0; j < NW; j++) cur[j] = nxt[j];
+    }
+    // pad10*1 with the SHA-3 domain bits: 0x06 after the message, 0x80 in the block's last byte
+#pragma unroll
+    for (int j = 0; j < NW; j++) {
+        if (static_cast<uint32_t>(j) == (rem >> 2)) cur[j] |= 0x06u << (8 * (rem & 3u));
+        if (j == NW - 1) cur[j] |= 0x80000000u;
+    }
+    absorb(cur);
+    // outer: the inner digest's DB bytes (little-endian lanes of s), then its padding
+    uint32_t w[NW];
+#pragma unroll
+    for (int j = 0; j < NW; j++) {
+        const uint32_t half = (j & 1) ? static_cast<uint32_t>(s[j / 2] >> 32) : static_cast<uint32_t>(s[j / 2]);
+        w[j] = 4 * j < DB ? half : 0u;
+        if (4 * j == DB) w[j] = 0x06u;
+        if (j == NW - 1) w[j] |= 0x80000000u;
+    }
+#pragma unroll
+    for (int j = 0; j < 25; j++) s[j] = mid.out[j];
+    absorb(w);
+    uint32_t* o = reinterpret_cast<uint32_t*>(out + static_cast<uint64_t>(c) * out_stride);
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+        if (4u * j < out_len) o[j] = (j & 1) ? static_cast<uint32_t>(s[j / 2] >> 32) : static_cast<uint32_t>(s[j / 2]);
+}
+
+// ------------------------------------------------------------------ BLAKE3 keyed hash
+// repo/hashing/blake3_hashes.go:10-27: blake3.NewKeyed(key) (github.com/zeebo/blake3, not
+// vendored), key = the 32-byte secret, or DeriveKey("kopia blake3 derived key v1", secret) for a
+// shorter one (host side, kcdc_hash_chunks_device).  BLAKE3 (the published spec): 1 KiB chunks
+// hashed independently (16 blocks, a 7-round BLAKE2s-like compression, counter = chunk index),
+// CVs merged in a left-complete binary tree of PARENT nodes; ROOT marks the last compression.
+// One wave per content: a round takes up to 256 chunks (4 per lane, in order), then merges their
+// CVs level by level in LDS; the level leftovers (odd counts) are the round's subtrees.  Full
+// rounds' 256-chunk subtrees go on a per-wave stack and merge as in the sequential algorithm;
+// the last round's subtrees are appended, and the stack is folded right to left at the end.
+// A merge is the ROOT when it covers every chunk of the content.
+constexpr uint32_t kB3ChunkStart = 1, kB3ChunkEnd = 2, kB3Parent = 4, kB3Root = 8, kB3Keyed = 16;
+constexpr int kB3Perm[16] = {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8};
+struct B3Sched {
+    int s[7][16];
+    constexpr B3Sched() : s{} {
+        for (int i = 0; i < 16; i++) s[0][i] = i;
+        for (int r = 1; r < 7; r++)
+            for (int i = 0; i < 16; i++) s[r][i] = s[r - 1][kB3Perm[i]];
+    }
+};
+constexpr B3Sched kB3S{};
+
+struct B3Key {
+    uint32_t k[8];
+};
+
+// Compression -> the 8-word chaining value (v[i] ^ v[i + 8]).
+__host__ __device__ __forceinline__ void b3_compress(const uint32_t (&cv)[8], const uint32_t (&m)[16], uint64_t t,
+                                                     uint32_t blen, uint32_t flags, uint32_t (&out)[8]) {
+    uint32_t v[16] = {cv[0], cv[1], cv[2], cv[3], cv[4], cv[5], cv[6], cv[7], kIV32[0], kIV32[1], kIV32[2], kIV32[3],
+                      static_cast<uint32_t>(t), static_cast<uint32_t>(t >> 32), blen, flags};
+    auto g = [](uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t x, uint32_t y) {
+        a = a + b + x;
+        d = ror32(d ^ a, 16);
+        c = c + d;
+        b = ror32(b ^ c, 12);
+        a = a + b + y;
+        d = ror32(d ^ a, 8);
+        c = c + d;
+        b = ror32(b ^ c, 7);
+    };
+#pragma unroll
+    for (int r = 0; r < 7; r++) {
+#define S3(i) m[kB3S.s[r][i]]
+        g(v[0], v[4], v[8], v[12], S3(0), S3(1));
+        g(v[1], v[5], v[9], v[13], S3(2), S3(3));
+        g(v[2], v[6], v[10], v[14], S3(4), S3(5));
+        g(v[3], v[7], v[11], v[15], S3(6), S3(7));
+        g(v[0], v[5], v[10], v[15], S3(8), S3(9));
+        g(v[1], v[6], v[11], v[12], S3(10), S3(11));
+        g(v[2], v[7], v[8], v[13], S3(12), S3(13));
+        g(v[3], v[4], v[9], v[14], S3(14), S3(15));
+#undef S3
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) out[i] = v[i] ^ v[i + 8];
+}
+
+constexpr int kB3PerLane = 4;                     // chunks per lane per round
+constexpr int kB3Round = 64 * kB3PerLane;         // chunks per round
+constexpr int kB3Stack = 48;                      // per-wave stack entries (2^48 rounds: never full)
+constexpr int kB3Waves = 4;                       // waves (contents) per workgroup
+
+struct B3Wave {
+    uint32_t x[kB3Round][8];   // the round's CVs, merged level by level in place
+    uint32_t st[kB3Stack][8];  // the stack's subtree CVs, left to right
+};
+
+__global__ __launch_bounds__(64 * kB3Waves) void blake3_keyed_kernel(const uint8_t* data, const uint64_t* offs,
+                                                                     const uint64_t* lens, const uint32_t* order,
+                                                                     uint32_t n, B3Key key, uint32_t out_len,
+                                                                     uint32_t out_stride, uint8_t* out) {
+    __shared__ B3Wave sw[kB3Waves];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t gi = blockIdx.x * kB3Waves + wv;
+    if (gi >= n) return;  // wave-uniform
+    B3Wave& W = sw[wv];
+    const uint32_t c = order ? order[gi] : gi;
+    const uint64_t len = lens[c];
+    const uint8_t* p = data + offs[c];
+    const uint64_t nch = len ? (len + 1023) / 1024 : 1;
+    uint32_t kcv[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) kcv[j] = key.k[j];
+    // chunk ch's CV (ROOT on its last block when it is the content's only chunk)
+    auto chunk_cv = [&](uint64_t ch, uint32_t (&cv)[8]) {
+        const uint64_t base = ch * 1024;
+        const uint64_t clen64 = len - base < 1024 ? len - base : 1024;
+        const uint32_t clen = static_cast<uint32_t>(clen64);
+        const uint32_t nb = clen ? (clen + 63) / 64 : 1;
+#pragma unroll
+        for (int j = 0; j < 8; j++) cv[j] = kcv[j];
+        uint32_t cur[16], nxt[16];
+        load_block<16>(p + base, clen < 64 ? clen : 64u, cur);
+        for (uint32_t b = 0; b < nb; b++) {
+            const uint32_t take = clen - 64 * b < 64 ? clen - 64 * b : 64u;
+            if (b + 1 < nb) {
+                const uint32_t tn = clen - 64 * (b + 1);
+                load_block<16>(p + base + 64 * (b + 1), tn < 64 ? tn : 64u, nxt);
+            }
+            const uint32_t fl = kB3Keyed | (b == 0 ? kB3ChunkStart : 0u) |
+                                (b + 1 == nb ? (kB3ChunkEnd | (nch == 1 ? kB3Root : 0u)) : 0u);
+            uint32_t o[8];
+            b3_compress(cv, cur, ch, take, fl, o);
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                cv[j] = o[j];
+                cur[j] = nxt[j];
+                cur[j + 8] = nxt[j + 8];
+            }
+        }
+    };
+    auto parent = [&](const uint32_t* l, const uint32_t* r, bool root, uint32_t (&o)[8]) {
+        uint32_t m[16];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            m[j] = l[j];
+            m[j + 8] = r[j];
+        }
+        b3_compress(kcv, m, 0, 64, kB3Keyed | kB3Parent | (root ? kB3Root : 0u), o);
+    };
+    if (nch == 1) {
+        if (lane == 0) {
+            uint32_t cv[8];
+            chunk_cv(0, cv);
+            uint32_t* o = reinterpret_cast<uint32_t*>(out + static_cast<uint64_t>(c) * out_stride);
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                if (4u * j < out_len) o[j] = cv[j];
+        }
+        return;
+    }
+    uint32_t* const o = reinterpret_cast<uint32_t*>(out + static_cast<uint64_t>(c) * out_stride);
+    uint32_t sdepth = 0;  // entries on the wave's stack (W.st), wave-uniform
+    const uint64_t rounds = (nch + kB3Round - 1) / kB3Round;
+    for (uint64_t rd = 0; rd < rounds; rd++) {
+        const uint64_t c0 = rd * kB3Round;
+        const uint32_t cnt = static_cast<uint32_t>(nch - c0 < static_cast<uint64_t>(kB3Round) ? nch - c0 : kB3Round);
+        for (int q = 0; q < kB3PerLane; q++) {  // lane: chunks [4 lane, 4 lane + 4) of the round
+            const uint32_t k = kB3PerLane * lane + q;
+            if (k < cnt) {
+                uint32_t cv[8];
+                chunk_cv(c0 + k, cv);
+#pragma unroll
+                for (int j = 0; j < 8; j++) W.x[k][j] = cv[j];
+            }
+        }
+        wave_lds_fence();
+        // level L holds floor(cnt / 2^L) items at stride 2^L; an odd count leaves its last item
+        // (slot (count - 1) 2^L) as one of the round's subtrees
+        uint32_t count = cnt, stride = 1;
+        bool lower_left = false;  // a lower level left a subtree over
+        while (count > 1) {
+            const uint32_t pairs = count / 2;
+            const bool whole = cnt == nch && count == 2 && !lower_left;  // this merge covers the content
+            for (uint32_t pr = lane; pr < pairs; pr += 64) {
+                uint32_t h[8];
+                parent(W.x[2 * pr * stride], W.x[(2 * pr + 1) * stride], whole, h);
+#pragma unroll
+                for (int j = 0; j < 8; j++) W.x[2 * pr * stride][j] = h[j];
+            }
+            wave_lds_fence();
+            if (whole) {  // the content is one power-of-two round: x[0] is the root's output
+                if (lane < 8 && 4u * lane < out_len) o[lane] = W.x[0][lane];
+                return;
+            }
+            lower_left = lower_left || (count & 1u);
+            count = pairs;
+            stride *= 2;
+        }
+        if (c0 + cnt < nch) {
+            // a full, non-final round: its 256-chunk subtree (slot 0) goes on the stack, merging
+            // equal sizes as the sequential algorithm does (rounds done = rd + 1, while even);
+            // never the root, since chunks remain
+            if (lane < 8) W.st[sdepth][lane] = W.x[0][lane];
+            sdepth++;
+            wave_lds_fence();
+            for (uint64_t t = rd + 1; (t & 1u) == 0; t >>= 1) {
+                uint32_t h[8];
+                parent(W.st[sdepth - 2], W.st[sdepth - 1], false, h);
+                wave_lds_fence();
+                if (lane == 0) {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) W.st[sdepth - 2][j] = h[j];
+                }
+                sdepth--;
+                wave_lds_fence();
+            }
+            continue;
+        }
+        // the final round: append its subtrees left to right (highest level first), then fold
+        // the stack right to left; the last merge is the root
+        for (int L = 31; L >= 0; L--) {
+            const uint32_t cL = cnt >> L;
+            if (cL & 1u) {
+                if (lane < 8) W.st[sdepth][lane] = W.x[(cL - 1) << L][lane];
+                sdepth++;
+            }
+        }
+        wave_lds_fence();
+        uint32_t acc[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) acc[j] = W.st[sdepth - 1][j];
+        for (int e = static_cast<int>(sdepth) - 2; e >= 0; e--) {
+            uint32_t h[8];
+            parent(W.st[e], acc, e == 0, h);
+#pragma unroll
+            for (int j = 0; j < 8; j++) acc[j] = h[j];
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 0; j < 8; j++)
+                if (4u * j < out_len) o[j] = acc[j];
+        }
+    }
+}
+
 }  // namespace hashdev
 
 int& test_hash_lanes() {  // kcdc_test_set(KCDC_TEST_HASH_LANES): 0 auto, 1 or 4 lanes per chunk
@@ -427,24 +867,164 @@ int& test_hash_lanes() {  // kcdc_test_set(KCDC_TEST_HASH_LANES): 0 auto, 1 or 4
 }
 
 namespace {
+enum class HashKind { Blake2b, Blake2s, HmacSha256, HmacSha224, HmacSha3_224, HmacSha3_256, Blake3 };
 struct HashAlgo {
     const char* name;
-    bool b64;       // BLAKE2b (else BLAKE2s)
-    uint32_t nn;    // digest length parameter
-    uint32_t out;   // bytes kept (truncation)
+    HashKind kind;
+    uint32_t nn;   // BLAKE2 digest length parameter
+    uint32_t out;  // bytes kept (truncation)
 };
-// repo/hashing/blake_hashes.go:8-13 (registered names and their truncation)
+// repo/hashing/{blake_hashes.go:8-13, blake3_hashes.go:24-27, sha_hashes.go:9-15}: every registered
+// name, in the order hashing.SupportedAlgorithms() returns them (sort.Strings, hashing.go:40-49)
 constexpr HashAlgo kHashAlgos[] = {
-    {"BLAKE2B-256-128", true, 32, 16},
-    {"BLAKE2B-256", true, 32, 32},
-    {"BLAKE2S-128", false, 16, 16},
-    {"BLAKE2S-256", false, 32, 32},
+    {"BLAKE2B-256", HashKind::Blake2b, 32, 32},
+    {"BLAKE2B-256-128", HashKind::Blake2b, 32, 16},
+    {"BLAKE2S-128", HashKind::Blake2s, 16, 16},
+    {"BLAKE2S-256", HashKind::Blake2s, 32, 32},
+    {"BLAKE3-256", HashKind::Blake3, 32, 32},
+    {"BLAKE3-256-128", HashKind::Blake3, 32, 16},
+    {"HMAC-SHA224", HashKind::HmacSha224, 0, 28},
+    {"HMAC-SHA256", HashKind::HmacSha256, 0, 32},
+    {"HMAC-SHA256-128", HashKind::HmacSha256, 0, 16},
+    {"HMAC-SHA3-224", HashKind::HmacSha3_224, 0, 28},
+    {"HMAC-SHA3-256", HashKind::HmacSha3_256, 0, 32},
 };
 const HashAlgo* find_hash(const char* name) {
     if (!name) return nullptr;
     for (const HashAlgo& h : kHashAlgos)
         if (std::strcmp(h.name, name) == 0) return &h;
     return nullptr;
+}
+
+// ---- host-side key preparation (per launch, a few blocks): HMAC midstates, BLAKE3 key derivation
+constexpr uint32_t kSha256IV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                   0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+constexpr uint32_t kSha224IV[8] = {0xc1059ed8u, 0x367cd507u, 0x3070dd17u, 0xf70e5939u,
+                                   0xffc00b31u, 0x68581511u, 0x64f98fa7u, 0xbefa4fa4u};
+
+void sha256_block_bytes(uint32_t (&h)[8], const uint8_t* b) {
+    uint32_t w[16];
+    for (int j = 0; j < 16; j++)
+        w[j] = (uint32_t(b[4 * j]) << 24) | (uint32_t(b[4 * j + 1]) << 16) | (uint32_t(b[4 * j + 2]) << 8) | b[4 * j + 3];
+    hashdev::sha256_block(h, w);
+}
+
+// SHA-256 / SHA-224 of a short message (a long HMAC key): FIPS 180-4 padding.
+void sha2_host(bool is224, const uint8_t* m, size_t n, uint8_t* digest) {
+    uint32_t h[8];
+    for (int j = 0; j < 8; j++) h[j] = is224 ? kSha224IV[j] : kSha256IV[j];
+    size_t i = 0;
+    for (; i + 64 <= n; i += 64) sha256_block_bytes(h, m + i);
+    uint8_t blk[128] = {};
+    const size_t r = n - i;
+    std::memcpy(blk, m + i, r);
+    blk[r] = 0x80;
+    const size_t tot = r < 56 ? 64 : 128;
+    const uint64_t bits = static_cast<uint64_t>(n) * 8;
+    for (int j = 0; j < 8; j++) blk[tot - 1 - j] = static_cast<uint8_t>(bits >> (8 * j));
+    sha256_block_bytes(h, blk);
+    if (tot == 128) sha256_block_bytes(h, blk + 64);
+    const int dw = is224 ? 7 : 8;
+    for (int j = 0; j < dw; j++)
+        for (int k = 0; k < 4; k++) digest[4 * j + k] = static_cast<uint8_t>(h[j] >> (24 - 8 * k));
+}
+
+void keccak_f_host(uint64_t (&s)[25]) {
+    for (int r = 0; r < 24; r++) {
+        uint64_t C[5], D[5], B[25];
+        for (int x = 0; x < 5; x++) C[x] = s[x] ^ s[x + 5] ^ s[x + 10] ^ s[x + 15] ^ s[x + 20];
+        for (int x = 0; x < 5; x++) D[x] = C[(x + 4) % 5] ^ ((C[(x + 1) % 5] << 1) | (C[(x + 1) % 5] >> 63));
+        for (int k = 0; k < 25; k++) {
+            const uint64_t v = s[k] ^ D[k % 5];
+            const int rho = hashdev::kKeccakRho[k];
+            B[hashdev::keccak_pi_dst(k)] = rho ? (v << rho) | (v >> (64 - rho)) : v;
+        }
+        for (int y = 0; y < 25; y += 5)
+            for (int x = 0; x < 5; x++) s[y + x] = B[y + x] ^ (~B[y + (x + 1) % 5] & B[y + (x + 2) % 5]);
+        s[0] ^= hashdev::kKeccakRC[r];
+    }
+}
+void keccak_absorb_block(uint64_t (&s)[25], const uint8_t* b, size_t rate) {
+    for (size_t j = 0; j < rate / 8; j++) {
+        uint64_t w = 0;
+        for (int k = 0; k < 8; k++) w |= static_cast<uint64_t>(b[8 * j + k]) << (8 * k);
+        s[j] ^= w;
+    }
+    keccak_f_host(s);
+}
+// SHA3-224 / SHA3-256 of a short message (a long HMAC key): FIPS 202.
+void sha3_host(size_t rate, size_t db, const uint8_t* m, size_t n, uint8_t* digest) {
+    uint64_t s[25] = {};
+    size_t i = 0;
+    for (; i + rate <= n; i += rate) keccak_absorb_block(s, m + i, rate);
+    uint8_t blk[200] = {};
+    std::memcpy(blk, m + i, n - i);
+    blk[n - i] ^= 0x06;
+    blk[rate - 1] ^= 0x80;
+    keccak_absorb_block(s, blk, rate);
+    for (size_t k = 0; k < db; k++) digest[k] = static_cast<uint8_t>(s[k / 8] >> (8 * (k % 8)));
+}
+
+// HMAC key block K0 (RFC 2104 / FIPS 198-1): the key, hashed first when longer than the block.
+void hmac_k0(const HashAlgo& h, const uint8_t* key, uint32_t key_len, size_t block, uint8_t* k0) {
+    std::memset(k0, 0, block);
+    if (key_len <= block) {
+        if (key_len) std::memcpy(k0, key, key_len);
+        return;
+    }
+    switch (h.kind) {
+        case HashKind::HmacSha256: sha2_host(false, key, key_len, k0); break;
+        case HashKind::HmacSha224: sha2_host(true, key, key_len, k0); break;
+        case HashKind::HmacSha3_224: sha3_host(144, 28, key, key_len, k0); break;
+        default: sha3_host(136, 32, key, key_len, k0); break;
+    }
+}
+
+// BLAKE3 (host, short inputs): the hash of `m` under key words `kw` and mode flags `mode`
+// (KEYED_HASH, DERIVE_KEY_CONTEXT, DERIVE_KEY_MATERIAL); recursive left-complete tree.
+void b3_words(const uint8_t* b, uint32_t len, uint32_t (&m)[16]) {
+    for (int j = 0; j < 16; j++) {
+        m[j] = 0;
+        for (int k = 0; k < 4; k++)
+            if (4u * j + k < len) m[j] |= static_cast<uint32_t>(b[4 * j + k]) << (8 * k);
+    }
+}
+void b3_chunk_host(const uint32_t (&kw)[8], const uint8_t* m, size_t n, uint64_t ctr, uint32_t mode, bool root,
+                   uint32_t (&cv)[8]) {
+    for (int j = 0; j < 8; j++) cv[j] = kw[j];
+    const size_t nb = n ? (n + 63) / 64 : 1;
+    for (size_t b = 0; b < nb; b++) {
+        const uint32_t take = static_cast<uint32_t>(n - 64 * b < 64 ? n - 64 * b : 64);
+        uint32_t w[16], o[8];
+        b3_words(m + 64 * b, take, w);
+        const uint32_t fl = mode | (b == 0 ? hashdev::kB3ChunkStart : 0u) |
+                            (b + 1 == nb ? (hashdev::kB3ChunkEnd | (root ? hashdev::kB3Root : 0u)) : 0u);
+        hashdev::b3_compress(cv, w, ctr, take, fl, o);
+        for (int j = 0; j < 8; j++) cv[j] = o[j];
+    }
+}
+void b3_subtree_host(const uint32_t (&kw)[8], const uint8_t* m, size_t n, uint64_t ctr0, uint32_t mode, bool root,
+                     uint32_t (&cv)[8]) {
+    const size_t nch = n ? (n + 1023) / 1024 : 1;
+    if (nch == 1) return b3_chunk_host(kw, m, n, ctr0, mode, root, cv);
+    size_t left = 1;
+    while (2 * left < nch) left *= 2;  // the largest power of two below nch chunks
+    uint32_t l[8], r[8], w[16];
+    b3_subtree_host(kw, m, 1024 * left, ctr0, mode, false, l);
+    b3_subtree_host(kw, m + 1024 * left, n - 1024 * left, ctr0 + left, mode, false, r);
+    for (int j = 0; j < 8; j++) {
+        w[j] = l[j];
+        w[8 + j] = r[j];
+    }
+    hashdev::b3_compress(kw, w, 0, 64, mode | hashdev::kB3Parent | (root ? hashdev::kB3Root : 0u), cv);
+}
+constexpr uint32_t kB3DeriveContext = 32, kB3DeriveMaterial = 64;
+// blake3.DeriveKey(context, material, out[:32])
+void b3_derive_key(const char* context, const uint8_t* material, size_t n, uint32_t (&key)[8]) {
+    uint32_t iv[8], ck[8];
+    for (int j = 0; j < 8; j++) iv[j] = hashdev::kIV32[j];
+    b3_subtree_host(iv, reinterpret_cast<const uint8_t*>(context), std::strlen(context), 0, kB3DeriveContext, true, ck);
+    b3_subtree_host(ck, material, n, 0, kB3DeriveMaterial, true, key);
 }
 }  // namespace
 }  // namespace kcdc
@@ -468,17 +1048,85 @@ extern "C" int kcdc_hash_chunks_device(const char* name, const uint8_t* d_data, 
                                        void* stream) {
     const HashAlgo* h = find_hash(name);
     if (!h) return set_error(-2, std::string("unknown hash: ") + (name ? name : "(null)"));
-    // blake2b.New256 / blake2s.New*: at most 64 / 32 key bytes; BLAKE2s-128 needs a key
-    // (golang.org/x/crypto/blake2s New128 rejects an empty one), as CreateHashFunc reports.
-    if (key_len > (h->b64 ? 64u : 32u) || (key_len && !key)) return set_error(-22, "hash key too long");
-    if (!h->b64 && h->nn == 16 && key_len == 0) return set_error(-22, "BLAKE2S-128 requires a key");
+    const bool blake2 = h->kind == HashKind::Blake2b || h->kind == HashKind::Blake2s;
+    if (key_len && !key) return set_error(-22, "null key");
+    if (blake2) {
+        // blake2b.New256 / blake2s.New*: at most 64 / 32 key bytes; BLAKE2s-128 needs a key
+        // (golang.org/x/crypto/blake2s New128 rejects an empty one), as CreateHashFunc reports.
+        if (key_len > (h->kind == HashKind::Blake2b ? 64u : 32u)) return set_error(-22, "hash key too long");
+        if (h->kind == HashKind::Blake2s && h->nn == 16 && key_len == 0)
+            return set_error(-22, "BLAKE2S-128 requires a key");
+    }
     if (out_stride < h->out || out_stride % 4) return set_error(-22, "out_stride must be >= the hash size and a multiple of 4");
     if (nchunks == 0) return 0;
     if (!d_data || !d_offsets || !d_lens || !d_out) return set_error(-22, "null argument");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const dim3 block(256), grid((nchunks + 255) / 256);
+    auto launched = [&]() {
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : set_error(-5, std::string("hash kernel launch: ") + hipGetErrorString(e));
+    };
+    switch (h->kind) {
+        case HashKind::HmacSha256:
+        case HashKind::HmacSha224: {
+            const bool is224 = h->kind == HashKind::HmacSha224;
+            uint8_t k0[64], pad[64];
+            hmac_k0(*h, key, key_len, 64, k0);
+            hashdev::ShaMid mid{};
+            for (int j = 0; j < 8; j++) mid.in[j] = mid.out[j] = is224 ? kSha224IV[j] : kSha256IV[j];
+            for (int j = 0; j < 64; j++) pad[j] = k0[j] ^ 0x36u;
+            sha256_block_bytes(mid.in, pad);
+            for (int j = 0; j < 64; j++) pad[j] = k0[j] ^ 0x5cu;
+            sha256_block_bytes(mid.out, pad);
+            if (is224)
+                hipLaunchKernelGGL(hashdev::hmac_sha256_kernel<7>, grid, block, 0, st, d_data, d_offsets, d_lens, d_order,
+                                   nchunks, mid, h->out, out_stride, d_out);
+            else
+                hipLaunchKernelGGL(hashdev::hmac_sha256_kernel<8>, grid, block, 0, st, d_data, d_offsets, d_lens, d_order,
+                                   nchunks, mid, h->out, out_stride, d_out);
+            return launched();
+        }
+        case HashKind::HmacSha3_224:
+        case HashKind::HmacSha3_256: {
+            const bool is224 = h->kind == HashKind::HmacSha3_224;
+            const size_t rate = is224 ? 144 : 136;
+            uint8_t k0[144], pad[144];
+            hmac_k0(*h, key, key_len, rate, k0);
+            hashdev::KeccakMid mid{};
+            for (size_t j = 0; j < rate; j++) pad[j] = k0[j] ^ 0x36u;
+            keccak_absorb_block(mid.in, pad, rate);
+            for (size_t j = 0; j < rate; j++) pad[j] = k0[j] ^ 0x5cu;
+            keccak_absorb_block(mid.out, pad, rate);
+            if (is224)
+                hipLaunchKernelGGL((hashdev::hmac_sha3_kernel<144, 28>), grid, block, 0, st, d_data, d_offsets, d_lens,
+                                   d_order, nchunks, mid, h->out, out_stride, d_out);
+            else
+                hipLaunchKernelGGL((hashdev::hmac_sha3_kernel<136, 32>), grid, block, 0, st, d_data, d_offsets, d_lens,
+                                   d_order, nchunks, mid, h->out, out_stride, d_out);
+            return launched();
+        }
+        case HashKind::Blake3: {
+            // blake3_hashes.go:10-22: a secret under 32 bytes is stretched with DeriveKey; otherwise
+            // its first 32 bytes are the key
+            hashdev::B3Key k{};
+            if (key_len < 32) {
+                b3_derive_key("kopia blake3 derived key v1", key, key_len, k.k);
+            } else {
+                for (int j = 0; j < 8; j++)
+                    k.k[j] = uint32_t(key[4 * j]) | (uint32_t(key[4 * j + 1]) << 8) | (uint32_t(key[4 * j + 2]) << 16) |
+                             (uint32_t(key[4 * j + 3]) << 24);
+            }
+            const dim3 g3((nchunks + hashdev::kB3Waves - 1) / hashdev::kB3Waves), b3(64 * hashdev::kB3Waves);
+            hipLaunchKernelGGL(hashdev::blake3_keyed_kernel, g3, b3, 0, st, d_data, d_offsets, d_lens, d_order, nchunks,
+                               k, h->out, out_stride, d_out);
+            return launched();
+        }
+        default: break;
+    }
     hashdev::HashKey k{};
     k.kk = key_len;
     for (uint32_t i = 0; i < key_len; i++) k.w[i / 4] |= static_cast<uint32_t>(key[i]) << (8 * (i % 4));
-    hipStream_t st = static_cast<hipStream_t>(stream);
+    const bool b64 = h->kind == HashKind::Blake2b;
     // Four lanes per chunk unless the launch holds over 2^20 chunks (64 waves per SIMD, where
     // the one-lane kernel's ~25 % lower VALU per block would matter).  Measured on config-2
     // chunk tables: 5,705 chunks 84 vs 540 ms, 136,920 chunks 263 vs 630 ms (one lane per
@@ -487,22 +1135,19 @@ extern "C" int kcdc_hash_chunks_device(const char* name, const uint8_t* d_data, 
     const bool x4 = forced ? forced == 4 : nchunks <= (1u << 20);
     if (x4) {
         const dim3 grid4((4ull * nchunks + 255) / 256), block4(256);
-        if (h->b64)
+        if (b64)
             hipLaunchKernelGGL(hashdev::blake2_chunks_x4_kernel<true>, grid4, block4, 0, st, d_data, d_offsets, d_lens,
                                d_order, nchunks, k, h->nn, h->out, out_stride, d_out);
         else
             hipLaunchKernelGGL(hashdev::blake2_chunks_x4_kernel<false>, grid4, block4, 0, st, d_data, d_offsets, d_lens,
                                d_order, nchunks, k, h->nn, h->out, out_stride, d_out);
-        const hipError_t e4 = hipGetLastError();
-        return e4 == hipSuccess ? 0 : set_error(-5, std::string("hash kernel launch: ") + hipGetErrorString(e4));
+        return launched();
     }
-    const dim3 grid((nchunks + 255) / 256), block(256);
-    if (h->b64)
+    if (b64)
         hipLaunchKernelGGL(hashdev::blake2b_chunks_kernel, grid, block, 0, st, d_data, d_offsets, d_lens, d_order, nchunks,
                            k, h->nn, h->out, out_stride, d_out);
     else
         hipLaunchKernelGGL(hashdev::blake2s_chunks_kernel, grid, block, 0, st, d_data, d_offsets, d_lens, d_order, nchunks,
                            k, h->nn, h->out, out_stride, d_out);
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? 0 : set_error(-5, std::string("hash kernel launch: ") + hipGetErrorString(e));
+    return launched();
 }

@@ -851,6 +851,13 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 struct DmaSlots {
     __attribute__((aligned(16))) uint8_t b[kDmaWaves][1][kSlotBytes];
 };
+#ifndef KCDC_RK_WAVES
+#define KCDC_RK_WAVES KCDC_DMA_WAVES
+#endif
+constexpr int kRkWaves = KCDC_RK_WAVES;  // waves per workgroup of the Rabin-Karp DMA kernels
+struct RkSlots {
+    __attribute__((aligned(16))) uint8_t b[kRkWaves][1][kSlotBytes];
+};
 
 // One LDS-DMA wave instruction (64 lanes x 16 B -> 1 KiB at LDS address m0), written as
 // inline asm so the waitcnt pass does not see an LDS-DMA: with several DMA sites and slots
@@ -1870,7 +1877,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
 //   D     drain: B's last 64 bytes (no fill: the slot takes the next tile's warm fill, or
 //         the next stream's queue entry).
 #ifndef KCDC_RK_2STEP
-#define KCDC_RK_2STEP 1  // 1: two bytes per chain hop (rk2_pair); 0: one byte per hop (round 2)
+#define KCDC_RK_2STEP 0  // 1: two bytes per chain hop (slower: 2.94 vs 2.51 ms, config 2); 0: one byte per hop
 #endif
 #if KCDC_RK_2STEP
 #ifndef KCDC_RK2_T
@@ -1900,7 +1907,7 @@ struct RkTables {
     uint32_t q[256 * 32];  // test family: row i (128 B), slots 0..15 (a x^53).lo, 16..31 outx[i].lo
     uint64_t m[256 * 32];  // main family: row i (256 B), slots 8t..8t+7 table t = T_lo, T_hi, O16, outx
 };
-static_assert(sizeof(RkTables) + sizeof(DmaSlots) <= 160 * 1024, "Rabin-Karp tables + step slots exceed LDS");
+static_assert(sizeof(RkTables) + sizeof(RkSlots) <= 160 * 1024, "Rabin-Karp tables + step slots exceed LDS");
 
 struct RkCtx {
     const char* qb;     // LDS byte address of RkTables::q
@@ -2102,12 +2109,15 @@ __device__ __forceinline__ void rk_warm(const RkCtx& kx, const uint32_t (&dw)[32
                            // but a 2-op out[] address: 3.01 vs 2.80 ms on config 2 (issue-bound)
 #endif
 constexpr int kRkModRep = KCDC_RK_MODREP;
-constexpr int kRkOutRep = 48 - kRkModRep;  // out[] gets the rest of the 96 KiB
+#ifndef KCDC_RK_OUTREP
+#define KCDC_RK_OUTREP (48 - KCDC_RK_MODREP)  // out[] gets the rest of the 96 KiB
+#endif
+constexpr int kRkOutRep = KCDC_RK_OUTREP;
 struct RkTables {
     uint64_t mod[256 * kRkModRep];  // mod[i*R + r]: first, so its addresses fit the 16-bit ds offset
     uint64_t out[256 * kRkOutRep];  // outx[b*R' + r] (rk_roll: out[] pre-shifted and pre-reduced)
 };
-static_assert(sizeof(RkTables) + sizeof(DmaSlots) <= 160 * 1024, "Rabin-Karp tables + step slots exceed LDS");
+static_assert(sizeof(RkTables) + sizeof(RkSlots) <= 160 * 1024, "Rabin-Karp tables + step slots exceed LDS");
 constexpr uint32_t kRkIdxBit = 13;  // u >> 45 = bits 13..20 of the high word (deg P = 53, host-checked)
 
 struct RkCtx {
@@ -2473,9 +2483,9 @@ __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int 
     }
 }
 
-__global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_rk_kernel(BatchArgs a) {
+__global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk_kernel(BatchArgs a) {
     __shared__ RkTables smt;
-    __shared__ DmaSlots smslots;
+    __shared__ RkSlots smslots;
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const RkCtx kx = rk_setup(smt, a, lane);
@@ -2494,7 +2504,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                 backlog = static_cast<int64_t>(ht >> 32) - static_cast<int64_t>(t) - 1;
             }
             const uint32_t held = t;
-            const int r = presolve(a, lane, held, cur, kDmaWaves);
+            const int r = presolve(a, lane, held, cur, kRkWaves);
             if (r == 0) return false;
             t = 0xFFFFFFFFu;
             if (claim != 0xFFFFFFFFu) {
@@ -2523,8 +2533,8 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             __hip_atomic_compare_exchange_strong((gu32*)(a.queue + kQFlags + blockIdx.x), &claim, 1u,
                                                  __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        const uint32_t gw0 = blockIdx.x * kDmaWaves + wave;
-        const int64_t nw = static_cast<int64_t>(gridDim.x) * kDmaWaves;
+        const uint32_t gw0 = blockIdx.x * kRkWaves + wave;
+        const int64_t nw = static_cast<int64_t>(gridDim.x) * kRkWaves;
         take_t = gw0 < a.nstreams ? gw0 : 0xFFFFFFFFu;
         take_backlog = static_cast<int64_t>(a.nstreams) - nw;
         take_claim = gw0 < a.nstreams ? (claim & 3u) : 0xFFFFFFFFu;
@@ -3135,15 +3145,15 @@ __global__ __launch_bounds__(kScanWaves * kWave, 2) void cand_scan_kernel(BatchA
 // chains per lane, alternating 128-byte line fills, outx[] folding): one 128 KiB segment per
 // tile, persistent grid-stride over the segments of every stream of the launch, the next
 // segment's warm fill issued during the drain step.  Records what cand_scan_kernel records.
-__global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void cand_scan_rk_kernel(BatchArgs a, LongArgs g) {
+__global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void cand_scan_rk_kernel(BatchArgs a, LongArgs g) {
     __shared__ RkTables smt;
-    __shared__ DmaSlots smslots;
+    __shared__ RkSlots smslots;
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const RkCtx kx = rk_setup(smt, a, lane);
     uint8_t* sl = smslots.b[wave][0];
     const uint32_t sl32 = lds_addr(sl);
-    const int64_t nw = static_cast<int64_t>(gridDim.x) * kDmaWaves;
+    const int64_t nw = static_cast<int64_t>(gridDim.x) * kRkWaves;
     struct Seg {
         const uint8_t* abase;
         int64_t off0, n, cs, lo, hi;
@@ -3163,7 +3173,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void cand_scan_rk
         const RkGeom t = rk_geom(q.cs, q.hi, q.abase, q.off0, q.off0 + q.n);
         rk_dma_warm(t.ld, sl32, q.cs, t.L, lane);
     };
-    int64_t seg = static_cast<int64_t>(blockIdx.x) * kDmaWaves + wave;
+    int64_t seg = static_cast<int64_t>(blockIdx.x) * kRkWaves + wave;
     if (seg >= g.nseg) return;
     Seg q = seg_of(seg);
     issue(q);
@@ -3898,7 +3908,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         const bool dma = (algo.kind == kBuzhash || (algo.kind == kRabinKarp && KCDC_RK_PIPE)) && KCDC_DMA;
         if (algo.kind == kRabinKarp && dma && tables().rk_shift != 45)
             return set_error(-22, "Rabin-Karp kernel: the polynomial must have degree 53");
-        const unsigned wg_waves = dma ? dev::kDmaWaves : dev::kBatchWaves;
+        const unsigned wg_waves = !dma ? dev::kBatchWaves : algo.kind == kRabinKarp ? dev::kRkWaves : dev::kDmaWaves;
         const unsigned need = (s.nstreams + wg_waves - 1) / wg_waves;
         unsigned grid = need < cus ? need : cus;
         if (dma && grid > dev::kMaxPipeGrid) grid = dev::kMaxPipeGrid;  // one claim flag per workgroup
@@ -3973,7 +3983,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         }
         // persistent grid: one workgroup per CU, never more workgroups than the streams need
         if (dma && algo.kind == kRabinKarp) {
-            hipLaunchKernelGGL(dev::split_batch_rk_kernel, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0, st, a);
+            hipLaunchKernelGGL(dev::split_batch_rk_kernel, dim3(grid), dim3(dev::kRkWaves * dev::kWave), 0, st, a);
             if (g_test.force_error)
                 hipLaunchKernelGGL(dev::poison_counts_kernel, dim3(std::min<unsigned>((s.nstreams + 255) / 256, 256u)),
                                    dim3(256), 0, st, a);
@@ -4301,8 +4311,8 @@ int launch_split_long_multi(const Algo& algo, uint32_t m, const uint8_t* const* 
                 hipLaunchKernelGGL(dev::cand_scan_dma_kernel<false>, pgrid, dim3(dev::kDmaWaves * dev::kWave), 0, st, a, g);
         } else if (algo.kind == kRabinKarp && KCDC_RK_PIPE) {  // two-chain LDS-DMA tiles, persistent
             const dim3 pgrid(static_cast<unsigned>(
-                std::min<int64_t>(t->cus, (nseg + dev::kDmaWaves - 1) / dev::kDmaWaves)));
-            hipLaunchKernelGGL(dev::cand_scan_rk_kernel, pgrid, dim3(dev::kDmaWaves * dev::kWave), 0, st, a, g);
+                std::min<int64_t>(t->cus, (nseg + dev::kRkWaves - 1) / dev::kRkWaves)));
+            hipLaunchKernelGGL(dev::cand_scan_rk_kernel, pgrid, dim3(dev::kRkWaves * dev::kWave), 0, st, a, g);
         } else if (algo.kind == kBuzhash) {
             hipLaunchKernelGGL(dev::cand_scan_kernel<kBuzhash>, grid, block, 0, st, a, g);
         } else {

@@ -67,7 +67,12 @@ struct kcdc_bw_batcher {
     std::vector<kcdc_bw*> open;        // writers not yet freed
     std::vector<uint8_t*> pool;        // free pinned blocks
     uint64_t staged = 0;               // unshipped bytes over all writers
+    std::chrono::steady_clock::time_point since;  // when `staged` last became nonzero
+    uint32_t capped = 0;               // writers blocked on their staging cap (a round is due)
     uint64_t rounds = 0;
+    // observability (kcdc_bw_stats): bytes shipped, seconds in the round thread's phases
+    uint64_t shipped_bytes = 0;
+    double t_submit = 0, t_wait = 0;
     bool stop = false;
     int error = 0;
     std::string errmsg;
@@ -151,11 +156,13 @@ int kcdc_bw_batcher::run_round(std::unique_lock<std::mutex>& lk) {
     cv_done.notify_all();  // writers blocked on their staging cap may continue
 
     int rc = KCDC_OK;
-    uint64_t total = 0;
+    uint64_t total = 0, fresh = 0;
     for (Job& j : jobs) {
         j.off = total;
         total += align16(j.tail_len + j.new_bytes);
+        fresh += j.new_bytes;
     }
+    const auto t0 = std::chrono::steady_clock::now();
     const int nxt = cur ^ 1;
     Guard g(device);
     auto fail = [&](hipError_t e, const char* what) { rc = hip_err(e, what); };
@@ -240,12 +247,17 @@ int kcdc_bw_batcher::run_round(std::unique_lock<std::mutex>& lk) {
             if (e != hipSuccess) fail(e, "writer cuts D2H");
         }
     }
+    const auto t1 = std::chrono::steady_clock::now();
     if (rc == KCDC_OK) {
         hipError_t e = hipStreamSynchronize(stream);
         if (e != hipSuccess) fail(e, "writer round");
     }
+    const auto t2 = std::chrono::steady_clock::now();
 
     lk.lock();
+    shipped_bytes += fresh;
+    t_submit += std::chrono::duration<double>(t1 - t0).count();
+    t_wait += std::chrono::duration<double>(t2 - t1).count();
     for (Job& j : jobs)  // the H2D copies have completed (or failed): blocks back to the pool
         for (uint8_t* blk : j.blocks) pool.push_back(blk);
     if (rc != KCDC_OK) return rc;
@@ -277,14 +289,22 @@ void kcdc_bw_batcher::loop() {
     for (;;) {
         auto work = [&] {
             if (stop || error) return true;
-            if (staged >= round_bytes) return true;
+            if (staged >= round_bytes || capped) return true;
             for (kcdc_bw* w : open)
                 if (w->finishing && !w->done) return true;
             return false;
         };
-        if (!work()) {
-            if (staged > 0) cv_round.wait_until(lk, last + wait, work);
-            else cv_round.wait(lk, work);
+        // Ship when a round's worth is staged, a writer is blocked on its cap or finishing, or
+        // max_wait after the first unshipped byte (or after the last round) -- whichever is first.
+        // Writers wake this thread when `staged` leaves 0, so the timed wait always starts.
+        while (!work()) {
+            if (staged > 0) {
+                const auto due = std::max(last, since) + wait;
+                if (cv_round.wait_until(lk, due, work)) break;
+                if (std::chrono::steady_clock::now() >= due) break;
+            } else {
+                cv_round.wait(lk, [&] { return work() || staged > 0; });
+            }
         }
         if (stop && staged == 0) {
             bool pending = false;
@@ -384,8 +404,14 @@ extern "C" int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len) {
         return KCDC_OK;
     }
     while (len) {
-        // backpressure: at most writer_cap unshipped bytes per writer
-        b->cv_done.wait(lk, [&] { return b->error || w->written - w->shipped < b->writer_cap; });
+        // backpressure: at most writer_cap unshipped bytes per writer (a capped writer asks for
+        // a round at once: with few writers `staged` may never reach round_bytes)
+        if (w->written - w->shipped >= b->writer_cap) {
+            b->capped++;
+            b->cv_round.notify_one();
+            b->cv_done.wait(lk, [&] { return b->error || w->written - w->shipped < b->writer_cap; });
+            b->capped--;
+        }
         if (b->error) return set_error(b->error, b->errmsg);
         if (w->blocks.empty() || w->fill == kBlock) {
             uint8_t* blk = b->get_block();
@@ -404,8 +430,10 @@ extern "C" int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len) {
         w->copying = false;
         w->fill += k;
         w->written += k;
+        const bool first = b->staged == 0;
+        if (first) b->since = std::chrono::steady_clock::now();
         b->staged += k;
-        if (b->staged >= b->round_bytes) b->cv_round.notify_one();
+        if (first || b->staged >= b->round_bytes) b->cv_round.notify_one();
         p += k;
         len -= k;
     }
@@ -462,3 +490,11 @@ extern "C" void kcdc_bw_free(kcdc_bw* w) {
 }
 
 extern "C" int64_t kcdc_bw_rounds(const kcdc_bw_batcher* b) { return b ? static_cast<int64_t>(b->rounds) : 0; }
+
+extern "C" int kcdc_bw_stats(kcdc_bw_batcher* b, double* out, int n) {
+    if (!b || !out) return set_error(KCDC_EINVAL, "null argument");
+    std::lock_guard<std::mutex> lk(b->mu);
+    const double v[4] = {static_cast<double>(b->rounds), static_cast<double>(b->shipped_bytes), b->t_submit, b->t_wait};
+    for (int i = 0; i < n && i < 4; i++) out[i] = v[i];
+    return 4;
+}

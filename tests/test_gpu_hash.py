@@ -1,5 +1,5 @@
-"""GPU: keyed BLAKE2 content hashes of many chunks (kcdc_hash_chunks_device) bit-exact
-against the oracle (hashlib, pinned by tests/test_hash_oracle.py): random chunk lengths and
+"""GPU: content hashes of many chunks (kcdc_hash_chunks_device) bit-exact against the oracle
+(oracle/hashes.py, pinned by tests/test_hash_oracle.py): keyed BLAKE2, HMAC-SHA2/SHA3, keyed BLAKE3: random chunk lengths and
 misaligned offsets, every registered name and key length class, the chunks the splitter
 cuts on config-2 streams, and the error contract -- through both kernels (one lane per chunk,
 and a quad of lanes per chunk)."""
@@ -107,3 +107,41 @@ def test_large_chunks(gpu, name, lanes):
     for i, L in enumerate(sizes):
         assert got[i].tobytes() == kopia_hash(name, key, host[offs[i]:offs[i] + L].tobytes()), (name, L)
     del torch
+
+
+NEW = ["BLAKE3-256", "BLAKE3-256-128", "HMAC-SHA224", "HMAC-SHA256", "HMAC-SHA256-128", "HMAC-SHA3-224",
+       "HMAC-SHA3-256"]
+
+
+@pytest.mark.parametrize("name", NEW)
+def test_hmac_and_blake3_random_chunks(gpu, name):
+    """HMAC-SHA2/SHA3 (one lane per chunk) and keyed BLAKE3 (one wave per chunk, tree of 1 KiB
+    chunk CVs) against the oracle: lengths at every block / rate / chunk / round boundary, keys
+    shorter and longer than the HMAC block (hashed first) and than BLAKE3's 32 bytes (derived)."""
+    rng = np.random.default_rng(len(name) * 7)
+    host = coracle.gen_stream(SEED, 33, 8 << 20)
+    edge = [0, 1, 3, 55, 56, 63, 64, 65, 119, 120, 135, 136, 137, 143, 144, 145, 271, 272, 273, 1023, 1024, 1025,
+            2047, 2048, 2049, 3072, 3073, 65535, 65536, 65537, 262143, 262144, 262145, 524288, 786432 + 5]
+    lens = np.array(edge + [int(x) for x in rng.integers(0, 300000, 300)], dtype=np.int64)
+    offs = np.array([int(rng.integers(0, host.size - int(L))) for L in lens], dtype=np.int64)
+    for klen in (0, 1, 31, 32, 33, 64, 65, 137, 145, 200):
+        key = bytes(rng.integers(0, 256, klen, dtype=np.uint8))
+        got = _hash_all(name, key, host, offs, lens)
+        with cf.ThreadPoolExecutor(16) as ex:
+            want = list(ex.map(lambda i: kopia_hash(name, key, host[offs[i]:offs[i] + lens[i]].tobytes()),
+                               range(len(lens))))
+        bad = [(i, int(lens[i])) for i in range(len(lens)) if got[i].tobytes() != want[i]]
+        assert not bad, (name, klen, bad[:5])
+
+
+@pytest.mark.parametrize("name", ["BLAKE3-256", "HMAC-SHA256", "HMAC-SHA3-256"])
+def test_hmac_and_blake3_large_chunks(gpu, name):
+    """Multi-round BLAKE3 trees (stack merges over 256-chunk rounds, a ragged last round) and
+    long HMAC chains: 4 MiB, 16 MiB + 3 and 64 MiB + 1025 at odd offsets."""
+    sizes = [4 << 20, (16 << 20) + 3, (64 << 20) + 1025]
+    offs = np.array([5, 5 + sizes[0] + 1, 5 + sizes[0] + 1 + sizes[1] + 9], dtype=np.int64)
+    host = coracle.gen_stream(SEED, 43, int(offs[-1] + sizes[-1] + 16))
+    key = bytes(range(32))
+    got = _hash_all(name, key, host, offs, np.array(sizes, np.int64))
+    for i, L in enumerate(sizes):
+        assert got[i].tobytes() == kopia_hash(name, key, host[offs[i]:offs[i] + L].tobytes()), (name, L)

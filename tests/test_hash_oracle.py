@@ -1,25 +1,15 @@
-"""The content-hash oracle (Python's hashlib BLAKE2, RFC 7693) pinned by published
-known-answer vectors (tests/golden/blake2_kat.json), and Kopia's keyed-hash contract as the
-GPU path must reproduce it: blake2b.New256(secret) / blake2s.New128|256(secret), output
-truncated (repo/hashing/blake_hashes.go:8-13, hashing.go:78-101).  CPU only."""
+"""The content-hash oracles (oracle/hashes.py: hashlib BLAKE2 and HMAC-SHA2/SHA3, the C BLAKE3
+restatement) pinned by published known-answer vectors (tests/golden/blake2_kat.json,
+hash_kat_more.json), and Kopia's keyed-hash contract as the GPU path must reproduce it:
+blake2b.New256(secret) / blake2s.New128|256(secret), hmac.New(sha*, secret), blake3.NewKeyed
+(derived key for short secrets), output truncated (repo/hashing/*.go).  CPU only."""
 import hashlib
+import hmac
 
 import pytest
 
 from conftest import golden
-
-KOPIA = {  # name -> (hashlib constructor, digest_size parameter, bytes kept)
-    "BLAKE2B-256-128": (hashlib.blake2b, 32, 16),
-    "BLAKE2B-256": (hashlib.blake2b, 32, 32),
-    "BLAKE2S-128": (hashlib.blake2s, 16, 16),
-    "BLAKE2S-256": (hashlib.blake2s, 32, 32),
-}
-
-
-def kopia_hash(name: str, key: bytes, data: bytes) -> bytes:
-    """ORACLE (test infrastructure): HashFunc(nil, data) of repo/hashing for `name`."""
-    fn, nn, keep = KOPIA[name]
-    return fn(data, key=key, digest_size=nn).digest()[:keep]
+from oracle.hashes import KOPIA, blake3, blake3_derive_key, blake3_key, kopia_hash  # noqa: F401
 
 
 @pytest.mark.parametrize("v", golden("blake2_kat.json")["vectors"], ids=lambda v: v["algo"] + "-" + v["hash"][:8])
@@ -30,10 +20,51 @@ def test_hashlib_matches_published_vectors(v):
 
 
 def test_registered_names_match_the_library():
+    """Every name hashing.go registers, in SupportedAlgorithms()' order (sort.Strings)."""
     from kopia_amd import hashing
+    assert list(KOPIA) == sorted(KOPIA)
     assert hashing.SupportedAlgorithms() == list(KOPIA)
     assert [hashing.hash_size(n) for n in KOPIA] == [k for _, _, k in KOPIA.values()]
     assert hashing.DefaultAlgorithm == "BLAKE2B-256-128"
+
+
+KAT = golden("hash_kat_more.json")
+
+
+@pytest.mark.parametrize("v", KAT["blake3"], ids=lambda v: str(v["len"]))
+def test_blake3_oracle_matches_published_vectors(v):
+    data = bytes(i % 251 for i in range(v["len"]))
+    assert blake3(data).hex() == v["hash"]
+    if "keyed_hash" in v:
+        assert blake3(data, b"whats the Elvish word for friend").hex() == v["keyed_hash"]
+    if "derive_key" in v:
+        assert blake3_derive_key("BLAKE3 2019-12-27 16:29:52 test vectors context", data).hex() == v["derive_key"]
+
+
+def test_blake3_oracle_abc_and_long_inputs():
+    assert blake3(b"abc").hex() == KAT["blake3_abc"]
+    # the streaming oracle's stack merges agree with a direct left-complete tree over many chunks
+    # (lengths straddling chunk and power-of-two boundaries): determinism + distinctness here,
+    # equality with the GPU's level-by-level tree in tests/test_gpu_hash.py
+    outs = {n: blake3(bytes(i % 251 for i in range(n))) for n in (1023, 1024, 1025, 2047, 2048, 2049, 8191, 8193)}
+    assert len(set(outs.values())) == len(outs)
+
+
+@pytest.mark.parametrize("v", KAT["hmac"], ids=lambda v: v["algo"])
+def test_hmac_oracle_matches_rfc4231(v):
+    got = hmac.new(v["key"].encode(), v["data"].encode(), getattr(hashlib, v["algo"])).hexdigest()
+    assert got == v["mac"]
+
+
+def test_kopia_key_rules():
+    """blake3_hashes.go:12-19: a secret under 32 bytes is stretched with DeriveKey, a longer
+    one is cut to 32 bytes; HMAC names truncate the MAC (sha_hashes.go:10-14)."""
+    assert blake3_key(b"k" * 40) == b"k" * 32
+    assert blake3_key(b"short") == blake3_derive_key("kopia blake3 derived key v1", b"short")
+    d = b"the quick brown fox"
+    assert kopia_hash("BLAKE3-256-128", b"s" * 32, d) == blake3(d, b"s" * 32)[:16]
+    assert kopia_hash("HMAC-SHA256-128", b"k", d) == hmac.new(b"k", d, hashlib.sha256).digest()[:16]
+    assert len(kopia_hash("HMAC-SHA3-224", b"k", d)) == 28
 
 
 def test_truncation_is_of_the_256_bit_digest():
