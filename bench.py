@@ -333,6 +333,8 @@ def bench_batch(args, comm: Comm):
 
     if args.hash and rank == 0 and world == 1:
         out["hash"] = bench_hash(args, data, ns, L, cuts, dev)
+    if args.encrypt and args.hash and rank == 0 and world == 1 and args.pipeline_slots > 0:
+        out["pipeline"] = bench_pipeline(args, data, ns, L, cuts, dev)
     if args.encrypt and rank == 0 and world == 1:
         out["encrypt"] = bench_encrypt(args, data, ns, L, cuts, dev)
         out["encrypt_aes"] = bench_encrypt(args, data, ns, L, cuts, dev, "AES256-GCM-HMAC-SHA256")
@@ -420,6 +422,125 @@ def bench_hash(args, data, ns: int, L: int, cuts: list, dev) -> dict:
             "inflight_1lane_ms": round(msR1, 3),
             "sample_parity_mismatches": int(bad), "sample_chunks": len(pick),
             "cpu_hashlib_1thread_gib_s": round(cpu, 3)}
+
+
+def bench_pipeline(args, data, ns: int, L: int, cuts: list, dev, algo: str = "AES256-GCM-HMAC-SHA256") -> dict:
+    """The upload path's device stages overlapped across batches: per batch split -> chunk table
+    (built on the device from the cut lists, no host round trip) -> content hash (Kopia's default
+    BLAKE2B-256-128 and `--pipeline-hash`) -> seal keyed by the content IDs (Kopia's default
+    AES256-GCM-HMAC-SHA256; content_manager.go:812, content_manager_lock_free.go:42-73).  Batch i
+    runs on stream i % slots, so batch i+1's split overlaps batch i's hash and batch i-1's seal.
+    Each slot has its own cut lists, chunk table, digests and sealed output.  Value: the stream
+    bytes of all batches over the wall time, and each stage alone on one batch for comparison.
+    Parity: one slot's sealed chunks are checked on a sample against the oracle."""
+    import ctypes as C
+    import torch
+    from kopia_amd import _lib, batch
+    from kopia_amd import encryption as ke
+    from kopia_amd import hashing as kh
+    lib = _lib.lib()
+    name = args.splitter
+    S, K = args.pipeline_slots, args.pipeline_batches
+    hashes = [kh.DefaultAlgorithm] + ([args.pipeline_hash] if args.pipeline_hash != kh.DefaultAlgorithm else [])
+    secret = ke.derive_key(bytes(range(64, 96)))
+    key = bytes(range(32))
+    cap_per = int(batch.make_device_batch(name, [data.data_ptr()], [L], dev).cap)
+    nent = ns * cap_per
+    starts = torch.arange(ns, dtype=torch.int64, device=dev) * L
+    jidx = torch.arange(cap_per, dtype=torch.int64, device=dev).view(1, -1)
+    nonces = torch.randint(0, 256, (12 * nent,), dtype=torch.uint8, device=dev)
+    work_bytes = int(lib.kcdc_crypt_workspace_size(nent))
+
+    class Slot:
+        def __init__(self):
+            self.stream = torch.cuda.Stream(dev)
+            self.b = batch.make_device_batch(name, [data.data_ptr() + i * L for i in range(ns)], [L] * ns, dev)
+            self.digest = torch.empty((nent, 32), dtype=torch.uint8, device=dev)
+            self.sealed = torch.empty(ns * L + 32 * nent, dtype=torch.uint8, device=dev)
+            self.status = torch.empty(nent, dtype=torch.int32, device=dev)
+            self.work = torch.empty(work_bytes, dtype=torch.uint8, device=dev)
+
+    slots = [Slot() for _ in range(S)]
+
+    def stage_split(sl):
+        batch.split_batch_device(name, sl.b, sl.stream)
+
+    def stage_table(sl):  # cut lists -> (offsets, lengths, order, sealed offsets) on the device
+        with torch.cuda.stream(sl.stream):
+            c = sl.b.cuts[:nent].view(ns, cap_per)
+            prev = torch.cat([torch.zeros((ns, 1), dtype=torch.int64, device=dev), c[:, :-1]], dim=1)
+            valid = jidx < sl.b.counts[:ns].view(-1, 1)
+            sl.lens = torch.where(valid, c - prev, torch.zeros_like(c)).reshape(-1).contiguous()
+            sl.offs = (starts.view(-1, 1) + torch.where(valid, prev, torch.zeros_like(prev))).reshape(-1).contiguous()
+            sl.order = torch.argsort(sl.lens, descending=True).to(torch.int32)
+            slen = ((sl.lens + 28 + 3) // 4) * 4
+            sl.oo = (torch.cumsum(slen, 0) - slen).contiguous()
+
+    def stage_hash(sl, hname):
+        _lib.check(lib.kcdc_hash_chunks_device(hname.encode(), C.c_void_p(data.data_ptr()), sl.offs.data_ptr(),
+                                               sl.lens.data_ptr(), sl.order.data_ptr(), nent, key, len(key),
+                                               sl.digest.data_ptr(), 32, C.c_void_p(sl.stream.cuda_stream)))
+
+    def stage_seal(sl, hname):
+        hs = kh.hash_size(hname)
+        _lib.check(lib.kcdc_encrypt_chunks_device(
+            algo.encode(), secret, len(secret), C.c_void_p(data.data_ptr()), sl.offs.data_ptr(), sl.lens.data_ptr(),
+            nent, C.c_void_p(sl.digest.data_ptr() + hs - 16), 16, 32, nonces.data_ptr(), sl.sealed.data_ptr(),
+            sl.oo.data_ptr(), sl.status.data_ptr(), sl.work.data_ptr(), work_bytes, C.c_void_p(sl.stream.cuda_stream)))
+
+    def one(sl, hname):
+        stage_split(sl)
+        stage_table(sl)
+        stage_hash(sl, hname)
+        stage_seal(sl, hname)
+
+    res = {"slots": S, "batches": K, "encrypt": algo, "chunk_table_entries": nent,
+           "valid_chunks": int(sum(c.size for c in cuts))}
+    for hname in hashes:
+        for sl in slots:  # warm every slot
+            one(sl, hname)
+        torch.cuda.synchronize(dev)
+        alone = {}
+        sl = slots[0]
+        for stage, fn in (("split", lambda: stage_split(sl)), ("table", lambda: stage_table(sl)),
+                          ("hash", lambda: stage_hash(sl, hname)), ("seal", lambda: stage_seal(sl, hname))):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(sl.stream)
+            fn()
+            e1.record(sl.stream)
+            torch.cuda.synchronize(dev)
+            alone[stage] = round(e0.elapsed_time(e1), 3)
+        t0 = time.perf_counter()
+        for i in range(K):
+            one(slots[i % S], hname)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        st = torch.stack([s_.status for s_ in slots]).cpu().numpy()
+        res[hname] = {"ms_per_batch": round(dt / K * 1e3, 3), "gib_s": round(K * ns * L / GiB / dt, 1),
+                      "stages_alone_ms": alone, "serial_sum_ms": round(sum(alone.values()), 3),
+                      "status_nonzero": int((st != 0).sum())}
+    # parity of the last slot used, on a sample: digest and sealed bytes against the oracle
+    from oracle import aesgcm, openssl_aead
+    from oracle.hashes import kopia_hash
+    seal_ref = openssl_aead.Sealer(algo).kopia_encrypt if openssl_aead.available() else aesgcm.kopia_encrypt
+    sl = slots[(K - 1) % S]
+    hname = hashes[-1]
+    hs = kh.hash_size(hname)
+    offs, lens, oo = sl.offs.cpu().numpy(), sl.lens.cpu().numpy(), sl.oo.cpu().numpy()
+    dig = sl.digest.cpu().numpy()
+    nz = np.nonzero(lens)[0]
+    pick = nz[:: max(1, len(nz) // 6)]
+    nh = nonces.cpu().numpy().tobytes()
+    bad = 0
+    for i in pick:
+        chunk = data[int(offs[i]):int(offs[i] + lens[i])].cpu().numpy().tobytes()
+        d = kopia_hash(hname, key, chunk)
+        bad += dig[i, :hs].tobytes() != d
+        want = seal_ref(secret, d[hs - 16:], nh[12 * i:12 * i + 12], chunk)
+        bad += sl.sealed[int(oo[i]):int(oo[i]) + len(want)].cpu().numpy().tobytes() != want
+    res["sample_parity_mismatches"] = int(bad)
+    res["sample_chunks"] = int(len(pick))
+    return res
 
 
 def bench_encrypt(args, data, ns: int, L: int, cuts: list, dev, algo: str = "CHACHA20-POLY1305-HMAC-SHA256") -> dict:
@@ -730,6 +851,9 @@ def parse(argv):
     ap.add_argument("--hash", default="BLAKE2B-256-128", help="configs 2/4, one GPU: also hash every chunk on "
                     "the device with this content hash (§8f #2; default Kopia's BLAKE2B-256-128)")
     ap.add_argument("--no-hash", action="store_true", help="skip the content-hash leg")
+    ap.add_argument("--pipeline-slots", type=int, default=3, help="split->hash->seal batches in flight (0: skip)")
+    ap.add_argument("--pipeline-batches", type=int, default=12, help="batches through the overlapped pipeline")
+    ap.add_argument("--pipeline-hash", default="BLAKE3-256-128", help="second hash timed through the pipeline")
     ap.add_argument("--encrypt", action="store_true", default=True,
                     help="configs 2/4, one GPU: also seal/open every chunk with CHACHA20-POLY1305-HMAC-SHA256 "
                          "(§8f #4; on by default)")

@@ -103,11 +103,11 @@ static void update(hasher* h, const uint8_t* p, int64_t n) {
 static void finish(hasher* h, uint8_t out[32]) {
     uint32_t o[16], cv[8];
     const uint32_t fl = h->flags | (h->blocks == 0 ? CHUNK_START : 0) | CHUNK_END;
+    uint8_t pad[64] = {0};  // the final block, zero padded
+    memcpy(pad, h->buf, h->buflen);
     if (h->depth == 0) {
-        compress(h->cv, h->buf, h->chunk, h->buflen, fl | ROOT, o);
+        compress(h->cv, pad, h->chunk, h->buflen, fl | ROOT, o);
     } else {
-        uint8_t pad[64] = {0};
-        memcpy(pad, h->buf, h->buflen);
         compress(h->cv, pad, h->chunk, h->buflen, fl, o);
         memcpy(cv, o, 32);
         for (int d = h->depth - 1; d >= 0; d--) {

@@ -73,3 +73,54 @@ def test_truncation_is_of_the_256_bit_digest():
     key, data = b"k" * 32, b"the quick brown fox"
     assert kopia_hash("BLAKE2B-256-128", key, data) == kopia_hash("BLAKE2B-256", key, data)[:16]
     assert kopia_hash("BLAKE2B-256-128", key, data) != hashlib.blake2b(data, key=key, digest_size=16).digest()
+
+
+def _b3_py(data: bytes, key: bytes) -> bytes:
+    """A second, recursive BLAKE3 keyed hash in plain Python (small inputs): cross-checks the C
+    oracle's streaming construction, including final blocks shorter than 64 bytes."""
+    M32 = 0xFFFFFFFF
+    IV = [0x6A09E667, 0xBB67AE85, 0x3C6EF372, 0xA54FF53A, 0x510E527F, 0x9B05688C, 0x1F83D9AB, 0x5BE0CD19]
+    P = [2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8]
+    rot = lambda x, n: ((x >> n) | (x << (32 - n))) & M32
+
+    def g(v, a, b, c, d, x, y):
+        v[a] = (v[a] + v[b] + x) & M32; v[d] = rot(v[d] ^ v[a], 16)
+        v[c] = (v[c] + v[d]) & M32; v[b] = rot(v[b] ^ v[c], 12)
+        v[a] = (v[a] + v[b] + y) & M32; v[d] = rot(v[d] ^ v[a], 8)
+        v[c] = (v[c] + v[d]) & M32; v[b] = rot(v[b] ^ v[c], 7)
+
+    def comp(cv, block, t, blen, fl):
+        m = [int.from_bytes(block[4 * i:4 * i + 4].ljust(4, b"\0"), "little") for i in range(16)]
+        v = cv[:] + IV[:4] + [t & M32, t >> 32, blen, fl]
+        for _ in range(7):
+            for a, b, c, d, i in ((0, 4, 8, 12, 0), (1, 5, 9, 13, 2), (2, 6, 10, 14, 4), (3, 7, 11, 15, 6),
+                                  (0, 5, 10, 15, 8), (1, 6, 11, 12, 10), (2, 7, 8, 13, 12), (3, 4, 9, 14, 14)):
+                g(v, a, b, c, d, m[i], m[i + 1])
+            m = [m[P[i]] for i in range(16)]
+        return [v[i] ^ v[i + 8] for i in range(8)]
+
+    k = [int.from_bytes(key[4 * i:4 * i + 4], "little") for i in range(8)]
+
+    def node(lo, n, root):
+        nch = max(1, -(-n // 1024))
+        if nch == 1:
+            cv, blocks = k[:], [data[lo + i:lo + min(i + 64, n)] for i in range(0, max(n, 1), 64)]
+            for j, blk in enumerate(blocks):
+                fl = 16 | (1 if j == 0 else 0) | ((2 | (8 if root else 0)) if j == len(blocks) - 1 else 0)
+                cv = comp(cv, blk.ljust(64, b"\0"), lo // 1024, len(blk), fl)
+            return cv
+        left = 1
+        while 2 * left < nch:
+            left *= 2
+        lcv, rcv = node(lo, 1024 * left, False), node(lo + 1024 * left, n - 1024 * left, False)
+        blk = b"".join(x.to_bytes(4, "little") for x in lcv + rcv)
+        return comp(k, blk, 0, 64, 16 | 4 | (8 if root else 0))
+
+    return b"".join(x.to_bytes(4, "little") for x in node(0, len(data), True))
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 119, 1023, 1024, 1025, 2049, 3072, 5000])
+def test_blake3_oracle_matches_python_restatement(n):
+    data = bytes((7 * i + 3) % 256 for i in range(n))
+    key = bytes(range(100, 132))
+    assert blake3(data, key) == _b3_py(data, key)

@@ -22,3 +22,4 @@ run compress 600 python -u -m pytest tests/test_gpu_compress.py tests/test_gpu_m
 for n in deflate-default deflate-best-compression s2-default zstd zstd-best-compression; do
   run cb_$n 200 python -u tools/compress_bench.py --gib 4 --name $n --iters 3 || exit 1
 done
+run bench 600 python -u bench.py --steps 20 --warmup 3 || exit 1
