@@ -153,8 +153,13 @@ int64_t kcdc_bw_cuts(kcdc_bw* w, uint64_t* out, uint64_t cap); /* final cuts tak
 int kcdc_bw_finish(kcdc_bw* w);
 void kcdc_bw_free(kcdc_bw* w);
 int64_t kcdc_bw_rounds(const kcdc_bw_batcher* b); /* rounds shipped so far (test hook) */
-/* Observability: out[0..n) = rounds, bytes shipped, seconds the round thread spent issuing copies
- * and launches, seconds it waited for the device.  Returns the number of values (4). */
+/* Observability: out[0..n) = rounds, bytes shipped, seconds the round thread spent building and
+ * issuing rounds, seconds it waited for the device, then the device seconds of the rounds' gathers
+ * (new bytes over PCIe into the writers' arenas) and of their splits (metadata in, splitter
+ * launch, cut lists out), from HIP events, then the device span of all rounds and the seconds of
+ * it in which a gather or a split ran, then the round thread's seconds per phase (collecting the
+ * writers' blocks, placing them in the arenas, issuing the gather, waiting for the previous round,
+ * issuing the split).  Returns 13. */
 int kcdc_bw_stats(kcdc_bw_batcher* b, double* out, int n);
 
 /* ------------------------------------------------------ batch (hot path)

@@ -15,10 +15,6 @@ struct Tables {
     int rk_shift = 0;       // deg(P) - 8
     uint64_t rk_out[256];   // b * x^(8*63) mod P
     uint64_t rk_mod[256];   // (b * x^deg mod P) | (b << deg)
-    // Two-byte Rabin-Karp step (kcdc_kernels.hip, rk2_*): v2 = (v << 16 | c1 c2) ^ T_lo[b] ^
-    // T_hi[a] ^ O16[l1] ^ outx[l2], a/b = bits 45..52 / 37..44 of v (deg P = 53).
-    uint64_t rk2_main[256][4];  // {T_lo = rk_mod, T_hi = (a x^61 mod P) | (a & 7) << 61, O16 = l x^520, outx = l x^512}
-    uint32_t rk2_test[256][2];  // {low word of a x^53 mod P, low word of outx}: the odd byte's test value
     uint64_t cooked[607];   // Go math/rand rngCooked (rng.go)
 };
 // rand.New(rand.NewSource(seed)).Read(p[:n]) (Go math/rand, 7 bytes per Int63).
@@ -68,6 +64,8 @@ struct SplitArgs {
     uint64_t* counts;
     const uint64_t* cut_end = nullptr;  // optional per-stream end of the cut range (device)
     const uint64_t* starts = nullptr;   // optional per-stream first chunk start (device; bytes before = history)
+    const uint64_t* resume = nullptr;   // optional (with starts): positions below resume[i] are known to hold no
+                                        // candidate of stream i's first chunk (a previous round tested them)
 };
 // Launch the batch splitter for `algo` on `stream` (hipStream_t as void*).
 int launch_split_batch(const Algo& algo, const SplitArgs& a, int device, void* stream);

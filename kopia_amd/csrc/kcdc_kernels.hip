@@ -677,12 +677,11 @@ struct BatchArgs {
     const uint64_t* cut_end;  // optional: stream i's cut range ends at cut_end[i] (else cut_base[i+1] / cuts_cap)
     const uint64_t* starts;   // optional: stream i's first chunk starts at starts[i] (else 0); the bytes before
                               // it are the window history of a continued stream (kcdc_bw_*)
+    const uint64_t* resume;   // optional (with starts): the first chunk's test range resumes at resume[i]
     uint64_t min_size, max_size;
     const uint32_t* buz;
     const uint64_t* rk_out;
     const uint64_t* rk_mod;
-    const uint64_t* rk2_main;  // Tables::rk2_main (two-byte Rabin-Karp step)
-    const uint32_t* rk2_test;  // Tables::rk2_test
     uint32_t nstreams;
     uint32_t mask;     // buzhash: the candidate mask in the rotated frame (below); rabin: as is
     uint32_t rk_shift;
@@ -1130,6 +1129,19 @@ __device__ __forceinline__ bool pstream_region(const BatchArgs& a, PStream& st, 
     return true;
 }
 
+// First tile coordinate of stream e's first region when a previous round already tested the
+// positions below resume[e] (kcdc_bw_*): the scan starts at the tile holding
+// min(resume, region end) instead of at s + min - 1; -1 (set up as usual) otherwise.
+__device__ __forceinline__ int64_t resume_ct(const BatchArgs& a, uint32_t e, int64_t s, int64_t n, int64_t off0) {
+    if (!a.resume) return -1;
+    const int64_t r = static_cast<int64_t>(a.resume[e]);
+    const int64_t lo = s + static_cast<int64_t>(a.min_size) - 1;
+    const int64_t mx = s + static_cast<int64_t>(a.max_size) - 1;
+    const int64_t hi = mx < n - 1 ? mx : n - 1;
+    if (lo > n - 1 || r <= lo) return -1;
+    return ((r > hi ? hi : r) + off0) & ~int64_t(127);
+}
+
 // Ring entry of a yielded stream: granule l (< 7) = {tag, lo, hi, l == 0 ? sid : 0} of
 // word l in {cnt, s, ct, ptr, n, cb, cap}.  Written by lane 0 alone (7 uniform 16-byte
 // stores): a per-lane select chain over the words miscompiled (a word's high half read
@@ -1306,6 +1318,7 @@ __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
         pstream_fresh(st, sid, uni64(reinterpret_cast<uint64_t>(a.ptrs[sid])), uni64(a.lens[sid]), cb,
                       uni64(cut_end_of(a, sid)));
         if (a.starts) st.s = static_cast<int64_t>(uni64(a.starts[sid]));
+        st.ct = resume_ct(a, sid, st.s, st.n, st.off0);
         uniformize(st);
         pwrite(a, lane, e0 + i, st, false);
     }
@@ -1876,230 +1889,9 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
 //   2K    line fills (A line 0, B line 0, A line 1, ...), K = L/256 lines per chain;
 //   D     drain: B's last 64 bytes (no fill: the slot takes the next tile's warm fill, or
 //         the next stream's queue entry).
-#ifndef KCDC_RK_2STEP
-#define KCDC_RK_2STEP 0  // 1: two bytes per chain hop (slower: 2.94 vs 2.51 ms, config 2); 0: one byte per hop
-#endif
-#if KCDC_RK_2STEP
-#ifndef KCDC_RK2_T
-#define KCDC_RK2_T true
-#endif
-// ---- two bytes per chain hop (round 3)
-// The roll is GF(2)-linear, so two rolls fold into one (v = the hash, a/b = its bits
-// 45..52 / 37..44, c1 c2 the entering and l1 l2 the leaving bytes):
-//   v2 = ((v << 16) | c1 << 8 | c2) ^ T_lo[b] ^ T_hi[a] ^ O16[l1] ^ outx[l2]
-// with T_lo[b] = b x^53 mod P | b << 53 (= mod[b]), T_hi[a] = a x^61 mod P | (a & 7) << 61
-// (both also clear the shifted-out bits 53..63), O16[l] = l x^520 mod P, outx[l] = l x^512
-// mod P (Tables::rk2_main).  All four reads depend on v or on data only, so the chain is one
-// LDS round trip per TWO bytes (round 2: one per byte).  The odd byte's hash is needed only
-// for its test, i.e. its low word: lo1 = (lo << 8 | c1) ^ (a x^53 mod P).lo ^ outx[l1].lo --
-// two 32-bit reads off the chain (Tables::rk2_test).
-//
-// Conflict-free without 32 replicas per table: every read's four results are only XORed
-// together, so WHICH table a lane reads in which instruction does not matter.  One 256-byte
-// row per index holds all four tables, 8 replicas each (slot 8 t + r); in read k lane l takes
-// table (g + k) & 3 (g = (l >> 3) & 3), replica l & 7 -- the 32 lanes of a ds_read_b64 group
-// hit 32 distinct 8-byte slots, whatever the indices.  The test family is the same idea with
-// 128-byte rows (two tables x 16 replicas, 32-bit entries, lanes 16..31 swap tables).
-// R4 = [b, a, l1, l2] (one v_perm of hi >> 5 and the leaving dword) holds the four row indices
-// in table order, so each address is ONE v_perm: [8 slot(l, k), R4 byte t, 0, 0].
-// LDS: 32 KiB test rows + 64 KiB main rows + 8 x 8 KiB step slots = 160 KiB.
-struct RkTables {
-    uint32_t q[256 * 32];  // test family: row i (128 B), slots 0..15 (a x^53).lo, 16..31 outx[i].lo
-    uint64_t m[256 * 32];  // main family: row i (256 B), slots 8t..8t+7 table t = T_lo, T_hi, O16, outx
-};
-static_assert(sizeof(RkTables) + sizeof(RkSlots) <= 160 * 1024, "Rabin-Karp tables + step slots exceed LDS");
-
-struct RkCtx {
-    const char* qb;     // LDS byte address of RkTables::q
-    const char* mb;     // LDS byte address of RkTables::m
-    uint32_t selr[2];   // R4 selector for byte pairs at j = 0, 2: R4 rotated by g bytes, so
-                        // R4 byte k = the row index of table (g + k) & 3, g = (l >> 3) & 3
-    uint32_t off;       // byte k: 8 * slot of read k = 8 (8 ((g + k) & 3) + (l & 7))
-    uint32_t offq;      // byte k': 2 * 4 * (16 tq + (l & 15)), tq = ((l >> 4) & 1) ^ k'
-    uint32_t selq[2];   // test read k': [OFFQ byte k', R4 byte of table 1 + tq, 0, 0] (halved:
-                        // 128-byte rows)
-    uint32_t mask;      // avg - 1
-};
-// Read k's address: [OFF byte k, R4 byte k, 0, 0] (the same selector in every lane).
-constexpr uint32_t rk2_sel(int k) { return 0x0c0c0000u | (static_cast<uint32_t>(k) << 8) | (4u + k); }
-
-// Fill the LDS tables from the device copies of Tables::rk2_main / rk2_test and set up the
-// lane's selectors (all threads of the workgroup; ends with a barrier).
-__device__ __forceinline__ RkCtx rk_setup(RkTables& smt, const BatchArgs& a, int lane) {
-    for (uint32_t i = threadIdx.x; i < 256u * 32u; i += blockDim.x) {
-        const uint32_t row = i >> 5, s = i & 31u;
-        smt.m[i] = a.rk2_main[4 * row + (s >> 3)];
-        smt.q[i] = a.rk2_test[2 * row + (s >> 4)];
-    }
-    __syncthreads();
-    RkCtx k;
-    k.qb = reinterpret_cast<const char*>(smt.q);
-    k.mb = reinterpret_cast<const char*>(smt.m);
-    const uint32_t l = static_cast<uint32_t>(lane), g = (l >> 3) & 3u;
-    k.off = 0;
-    k.selr[0] = k.selr[1] = 0;
-#pragma unroll
-    for (uint32_t r = 0; r < 4; r++) {
-        const uint32_t t = (g + r) & 3u;  // R4 (unrotated) = [b, a, l1, l2]: bytes 0, 1 of hi >> 5, then pl
-        k.off |= (8u * (8u * t + (l & 7u))) << (8 * r);
-        k.selr[0] |= (t < 2 ? t : 4u + (t - 2)) << (8 * r);
-        k.selr[1] |= (t < 2 ? t : 6u + (t - 2)) << (8 * r);
-    }
-    k.offq = 0;
-#pragma unroll
-    for (uint32_t r = 0; r < 2; r++) {
-        const uint32_t tq = ((l >> 4) & 1u) ^ r;
-        k.offq |= (8u * (16u * tq + (l & 15u))) << (8 * r);
-        k.selq[r] = 0x0c0c0000u | (((1u + tq - g) & 3u) << 8) | (4u + r);
-    }
-    k.mask = a.mask;
-    return k;
-}
-
-// One chain's two-byte hop at byte pair (x, x + 1) of a 64-byte piece: `w` the entering
-// dword, `pl` the leaving dword (the same bytes 64 positions earlier), j = x & 3 (0 or 2).
-// Issues the six table reads (R4 = [b, a, l1, l2] rotated by g bytes); rk2_finish consumes them.
-struct Rk2Reads {
-    uint64_t m[4];
-    uint32_t q[2];
-};
-template <int J, bool TEST>
-__device__ __forceinline__ Rk2Reads rk2_issue(const RkCtx& k, uint32_t hi, uint32_t pl) {
-    Rk2Reads r;
-    const uint32_t t = hi >> 5;  // [b, a, 0, 0] (hi < 2^21)
-    const uint32_t r4 = __builtin_amdgcn_perm(pl, t, k.selr[J >> 1]);
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-        r.m[i] = *reinterpret_cast<const uint64_t*>(k.mb + __builtin_amdgcn_perm(k.off, r4, rk2_sel(i)));
-    if (TEST) {
-#pragma unroll
-        for (int i = 0; i < 2; i++)
-            r.q[i] = *reinterpret_cast<const uint32_t*>(k.qb + (__builtin_amdgcn_perm(k.offq, r4, k.selq[i]) >> 1));
-    }
-    return r;
-}
-// The hop's new state; with TEST, mm = min(mm, lo1 & mask, lo2 & mask).
-template <int J, bool TEST>
-__device__ __forceinline__ void rk2_finish(const RkCtx& k, uint32_t& hi, uint32_t& lo, uint32_t w, const Rk2Reads& r,
-                                           uint32_t& mm) {
-    const uint32_t sh = __builtin_amdgcn_alignbit(hi, lo, 16);  // (v << 16), high word
-    // (v << 16) | c1 << 8 | c2, low word: [c2, c1, lo.b0, lo.b1]
-    const uint32_t sl = __builtin_amdgcn_perm(w, lo, 0x01000000u | (static_cast<uint32_t>(4 + J) << 8) | (5u + J));
-    uint32_t l1 = 0;
-    if (TEST)  // (v << 8) | c1, low word: [c1, lo.b0, lo.b1, lo.b2]
-        l1 = __builtin_amdgcn_perm(w, lo, 0x02010000u | (4u + J));
-    const uint32_t h2 = __builtin_amdgcn_bitop3_b32(sh, static_cast<uint32_t>(r.m[0] >> 32),
-                                                    static_cast<uint32_t>(r.m[1] >> 32), 0x96);
-    const uint32_t l2 = __builtin_amdgcn_bitop3_b32(sl, static_cast<uint32_t>(r.m[0]), static_cast<uint32_t>(r.m[1]), 0x96);
-    hi = __builtin_amdgcn_bitop3_b32(h2, static_cast<uint32_t>(r.m[2] >> 32), static_cast<uint32_t>(r.m[3] >> 32), 0x96);
-    lo = __builtin_amdgcn_bitop3_b32(l2, static_cast<uint32_t>(r.m[2]), static_cast<uint32_t>(r.m[3]), 0x96);
-    if (TEST) {
-        const uint32_t v1 = __builtin_amdgcn_bitop3_b32(l1, r.q[0], r.q[1], 0x96);
-        mm = min(mm, min(v1 & k.mask, lo & k.mask));
-    }
-}
-
-// 64 bytes of chain A (in a / leaving pa) and of chain B (in b / leaving pb), interleaved
-// hop by hop; ma/mb: running min of (lo & mask) over the piece's 64 positions.  ACT_A/ACT_B:
-// whether that chain's bytes are real (an idle chain is not rolled at all).
-template <bool ACT_A, bool ACT_B>
-__device__ __forceinline__ void rk2_step64(const RkCtx& k, uint32_t& ha, uint32_t& la, const uint32_t (&a)[16],
-                                           const uint32_t (&pa)[16], uint32_t& hb, uint32_t& lb,
-                                           const uint32_t (&b)[16], const uint32_t (&pb)[16], uint32_t& ma,
-                                           uint32_t& mb) {
-#pragma unroll
-    for (int x = 0; x < 64; x += 2) {
-        __builtin_amdgcn_sched_barrier(0);
-        Rk2Reads ra, rb;
-        if ((x & 3) == 0) {
-            if (ACT_A) ra = rk2_issue<0, KCDC_RK2_T>(k, ha, pa[x >> 2]);
-            if (ACT_B) rb = rk2_issue<0, KCDC_RK2_T>(k, hb, pb[x >> 2]);
-        } else {
-            if (ACT_A) ra = rk2_issue<2, KCDC_RK2_T>(k, ha, pa[x >> 2]);
-            if (ACT_B) rb = rk2_issue<2, KCDC_RK2_T>(k, hb, pb[x >> 2]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if ((x & 3) == 0) {
-            if (ACT_A) rk2_finish<0, KCDC_RK2_T>(k, ha, la, a[x >> 2], ra, ma);
-            if (ACT_B) rk2_finish<0, KCDC_RK2_T>(k, hb, lb, b[x >> 2], rb, mb);
-        } else {
-            if (ACT_A) rk2_finish<2, KCDC_RK2_T>(k, ha, la, a[x >> 2], ra, ma);
-            if (ACT_B) rk2_finish<2, KCDC_RK2_T>(k, hb, lb, b[x >> 2], rb, mb);
-        }
-        // keep the running mins sequential (reassociated into trees they hold ~2 x 64 values)
-        if (ACT_A) asm volatile("" : "+v"(ma));
-        if (ACT_B) asm volatile("" : "+v"(mb));
-    }
-}
-
-// Exact re-run of one chain's 64 bytes at coordinate c from (hi, lo) (rare): first index in
-// [lo_i, hi_i] with (lo & mask) == 0, else 64.  The bytes are re-read from global memory one
-// dword pair at a time (the walk's 32-register copies of them pushed the kernel into spills
-// whose reloads waited on the line DMA); plain per-lane table addressing (conflicts do not
-// matter here).  Bytes before the stream start read as zero, as in the walk.
-__device__ uint32_t rk_exact64(const RkCtx& k, uint32_t hi, uint32_t lo, const Loader& ld, int64_t c, int lo_i,
-                               int hi_i) {
-    const uint32_t l = static_cast<uint32_t>(__lane_id());
-    uint32_t first = 64;
-    auto dword_at = [&](int64_t cc) -> uint32_t {
-        uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(ld.rsrc, static_cast<int32_t>(cc - ld.tb), 0, 0);
-        const int64_t keep_from = ld.off0 - cc;  // first byte of the dword inside the stream
-        if (keep_from > 0) v = keep_from >= 4 ? 0u : v & (0xFFFFFFFFu << (8 * keep_from));
-        return v;
-    };
-#pragma unroll 1
-    for (int j = 0; j < 16; j++) {
-        const uint32_t w = dword_at(c + 4 * j), pl = c - 64 + 4 * j >= 0 ? dword_at(c - 64 + 4 * j) : 0u;
-#pragma unroll
-        for (int J = 0; J < 4; J += 2) {
-            const uint32_t ib = (hi >> 5) & 0xFFu, ia = (hi >> 13) & 0xFFu, i1 = (pl >> (8 * J)) & 0xFFu,
-                           i2 = (pl >> (8 * J + 8)) & 0xFFu;  // rows of T_lo, T_hi, O16, outx
-            auto ent = [&](uint32_t row, uint32_t t) {
-                return *reinterpret_cast<const uint64_t*>(k.mb + 256u * row + 8u * (8u * t + (l & 7u)));
-            };
-            const uint64_t m = ent(ib, 0) ^ ent(ia, 1) ^ ent(i1, 2) ^ ent(i2, 3);
-            const uint32_t q0 = *reinterpret_cast<const uint32_t*>(k.qb + 128u * ia + 4u * (l & 15u));
-            const uint32_t q1 = *reinterpret_cast<const uint32_t*>(k.qb + 128u * i1 + 4u * (16u + (l & 15u)));
-            const uint32_t c1 = (w >> (8 * J)) & 0xFFu, c2 = (w >> (8 * J + 8)) & 0xFFu;
-            const uint32_t lo1 = ((lo << 8) | c1) ^ q0 ^ q1;
-            const uint32_t nhi = ((hi << 16) | (lo >> 16)) ^ static_cast<uint32_t>(m >> 32);
-            lo = ((lo << 16) | (c1 << 8) | c2) ^ static_cast<uint32_t>(m);
-            hi = nhi;
-            const int i = 4 * j + J;
-            if (first == 64 && (lo1 & k.mask) == 0 && i >= lo_i && i <= hi_i) first = static_cast<uint32_t>(i);
-            if (first == 64 && (lo & k.mask) == 0 && i + 1 >= lo_i && i + 1 <= hi_i) first = static_cast<uint32_t>(i + 1);
-        }
-    }
-    return first;
-}
-
-// Warm fill of a tile -> both chains' 64-byte histories (pa, pb) and states (leaving bytes 0:
-// every leaving-table row 0 is zero).
-__device__ __forceinline__ void rk_warm(const RkCtx& kx, const uint32_t (&dw)[32], uint32_t& ha, uint32_t& la,
-                                        uint32_t& hb, uint32_t& lb, uint32_t (&pa)[16], uint32_t (&pb)[16]) {
-    ha = la = hb = lb = 0;
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-        pa[i] = dw[i];
-        pb[i] = dw[16 + i];
-    }
-    uint32_t mm = 0;
-#pragma unroll
-    for (int x = 0; x < 64; x += 2) {
-        __builtin_amdgcn_sched_barrier(0);
-        if ((x & 3) == 0) {
-            const Rk2Reads ra = rk2_issue<0, false>(kx, ha, 0u), rb = rk2_issue<0, false>(kx, hb, 0u);
-            rk2_finish<0, false>(kx, ha, la, pa[x >> 2], ra, mm);
-            rk2_finish<0, false>(kx, hb, lb, pb[x >> 2], rb, mm);
-        } else {
-            const Rk2Reads ra = rk2_issue<2, false>(kx, ha, 0u), rb = rk2_issue<2, false>(kx, hb, 0u);
-            rk2_finish<2, false>(kx, ha, la, pa[x >> 2], ra, mm);
-            rk2_finish<2, false>(kx, hb, lb, pb[x >> 2], rb, mm);
-        }
-    }
-}
-#define RK_STEP rk2_step64
-#else  // KCDC_RK_2STEP == 0: one byte per chain hop (round 2)
+// (Round 3 tried two bytes per chain hop -- v2 = (v << 16 | c1 c2) ^ T_lo[b] ^ T_hi[a] ^ O16[l1] ^
+// outx[l2], GF(2)-linear -- with conflict-free rotated tables: one LDS round trip per two bytes but
+// 10.8 VALU per byte instead of 8.9, 2.94-2.97 vs 2.51-2.54 ms on config 2)
 // Tables (96 KiB, conflict-free or nearly): out[] with 32 replicas at a 256-byte stride
 // (lane l reads replica l % 32, bank pair 2(l % 32); address = one v_perm of the leaving
 // byte), mod[] with 16 replicas at a 128-byte stride (lanes l and l+16 share a bank pair
@@ -2341,15 +2133,12 @@ __device__ __forceinline__ RkCtx rk_setup(RkTables& smt, const BatchArgs& a, int
 #else
 #define RK_STEP rk_step64
 #endif
-#endif  // KCDC_RK_2STEP
 // The rare exact re-run of a 64-byte piece at coordinate c whose running test passed.
 __device__ __forceinline__ uint32_t rk_exact(const RkCtx& k, uint32_t h0, uint32_t l0, const Loader& ld, int64_t c,
                                             const uint32_t (&in)[16], const uint32_t (&prv)[16], int lo_i, int hi_i) {
-#if KCDC_RK_2STEP
-    return rk_exact64(k, h0, l0, ld, c, lo_i, hi_i);
-#else
+    (void)ld;
+    (void)c;
     return rk_exact64(k, h0, l0, in, prv, lo_i, hi_i);
-#endif
 }
 
 // Geometry of a Rabin-Karp tile at ct: L bytes per lane (a multiple of 256: two chains of
@@ -2740,7 +2529,9 @@ __global__ void init_ring_kernel(BatchArgs a, uint32_t nslots, uint32_t nwaves, 
         const uint64_t cend = cut_end_of(a, e);
         const uint64_t w = g == 0 ? 0ull                           // cnt
                          : g == 1 ? (a.starts ? a.starts[e] : 0ull)  // s
-                         : g == 2 ? ~0ull                          // ct = -1: region not set up
+                         : g == 2 ? static_cast<uint64_t>(resume_ct(a, e, a.starts ? static_cast<int64_t>(a.starts[e]) : 0,
+                                                                     static_cast<int64_t>(a.lens[e]),
+                                                                     static_cast<int64_t>(p & 15u)))  // ct (-1: not set up)
                          : g == 3 ? p
                          : g == 4 ? a.lens[e]
                          : g == 5 ? cb
@@ -3717,8 +3508,6 @@ struct DeviceTables {
     uint32_t* buz = nullptr;
     uint64_t* rk_out = nullptr;
     uint64_t* rk_mod = nullptr;
-    uint64_t* rk2_main = nullptr;
-    uint32_t* rk2_test = nullptr;
     int cus = 0;
 };
 
@@ -3785,8 +3574,6 @@ dev::BatchArgs base_args(const Algo& algo, const DeviceTables& t) {
     a.buz = t.buz;
     a.rk_out = t.rk_out;
     a.rk_mod = t.rk_mod;
-    a.rk2_main = t.rk2_main;
-    a.rk2_test = t.rk2_test;
     a.rk_shift = static_cast<uint32_t>(tables().rk_shift);
     // largest power of two <= avg / 256, within [256, kLaneMax]: tiles of ~avg/4 (1 MiB and
     // larger averages keep the full 2 KiB lane segments)
@@ -3869,10 +3656,6 @@ const DeviceTables* device_tables(int device, int* err) {
     if (e == hipSuccess) e = hipMemcpy(d.buz, T.buz, sizeof(T.buz), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d.rk_out, T.rk_out, sizeof(T.rk_out), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d.rk_mod, T.rk_mod, sizeof(T.rk_mod), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&d.rk2_main, sizeof(T.rk2_main));
-    if (e == hipSuccess) e = hipMalloc(&d.rk2_test, sizeof(T.rk2_test));
-    if (e == hipSuccess) e = hipMemcpy(d.rk2_main, T.rk2_main, sizeof(T.rk2_main), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(d.rk2_test, T.rk2_test, sizeof(T.rk2_test), hipMemcpyHostToDevice);
     (void)hipSetDevice(prev);
     if (e != hipSuccess) {
         *err = hip_fail(e, "table upload");
@@ -3897,6 +3680,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
     a.cut_base = s.cut_base;
     a.cut_end = s.cut_end;
     a.starts = s.starts;
+    a.resume = s.starts ? s.resume : nullptr;
     a.counts = s.counts;
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (s.starts && (algo.kind == kFixed || !KCDC_DMA || (algo.kind == kRabinKarp && !KCDC_RK_PIPE)))

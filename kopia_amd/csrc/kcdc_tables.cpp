@@ -196,20 +196,6 @@ void build_tables() {
             g_tables.rk_out[b] = gf2_mulmod(b, xw, f);
             g_tables.rk_mod[b] = gf2_mod(b << k, f) | (b << k);
         }
-        // two-byte step tables (the device kernels assume deg P = 53, as the registry's P has)
-        uint64_t x8 = 1ull << 8;  // multiply a residue by x^8: one more reduction step
-        auto times_x8 = [&](uint64_t v) { return gf2_mulmod(v, x8, f); };
-        for (uint64_t b = 0; b < 256; b++) {
-            const uint64_t lowmask = (1ull << k) - 1;
-            const uint64_t m = g_tables.rk_mod[b] & lowmask;  // b x^53 mod P
-            const uint64_t outx = times_x8(g_tables.rk_out[b]);
-            g_tables.rk2_main[b][0] = g_tables.rk_mod[b];
-            g_tables.rk2_main[b][1] = times_x8(m) | ((b & 7u) << 61);
-            g_tables.rk2_main[b][2] = times_x8(outx);
-            g_tables.rk2_main[b][3] = outx;
-            g_tables.rk2_test[b][0] = static_cast<uint32_t>(m);
-            g_tables.rk2_test[b][1] = static_cast<uint32_t>(outx);
-        }
     }
 }
 

@@ -1,21 +1,29 @@
 // Batching object writers (the writer-level remainder): many concurrent
 // objectWriter.Write streams (repo/object/object_writer.go:113-139) fed in 64 KiB slices
-// (snapshot/upload/upload.go:394-407) are accumulated per writer in pinned host staging and
-// split together: one round = every writer's new bytes up in one burst of H2D copies, one
-// batch-splitter launch over all writers' unresolved regions, their cut lists back.  Each
-// byte crosses PCIe once; a writer's unresolved tail (the chunk in progress plus the 64-byte
-// window before it) stays on the device from round to round.
+// (snapshot/upload/upload.go:394-407) are staged per writer in pinned host blocks and split
+// together: one round = one gather launch that pulls every writer's new bytes over PCIe into its
+// device arena, one batch-splitter launch over all writers' unresolved regions, their cut lists
+// back.  Each byte crosses PCIe once.
+//
+// Device layout: every writer owns an arena in HBM holding its stream contiguously from the
+// window before its last final cut (the chunk in progress) up to the bytes shipped so far; arena
+// offset = stream position - origin, origin a multiple of 16.  Host blocks place each byte at a
+// block offset congruent to its stream position mod 16, so the gather copies 16-byte vectors.
+// Rounds are pipelined: round k+1's gather (new bytes, past round k's regions) runs while round
+// k splits; round k+1's launch waits for round k's cuts (its chunk starts).
 //
 // Exactness: the rolling hash at position p is a function of the 64 bytes ending at p
 // (SURVEY.md §0.4), and a chunk's cut is the first candidate in [s+min-1, s+max-1] (or the
 // forced cut).  A round splits region [tail_pos, shipped) starting its first chunk at the
-// writer's last final cut (kernel `starts`: the bytes before it are window history only).
-// Every cut it reports is final except the last one, which is the region end (the chunk
-// still growing), unless the writer is finishing.  So the cuts equal one NextSplitPoint pass
-// over the whole object, however the bytes were sliced (tests/test_gpu_writer.py).
+// writer's last final cut (kernel `starts`: the bytes before it are window history only), and
+// skips the positions the previous round already tested for that chunk (kernel `resume`).
+// Every cut it reports is final except the last one, which is the region end (the chunk still
+// growing), unless the writer is finishing.  So the cuts equal one NextSplitPoint pass over the
+// whole object, however the bytes were sliced (tests/test_gpu_writer.py).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -31,8 +39,9 @@ using namespace kcdc;
 
 namespace {
 
-constexpr size_t kBlock = 4u << 20;  // pinned staging block (one H2D copy each)
-constexpr uint64_t kHist = 64;       // window history kept before a writer's last final cut
+constexpr size_t kBlock = 4u << 20;    // pinned staging block
+constexpr uint64_t kHist = 64;         // window history kept before a writer's last final cut
+constexpr uint32_t kTask = 64u << 10;  // gather: bytes per workgroup
 
 int hip_err(hipError_t e, const char* what) { return set_error(KCDC_EIO, std::string(what) + ": " + hipGetErrorString(e)); }
 
@@ -47,7 +56,71 @@ struct Guard {
     }
 };
 
-uint64_t align16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
+// One gather piece: len bytes from pinned host memory (device-visible) to a writer's arena;
+// src and dst are congruent mod 16.
+struct Piece {
+    const uint8_t* src;
+    uint8_t* dst;
+    uint64_t len;
+    uint64_t task0;  // first 64 KiB task of this piece (exclusive prefix over pieces)
+};
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) v4u gv4u;
+typedef __attribute__((address_space(1))) uint8_t gu8;
+
+// A bounded grid (kGatherWGs workgroups, grid-stride over 64 KiB tasks): the gather needs few
+// CUs to saturate PCIe, and a grid of one workgroup per task filled the machine, so the split
+// launch queued behind it and the two never overlapped.  Per task: the bytes before the first
+// 16-byte boundary and after the last one singly, the rest as 16-byte vectors, four in flight
+// per thread (the reads cross PCIe: latency, not bandwidth, limits one workgroup).
+constexpr unsigned kGatherWGs = 96;
+__global__ __launch_bounds__(256) void bw_gather_kernel(const Piece* pieces, uint32_t npieces, uint64_t ntasks) {
+    for (uint64_t task = blockIdx.x; task < ntasks; task += gridDim.x) {
+        uint32_t lo = 0, hi = npieces;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pieces[mid].task0 <= task) lo = mid;
+            else hi = mid;
+        }
+        const Piece pc = pieces[lo];
+        const uint64_t off = (task - pc.task0) * kTask;
+        if (off >= pc.len) continue;
+        const uint64_t len = pc.len - off < kTask ? pc.len - off : kTask;
+        // global, not flat, accesses (the pinned host blocks are mapped into the device's address space)
+        const gu8* s = reinterpret_cast<const gu8*>(reinterpret_cast<uintptr_t>(pc.src) + off);
+        gu8* d = reinterpret_cast<gu8*>(reinterpret_cast<uintptr_t>(pc.dst) + off);
+        const uint32_t head = static_cast<uint32_t>((16u - ((reinterpret_cast<uintptr_t>(pc.dst) + off) & 15u)) & 15u);
+        const uint32_t h = head < len ? head : static_cast<uint32_t>(len);
+        const uint32_t t = threadIdx.x;
+        if (t < h) d[t] = s[t];
+        const uint64_t nv = (len - h) / 16;
+        const gv4u* sv = reinterpret_cast<const gv4u*>(s + h);
+        gv4u* dv = reinterpret_cast<gv4u*>(d + h);
+        for (uint64_t i = t; i < nv; i += 4 * 256) {
+            v4u v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (i + 256 * k < nv) v[k] = __builtin_nontemporal_load(sv + i + 256 * k);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (i + 256 * k < nv) dv[i + 256 * k] = v[k];
+        }
+        const uint64_t done = h + 16 * nv;
+        if (t < len - done) d[done + t] = s[done + t];
+    }
+}
+
+struct Blk {  // a pinned block: bytes [start, end) are stream bytes [pos, pos + end - start)
+    uint8_t* p = nullptr;
+    uint32_t start = 0, end = 0;
+    uint64_t pos = 0;
+};
+
+int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
 
 }  // namespace
 
@@ -56,44 +129,58 @@ struct kcdc_bw;
 struct kcdc_bw_batcher {
     const Algo* algo = nullptr;
     int device = 0;
-    uint64_t round_bytes = 0;    // ship once this many new bytes are staged across writers
-    uint64_t writer_cap = 0;     // a writer blocks in write() while this many of its bytes are unshipped
+    uint64_t round_bytes = 0;  // ship once this many new bytes are staged across writers
+    uint64_t writer_cap = 0;   // a writer blocks in write() while this many of its bytes are unshipped
+    uint64_t arena_cap = 0;    // device bytes per writer
     std::chrono::microseconds wait{0};
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr, copy = nullptr;
 
-    std::mutex mu;
+    std::mutex mu;                     // open list, pool, writer cut state (lock order: mu, then a writer's mu)
     std::condition_variable cv_round;  // round thread: work arrived
-    std::condition_variable cv_done;   // writers: a round finished
+    std::condition_variable cv_done;   // finishing writers: a round completed
     std::vector<kcdc_bw*> open;        // writers not yet freed
     std::vector<uint8_t*> pool;        // free pinned blocks
-    uint64_t staged = 0;               // unshipped bytes over all writers
-    std::chrono::steady_clock::time_point since;  // when `staged` last became nonzero
-    uint32_t capped = 0;               // writers blocked on their staging cap (a round is due)
+    std::atomic<uint64_t> staged{0};   // unshipped bytes over all writers
+    std::atomic<int64_t> since{0};     // when `staged` last became nonzero (steady ns)
+    std::atomic<uint32_t> capped{0};   // writers blocked on their staging cap (a round is due)
+    std::atomic<uint32_t> finish_pending{0};  // finishing writers whose last region is not issued
     uint64_t rounds = 0;
-    // observability (kcdc_bw_stats): bytes shipped, seconds in the round thread's phases
-    uint64_t shipped_bytes = 0;
-    double t_submit = 0, t_wait = 0;
     bool stop = false;
-    int error = 0;
+    std::atomic<int> error{0};
     std::string errmsg;
     std::thread th;
 
-    // device: ping-pong region buffers (tails + new bytes of every writer), metadata
-    uint8_t* dreg[2] = {nullptr, nullptr};
-    size_t dreg_cap[2] = {0, 0};
-    int cur = 0;
-    uint64_t* dmeta = nullptr;  // ptrs | lens | starts | cut_base | counts | cuts
-    size_t dmeta_cap = 0;
-    uint64_t* hmeta = nullptr;  // pinned mirror
-    size_t hmeta_cap = 0;
+    // per-round device/pinned metadata, two sets (round k+1 is built while round k is in flight)
+    struct Meta {
+        uint64_t* d = nullptr;  // ptrs | lens | starts | cut_base | resume | counts | cuts
+        uint64_t* h = nullptr;  // pinned mirror
+        size_t cap = 0;         // words
+        Piece* dp = nullptr;    // gather pieces
+        Piece* hp = nullptr;
+        size_t pcap = 0;
+        hipEvent_t gathered = nullptr, g0 = nullptr, k0 = nullptr, done = nullptr;
+    } meta[2];
+
+    // observability (kcdc_bw_stats)
+    uint64_t shipped_bytes = 0;
+    double t_submit = 0, t_wait = 0, t_gather = 0, t_kernel = 0;
+    double t_seg[5] = {0, 0, 0, 0, 0};  // host seconds per round phase: collect, place, gather issue, wait, launch
+    hipEvent_t ev_ref = nullptr;                   // recorded once: the origin of the intervals below
+    std::vector<std::pair<float, float>> busy;     // device intervals (ms after ev_ref) of gathers and splits
 
     ~kcdc_bw_batcher() {
         Guard g(device);
         for (uint8_t* b : pool) (void)hipHostFree(b);
-        for (auto* p : dreg)
-            if (p) (void)hipFree(p);
-        if (dmeta) (void)hipFree(dmeta);
-        if (hmeta) (void)hipHostFree(hmeta);
+        for (Meta& m : meta) {
+            if (m.d) (void)hipFree(m.d);
+            if (m.h) (void)hipHostFree(m.h);
+            if (m.dp) (void)hipFree(m.dp);
+            if (m.hp) (void)hipHostFree(m.hp);
+            for (hipEvent_t e : {m.gathered, m.g0, m.k0, m.done})
+                if (e) (void)hipEventDestroy(e);
+        }
+        if (ev_ref) (void)hipEventDestroy(ev_ref);
+        if (copy) (void)hipStreamDestroy(copy);
         if (stream) (void)hipStreamDestroy(stream);
     }
     uint8_t* get_block() {  // mu held
@@ -106,225 +193,338 @@ struct kcdc_bw_batcher {
         Guard g(device);
         return hipHostMalloc(&p, kBlock, hipHostMallocDefault) == hipSuccess ? static_cast<uint8_t*>(p) : nullptr;
     }
-    int run_round(std::unique_lock<std::mutex>& lk);
     void loop();
 };
 
 struct kcdc_bw {
     kcdc_bw_batcher* b = nullptr;
-    // host staging: bytes [shipped, written) in blocks (the last one filled up to `fill`)
-    std::vector<uint8_t*> blocks;
-    size_t fill = 0;
-    uint64_t written = 0, shipped = 0;
-    // device tail: stream bytes [tail_pos, shipped) at dtail (inside the batcher's region buffer)
-    const uint8_t* dtail = nullptr;
-    uint64_t tail_pos = 0;
-    uint64_t frontier = 0;          // last final cut (0: none yet)
-    std::vector<uint64_t> ready;    // final cuts not taken yet
+    std::mutex mu;               // staging (the writer's thread vs the round thread's collection)
+    std::condition_variable cv;  // write(): bytes were shipped
+    std::vector<Blk> blocks;     // unshipped bytes [shipped, written); only the last may be partial
+    uint64_t written = 0;        // (mu)
+    uint64_t shipped = 0;        // bytes handed to a round (mu)
+    bool finishing = false;      // (mu)
+    // round thread (and batcher mu for what writers read):
+    uint8_t* arena = nullptr;    // device: stream byte p at arena + (p - origin)
+    uint8_t* spare = nullptr;    // the other arena: compaction copies the live bytes over and swaps
+    uint64_t origin = 0;
+    uint64_t tail_pos = 0;       // first byte the next region needs (last final cut - 64)
+    uint64_t launched_to = 0;    // end of the last completed region (the chunk in progress was tested up to it)
+    uint64_t frontier = 0;       // last final cut (0: none yet)
+    bool final_sent = false;     // the finishing region is issued
+    std::vector<uint64_t> ready; // final cuts not taken yet (batcher mu)
     size_t ready_head = 0;
-    bool finishing = false, done = false;
-    bool copying = false;           // write() is copying into its last block (lock dropped)
-    uint64_t fixed_next = 0;        // FIXED names: the next cut (no data is read)
+    bool done = false;           // (batcher mu)
+    uint64_t fixed_next = 0;     // FIXED names: the next cut (no data is read)
 };
 
-// One round (called by the round thread with `lk` held; drops it while the device works).
-int kcdc_bw_batcher::run_round(std::unique_lock<std::mutex>& lk) {
-    struct Job {
-        kcdc_bw* w;
-        std::vector<uint8_t*> blocks;
-        uint64_t new_bytes, tail_len, off;  // off: region offset in the new buffer
-        bool finishing, launch;
-    };
+namespace {
+struct SrcPiece {
+    const uint8_t* src;
+    uint64_t pos, len;  // stream position of the first byte
+};
+struct Job {
+    kcdc_bw* w;
+    uint64_t to;  // region end (shipped after this round)
+    bool finishing;
+    std::vector<SrcPiece> pcs;
+    std::vector<uint8_t*> retire;  // blocks fully shipped by this round (free after its gather)
+};
+struct Round {
+    int m = 0;  // meta set
     std::vector<Job> jobs;
-    for (kcdc_bw* w : open) {
-        if (w->done) continue;
-        if (w->copying) {  // its staged bytes wait for the next round; the tail still moves
-            if (w->shipped > w->tail_pos) jobs.push_back(Job{w, {}, 0, w->shipped - w->tail_pos, 0, false, false});
-            continue;
-        }
-        Job j{w, {}, w->written - w->shipped, w->shipped - w->tail_pos, 0, w->finishing, false};
-        j.blocks.swap(w->blocks);
-        w->fill = 0;
-        w->shipped = w->written;
-        staged -= j.new_bytes;
-        // launch it when it has new bytes past what a final cut could need, or finishes
-        j.launch = j.finishing || j.new_bytes > 0;
-        if (j.launch || j.tail_len) jobs.push_back(std::move(j));
-    }
-    rounds++;
-    lk.unlock();
-    cv_done.notify_all();  // writers blocked on their staging cap may continue
-
-    int rc = KCDC_OK;
-    uint64_t total = 0, fresh = 0;
-    for (Job& j : jobs) {
-        j.off = total;
-        total += align16(j.tail_len + j.new_bytes);
-        fresh += j.new_bytes;
-    }
-    const auto t0 = std::chrono::steady_clock::now();
-    const int nxt = cur ^ 1;
-    Guard g(device);
-    auto fail = [&](hipError_t e, const char* what) { rc = hip_err(e, what); };
-    if (dreg_cap[nxt] < total) {
-        if (dreg[nxt]) (void)hipFree(dreg[nxt]);
-        dreg[nxt] = nullptr;
-        dreg_cap[nxt] = 0;
-        const size_t want = std::max<size_t>(total + total / 4, 64u << 20);
-        hipError_t e = hipMalloc(&dreg[nxt], want);
-        if (e != hipSuccess) fail(e, "writer region buffer");
-        else dreg_cap[nxt] = want;
-    }
-    std::vector<uint32_t> li;  // jobs launched
-    for (uint32_t i = 0; i < jobs.size(); i++)
-        if (jobs[i].launch) li.push_back(i);
-    const uint32_t n = static_cast<uint32_t>(li.size());
-    uint64_t cuts_cap = 0;
-    std::vector<uint64_t> cbase(n);
-    for (uint32_t k = 0; k < n; k++) {
-        const Job& j = jobs[li[k]];
-        cbase[k] = cuts_cap;
-        cuts_cap += (j.tail_len + j.new_bytes) / algo->min_size() + 2;
-    }
-    const size_t meta_words = 5ull * n + cuts_cap + 1;
-    if (rc == KCDC_OK && dmeta_cap < meta_words) {
-        if (dmeta) (void)hipFree(dmeta);
-        if (hmeta) (void)hipHostFree(hmeta);
-        dmeta = hmeta = nullptr;
-        dmeta_cap = hmeta_cap = 0;
-        const size_t want = std::max<size_t>(meta_words * 2, 1u << 16);
-        hipError_t e = hipMalloc(&dmeta, want * 8);
-        if (e == hipSuccess) e = hipHostMalloc(&hmeta, want * 8, hipHostMallocDefault);
-        if (e != hipSuccess) fail(e, "writer metadata");
-        else dmeta_cap = hmeta_cap = want;
-    }
-    if (rc == KCDC_OK) {
-        // tails (device to device) and new bytes (pinned host to device) into the new buffer
-        for (Job& j : jobs) {
-            uint8_t* dst = dreg[nxt] + j.off;
-            if (j.tail_len && rc == KCDC_OK) {
-                hipError_t e = hipMemcpyAsync(dst, j.w->dtail, j.tail_len, hipMemcpyDeviceToDevice, stream);
-                if (e != hipSuccess) fail(e, "writer tail copy");
-            }
-            uint64_t left = j.new_bytes, at = j.tail_len;
-            for (uint8_t* blk : j.blocks) {
-                const size_t k = left < kBlock ? static_cast<size_t>(left) : kBlock;
-                if (k && rc == KCDC_OK) {
-                    hipError_t e = hipMemcpyAsync(dst + at, blk, k, hipMemcpyHostToDevice, stream);
-                    if (e != hipSuccess) fail(e, "writer H2D");
-                }
-                at += k;
-                left -= k;
-            }
-        }
-    }
-    uint64_t* hp = hmeta;
-    if (rc == KCDC_OK && n) {
-        uint64_t* dp = dmeta;
-        for (uint32_t k = 0; k < n; k++) {
-            const Job& j = jobs[li[k]];
-            hp[k] = reinterpret_cast<uint64_t>(dreg[nxt] + j.off);                 // ptrs
-            hp[n + k] = j.tail_len + j.new_bytes;                                  // lens
-            hp[2 * n + k] = j.w->frontier - j.w->tail_pos;                         // starts
-            hp[3 * n + k] = cbase[k];                                              // cut_base
-        }
-        hipError_t e = hipMemcpyAsync(dp, hp, 4ull * n * 8, hipMemcpyHostToDevice, stream);
-        if (e != hipSuccess) fail(e, "writer metadata H2D");
-        if (rc == KCDC_OK) {
-            SplitArgs s;
-            s.ptrs = reinterpret_cast<const uint8_t* const*>(dp);
-            s.lens = dp + n;
-            s.starts = dp + 2 * n;
-            s.cut_base = dp + 3 * n;
-            s.counts = dp + 4 * n;
-            s.cuts = dp + 5 * n;
-            s.cuts_cap = cuts_cap;
-            s.nstreams = n;
-            rc = launch_split_batch(*algo, s, device, stream);
-        }
-        if (rc == KCDC_OK) {
-            e = hipMemcpyAsync(hp + 4 * n, dp + 4 * n, (n + cuts_cap) * 8, hipMemcpyDeviceToHost, stream);
-            if (e != hipSuccess) fail(e, "writer cuts D2H");
-        }
-    }
-    const auto t1 = std::chrono::steady_clock::now();
-    if (rc == KCDC_OK) {
-        hipError_t e = hipStreamSynchronize(stream);
-        if (e != hipSuccess) fail(e, "writer round");
-    }
-    const auto t2 = std::chrono::steady_clock::now();
-
-    lk.lock();
-    shipped_bytes += fresh;
-    t_submit += std::chrono::duration<double>(t1 - t0).count();
-    t_wait += std::chrono::duration<double>(t2 - t1).count();
-    for (Job& j : jobs)  // the H2D copies have completed (or failed): blocks back to the pool
-        for (uint8_t* blk : j.blocks) pool.push_back(blk);
-    if (rc != KCDC_OK) return rc;
-    for (uint32_t k = 0; k < n; k++) {
-        Job& j = jobs[li[k]];
-        kcdc_bw* w = j.w;
-        const uint64_t cnt = hp[4 * n + k];
-        if (cnt == ~0ull || cnt > (j.tail_len + j.new_bytes) / algo->min_size() + 2)
-            return set_error(KCDC_EIO, "writer round: the device lost a stream");
-        const uint64_t* c = hp + 5 * n + cbase[k];
-        const uint64_t fin = j.finishing ? cnt : (cnt ? cnt - 1 : 0);
-        for (uint64_t t = 0; t < fin; t++) w->ready.push_back(w->tail_pos + c[t]);
-        if (fin) w->frontier = w->tail_pos + c[fin - 1];
-        if (j.finishing) w->done = true;
-    }
-    for (Job& j : jobs) {  // new tails: [frontier - 64, shipped) inside the new buffer
-        kcdc_bw* w = j.w;
-        const uint64_t keep = w->frontier >= kHist ? w->frontier - kHist : 0;
-        w->dtail = dreg[nxt] + j.off + (keep - w->tail_pos);
-        w->tail_pos = keep;
-    }
-    cur = nxt;
-    return KCDC_OK;
-}
+    uint32_t n = 0;
+    std::vector<uint64_t> cbase;
+    uint64_t fresh = 0;
+    bool live = false;
+};
+}  // namespace
 
 void kcdc_bw_batcher::loop() {
+    Guard g(device);
+    Round inflight;
+    int next_meta = 0;
+    auto fail = [&](int rc) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!error) {
+            errmsg = kcdc_last_error();
+            error = rc;
+        }
+        cv_done.notify_all();
+        for (kcdc_bw* w : open) {
+            std::lock_guard<std::mutex> wl(w->mu);
+            w->cv.notify_all();
+        }
+    };
+    // Wait for round r's cuts and apply them (final cuts, frontier, tail position).  mu not held.
+    auto complete = [&](Round& r) -> int {
+        if (!r.live) return KCDC_OK;
+        r.live = false;
+        Meta& M = meta[r.m];
+        const auto t0 = std::chrono::steady_clock::now();
+        hipError_t e = hipEventSynchronize(M.done);
+        t_wait += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (e != hipSuccess) return hip_err(e, "writer round");
+        float gms = 0, kms = 0, a = 0, z = 0;
+        if (hipEventElapsedTime(&gms, M.g0, M.gathered) == hipSuccess) {
+            t_gather += gms * 1e-3;
+            if (hipEventElapsedTime(&a, ev_ref, M.g0) == hipSuccess) busy.emplace_back(a, a + gms);
+        }
+        if (r.n && hipEventElapsedTime(&kms, M.k0, M.done) == hipSuccess) {
+            t_kernel += kms * 1e-3;
+            if (hipEventElapsedTime(&z, ev_ref, M.k0) == hipSuccess) busy.emplace_back(z, z + kms);
+        }
+        const uint32_t n = r.n;
+        const uint64_t* hp = M.h;
+        std::lock_guard<std::mutex> lk(mu);
+        shipped_bytes += r.fresh;
+        for (uint32_t k = 0; k < n; k++) {
+            Job& j = r.jobs[k];
+            kcdc_bw* w = j.w;
+            for (uint8_t* blk : j.retire) pool.push_back(blk);
+            const uint64_t len = j.to - w->tail_pos;
+            const uint64_t cnt = hp[5 * n + k];
+            if (cnt == ~0ull || cnt > len / algo->min_size() + 2)
+                return set_error(KCDC_EIO, "writer round: the device lost a stream");
+            const uint64_t* c = hp + 6 * n + r.cbase[k];
+            const uint64_t fin = j.finishing ? cnt : (cnt ? cnt - 1 : 0);
+            for (uint64_t t = 0; t < fin; t++) w->ready.push_back(w->tail_pos + c[t]);
+            if (fin) w->frontier = w->tail_pos + c[fin - 1];
+            w->launched_to = j.to;
+            w->tail_pos = w->frontier >= kHist ? w->frontier - kHist : 0;
+            if (j.finishing) w->done = true;
+        }
+        cv_done.notify_all();
+        return KCDC_OK;
+    };
+
     std::unique_lock<std::mutex> lk(mu);
     auto last = std::chrono::steady_clock::now();
     for (;;) {
         auto work = [&] {
-            if (stop || error) return true;
-            if (staged >= round_bytes || capped) return true;
-            for (kcdc_bw* w : open)
-                if (w->finishing && !w->done) return true;
-            return false;
+            return stop || error || staged.load() >= round_bytes || capped.load() > 0 || finish_pending.load() > 0;
         };
         // Ship when a round's worth is staged, a writer is blocked on its cap or finishing, or
-        // max_wait after the first unshipped byte (or after the last round) -- whichever is first.
-        // Writers wake this thread when `staged` leaves 0, so the timed wait always starts.
-        while (!work()) {
-            if (staged > 0) {
-                const auto due = std::max(last, since) + wait;
+        // max_wait after the first unshipped byte (or after the last round).  Meanwhile apply
+        // the round in flight as soon as the device has finished it (its writers may be waiting
+        // for cuts) -- but do not block on it: the next round's gather should start while it splits.
+        bool timed_out = false;
+        while (!work() && !timed_out) {
+            if (inflight.live) {
+                if (hipEventQuery(meta[inflight.m].done) == hipSuccess) {
+                    lk.unlock();
+                    const int rc = complete(inflight);
+                    lk.lock();
+                    if (rc != KCDC_OK) {
+                        lk.unlock();
+                        fail(rc);
+                        lk.lock();
+                    }
+                } else {
+                    cv_round.wait_for(lk, std::chrono::microseconds(100), work);
+                }
+                continue;
+            }
+            if (staged.load() > 0) {
+                const auto since_tp = std::chrono::steady_clock::time_point(std::chrono::nanoseconds(since.load()));
+                const auto due = std::max(last, since_tp) + wait;
                 if (cv_round.wait_until(lk, due, work)) break;
-                if (std::chrono::steady_clock::now() >= due) break;
+                timed_out = std::chrono::steady_clock::now() >= due;
             } else {
-                cv_round.wait(lk, [&] { return work() || staged > 0; });
+                cv_round.wait(lk, [&] { return work() || staged.load() > 0; });
             }
         }
-        if (stop && staged == 0) {
-            bool pending = false;
-            for (kcdc_bw* w : open) pending = pending || (w->finishing && !w->done);
-            if (!pending) break;
-        }
         if (error) break;
-        if (staged == 0) {
-            bool pending = false;
-            for (kcdc_bw* w : open) pending = pending || (w->finishing && !w->done);
-            if (!pending) continue;
+        if (staged.load() == 0 && finish_pending.load() == 0) {
+            if (stop) break;
+            continue;
         }
-        const int rc = run_round(lk);
+        // ---- collect round R: every writer's staged bytes (writers keep writing meanwhile)
+        const auto t0 = std::chrono::steady_clock::now();
+        Round R;
+        R.m = next_meta;
+        struct Move {
+            uint8_t* dst;
+            const uint8_t* src;
+            uint64_t len;
+        };
+        std::vector<Move> compact;
+        bool overflow = false;
+        for (kcdc_bw* w : open) {
+            if (w->done || w->final_sent) continue;
+            std::lock_guard<std::mutex> wl(w->mu);
+            const uint64_t to = w->written;
+            if (to == w->shipped && !w->finishing) continue;
+            Job j{w, to, w->finishing, {}, {}};
+            for (size_t i = 0; i < w->blocks.size(); i++) {
+                Blk& bk = w->blocks[i];
+                if (bk.end > bk.start) j.pcs.push_back(SrcPiece{bk.p + bk.start, bk.pos, bk.end - bk.start});
+                bk.pos += bk.end - bk.start;
+                bk.start = bk.end;
+                if (bk.end == kBlock || i + 1 < w->blocks.size()) j.retire.push_back(bk.p);
+            }
+            if (!w->blocks.empty() && w->blocks.back().end < kBlock) {  // the writer keeps filling it
+                const Blk keep = w->blocks.back();
+                w->blocks.assign(1, keep);
+            } else {
+                w->blocks.clear();
+            }
+            staged -= to - w->shipped;
+            R.fresh += to - w->shipped;
+            w->shipped = to;
+            w->cv.notify_all();
+            if (w->finishing) {
+                w->final_sent = true;
+                finish_pending--;
+            }
+            if (to - w->origin > arena_cap) {
+                // compact: the live bytes [tail_pos, shipped before this round) -- a superset of what
+                // the round in flight will leave -- to the spare arena (congruent mod 16), queued on
+                // the copy stream after the in-flight gather; the round in flight keeps reading the
+                // old arena, so nothing waits for it
+                const uint64_t from = w->tail_pos, norigin = from & ~uint64_t(15);
+                const uint64_t have = j.pcs.empty() ? to - from : j.pcs.front().pos - from;
+                compact.push_back({w->spare + (from - norigin), w->arena + (from - w->origin), have});
+                std::swap(w->arena, w->spare);
+                w->origin = norigin;
+                if (to - w->origin > arena_cap) overflow = true;
+            }
+            R.jobs.push_back(std::move(j));
+        }
+        rounds++;
+        lk.unlock();
+        auto lap = [&, tp = std::chrono::steady_clock::now()](int i) mutable {
+            const auto t = std::chrono::steady_clock::now();
+            t_seg[i] += std::chrono::duration<double>(t - tp).count();
+            tp = t;
+        };
+        t_seg[0] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        int rc = overflow ? set_error(KCDC_EIO, "writer arena overflow") : KCDC_OK;
+        for (const Move& mv : compact) {
+            if (rc != KCDC_OK || !mv.len) continue;
+            hipError_t e = hipMemcpyAsync(mv.dst, mv.src, mv.len, hipMemcpyDeviceToDevice, copy);
+            if (e != hipSuccess) rc = hip_err(e, "writer arena compaction");
+        }
+        std::vector<Piece> pieces;
+        uint64_t tasks = 0;
+        for (Job& j : R.jobs) {
+            for (const SrcPiece& sp : j.pcs) {
+                pieces.push_back(Piece{sp.src, j.w->arena + (sp.pos - j.w->origin), sp.len, tasks});
+                tasks += (sp.len + kTask - 1) / kTask;
+            }
+        }
+        Meta& M = meta[R.m];
+        lap(1);
+        if (rc == KCDC_OK && M.pcap < pieces.size()) {
+            if (M.dp) (void)hipFree(M.dp);
+            if (M.hp) (void)hipHostFree(M.hp);
+            M.dp = M.hp = nullptr;
+            M.pcap = 0;
+            const size_t want = std::max<size_t>(pieces.size() * 2, 1024);
+            hipError_t e = hipMalloc(&M.dp, want * sizeof(Piece));
+            if (e == hipSuccess) e = hipHostMalloc(&M.hp, want * sizeof(Piece), hipHostMallocDefault);
+            if (e != hipSuccess) rc = hip_err(e, "writer gather list");
+            else M.pcap = want;
+        }
+        if (rc == KCDC_OK) {
+            hipError_t e = hipEventRecord(M.g0, copy);
+            if (e == hipSuccess && !pieces.empty()) {
+                std::memcpy(M.hp, pieces.data(), pieces.size() * sizeof(Piece));
+                e = hipMemcpyAsync(M.dp, M.hp, pieces.size() * sizeof(Piece), hipMemcpyHostToDevice, copy);
+                if (e == hipSuccess) {
+                    const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(tasks, kGatherWGs));
+                    hipLaunchKernelGGL(bw_gather_kernel, dim3(grid), dim3(256), 0, copy, M.dp,
+                                       static_cast<uint32_t>(pieces.size()), tasks);
+                    e = hipGetLastError();
+                }
+            }
+            if (e == hipSuccess) e = hipEventRecord(M.gathered, copy);
+            if (e != hipSuccess) rc = hip_err(e, "writer gather");
+        }
+        lap(2);
+        // round k's cuts are round k+1's chunk starts
+        if (rc == KCDC_OK && inflight.live) rc = complete(inflight);
+        lap(3);
+        // ---- launch R over every job's region [tail_pos, to)
+        if (rc == KCDC_OK) {
+            const uint32_t n = static_cast<uint32_t>(R.jobs.size());
+            R.n = n;
+            R.cbase.resize(n);
+            uint64_t cuts_cap = 0;
+            for (uint32_t k = 0; k < n; k++) {
+                R.cbase[k] = cuts_cap;
+                cuts_cap += (R.jobs[k].to - R.jobs[k].w->tail_pos) / algo->min_size() + 2;
+            }
+            const size_t words = 6ull * n + cuts_cap + 1;
+            if (M.cap < words) {
+                if (M.d) (void)hipFree(M.d);
+                if (M.h) (void)hipHostFree(M.h);
+                M.d = M.h = nullptr;
+                M.cap = 0;
+                const size_t want = std::max<size_t>(words * 2, 1u << 16);
+                hipError_t e = hipMalloc(&M.d, want * 8);
+                if (e == hipSuccess) e = hipHostMalloc(&M.h, want * 8, hipHostMallocDefault);
+                if (e != hipSuccess) rc = hip_err(e, "writer metadata");
+                else M.cap = want;
+            }
+            if (rc == KCDC_OK && n) {
+                uint64_t* hp = M.h;
+                for (uint32_t k = 0; k < n; k++) {
+                    kcdc_bw* w = R.jobs[k].w;
+                    hp[k] = reinterpret_cast<uint64_t>(w->arena + (w->tail_pos - w->origin));  // ptrs
+                    hp[n + k] = R.jobs[k].to - w->tail_pos;                                      // lens
+                    hp[2 * n + k] = w->frontier - w->tail_pos;                                   // starts
+                    hp[3 * n + k] = R.cbase[k];                                                  // cut_base
+                    // the chunk in progress was tested up to the last completed region's end
+                    hp[4 * n + k] = w->launched_to > w->tail_pos ? w->launched_to - w->tail_pos : 0;  // resume
+                }
+                uint64_t* dp = M.d;
+                hipError_t e = hipStreamWaitEvent(stream, M.gathered, 0);
+                if (e == hipSuccess) e = hipEventRecord(M.k0, stream);
+                if (e == hipSuccess) e = hipMemcpyAsync(dp, hp, 5ull * n * 8, hipMemcpyHostToDevice, stream);
+                if (e != hipSuccess) rc = hip_err(e, "writer metadata H2D");
+                if (rc == KCDC_OK) {
+                    SplitArgs s;
+                    s.ptrs = reinterpret_cast<const uint8_t* const*>(dp);
+                    s.lens = dp + n;
+                    s.starts = dp + 2 * n;
+                    s.cut_base = dp + 3 * n;
+                    s.resume = dp + 4 * n;
+                    s.counts = dp + 5 * n;
+                    s.cuts = dp + 6 * n;
+                    s.cuts_cap = cuts_cap;
+                    s.nstreams = n;
+                    rc = launch_split_batch(*algo, s, device, stream);
+                }
+                if (rc == KCDC_OK) {
+                    e = hipMemcpyAsync(hp + 5 * n, dp + 5 * n, (n + cuts_cap) * 8, hipMemcpyDeviceToHost, stream);
+                    if (e == hipSuccess) e = hipEventRecord(M.done, stream);
+                    if (e != hipSuccess) rc = hip_err(e, "writer cuts D2H");
+                }
+            } else if (rc == KCDC_OK) {
+                hipError_t e = hipEventRecord(M.done, copy);
+                if (e != hipSuccess) rc = hip_err(e, "writer round event");
+            }
+        }
+        lap(4);
+        t_submit += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         last = std::chrono::steady_clock::now();
         if (rc != KCDC_OK) {
-            error = rc;
-            errmsg = kcdc_last_error();
+            fail(rc);
+            lk.lock();
+            break;
         }
-        cv_done.notify_all();
+        R.live = true;
+        inflight = std::move(R);
+        next_meta ^= 1;
+        lk.lock();
     }
+    lk.unlock();
+    if (inflight.live && !error) {
+        const int rc = complete(inflight);
+        if (rc != KCDC_OK) fail(rc);
+    }
+    lk.lock();
     cv_done.notify_all();
 }
 
@@ -344,7 +544,10 @@ extern "C" kcdc_bw_batcher* kcdc_bw_batcher_new(const char* name, int device, ui
     b->algo = a;
     b->device = device;
     b->round_bytes = round_bytes ? round_bytes : (256ull << 20);
-    b->writer_cap = std::max<uint64_t>(b->round_bytes / 2, 4ull * kBlock);
+    b->writer_cap = std::max<uint64_t>(b->round_bytes / 8, 4ull * kBlock);
+    // two arenas per writer, each: the chunk in progress (+ window) and up to four caps of new
+    // bytes between compactions (a compaction needs room for the tail and two rounds' bytes)
+    b->arena_cap = (a->max_size() + kHist + 4 * (b->writer_cap + kBlock) + 4095) & ~uint64_t(4095);
     b->wait = std::chrono::microseconds(max_wait_us ? max_wait_us : 2000);
     if (a->kind != kFixed) {
         Guard g(device);
@@ -353,9 +556,18 @@ extern "C" kcdc_bw_batcher* kcdc_bw_batcher_new(const char* name, int device, ui
             delete b;
             return nullptr;
         }
-        hipError_t e = hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
+        // the splits (short, on the round's critical path) go first when both streams have work
+        int prio_lo = 0, prio_hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+        hipError_t e = hipStreamCreateWithPriority(&b->stream, hipStreamNonBlocking, prio_hi);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->copy, hipStreamNonBlocking);
+        for (auto& m : b->meta)
+            for (hipEvent_t* ev : {&m.gathered, &m.g0, &m.k0, &m.done})
+                if (e == hipSuccess) e = hipEventCreate(ev);
+        if (e == hipSuccess) e = hipEventCreate(&b->ev_ref);
+        if (e == hipSuccess) e = hipEventRecord(b->ev_ref, b->stream);
         if (e != hipSuccess) {
-            hip_err(e, "writer stream");
+            hip_err(e, "writer streams");
             delete b;
             return nullptr;
         }
@@ -373,6 +585,11 @@ extern "C" void kcdc_bw_batcher_free(kcdc_bw_batcher* b) {
     b->cv_round.notify_all();
     if (b->th.joinable()) b->th.join();
     for (kcdc_bw* w : b->open) w->b = nullptr;  // writers not freed: unusable from now on
+    if (b->algo->kind != kFixed) {
+        Guard g(b->device);
+        (void)hipStreamSynchronize(b->stream);
+        (void)hipStreamSynchronize(b->copy);
+    }
     delete b;
 }
 
@@ -384,6 +601,20 @@ extern "C" kcdc_bw* kcdc_bw_open(kcdc_bw_batcher* b) {
     auto* w = new kcdc_bw();
     w->b = b;
     w->fixed_next = b->algo->kind == kFixed ? b->algo->avg : 0;
+    if (b->algo->kind != kFixed) {
+        Guard g(b->device);
+        void *p = nullptr, *q = nullptr;
+        hipError_t e = hipMalloc(&p, b->arena_cap);
+        if (e == hipSuccess) e = hipMalloc(&q, b->arena_cap);
+        if (e != hipSuccess) {
+            if (p) (void)hipFree(p);
+            hip_err(e, "writer arena");
+            delete w;
+            return nullptr;
+        }
+        w->arena = static_cast<uint8_t*>(p);
+        w->spare = static_cast<uint8_t*>(q);
+    }
     std::lock_guard<std::mutex> lk(b->mu);
     b->open.push_back(w);
     return w;
@@ -392,10 +623,9 @@ extern "C" kcdc_bw* kcdc_bw_open(kcdc_bw_batcher* b) {
 extern "C" int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len) {
     if (!w || !w->b) return set_error(KCDC_EINVAL, "writer not open");
     kcdc_bw_batcher* b = w->b;
-    std::unique_lock<std::mutex> lk(b->mu);
-    if (w->finishing) return set_error(KCDC_EINVAL, "write after finish");
-    if (b->error) return set_error(b->error, b->errmsg);
     if (b->algo->kind == kFixed) {  // splitter_fixed.go:15-26: no data is read
+        std::lock_guard<std::mutex> lk(b->mu);
+        if (w->finishing) return set_error(KCDC_EINVAL, "write after finish");
         w->written += len;
         while (w->fixed_next <= w->written) {
             w->ready.push_back(w->fixed_next);
@@ -403,37 +633,42 @@ extern "C" int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len) {
         }
         return KCDC_OK;
     }
+    std::unique_lock<std::mutex> wl(w->mu);
+    if (w->finishing) return set_error(KCDC_EINVAL, "write after finish");
     while (len) {
-        // backpressure: at most writer_cap unshipped bytes per writer (a capped writer asks for
-        // a round at once: with few writers `staged` may never reach round_bytes)
+        if (b->error) return set_error(b->error, b->errmsg);  // errmsg is set before error
+        // backpressure: at most writer_cap unshipped bytes (a capped writer asks for a round at
+        // once: with few writers `staged` may never reach round_bytes)
         if (w->written - w->shipped >= b->writer_cap) {
             b->capped++;
             b->cv_round.notify_one();
-            b->cv_done.wait(lk, [&] { return b->error || w->written - w->shipped < b->writer_cap; });
+            w->cv.wait(wl, [&] { return b->error || w->written - w->shipped < b->writer_cap; });
             b->capped--;
+            continue;
         }
-        if (b->error) return set_error(b->error, b->errmsg);
-        if (w->blocks.empty() || w->fill == kBlock) {
-            uint8_t* blk = b->get_block();
+        if (w->blocks.empty() || w->blocks.back().end == kBlock) {
+            wl.unlock();  // lock order: the batcher's mutex is never taken under a writer's
+            uint8_t* blk;
+            {
+                std::lock_guard<std::mutex> lk(b->mu);
+                blk = b->get_block();
+            }
+            wl.lock();
             if (!blk) return set_error(KCDC_ENOMEM, "pinned staging block");
-            w->blocks.push_back(blk);
-            w->fill = 0;
+            Blk nb;
+            nb.p = blk;
+            nb.start = nb.end = static_cast<uint32_t>(w->written & 15u);  // congruent with the arena mod 16
+            nb.pos = w->written;
+            w->blocks.push_back(nb);
         }
-        const size_t k = std::min(len, kBlock - w->fill);
-        uint8_t* dst = w->blocks.back() + w->fill;
-        // Copy outside the lock; while `copying` the round thread leaves this writer's blocks
-        // alone (it still moves the device tail), and the bytes count only once they landed.
-        w->copying = true;
-        lk.unlock();
-        std::memcpy(dst, p, k);
-        lk.lock();
-        w->copying = false;
-        w->fill += k;
+        Blk& bk = w->blocks.back();
+        const size_t k = std::min<size_t>(len, kBlock - bk.end);
+        std::memcpy(bk.p + bk.end, p, k);
+        bk.end += static_cast<uint32_t>(k);
         w->written += k;
-        const bool first = b->staged == 0;
-        if (first) b->since = std::chrono::steady_clock::now();
-        b->staged += k;
-        if (first || b->staged >= b->round_bytes) b->cv_round.notify_one();
+        const uint64_t before = b->staged.fetch_add(k);
+        if (before == 0) b->since = now_ns();
+        if (before == 0 || before + k >= b->round_bytes) b->cv_round.notify_one();
         p += k;
         len -= k;
     }
@@ -458,16 +693,23 @@ extern "C" int64_t kcdc_bw_cuts(kcdc_bw* w, uint64_t* out, uint64_t cap) {
 extern "C" int kcdc_bw_finish(kcdc_bw* w) {
     if (!w || !w->b) return set_error(KCDC_EINVAL, "writer not open");
     kcdc_bw_batcher* b = w->b;
-    std::unique_lock<std::mutex> lk(b->mu);
     if (b->algo->kind == kFixed) {
+        std::lock_guard<std::mutex> lk(b->mu);
+        if (w->finishing) return KCDC_OK;
         const uint64_t last = w->ready.empty() ? w->fixed_next - b->algo->avg : w->ready.back();
         if (w->written > last) w->ready.push_back(w->written);  // the trailing chunk
         w->finishing = w->done = true;
         return KCDC_OK;
     }
-    // A staging copy that raced the lock must have landed: calls on one writer are serialised.
-    w->finishing = true;
+    {
+        std::lock_guard<std::mutex> wl(w->mu);
+        if (!w->finishing) {
+            w->finishing = true;
+            b->finish_pending++;
+        }
+    }
     b->cv_round.notify_one();
+    std::unique_lock<std::mutex> lk(b->mu);
     b->cv_done.wait(lk, [&] { return w->done || b->error; });
     return b->error && !w->done ? set_error(b->error, b->errmsg) : KCDC_OK;
 }
@@ -476,15 +718,21 @@ extern "C" void kcdc_bw_free(kcdc_bw* w) {
     if (!w) return;
     kcdc_bw_batcher* b = w->b;
     if (b) {
-        std::unique_lock<std::mutex> lk(b->mu);
-        if (!w->done && b->algo->kind != kFixed && !b->error) {  // abandoned object: drop its bytes
-            w->finishing = true;
-            b->cv_round.notify_one();
-            b->cv_done.wait(lk, [&] { return w->done || b->error; });
-        }
-        for (uint8_t* blk : w->blocks) b->pool.push_back(blk);
-        if (!w->done) b->staged -= w->written - w->shipped;
+        // an abandoned object: split (and drop) what it staged, so no round still reads its arena
+        if (b->algo->kind != kFixed && !b->error) (void)kcdc_bw_finish(w);
+        std::lock_guard<std::mutex> lk(b->mu);
+        for (Blk& bk : w->blocks) b->pool.push_back(bk.p);
         b->open.erase(std::find(b->open.begin(), b->open.end(), w));
+        if (w->arena) {
+            Guard g(b->device);
+            (void)hipStreamSynchronize(b->copy);
+            (void)hipStreamSynchronize(b->stream);
+            (void)hipFree(w->arena);
+            (void)hipFree(w->spare);
+        }
+    } else if (w->arena) {
+        (void)hipFree(w->arena);
+        (void)hipFree(w->spare);
     }
     delete w;
 }
@@ -494,7 +742,29 @@ extern "C" int64_t kcdc_bw_rounds(const kcdc_bw_batcher* b) { return b ? static_
 extern "C" int kcdc_bw_stats(kcdc_bw_batcher* b, double* out, int n) {
     if (!b || !out) return set_error(KCDC_EINVAL, "null argument");
     std::lock_guard<std::mutex> lk(b->mu);
-    const double v[4] = {static_cast<double>(b->rounds), static_cast<double>(b->shipped_bytes), b->t_submit, b->t_wait};
-    for (int i = 0; i < n && i < 4; i++) out[i] = v[i];
-    return 4;
+    // device span from the first round's start to the last one's end, and the part of it in which
+    // a gather or a split ran (their union: overlapped rounds count once)
+    std::vector<std::pair<float, float>> iv = b->busy;
+    std::sort(iv.begin(), iv.end());
+    double span = 0, busy = 0;
+    if (!iv.empty()) {
+        float s0 = iv[0].first, e0 = iv[0].second, hi = iv[0].second;
+        for (size_t i = 1; i < iv.size(); i++) {
+            if (iv[i].first > e0) {
+                busy += e0 - s0;
+                s0 = iv[i].first;
+                e0 = iv[i].second;
+            } else {
+                e0 = std::max(e0, iv[i].second);
+            }
+            hi = std::max(hi, iv[i].second);
+        }
+        busy += e0 - s0;
+        span = hi - iv[0].first;
+    }
+    const double v[13] = {static_cast<double>(b->rounds), static_cast<double>(b->shipped_bytes), b->t_submit, b->t_wait,
+                          b->t_gather, b->t_kernel, span * 1e-3, busy * 1e-3,
+                          b->t_seg[0], b->t_seg[1], b->t_seg[2], b->t_seg[3], b->t_seg[4]};
+    for (int i = 0; i < n && i < 13; i++) out[i] = v[i];
+    return 13;
 }
