@@ -1,4 +1,8 @@
-// Kopia content compression on gfx950: the deflate family.
+// Kopia content compression on gfx950: the deflate family (deflate, gzip,
+// pgzip), S2 (s2-default/-better/-parallel-4/-8: Snappy elements in S2's framing format,
+// compressor_s2.go:20-23) and Zstandard (zstd, -fastest, -better-, -best-compression: RFC 8878
+// frames, compressor_zstd.go:15-18).  All three share the span/segment layout and the LZ77 parse
+// below; they differ in how a segment's literals and matches are written (lz_spans_kernel<FMT>).
 //
 // What the reference does per content (repo/content/content_manager_lock_free.go:42-73,
 // repo/compression/compressor.go:67-72, compressor_deflate.go:14-62):

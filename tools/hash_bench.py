@@ -20,7 +20,8 @@ def main():
     data = torch.randint(0, 256, (int(lens.sum()) + 64,), dtype=torch.uint8, device=dev)
     key = bytes(range(32))
     out = {}
-    for name in ("BLAKE2B-256-128", "BLAKE2S-256"):
+    names = sys.argv[1:] or kh.SupportedAlgorithms()
+    for name in names:
         kh.hash_chunks_device(name, data.data_ptr(), offs, lens, key, dev)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -30,7 +31,9 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         out[name] = round(e0.elapsed_time(e1) / 3, 2)
+    total = int(lens.sum())
     print(json.dumps({"lib": os.environ.get("KCDC_LIB", "default"), "ms": out, "chunks": len(lens),
+                      "bytes": total, "gib_s": {k: round(total / 2**30 / (v * 1e-3), 1) for k, v in out.items()},
                       "largest": int(lens.max())}))
 
 
