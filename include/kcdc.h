@@ -233,13 +233,18 @@ int kcdc_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint32
 int kcdc_gorand_read(int64_t seed, uint8_t* out, uint64_t n);
 
 /* ------------------------------------------------------------- content hashes
- * Keyed BLAKE2 of many chunks of device-resident bytes: the content hash Kopia computes
- * for every chunk the splitter cuts (repo/content/content_manager.go:812 ->
- * repo/hashing/hashing.go:78-101, truncatedKeyedHashFuncFactory).  Names as registered in
- * repo/hashing/blake_hashes.go:8-13: "BLAKE2B-256-128" (the default, hashing.go:51),
- * "BLAKE2B-256", "BLAKE2S-128", "BLAKE2S-256".
+ * The content hash Kopia computes for every chunk the splitter cuts, for many chunks of
+ * device-resident bytes (repo/content/content_manager.go:812 -> repo/hashing/hashing.go:55-103).
+ * Every registered name (hashing.SupportedAlgorithms(), sorted):
+ *   "BLAKE2B-256", "BLAKE2B-256-128" (the default, hashing.go:51), "BLAKE2S-128", "BLAKE2S-256"
+ *     keyed BLAKE2 (blake_hashes.go:8-13, truncatedKeyedHashFuncFactory);
+ *   "BLAKE3-256", "BLAKE3-256-128": blake3.NewKeyed(key), key = the secret's first 32 bytes, or
+ *     blake3.DeriveKey("kopia blake3 derived key v1", secret) for a shorter secret
+ *     (blake3_hashes.go:10-27);
+ *   "HMAC-SHA224", "HMAC-SHA256", "HMAC-SHA256-128", "HMAC-SHA3-224", "HMAC-SHA3-256":
+ *     hmac.New(sha*, secret), truncated (sha_hashes.go:9-15; any key length).
  * kcdc_hash_algorithms: fills names[0..cap) and returns the count.
- * kcdc_hash_size: output bytes per chunk (16 or 32), or KCDC_ENOENT.
+ * kcdc_hash_size: output bytes per chunk (16, 28 or 32), or KCDC_ENOENT.
  * kcdc_hash_chunks_device: chunk i is bytes [d_offsets[i], d_offsets[i] + d_lens[i]) of
  *   d_data (any alignment); its hash goes to d_out + i * out_stride (out_stride >= the hash
  *   size, a multiple of 4).  key: the repository's HMAC secret (<= 64 bytes for BLAKE2B,
@@ -297,14 +302,17 @@ int kcdc_decrypt_chunks_device(const char* algorithm, const uint8_t* secret, uin
                                void* hip_stream);
 
 /* ------------------------------------------------------------- content compression
- * Kopia's deflate, gzip and pgzip compressors (repo/compression/compressor_deflate.go:14-62,
- * compressor_gzip.go:15-17, compressor_pgzip.go:16-18; header IDs compression_ids.go:8-30) for many
- * chunks per call (gzip names: the stream inside an RFC 1952 member with its CRC-32 and ISIZE), with the content manager's keep-or-drop
- * rule (maybeCompressAndEncryptDataForPacking, repo/content/content_manager_lock_free.go:42-73):
- *   out_i = BE32(header ID) || raw DEFLATE stream (RFC 1951) of chunk i
+ * Kopia's compressors (header IDs compression_ids.go:8-30) for many chunks per call, with the
+ * content manager's keep-or-drop rule (maybeCompressAndEncryptDataForPacking,
+ * repo/content/content_manager_lock_free.go:42-73):
+ *   out_i = BE32(header ID) || the compressed stream of chunk i
  *   id_i  = header ID if len(out_i) < len(chunk i), else 0 (NoCompression: store chunk i as is)
- * Any RFC 1951 inflater (flate.NewReader in Decompress, compressor_deflate.go:64-78) reads out_i
- * after its 4 header bytes; the bytes are this encoder's, not klauspost/compress's.
+ * Streams: deflate-* raw DEFLATE (RFC 1951; compressor_deflate.go:14-62), gzip* / pgzip* the same
+ * stream in an RFC 1952 member with its CRC-32 and ISIZE (compressor_gzip.go:15-17,
+ * compressor_pgzip.go:16-18), s2-* the S2 framing format with CRC-32C-checked chunks of Snappy
+ * elements (compressor_s2.go:20-23), zstd* one RFC 8878 frame (compressor_zstd.go:15-18).  The
+ * reference's readers (flate/gzip/pgzip/s2/zstd NewReader) read out_i after its 4 header bytes;
+ * the bytes are this encoder's, not klauspost/compress's.
  * kcdc_compression_algorithms: the names encoded on the device; kcdc_compression_header_id: a
  *   name's header ID (or a negative error).
  * kcdc_compress_bound(len): the largest out_i for a chunk of len bytes (24 + len + 5 per 512 bytes).
