@@ -258,6 +258,10 @@ int kcdc_hash_chunks_device(const char* hash_name, const uint8_t* d_data, const 
                             uint32_t key_len, uint8_t* d_out, uint32_t out_stride, void* hip_stream);
 
 /* ------------------------------------------------------------- content encryption
+ * Side channels: the AES-256-GCM kernels look up AES T-tables and GHASH tables in LDS with key- and
+ * data-dependent indices (gfx950 has no AES or carry-less-multiply instructions), so they are not
+ * constant-time, unlike Go's AES-NI path; use them on a single-tenant GPU.  ChaCha20-Poly1305 has no
+ * table lookups.  
  * Kopia's two encryptors, AES256-GCM-HMAC-SHA256 (the default; repo/encryption/
  * aes256_gcm_hmac_sha256_encryptor.go:24-72) and CHACHA20-POLY1305-HMAC-SHA256
  * (chacha20_poly1305_hmac_sha256_encryptor.go: Encrypt/Decrypt/Overhead, 24-80; both through

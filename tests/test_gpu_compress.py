@@ -198,3 +198,18 @@ def test_tiny_chunks_frame(name, gpu):
     offs, lens = [0, 0, 3, 0], [0, 1, 4, 21]
     out, oo, ol, ids = _compress(name, host, offs, lens, gpu)
     _check(name, host, offs, lens, out, oo, ol, ids)
+
+
+def test_mixed_ratio_does_not_regress(gpu):
+    """Pins the device encoders' ratio on text-like data (DESIGN.md §2.7 measures 0.37-0.40; zlib
+    -6: 0.30): the levels order as their search effort, and no name falls past 0.42."""
+    host = _mixed(8 << 20, 31)
+    offs, lens = [i << 20 for i in range(8)], [1 << 20] * 8
+    ratio = {}
+    for name in ["deflate-best-speed", "deflate-default", "deflate-best-compression", "s2-default", "zstd"]:
+        out, oo, ol, ids = _compress(name, host, offs, lens, gpu)
+        _check(name, host, offs, lens, out, oo, ol, ids)
+        ratio[name] = float(ol.sum()) / host.size
+    assert ratio["deflate-default"] <= ratio["deflate-best-speed"], ratio
+    assert ratio["deflate-best-compression"] <= ratio["deflate-default"] + 1e-3, ratio
+    assert max(ratio.values()) < 0.42, ratio

@@ -141,7 +141,10 @@ def _beside_occupier(gpu, nwg, usec):
     _data, b = _streams(gpu, ns, L)
     batch.split_batch_device(NAME, b)  # warm (tables, workspaces)
     torch.cuda.synchronize()
-    sa, sb = torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)
+    # the batch on a high-priority stream: two default-priority streams may share a hardware
+    # queue (HIP assigns them round-robin as a process creates streams), which would serialise
+    # the batch behind the occupier whatever the kernel does
+    sa, sb = torch.cuda.Stream(gpu), torch.cuda.Stream(gpu, priority=-1)
     t0 = torch.cuda.Event(enable_timing=True)
     ea = torch.cuda.Event(enable_timing=True)
     eb = torch.cuda.Event(enable_timing=True)
