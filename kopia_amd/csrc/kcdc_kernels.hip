@@ -1896,6 +1896,15 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
 // (lane l reads replica l % 32, bank pair 2(l % 32); address = one v_perm of the leaving
 // byte), mod[] with 16 replicas at a 128-byte stride (lanes l and l+16 share a bank pair
 // only for indices of equal parity).  8 waves x 8 KiB slots + 96 KiB = 160 KiB.
+//
+// Bit-reversed state (round 3).  The hash v (53 bits, deg P = 53) is kept as R = bitreverse64(v)
+// in (hi, lo): v's bit j is R's bit 63 - j, so v's low bits -- the ones the cut test reads -- are
+// the TOP bits of hi, and `(v & mask) == 0` is `hi < 2^(32 - log2(avg))`: the running test is one
+// v_min3 per two bytes instead of a v_and + v_min per byte.  A roll v << 8 | c is R >> 8 with the
+// bit-reversed entering byte on top: hi' = one v_perm of hi and the byte (the input dwords are
+// bit-reversed once as they leave the step slot, so byte b of w sits bit-reversed in byte 3 - b),
+// lo' = one v_alignbit.  The reduction index (v's bits 45..52) is lo's bits 11..18, bit-reversed:
+// the tables are stored bit-reversed at bit-reversed rows.  8.9 -> ~7.9 VALU per byte.
 #ifndef KCDC_RK_MODREP
 #define KCDC_RK_MODREP 16  // mod[] replicas: 16 = 2-way conflicts, perm-addressed out[]; 32 = conflict-free mod[]
                            // but a 2-op out[] address: 3.01 vs 2.80 ms on config 2 (issue-bound)
@@ -1906,62 +1915,63 @@ constexpr int kRkModRep = KCDC_RK_MODREP;
 #endif
 constexpr int kRkOutRep = KCDC_RK_OUTREP;
 struct RkTables {
-    uint64_t mod[256 * kRkModRep];  // mod[i*R + r]: first, so its addresses fit the 16-bit ds offset
-    uint64_t out[256 * kRkOutRep];  // outx[b*R' + r] (rk_roll: out[] pre-shifted and pre-reduced)
+    uint64_t mod[256 * kRkModRep];  // row f (replicas at f*R + r): rev64(mod[rev8(f)]); first, so its
+                                    // addresses fit the 16-bit ds offset
+    uint64_t out[256 * kRkOutRep];  // row f: rev64(outx[rev8(f)]) (outx[] pre-shifted and pre-reduced)
 };
 static_assert(sizeof(RkTables) + sizeof(RkSlots) <= 160 * 1024, "Rabin-Karp tables + step slots exceed LDS");
-constexpr uint32_t kRkIdxBit = 13;  // u >> 45 = bits 13..20 of the high word (deg P = 53, host-checked)
+constexpr uint32_t kRkIdxBit = 11;  // the reduction index (v >> 45, bit-reversed) = lo bits 11..18
 
 struct RkCtx {
     const char* modb;  // LDS byte address of RkTables::mod
     const char* outb;  // LDS byte address of RkTables::out
     uint32_t lane8o;   // (lane % out replicas) * 8
     uint32_t lane8m;   // (lane % mod replicas) * 8
-    uint32_t mask;     // avg - 1
+    uint32_t thr;      // 2^(32 - log2(avg)): a position is a candidate iff hi < thr
 };
 
-__device__ __forceinline__ uint64_t rk_out(const RkCtx& k, uint32_t w, int b) {
-    uint32_t a;
-    if constexpr (kRkOutRep == 32) {  // (byte b of w) << 8 | lane8o: the replica address in one v_perm
-        a = __builtin_amdgcn_perm(w, k.lane8o, 0x0c0c0000u | ((4u + b) << 8));
-    } else {  // 16 replicas, 128-byte stride: (byte b of w) << 7 | lane8o
-        a = ((b == 0 ? (w << 7) : (w >> (8 * b - 7))) & 0x7F80u) | k.lane8o;
-    }
-#if KCDC_RK_ABL == 1
-    return static_cast<uint64_t>(a);
-#else
-    return *reinterpret_cast<const uint64_t*>(k.outb + a);
-#endif
+// The RK kernels' view of a step slot: read_step128, then every dword bit-reversed.
+__device__ __forceinline__ void rk_read_step128(const uint8_t* slot, int lane, int64_t c, int64_t off0,
+                                                uint32_t (&dw)[32]) {
+    read_step128(slot, lane, c, off0, dw);
+#pragma unroll
+    for (int i = 0; i < 32; i++) dw[i] = __builtin_bitreverse32(dw[i]);
 }
-// One roll with the leaving byte's out[] value already read: returns nothing, updates (hi, lo).
+
+// outx[] of the leaving byte b of a (bit-reversed) dword: its row is byte 3 - b.
+__device__ __forceinline__ uint64_t rk_out(const RkCtx& k, uint32_t w, int b) {
+    const int bb = 3 - b;
+    uint32_t a;
+    if constexpr (kRkOutRep == 32) {  // row << 8 | lane8o: the replica address in one v_perm
+        a = __builtin_amdgcn_perm(w, k.lane8o, 0x0c0c0000u | ((4u + bb) << 8));
+    } else {  // 16 replicas, 128-byte stride: row << 7 | lane8o
+        a = ((bb == 0 ? (w << 7) : (w >> (8 * bb - 7))) & 0x7F80u) | k.lane8o;
+    }
+    return *reinterpret_cast<const uint64_t*>(k.outb + a);
+}
+// v << 8 | c, high word: [hi.b1, hi.b2, hi.b3, the entering byte (byte 3 - b of the reversed dword)]
+constexpr uint32_t rk_in_sel(int b) { return 0x00030201u | (static_cast<uint32_t>(7 - b) << 24); }
+__device__ __forceinline__ uint32_t rk_mod_addr(const RkCtx& k, uint32_t lo) {
+    return (__builtin_amdgcn_ubfe(lo, kRkIdxBit, 8) << (kRkModRep == 32 ? 8 : 7)) | k.lane8m;
+}
+// One roll with the leaving byte's out[] value already read: updates (hi, lo).
 // Linearity folds the leaving byte's removal into one table read that is off the chain:
 // mod[] is GF(2)-linear in its index and idx(v ^ o) = idx(v) ^ idx(o), so
 //   ((v ^ o) << 8 | c) ^ mod[idx(v ^ o)] = ((v << 8) | c) ^ mod[idx(v)] ^ outx[l],
 //   outx[l] = (out[l] << 8) ^ mod[idx(out[l])]   (bits 53..60 cancel on both sides).
-// The chain is then v -> address (2 VALU) -> mod[] read -> one v_bitop3, and a roll costs
-// ~8.5 VALU instead of 10.5 (the u = v ^ out xors are gone).
-#ifndef KCDC_RK_ABL
-#define KCDC_RK_ABL 0  // ablations (timing only, wrong cuts): 1 no out[] reads, 2 mod[] off the chain,
-                       // 3 no wait for the line fills
-#endif
+// The chain is lo -> address (2 VALU) -> mod[] read -> one v_bitop3.
 __device__ __forceinline__ void rk_roll(const RkCtx& k, uint32_t& hi, uint32_t& lo, uint64_t ox, uint32_t w, int b) {
-#if KCDC_RK_ABL == 2
-    const uint32_t am = (__builtin_amdgcn_ubfe(w, 8 * b, 8) << (kRkModRep == 32 ? 8 : 7)) | k.lane8m;
-#else
-    const uint32_t am = (__builtin_amdgcn_ubfe(hi, kRkIdxBit, 8) << (kRkModRep == 32 ? 8 : 7)) | k.lane8m;
-#endif
-    const uint64_t m = *reinterpret_cast<const uint64_t*>(k.modb + am);
-    const uint32_t th = __builtin_amdgcn_alignbit(hi, lo, 24);                          // v << 8, high word
-    const uint32_t tl = __builtin_amdgcn_perm(w, lo, 0x02010000u | (4u + b));           // v << 8 | enter
+    const uint64_t m = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, lo));
+    const uint32_t th = __builtin_amdgcn_perm(w, hi, rk_in_sel(b));
+    const uint32_t tl = __builtin_amdgcn_alignbit(hi, lo, 8);
     hi = __builtin_amdgcn_bitop3_b32(th, static_cast<uint32_t>(m >> 32), static_cast<uint32_t>(ox >> 32), 0x96);
     lo = __builtin_amdgcn_bitop3_b32(tl, static_cast<uint32_t>(m), static_cast<uint32_t>(ox), 0x96);
 }
 // Warm roll (leaving byte 0: out[0] = 0).
 __device__ __forceinline__ void rk_roll0(const RkCtx& k, uint32_t& hi, uint32_t& lo, uint32_t w, int b) {
-    const uint32_t am = (__builtin_amdgcn_ubfe(hi, kRkIdxBit, 8) << (kRkModRep == 32 ? 8 : 7)) | k.lane8m;
-    const uint64_t m = *reinterpret_cast<const uint64_t*>(k.modb + am);
-    const uint32_t th = __builtin_amdgcn_alignbit(hi, lo, 24);
-    const uint32_t tl = __builtin_amdgcn_perm(w, lo, 0x02010000u | (4u + b));
+    const uint64_t m = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, lo));
+    const uint32_t th = __builtin_amdgcn_perm(w, hi, rk_in_sel(b));
+    const uint32_t tl = __builtin_amdgcn_alignbit(hi, lo, 8);
     hi = th ^ static_cast<uint32_t>(m >> 32);
     lo = tl ^ static_cast<uint32_t>(m);
 }
@@ -1969,100 +1979,82 @@ __device__ __forceinline__ void rk_roll0(const RkCtx& k, uint32_t& hi, uint32_t&
 #ifndef KCDC_RK_W
 #define KCDC_RK_W 2  // bytes per lookahead window: outx[] reads of both chains issued one window ahead (2: 2.58 ms, 4: 2.65)
 #endif
-// 64 bytes of chain A (in a / leaving pa) and of chain B (in b / leaving pb), interleaved;
-// returns the running min of (lo & mask) per chain.  ACT_A/ACT_B: whether that chain's
-// bytes are real (an idle chain is not rolled at all).
+// 64 bytes of chain A (in a / leaving pa) and of chain B (in b / leaving pb), interleaved
+// byte by byte; ma/mb: running min of hi over the piece's positions (a candidate iff < thr).
+// Software-pipelined across the chains: a chain's next mod[] read issues right after its own
+// roll, so it is in flight while the other chain rolls (one LDS latency + one roll per byte,
+// not one latency + two rolls).  The outx[] reads of byte x + W follow each chain's mod[] read
+// (the in-order LDS return then never queues a chain's read behind a prefetch).
+// ACT_A/ACT_B: whether that chain's bytes are real (an idle chain is not rolled at all).
+#ifndef KCDC_RK_SWP
+#define KCDC_RK_SWP 1  // 0: both chains' mod[] reads issue together at the top of each byte
+#endif
 template <bool ACT_A, bool ACT_B>
 __device__ __forceinline__ void rk_step64(const RkCtx& k, uint32_t& ha, uint32_t& la, const uint32_t (&a)[16],
                                           const uint32_t (&pa)[16], uint32_t& hb, uint32_t& lb,
                                           const uint32_t (&b)[16], const uint32_t (&pb)[16], uint32_t& ma,
                                           uint32_t& mb) {
     constexpr int W = KCDC_RK_W;
-    uint64_t oa[W], ob[W], na[W], nb[W];
-#pragma unroll
-    for (int i = 0; i < W; i++) {
-        if (ACT_A) oa[i] = rk_out(k, pa[i >> 2], i & 3);
-        if (ACT_B) ob[i] = rk_out(k, pb[i >> 2], i & 3);
-    }
-#pragma unroll
-    for (int w = 0; w < 64 / W; w++) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (w < 64 / W - 1) {
-#pragma unroll
-            for (int i = 0; i < W; i++) {
-                const int x = W * (w + 1) + i;
-                if (ACT_A) na[i] = rk_out(k, pa[x >> 2], x & 3);
-                if (ACT_B) nb[i] = rk_out(k, pb[x >> 2], x & 3);
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < W; i++) {
-            const int x = W * w + i;
-            if (ACT_A) {
-                rk_roll(k, ha, la, oa[i], a[x >> 2], x & 3);
-                ma = min(ma, la & k.mask);
-            }
-            if (ACT_B) {
-                rk_roll(k, hb, lb, ob[i], b[x >> 2], x & 3);
-                mb = min(mb, lb & k.mask);
-            }
-            if ((x & 3) == 3) {
-                if (ACT_A) asm volatile("" : "+v"(ma));
-                if (ACT_B) asm volatile("" : "+v"(mb));
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < W; i++) {
-            if (ACT_A) oa[i] = na[i];
-            if (ACT_B) ob[i] = nb[i];
-        }
-    }
-}
-
-#ifndef KCDC_RK_ORDER
-#define KCDC_RK_ORDER 1  // 1: per byte, the two mod[] reads issue BEFORE the outx[] prefetches of byte
-                         // x + W, so the in-order LDS return of the chain's read is not queued
-                         // behind them (0: prefetch the next window first): 2.57 vs 2.72 ms
-#endif
-template <bool ACT_A, bool ACT_B>
-__device__ __forceinline__ void rk_step64_ord(const RkCtx& k, uint32_t& ha, uint32_t& la, const uint32_t (&a)[16],
-                                              const uint32_t (&pa)[16], uint32_t& hb, uint32_t& lb,
-                                              const uint32_t (&b)[16], const uint32_t (&pb)[16], uint32_t& ma,
-                                              uint32_t& mb) {
-    constexpr int W = KCDC_RK_W;
     uint64_t oa[64], ob[64];  // only W live at a time (unrolled: register renaming)
+    uint64_t mA = 0, mB = 0;
+#if KCDC_RK_SWP
+    if (ACT_A) mA = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, la));
+#pragma unroll
+    for (int i = 0; i < W; i++)
+        if (ACT_A) oa[i] = rk_out(k, pa[i >> 2], i & 3);
+    if (ACT_B) mB = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, lb));
+#pragma unroll
+    for (int i = 0; i < W; i++)
+        if (ACT_B) ob[i] = rk_out(k, pb[i >> 2], i & 3);
+#else
 #pragma unroll
     for (int i = 0; i < W; i++) {
         if (ACT_A) oa[i] = rk_out(k, pa[i >> 2], i & 3);
         if (ACT_B) ob[i] = rk_out(k, pb[i >> 2], i & 3);
     }
+#endif
+    uint32_t pha = 0xFFFFFFFFu, phb = 0xFFFFFFFFu;  // the previous byte's hi (tested in pairs)
 #pragma unroll
     for (int x = 0; x < 64; x++) {
-        const int sh = kRkModRep == 32 ? 8 : 7;
-        uint64_t mA = 0, mB = 0;
         __builtin_amdgcn_sched_barrier(0);
-        if (ACT_A) mA = *reinterpret_cast<const uint64_t*>(k.modb + ((__builtin_amdgcn_ubfe(ha, kRkIdxBit, 8) << sh) | k.lane8m));
-        if (ACT_B) mB = *reinterpret_cast<const uint64_t*>(k.modb + ((__builtin_amdgcn_ubfe(hb, kRkIdxBit, 8) << sh) | k.lane8m));
+#if !KCDC_RK_SWP
+        if (ACT_A) mA = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, la));
+        if (ACT_B) mB = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, lb));
         if (x + W < 64) {
             if (ACT_A) oa[x + W] = rk_out(k, pa[(x + W) >> 2], (x + W) & 3);
             if (ACT_B) ob[x + W] = rk_out(k, pb[(x + W) >> 2], (x + W) & 3);
         }
         __builtin_amdgcn_sched_barrier(0);
+#endif
         if (ACT_A) {
-            const uint32_t th = __builtin_amdgcn_alignbit(ha, la, 24);
-            const uint32_t tl = __builtin_amdgcn_perm(a[x >> 2], la, 0x02010000u | (4u + (x & 3)));
+            const uint32_t th = __builtin_amdgcn_perm(a[x >> 2], ha, rk_in_sel(x & 3));
+            const uint32_t tl = __builtin_amdgcn_alignbit(ha, la, 8);
             ha = __builtin_amdgcn_bitop3_b32(th, static_cast<uint32_t>(mA >> 32), static_cast<uint32_t>(oa[x] >> 32), 0x96);
             la = __builtin_amdgcn_bitop3_b32(tl, static_cast<uint32_t>(mA), static_cast<uint32_t>(oa[x]), 0x96);
-            ma = min(ma, la & k.mask);
+#if KCDC_RK_SWP
+            __builtin_amdgcn_sched_barrier(0);
+            if (x + 1 < 64) mA = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, la));
+            if (x + W < 64) oa[x + W] = rk_out(k, pa[(x + W) >> 2], (x + W) & 3);
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+            if (x & 1) ma = min(ma, min(pha, ha));  // v_min3
+            else pha = ha;
         }
         if (ACT_B) {
-            const uint32_t th = __builtin_amdgcn_alignbit(hb, lb, 24);
-            const uint32_t tl = __builtin_amdgcn_perm(b[x >> 2], lb, 0x02010000u | (4u + (x & 3)));
+            const uint32_t th = __builtin_amdgcn_perm(b[x >> 2], hb, rk_in_sel(x & 3));
+            const uint32_t tl = __builtin_amdgcn_alignbit(hb, lb, 8);
             hb = __builtin_amdgcn_bitop3_b32(th, static_cast<uint32_t>(mB >> 32), static_cast<uint32_t>(ob[x] >> 32), 0x96);
             lb = __builtin_amdgcn_bitop3_b32(tl, static_cast<uint32_t>(mB), static_cast<uint32_t>(ob[x]), 0x96);
-            mb = min(mb, lb & k.mask);
+#if KCDC_RK_SWP
+            __builtin_amdgcn_sched_barrier(0);
+            if (x + 1 < 64) mB = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, lb));
+            if (x + W < 64) ob[x + W] = rk_out(k, pb[(x + W) >> 2], (x + W) & 3);
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+            if (x & 1) mb = min(mb, min(phb, hb));
+            else phb = hb;
         }
-        if ((x & 3) == 3) {
+        if ((x & 3) == 3) {  // keep the running mins sequential (reassociated trees hold ~2 x 64 values)
             if (ACT_A) asm volatile("" : "+v"(ma));
             if (ACT_B) asm volatile("" : "+v"(mb));
         }
@@ -2070,9 +2062,9 @@ __device__ __forceinline__ void rk_step64_ord(const RkCtx& k, uint32_t& ha, uint
 }
 
 // Exact re-run of one chain's 64 bytes from (hi, lo) (rare): first index in [lo_i, hi_i]
-// with (lo & mask) == 0, else 64.
+// that is a candidate, else 64.
 __device__ uint32_t rk_exact64(const RkCtx& k, uint32_t hi, uint32_t lo, const uint32_t (&in)[16],
-                                            const uint32_t (&prv)[16], int lo_i, int hi_i) {
+                               const uint32_t (&prv)[16], int lo_i, int hi_i) {
     uint32_t e[16], o[16];
 #pragma unroll
     for (int j = 0; j < 16; j++) {
@@ -2086,7 +2078,7 @@ __device__ uint32_t rk_exact64(const RkCtx& k, uint32_t hi, uint32_t lo, const u
         for (int b = 0; b < 4; b++) {
             rk_roll(k, hi, lo, rk_out(k, o[0], b), e[0], b);
             const int i = 4 * j + b;
-            if (first == 64 && (lo & k.mask) == 0 && i >= lo_i && i <= hi_i) first = static_cast<uint32_t>(i);
+            if (first == 64 && hi < k.thr && i >= lo_i && i <= hi_i) first = static_cast<uint32_t>(i);
         }
 #pragma unroll
         for (int q = 0; q < 15; q++) {
@@ -2114,10 +2106,12 @@ __device__ __forceinline__ void rk_warm(const RkCtx& kx, const uint32_t (&dw)[32
     }
 }
 __device__ __forceinline__ RkCtx rk_setup(RkTables& smt, const BatchArgs& a, int lane) {
-    for (uint32_t i = threadIdx.x; i < 256u * kRkModRep; i += blockDim.x) smt.mod[i] = a.rk_mod[i / kRkModRep];
+    auto rev8 = [](uint32_t f) { return __builtin_bitreverse32(f) >> 24; };
+    for (uint32_t i = threadIdx.x; i < 256u * kRkModRep; i += blockDim.x)
+        smt.mod[i] = __builtin_bitreverse64(a.rk_mod[rev8(i / kRkModRep)]);
     for (uint32_t i = threadIdx.x; i < 256u * kRkOutRep; i += blockDim.x) {  // outx[] (rk_roll)
-        const uint64_t o = a.rk_out[i / kRkOutRep];
-        smt.out[i] = (o << 8) ^ a.rk_mod[(o >> 45) & 0xFFu];
+        const uint64_t o = a.rk_out[rev8(i / kRkOutRep)];
+        smt.out[i] = __builtin_bitreverse64((o << 8) ^ a.rk_mod[(o >> 45) & 0xFFu]);
     }
     __syncthreads();
     RkCtx kx;
@@ -2125,14 +2119,10 @@ __device__ __forceinline__ RkCtx rk_setup(RkTables& smt, const BatchArgs& a, int
     kx.outb = reinterpret_cast<const char*>(smt.out);
     kx.lane8o = static_cast<uint32_t>(lane & (kRkOutRep - 1)) * 8u;
     kx.lane8m = static_cast<uint32_t>(lane & (kRkModRep - 1)) * 8u;
-    kx.mask = a.mask;
+    kx.thr = 1u << (32 - __builtin_popcount(a.mask));  // mask = avg - 1, avg a power of two in [2, 2^31]
     return kx;
 }
-#if KCDC_RK_ORDER
-#define RK_STEP rk_step64_ord
-#else
 #define RK_STEP rk_step64
-#endif
 // The rare exact re-run of a 64-byte piece at coordinate c whose running test passed.
 __device__ __forceinline__ uint32_t rk_exact(const RkCtx& k, uint32_t h0, uint32_t l0, const Loader& ld, int64_t c,
                                             const uint32_t (&in)[16], const uint32_t (&prv)[16], int lo_i, int hi_i) {
@@ -2209,10 +2199,8 @@ __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int 
         {
             uint32_t dw[32], na[16];
             __builtin_amdgcn_sched_barrier(0);
-#if KCDC_RK_ABL != 3
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-            read_step128(sl, lane, head && j == 0 ? 0 : 1, off0, dw);
+            rk_read_step128(sl, lane, head && j == 0 ? 0 : 1, off0, dw);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             refill(2 * j + 1);
@@ -2240,10 +2228,8 @@ __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int 
         {
             uint32_t dw[32], nb[16];
             __builtin_amdgcn_sched_barrier(0);
-#if KCDC_RK_ABL != 3
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-            read_step128(sl, lane, 1, off0, dw);
+            rk_read_step128(sl, lane, 1, off0, dw);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             refill(2 * j + 2);
@@ -2361,7 +2347,7 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             uint32_t dw[32];
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_waitcnt vmcnt(0)" : "+v"(ht_lo), "+v"(ht_hi)::"memory");
-            read_step128(sl, lane, -1, cur.off0, dw);
+            rk_read_step128(sl, lane, -1, cur.off0, dw);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             rk_dma_line(g.ld, sl32, ct, g.L, 1, lane);
@@ -2406,7 +2392,7 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
         // wave-uniform values and an opaque lane id (nothing 64-bit per lane lives across the walk).
         auto check = [&](uint32_t mm, int chain, int rel, uint32_t h0, uint32_t l0, const uint32_t (&in)[16],
                          const uint32_t (&prv)[16]) {
-            if (mm == 0 && (chain ? found_b : found_a) < 0) {
+            if (mm < kx.thr && (chain ? found_b : found_a) < 0) {
                 int ln = lane;
                 asm volatile("" : "+v"(ln));
                 const int64_t c = ct + ln * g.L + (chain ? g.L / 2 : 0) + rel;
@@ -2979,7 +2965,7 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void cand_scan_rk_k
             uint32_t dw[32];
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            read_step128(sl, lane, -1, q.off0, dw);
+            rk_read_step128(sl, lane, -1, q.off0, dw);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             rk_dma_line(t.ld, sl32, q.cs, t.L, 1, lane);
@@ -3002,7 +2988,7 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void cand_scan_rk_k
                          const uint32_t (&prv)[16]) {
             int& nf = chain ? nb : na;
             uint32_t(&fnd)[kSegK / 2] = chain ? fb : fa;
-            if (mm == 0 && nf <= kSegK) {  // rare: enumerate the piece's candidates exactly
+            if (mm < kx.thr && nf <= kSegK) {  // rare: enumerate the piece's candidates exactly
                 int ln = lane;
                 asm volatile("" : "+v"(ln));  // the coordinate is formed here only (rk_walk)
                 const int64_t c = q.cs + ln * t.L + (chain ? t.L / 2 : 0) + crel;
@@ -3623,9 +3609,6 @@ const char* ablations_kernels() {
 #endif
 #ifdef KCDC_EXP_MEMONLY
            "KCDC_EXP_MEMONLY,"
-#endif
-#if defined(KCDC_RK_ABL) && KCDC_RK_ABL
-           "KCDC_RK_ABL,"
 #endif
         ;
 }
