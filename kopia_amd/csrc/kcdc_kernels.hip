@@ -3700,13 +3700,16 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
                 (void)hipSetDevice(device);
                 char* nb = nullptr;
                 size_t nbytes = bytes > 2 * q.bytes ? bytes : 2 * q.bytes;
-                hipError_t e = hipMalloc(&nb, nbytes);
+                // Stream-ordered: a plain hipFree synchronises the whole device, so a launch that
+                // grows its slot would wait for every kernel on every stream (tests/test_gpu_queue.py
+                // steal test: the batch waited out a 300 ms occupier on another stream).
+                hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&nb), nbytes, st);
+                if (e == hipSuccess && q.base) {  // the slot's previous launches are the old buffer's only users
+                    if (q.done) e = hipStreamWaitEvent(st, q.done, 0);
+                    if (e == hipSuccess) e = hipFreeAsync(q.base, st);
+                }
                 (void)hipSetDevice(prev);
                 if (e != hipSuccess) return hip_fail(e, "queue workspace");
-                if (q.base) {  // the slot's previous launches are the only users of the old buffer
-                    if (q.done) (void)hipEventSynchronize(q.done);
-                    (void)hipFree(q.base);
-                }
                 q.base = nb;
                 q.bytes = nbytes;
             }

@@ -82,4 +82,4 @@ for _ in range(3):
 e1.record(stream)
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / 3
-print(f"torch.sum over {ns * L / 2**30:.0f} GiB: {ms:.3f} ms = {ns * L / ms / 1e9:.0f} GB/s")
+print(f"torch.sum over {ns * L / 2**30:.0f} GiB: {ms:.3f} ms = {ns * L / ms / 1e6:.0f} GB/s")
