@@ -294,9 +294,17 @@ def bench_batch(args, comm: Comm):
     b = batch.make_device_batch(name, [data.data_ptr() + i * L for i in range(ns)], [L] * ns, dev)
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize(dev)
-    for _ in range(args.warmup):
+    warm_steps, tw = 0, time.perf_counter()
+    # W untimed steps, continued until the warm-up has lasted --warmup-min-s: after idle the
+    # chip's clock ramps over ~10 launches (1.6-1.7 ms -> 1.35 ms; profiles/r03/buz/ramp.log),
+    # so a 5-step warm-up leaves the first timed launches on the ramp.
+    while warm_steps < args.warmup or time.perf_counter() - tw < args.warmup_min_s:
         batch.split_batch_device(name, b, stream)
+        warm_steps += 1
+        if warm_steps % 8 == 0:
+            torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
+    warm_s = time.perf_counter() - tw
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     comm.barrier()
@@ -320,7 +328,8 @@ def bench_batch(args, comm: Comm):
     cfg = f"config{args.config}" + ("-rk" if int(info.kind) == 2 else "")
     out = {
         "metric": METRIC, "value": agg["value"], "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": agg["ms_per_step"], "higher_is_better": True,
+        "warmup": args.warmup, "warmup_steps_run": warm_steps, "warmup_s": round(warm_s, 3),
+        "ms_per_step": agg["ms_per_step"], "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "config": {"workload": f"{cfg}: {ns} x {args.stream_mib} MiB independent streams per GPU "
                                f"(counter-PRNG bytes, HBM-resident), {name}",
@@ -846,6 +855,9 @@ def parse(argv):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup-min-s", type=float, default=0.3,
+                    help="configs 2/4: keep taking untimed warm-up steps until this many seconds have passed "
+                         "(the clock ramps after idle); 0: exactly --warmup steps")
     ap.add_argument("--splitter", default="DYNAMIC-4M-BUZHASH")
     ap.add_argument("--streams", type=int, default=4096)
     ap.add_argument("--stream-mib", type=int, default=4)
