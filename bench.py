@@ -162,7 +162,23 @@ def roofline(kernel: str, config: str, kern_ms: float, rolled: int, stream_bytes
             "hbm_frac_measured": round(traffic / kern_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
             "traffic_source": "profiles/pmc_traffic.json[" + f"{kernel}|{config}" + "] (FETCH_SIZE x 1024 x 2)",
             "stream_bytes_per_launch": stream_bytes,
-            "stream_gbs": round(stream_bytes / kern_s / 1e9, 1)}
+            "stream_gbs": round(stream_bytes / kern_s / 1e9, 1)} | valu_note(kernel, config)
+
+
+# Rabin-Karp's limiter is VALU issue, not HBM: SQ_INSTS_VALU per config-2
+# launch (profiles/r03/rk/sq1_counter_collection.csv, 7 launches) at 4 cycles per wave64
+# instruction on each of the 1,024 SIMDs gives the launch's VALU floor at the measured clock.
+RK_VALU_PER_LAUNCH = {"config2-rk": 1.0146e9}
+SIMDS, VALU_CYCLES, CLOCK_HZ = 1024, 4, 2.13e9
+
+
+def valu_note(kernel: str, config: str) -> dict:
+    n = RK_VALU_PER_LAUNCH.get(config)
+    if not n:
+        return {}
+    floor_ms = n * VALU_CYCLES / SIMDS / CLOCK_HZ * 1e3
+    return {"limited_by": "VALU", "valu_insts_per_launch": n, "valu_floor_ms": round(floor_ms, 3),
+            "valu_source": "profiles/r03/rk/sq1_counter_collection.csv (SQ_INSTS_VALU)"}
 
 
 def h2d_rates(host: np.ndarray, dev) -> dict:
@@ -338,6 +354,8 @@ def bench_batch(args, comm: Comm):
         "per_gpu_gib_s": agg["per_gpu_gib_s"],
     }
     out["roofline"] = roofline(BATCH_KERNEL[int(info.kind)], cfg, kern_ms, rolled, ns * L)
+    if "valu_floor_ms" in out["roofline"]:
+        out["roofline"]["valu_busy"] = round(out["roofline"]["valu_floor_ms"] / kern_ms, 3)
     out["cut_stats"] = {"chunks": int(sum(c.size for c in cuts)), "rolled_fraction": round(rolled / (ns * L), 4)}
 
     if args.hash and rank == 0 and world == 1:

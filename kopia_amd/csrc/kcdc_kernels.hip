@@ -2258,6 +2258,11 @@ __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int 
     }
 }
 
+#ifndef KCDC_RK_LMUL
+#define KCDC_RK_LMUL 2  // Rabin-Karp lane segments: this many times the buzhash cap (warm-up vs tile overshoot;
+                        // 2 vs 1: 4M 2.542 vs 2.554 ms, 128K 5.536 vs 5.643 ms, profiles/r03/rk/kbench_lmul_*.log)
+#endif
+constexpr int64_t kRkLaneMul = KCDC_RK_LMUL;
 __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk_kernel(BatchArgs a) {
     __shared__ RkTables smt;
     __shared__ RkSlots smslots;
@@ -2325,7 +2330,7 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
         if (!pcheck(a, lane, cur, 0xFFFFFFFFu, 5)) return;
         int64_t lo, hi;
         pregion(a, cur, lo, hi);
-        const RkGeom g = rk_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n, a.lane_cap);
+        const RkGeom g = rk_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n, kRkLaneMul * a.lane_cap);
         const int64_t ct = cur.ct, ct_next = ct + kWave * g.L;
         const bool last_of_region = ct_next > hi;
         const bool budget_out = budget - kWave * g.L <= 0;
@@ -2373,7 +2378,7 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
                 pentry_dma(a, lane, tk, sl32);
                 entry_issued = true;
             } else if (!last_of_region) {  // the next tile has its own geometry
-                const RkGeom gn = rk_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n, a.lane_cap);
+                const RkGeom gn = rk_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n, kRkLaneMul * a.lane_cap);
                 rk_dma_warm(gn.ld, sl32, ct_next, gn.L, lane);
                 next_issued = true;
             }
