@@ -293,6 +293,20 @@ def cpu_config1(seconds_cap: float = 12.0) -> dict:
 
 
 # ------------------------------------------------------------- configs
+def warm_up(fn, min_steps: int, min_s: float, dev) -> tuple[int, float]:
+    """Untimed warm-up: at least `min_steps` calls of fn and at least `min_s` seconds (the chip's
+    clock ramps over ~10 config-2 launches after idle, profiles/r03/buz/ramp.log)."""
+    import torch
+    n, t0 = 0, time.perf_counter()
+    while n < min_steps or time.perf_counter() - t0 < min_s:
+        fn()
+        n += 1
+        if n % 8 == 0:
+            torch.cuda.synchronize(dev)
+    torch.cuda.synchronize(dev)
+    return n, time.perf_counter() - t0
+
+
 def bench_batch(args, comm: Comm):
     """Configs 2 and 4: `streams` x `stream_mib` per GPU, one batch launch per step."""
     import torch
@@ -310,17 +324,10 @@ def bench_batch(args, comm: Comm):
     b = batch.make_device_batch(name, [data.data_ptr() + i * L for i in range(ns)], [L] * ns, dev)
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize(dev)
-    warm_steps, tw = 0, time.perf_counter()
     # W untimed steps, continued until the warm-up has lasted --warmup-min-s: after idle the
     # chip's clock ramps over ~10 launches (1.6-1.7 ms -> 1.35 ms; profiles/r03/buz/ramp.log),
     # so a 5-step warm-up leaves the first timed launches on the ramp.
-    while warm_steps < args.warmup or time.perf_counter() - tw < args.warmup_min_s:
-        batch.split_batch_device(name, b, stream)
-        warm_steps += 1
-        if warm_steps % 8 == 0:
-            torch.cuda.synchronize(dev)
-    torch.cuda.synchronize(dev)
-    warm_s = time.perf_counter() - tw
+    warm_steps, warm_s = warm_up(lambda: batch.split_batch_device(name, b, stream), args.warmup, args.warmup_min_s, dev)
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     comm.barrier()
@@ -688,6 +695,8 @@ def bench_long(args, comm: Comm):
     stream = torch.cuda.current_stream(dev)
     cuts, count, ws = batch.split_long_device(name, data.data_ptr(), L, dev, stream)
     torch.cuda.synchronize(dev)
+    warm_steps, warm_s = warm_up(lambda: batch.split_long_device(name, data.data_ptr(), L, dev, stream), 1,
+                                 args.warmup_min_s, dev)
     steps = max(1, min(args.steps, 10))
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     comm.barrier()
@@ -705,7 +714,7 @@ def bench_long(args, comm: Comm):
     per = comm.gather({"bytes_per_step": L, "elapsed_s": elapsed, "own_s": own})
     agg = aggregate(per, steps)
     out = {"metric": METRIC, "value": agg["value"], "unit": "GiB/s", "n_gpus": comm.world, "steps": steps,
-           "warmup": 1, "ms_per_step": agg["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+           "warmup": 1, "warmup_steps_run": warm_steps + 1, "warmup_s": round(warm_s, 3), "ms_per_step": agg["ms_per_step"], "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
            "config": {"workload": f"config3: one {args.long_gib} GiB stream per GPU, exact intra-stream tiled CDC, "
                                   f"{name}", "splitter": name, "stream_bytes": L,
@@ -761,9 +770,7 @@ def bench_files(args, comm: Comm):
     stream = torch.cuda.current_stream(dev)
 
     def run(name, steps, warmup):
-        for _ in range(warmup):
-            batch.split_files_device(name, ptrs, lens, dev, stream)
-        torch.cuda.synchronize(dev)
+        warm_up(lambda: batch.split_files_device(name, ptrs, lens, dev, stream), warmup, args.warmup_min_s, dev)
         comm.barrier()
         t0 = time.perf_counter()
         res = None
@@ -874,7 +881,7 @@ def parse(argv):
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--warmup-min-s", type=float, default=0.3,
-                    help="configs 2/4: keep taking untimed warm-up steps until this many seconds have passed "
+                    help="keep taking untimed warm-up steps until this many seconds have passed "
                          "(the clock ramps after idle); 0: exactly --warmup steps")
     ap.add_argument("--splitter", default="DYNAMIC-4M-BUZHASH")
     ap.add_argument("--streams", type=int, default=4096)
