@@ -329,19 +329,22 @@ def bench_batch(args, comm: Comm):
     # so a 5-step warm-up leaves the first timed launches on the ramp.
     warm_steps, warm_s = warm_up(lambda: batch.split_batch_device(name, b, stream), args.warmup, args.warmup_min_s, dev)
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # One event pair around the K launches (on the launch stream): the average launch duration,
+    # init kernel and inter-launch gaps included.  An event pair per launch put ~9 us of timing
+    # packets between consecutive launches (kernel traces, profiles/r03/launch_gaps/).
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     comm.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for e0, e1 in evs:
-        e0.record(stream)
+    e0.record(stream)
+    for _ in range(args.steps):
         batch.split_batch_device(name, b, stream)
-        e1.record(stream)
+    e1.record(stream)
     torch.cuda.synchronize(dev)
     own = time.perf_counter() - t0
     comm.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    kern_ms = e0.elapsed_time(e1) / args.steps
 
     cuts = batch.read_cuts(b)
     rolled = sum(rolled_bytes(c, int(info.min_size)) for c in cuts)

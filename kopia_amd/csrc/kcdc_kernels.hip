@@ -3514,8 +3514,22 @@ struct QueueWs {
     size_t bytes = 0;
     hipEvent_t done = nullptr;  // recorded after the slot's last launch: a reuse from another
                                 // stream waits for it (more than kQueueSlots launches in flight)
+    hipStream_t last = nullptr;  // the stream of the slot's last launch
+    bool used = false;
 };
 QueueWs g_qws[kMaxDevices][kQueueSlots];
+// Slot affinity: back-to-back launches on one stream reuse that stream's slot (stream order
+// already serialises them, so no event wait, and the workspace stays warm); other streams
+// take slots round-robin.  A few recent streams per device, least recently used replaced.
+struct StreamSlot {
+    hipStream_t st = nullptr;
+    unsigned slot = 0;
+    uint64_t tick = 0;
+    bool valid = false;
+};
+constexpr int kStreamSlots = 8;
+StreamSlot g_stream_slot[kMaxDevices][kStreamSlots];
+uint64_t g_slot_tick[kMaxDevices];
 bool g_dev_ready[kMaxDevices];
 unsigned g_queue_next[kMaxDevices];
 std::mutex g_dev_mu;
@@ -3696,8 +3710,26 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         // The slot stays locked from its selection to its event record, so a later user of the
         // same slot always waits for this launch.
         std::lock_guard<std::mutex> lk(g_dev_mu);
-        const unsigned slot = g_queue_next[device]++ % kQueueSlots;
+        unsigned slot = kQueueSlots;
+        StreamSlot* aff = nullptr;
+        for (StreamSlot& e : g_stream_slot[device]) {
+            if (e.valid && e.st == st) aff = &e;
+        }
+        if (aff && g_qws[device][aff->slot].last == st) slot = aff->slot;
+        if (slot == kQueueSlots) {
+            slot = g_queue_next[device]++ % kQueueSlots;
+            if (!aff) {  // remember this stream in the least recently used entry
+                aff = &g_stream_slot[device][0];
+                for (StreamSlot& e : g_stream_slot[device])
+                    if (!e.valid || e.tick < aff->tick) aff = &e;
+                aff->valid = true;
+                aff->st = st;
+            }
+            aff->slot = slot;
+        }
+        aff->tick = ++g_slot_tick[device];
         QueueWs& q = g_qws[device][slot];
+        const bool same_stream = q.used && q.last == st;  // stream order covers the previous launch
         {
             if (q.bytes < bytes) {
                 int prev = 0;
@@ -3723,13 +3755,15 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
                 int prev = 0;
                 (void)hipGetDevice(&prev);
                 (void)hipSetDevice(device);
-                const hipError_t e = hipEventCreateWithFlags(&q.done, hipEventDisableTiming);
+                const hipError_t e = hipEventCreateWithFlags(&q.done, hipEventDisableTiming | hipEventDisableSystemFence);
                 (void)hipSetDevice(prev);
                 if (e != hipSuccess) return hip_fail(e, "queue workspace event");
-            } else {
+            } else if (!same_stream) {
                 const hipError_t e = hipStreamWaitEvent(st, q.done, 0);
                 if (e != hipSuccess) return hip_fail(e, "queue workspace wait");
             }
+            q.last = st;
+            q.used = true;
         }
         a.queue = reinterpret_cast<uint32_t*>(ws);
         g_test.last_ws = ws;
