@@ -35,10 +35,11 @@ clean:
 
 # Instrumented builds for tools/debug_pipe.py (queue invariants, KCDC_DEBUG_CHECKS) and
 # tools/trace_pipe.py (per-wave s_memrealtime trace, KCDC_TRACE); not used by the product.
-build/libkcdc_dbg.so build/libkcdc_trace.so: $(CSRC)/kcdc_kernels.hip $(CSRC)/kcdc_api.cpp $(CSRC)/kcdc_internal.h include/kcdc.h
+build/libkcdc_dbg.so build/libkcdc_trace.so: $(SRCS) $(CSRC)/kcdc_internal.h include/kcdc.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) $(if $(findstring dbg,$@),-DKCDC_DEBUG_CHECKS=1,-DKCDC_TRACE=1) -shared -o $@ \
-	  $(CSRC)/kcdc_kernels.hip -x hip $(CSRC)/kcdc_api.cpp $(CSRC)/kcdc_tables.cpp $(CSRC)/kcdc_registry.cpp
+	  $(CSRC)/kcdc_kernels.hip $(CSRC)/kcdc_hash.hip $(CSRC)/kcdc_crypt.hip $(CSRC)/kcdc_compress.hip \
+	  -x hip $(CSRC)/kcdc_api.cpp $(CSRC)/kcdc_writer.cpp $(CSRC)/kcdc_tables.cpp $(CSRC)/kcdc_registry.cpp
 instrumented: build/libkcdc_dbg.so build/libkcdc_trace.so
 .PHONY: instrumented
 

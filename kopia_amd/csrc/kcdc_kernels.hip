@@ -169,8 +169,23 @@ __device__ __forceinline__ Loader make_loader(const uint8_t* abase, int64_t off0
 // buzhash32: h(p) = rotl(h(p-1),1) ^ T[b[p-64]] ^ T[b[p]]  (rollinghash Roll with
 // window 64: rotl(T[leave], 64 % 32 = 0)).
 struct BuzShared {
-    uint32_t tab[256 * 64];  // tab[v*64 + r] = T[v]  (64 KiB, replica r read by lane r)
+    __attribute__((aligned(16))) uint32_t tab[256 * 64];  // tab[v*64 + r] = T[v]  (64 KiB, replica r read by lane r)
 };
+// Fill the replicated table at kernel start: one global load per thread (two threads per
+// entry, 32 replicas each, as four-dword stores rotated by entry so a store instruction's
+// lanes spread over the banks).  The loop of one load per replica took 4 dependent rounds of
+// L2 loads at every workgroup's start.
+__device__ __forceinline__ void fill_buz_table(BuzShared& sm, const uint32_t* buz, uint32_t rot) {
+    static_assert(sizeof(BuzShared) == 256 * 64 * 4, "table layout");
+    for (uint32_t t = threadIdx.x; t < 512u; t += blockDim.x) {
+        const uint32_t e = t & 255u, h = t >> 8;
+        const uint32_t v = rotl_n(buz[e], rot);
+        const u32x4 q = {v, v, v, v};
+        u32x4* row = reinterpret_cast<u32x4*>(sm.tab + e * 64u + h * 32u);
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) row[(k + e) & 7u] = q;
+    }
+}
 
 struct Buz {
     const char* tab;  // LDS byte address of BuzShared::tab
@@ -1454,7 +1469,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
     __shared__ BuzShared smtab;
     __shared__ DmaSlots smslots;
     __shared__ WarmSlots smwarm;
-    for (uint32_t i = threadIdx.x; i < 256u * 64u; i += blockDim.x) smtab.tab[i] = rotl_n(a.buz[i >> 6], a.buz_rot);
+    fill_buz_table(smtab, a.buz, a.buz_rot);
     __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -3055,7 +3070,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void cand_scan_dm
     __shared__ BuzShared smtab;
     __shared__ DmaSlots smslots;
     __shared__ WarmSlots smwarm;
-    for (uint32_t i = threadIdx.x; i < 256u * 64u; i += blockDim.x) smtab.tab[i] = rotl_n(a.buz[i >> 6], a.buz_rot);
+    fill_buz_table(smtab, a.buz, a.buz_rot);
     __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
