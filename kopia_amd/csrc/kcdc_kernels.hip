@@ -1341,6 +1341,13 @@ __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
     return true;
 }
 
+#ifndef KCDC_POLL_BACKOFF
+#define KCDC_POLL_BACKOFF 32  // s_sleep argument once KCDC_POLL_AFTER polls saw no stream finish (0: always 16);
+                             // 32: 1.339-1.344 vs 1.363 ms on config 2 (profiles/r03/buz/kbench_poll_*.log)
+#endif
+#ifndef KCDC_POLL_AFTER
+#define KCDC_POLL_AFTER 8u
+#endif
 // Blocking resolution of ticket t (its ring entry, polled): 1 resolved, 2 tombstone (take
 // another ticket), 0 every stream is done, or the wave gave up (error word) -- it exits.
 __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, uint32_t wg_waves) {
@@ -1375,6 +1382,13 @@ __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, u
             try_steal(a, lane, wg_waves);
             continue;  // poll the entry again at once
         }
+#if KCDC_POLL_BACKOFF
+        // back off while nothing finishes: ~1,000 waiting waves polling two words every 0.5 us
+        // load the L2 channel of the done counter in the batch's tail
+        if (bcast(idle) >= KCDC_POLL_AFTER)
+            __builtin_amdgcn_s_sleep(KCDC_POLL_BACKOFF);
+        else
+#endif
         __builtin_amdgcn_s_sleep(16);
     }
 }
