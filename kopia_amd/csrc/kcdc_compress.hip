@@ -863,8 +863,11 @@ __global__ __launch_bounds__(256) void deflate_frame_kernel(CompArgs a) {
         for (uint32_t t = 0; t < kS2StreamId; t++) dst[4 + t] = id[t];
         out_len = 4u + kS2StreamId + body;
     } else if (a.gzip) {
-        // RFC 1952 member: ID1 ID2 CM=8 FLG=0 MTIME=0 XFL=0 OS=255, the stream, CRC32, ISIZE
-        const uint8_t gz[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 0, 0xff};
+        // RFC 1952 member: ID1 ID2 CM=8 FLG=0 MTIME=0 XFL OS=255, the stream, CRC32, ISIZE.  XFL as
+        // Go's compress/gzip (and klauspost/pgzip) Writer sets it from the level: 2 for
+        // BestCompression, 4 for BestSpeed, else 0 (effort 2 / 0 / 1 here).
+        const uint8_t xfl = a.effort == 2u ? 2u : a.effort == 0u ? 4u : 0u;
+        const uint8_t gz[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, xfl, 0xff};
         for (uint32_t t = 0; t < 10u; t++) dst[4 + t] = gz[t];
         uint8_t* e = dst + 14 + body;
         e[0] = 0x03u;

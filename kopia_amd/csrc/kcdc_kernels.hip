@@ -1348,6 +1348,10 @@ __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
 #ifndef KCDC_POLL_AFTER
 #define KCDC_POLL_AFTER 8u
 #endif
+#ifndef KCDC_DONE_EVERY
+#define KCDC_DONE_EVERY 4u  // waiting waves read the done counter every this many polls of their entry
+                           // (4 vs 1: -1.3 % and -0.3 % in two A/Bs, profiles/r03/buz/kbench_done_*.log)
+#endif
 // Blocking resolution of ticket t (its ring entry, polled): 1 resolved, 2 tombstone (take
 // another ticket), 0 every stream is done, or the wave gave up (error word) -- it exits.
 __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, uint32_t wg_waves) {
@@ -1363,7 +1367,7 @@ __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, u
             return 1;
         }
         uint32_t stop = 0;
-        if (lane == 0) {
+        if (lane == 0 && spin % KCDC_DONE_EVERY == 0) {
             // Progress = streams finishing.  Not the {head, tail} word: every ticket take and
             // yield is an atomic on it, and waiting waves polling it slowed those by ~7%.
             const uint32_t done = ld_agent(a.queue + kQDone);

@@ -77,6 +77,9 @@ def test_reference_properties(name, gpu):
     assert ol[0] < 10000 and ids[0] == deflate.HEADER_IDS[name]
     assert ol[1] >= 10000 and ids[1] == 0
     blob = out[oo[0]:oo[0] + ol[0]].tobytes()
+    if name in GZIP:  # the member header as Go's gzip.Writer (and pgzip's) writes it: XFL from the level
+        xfl = 2 if name.endswith("best-compression") else 4 if name.endswith("best-speed") else 0
+        assert blob[4:14] == bytes([0x1F, 0x8B, 8, 0, 0, 0, 0, 0, xfl, 0xFF]), blob[4:14].hex()
     for other in ALL:
         if other != name:
             with pytest.raises(ValueError):
