@@ -351,7 +351,11 @@ def bench_batch(args, comm: Comm):
     per = comm.gather({"bytes_per_step": ns * L, "elapsed_s": elapsed, "own_s": own, "kernel_ms": kern_ms,
                        "rolled": rolled})
     agg = aggregate(per, args.steps)
+    # traffic is looked up per (kernel, config) and measured for the 4M names only: another
+    # average gets its own key (no FETCH pass: traffic null rather than another name's bytes)
     cfg = f"config{args.config}" + ("-rk" if int(info.kind) == 2 else "")
+    if name not in ("DYNAMIC-4M-BUZHASH", "DYNAMIC-4M-RABINKARP"):
+        cfg += "-" + name
     out = {
         "metric": METRIC, "value": agg["value"], "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "warmup_steps_run": warm_steps, "warmup_s": round(warm_s, 3),
