@@ -1391,6 +1391,33 @@ __global__ __launch_bounds__(256) void gcm_finish_kernel(CryptArgs a, const GcmK
     }
 }
 
+// Open: a chunk that fails its check hands back no plaintext, as Go's Open returns nil on a bad
+// tag (aeadOpenPrefixedWithNonce, repo/encryption/aes256_gcm_hmac_sha256_encryptor.go:49-56,
+// aead_helpers.go).  The byte pass has already written the unauthenticated plaintext, so the
+// chunk's output slot (sealed length - 28 bytes) is zeroed.  One wave per chunk; the wave of a
+// chunk that opened cleanly exits at once.
+__global__ __launch_bounds__(256) void open_mask_kernel(CryptArgs a) {
+    const uint32_t c = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (c >= a.n || a.status[c] == 0) return;
+    const uint64_t in_len = a.in_lens[c];
+    if (in_len <= 28u) return;  // too short: nothing was written
+    const uint64_t len = in_len - 28u;
+    uint8_t* p = a.out + a.out_offs[c];  // a multiple of 4
+    const uint64_t nq = len / 16u;
+    u32x4* pq = reinterpret_cast<u32x4*>(p);
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    if ((reinterpret_cast<uintptr_t>(p) & 15u) == 0) {
+        for (uint64_t i = lane; i < nq; i += 64u) pq[i] = z;
+        for (uint64_t i = 16u * nq + lane; i < len; i += 64u) p[i] = 0;
+    } else {
+        uint32_t* pw = reinterpret_cast<uint32_t*>(p);
+        const uint64_t nw = len / 4u;
+        for (uint64_t i = lane; i < nw; i += 64u) pw[i] = 0u;
+        for (uint64_t i = 4u * nw + lane; i < len; i += 64u) p[i] = 0;
+    }
+}
+
 }  // namespace cryptdev
 
 namespace {
@@ -1525,6 +1552,7 @@ int crypt_run(const char* name, const uint8_t* secret, uint32_t secret_len, cons
         hipLaunchKernelGGL(cryptdev::unit_scan_kernel, dim3(1), dim3(1024), 0, st, n, a.units);
         hipLaunchKernelGGL(cryptdev::gcm_units_kernel<kOpen>, dim3(ggrid), dim3(64 * cryptdev::kGcmWaves), 0, st, a, gk, gk, a.units);
         hipLaunchKernelGGL(cryptdev::gcm_finish_kernel<kOpen>, dim3((n + 255u) / 256u), dim3(256), 0, st, a, gk);
+        if (kOpen) hipLaunchKernelGGL(cryptdev::open_mask_kernel, dim3((n + 3u) / 4u), dim3(256), 0, st, a);
         const hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : set_error(-5, std::string("encryption kernel launch: ") + hipGetErrorString(e));
     }
@@ -1533,6 +1561,7 @@ int crypt_run(const char* name, const uint8_t* secret, uint32_t secret_len, cons
     hipLaunchKernelGGL(cryptdev::crypt_units_kernel<kOpen>, dim3(grid), dim3(256), 0, st, a, a.keys, a.units, a.in_offs,
                        a.out_offs, a.tabs, a.out, a.acc);
     hipLaunchKernelGGL(cryptdev::crypt_finish_kernel<kOpen>, dim3((n + 255u) / 256u), dim3(256), 0, st, a);
+    if (kOpen) hipLaunchKernelGGL(cryptdev::open_mask_kernel, dim3((n + 3u) / 4u), dim3(256), 0, st, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : set_error(-5, std::string("encryption kernel launch: ") + hipGetErrorString(e));
 }

@@ -3565,7 +3565,9 @@ StreamSlot g_stream_slot[kMaxDevices][kStreamSlots];
 uint64_t g_slot_tick[kMaxDevices];
 bool g_dev_ready[kMaxDevices];
 unsigned g_queue_next[kMaxDevices];
-std::mutex g_dev_mu;
+// Per-device locks: table setup and a launch's slot / workspace / enqueue sequence are
+// serialised per device only, so threads driving different devices never wait on each other.
+std::mutex g_dev_mu[kMaxDevices];
 
 int hip_fail(hipError_t e, const char* what) { return set_error(-5, std::string(what) + ": " + hipGetErrorString(e)); }
 
@@ -3671,7 +3673,7 @@ const DeviceTables* device_tables(int device, int* err) {
         *err = set_error(-22, "device index out of range");
         return nullptr;
     }
-    std::lock_guard<std::mutex> lk(g_dev_mu);
+    std::lock_guard<std::mutex> lk(g_dev_mu[device]);
     if (g_dev_ready[device]) return &g_dev_tables[device];
     const Tables& T = tables();
     int prev = 0;
@@ -3742,7 +3744,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         char* ws = nullptr;
         // The slot stays locked from its selection to its event record, so a later user of the
         // same slot always waits for this launch.
-        std::lock_guard<std::mutex> lk(g_dev_mu);
+        std::lock_guard<std::mutex> lk(g_dev_mu[device]);
         unsigned slot = kQueueSlots;
         StreamSlot* aff = nullptr;
         for (StreamSlot& e : g_stream_slot[device]) {

@@ -475,8 +475,10 @@ void kcdc_bw_batcher::loop() {
                     hp[n + k] = R.jobs[k].to - w->tail_pos;                                      // lens
                     hp[2 * n + k] = w->frontier - w->tail_pos;                                   // starts
                     hp[3 * n + k] = R.cbase[k];                                                  // cut_base
-                    // the chunk in progress was tested up to the last completed region's end
-                    hp[4 * n + k] = w->launched_to > w->tail_pos ? w->launched_to - w->tail_pos : 0;  // resume
+                    // the chunk in progress was tested up to the last completed region's end; its
+                    // last byte is tested again: a candidate there cut the region at its end, and
+                    // complete() cannot tell that cut from the region end, so it was not taken
+                    hp[4 * n + k] = w->launched_to > w->tail_pos + 1 ? w->launched_to - w->tail_pos - 1 : 0;  // resume
                 }
                 uint64_t* dp = M.d;
                 hipError_t e = hipStreamWaitEvent(stream, M.gathered, 0);

@@ -120,9 +120,9 @@ class Encryptor:
         """Open sealed chunk i = [offsets[i], +sealed_lengths[i]) into d_out at out_offsets[i].
         Returns the device int32 status tensor: 0, KCDC_EBADMSG, KCDC_EINVAL or KCDC_EFBIG.
 
-        The plaintext is written before its tag is checked: d_out's slot of a chunk whose
-        status is not 0 holds unauthenticated bytes and must not be used (Go's AEAD.Open
-        returns no plaintext on failure).  raise_on_status(status) syncs and raises on any
+        A chunk whose status is not 0 hands back no plaintext: its d_out slot (sealed length
+        - 28 bytes) is zeroed on the device after the tag check, as Go's AEAD.Open returns nil
+        on failure (aeadOpenPrefixedWithNonce).  raise_on_status(status) syncs and raises on any
         failed chunk."""
         import torch
         n = len(offsets)

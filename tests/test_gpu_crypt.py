@@ -120,6 +120,41 @@ def test_open_rejects(alg, gpu):
         assert plain[po[i]:po[i] + L].tobytes() == host[i * L:(i + 1) * L].tobytes()
 
 
+def test_failed_open_leaves_no_plaintext(alg, gpu):
+    """A forged chunk's output slot is all zero after the call and its neighbours are intact (Go's
+    Open returns no plaintext on a bad tag: aes256_gcm_hmac_sha256_encryptor.go:49-56).  The output
+    buffer starts as 0xAB fill, so a slot the byte pass wrote and the mask missed would show."""
+    import torch
+    rng = np.random.default_rng(12)
+    lens = [5000, 4096, 1, 70001, 33, 65536, 0, 777]
+    offs = np.concatenate(([0], np.cumsum(lens)[:-1])).astype(np.int64)
+    host = rng.integers(0, 256, int(sum(lens)) + 16, dtype=np.uint8)
+    ivs = [bytes([i + 1]) * 16 for i in range(len(lens))]
+    enc = ke.Encryptor(alg, MASTER)
+    out, oo, st = _seal(enc, host, offs, lens, ivs, None, gpu)
+    assert not st.any()
+    slens = np.asarray(lens, np.int64) + 28
+    sealed = out.copy()
+    forged = [1, 3, 4, 7]
+    for i in forged:
+        sealed[oo[i] + 12 + lens[i]] ^= 0x40  # first tag byte
+    d = torch.from_numpy(np.ascontiguousarray(sealed)).to(gpu)
+    d_ivs = torch.from_numpy(np.frombuffer(b"".join(ivs), np.uint8).copy()).to(gpu)
+    po, total = ke.plain_layout(slens)
+    dout = torch.full((total + 64,), 0xAB, dtype=torch.uint8, device=gpu)
+    st2 = enc.decrypt_chunks_device(d.data_ptr(), oo, slens, d_ivs, 16, dout, po, gpu).cpu().numpy()
+    plain = dout.cpu().numpy()
+    assert [i for i in range(len(lens)) if st2[i]] == forged
+    assert all(st2[i] == _lib.KCDC_EBADMSG for i in forged)
+    for i in range(len(lens)):
+        got = plain[po[i]:po[i] + lens[i]]
+        if i in forged:
+            assert not got.any(), f"chunk {i}: {int(np.count_nonzero(got))} unauthenticated bytes left"
+        else:
+            assert got.tobytes() == host[offs[i]:offs[i] + lens[i]].tobytes(), i
+    assert (plain[total:] == 0xAB).all()  # nothing written past the layout
+
+
 def test_nonces_differ_by_default(alg, gpu):
     """Without caller nonces, two seals of the same chunk differ (random nonce prefix) and
     both open."""

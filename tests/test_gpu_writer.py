@@ -106,6 +106,55 @@ def test_kat_rows_through_writers(gpu):
         assert (len(split), int(sizes.min()), int(sizes.max())) == want
 
 
+def _aligned_candidate_stops(cuts, limit):
+    """Cut positions c at which a round's region can end so that the next round's resume tile
+    starts exactly at c: the coordinate of c in the next round's stream (c - tail_pos + tail_pos
+    mod 16, tail_pos = previous cut - 64) is a multiple of 128."""
+    stops, prev = [], 0
+    for c in cuts[:-1]:
+        tail = max(prev - 64, 0)
+        if (c - (tail & ~15)) % 128 == 0 and c - prev > 0:
+            stops.append(c)
+            if len(stops) == limit:
+                break
+        prev = c
+    return stops
+
+
+def test_region_ending_on_a_candidate(gpu):
+    """A round whose region ends right after a candidate: its last cut equals the region end, so
+    the batcher keeps it open, and the next round must test that last byte again.  Before the fix
+    (kcdc_writer.cpp resume) a resume tile starting at the region end skipped it and two
+    chunks merged.  Every write here ends at such a cut and is shipped as a round of its own."""
+    import time
+    kat = coracle.gorand_read(5, 5_000_000)
+    for kind, oname, avg in [(1, "buzhash", 32), (1, "buzhash", 1024), (2, "rabinkarp", 32),
+                             (2, "rabinkarp", 1024)]:
+        name = _lib.lib().kcdc_custom_algorithm(kind, avg).decode()
+        want = coracle.split_stream_kind(oname, avg, kat).tolist()
+        stops = _aligned_candidate_stops(want, 120)
+        assert len(stops) >= 20, (name, len(stops))
+        b = WriterBatcher(name, round_bytes=64 << 20, max_wait_us=20)
+        w = b.open()
+        got, pos = [], 0
+        for c in stops + [kat.size]:
+            r0 = b.rounds()
+            w.write(kat[pos:c])
+            pos = c
+            t0 = time.monotonic()
+            while b.rounds() == r0 and time.monotonic() - t0 < 5:
+                time.sleep(0.0002)
+            time.sleep(0.001)
+            got.extend(w.cuts())
+        got.extend(w.finish())
+        rounds = b.rounds()
+        w.close()
+        b.close()
+        assert rounds >= len(stops), (name, rounds, len(stops))
+        assert got == want, f"{name}: {len(got)} vs {len(want)} cuts, first diff at " + str(
+            next((i for i, (x, y) in enumerate(zip(got, want)) if x != y), None))
+
+
 def test_errors(gpu):
     b = WriterBatcher("DYNAMIC-4M-BUZHASH")
     w = b.open()
