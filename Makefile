@@ -50,14 +50,15 @@ build/group_bench: tools/group_bench.cpp include/kcdc.h $(LIB)
 
 .PHONY: all oracle clean asm
 
-# ---- experiment builds (A/B of compile-time tunables; not used by the product)
-VARIANTS ?= b64w8:-DKCDC_BLK=64,-DKCDC_BATCH_WAVES=8 b128w8:-DKCDC_BLK=128,-DKCDC_BATCH_WAVES=8 b128w12:-DKCDC_BLK=128,-DKCDC_BATCH_WAVES=12
+# ---- experiment builds (A/B of compile-time tunables through tools/kbench.py; not the product)
+# e.g. make variants VARIANTS="gap1:-DKCDC_HELP_GAP=1u lane1k:-DKCDC_LANE_MAX=1024"
+VARIANTS ?=
 variants:
 	@mkdir -p build/variants
 	@for v in $(VARIANTS); do \
 	  n=$${v%%:*}; f=$$(echo $${v#*:} | tr ',' ' '); \
 	  echo "variant $$n: $$f"; \
-	  $(HIPCC) $(HIPFLAGS) $$f -shared -o build/variants/libkcdc_$$n.so $(CSRC)/kcdc_kernels.hip $(CSRC)/kcdc_hash.hip $(CSRC)/kcdc_crypt.hip $(CSRC)/kcdc_compress.hip -x hip $(CSRC)/kcdc_api.cpp $(CSRC)/kcdc_tables.cpp $(CSRC)/kcdc_registry.cpp || exit 1; \
+	  $(HIPCC) $(HIPFLAGS) $$f -shared -o build/variants/libkcdc_$$n.so $(CSRC)/kcdc_kernels.hip $(CSRC)/kcdc_hash.hip $(CSRC)/kcdc_crypt.hip $(CSRC)/kcdc_compress.hip -x hip $(CSRC)/kcdc_api.cpp $(CSRC)/kcdc_writer.cpp $(CSRC)/kcdc_tables.cpp $(CSRC)/kcdc_registry.cpp || exit 1; \
 	done
 .PHONY: variants
 

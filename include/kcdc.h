@@ -142,18 +142,38 @@ void kcdc_group_free(kcdc_group* g);
  * object, however it was sliced.  The writer must keep the bytes of its unflushed chunks
  * (objectWriter already buffers them in gather.WriteBuffer) and flush each chunk when its cut
  * arrives.  Calls on one writer are serialised by the caller; writers are independent.
- * kcdc_bw_write blocks while half a round of the writer's bytes is still unshipped. */
+ * kcdc_bw_write blocks while half a round of the writer's bytes is still unshipped.
+ *
+ * Devices: kcdc_bw_batcher_new_devices spreads the writers over a device set (`devices`, or
+ * every device when NULL / ndev <= 0; an index may repeat, e.g. two logical devices on one
+ * GPU).  Each device has its own round thread, streams and arenas; kcdc_bw_open assigns a writer
+ * to the device with the least load (the bytes of its open writers, each counted as the larger
+ * of its size hint and its bytes written: kcdc_bw_open_hint passes the object's expected size,
+ * e.g. the file size the uploader knows, snapshot/upload/upload.go:769-782).  kcdc_bw_device
+ * returns the writer's position in the device list.
+ * Device memory: every open writer holds two arenas of about max_size + 4 x (round_bytes / 8 +
+ * 4 MiB) bytes each (152 MiB at the defaults); kcdc_bw_open fails with KCDC_ENOMEM when the
+ * device cannot hold them.
+ * kcdc_bw_batcher_free ships what is staged, then fails every writer call still blocked in it
+ * (KCDC_EINVAL) and waits for those calls to return; writers not freed before it stay valid for
+ * kcdc_bw_free only. */
 typedef struct kcdc_bw_batcher kcdc_bw_batcher;
 typedef struct kcdc_bw kcdc_bw;
 kcdc_bw_batcher* kcdc_bw_batcher_new(const char* name, int device, uint64_t round_bytes, uint32_t max_wait_us);
-void kcdc_bw_batcher_free(kcdc_bw_batcher* b);  /* after every writer is freed */
+kcdc_bw_batcher* kcdc_bw_batcher_new_devices(const char* name, const int* devices, int ndev, uint64_t round_bytes,
+                                             uint32_t max_wait_us);
+int kcdc_bw_batcher_devices(const kcdc_bw_batcher* b);  /* devices in the set */
+void kcdc_bw_batcher_free(kcdc_bw_batcher* b);
 kcdc_bw* kcdc_bw_open(kcdc_bw_batcher* b);        /* Factory() for one object */
+kcdc_bw* kcdc_bw_open_hint(kcdc_bw_batcher* b, uint64_t size_hint);
+int kcdc_bw_device(const kcdc_bw* w);             /* the writer's device (position in the list) */
 int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len);
 int64_t kcdc_bw_cuts(kcdc_bw* w, uint64_t* out, uint64_t cap); /* final cuts taken (<= cap), or KCDC_E* */
 int kcdc_bw_finish(kcdc_bw* w);
 void kcdc_bw_free(kcdc_bw* w);
 int64_t kcdc_bw_rounds(const kcdc_bw_batcher* b); /* rounds shipped so far (test hook) */
-/* Observability: out[0..n) = rounds, bytes shipped, seconds the round thread spent building and
+/* Observability (summed over the batcher's devices; the span and busy seconds are the largest
+ * device's): out[0..n) = rounds, bytes shipped, seconds the round thread spent building and
  * issuing rounds, seconds it waited for the device, then the device seconds of the rounds' gathers
  * (new bytes over PCIe into the writers' arenas) and of their splits (metadata in, splitter
  * launch, cut lists out), from HIP events, then the device span of all rounds and the seconds of
@@ -193,6 +213,15 @@ int kcdc_split_batch_device(const char* name, const uint8_t* const* d_ptrs, cons
  * path the Go cgo shim calls. */
 int kcdc_split_batch_host(const char* name, const uint8_t* const* h_ptrs, const uint64_t* lens, uint32_t nstreams,
                           uint64_t* cuts, uint64_t cuts_cap, const uint64_t* cut_base, uint64_t* counts, int device);
+/* The same over a device set (`devices`, repeats allowed; NULL / ndev <= 0: every device): the
+ * streams are spread by bytes with kcdc_lpt_assign and each device splits its share from a host
+ * thread of its own (no collectives: SURVEY.md §8e).  Same output contract as one device. */
+int kcdc_split_batch_host_devices(const char* name, const int* devices, int ndev, const uint8_t* const* h_ptrs,
+                                  const uint64_t* lens, uint32_t nstreams, uint64_t* cuts, uint64_t cuts_cap,
+                                  const uint64_t* cut_base, uint64_t* counts);
+/* Longest-processing-time-first assignment by bytes (largest stream first, each to the least
+ * loaded of `ndev` devices, ties to the lower index): dev_of[i] = position of stream i's device. */
+int kcdc_lpt_assign(const uint64_t* lens, uint32_t nstreams, uint32_t ndev, uint32_t* dev_of);
 
 /* ------------------------------------------- one long stream, tiled (config 3)
  * Exact intra-stream parallel CDC of a single device-resident stream: candidate
@@ -347,22 +376,26 @@ int kcdc_compress_chunks_device(const char* algorithm, const uint8_t* d_data, co
  *                         chunks, else 1), 1 or 4
  *   KCDC_TEST_NO_SERVER   1: private streaming handles launch one scan per call instead of using
  *                         the device's resident scan server
+ *   KCDC_TEST_NO_HELP     1: buzhash batch launches without intra-region help (each region is
+ *                         scanned by the wave that owns its stream only)
  * kcdc_test_occupy: occupy `nwg` CUs (one workgroup with all of the CU's LDS each) for
  * `usec` microseconds on `hip_stream`, e.g. to run a batch beside a kernel that holds CUs.
  * kcdc_test_queue_stat: after the last pipelined batch launch has finished (synchronise
  * first), read one word of its queue header: KCDC_TEST_STAT_GIVEUPS (waves that gave up
  * waiting), KCDC_TEST_STAT_DONE (streams finished), KCDC_TEST_STAT_STEALS (requeued
- * workgroups).  Synchronous copy; returns the word, or a negative KCDC_E* code. */
+ * workgroups), KCDC_TEST_STAT_HELPS (tiles scanned by waves that helped another wave's region).  Synchronous copy; returns the word, or a negative KCDC_E* code. */
 #define KCDC_TEST_SPIN_CAP 1
 #define KCDC_TEST_NO_STEAL 2
 #define KCDC_TEST_FORCE_ERROR 3
 #define KCDC_TEST_HASH_LANES 4
 #define KCDC_TEST_NO_SERVER 5
+#define KCDC_TEST_NO_HELP 6
 int kcdc_test_set(int32_t key, int64_t value);
 int kcdc_test_occupy(uint32_t nwg, uint32_t usec, void* hip_stream);
 #define KCDC_TEST_STAT_GIVEUPS 1
 #define KCDC_TEST_STAT_DONE 2
 #define KCDC_TEST_STAT_STEALS 3
+#define KCDC_TEST_STAT_HELPS 4
 int64_t kcdc_test_queue_stat(int32_t key);
 /* Requests the resident scan server has answered in this process (private streaming handles use
  * it while exactly one private handle is open). */

@@ -31,8 +31,8 @@ KCDC_EBADMSG = -74
 
 KIND_FIXED, KIND_BUZHASH, KIND_RABINKARP = 0, 1, 2
 COUNT_FAILED = (1 << 64) - 1  # KCDC_COUNT_FAILED: the batch launch failed on the device
-TEST_SPIN_CAP, TEST_NO_STEAL, TEST_FORCE_ERROR, TEST_HASH_LANES, TEST_NO_SERVER = 1, 2, 3, 4, 5
-STAT_GIVEUPS, STAT_DONE, STAT_STEALS = 1, 2, 3
+TEST_SPIN_CAP, TEST_NO_STEAL, TEST_FORCE_ERROR, TEST_HASH_LANES, TEST_NO_SERVER, TEST_NO_HELP = 1, 2, 3, 4, 5, 6
+STAT_GIVEUPS, STAT_DONE, STAT_STEALS, STAT_HELPS = 1, 2, 3, 4
 
 
 class KcdcError(RuntimeError):
@@ -73,9 +73,15 @@ _SIGS = {
     "kcdc_group_new": (_P, [C.c_char_p, C.c_int, C.c_uint32, C.c_uint32]),
     "kcdc_group_splitter": (_P, [_P]),
     "kcdc_group_free": (None, [_P]),
+    "kcdc_split_batch_host_devices": (C.c_int, [C.c_char_p, _P, C.c_int, _P, _P, C.c_uint32, _P, C.c_uint64, _P, _P]),
+    "kcdc_lpt_assign": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P]),
     "kcdc_bw_batcher_new": (_P, [C.c_char_p, C.c_int, C.c_uint64, C.c_uint32]),
     "kcdc_bw_batcher_free": (None, [_P]),
+    "kcdc_bw_batcher_new_devices": (_P, [C.c_char_p, _P, C.c_int, C.c_uint64, C.c_uint32]),
+    "kcdc_bw_batcher_devices": (C.c_int, [_P]),
     "kcdc_bw_open": (_P, [_P]),
+    "kcdc_bw_open_hint": (_P, [_P, C.c_uint64]),
+    "kcdc_bw_device": (C.c_int, [_P]),
     "kcdc_bw_write": (C.c_int, [_P, _P, C.c_size_t]),
     "kcdc_bw_cuts": (C.c_int64, [_P, _P, C.c_uint64]),
     "kcdc_bw_finish": (C.c_int, [_P]),

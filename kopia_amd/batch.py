@@ -88,6 +88,37 @@ def split_batch_host(name: str, streams, device: int = 0) -> list[np.ndarray]:
     return [cuts[int(base[i]):int(base[i]) + int(counts[i])].astype(np.int64) for i in range(n)]
 
 
+def split_batch_host_devices(name: str, streams, devices=None) -> list[np.ndarray]:
+    """split_batch_host over a device set (None or []: every device; repeats allowed): the streams
+    are spread over the devices by bytes (lpt_assign), each device splits its share."""
+    arrs = [np.frombuffer(s, dtype=np.uint8) if not isinstance(s, np.ndarray) else np.ascontiguousarray(s)
+            for s in streams]
+    n = len(arrs)
+    lens = np.array([a.size for a in arrs], dtype=np.uint64)
+    caps = np.array([cut_capacity(name, int(L)) for L in lens], dtype=np.uint64)
+    base = np.zeros(n, dtype=np.uint64)
+    if n > 1:
+        base[1:] = np.cumsum(caps)[:-1]
+    cap = int(caps.sum())
+    cuts = np.zeros(max(cap, 1), dtype=np.uint64)
+    counts = np.zeros(max(n, 1), dtype=np.uint64)
+    ptrs = (C.c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
+    devs = list(devices or [])
+    darr = (C.c_int * max(len(devs), 1))(*devs)
+    _lib.check(_lib.lib().kcdc_split_batch_host_devices(
+        name.encode(), C.cast(darr, C.c_void_p) if devs else None, len(devs), C.cast(ptrs, C.c_void_p),
+        lens.ctypes.data, n, cuts.ctypes.data, cap, base.ctypes.data, counts.ctypes.data))
+    return [cuts[int(base[i]):int(base[i]) + int(counts[i])].astype(np.int64) for i in range(n)]
+
+
+def lpt_assign(lens, ndev: int) -> np.ndarray:
+    """kcdc_lpt_assign: device position of every stream (largest first to the least loaded)."""
+    a = np.ascontiguousarray(np.asarray(lens, dtype=np.uint64))
+    out = np.zeros(max(a.size, 1), dtype=np.uint32)
+    _lib.check(_lib.lib().kcdc_lpt_assign(a.ctypes.data, a.size, ndev, out.ctypes.data))
+    return out[:a.size]
+
+
 def fill_prng(data: "torch.Tensor", stream_len: int, nstreams: int, stride: int, seed: int, first_sid: int = 0,
               stream=None) -> None:
     import torch

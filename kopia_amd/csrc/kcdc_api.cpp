@@ -800,6 +800,99 @@ extern "C" int kcdc_split_batch_host(const char* name, const uint8_t* const* h_p
     return rc;
 }
 
+// Longest processing time first: streams by bytes, largest first (ties: lower index), each to
+// the least-loaded of `ndev` devices (ties: lower index).  dev_of[i] = position of stream i's
+// device.  Host arithmetic (kopia_amd/dist.py lpt_plan is the same rule).
+extern "C" int kcdc_lpt_assign(const uint64_t* lens, uint32_t n, uint32_t ndev, uint32_t* dev_of) {
+    if (n == 0) return KCDC_OK;
+    if (!lens || !dev_of || ndev == 0) return set_error(KCDC_EINVAL, "null argument or no devices");
+    std::vector<uint32_t> order(n);
+    for (uint32_t i = 0; i < n; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return lens[x] > lens[y]; });
+    std::vector<uint64_t> load(ndev, 0);
+    for (uint32_t i : order) {
+        uint32_t d = 0;
+        for (uint32_t k = 1; k < ndev; k++)
+            if (load[k] < load[d]) d = k;
+        dev_of[i] = d;
+        load[d] += lens[i];
+    }
+    return KCDC_OK;
+}
+
+// kcdc_split_batch_host over a device set: the streams are spread by bytes (kcdc_lpt_assign) and
+// every device runs the double-buffered host path on its share from a thread of its own; the
+// answers land in the caller's arrays as for one device.  Files in host memory in, cut lists out,
+// for a node's GPUs (no collectives, each device independent).
+extern "C" int kcdc_split_batch_host_devices(const char* name, const int* devices, int ndev, const uint8_t* const* h_ptrs,
+                                             const uint64_t* lens, uint32_t nstreams, uint64_t* cuts, uint64_t cuts_cap,
+                                             const uint64_t* cut_base, uint64_t* counts) {
+    const Algo* a = find_algo(name);
+    if (!a) return set_error(KCDC_ENOENT, std::string("unknown splitter: ") + (name ? name : "(null)"));
+    if (nstreams == 0) return KCDC_OK;
+    if (!h_ptrs || !lens || !cuts || !cut_base || !counts) return set_error(KCDC_EINVAL, "null argument");
+    std::vector<int> list;
+    if (!devices || ndev <= 0) {
+        const int nd = kcdc_device_count();
+        if (nd <= 0) return set_error(KCDC_ENODEV, "no HIP device");
+        for (int d = 0; d < nd; d++) list.push_back(d);
+    } else {
+        list.assign(devices, devices + ndev);
+    }
+    for (int d : list) {
+        const int rc = check_device(d);
+        if (rc) return rc;
+    }
+    for (uint32_t i = 0; i < nstreams; i++)
+        if (cut_base[i] > cuts_cap || (i + 1 < nstreams && cut_base[i + 1] < cut_base[i]))
+            return set_error(KCDC_EINVAL, "cut_base must be non-decreasing and within cuts_cap");
+    const uint32_t nd = static_cast<uint32_t>(list.size());
+    std::vector<uint32_t> dev_of(nstreams);
+    (void)kcdc_lpt_assign(lens, nstreams, nd, dev_of.data());
+    struct Share {
+        std::vector<uint32_t> idx;
+        std::vector<const uint8_t*> ptrs;
+        std::vector<uint64_t> lens, base, counts, cuts;
+        uint64_t cap = 0;
+        int rc = KCDC_OK;
+        std::string err;
+    };
+    std::vector<Share> sh(nd);
+    for (uint32_t i = 0; i < nstreams; i++) {
+        Share& S = sh[dev_of[i]];
+        const uint64_t capi = (i + 1 < nstreams ? cut_base[i + 1] : cuts_cap) - cut_base[i];
+        S.idx.push_back(i);
+        S.ptrs.push_back(h_ptrs[i]);
+        S.lens.push_back(lens[i]);
+        S.base.push_back(S.cap);
+        S.cap += capi;
+    }
+    std::vector<std::thread> th;
+    for (uint32_t k = 0; k < nd; k++) {
+        if (sh[k].idx.empty()) continue;
+        th.emplace_back([&, k] {
+            Share& S = sh[k];
+            S.counts.assign(S.idx.size(), 0);
+            S.cuts.assign(std::max<uint64_t>(S.cap, 1), 0);
+            S.rc = kcdc_split_batch_host(name, S.ptrs.data(), S.lens.data(), static_cast<uint32_t>(S.idx.size()),
+                                         S.cuts.data(), S.cap, S.base.data(), S.counts.data(), list[k]);
+            if (S.rc) S.err = kcdc_last_error();
+        });
+    }
+    for (auto& t : th) t.join();
+    for (uint32_t k = 0; k < nd; k++)
+        if (sh[k].rc) return set_error(sh[k].rc, "device " + std::to_string(list[k]) + ": " + sh[k].err);
+    for (uint32_t k = 0; k < nd; k++) {
+        const Share& S = sh[k];
+        for (size_t j = 0; j < S.idx.size(); j++) {
+            const uint32_t i = S.idx[j];
+            counts[i] = S.counts[j];
+            std::memcpy(cuts + cut_base[i], S.cuts.data() + S.base[j], S.counts[j] * sizeof(uint64_t));
+        }
+    }
+    return KCDC_OK;
+}
+
 // ================================================================ long stream
 extern "C" size_t kcdc_long_workspace_bytes(const char* name, uint64_t len) {
     const Algo* a = find_algo(name);

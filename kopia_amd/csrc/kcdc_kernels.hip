@@ -683,11 +683,12 @@ struct BatchArgs {
     // Time-sliced stream queue (LDS-DMA kernel): header words kQHead (tickets taken),
     // kQTail (streams yielded), kQDone (streams finished), kQErr (spin give-ups); ring[P]
     // holds {push number + 1, sid} of yielded streams (0 = empty; zeroed per launch, reset
-    // on take); states[n] the yielded streams' progress.
+    // on take).
     uint32_t* ring;
-    uint64_t* states;
+    uint64_t* help;       // help slots of the pipelined buzhash kernel (split_batch_pipe_kernel), else null
+    uint32_t help_waves;  // launch waves = help slots
     uint32_t ring_mask;
-    uint64_t* trace;  // KCDC_TRACE builds: per stream {start, end, workgroup | wave << 16} (else null)
+    uint64_t* trace;  // KCDC_TRACE builds: 8 words per wave (split_batch_pipe_kernel) (else null)
     uint64_t cuts_cap;
     const uint64_t* cut_end;  // optional: stream i's cut range ends at cut_end[i] (else cut_base[i+1] / cuts_cap)
     const uint64_t* starts;   // optional: stream i's first chunk starts at starts[i] (else 0); the bytes before
@@ -1008,7 +1009,7 @@ __device__ __forceinline__ uint64_t bcast64(uint64_t v) {
 }
 // Header words (uint32 offsets) 2 KiB apart: hammered counters do not share DRAM pages.
 // Word 0 holds the 64-bit {head, tail} ticket counter (kQHT, below).
-constexpr int kQDone = 512, kQErr = 1536, kQSteal = 1024;
+constexpr int kQDone = 512, kQErr = 1536, kQSteal = 1024, kQHelp = 1600;
 // Rarely read words (kept out of the kernel arguments, whose SGPRs the hot loop needs):
 // kQCfg+0 spin cap, kQCfg+1 steal period; kQFlags.. one flag per workgroup (grid <= 256):
 // 0 until workgroup b starts (1) or a waiting wave requeues its preassigned streams (2).
@@ -1028,51 +1029,29 @@ constexpr uint32_t kStealSpins = 256;                            // ~0.5 ms of p
 // before their segments (a 4 KiB piece in the wave's warm slot) and hashes 16 steps of
 // 128-byte runs (8 KiB step slot).  The warm piece and first step of the NEXT tile are
 // DMA'd during the current tile's last step, so a tile boundary exposes no latency:
-//  * next tile of the same region: always known in advance;
+//  * next tile of the same region: known in advance (the owner's claim on it, below);
 //  * next stream (quantum spent, or the region's last tile with no further region): the
 //    next ticket is taken by an atomic at the START of that tile and its ring entry
 //    (progress + stream parameters, 7 tagged 16-byte sc1 granules) loaded mid-tile, so
 //    both global round trips (~5 us each under full HBM load) hide under the hashing.
 // Only a candidate that ends a region early (the next region is not known before the
 // tile ends) and the first tile of the launch expose a DMA latency.
-#ifndef KCDC_PIPE_YIELD_BYTES
-#define KCDC_PIPE_YIELD_BYTES (768 << 10)
-#endif
-constexpr int64_t kPipeYield = KCDC_PIPE_YIELD_BYTES;
-#ifndef KCDC_PIPE_TAIL_YIELD_BYTES
-#define KCDC_PIPE_TAIL_YIELD_BYTES (768 << 10)  // = the long quantum: short tail quanta measured no gain (128K 1.366 vs 1.347 ms)
-#endif
-#ifndef KCDC_PIPE_TAIL_BACKLOG
-#define KCDC_PIPE_TAIL_BACKLOG 512
-#endif
-// Quantum of a visit from the number of streams queued behind the taken ticket: none
-// waiting -> run to completion; a long queue -> long quanta (few hand-offs); a short queue
-// (the end of the batch) -> short quanta, so streams finish together instead of the last
-// ones running a whole long quantum alone (the final idle tail was ~1 quantum per wave).
-constexpr int64_t kPipeTailYield = KCDC_PIPE_TAIL_YIELD_BYTES;
-constexpr int64_t kPipeTailBacklog = KCDC_PIPE_TAIL_BACKLOG;
-__device__ __forceinline__ int64_t pipe_quantum(int64_t backlog) {
-    if (backlog <= 0 || kPipeYield <= 0) return kNoYield;
-    return backlog > kPipeTailBacklog ? kPipeYield : kPipeTailYield;
-}
+//
+// Intra-region help (round 4).  At the end of a batch -- and in any launch with fewer streams
+// than waves (a writer round, a handful of files) -- waves wait with nothing to scan while each
+// remaining region is walked tile by tile by the one wave that owns its stream: launch time vs
+// stream count (profiles/r04/tail) put that tail at ~0.2 ms of a 1.4 ms config-2 launch.
+// cand(p) is a pure function of the 64 bytes ending at p, so any wave can scan
+// any tile of a region; only the FIRST candidate decides the cut.  So every owner publishes its
+// region in its help slot: the tile grid (tile 0 at ct0, T bytes per tile, K tiles, region end
+// hi) and a claim word {epoch | top | bottom}.  The owner claims its tiles from the bottom (one
+// atomic add per tile, issued a step ahead of need); a waiting wave claims the top tile by
+// compare-and-swap, scans it as a one-tile task and posts the tile's first candidate, tagged with
+// the slot's epoch, in the slot's result row.  An owner whose claim fails resolves the region
+// from the row: the first candidate in tile order, else the forced cut; a row entry still pending
+// after kHelpWaitTicks is scanned by the owner itself, so no owner depends on another wave.
+constexpr int64_t kPipeYield = 768 << 10;  // visit quantum while streams wait (384 K-1.5 M: within noise)
 constexpr int kPEntryLanes = 8;
-// Probe entries (sid | kProbeBit): when waves wait for work at the end of a batch, an owner
-// with at least two tiles of its region left queues a probe that scans the region's upper
-// half while the owner scans the lower half; a handshake word (pword) decides which of the
-// two finishes the region.  Off by default: correct (debug-checked parity), but no faster on
-// the 4096 x 4 MiB batch -- the tail's idle waves are largely compensated by their SIMD
-// siblings running alone.
-constexpr uint32_t kProbeBit = 0x80000000u;
-#ifndef KCDC_PROBES
-#define KCDC_PROBES 0
-#endif
-constexpr int64_t kProbeMinHalf = int64_t(64) * KCDC_LANE_MAX;  // one full tile
-#ifndef KCDC_PROBE_BACKLOG
-#define KCDC_PROBE_BACKLOG 64
-#endif
-// Owners poll the queue counter (are waves waiting?) only in visits taken with a backlog
-// below this: a per-tile load of the hammered counter costs ~10% outside the tail.
-constexpr int64_t kProbeBacklog = KCDC_PROBE_BACKLOG;
 constexpr int kPEntryStride = 128;
 
 struct WarmSlots {
@@ -1082,14 +1061,15 @@ static_assert(sizeof(DmaSlots) + sizeof(WarmSlots) + sizeof(BuzShared) <= 160 * 
               "step slots + warm slots + table exceed the CU's 160 KiB of LDS");
 
 struct PStream {
-    uint32_t sid;    // | kProbeBit for a probe
+    uint32_t sid;    // | kHelpBit for a help task
     int64_t n, off0;
     const uint8_t* abase;
-    uint64_t cb, cap, cnt;
-    int64_t s, ct;   // chunk start (a probe carries its owner's); next tile coordinate (< 0: not set up)
-    uint32_t epoch;  // the stream's probe epoch (one per region that spawned a probe)
-    int64_t aux;     // owner: coordinate where this region's probe starts (0: none); probe: range end
+    uint64_t cb, cap, cnt;  // help task: cb = owner slot, cnt = tile index
+    int64_t s, ct;          // chunk start (help task: the owner's tile 0); next tile coordinate (< 0: not set up)
+    uint32_t epoch;         // help task: the owner slot's epoch
+    int64_t aux;            // help task: the region end (coordinate)
 };
+constexpr uint32_t kHelpBit = 0x80000000u;
 
 __device__ __forceinline__ void pstream_fresh(PStream& st, uint32_t sid, uint64_t p, uint64_t n, uint64_t cb,
                                               uint64_t cend) {
@@ -1145,8 +1125,8 @@ __device__ __forceinline__ bool pstream_region(const BatchArgs& a, PStream& st, 
 }
 
 // First tile coordinate of stream e's first region when a previous round already tested the
-// positions below resume[e] (kcdc_bw_*): the scan starts at the tile holding
-// min(resume, region end) instead of at s + min - 1; -1 (set up as usual) otherwise.
+// positions below resume[e] (kcdc_bw_*): the scan starts at the tile holding min(resume, region
+// end) instead of at s + min - 1; -1 (set up as usual) otherwise.
 __device__ __forceinline__ int64_t resume_ct(const BatchArgs& a, uint32_t e, int64_t s, int64_t n, int64_t off0) {
     if (!a.resume) return -1;
     const int64_t r = static_cast<int64_t>(a.resume[e]);
@@ -1187,8 +1167,8 @@ __device__ __forceinline__ void pentry_decode(PStream& st, const u32x4& v) {
     st.n = static_cast<int64_t>(rl64(v, 4));
     st.cb = rl64(v, 5);
     st.cap = rl64(v, 6);
-    st.aux = static_cast<int64_t>(rl64(v, 7));
-    st.epoch = static_cast<uint32_t>(__builtin_amdgcn_readlane(v.w, 7));
+    st.aux = 0;
+    st.epoch = 0;
 }
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t pring_rsrc(const BatchArgs& a) {
     return __builtin_amdgcn_make_buffer_rsrc(a.ring, static_cast<short>(0),
@@ -1202,7 +1182,7 @@ __device__ __forceinline__ u32x4 pentry_load(const BatchArgs& a, int lane, uint3
                                                  16 /* sc1 */);
 }
 __device__ __forceinline__ bool pentry_ok(const u32x4& v, int lane, uint32_t e) {
-    return __ballot(lane < kPEntryLanes && v.x != e + 1u) == 0;
+    return __ballot(lane < kPEntryLanes - 1 && v.x != e + 1u) == 0;
 }
 
 #ifndef KCDC_DEBUG_CHECKS
@@ -1212,9 +1192,10 @@ __device__ __forceinline__ bool pentry_ok(const u32x4& v, int lane, uint32_t e) 
 // {code, sid, ticket, detail} in header words kQStat+16.. and return false (wave exits).
 __device__ __forceinline__ bool pcheck(const BatchArgs& a, int lane, const PStream& st, uint32_t tk, uint32_t where) {
 #if KCDC_DEBUG_CHECKS
+    if (st.sid & kHelpBit) return true;
     uint32_t code = 0;
     uint64_t detail = 0;
-    const uint32_t sid = st.sid & ~kProbeBit;
+    const uint32_t sid = st.sid;
     if (sid >= a.nstreams) {
         code = 1;
         detail = st.sid;
@@ -1236,7 +1217,7 @@ __device__ __forceinline__ bool pcheck(const BatchArgs& a, int lane, const PStre
         } else if (st.cap != uni64(cut_end_of(a, sid)) - cb) {
             code = 7;
             detail = st.cap;
-        } else if (!(st.sid & kProbeBit) && (st.s < 0 || st.s > st.n)) {
+        } else if (st.s < 0 || st.s > st.n) {
             code = 6;
             detail = static_cast<uint64_t>(st.s);
         }
@@ -1285,13 +1266,15 @@ __device__ __forceinline__ uint64_t qht_take(const BatchArgs& a, int lane, uint6
     return qht_value(static_cast<uint32_t>(raw), static_cast<uint32_t>(raw >> 32));
 }
 
-__device__ __forceinline__ void pwrite(const BatchArgs& a, int lane, uint32_t e, const PStream& st, bool tomb);
-#ifndef KCDC_STEAL
-#define KCDC_STEAL 1
-#endif
+// Preassigned first tickets are spread over the grid: wave w of workgroup b holds ticket
+// w * grid + b, so a launch with fewer streams than waves puts at most one owner on a CU (the
+// others' SIMDs and DMA queues stay free for helpers).
+__device__ __forceinline__ uint32_t first_ticket(uint32_t block, uint32_t wave) { return wave * gridDim.x + block; }
 
-// Forward progress without co-residency.  Each wave's first ticket is preassigned (its global
-// wave index, init_ring_kernel), so a workgroup that is not resident -- another kernel holds
+__device__ __forceinline__ void pwrite(const BatchArgs& a, int lane, uint32_t e, const PStream& st, bool tomb);
+
+// Forward progress without co-residency.  Each wave's first ticket is preassigned
+// (first_ticket, init_ring_kernel), so a workgroup that is not resident -- another kernel holds
 // its CU -- would keep its streams while the resident waves wait for them.  A wave that has
 // waited kStealSpins polls scans the workgroup flags; for a workgroup that has not started it
 // swaps the flag 0 -> 2 and requeues that workgroup's preassigned streams as fresh ring
@@ -1321,13 +1304,13 @@ __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (bcast(old) != 0u) return false;  // it started (or another wave stole it) meanwhile
-    const uint32_t first = found * wg_waves;
-    const uint32_t k = first >= a.nstreams ? 0u : min(wg_waves, a.nstreams - first);
+    uint32_t k = 0;
+    for (uint32_t w = 0; w < wg_waves; w++) k += first_ticket(found, w) < a.nstreams ? 1u : 0u;
     if (k == 0) return true;
     const uint64_t ht = qht_take(a, lane, static_cast<uint64_t>(k) << 32);  // reserve k entries
     const uint32_t e0 = static_cast<uint32_t>(ht >> 32);
-    for (uint32_t i = 0; i < k; i++) {
-        const uint32_t sid = first + i;
+    for (uint32_t w = 0; w < k; w++) {  // first_ticket grows with w: the first k waves held streams
+        const uint32_t sid = first_ticket(found, w);
         PStream st;
         const uint64_t cb = uni64(a.cut_base[sid]);
         pstream_fresh(st, sid, uni64(reinterpret_cast<uint64_t>(a.ptrs[sid])), uni64(a.lens[sid]), cb,
@@ -1335,26 +1318,208 @@ __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
         if (a.starts) st.s = static_cast<int64_t>(uni64(a.starts[sid]));
         st.ct = resume_ct(a, sid, st.s, st.n, st.off0);
         uniformize(st);
-        pwrite(a, lane, e0 + i, st, false);
+        pwrite(a, lane, e0 + w, st, false);
     }
     if (lane == 0) add_agent(a.queue + kQSteal, 1u);
     return true;
 }
 
-#ifndef KCDC_POLL_BACKOFF
-#define KCDC_POLL_BACKOFF 32  // s_sleep argument once KCDC_POLL_AFTER polls saw no stream finish (0: always 16);
-                             // 32: 1.339-1.344 vs 1.363 ms on config 2 (profiles/r03/buz/kbench_poll_*.log)
+// ------------------------------------------------------------------ help slots
+// Slot g (one per launch wave) in the help area: claim word at 128 * g (own line), the region
+// granules at kHelpParams + 64 * g, the result row at kHelpRows + 8 * kHelpTiles * g.
+//   claim  {epoch:24 | top:20 | bottom:20}: tiles [0, bottom) are the owner's, [top, K) the
+//          helpers'; epoch 0 = nothing published (init_ring_kernel zeroes every claim word).
+//   params 4 granules {epoch, lo, hi, x}: {ptr, sid}, {n, K}, {ct0, T}, {hi, 0}.
+//   row[k] {epoch:24 | state:8 | rel:32}: state 1 no candidate in tile k, 2 first candidate at
+//          ct0 + rel; anything else (or another epoch) pending.  Posted by atomic max, so a
+//          stale helper's older epoch never overwrites a newer result.
+#ifndef KCDC_HELP_EVERY
+#define KCDC_HELP_EVERY 2
 #endif
-#ifndef KCDC_POLL_AFTER
-#define KCDC_POLL_AFTER 8u
+#ifndef KCDC_HELP_GAP
+#define KCDC_HELP_GAP 2u
 #endif
-#ifndef KCDC_DONE_EVERY
-#define KCDC_DONE_EVERY 4u  // waiting waves read the done counter every this many polls of their entry
-                           // (4 vs 1: -1.3 % and -0.3 % in two A/Bs, profiles/r03/buz/kbench_done_*.log)
+constexpr int kHelpTiles = 128;          // regions of up to 128 tiles take help (every registered name)
+constexpr uint32_t kHelpMinTiles = 3;    // the owner's tile, its next one, and at least one more
+constexpr uint64_t kHelpWaitTicks = 20000;  // 200 us of s_memrealtime (a tile takes 15-40 us)
+__device__ __forceinline__ size_t help_params_off(uint32_t nw) { return 128ull * nw; }
+__device__ __forceinline__ size_t help_rows_off(uint32_t nw) { return 128ull * nw + 64ull * nw; }
+__device__ __forceinline__ uint64_t* help_claim(const BatchArgs& a, uint32_t g) {
+    return reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(a.help) + 128ull * g);
+}
+__device__ __forceinline__ uint64_t* help_row(const BatchArgs& a, uint32_t g) {
+    return reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(a.help) + help_rows_off(a.help_waves)) +
+           static_cast<uint64_t>(kHelpTiles) * g;
+}
+__device__ __forceinline__ uint64_t hclaim(uint32_t ep, uint32_t top, uint32_t bot) {
+    return (static_cast<uint64_t>(ep) << 40) | (static_cast<uint64_t>(top) << 20) | bot;
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t help_params_rsrc(const BatchArgs& a) {
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(a.help) + help_params_off(a.help_waves),
+                                             static_cast<short>(0), static_cast<int>(64u * a.help_waves), 0x00020000);
+}
+
+// Owner: publish region [ct0, hi] (K tiles of T bytes, tile 0 already the owner's) in slot g
+// under epoch ep.  Order: the row zeroed and the granules stored write-through (sc1), drained,
+// then the claim word -- a helper that sees epoch ep in the claim word reads granules and a row
+// of that epoch (or of a later one, when the owner has moved on and waits for nothing).
+__device__ void help_publish(const BatchArgs& a, int lane, uint32_t g, uint32_t ep, const PStream& st, int64_t ct0,
+                             int64_t hi, uint32_t K, int64_t T) {
+    uint64_t* row = help_row(a, g);
+    for (uint32_t k = static_cast<uint32_t>(lane); k < K; k += kWave)
+        __hip_atomic_store((gu64*)(row + k), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) {
+        const __amdgpu_buffer_rsrc_t r = help_params_rsrc(a);
+        const int base = static_cast<int>(64u * g);
+        const uint64_t p = reinterpret_cast<uint64_t>(st.abase) + static_cast<uint64_t>(st.off0);
+        __builtin_amdgcn_raw_buffer_store_b128(pgranule(ep, p, st.sid), r, base + 0, 0, 16 /* sc1 */);
+        __builtin_amdgcn_raw_buffer_store_b128(pgranule(ep, static_cast<uint64_t>(st.n), K), r, base + 16, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(pgranule(ep, static_cast<uint64_t>(ct0), static_cast<uint32_t>(T)), r,
+                                               base + 32, 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(pgranule(ep, static_cast<uint64_t>(hi), 0), r, base + 48, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store((gu64*)help_claim(a, g), hclaim(ep, K, 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Owner: no more tiles of this slot's region for helpers (the region or the visit ended).
+__device__ __forceinline__ void help_close(const BatchArgs& a, int lane, uint32_t g, uint32_t ep) {
+    if (lane == 0) __hip_atomic_store((gu64*)help_claim(a, g), hclaim(ep, 0, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Owner: read its claim word back by LDS-DMA (sc1, past L1) into LDS at m0 (16 bytes per lane,
+// every lane the same granule: the word lands at m0).  The waitcnt pass does not see it (as the
+// slot fills), so nothing waits for it inside the hash loop; the reader's own vmcnt wait does.
+__device__ __forceinline__ void help_claim_dma(const BatchArgs& a, int lane, uint32_t g, uint32_t m0) {
+    (void)lane;
+    u32x4 d;
+    const uint64_t base = reinterpret_cast<uint64_t>(a.help);
+    d.x = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(base));
+    d.y = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(base >> 32) & 0xFFFFu);
+    d.z = __builtin_amdgcn_readfirstlane(128u * a.help_waves);
+    d.w = 0x00020000u;
+    const int32_t off = static_cast<int32_t>(128u * g);
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen sc1 lds"
+                 :: "s"(m0), "v"(off), "s"(d) : "memory");
+}
+// Helper: post tile k's first candidate (coordinate f, or -1) to slot g's row under epoch ep.
+__device__ __forceinline__ void help_post(const BatchArgs& a, int lane, uint32_t g, uint32_t ep, uint32_t k,
+                                          int64_t ct0, int64_t f) {
+    const uint64_t v = (static_cast<uint64_t>(ep) << 40) |
+                       (f >= 0 ? (2ull << 32) | static_cast<uint64_t>(static_cast<uint32_t>(f - ct0)) : (1ull << 32));
+    if (lane == 0) {
+        __hip_atomic_fetch_max((gu64*)(help_row(a, g) + k), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        add_agent(a.queue + kQHelp, 1u);
+    }
+}
+// Owner whose claim failed: the helpers hold tiles [k0, K).  Returns the region's first
+// candidate (coordinate) among them, -1 if they have none, or -2 - k when tile k is still
+// pending after kHelpWaitTicks (the owner then scans from tile k itself).
+__device__ int64_t help_wait(const BatchArgs& a, int lane, uint32_t g, uint32_t ep, uint32_t k0, uint32_t K,
+                             int64_t ct0) {
+    const uint64_t* row = help_row(a, g);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        int64_t res = -1;
+        uint32_t pend_at = 0xFFFFFFFFu;
+        for (uint32_t b = k0; b < K; b += kWave) {
+            const uint32_t k = b + static_cast<uint32_t>(lane);
+            const uint64_t v = k < K ? ld_agent64(const_cast<uint64_t*>(row + k)) : 0ull;
+            const bool mine = k < K && static_cast<uint32_t>(v >> 40) == ep;
+            const uint32_t stt = mine ? static_cast<uint32_t>(v >> 32) & 0xFFu : 0u;
+            const uint64_t pend = __ballot(k < K && stt != 1u && stt != 2u);
+            const uint64_t cand = __ballot(stt == 2u);
+            const uint64_t ev = pend | cand;
+            if (ev) {
+                const int f = __builtin_ctzll(ev);
+                if ((cand >> f) & 1ull) {
+                    const uint32_t rel = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(v), f));
+                    res = ct0 + static_cast<int64_t>(rel);
+                } else {
+                    pend_at = b + static_cast<uint32_t>(f);
+                }
+                break;
+            }
+        }
+        if (pend_at == 0xFFFFFFFFu) return res;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kHelpWaitTicks) return -2 - static_cast<int64_t>(pend_at);
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+// Waiting wave: claim the top tile of the published region with the most unclaimed tiles
+// among 64 slots (a window that moves with every attempt).  On success `task` is a one-tile
+// help task: sid | kHelpBit, the stream's pointer and length, s = the owner's tile 0,
+// ct = the tile, aux = the region end, cb = slot, cnt = tile index, epoch.
+__device__ bool help_find(const BatchArgs& a, int lane, uint32_t me, uint32_t attempt, PStream& task) {
+    const uint32_t nw = a.help_waves;
+    const uint32_t base = (me * 97u + attempt * static_cast<uint32_t>(kWave)) % nw;
+    const uint32_t g = (base + static_cast<uint32_t>(lane)) % nw;
+    const uint64_t c = lane < static_cast<int>(nw) ? ld_agent64(help_claim(a, g)) : 0ull;
+    const uint32_t ep = static_cast<uint32_t>(c >> 40), top = static_cast<uint32_t>(c >> 20) & 0xFFFFFu,
+                   bot = static_cast<uint32_t>(c) & 0xFFFFFu;
+    // leave the owner its next tile: claim only tiles >= bottom + 1
+    uint32_t avail = ep != 0u && g != me && top >= bot + KCDC_HELP_GAP ? top - bot - (KCDC_HELP_GAP - 1u) : 0u;
+    uint32_t best = avail;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) best = max(best, static_cast<uint32_t>(__shfl_xor(static_cast<int>(best), d)));
+    best = __builtin_amdgcn_readfirstlane(best);
+#if KCDC_TRACE  // header words kQStat + 0..4: attempts, empty windows, lost races, stale records, tasks
+    if (lane == 0) add_agent(a.queue + kQStat, 1u);
+    if (best == 0u && lane == 0) add_agent(a.queue + kQStat + 1, 1u);
 #endif
+    if (best == 0u) return false;
+    const int f = __builtin_ctzll(__ballot(avail == best));
+    const uint32_t gs = static_cast<uint32_t>(__builtin_amdgcn_readlane(g, f));
+    const uint64_t cw = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(c >> 32), f)))
+                         << 32) |
+                        static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(c), f));
+    uint64_t old = cw;
+    if (lane == 0)
+        __hip_atomic_compare_exchange_strong((gu64*)help_claim(a, gs), &old, cw - (1ull << 20), __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (qht_value(static_cast<uint32_t>(old), static_cast<uint32_t>(old >> 32)) != cw) {  // lost the race
+#if KCDC_TRACE
+        if (lane == 0) add_agent(a.queue + kQStat + 2, 1u);
+#endif
+        return false;
+    }
+    const uint32_t eps = static_cast<uint32_t>(cw >> 40);
+    const uint32_t k = (static_cast<uint32_t>(cw >> 20) & 0xFFFFFu) - 1u;
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(help_params_rsrc(a), static_cast<int>(64u * gs) + 16 * (lane & 3),
+                                                          0, 16 /* sc1 */);
+    if (__ballot(lane < 4 && v.x != eps) != 0) {  // the owner has moved on: nobody waits for this tile
+#if KCDC_TRACE
+        if (lane == 0) add_agent(a.queue + kQStat + 3, 1u);
+#endif
+        return false;
+    }
+#if KCDC_TRACE
+    if (lane == 0) add_agent(a.queue + kQStat + 4, 1u);
+#endif
+    const uint64_t p = rl64(v, 0);
+    task.sid = static_cast<uint32_t>(__builtin_amdgcn_readlane(v.w, 0)) | kHelpBit;
+    task.off0 = static_cast<int64_t>(p & 15u);
+    task.abase = reinterpret_cast<const uint8_t*>(p - static_cast<uint64_t>(task.off0));
+    task.n = static_cast<int64_t>(rl64(v, 1));
+    task.s = static_cast<int64_t>(rl64(v, 2));  // tile 0
+    const int64_t T = static_cast<int64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(v.w, 2)));
+    task.ct = task.s + static_cast<int64_t>(k) * T;
+    task.aux = static_cast<int64_t>(rl64(v, 3));
+    task.cb = gs;
+    task.cnt = k;
+    task.cap = 0;
+    task.epoch = eps;
+    return true;
+}
+
 // Blocking resolution of ticket t (its ring entry, polled): 1 resolved, 2 tombstone (take
-// another ticket), 0 every stream is done, or the wave gave up (error word) -- it exits.
-__device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, uint32_t wg_waves) {
+// another ticket), 3 a help task in st (the ticket is still held), 0 every stream is done, or
+// the wave gave up (error word) -- it exits.
+//   Polling backoff: in the tail ~1,000 waves poll their entry and the done counter; once 8 polls
+//   in a row saw no stream finish they sleep s_sleep 32 (1.339-1.344 vs 1.363 ms on config 2,
+//   profiles/r03/buz/kbench_poll_*.log) and read the done counter every 4th poll.
+//   Help: a waiting wave looks for a tile to help with every kHelpEvery polls (help_find).
+constexpr uint32_t kPollAfter = 8, kDoneEvery = 4, kHelpEvery = KCDC_HELP_EVERY;
+__device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, uint32_t wg_waves, uint32_t me,
+                        bool can_help) {
     const uint32_t n = a.nstreams;
     const uint32_t spin_cap = ld_agent(a.queue + kQCfg), steal_spins = ld_agent(a.queue + kQCfg + 1);
     uint32_t idle = 0;            // polls since a stream last finished
@@ -1367,7 +1532,7 @@ __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, u
             return 1;
         }
         uint32_t stop = 0;
-        if (lane == 0 && spin % KCDC_DONE_EVERY == 0) {
+        if (lane == 0 && spin % kDoneEvery == 0) {
             // Progress = streams finishing.  Not the {head, tail} word: every ticket take and
             // yield is an atomic on it, and waiting waves polling it slowed those by ~7%.
             const uint32_t done = ld_agent(a.queue + kQDone);
@@ -1381,19 +1546,21 @@ __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, u
             }
         }
         if (bcast(stop)) return 0;
-        if (KCDC_STEAL && steal_spins && spin % steal_spins == steal_spins - 1) {
+        if (steal_spins && spin % steal_spins == steal_spins - 1) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA is in flight here either
             try_steal(a, lane, wg_waves);
             continue;  // poll the entry again at once
         }
-#if KCDC_POLL_BACKOFF
+        if (can_help && spin % kHelpEvery == kHelpEvery - 1) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (help_find(a, lane, me, spin / kHelpEvery, st)) return 3;
+        }
         // back off while nothing finishes: ~1,000 waiting waves polling two words every 0.5 us
         // load the L2 channel of the done counter in the batch's tail
-        if (bcast(idle) >= KCDC_POLL_AFTER)
-            __builtin_amdgcn_s_sleep(KCDC_POLL_BACKOFF);
+        if (bcast(idle) >= kPollAfter)
+            __builtin_amdgcn_s_sleep(32);
         else
-#endif
-        __builtin_amdgcn_s_sleep(16);
+            __builtin_amdgcn_s_sleep(16);
     }
 }
 
@@ -1412,8 +1579,6 @@ __device__ __forceinline__ void pwrite(const BatchArgs& a, int lane, uint32_t e,
         __builtin_amdgcn_raw_buffer_store_b128(pgranule(tag, static_cast<uint64_t>(st.n), 0), r, base + 64, 0, 16);
         __builtin_amdgcn_raw_buffer_store_b128(pgranule(tag, st.cb, 0), r, base + 80, 0, 16);
         __builtin_amdgcn_raw_buffer_store_b128(pgranule(tag, st.cap, 0), r, base + 96, 0, 16);
-        __builtin_amdgcn_raw_buffer_store_b128(pgranule(tag, static_cast<uint64_t>(st.aux), st.epoch), r, base + 112,
-                                               0, 16);
     }
 }
 
@@ -1434,9 +1599,10 @@ __device__ __forceinline__ void pentry_dma(const BatchArgs& a, int lane, uint32_
                  :: "s"(m0), "v"(off), "s"(d) : "memory");
 }
 
-// Region bounds (coordinates) of the stream's current chunk.
+// Region bounds (coordinates) of the stream's current chunk; a help task's is its tile
+// [ct, region end].
 __device__ __forceinline__ void pregion(const BatchArgs& a, const PStream& st, int64_t& lo, int64_t& hi) {
-    if (st.sid & kProbeBit) {  // a probe scans [ct, aux] (coordinates); s stays the owner's
+    if (st.sid & kHelpBit) {
         lo = st.ct;
         hi = st.aux;
         return;
@@ -1446,41 +1612,17 @@ __device__ __forceinline__ void pregion(const BatchArgs& a, const PStream& st, i
     hi = (st.s + mx - 1 < st.n - 1 ? st.s + mx - 1 : st.n - 1) + st.off0;
 }
 
-// Probe handshake: one 64-bit word per stream (16-B stride in the queue workspace),
-// lo = epoch << 2 | state, hi = the probe's first candidate - (s + off0) + 1 (0: none).
-// state 0: probe running (or none out), 1: the probe posted its candidate, 2: the owner
-// found nothing below the probe's start and handed the region over.  Whoever arrives
-// second finishes the region; the owner cancels a probe by moving to the next epoch.
-// Invariant: while a stream has no probe out its word is {epoch, 0, 0}.
-__device__ __forceinline__ uint64_t pword(uint32_t epoch, uint32_t state, uint32_t cand) {
-    return (static_cast<uint64_t>(cand) << 32) | ((epoch & 0x3FFFFFFFu) << 2) | state;
-}
-__device__ __forceinline__ uint64_t* probe_word(const BatchArgs& a, uint32_t sid) {
-    return reinterpret_cast<uint64_t*>(reinterpret_cast<uint32_t*>(a.states) + 4ull * (sid & ~kProbeBit));
-}
-// Lane 0 compare-and-swaps the word; returns the value it found (== expect: swapped).
-__device__ __forceinline__ uint64_t probe_cas(const BatchArgs& a, int lane, uint32_t sid, uint64_t expect,
-                                              uint64_t desired) {
-    uint64_t old = expect;
-    if (lane == 0)
-        __hip_atomic_compare_exchange_strong((gu64*)probe_word(a, sid), &old, desired, __ATOMIC_RELAXED,
-                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return qht_value(static_cast<uint32_t>(old), static_cast<uint32_t>(old >> 32));
-}
-__device__ __forceinline__ void probe_reset(const BatchArgs& a, int lane, uint32_t sid, uint32_t epoch) {
-    if (lane == 0) st_agent64(probe_word(a, sid), pword(epoch, 0, 0));
-}
-// A probe's per-tile poll of the word (lane 0; consume it behind a wait point).
-__device__ __forceinline__ uint64_t probe_poll(const BatchArgs& a, int lane, uint32_t sid) {
-    return lane == 0 ? ld_agent64(probe_word(a, sid)) : 0ull;
-}
-
 __device__ __forceinline__ void ptile_issue(const PStream& st, int64_t hi, uint32_t wl, uint32_t sl, int lane,
                                             int64_t lane_cap) {
     const TileGeom g = tile_geom(st.ct, hi, st.abase, st.off0, st.off0 + st.n, lane_cap);
     dma_piece(g.ld, g.ld.tb, wl, st.ct, g.L, -1, lane);
     dma_step128(g.ld, g.ld.tb, sl, st.ct, g.L, 0, lane);
 }
+
+// Visit quantum from the number of streams queued behind the taken ticket: none waiting ->
+// run to completion; otherwise 768 KiB (short tail quanta measured no gain, and helpers now
+// split the tail's regions).
+__device__ __forceinline__ int64_t pipe_quantum(int64_t backlog) { return backlog <= 0 ? kNoYield : kPipeYield; }
 
 template <bool TOP>
 __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_pipe_kernel(BatchArgs a) {
@@ -1491,12 +1633,8 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
     __syncthreads();
     const int lane = threadIdx.x & (kWave - 1);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-#if KCDC_REREAD
-    using Hash = BuzRe;
-#else
-    using Hash = BuzRing;
-#endif
-    Hash hash;
+    const uint32_t me = blockIdx.x * kDmaWaves + wave;  // this wave's help slot
+    BuzRing hash;
     hash.tab = reinterpret_cast<const char*>(smtab.tab);
     hash.lane4 = static_cast<uint32_t>(lane) * 4u;
     hash.mask = a.mask;
@@ -1504,16 +1642,21 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
     uint8_t* sl = smslots.b[wave][0];
     uint8_t* wl = smwarm.b[wave];
     const uint32_t sl32 = lds_addr(sl), wl32 = lds_addr(wl);
-#if KCDC_TRACE  // per wave at trace[4 * global wave]: start, end, ticks in blocking takes, count
+#if KCDC_TRACE  // per wave at trace[8 * global wave]: start, end, ticks in blocking takes, the last take's
+                // start, help tiles, their ticks, the end of the wave's last own tile, own tiles
     const uint32_t gw = blockIdx.x * kDmaWaves + wave;
-    uint64_t tr_block = 0, tr_nblock = 0, tr_last = 0;
-    if (lane == 0) a.trace[4 * gw] = __builtin_amdgcn_s_memrealtime();
+    uint64_t tr_block = 0, tr_nblock = 0, tr_last = 0, tr_help = 0, tr_help_t = 0, tr_own_end = 0, tr_own = 0;
+    if (lane == 0) a.trace[8 * gw] = __builtin_amdgcn_s_memrealtime();
 #define KCDC_PRET                                                                 \
     do {                                                                          \
         if (lane == 0) {                                                          \
-            a.trace[4 * gw + 1] = __builtin_amdgcn_s_memrealtime();                \
-            a.trace[4 * gw + 2] = tr_block;                                       \
-            a.trace[4 * gw + 3] = tr_last;                                        \
+            a.trace[8 * gw + 1] = __builtin_amdgcn_s_memrealtime();                \
+            a.trace[8 * gw + 2] = tr_block;                                       \
+            a.trace[8 * gw + 3] = tr_last;                                        \
+            a.trace[8 * gw + 4] = tr_help;                                        \
+            a.trace[8 * gw + 5] = tr_help_t;                                      \
+            a.trace[8 * gw + 6] = tr_own_end;                                     \
+            a.trace[8 * gw + 7] = tr_own;                                         \
         }                                                                         \
         return;                                                                   \
     } while (0)
@@ -1525,7 +1668,16 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
 
     PStream cur;
     int64_t budget = kNoYield;
-    bool dry = false;  // the queue was (nearly) dry when this stream was taken: probes may pay
+    // Help state of this wave's own slot (wave-uniform, packed: SGPRs are what this kernel runs
+    // short of): hep = the epoch of the last publish; hs = the published region's tile count
+    // (bits 0-7), the index of the tile being scanned (8-15) and the flags below.
+    uint32_t hep = 0, hs = 0;
+    constexpr uint32_t kHsPub = 1u << 16;     // the current region is published (claims are on)
+    constexpr uint32_t kHsNeedPub = 1u << 17; // the region at cur.ct is new to this wave
+    constexpr uint32_t kHsHelped = 1u << 18;  // the last claim saw helpers on the region: no yield
+    hs = kHsNeedPub;
+    auto hK = [&] { return hs & 0xFFu; };
+    auto htile = [&] { return (hs >> 8) & 0xFFu; };
     // Blocking take of the next stream with a region to scan (t: a ticket already held,
     // or ~0u to take one); false when every stream is done.  No LDS-DMA may be in flight.
     // claim: the first take's claim of this workgroup's preassigned tickets (lane 0's CAS
@@ -1552,8 +1704,13 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                 backlog = static_cast<int64_t>(ht >> 32) - static_cast<int64_t>(t) - 1;
             }
             const uint32_t held = t;
-            const int r = presolve(a, lane, held, cur, kDmaWaves);
+            const int r = presolve(a, lane, held, cur, kDmaWaves, me, a.help != nullptr && claim == 0xFFFFFFFFu);
             if (r == 0) return false;
+            if (r == 3) {  // a help task; the ticket stays held (in cap, unused by help tasks)
+                cur.cap = held;
+                uniformize(cur);
+                return true;
+            }
             t = 0xFFFFFFFFu;
             if (claim != 0xFFFFFFFFu) {
                 const bool requeued = bcast(claim) == 2u;
@@ -1563,8 +1720,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             if (r == 2) continue;  // tombstone
             uniformize(cur);
             if (!pcheck(a, lane, cur, held, 1)) return false;
-            budget = (cur.sid & kProbeBit) ? kNoYield : pipe_quantum(backlog);
-            dry = backlog < kProbeBacklog;
+            budget = pipe_quantum(backlog);
             if (pstream_region(a, cur, lane)) return true;
             if (lane == 0) {  // nothing left to scan
                 a.counts[cur.sid] = cur.cnt;
@@ -1586,11 +1742,11 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             __hip_atomic_compare_exchange_strong((gu32*)(a.queue + kQFlags + blockIdx.x), &claim, 1u,
                                                  __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        const uint32_t gw0 = blockIdx.x * kDmaWaves + wave;
+        const uint32_t t0 = first_ticket(blockIdx.x, wave);
         const int64_t nw = static_cast<int64_t>(gridDim.x) * kDmaWaves;
-        take_t = gw0 < a.nstreams ? gw0 : 0xFFFFFFFFu;
+        take_t = t0 < a.nstreams ? t0 : 0xFFFFFFFFu;
         take_backlog = static_cast<int64_t>(a.nstreams) - nw;
-        take_claim = gw0 < a.nstreams ? (claim & 3u) : 0xFFFFFFFFu;
+        take_claim = t0 < a.nstreams ? (claim & 3u) : 0xFFFFFFFFu;
     }
     bool issued = false;  // this tile's warm piece + step 0 are in flight
     for (;;) {
@@ -1599,78 +1755,66 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             if (!take_blocking(take_t, take_backlog, take_claim)) KCDC_PRET;
             need_take = false;
             issued = false;
+            hs |= kHsNeedPub;
         }
         uniformize(cur);
         if (!pcheck(a, lane, cur, 0xFFFFFFFFu, 5)) return;
+        const bool is_help = (cur.sid & kHelpBit) != 0;
+#if KCDC_TRACE
+        const uint64_t tr_t0 = __builtin_amdgcn_s_memrealtime();
+        if (is_help) tr_help++;
+        else tr_own++;
+#endif
         int64_t lo, hi;
         pregion(a, cur, lo, hi);
         const TileGeom g = tile_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n, a.lane_cap);
         const int64_t ct = cur.ct, ct_next = ct + kWave * g.L;
-        const bool last_of_region = ct_next > hi;
-        const bool budget_out = budget - kWave * g.L <= 0;
-        const bool is_probe = (cur.sid & kProbeBit) != 0;
-        bool ends_nocand = false;  // no candidate in this tile => the stream (or probe) is finished
-        if (is_probe) {
-            ends_nocand = last_of_region;
-        } else if (last_of_region) {
+        const bool last_of_region = is_help || ct_next > hi;
+        if (!issued) ptile_issue(cur, hi, wl32, sl32, lane, a.lane_cap);
+        // A region new to this wave: publish it when it is long enough to share.
+        if ((hs & kHsNeedPub) && !is_help) {
+            const int64_t T = kWave * static_cast<int64_t>(a.lane_cap);  // bytes per full tile
+            const uint32_t K = static_cast<uint32_t>((hi - ct + T) / T);
+            hs = 0;
+            if (a.help && K >= kHelpMinTiles && K <= static_cast<uint32_t>(kHelpTiles)) {
+                hep++;
+                hs = kHsPub | K;
+                help_publish(a, lane, me, hep, cur, ct, hi, K, T);
+            }
+        }
+        // The owner's claim on its next tile (atomic add on its slot's bottom), issued in step 0
+        // behind the refill DMA and read in step 2 (or at the tile end for one- and two-step tiles).
+        const bool claim_next_r = (hs & kHsPub) && !is_help && !last_of_region && htile() + 1u < hK();
+        const bool budget_out = !(hs & kHsHelped) && budget - kWave * g.L <= 0;  // (with helpers: no yield)
+        bool ends_nocand = false;  // no candidate in this tile => the stream is finished
+        if (!is_help && last_of_region) {
             const int64_t s2 = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;
             ends_nocand = s2 >= cur.n || s2 + static_cast<int64_t>(a.min_size) - 1 >= cur.n;
         }
-        // The owner's last tile below its probe's start: it hands the region over (or takes
-        // the probe's posted answer) at the tile end.
-        const bool lower_end = KCDC_PROBES && !is_probe && cur.aux > 0 && ct_next >= cur.aux;
         // The visit's last tile (absent a candidate): take the next ticket now, and reserve
         // this stream's entry too when it will be yielded -- one atomic, hidden by the DMAs.
-        const bool switching = budget_out || ends_nocand || lower_end;
-        const bool reserve = budget_out && !ends_nocand && !lower_end;
+        const bool switching = !is_help && (budget_out || ends_nocand);
+        const bool reserve = budget_out && !ends_nocand;
+        const bool claim_next = claim_next_r && !switching;  // a yielding owner claims nothing more
         uint64_t ht_raw = 0;
         if (switching) ht_raw = qht_add(a, lane, 1);  // the next stream's ticket
-        // May this tile spawn a probe (no probe out, the queue dry: waves wait for work, room
-        // for two halves)?  A probe polls its stream's handshake word (cancelled?) every tile.
-        const bool may_split = KCDC_PROBES && dry && !is_probe && cur.aux == 0 && !last_of_region &&
-                               hi - ct_next + 1 >= 2 * kProbeMinHalf;
-        u32x4 pr = {0, 0, 0, 0};
-        if (is_probe) {
-            const uint64_t w = probe_poll(a, lane, cur.sid);
-            pr.x = static_cast<uint32_t>(w);
-            pr.y = static_cast<uint32_t>(w >> 32);
-        }
-        uint64_t qc_raw = 0;
-        if (may_split && lane == 0) qc_raw = ld_agent64(reinterpret_cast<uint64_t*>(a.queue + kQHT));
-        if (!issued) ptile_issue(cur, hi, wl32, sl32, lane, a.lane_cap);
         const int64_t c0 = ct + lane * g.L;
         uint32_t ht_lo = static_cast<uint32_t>(ht_raw), ht_hi = static_cast<uint32_t>(ht_raw >> 32);
-        uint32_t qc_lo = static_cast<uint32_t>(qc_raw), qc_hi = static_cast<uint32_t>(qc_raw >> 32);
         {
             uint32_t w16[16];
             __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt vmcnt(0)"
-                         : "+v"(ht_lo), "+v"(ht_hi), "+v"(qc_lo), "+v"(qc_hi), "+v"(pr.x), "+v"(pr.y), "+v"(pr.z),
-                           "+v"(pr.w)::"memory");
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(ht_lo), "+v"(ht_hi)::"memory");
             read_piece(wl, lane, c0 - 64, cur.off0, w16);
-#if KCDC_REREAD
-            hash.warm(w16);
-#else
             hash.clear();
             hash.template block<kWarm>(w16);
-#endif
         }
-        uint32_t tk = 0, pe = 0;
+        uint32_t tk = 0;
         int64_t nbacklog = 0;
         if (switching) {
             const uint64_t ht = qht_value(ht_lo, ht_hi);
             tk = static_cast<uint32_t>(ht);
             nbacklog = static_cast<int64_t>(ht >> 32) + (reserve ? 1 : 0) - static_cast<int64_t>(tk) - 1;
         }
-        // a probe whose owner moved on (found a cut below it): drop it, skip the tile
-        const bool probe_dead = is_probe && (static_cast<uint32_t>(__builtin_amdgcn_readlane(pr.x, 0)) >> 2) !=
-                                                (cur.epoch & 0x3FFFFFFFu);
-        bool split = false;
-        if (may_split) {
-            const uint64_t qc = qht_value(qc_lo, qc_hi);
-            split = static_cast<uint32_t>(qc) >= static_cast<uint32_t>(qc >> 32);  // head >= tail: waves wait
-        }
-        const uint64_t nres = (reserve ? 1u : 0u) + (split ? 1u : 0u);  // entries this tile will write
         uint64_t pe_raw = 0;
         bool res_issued = false;
         int nstate = 0;  // 0: next stream unresolved, 2: resolved, 3: + its first tile prefetched
@@ -1679,58 +1823,50 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         bool next_issued = false;
         int64_t found = -1;
         const int poll_step = g.nb > 1 ? g.nb / 2 : 0;
-        for (int n = 0; n < (probe_dead ? 0 : g.nb); n++) {
+        // The owner's claim on tile htile + 1: an atomic add on its slot's bottom in step 0 (no
+        // return value: nothing stays live across the hashing), the word read back by an sc1
+        // LDS-DMA into the idle warm slot in step 1 (behind step 1's wait, which the add has
+        // passed) and looked at in the last step, before the next tile's prefetch.  One- and
+        // two-step tiles read it at the tile end (and prefetch nothing).
+        bool claim_ok = false, claim_known = !claim_next;
+        auto claim_decode = [&](uint64_t cw) {  // cw: the claim word after this tile's add
+            const uint32_t top = static_cast<uint32_t>(cw >> 20) & 0xFFFFFu, bot = static_cast<uint32_t>(cw) & 0xFFFFFu;
+            claim_ok = static_cast<uint32_t>(cw >> 40) == hep && bot <= top;
+            if (top < hK()) hs |= kHsHelped;
+            claim_known = true;
+        };
+        for (int n = 0; n < g.nb; n++) {
             const int64_t c = c0 + 128 * n;
-            const typename Hash::State st0 = hash.save();
+            const uint32_t st0 = hash.save();
             uint32_t dw[32];
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#if KCDC_STEP_PRIO
-            __builtin_amdgcn_s_setprio(3);  // win the SIMD for the slot read + refill
-#endif
             read_step128(sl, lane, c, cur.off0, dw);
+            if (claim_next && n >= 2 && n == g.nb - 1) claim_decode(*reinterpret_cast<const uint64_t*>(wl));
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot free: refill it
             __builtin_amdgcn_sched_barrier(0);
-            if (nres && n == g.nb - 1) {  // this stream's entry (and its probe's), reserved late
-                pe_raw = qht_add(a, lane, nres << 32);
+            if (reserve && n == g.nb - 1) {  // this stream's entry, reserved late
+                pe_raw = qht_add(a, lane, 1ull << 32);
                 res_issued = true;
             }
             if (switching && n == poll_step) {
                 pentry_dma(a, lane, tk, wl32);
                 if (n == g.nb - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing to hide it under
             }
+            if (claim_next && n == 1) help_claim_dma(a, lane, me, wl32);
             if (n + 1 < g.nb) {
                 dma_step128(g.ld, g.ld.tb, sl32, ct, g.L, n + 1, lane);
-            } else if (!switching) {  // next tile of this region
-                if (!last_of_region) {
-                    PStream t2 = cur;
-                    t2.ct = ct_next;
-                    ptile_issue(t2, hi, wl32, sl32, lane, a.lane_cap);
-                    next_issued = true;
-                }
+            } else if (!switching && !last_of_region && claim_known && (!claim_next || claim_ok)) {
+                PStream t2 = cur;  // next tile of this region (ours)
+                t2.ct = ct_next;
+                ptile_issue(t2, hi, wl32, sl32, lane, a.lane_cap);
+                next_issued = true;
             }
-#if KCDC_STEP_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
+            if (claim_next && n == 0 && lane == 0)
+                __hip_atomic_fetch_add((gu64*)help_claim(a, me), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __builtin_amdgcn_sched_barrier(0);
-#ifdef KCDC_EXP_MEMONLY
-            uint32_t m = 0;
-#pragma unroll
-            for (int i = 0; i < 32; i++) m |= dw[i];
-            asm volatile("" : "+v"(m));
-#else
             const uint32_t m = hash.template step128<TOP>(dw, 0u);
-#endif
             __builtin_amdgcn_sched_barrier(0);
-#if KCDC_REREAD
-            if (m <= lim && found < 0 && c <= hi) {  // rare: exact re-run from the step's registers
-                const int64_t blo = lo - c, bhi = hi - c;
-                const uint32_t idx = hash.exact(st0, dw, blo < 0 ? 0 : static_cast<int>(blo),
-                                                bhi > 127 ? 127 : static_cast<int>(bhi));
-                if (idx < 128u) found = c + idx;
-            }
-            hash.advance(dw);
-#else
             if (m <= lim && found < 0 && c <= hi) {  // rare: exact re-run from global memory
                 uint32_t prv[16], cur32[32];
                 g.ld.load(c - 64, prv);
@@ -1743,110 +1879,79 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                 // pending around the loop and waits for them in the hash loop (draining DMAs)
                 __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
             }
-#endif
         }
         // ---- end of tile
-        if (probe_dead) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's DMAs, unused
-        if (nres && !res_issued) {
-            pe_raw = qht_add(a, lane, nres << 32);
+        if (!claim_known) {  // a one- or two-step tile: its claim is read here
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (g.nb == 2) {
+                claim_decode(*reinterpret_cast<const uint64_t*>(wl));
+            } else {
+                const uint64_t raw = ld_agent64(help_claim(a, me));
+                claim_decode(qht_value(static_cast<uint32_t>(raw), static_cast<uint32_t>(raw >> 32)));
+            }
+        }
+        if (reserve && !res_issued) {
+            pe_raw = qht_add(a, lane, 1ull << 32);
             res_issued = true;
         }
         const uint64_t hit = __ballot(found >= 0);
+#if KCDC_TRACE
+        if (is_help) tr_help_t += __builtin_amdgcn_s_memrealtime() - tr_t0;
+        else tr_own_end = __builtin_amdgcn_s_memrealtime();
+#endif
+        if (is_help) {  // post the tile's first candidate to its owner's row; back to the held ticket
+            int64_t f = -1;
+            if (hit) f = static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, __builtin_ctzll(hit)))));
+            help_post(a, lane, static_cast<uint32_t>(cur.cb), cur.epoch, static_cast<uint32_t>(cur.cnt), cur.s, f);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            need_take = true;
+            take_t = static_cast<uint32_t>(cur.cap);
+            take_backlog = 0;
+            take_claim = 0xFFFFFFFFu;
+            continue;
+        }
         bool region_changed = true;
-        bool live;
-        int64_t probe_at = 0;  // probe spawned by this tile (start coordinate)
         const int64_t forced = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;  // max-size cut / the end
-        if (is_probe) {  // post the first candidate of [start, aux] to the owner; no cuts
-            region_changed = hit || last_of_region || probe_dead;
-            live = !region_changed;
-            if (!region_changed) {
-                cur.ct = ct_next;
-            } else if (!probe_dead) {
-                int64_t cand = -1;
-                if (hit) {
-                    const int first = __builtin_ctzll(hit);
-                    cand = static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, first))));
-                }
-                const uint32_t rel = cand >= 0 ? static_cast<uint32_t>(cand - cur.s - cur.off0 + 1) : 0u;
-                const uint64_t ex = pword(cur.epoch, 0, 0);
-                const uint64_t old = probe_cas(a, lane, cur.sid, ex, pword(cur.epoch, 1, rel));
-                if (old == pword(cur.epoch, 2, 0)) {  // the owner handed the region over: finish it
-                    const int64_t next = cand >= 0 ? cand - cur.off0 + 1 : forced;
-                    cur.sid &= ~kProbeBit;
-                    cur.aux = 0;
-                    cur.epoch++;
-                    probe_reset(a, lane, cur.sid, cur.epoch);
-                    emit_cut(a, cur, lane, next);
-                    cur.s = next;
-                    cur.ct = -1;
-                    live = pstream_region(a, cur, lane);
-                    if (!live && lane == 0) {
-                        a.counts[cur.sid] = cur.cnt;
-                        add_agent(a.queue + kQDone, 1u);
-                    }
-                }
-            }
-        } else {
-        bool handed = false;  // the probe finishes this region
+        int64_t cut = -1;  // this region's cut, once known
         if (hit) {
             const int first = __builtin_ctzll(hit);
             const int64_t f = static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, first))));
-            const int64_t next = f - cur.off0 + 1;
-            emit_cut(a, cur, lane, next);
-            cur.s = next;
-            cur.ct = -1;
-        } else if (lower_end) {  // nothing below the probe: hand over, unless it has posted
-            const uint64_t ex = pword(cur.epoch, 0, 0);
-            const uint64_t old = probe_cas(a, lane, cur.sid, ex, pword(cur.epoch, 2, 0));
-            if (old == ex) {
-                handed = true;
-            } else {  // {epoch, 1, rel}: the probe's first candidate, or none up to the region end
-                const uint32_t rel = static_cast<uint32_t>(old >> 32);
-                const int64_t next = rel ? cur.s + static_cast<int64_t>(rel) : forced;
-                emit_cut(a, cur, lane, next);
-                cur.s = next;
-                cur.ct = -1;
-            }
+            cut = f - cur.off0 + 1;
         } else if (last_of_region) {  // forced cut at max size (splitter_buzhash32.go:60-64) or the end
-            emit_cut(a, cur, lane, forced);
-            cur.s = forced;
-            cur.ct = -1;
+            cut = forced;
+        } else if (claim_next && !claim_ok) {  // the helpers hold the rest of the region
+            const int64_t T = kWave * static_cast<int64_t>(a.lane_cap);
+            const int64_t ct0 = ct - static_cast<int64_t>(htile()) * T;  // the published tile 0
+            const int64_t r = help_wait(a, lane, me, hep, htile() + 1u, hK(), ct0);
+            if (r >= 0) {
+                cut = r - cur.off0 + 1;
+            } else if (r == -1) {
+                cut = forced;
+            } else {  // a tile still pending: scan on from it, unshared
+                cur.ct = ct0 + (-2 - r) * T;
+                help_close(a, lane, me, hep);
+                hs = 0;
+                region_changed = false;
+            }
         } else {
             cur.ct = ct_next;
+            hs += 1u << 8;  // htile++
             budget -= kWave * g.L;
             region_changed = false;
-            if (split) probe_at = ct_next + (((hi - ct_next + 1) / 2) & ~(kProbeMinHalf - 1));
         }
-        if (handed) {
-            live = false;
-        } else {
-            if (region_changed && cur.aux != 0) {  // the region that spawned a probe is over: cancel it
-                cur.aux = 0;
-                cur.epoch++;
-                probe_reset(a, lane, cur.sid, cur.epoch);
-            }
-            live = pstream_region(a, cur, lane);
-            if (!live && lane == 0) {
-                a.counts[cur.sid] = cur.cnt;
-                add_agent(a.queue + kQDone, 1u);
-            }
+        if (cut >= 0) {
+            emit_cut(a, cur, lane, cut);
+            cur.s = cut;
+            cur.ct = -1;
         }
-        }  // owner
-        if (split) {  // write the probe entry, or a tombstone: the region ended in this tile, or no
-                      // wave was waiting for the entry (the reserve atomic returned head <= e)
-            const uint64_t r_old = qht_value(static_cast<uint32_t>(pe_raw), static_cast<uint32_t>(pe_raw >> 32));
-            const uint32_t e = static_cast<uint32_t>(r_old >> 32) + (reserve ? 1u : 0u);
-            const bool waiter = static_cast<uint32_t>(r_old) > e;
-            PStream pb = cur;
-            pb.sid = cur.sid | kProbeBit;
-            pb.ct = probe_at;
-            pb.aux = hi;
-            const bool spawn = probe_at != 0 && waiter;
-            pwrite(a, lane, e, pb, !spawn);
-            if (spawn) {
-                cur.aux = probe_at;
-                budget = kNoYield;  // not yielded while its probe is out
-            }
+        if (region_changed) {
+            if (hs & kHsPub) help_close(a, lane, me, hep);
+            hs = kHsNeedPub;
+        }
+        const bool live = pstream_region(a, cur, lane);
+        if (!live && lane == 0) {
+            a.counts[cur.sid] = cur.cnt;
+            add_agent(a.queue + kQDone, 1u);
         }
         if (!switching && live) {  // same stream, next tile
             issued = next_issued && !region_changed;
@@ -1855,14 +1960,17 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         }
         // ---- switch streams: requeue this one first (its reserve atomic was issued in the
         // last step, so no prefetch DMA is in flight behind it), then prefetch the next
+        if (hs & kHsPub) help_close(a, lane, me, hep);  // a yielded region is not ours to share any more
+        hs = kHsNeedPub;
         if (reserve) {
-            pe = static_cast<uint32_t>(qht_value(static_cast<uint32_t>(pe_raw), static_cast<uint32_t>(pe_raw >> 32)) >> 32);
+            const uint32_t pe = static_cast<uint32_t>(
+                qht_value(static_cast<uint32_t>(pe_raw), static_cast<uint32_t>(pe_raw >> 32)) >> 32);
             pwrite(a, lane, pe, cur, !live);
         } else if (live) {  // a candidate kept the stream alive past its predicted last tile
             const uint64_t ht = qht_take(a, lane, 1ull << 32);
             pwrite(a, lane, static_cast<uint32_t>(ht >> 32), cur, false);
         }
-        if (switching && !probe_dead) {  // next stream: its entry landed in the warm slot (the last step's wait drained it)
+        if (switching) {  // next stream: its entry landed in the warm slot (the last step's wait drained it)
             const u32x4 ev = *reinterpret_cast<const u32x4*>(wl + 16 * (lane & 7));
             if (pentry_ok(ev, lane, tk) && static_cast<uint32_t>(__builtin_amdgcn_readlane(ev.w, 0)) != kTombstone) {
                 pentry_decode(nx, ev);
@@ -1883,8 +1991,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         if (nstate >= 2) {
             cur = nx;
             issued = nstate == 3;
-            budget = (cur.sid & kProbeBit) ? kNoYield : pipe_quantum(nbacklog);
-            dry = nbacklog < kProbeBacklog;
+            budget = pipe_quantum(nbacklog);
             if (pstream_region(a, cur, lane)) continue;
             if (lane == 0) {  // nothing left to scan in it
                 a.counts[cur.sid] = cur.cnt;
@@ -2317,7 +2424,7 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
                 backlog = static_cast<int64_t>(ht >> 32) - static_cast<int64_t>(t) - 1;
             }
             const uint32_t held = t;
-            const int r = presolve(a, lane, held, cur, kRkWaves);
+            const int r = presolve(a, lane, held, cur, kRkWaves, 0u, false);
             if (r == 0) return false;
             t = 0xFFFFFFFFu;
             if (claim != 0xFFFFFFFFu) {
@@ -2346,11 +2453,11 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             __hip_atomic_compare_exchange_strong((gu32*)(a.queue + kQFlags + blockIdx.x), &claim, 1u,
                                                  __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        const uint32_t gw0 = blockIdx.x * kRkWaves + wave;
+        const uint32_t t0 = first_ticket(blockIdx.x, wave);
         const int64_t nw = static_cast<int64_t>(gridDim.x) * kRkWaves;
-        take_t = gw0 < a.nstreams ? gw0 : 0xFFFFFFFFu;
+        take_t = t0 < a.nstreams ? t0 : 0xFFFFFFFFu;
         take_backlog = static_cast<int64_t>(a.nstreams) - nw;
-        take_claim = gw0 < a.nstreams ? (claim & 3u) : 0xFFFFFFFFu;
+        take_claim = t0 < a.nstreams ? (claim & 3u) : 0xFFFFFFFFu;
     }
     bool issued = false;  // this tile's warm fill is in flight
     for (;;) {
@@ -2530,11 +2637,13 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
 
 // Before each pipelined launch: zero the queue header (tail := n) and write ring entries
 // 0..n-1 = every stream's initial state; later entries get tag 0 (never a valid tag).
-// Head starts at min(n, launch waves): wave w's first ticket is w, taken without an atomic
-// (2048 waves hitting one counter at launch serialised for ~100 us).
+// Head starts at min(n, launch waves): every wave's first ticket is preassigned
+// (first_ticket: w * grid + b), taken without an atomic (2048 waves hitting one counter at
+// launch serialised for ~100 us).  The help slots' claim words start at zero (nothing published).
 __global__ void init_ring_kernel(BatchArgs a, uint32_t nslots, uint32_t nwaves, uint32_t spin_cap,
                                  uint32_t steal_spins) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a.help && i < a.help_waves) *help_claim(a, i) = 0ull;  // help slot i: nothing published
     if (i < kQHeaderBytes / 4)  // (workgroup flags kQFlags.. start at 0: none has started)
         a.queue[i] = i == static_cast<uint32_t>(kQHT) + 1u ? a.nstreams  // tail = n
                    : i == static_cast<uint32_t>(kQHT) ? (nwaves < a.nstreams ? nwaves : a.nstreams)
@@ -2564,10 +2673,6 @@ __global__ void init_ring_kernel(BatchArgs a, uint32_t nslots, uint32_t nwaves, 
         v = pgranule(e + 1u, w, g == 0 ? e : 0u);
     }
     *reinterpret_cast<u32x4*>(reinterpret_cast<uint8_t*>(a.ring) + static_cast<size_t>(e) * kPEntryStride + 16 * g) = v;
-    if (g == 0 && e < a.nstreams) {  // probe result slot of stream e: epoch 0, not done
-        const u32x4 z = {0, 0, 0, 0};
-        *reinterpret_cast<u32x4*>(reinterpret_cast<uint32_t*>(a.states) + 4ull * e) = z;
-    }
 }
 
 // Test hook (KCDC_TEST_FORCE_ERROR): mark a finished launch as failed.
@@ -3576,6 +3681,7 @@ struct TestKnobs {
     uint32_t spin_cap = 0;     // 0: dev::kSpinCap
     bool no_steal = false;     // disable try_steal
     bool force_error = false;  // mark every pipelined launch as failed
+    bool no_help = false;      // buzhash batches without help slots (A/B, tests)
     char* last_ws = nullptr;   // queue header of the last pipelined launch (kcdc_test_queue_stat)
     int last_dev = 0;
 };
@@ -3731,7 +3837,10 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
             return set_error(-22, "Rabin-Karp kernel: the polynomial must have degree 53");
         const unsigned wg_waves = !dma ? dev::kBatchWaves : algo.kind == kRabinKarp ? dev::kRkWaves : dev::kDmaWaves;
         const unsigned need = (s.nstreams + wg_waves - 1) / wg_waves;
-        unsigned grid = need < cus ? need : cus;
+        // The buzhash pipe kernel takes the whole chip even for a few streams: the waves without
+        // a stream help scan the owners' regions (help slots).
+        const bool helpers = dma && algo.kind == kBuzhash && !g_test.no_help;
+        unsigned grid = helpers || need >= cus ? cus : need;
         if (dma && grid > dev::kMaxPipeGrid) grid = dev::kMaxPipeGrid;  // one claim flag per workgroup
         uint64_t ring = 1;
         // every push (yields, probes, tombstones) takes a fresh slot; a launch pushes at most
@@ -3740,7 +3849,9 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         while (ring <= live) ring <<= 1;
         const size_t ring_bytes = dma ? static_cast<size_t>(dev::kPEntryStride) * ring : 0;
         const size_t hdr = dev::kQHeaderBytes;
-        const size_t bytes = hdr + ring_bytes + (dma ? 24ull * s.nstreams : 0);
+        const uint32_t hwaves = helpers ? grid * wg_waves : 0u;
+        const size_t help_bytes = static_cast<size_t>(hwaves) * (128u + 64u + 8u * dev::kHelpTiles);
+        const size_t bytes = hdr + ring_bytes + help_bytes;
         char* ws = nullptr;
         // The slot stays locked from its selection to its event record, so a later user of the
         // same slot always waits for this launch.
@@ -3807,17 +3918,18 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         g_last_ws = ws;
 #endif
         a.ring = reinterpret_cast<uint32_t*>(ws + hdr);
-        a.states = reinterpret_cast<uint64_t*>(ws + hdr + ring_bytes);
+        a.help = helpers ? reinterpret_cast<uint64_t*>(ws + hdr + ring_bytes) : nullptr;
+        a.help_waves = hwaves;
         a.ring_mask = static_cast<uint32_t>(ring - 1);
 
 #if KCDC_TRACE
-        if (trace_reserve(std::max<uint64_t>(s.nstreams, 2ull * grid * wg_waves)) != 0) return set_error(-12, "trace buffer");
+        if (trace_reserve(std::max<uint64_t>(s.nstreams, 3ull * grid * wg_waves)) != 0) return set_error(-12, "trace buffer");
         a.trace = g_trace;
 #endif
         // header + ring zeroed per launch (the ring is also left empty by every finished launch)
         if (dma) {
             const uint32_t slots = static_cast<uint32_t>(ring);
-            const uint64_t threads = std::max<uint64_t>(8ull * slots, dev::kQHeaderBytes / 4);  // >= nstreams
+            const uint64_t threads = std::max<uint64_t>(std::max<uint64_t>(8ull * slots, dev::kQHeaderBytes / 4), hwaves);  // >= nstreams
             hipLaunchKernelGGL(dev::init_ring_kernel, dim3(static_cast<unsigned>((threads + 255) / 256)), dim3(256), 0, st, a,
                                slots, grid * wg_waves, g_test.spin_cap ? g_test.spin_cap : dev::kSpinCap,
                                g_test.no_steal ? 0u : dev::kStealSpins);
@@ -4200,12 +4312,13 @@ extern "C" int kcdc_test_set(int32_t key, int64_t value) {
         case 3: g_test.force_error = value != 0; return 0;                  // KCDC_TEST_FORCE_ERROR
         case 4: test_hash_lanes() = static_cast<int>(value); return 0;     // KCDC_TEST_HASH_LANES
         case 5: set_scan_server_off(value != 0); return 0;                 // KCDC_TEST_NO_SERVER
+        case 6: g_test.no_help = value != 0; return 0;                      // KCDC_TEST_NO_HELP
         default: return set_error(-22, "unknown test knob");
     }
 }
 
 extern "C" int64_t kcdc_test_queue_stat(int32_t key) {
-    const int word = key == 1 ? dev::kQErr : key == 2 ? dev::kQDone : key == 3 ? dev::kQSteal : -1;
+    const int word = key == 1 ? dev::kQErr : key == 2 ? dev::kQDone : key == 3 ? dev::kQSteal : key == 4 ? dev::kQHelp : -1;
     if (word < 0) return set_error(-22, "unknown queue statistic");
     if (!g_test.last_ws) return set_error(-22, "no pipelined batch launch yet");
     int prev = 0;

@@ -126,9 +126,13 @@ int64_t now_ns() {
 
 struct kcdc_bw;
 
-struct kcdc_bw_batcher {
+// One device's batcher: its round thread, streams, pinned blocks and round metadata.  A
+// kcdc_bw_batcher holds one per device of its device set and assigns each writer to one.
+struct BwDev {
     const Algo* algo = nullptr;
     int device = 0;
+    int index = 0;                     // position in the batcher's device list
+    std::atomic<uint64_t> load{0};     // assignment load: max(size hint, bytes written) over open writers
     uint64_t round_bytes = 0;  // ship once this many new bytes are staged across writers
     uint64_t writer_cap = 0;   // a writer blocks in write() while this many of its bytes are unshipped
     uint64_t arena_cap = 0;    // device bytes per writer
@@ -168,7 +172,8 @@ struct kcdc_bw_batcher {
     hipEvent_t ev_ref = nullptr;                   // recorded once: the origin of the intervals below
     std::vector<std::pair<float, float>> busy;     // device intervals (ms after ev_ref) of gathers and splits
 
-    ~kcdc_bw_batcher() {
+    ~BwDev() {
+        if (algo->kind == kFixed) return;
         Guard g(device);
         for (uint8_t* b : pool) (void)hipHostFree(b);
         for (Meta& m : meta) {
@@ -196,8 +201,20 @@ struct kcdc_bw_batcher {
     void loop();
 };
 
+struct kcdc_bw_batcher {
+    const Algo* algo = nullptr;
+    std::vector<BwDev*> devs;
+    std::mutex mu;                   // writer assignment
+    std::atomic<int> inside{0};      // threads inside a writer call (batcher_free waits for them)
+    std::atomic<bool> closing{false};
+};
+
 struct kcdc_bw {
-    kcdc_bw_batcher* b = nullptr;
+    BwDev* b = nullptr;              // the device batcher this writer ships through (null once freed)
+    kcdc_bw_batcher* top = nullptr;
+    int device = 0;                  // HIP device of the arenas
+    uint64_t hint = 0;               // expected object size (0: unknown)
+    uint64_t counted = 0;            // this writer's share of b->load
     std::mutex mu;               // staging (the writer's thread vs the round thread's collection)
     std::condition_variable cv;  // write(): bytes were shipped
     std::vector<Blk> blocks;     // unshipped bytes [shipped, written); only the last may be partial
@@ -240,7 +257,7 @@ struct Round {
 };
 }  // namespace
 
-void kcdc_bw_batcher::loop() {
+void BwDev::loop() {
     Guard g(device);
     Round inflight;
     int next_meta = 0;
@@ -331,7 +348,9 @@ void kcdc_bw_batcher::loop() {
                 if (cv_round.wait_until(lk, due, work)) break;
                 timed_out = std::chrono::steady_clock::now() >= due;
             } else {
-                cv_round.wait(lk, [&] { return work() || staged.load() > 0; });
+                // bounded: writers change `staged`, `capped` and `finish_pending` without this
+                // mutex, so a notify can land between the predicate check and the wait
+                cv_round.wait_for(lk, std::chrono::milliseconds(1), [&] { return work() || staged.load() > 0; });
             }
         }
         if (error) break;
@@ -530,78 +549,187 @@ void kcdc_bw_batcher::loop() {
     cv_done.notify_all();
 }
 
-extern "C" kcdc_bw_batcher* kcdc_bw_batcher_new(const char* name, int device, uint64_t round_bytes,
-                                                uint32_t max_wait_us) {
-    const Algo* a = find_algo(name);
-    if (!a) {
-        set_error(KCDC_ENOENT, std::string("unknown splitter: ") + (name ? name : "(null)"));
-        return nullptr;
+namespace {
+// A writer call in progress on batcher t (batcher_free waits until none is left); false when
+// the batcher is closing (the caller must not touch it).
+struct Inside {
+    kcdc_bw_batcher* t;
+    bool ok;
+    explicit Inside(kcdc_bw_batcher* top) : t(top) {
+        t->inside++;
+        ok = !t->closing.load();
     }
-    int n = 0;
-    if (a->kind != kFixed && (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)) {
-        set_error(KCDC_ENODEV, "no such HIP device");  // FIXED reads no data: host arithmetic only
-        return nullptr;
-    }
-    auto* b = new kcdc_bw_batcher();
+    ~Inside() { t->inside--; }
+};
+
+int dev_error(BwDev* b) { return set_error(b->error, b->errmsg); }  // errmsg is set before error
+
+BwDev* dev_new(const Algo* a, int device, int index, uint64_t round_bytes, uint32_t max_wait_us) {
+    auto* b = new BwDev();
     b->algo = a;
     b->device = device;
+    b->index = index;
     b->round_bytes = round_bytes ? round_bytes : (256ull << 20);
     b->writer_cap = std::max<uint64_t>(b->round_bytes / 8, 4ull * kBlock);
     // two arenas per writer, each: the chunk in progress (+ window) and up to four caps of new
     // bytes between compactions (a compaction needs room for the tail and two rounds' bytes)
     b->arena_cap = (a->max_size() + kHist + 4 * (b->writer_cap + kBlock) + 4095) & ~uint64_t(4095);
     b->wait = std::chrono::microseconds(max_wait_us ? max_wait_us : 2000);
-    if (a->kind != kFixed) {
-        Guard g(device);
-        int err = 0;
-        if (!device_tables(device, &err)) {
-            delete b;
-            return nullptr;
-        }
-        // the splits (short, on the round's critical path) go first when both streams have work
-        int prio_lo = 0, prio_hi = 0;
-        (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-        hipError_t e = hipStreamCreateWithPriority(&b->stream, hipStreamNonBlocking, prio_hi);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->copy, hipStreamNonBlocking);
-        for (auto& m : b->meta)
-            for (hipEvent_t* ev : {&m.gathered, &m.g0, &m.k0, &m.done})
-                if (e == hipSuccess) e = hipEventCreate(ev);
-        if (e == hipSuccess) e = hipEventCreate(&b->ev_ref);
-        if (e == hipSuccess) e = hipEventRecord(b->ev_ref, b->stream);
-        if (e != hipSuccess) {
-            hip_err(e, "writer streams");
-            delete b;
-            return nullptr;
-        }
-        b->th = std::thread([b] { b->loop(); });
+    if (a->kind == kFixed) return b;
+    Guard g(device);
+    int err = 0;
+    if (!device_tables(device, &err)) {
+        delete b;
+        return nullptr;
     }
+    // the splits (short, on the round's critical path) go first when both streams have work
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    hipError_t e = hipStreamCreateWithPriority(&b->stream, hipStreamNonBlocking, prio_hi);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&b->copy, hipStreamNonBlocking);
+    for (auto& m : b->meta)
+        for (hipEvent_t* ev : {&m.gathered, &m.g0, &m.k0, &m.done})
+            if (e == hipSuccess) e = hipEventCreate(ev);
+    if (e == hipSuccess) e = hipEventCreate(&b->ev_ref);
+    if (e == hipSuccess) e = hipEventRecord(b->ev_ref, b->stream);
+    if (e != hipSuccess) {
+        hip_err(e, "writer streams");
+        delete b;
+        return nullptr;
+    }
+    b->th = std::thread([b] { b->loop(); });
     return b;
 }
 
-extern "C" void kcdc_bw_batcher_free(kcdc_bw_batcher* b) {
-    if (!b) return;
+// Stop the device batcher's round thread (every staged byte is shipped first), then fail every
+// later or still-blocked writer call on it.
+void dev_stop(BwDev* b) {
     {
         std::lock_guard<std::mutex> lk(b->mu);
         b->stop = true;
     }
     b->cv_round.notify_all();
     if (b->th.joinable()) b->th.join();
-    for (kcdc_bw* w : b->open) w->b = nullptr;  // writers not freed: unusable from now on
-    if (b->algo->kind != kFixed) {
-        Guard g(b->device);
-        (void)hipStreamSynchronize(b->stream);
-        (void)hipStreamSynchronize(b->copy);
+    std::lock_guard<std::mutex> lk(b->mu);
+    if (!b->error) {
+        b->errmsg = "writer batcher closed";
+        b->error = KCDC_EINVAL;
     }
-    delete b;
+    b->cv_done.notify_all();
+    for (kcdc_bw* w : b->open) {
+        std::lock_guard<std::mutex> wl(w->mu);
+        w->cv.notify_all();
+    }
+}
+}  // namespace
+
+extern "C" kcdc_bw_batcher* kcdc_bw_batcher_new_devices(const char* name, const int* devices, int ndev,
+                                                        uint64_t round_bytes, uint32_t max_wait_us) {
+    const Algo* a = find_algo(name);
+    if (!a) {
+        set_error(KCDC_ENOENT, std::string("unknown splitter: ") + (name ? name : "(null)"));
+        return nullptr;
+    }
+    std::vector<int> list;
+    if (a->kind == kFixed) {  // FIXED reads no data: host arithmetic only, the devices are labels
+        if (!devices || ndev <= 0) list.assign(1, 0);
+        for (int i = 0; devices && i < ndev; i++) {
+            if (devices[i] < 0) {
+                set_error(KCDC_ENODEV, "no such HIP device");
+                return nullptr;
+            }
+            list.push_back(devices[i]);
+        }
+    } else {
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+            set_error(KCDC_ENODEV, "no HIP device");
+            return nullptr;
+        }
+        if (!devices || ndev <= 0) {
+            for (int d = 0; d < count; d++) list.push_back(d);
+        } else {
+            for (int i = 0; i < ndev; i++) {
+                if (devices[i] < 0 || devices[i] >= count) {
+                    set_error(KCDC_ENODEV, "no such HIP device");
+                    return nullptr;
+                }
+                list.push_back(devices[i]);
+            }
+        }
+    }
+    auto* t = new kcdc_bw_batcher();
+    t->algo = a;
+    for (size_t i = 0; i < list.size(); i++) {
+        BwDev* b = dev_new(a, list[i], static_cast<int>(i), round_bytes, max_wait_us);
+        if (!b) {
+            for (BwDev* d : t->devs) {
+                dev_stop(d);
+                delete d;
+            }
+            delete t;
+            return nullptr;
+        }
+        t->devs.push_back(b);
+    }
+    return t;
 }
 
-extern "C" kcdc_bw* kcdc_bw_open(kcdc_bw_batcher* b) {
-    if (!b) {
+extern "C" kcdc_bw_batcher* kcdc_bw_batcher_new(const char* name, int device, uint64_t round_bytes,
+                                                uint32_t max_wait_us) {
+    return kcdc_bw_batcher_new_devices(name, &device, 1, round_bytes, max_wait_us);
+}
+
+extern "C" int kcdc_bw_batcher_devices(const kcdc_bw_batcher* t) {
+    return t ? static_cast<int>(t->devs.size()) : set_error(KCDC_EINVAL, "null batcher");
+}
+
+extern "C" void kcdc_bw_batcher_free(kcdc_bw_batcher* t) {
+    if (!t) return;
+    t->closing = true;
+    for (BwDev* b : t->devs) dev_stop(b);
+    while (t->inside.load() > 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    for (BwDev* b : t->devs) {
+        for (kcdc_bw* w : b->open) {  // writers not freed: unusable from now on (kcdc_bw_free frees their arenas)
+            w->b = nullptr;
+            w->top = nullptr;
+        }
+        if (b->algo->kind != kFixed) {
+            Guard g(b->device);
+            (void)hipStreamSynchronize(b->stream);
+            (void)hipStreamSynchronize(b->copy);
+        }
+        delete b;
+    }
+    delete t;
+}
+
+extern "C" kcdc_bw* kcdc_bw_open_hint(kcdc_bw_batcher* t, uint64_t size_hint) {
+    if (!t) {
         set_error(KCDC_EINVAL, "null batcher");
         return nullptr;
     }
+    Inside in(t);
+    if (!in.ok) {
+        set_error(KCDC_EINVAL, "writer batcher closed");
+        return nullptr;
+    }
+    // Assign the writer to the device with the least load (bytes of its open writers, each
+    // counted as max(size hint, bytes written)): the longest-processing-time rule as bytes
+    // arrive (snapshot/upload/upload.go:769-782 runs NumCPU writers against one repository).
+    BwDev* b = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(t->mu);
+        for (BwDev* d : t->devs)
+            if (!b || d->load.load() < b->load.load()) b = d;
+        b->load += size_hint;
+    }
     auto* w = new kcdc_bw();
     w->b = b;
+    w->top = t;
+    w->device = b->device;
+    w->hint = size_hint;
+    w->counted = size_hint;
     w->fixed_next = b->algo->kind == kFixed ? b->algo->avg : 0;
     if (b->algo->kind != kFixed) {
         Guard g(b->device);
@@ -610,7 +738,9 @@ extern "C" kcdc_bw* kcdc_bw_open(kcdc_bw_batcher* b) {
         if (e == hipSuccess) e = hipMalloc(&q, b->arena_cap);
         if (e != hipSuccess) {
             if (p) (void)hipFree(p);
-            hip_err(e, "writer arena");
+            b->load -= size_hint;
+            set_error(KCDC_ENOMEM, "writer arenas: 2 x " + std::to_string(b->arena_cap >> 20) +
+                                       " MiB of device memory per open writer (" + hipGetErrorString(e) + ")");
             delete w;
             return nullptr;
         }
@@ -622,13 +752,25 @@ extern "C" kcdc_bw* kcdc_bw_open(kcdc_bw_batcher* b) {
     return w;
 }
 
+extern "C" kcdc_bw* kcdc_bw_open(kcdc_bw_batcher* t) { return kcdc_bw_open_hint(t, 0); }
+
+extern "C" int kcdc_bw_device(const kcdc_bw* w) {
+    return w && w->b ? w->b->index : set_error(KCDC_EINVAL, "writer not open");
+}
+
 extern "C" int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len) {
     if (!w || !w->b) return set_error(KCDC_EINVAL, "writer not open");
-    kcdc_bw_batcher* b = w->b;
+    Inside in(w->top);
+    if (!in.ok) return set_error(KCDC_EINVAL, "writer batcher closed");
+    BwDev* b = w->b;
     if (b->algo->kind == kFixed) {  // splitter_fixed.go:15-26: no data is read
         std::lock_guard<std::mutex> lk(b->mu);
         if (w->finishing) return set_error(KCDC_EINVAL, "write after finish");
         w->written += len;
+        if (w->written > w->counted) {
+            b->load += w->written - w->counted;
+            w->counted = w->written;
+        }
         while (w->fixed_next <= w->written) {
             w->ready.push_back(w->fixed_next);
             w->fixed_next += b->algo->avg;
@@ -638,7 +780,7 @@ extern "C" int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len) {
     std::unique_lock<std::mutex> wl(w->mu);
     if (w->finishing) return set_error(KCDC_EINVAL, "write after finish");
     while (len) {
-        if (b->error) return set_error(b->error, b->errmsg);  // errmsg is set before error
+        if (b->error) return dev_error(b);
         // backpressure: at most writer_cap unshipped bytes (a capped writer asks for a round at
         // once: with few writers `staged` may never reach round_bytes)
         if (w->written - w->shipped >= b->writer_cap) {
@@ -668,6 +810,10 @@ extern "C" int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len) {
         std::memcpy(bk.p + bk.end, p, k);
         bk.end += static_cast<uint32_t>(k);
         w->written += k;
+        if (w->written > w->counted) {  // bytes beyond the size hint count toward the device's load
+            b->load += w->written - w->counted;
+            w->counted = w->written;
+        }
         const uint64_t before = b->staged.fetch_add(k);
         if (before == 0) b->since = now_ns();
         if (before == 0 || before + k >= b->round_bytes) b->cv_round.notify_one();
@@ -679,7 +825,10 @@ extern "C" int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len) {
 
 extern "C" int64_t kcdc_bw_cuts(kcdc_bw* w, uint64_t* out, uint64_t cap) {
     if (!w || !w->b) return set_error(KCDC_EINVAL, "writer not open");
-    std::lock_guard<std::mutex> lk(w->b->mu);
+    Inside in(w->top);
+    if (!in.ok) return set_error(KCDC_EINVAL, "writer batcher closed");
+    BwDev* b = w->b;
+    std::lock_guard<std::mutex> lk(b->mu);
     const uint64_t avail = w->ready.size() - w->ready_head;
     const uint64_t k = std::min<uint64_t>(avail, cap);
     if (k) std::memcpy(out, w->ready.data() + w->ready_head, k * 8);
@@ -688,13 +837,15 @@ extern "C" int64_t kcdc_bw_cuts(kcdc_bw* w, uint64_t* out, uint64_t cap) {
         w->ready.clear();
         w->ready_head = 0;
     }
-    if (w->b->error && k == 0) return set_error(w->b->error, w->b->errmsg);
+    if (b->error && k == 0) return dev_error(b);
     return static_cast<int64_t>(k);
 }
 
 extern "C" int kcdc_bw_finish(kcdc_bw* w) {
     if (!w || !w->b) return set_error(KCDC_EINVAL, "writer not open");
-    kcdc_bw_batcher* b = w->b;
+    Inside in(w->top);
+    if (!in.ok) return set_error(KCDC_EINVAL, "writer batcher closed");
+    BwDev* b = w->b;
     if (b->algo->kind == kFixed) {
         std::lock_guard<std::mutex> lk(b->mu);
         if (w->finishing) return KCDC_OK;
@@ -710,19 +861,23 @@ extern "C" int kcdc_bw_finish(kcdc_bw* w) {
             b->finish_pending++;
         }
     }
-    b->cv_round.notify_one();
+    {
+        std::lock_guard<std::mutex> lk(b->mu);  // no lost wakeup: the round thread checks under this mutex
+        b->cv_round.notify_one();
+    }
     std::unique_lock<std::mutex> lk(b->mu);
     b->cv_done.wait(lk, [&] { return w->done || b->error; });
-    return b->error && !w->done ? set_error(b->error, b->errmsg) : KCDC_OK;
+    return b->error && !w->done ? dev_error(b) : KCDC_OK;
 }
 
 extern "C" void kcdc_bw_free(kcdc_bw* w) {
     if (!w) return;
-    kcdc_bw_batcher* b = w->b;
+    BwDev* b = w->b;
     if (b) {
         // an abandoned object: split (and drop) what it staged, so no round still reads its arena
         if (b->algo->kind != kFixed && !b->error) (void)kcdc_bw_finish(w);
         std::lock_guard<std::mutex> lk(b->mu);
+        b->load -= std::min<uint64_t>(b->load.load(), w->counted);
         for (Blk& bk : w->blocks) b->pool.push_back(bk.p);
         b->open.erase(std::find(b->open.begin(), b->open.end(), w));
         if (w->arena) {
@@ -732,41 +887,52 @@ extern "C" void kcdc_bw_free(kcdc_bw* w) {
             (void)hipFree(w->arena);
             (void)hipFree(w->spare);
         }
-    } else if (w->arena) {
+    } else if (w->arena) {  // its batcher was freed first
+        Guard g(w->device);
         (void)hipFree(w->arena);
         (void)hipFree(w->spare);
     }
     delete w;
 }
 
-extern "C" int64_t kcdc_bw_rounds(const kcdc_bw_batcher* b) { return b ? static_cast<int64_t>(b->rounds) : 0; }
+extern "C" int64_t kcdc_bw_rounds(const kcdc_bw_batcher* t) {
+    if (!t) return 0;
+    int64_t r = 0;
+    for (const BwDev* b : t->devs) r += static_cast<int64_t>(b->rounds);
+    return r;
+}
 
-extern "C" int kcdc_bw_stats(kcdc_bw_batcher* b, double* out, int n) {
-    if (!b || !out) return set_error(KCDC_EINVAL, "null argument");
-    std::lock_guard<std::mutex> lk(b->mu);
-    // device span from the first round's start to the last one's end, and the part of it in which
-    // a gather or a split ran (their union: overlapped rounds count once)
-    std::vector<std::pair<float, float>> iv = b->busy;
-    std::sort(iv.begin(), iv.end());
-    double span = 0, busy = 0;
-    if (!iv.empty()) {
-        float s0 = iv[0].first, e0 = iv[0].second, hi = iv[0].second;
-        for (size_t i = 1; i < iv.size(); i++) {
-            if (iv[i].first > e0) {
-                busy += e0 - s0;
-                s0 = iv[i].first;
-                e0 = iv[i].second;
-            } else {
-                e0 = std::max(e0, iv[i].second);
+extern "C" int kcdc_bw_stats(kcdc_bw_batcher* t, double* out, int n) {
+    if (!t || !out) return set_error(KCDC_EINVAL, "null argument");
+    // per device: the device span from its first round's start to its last one's end, and the
+    // part of it in which a gather or a split ran (their union: overlapped rounds count once);
+    // over devices: counts and host seconds add up, spans and busy times are the maximum
+    double v[13] = {0};
+    for (BwDev* b : t->devs) {
+        std::lock_guard<std::mutex> lk(b->mu);
+        std::vector<std::pair<float, float>> iv = b->busy;
+        std::sort(iv.begin(), iv.end());
+        double span = 0, busy = 0;
+        if (!iv.empty()) {
+            float s0 = iv[0].first, e0 = iv[0].second, hi = iv[0].second;
+            for (size_t i = 1; i < iv.size(); i++) {
+                if (iv[i].first > e0) {
+                    busy += e0 - s0;
+                    s0 = iv[i].first;
+                    e0 = iv[i].second;
+                } else {
+                    e0 = std::max(e0, iv[i].second);
+                }
+                hi = std::max(hi, iv[i].second);
             }
-            hi = std::max(hi, iv[i].second);
+            busy += e0 - s0;
+            span = hi - iv[0].first;
         }
-        busy += e0 - s0;
-        span = hi - iv[0].first;
+        const double d[13] = {static_cast<double>(b->rounds), static_cast<double>(b->shipped_bytes), b->t_submit,
+                              b->t_wait, b->t_gather, b->t_kernel, span * 1e-3, busy * 1e-3,
+                              b->t_seg[0], b->t_seg[1], b->t_seg[2], b->t_seg[3], b->t_seg[4]};
+        for (int i = 0; i < 13; i++) v[i] = (i == 6 || i == 7) ? std::max(v[i], d[i]) : v[i] + d[i];
     }
-    const double v[13] = {static_cast<double>(b->rounds), static_cast<double>(b->shipped_bytes), b->t_submit, b->t_wait,
-                          b->t_gather, b->t_kernel, span * 1e-3, busy * 1e-3,
-                          b->t_seg[0], b->t_seg[1], b->t_seg[2], b->t_seg[3], b->t_seg[4]};
     for (int i = 0; i < n && i < 13; i++) out[i] = v[i];
     return 13;
 }

@@ -66,3 +66,25 @@ def test_lpt_plan_balanced_and_deterministic():
 
 def test_max_over_ranks_single_process():
     assert kd.max_over_ranks(3.5) == 3.5
+
+
+def test_library_lpt_assign_matches_lpt_plan():
+    """The library's kcdc_lpt_assign (the device-set host path, kcdc_split_batch_host_devices)
+    makes the same assignment as kd.lpt_plan (bench.py's rank plan)."""
+    from kopia_amd import batch
+    rng = np.random.default_rng(8)
+    for world in (1, 2, 3, 8):
+        sizes = kd.zipf_sizes(64 << 30, seed=world)
+        sizes[::7] = sizes[1]  # ties
+        plan = kd.lpt_plan(sizes, world)
+        got = batch.lpt_assign(sizes, world)
+        want = np.zeros(len(sizes), np.uint32)
+        for r, idx in enumerate(plan):
+            want[idx] = r
+        assert (got == want).all(), world
+        sizes2 = rng.integers(0, 1 << 30, 500)
+        plan2 = kd.lpt_plan(sizes2, world)
+        want2 = np.zeros(500, np.uint32)
+        for r, idx in enumerate(plan2):
+            want2[idx] = r
+        assert (batch.lpt_assign(sizes2, world) == want2).all()

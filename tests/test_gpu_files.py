@@ -137,3 +137,16 @@ def test_files_overflowing_batch_stream_stays_in_its_range():
         assert k[i] == len(want[i])
         assert np.array_equal(c[int(base[i]):int(base[i]) + k[i]], want[i]), i
     assert (c[cap:] == -7).all()
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0], []])
+def test_host_batch_device_set(devices):
+    """kcdc_split_batch_host_devices: host files spread over a device set by bytes (LPT), each
+    device splitting its share from its own thread; every file's cuts equal the oracle's."""
+    rng = np.random.default_rng(31)
+    sizes = [int(x) for x in rng.integers(0, 9 << 20, 40)] + [70 << 20, 0, 1, 63]
+    streams = [coracle.gen_stream(0x6B6F706961, 500 + i, n) for i, n in enumerate(sizes)]
+    for name in ("DYNAMIC-4M-BUZHASH", "DYNAMIC-512K-RABINKARP", "FIXED-1M"):
+        got = batch.split_batch_host_devices(name, streams, devices)
+        for i, d in enumerate(streams):
+            assert got[i].tolist() == coracle.split_stream(name, d).tolist(), (name, i, sizes[i])

@@ -37,15 +37,17 @@ def _feed(w, data, mode, rng):
     return got
 
 
-def _run(name, sizes, modes, round_bytes=0, wait_us=0, sid0=0):
-    b = WriterBatcher(name, round_bytes=round_bytes, max_wait_us=wait_us)
+def _run(name, sizes, modes, round_bytes=0, wait_us=0, sid0=0, devices=None, hints=False):
+    b = WriterBatcher(name, round_bytes=round_bytes, max_wait_us=wait_us, devices=devices)
     datas = [coracle.gen_stream(SEED, sid0 + i, int(n)) for i, n in enumerate(sizes)]
     got = [None] * len(sizes)
+    placed = [None] * len(sizes)
     errs = []
 
     def work(i):
         try:
-            w = b.open()
+            w = b.open(size_hint=int(sizes[i]) if hints else 0)
+            placed[i] = w.device
             got[i] = _feed(w, datas[i], modes[i % len(modes)], np.random.default_rng(i))
             w.close()
         except Exception as e:  # noqa: BLE001
@@ -62,6 +64,8 @@ def _run(name, sizes, modes, round_bytes=0, wait_us=0, sid0=0):
     for i, d in enumerate(datas):
         want = coracle.split_stream(name, d).tolist()
         assert got[i] == want, f"writer {i} ({modes[i % len(modes)]}, {d.size} B): {len(got[i])} vs {len(want)} cuts"
+    if devices is not None:
+        _run.placed = placed
     return rounds
 
 
@@ -79,6 +83,29 @@ def test_sixty_four_writers_64k_slices(gpu):
     rounds = _run("DYNAMIC-4M-BUZHASH", [12 << 20] * 48 + [int(x) for x in range(1 << 20, 17 << 20, 1 << 20)],
                   ["64k", "64k", "64k", "rand"], round_bytes=64 << 20)
     assert rounds >= 4
+
+
+def test_device_set_two_logical_devices(gpu):
+    """kcdc_bw_batcher_new_devices over [0, 0]: two device batchers (own round threads, streams
+    and arenas) on the one GPU, 64 writers with size hints spread over both, every object's cuts
+    exact (snapshot/upload/upload.go:769-782 drives NumCPU writers; the shim binds every GPU)."""
+    rng = np.random.default_rng(21)
+    sizes = [int(x) for x in rng.integers(1 << 20, 24 << 20, 64)]
+    rounds = _run("DYNAMIC-4M-BUZHASH", sizes, ["64k", "64k", "rand"], round_bytes=64 << 20, devices=[0, 0],
+                  hints=True)
+    placed = _run.placed
+    assert sorted(set(placed)) == [0, 1]
+    load = [sum(s for s, p in zip(sizes, placed) if p == d) for d in (0, 1)]
+    assert min(load) > 0.6 * max(load), load
+    assert rounds >= 4
+
+
+def test_device_set_rabinkarp_and_all_devices(gpu):
+    """The device set with a Rabin-Karp name, and devices=[] (every device of the box)."""
+    rng = np.random.default_rng(22)
+    sizes = [int(x) for x in rng.integers(0, 6 << 20, 12)]
+    _run("DYNAMIC-1M-RABINKARP", sizes, ["64k", "rand"], devices=[0, 0, 0])
+    _run("DYNAMIC-1M-BUZHASH", sizes, ["64k"], devices=[])
 
 
 def test_tiny_rounds_carry_the_tail(gpu):

@@ -152,3 +152,54 @@ def test_product_build_has_no_wrong_output_ablations():
     kernels cut or encrypt wrongly; the shipped library must have none compiled in."""
     v = _lib.lib().kcdc_version().decode()
     assert v.endswith("ablations=none"), v
+
+
+def _greedy(hints, writes, ndev):
+    """The batcher's assignment rule: each new writer goes to the device with the least load,
+    load = sum over its open writers of max(size hint, bytes written) (ties: the lowest index)."""
+    load = [0] * ndev
+    got = []
+    for h, wr in zip(hints, writes):
+        d = min(range(ndev), key=lambda i: (load[i], i))
+        got.append(d)
+        load[d] += max(h, wr)
+    return got
+
+
+def test_writer_device_assignment():
+    """kcdc_bw_batcher_new_devices: writers land on the least-loaded device of the set, by size
+    hint and bytes written (host logic; FIXED names read no data, so no GPU is involved)."""
+    from kopia_amd.writer import WriterBatcher
+    rng = np.random.default_rng(3)
+    hints = [int(x) for x in rng.integers(0, 50 << 20, 40)]
+    writes = [int(x) for x in rng.integers(0, 50 << 20, 40)]
+    hints[5] = 0
+    b = WriterBatcher("FIXED-4M", devices=[0, 0, 0])
+    assert b.ndevices == 3
+    ws, devs = [], []
+    for h, wr in zip(hints, writes):
+        w = b.open(size_hint=h)
+        devs.append(w.device)
+        w.write(bytes(wr))  # counts toward the device's load beyond the hint
+        ws.append(w)
+    assert devs == _greedy(hints, writes, 3)
+    # freeing writers returns their load: the next writer goes to the emptied device
+    for i, w in enumerate(ws):
+        if devs[i] == 1:
+            w.close()
+    assert b.open(size_hint=1).device == 1
+    b.close()  # closes the remaining writers first
+    assert all(w._h is None for w in ws)
+
+
+def test_writer_batcher_free_fails_late_calls():
+    """Writers outlive their batcher only for free(): a call after batcher_free fails cleanly."""
+    from kopia_amd.writer import WriterBatcher
+    lib = _lib.lib()
+    b = WriterBatcher("FIXED-1M")
+    h = lib.kcdc_bw_open(b._h)
+    assert lib.kcdc_bw_write(h, bytes(10).__class__(b"x" * 10), 10) == 0
+    lib.kcdc_bw_batcher_free(b._h)
+    b._h = None
+    assert lib.kcdc_bw_write(h, b"y", 1) == _lib.KCDC_EINVAL
+    lib.kcdc_bw_free(h)

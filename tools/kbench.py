@@ -22,6 +22,9 @@ ap.add_argument("--mib", type=int, default=4)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--glob", default="build/variants/libkcdc_*.so")
+ap.add_argument("--knob", action="append", default=[],
+                help="KEY=VALUE: also time the production library with kcdc_test_set(KEY, VALUE) "
+                     "(e.g. 6=1: no intra-region help)")
 args = ap.parse_args()
 
 dev = torch.device("cuda:0")
@@ -42,18 +45,28 @@ for p in sorted(glob.glob(os.path.join(ROOT, args.glob))):
     f.argtypes = _lib._SIGS["kcdc_split_batch_device"][1]
     libs[os.path.basename(p)[8:-3]] = f
 libs["prod"] = _lib.lib().kcdc_split_batch_device
+knobs = {}
+for kv in args.knob:
+    k, v = (int(x) for x in kv.split("="))
+    libs[f"prod_knob{k}={v}"] = _lib.lib().kcdc_split_batch_device
+    knobs[f"prod_knob{k}={v}"] = (k, v)
 
 
-def run(f):
+def run(f, key=None):
+    kv = knobs.get(key)
+    if kv:
+        _lib.lib().kcdc_test_set(kv[0], kv[1])
     rc = f(name.encode(), b.ptrs.data_ptr(), b.lens.data_ptr(), b.n, b.cuts.data_ptr(), b.cap,
            b.cut_base.data_ptr(), b.counts.data_ptr(), C.c_void_p(stream.cuda_stream))
+    if kv:
+        _lib.lib().kcdc_test_set(kv[0], 0)
     assert rc == 0, rc
 
 
 times = {k: [] for k in libs}
 for k, f in libs.items():  # warm + parity
     b.cuts.zero_()
-    run(f)
+    run(f, k)
     torch.cuda.synchronize()
     got = batch.read_cuts(b)
     bad = sum(1 for i in range(ns) if not np.array_equal(got[i], ref[i]))
@@ -63,7 +76,7 @@ for r in range(args.rounds):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(args.reps):
-            run(f)
+            run(f, k)
         e1.record(stream)
         torch.cuda.synchronize()
         times[k].append(e0.elapsed_time(e1) / args.reps)
