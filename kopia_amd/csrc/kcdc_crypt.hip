@@ -36,9 +36,6 @@ constexpr uint32_t kUnit = 4096;                      // bytes per wave step
 constexpr uint32_t kTabT = 0, kTabA = 256, kTabB = 320, kTabC = 384, kTabN = 448;  // r^a, r^256b, r^16384c, r^(2^20)d
 constexpr uint64_t kMaxLen = (1ull << 30) - 64;       // exponents stay below 2^26
 constexpr uint32_t kM26 = 0x3FFFFFFu;
-#ifndef KCDC_CRYPT_ABL
-#define KCDC_CRYPT_ABL 0  // ablations for measurement (bit 0: no ChaCha20, bit 1: no Poly1305); 0 in the product
-#endif
 
 struct Fe {  // element of GF(2^130 - 5), radix 2^26, limbs not fully reduced
     uint32_t v[5];
@@ -480,11 +477,9 @@ constexpr uint32_t kSlotBytes = kUnit + 32;
 // Horner as acc = acc r^253 + m0, then acc r + m1..m3.  The run is folded into the chunk
 // sum (lane l scaled by r^(4(63-l)), reduced across the wave, scaled by r^Q) only when the
 // chunk or the wave's range ends, or at the chunk's partial last unit.
+constexpr int kCryptWaves = 4;  // waves per SIMD: 127 VGPRs, no VGPR spills; seal 3.08-3.12 vs 3.17-3.20 ms at 3
 template <bool kOpen>
-#ifndef KCDC_CRYPT_WAVES
-#define KCDC_CRYPT_WAVES 4  // waves per SIMD: 127 VGPRs, no VGPR spills; seal 3.08-3.12 vs 3.17-3.20 ms at 3
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KCDC_CRYPT_WAVES, KCDC_CRYPT_WAVES))) void crypt_units_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kCryptWaves, kCryptWaves))) void crypt_units_kernel(
     CryptArgs a, const ChunkKey* __restrict__ keys, const uint32_t* __restrict__ units,
     const uint64_t* __restrict__ in_offs, const uint64_t* __restrict__ out_offs, const Fe* __restrict__ tabs,
     uint8_t* __restrict__ out, unsigned long long* __restrict__ acc) {
@@ -602,12 +597,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KCDC_CRYPT_
             for (int j = 0; j < 8; j++) kk[j] = ck.key[j];
 #pragma unroll
             for (int j = 0; j < 3; j++) nc[j] = ck.nonce[j];
-#if KCDC_CRYPT_ABL & 1  // measurement only: keystream replaced by a cheap stand-in
-#pragma unroll
-            for (int j = 0; j < 16; j++) ks[j] = (1u + uu * 64u + lane) * (j + 1u) ^ kk[j & 7];
-#else
             chacha20_block(kk, 1u + uu * 64u + lane, nc, ks);
-#endif
         }
         // 3. wait for this unit's DMA (only the prefetch may stay in flight), read this lane's
         //    bytes [64 lane + mis, +64) from granules 4 lane .. 4 lane + 4
@@ -678,12 +668,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KCDC_CRYPT_
 #pragma unroll
         for (int j = 0; j < 5; j++) r.v[j] = ck.r[j];
         const Fe* tab = tabs + static_cast<uint64_t>(c) * kTabN;
-#if KCDC_CRYPT_ABL & 2  // measurement only: no Poly1305 work on full units
-        if (full) {
-            run.v[0] ^= m[0] ^ m[5] ^ m[10] ^ m[15];
-            run_end = uu;
-        } else
-#endif
         if (full) {
             run = fe_add(fe_mul(run, tab[kTabT + 253u]), fe_block(m[0], m[1], m[2], m[3]));
 #pragma unroll
@@ -855,28 +839,21 @@ __device__ __forceinline__ uint32_t aes_sbox_entry(uint32_t x) {
 // was 60 % bank-conflict cycles), and the byte address (x << 8) | lane offset is ONE v_perm of
 // the state word.  Kernels keep the table first in their LDS so the base folds
 // into the ds_read offset.  Sb[x] = S for the key schedule.
-#ifndef KCDC_GCM_WIDE
-#define KCDC_GCM_WIDE 1  // 1: Te0 + Te1 rows of 256 B (one v_perm address); 0: Te0 only, 128-B rows (32 KiB)
-#endif
+// Te0 + Te1 rows of 256 B, 32 replicas each (one v_perm address; a Te0-only 32 KiB table fits 12
+// waves but spills at 168 VGPRs: 333/306 vs 409 GiB/s, profiles/r02/aes/ab_narrow_table.log).
 struct alignas(256) AesTabs {
-    uint32_t te[256 * (KCDC_GCM_WIDE ? 64 : 32)];
+    uint32_t te[256 * 64];
     uint32_t sb[256];
 };
 __device__ __forceinline__ void aes_tabs_build(AesTabs& t, uint32_t tid, uint32_t nthreads) {
     for (uint32_t x = tid; x < 256u; x += nthreads) {
         const uint32_t sx = aes_sbox_entry(x), s2 = xt8(sx), s3 = s2 ^ sx;
         const uint32_t w = (s2 << 24) | (sx << 16) | (sx << 8) | s3, w1 = ror32(w, 8);
-#if KCDC_GCM_WIDE
 #pragma unroll 8
         for (uint32_t c = 0; c < 64u; c++) {
             const uint32_t cc = (c + x) & 63u;  // lanes start on different banks
             t.te[64u * x + cc] = (cc & 32u) ? w1 : w;
         }
-#else
-        (void)w1;
-#pragma unroll 8
-        for (uint32_t c = 0; c < 32u; c++) t.te[32u * x + ((c + x) & 31u)] = w;
-#endif
         t.sb[x] = sx;
     }
 }
@@ -884,11 +861,7 @@ __device__ __forceinline__ void aes_tabs_build(AesTabs& t, uint32_t tid, uint32_
 // (in byte 0 of `off`: 4 (lane & 31), + 128 for Te1) in byte 0.
 template <int k>
 __device__ __forceinline__ uint32_t te_at(const AesTabs& t, uint32_t s, uint32_t off) {
-#if KCDC_GCM_WIDE
     const uint32_t byte = __builtin_amdgcn_perm(s, off, 0x0C0C0000u | ((4u + k) << 8));
-#else
-    const uint32_t byte = (__builtin_amdgcn_ubfe(s, 8u * k, 8u) << 7) | off;
-#endif
     return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(t.te) + byte);
 }
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
@@ -955,13 +928,8 @@ template <typename RK>
 __device__ __forceinline__ void aes256_block(const AesTabs& t, uint32_t o0, uint32_t o1, const RK& rk, uint32_t (&s)[4]) {
     uint32_t s0 = s[0] ^ rk[0], s1 = s[1] ^ rk[1], s2 = s[2] ^ rk[2], s3 = s[3] ^ rk[3];
     auto col = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
-#if KCDC_GCM_WIDE
         const uint32_t t0 = te_at<3>(t, a, o0), t1 = te_at<2>(t, b, o1);
         const uint32_t t2 = ror32(te_at<1>(t, c, o0), 16), t3 = ror32(te_at<0>(t, d, o1), 16);
-#else
-        const uint32_t t0 = te_at<3>(t, a, o0), t1 = ror32(te_at<2>(t, b, o0), 8);
-        const uint32_t t2 = ror32(te_at<1>(t, c, o0), 16), t3 = ror32(te_at<0>(t, d, o0), 24);
-#endif
         return xor3(xor3(t0, t1, t2), t3, k);
     };
 #pragma unroll
@@ -1206,20 +1174,15 @@ __device__ __forceinline__ void gcm_tab_mul(const GcmWave& g, uint32_t (&x)[4]) 
     x[3] = z3;
 }
 
-#ifndef KCDC_GCM_WAVES
-#define KCDC_GCM_WAVES (KCDC_GCM_WIDE ? 2 : 3)  // waves per SIMD the register budget is sized for
-#endif
-#ifndef KCDC_GCM_RB
-#define KCDC_GCM_RB 2  // AES blocks in flight per lane (rows of a unit per batch)
-#endif
-// waves per workgroup: 64 KiB table + 8 GHASH tables = 146 KiB, or 32 KiB + 12 = 153 KiB
-constexpr uint32_t kGcmWaves = KCDC_GCM_WIDE ? 8 : 12;
+constexpr int kGcmSimdWaves = 2;  // waves per SIMD the register budget is sized for
+constexpr int kGcmRb = 2;         // AES blocks in flight per lane (rows of a unit per batch)
+constexpr uint32_t kGcmWaves = 8;  // waves per workgroup: 64 KiB table + 8 GHASH tables = 146 KiB
 struct GcmLds {
     AesTabs t;  // first: at LDS address 0
     GcmWave gw[kGcmWaves];
 };
 template <bool kOpen>
-__global__ __launch_bounds__(64 * kGcmWaves) __attribute__((amdgpu_waves_per_eu(KCDC_GCM_WAVES, KCDC_GCM_WAVES))) void gcm_units_kernel(
+__global__ __launch_bounds__(64 * kGcmWaves) __attribute__((amdgpu_waves_per_eu(kGcmSimdWaves, kGcmSimdWaves))) void gcm_units_kernel(
     CryptArgs a, const GcmKey* __restrict__ keys, GcmKey* acc_keys, const uint32_t* __restrict__ segp) {
     __shared__ GcmLds L;
     aes_tabs_build(L.t, threadIdx.x, 64u * kGcmWaves);
@@ -1263,11 +1226,11 @@ __global__ __launch_bounds__(64 * kGcmWaves) __attribute__((amdgpu_waves_per_eu(
         uint32_t acc[4] = {0u, 0u, 0u, 0u};
         for (uint32_t u = u0; u < u1; u++)
 #pragma unroll
-        for (int rb = 0; rb < 4; rb += KCDC_GCM_RB) {
-            uint32_t st[KCDC_GCM_RB][4];
-            int64_t jb[KCDC_GCM_RB];
+        for (int rb = 0; rb < 4; rb += kGcmRb) {
+            uint32_t st[kGcmRb][4];
+            int64_t jb[kGcmRb];
 #pragma unroll
-            for (int r = 0; r < KCDC_GCM_RB; r++) {
+            for (int r = 0; r < kGcmRb; r++) {
                 const int64_t j = static_cast<int64_t>(256u * u + 64u * (rb + r) + lane) - pre;
                 jb[r] = j;
                 st[r][0] = k.nonce[0];
@@ -1276,9 +1239,9 @@ __global__ __launch_bounds__(64 * kGcmWaves) __attribute__((amdgpu_waves_per_eu(
                 st[r][3] = static_cast<uint32_t>(j + 2);
             }
 #pragma unroll
-            for (int r = 0; r < KCDC_GCM_RB; r++) aes256_block(L.t, o0, o1, k.rk, st[r]);
+            for (int r = 0; r < kGcmRb; r++) aes256_block(L.t, o0, o1, k.rk, st[r]);
 #pragma unroll
-            for (int r = 0; r < KCDC_GCM_RB; r++) {
+            for (int r = 0; r < kGcmRb; r++) {
                 const int64_t j = jb[r];
                 const int64_t rem = j >= 0 ? static_cast<int64_t>(len) - 16 * j : 0;
                 const uint32_t hiB = rem <= 0 ? 0u : rem >= 16 ? 16u : static_cast<uint32_t>(rem);
@@ -1605,5 +1568,5 @@ extern "C" int kcdc_decrypt_chunks_device(const char* name, const uint8_t* secre
 
 namespace kcdc {
 // Timing ablations of the encryption byte pass (wrong output); none in the product build.
-const char* ablations_crypt() { return KCDC_CRYPT_ABL ? "KCDC_CRYPT_ABL," : ""; }
+const char* ablations_crypt() { return ""; }  // none left in the source (round 4)
 }  // namespace kcdc

@@ -23,8 +23,8 @@
 //       table (lane l hits bank l%32), a T-ring register for the leaving byte, v_alignbit
 //       and v_bitop3, and a running v_min3 candidate test in the rotated frame.  A step
 //       whose min passes is re-run exactly; the earliest lane's candidate is the cut.
-//   split_batch_kernel       the same walk with per-lane buffer loads (Rabin-Karp).
-//   cand_scan_dma_kernel / cand_scan_kernel, seg_prefix, compact, resolve   the long path.
+//   split_batch_rk_kernel    the Rabin-Karp batch walk (two chains per lane).
+//   cand_scan_dma_kernel / cand_scan_rk_kernel, seg_prefix, compact, resolve   the long path.
 //   scan_first_kernel        one region's first candidate (streaming handle).
 //   split_fixed_kernel       FIXED names (reads no data).
 #include <hip/hip_runtime.h>
@@ -46,40 +46,12 @@ namespace dev {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWave = 64;
-#ifndef KCDC_TRING
-#define KCDC_TRING 1
-#endif
-#ifndef KCDC_XOR3_ASM
-#define KCDC_XOR3_ASM 1
-#endif
-#ifndef KCDC_LOOKAHEAD
-#define KCDC_LOOKAHEAD 1
-#endif
-#ifndef KCDC_LA_W
-#define KCDC_LA_W 16  // 128-byte steps: table reads issued this many bytes ahead (VGPR bound)
-#endif
-#ifndef KCDC_BLK
-#define KCDC_BLK 128
-#endif
-constexpr int kBlk = KCDC_BLK;          // bytes per lane per step (a multiple of 64)
+constexpr int kBlk = 128;               // bytes per lane per step (one cache line)
 constexpr int kNdw = kBlk / 4;          // dwords per lane per step
-#ifndef KCDC_LANE_MAX
-#define KCDC_LANE_MAX 2048
-#endif
-constexpr int64_t kLaneMax = KCDC_LANE_MAX;  // max bytes per lane segment (tile = 64 x kLaneMax)
-#ifndef KCDC_TILE_DIV
-#define KCDC_TILE_DIV 256  // batch lane segments <= avg / KCDC_TILE_DIV (tiles ~ 64 avg / DIV), >= 256 B
-#endif
-#ifndef KCDC_BATCH_WAVES
-#define KCDC_BATCH_WAVES 8
-#endif
-constexpr int kBatchWaves = KCDC_BATCH_WAVES;  // waves per workgroup, persistent batch kernel
-constexpr int kScanWaves = 8;                  // waves per workgroup, long-path candidate scan
-#ifndef KCDC_SCHED_WINDOW
-#define KCDC_SCHED_WINDOW 16
-#endif
-constexpr int kSchedWindow = KCDC_SCHED_WINDOW;  // bytes per scheduling window in the hash loop
-
+constexpr int64_t kLaneMax = 2048;      // max bytes per lane segment (tile = 64 x kLaneMax)
+constexpr uint64_t kTileDiv = 256;      // batch lane segments <= avg / kTileDiv (tiles ~ avg / 4), >= 256 B
+constexpr int kSchedWindow = 16;        // bytes per scheduling window in the warm-up / exact loops
+constexpr int kLookahead = 16;          // 128-byte steps: table reads issued this many bytes ahead (VGPR bound)
 
 enum Mode { kWarm = 0, kFast = 1 };
 
@@ -88,13 +60,9 @@ __device__ __forceinline__ uint32_t rotl_n(uint32_t v, uint32_t r) { return r ? 
 
 // h' = rotl(h,1) ^ a ^ b as ONE v_bitop3 (truth table 0x96 = 3-input XOR; gfx950 has no
 // v_xor3).  hipcc otherwise emits xor + bitop3 per byte.  The builtin, not inline asm:
-// the hazard recognizer pads every inline-asm VALU with an s_nop (76 per 128 bytes).
+// the hazard recognizer pads inline-asm VALU with s_nops (76 per 128 bytes).
 __device__ __forceinline__ uint32_t roll3(uint32_t h, uint32_t a, uint32_t b) {
-#if KCDC_XOR3_ASM && defined(__HIP_DEVICE_COMPILE__)
     return __builtin_amdgcn_bitop3_b32(rotl1(h), a, b, 0x96);
-#else
-    return rotl1(h) ^ a ^ b;
-#endif
 }
 
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
@@ -187,79 +155,6 @@ __device__ __forceinline__ void fill_buz_table(BuzShared& sm, const uint32_t* bu
     }
 }
 
-struct Buz {
-    const char* tab;  // LDS byte address of BuzShared::tab
-    uint32_t lane4;
-    uint32_t mask;
-    uint32_t h;
-    uint32_t prev[16];
-    using State = uint32_t;
-    __device__ __forceinline__ State save() const { return h; }
-
-    __device__ __forceinline__ uint32_t look(uint32_t dwv, int k) const {
-        // (byte_k << 8) | lane*4 in one v_perm: byte 0 from lane4, byte 1 = data byte k.
-        const uint32_t a = __builtin_amdgcn_perm(dwv, lane4, 0x0c0c0000u | ((4u + k) << 8));
-        return *reinterpret_cast<const uint32_t*>(tab + a);
-    }
-    __device__ __forceinline__ void clear() {
-        h = 0;
-#pragma unroll
-        for (int i = 0; i < 16; i++) prev[i] = 0;
-    }
-    // kWarm: no test (run on a zero history: the G-recurrence warm-up);
-    // kFast: returns the min over the step of (h & mask) (0 => maybe a candidate).
-    template <int MODE, int N>
-    __device__ __forceinline__ uint32_t block(const uint32_t (&dw)[N]) {
-        uint32_t m = 0xFFFFFFFFu;
-#pragma unroll
-        for (int i = 0; i < 4 * N; i++) {
-            if (kSchedWindow && i % kSchedWindow == 0) __builtin_amdgcn_sched_barrier(0);
-            const uint32_t ti = look(dw[i >> 2], i & 3);
-            if (MODE == kWarm) {
-                h = rotl1(h) ^ ti;
-            } else {
-                const uint32_t to = i < 64 ? look(prev[i >> 2], i & 3) : look(dw[(i - 64) >> 2], i & 3);
-                h = rotl1(h) ^ to ^ ti;
-                m = min(m, h & mask);
-                // Pin the running min every 4 bytes: otherwise the compiler re-associates the
-                // min into a tree at the step end and keeps every hash live (VGPR blow-up).
-                if ((i & 3) == 3) asm volatile("" : "+v"(m));
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 16; i++) prev[i] = dw[N - 16 + i];
-        return m;
-    }
-    // Exact re-run of one step from state st0 with history prv (rare path, compact
-    // rolled loop): index of the first i in [lo, hi] with (h & mask) == 0, else 4N.
-    template <int N>
-    __device__ __forceinline__ uint32_t exact(State st0, const uint32_t (&prv)[16], const uint32_t (&dw)[N], int lo,
-                                              int hi) const {
-        uint32_t e[N], o[N];
-#pragma unroll
-        for (int j = 0; j < N; j++) {
-            e[j] = dw[j];
-            o[j] = j < 16 ? prv[j] : dw[j - 16];
-        }
-        uint32_t hh = st0, first = 4 * N;
-#pragma unroll 1
-        for (int j = 0; j < N; j++) {
-#pragma unroll
-            for (int b = 0; b < 4; b++) {
-                hh = rotl1(hh) ^ look(o[0], b) ^ look(e[0], b);
-                const int i = 4 * j + b;
-                if (first == 4 * N && (hh & mask) == 0 && i >= lo && i <= hi) first = static_cast<uint32_t>(i);
-            }
-#pragma unroll
-            for (int k = 0; k < N - 1; k++) {
-                e[k] = e[k + 1];
-                o[k] = o[k + 1];
-            }
-        }
-        return first;
-    }
-};
-
 // buzhash32 with a register T-ring: ring[j] holds T[b] of the j-th of the 64 bytes
 // before the current step, so each byte costs ONE table read (the entering byte);
 // the leaving byte's value comes from the ring (first half of a 128-byte step) or
@@ -336,7 +231,7 @@ struct BuzRing {
     // Positions 0..62 keep their own running min m0, or-ed with hmask at the end.
     template <bool TOP>
     __device__ __forceinline__ uint32_t step128(const uint32_t (&dw)[32], uint32_t hmask) {
-        constexpr int W = KCDC_LA_W;  // bytes per lookahead window
+        constexpr int W = kLookahead;  // bytes per lookahead window
         uint32_t loc[64];
         uint32_t m = 0xFFFFFFFFu, m0 = 0xFFFFFFFFu;
         uint32_t tw[W], tn[W];
@@ -393,121 +288,6 @@ struct BuzRing {
             }
 #pragma unroll
             for (int k = 0; k < N - 1; k++) {
-                e[k] = e[k + 1];
-                o[k] = o[k + 1];
-            }
-        }
-        return first;
-    }
-};
-
-// buzhash32 without the T-ring: the leaving byte's table value is read from LDS again (a
-// second v_perm + ds_read_b32 per byte), and the raw bytes of the 64 positions before the
-// step (16 VGPRs) stand in for the 64 ring registers.  Those bytes also feed the rare exact
-// re-run, so it needs no global loads.  One more VALU per byte for the registers a third
-// wave per SIMD would need (DESIGN.md §5, round-2 plan).  Off (KCDC_REREAD 0): at 8 waves/CU
-// it is bit-exact but 15 % slower (1.58 vs 1.38 ms).
-#ifndef KCDC_REREAD
-#define KCDC_REREAD 0
-#endif
-#ifndef KCDC_RR_W
-#define KCDC_RR_W 8  // bytes per lookahead window (2 table reads each)
-#endif
-struct BuzRe {
-    const char* tab;
-    uint32_t lane4;
-    uint32_t mask;
-    uint32_t h;
-    uint32_t prev[16];  // raw bytes of the 64 positions before the current step
-    using State = uint32_t;
-    __device__ __forceinline__ State save() const { return h; }
-    __device__ __forceinline__ uint32_t look(uint32_t dwv, int k) const {
-        const uint32_t a = __builtin_amdgcn_perm(dwv, lane4, 0x0c0c0000u | ((4u + k) << 8));
-        return *reinterpret_cast<const uint32_t*>(tab + a);
-    }
-    // hash of the 64 bytes w (the window before the first step), from a zero history
-    __device__ __forceinline__ void warm(const uint32_t (&w)[16]) {
-        h = 0;
-        uint32_t t[16];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int i = 0; i < 16; i++) t[i] = look(w[(16 * q + i) >> 2], i & 3);
-#pragma unroll
-            for (int i = 0; i < 16; i++) h = rotl1(h) ^ t[i];
-        }
-#pragma unroll
-        for (int i = 0; i < 16; i++) prev[i] = w[i];
-    }
-    // One 128-byte step; returns min over positions 63..127 of the (rotated-frame) hash and,
-    // or-ed with hmask, over positions 0..62.  prev is left for the caller (advance()).
-    template <bool TOP>
-    __device__ __forceinline__ uint32_t step128(const uint32_t (&dw)[32], uint32_t hmask) {
-        constexpr int W = KCDC_RR_W;
-        uint32_t m = 0xFFFFFFFFu, m0 = 0xFFFFFFFFu;
-        uint32_t ti[W], to[W], ni[W], no[W];
-        auto leave = [&](int b) -> uint32_t { return b < 64 ? prev[b >> 2] : dw[(b - 64) >> 2]; };
-#pragma unroll
-        for (int i = 0; i < W; i++) {
-            ti[i] = look(dw[i >> 2], i & 3);
-            to[i] = look(leave(i), i & 3);
-        }
-#pragma unroll
-        for (int w = 0; w < 128 / W; w++) {
-            __builtin_amdgcn_sched_barrier(0);
-            if (w < 128 / W - 1) {
-#pragma unroll
-                for (int i = 0; i < W; i++) {
-                    const int b = W * (w + 1) + i;
-                    ni[i] = look(dw[b >> 2], b & 3);
-                    no[i] = look(leave(b), b & 3);
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < W; i++) {
-                const int b = W * w + i;
-                h = roll3(h, to[i], ti[i]);
-                const uint32_t t = TOP ? h : h & mask;
-                if (b < 63) {
-                    m0 = min(m0, t);
-                    if ((b & 3) == 3) asm volatile("" : "+v"(m0));
-                } else {
-                    m = min(m, t);
-                    if ((b & 3) == 3) asm volatile("" : "+v"(m));
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < W; i++) {
-                ti[i] = ni[i];
-                to[i] = no[i];
-            }
-        }
-        return min(m, m0 | hmask);
-    }
-    __device__ __forceinline__ void advance(const uint32_t (&dw)[32]) {
-#pragma unroll
-        for (int i = 0; i < 16; i++) prev[i] = dw[16 + i];
-    }
-    // index of the first i in [lo, hi] of the step with (h & mask) == 0, else 128
-    __device__ __forceinline__ uint32_t exact(State st0, const uint32_t (&dw)[32], int lo, int hi) const {
-        uint32_t e[32], o[32];
-#pragma unroll
-        for (int j = 0; j < 32; j++) {
-            e[j] = dw[j];
-            o[j] = j < 16 ? prev[j] : dw[j - 16];
-        }
-        uint32_t hh = st0, first = 128;
-#pragma unroll 1
-        for (int j = 0; j < 32; j++) {
-#pragma unroll
-            for (int b = 0; b < 4; b++) {
-                hh = rotl1(hh) ^ look(o[0], b) ^ look(e[0], b);
-                const int i = 4 * j + b;
-                if (first == 128 && (hh & mask) == 0 && i >= lo && i <= hi) first = static_cast<uint32_t>(i);
-            }
-#pragma unroll
-            for (int k = 0; k < 31; k++) {
                 e[k] = e[k + 1];
                 o[k] = o[k + 1];
             }
@@ -620,31 +400,14 @@ __device__ int64_t scan_region(H hash, const uint8_t* abase, int64_t off0, int64
                 typename H::State st0 = hash.save();
                 for (; k < nb; k++) {
                     if (c0 + kBlk * k > hi) break;
-#ifndef KCDC_EXP_COMPONLY
                     if (k + 1 < nb) ld.load(c0 + kBlk * (k + 1), nxt);
-#endif
                     st0 = hash.save();
-#ifdef KCDC_EXP_MEMONLY  // ablation: loads only, no hashing (timing experiments)
-                    {
-                        uint32_t x = 1;
-#pragma unroll
-                        for (int i = 0; i < kNdw; i++) x |= cur[i];
-                        asm volatile("" : "+v"(x));
-                        if (x == 0) { hit = true; break; }
-                    }
-#else
                     if (hash.template block<kFast>(cur) == 0) {
                         hit = true;
                         break;
                     }
-#endif
-#ifndef KCDC_EXP_COMPONLY
 #pragma unroll
                     for (int i = 0; i < kNdw; i++) cur[i] = nxt[i];
-#else
-#pragma unroll
-                    for (int i = 0; i < kNdw; i++) cur[i] = cur[i] * 0x9E3779B1u + 1u;  // fresh bytes, no loads
-#endif
                 }
                 if (!hit) break;
                 // rare: re-run step k exactly (the fast pass already left the end state)
@@ -745,11 +508,7 @@ __device__ __forceinline__ void fill_tables(HashSmem<KIND>& sm, const BatchArgs&
 template <int KIND>
 __device__ __forceinline__ auto make_hash(HashSmem<KIND>& sm, const BatchArgs& a, int lane) {
     if constexpr (KIND == kBuzhash) {
-#if KCDC_TRING
         BuzRing h;
-#else
-        Buz h;
-#endif
         h.tab = reinterpret_cast<const char*>(sm.s.tab);
         h.lane4 = static_cast<uint32_t>(lane) * 4u;
         h.mask = a.mask;
@@ -765,93 +524,19 @@ __device__ __forceinline__ auto make_hash(HashSmem<KIND>& sm, const BatchArgs& a
     }
 }
 
-// Split one stream (wave-uniform sid): walk it chunk by chunk.
-template <class H>
-__device__ __forceinline__ void split_one(const BatchArgs& a, const H& hash, uint32_t sid, int lane) {
-    const uint64_t p = uni64(reinterpret_cast<uint64_t>(a.ptrs[sid]));
-    const int64_t n = static_cast<int64_t>(uni64(a.lens[sid]));
-    const uint64_t cb = uni64(a.cut_base[sid]);
-    const uint64_t cend = uni64(cut_end_of(a, sid));
-    const uint64_t cap = cend > cb ? cend - cb : 0;
-    const int64_t off0 = static_cast<int64_t>(p & 15u);
-    const uint8_t* abase = reinterpret_cast<const uint8_t*>(p - static_cast<uint64_t>(off0));
-    const int64_t mn = static_cast<int64_t>(a.min_size), mx = static_cast<int64_t>(a.max_size);
-    int64_t s = 0;
-    uint64_t cnt = 0;
-    while (s < n) {
-        const int64_t pf = s + mn - 1;
-        int64_t next;
-        if (pf >= n) {
-            next = n;  // trailing chunk shorter than min
-        } else {
-            const int64_t pl = s + mx - 1 < n - 1 ? s + mx - 1 : n - 1;
-            const int64_t f = scan_region(hash, abase, off0, off0 + n, pf + off0, pl + off0, lane);
-            if (f >= 0)
-                next = f - off0 + 1;
-            else if (s + mx - 1 <= n - 1)
-                next = s + mx;  // forced cut at max size (splitter_buzhash32.go:60-64)
-            else
-                next = n;       // trailing remainder
-        }
-        if (lane == 0 && cnt < cap) a.cuts[cb + cnt] = static_cast<uint64_t>(next);
-        cnt++;
-        s = next;
-    }
-    if (lane == 0) a.counts[sid] = cnt;
-}
-
-// Persistent waves; each pulls the next stream id from the queue counter.
-template <int KIND>
-__global__ __launch_bounds__(kBatchWaves * kWave, kBatchWaves / 4) void split_batch_kernel(BatchArgs a) {
-    __shared__ HashSmem<KIND> sm;
-    fill_tables<KIND>(sm, a);
-    const int lane = threadIdx.x & (kWave - 1);
-    const auto hash = make_hash<KIND>(sm, a, lane);
-    // Bounded: a wave can never take more than nstreams tickets (exit guaranteed).
-    for (uint32_t iter = 0; iter <= a.nstreams; iter++) {
-        // Lane 0 takes a ticket; broadcast it with an explicit cross-lane read.  (A bare
-        // readfirstlane of the lane-0-only atomic result is folded away by hipcc after
-        // its atomic optimizer rewrites the add, leaving lanes 1..63 with a stale id.)
-        uint32_t got = 0;
-        if (lane == 0) got = atomicAdd(a.queue, 1u);
-        const uint32_t sid = __builtin_amdgcn_readfirstlane(__shfl(got, 0));
-        if (sid >= a.nstreams) break;
-        split_one(a, hash, sid, lane);
-    }
-}
-
 // ------------------------------------------------ LDS-DMA fed batch path
-// The per-lane 16-byte loads of scan_region() touch 64 different cache lines per
-// instruction and are bound by the L1/L2 request rate, not HBM.  Here each
-// 64-byte piece of all 64 lane segments is fetched by 4 LDS-DMA instructions
-// (buffer_load_dwordx4 ... lds): DMA lane d of instruction i fetches chunk
-// (d&3)^((l>>2)&3) of lane l = 16i + d/4, so every 64-byte run is one coalesced
-// request, and lane l later reads chunk j at LDS granule 4l + (j ^ ((l>>2)&3)),
-// which makes every ds_read_b128 lane group hit 16 distinct 16-byte bank slots.
-// Two 4 KiB slots per wave: piece 2n (first half of step n) and 2n+1 (second
-// half); each half's DMA is issued one half-step before it is read.
-#ifndef KCDC_DMA
-#define KCDC_DMA 1
-#endif
-#ifndef KCDC_RK_PIPE
-#define KCDC_RK_PIPE 1  // Rabin-Karp batches through split_batch_rk_kernel (two chains per lane)
-#endif
+// The per-lane 16-byte loads of scan_region() touch 64 different cache lines per instruction
+// and are bound by the L1/L2 request rate, not HBM.  The batch and long-path kernels instead
+// fetch every step by LDS-DMA (buffer_load_dwordx4 ... nt lds): each 128-byte line of a lane
+// segment is one coalesced request (dma_step128), written to the wave's slot with a swizzle
+// that keeps the ds_read_b128 lane groups conflict-free (read_step128).
 #ifndef KCDC_TRACE
-#define KCDC_TRACE 0  // timing-trace builds only (tools/trace_sched.py)
+#define KCDC_TRACE 0  // timing-trace builds only (tools/trace_pipe.py)
 #endif
-#ifndef KCDC_DMA_WAVES
-// 8 waves x 2 slots (64 KiB table + 64 KiB slots; 2 waves/SIMD, no VGPR spills):
-// 4096 x 4 MiB 1.62 ms vs 12 waves 1.68, 7 waves 1.68; deeper pipelines were slower
+// 8 waves x one 8 KiB step slot + 4 KiB warm slot (64 KiB table; 2 waves/SIMD, no VGPR spills):
+// 4096 x 4 MiB 1.62 ms vs 12 waves 1.68, 7 waves 1.68 (round 1); deeper pipelines were slower
 // (8 x 3 slots 1.68, 6 x 4 1.81, 4 x 6 2.00).
-#define KCDC_DMA_WAVES 8
-#endif
-constexpr int kDmaWaves = KCDC_DMA_WAVES;  // waves per workgroup (one workgroup per CU)
-#ifndef KCDC_STEP_PRIO
-#define KCDC_STEP_PRIO 0  // raise the wave priority from the step's slot read to its refill DMA
-#endif
-#ifndef KCDC_DMA_AUX
-#define KCDC_DMA_AUX 2  // nt: once-read stream bytes (membench: 128-B runs 6.65 vs 6.38 TB/s)
-#endif
+constexpr int kDmaWaves = 8;  // waves per workgroup (one workgroup per CU)
 // Each step fetches 128 bytes (one whole cache line) of every lane segment, staged through
 // ONE 8 KiB slot per wave: the step's bytes move to VGPRs at its start, which frees the
 // slot for the next step's DMA while the step is hashed.
@@ -866,10 +551,7 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 struct DmaSlots {
     __attribute__((aligned(16))) uint8_t b[kDmaWaves][1][kSlotBytes];
 };
-#ifndef KCDC_RK_WAVES
-#define KCDC_RK_WAVES KCDC_DMA_WAVES
-#endif
-constexpr int kRkWaves = KCDC_RK_WAVES;  // waves per workgroup of the Rabin-Karp DMA kernels
+constexpr int kRkWaves = kDmaWaves;  // waves per workgroup of the Rabin-Karp DMA kernels
 struct RkSlots {
     __attribute__((aligned(16))) uint8_t b[kRkWaves][1][kSlotBytes];
 };
@@ -879,31 +561,25 @@ struct RkSlots {
 // it ran out of alias-tracking slots and made table reads wait vmcnt for in-flight slot
 // fills.  Every slot read here is preceded by an explicit s_waitcnt; M0 is used by no other
 // code in these kernels.
-#if KCDC_DMA_AUX == 2
-#define KCDC_DMA_POLICY " nt"
-#else
-#define KCDC_DMA_POLICY ""
-#endif
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {  // LDS byte address of a __shared__ pointer
     return __builtin_amdgcn_readfirstlane(
         static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_ptr_t)(const_cast<void*>(p)))));
 }
 __device__ __forceinline__ void dma_lds16(const u32x4& d, uint32_t m0, int32_t voff) {
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen" KCDC_DMA_POLICY " lds"
+    // nt: the stream bytes are read once (membench: 128-B runs 6.65 vs 6.38 TB/s without it)
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds"
                  :: "s"(m0), "v"(voff), "s"(d) : "memory");
 }
 
 __device__ __forceinline__ void dma_piece(const Loader& ld, int64_t tb, uint32_t slot, int64_t ct,
                                           int64_t L, int64_t piece, int lane) {
-#ifdef KCDC_EXP_COMPONLY  // ablation: hashing only (slots keep a fixed random pattern)
-    return;
-#endif
+    // descriptor offsets in 32 bits (ct - tb <= 64, a tile < 2^31 bytes): no per-lane 64-bit values
+    const int32_t base = static_cast<int32_t>(ct - tb) + 64 * static_cast<int32_t>(piece), Li = static_cast<int32_t>(L);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int l = 16 * i + (lane >> 2);
         const int jj = (lane & 3) ^ ((l >> 2) & 3);
-        const int64_t coord = ct + l * L + 64 * piece + 16 * jj;
-        dma_lds16(ld.d, slot + 1024u * i, static_cast<int32_t>(coord - tb));
+        dma_lds16(ld.d, slot + 1024u * i, base + l * Li + 16 * jj);
     }
 }
 
@@ -934,15 +610,12 @@ __device__ __forceinline__ void read_piece(const uint8_t* slot, int lane, int64_
 // sw(l) = (l >> 1) & 7 gives every ds_read_b128 lane group 16 distinct 16-byte bank slots.
 __device__ __forceinline__ void dma_step128(const Loader& ld, int64_t tb, uint32_t slot, int64_t ct,
                                             int64_t L, int64_t n, int lane) {
-#ifdef KCDC_EXP_COMPONLY
-    return;
-#endif
+    const int32_t base = static_cast<int32_t>(ct - tb) + 128 * static_cast<int32_t>(n), Li = static_cast<int32_t>(L);
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         const int l = 8 * i + (lane >> 3);
         const int jj = (lane & 7) ^ ((l >> 1) & 7);
-        const int64_t coord = ct + l * L + 128 * n + 16 * jj;
-        dma_lds16(ld.d, slot + 1024u * i, static_cast<int32_t>(coord - tb));
+        dma_lds16(ld.d, slot + 1024u * i, base + l * Li + 16 * jj);
     }
 }
 
@@ -965,6 +638,12 @@ __device__ __forceinline__ void read_step128(const uint8_t* slot, int lane, int6
             dw[d] &= m;
         }
     }
+}
+
+// The same with the head test precomputed (head: this lane's step starts at coordinate 0).
+__device__ __forceinline__ void read_step128h(const uint8_t* slot, int lane, bool head, int64_t off0,
+                                              uint32_t (&dw)[32]) {
+    read_step128(slot, lane, head ? 0 : 1, off0, dw);
 }
 
 // Geometry of the tile starting at ct (lane segments of L bytes, nb 128-byte steps).
@@ -1326,7 +1005,9 @@ __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
 
 // ------------------------------------------------------------------ help slots
 // Slot g (one per launch wave) in the help area: claim word at 128 * g (own line), the region
-// granules at kHelpParams + 64 * g, the result row at kHelpRows + 8 * kHelpTiles * g.
+// granules at kHelpParams + 64 * g, the result row at kHelpRows + 8 * kHelpTiles * g, and bit g
+// of the published-slots bitmap at kHelpBits (set while the region is open: waiting waves read
+// the bitmap, then the claim words of set slots, instead of probing slots blindly).
 //   claim  {epoch:24 | top:20 | bottom:20}: tiles [0, bottom) are the owner's, [top, K) the
 //          helpers'; epoch 0 = nothing published (init_ring_kernel zeroes every claim word).
 //   params 4 granules {epoch, lo, hi, x}: {ptr, sid}, {n, K}, {ct0, T}, {hi, 0}.
@@ -1339,11 +1020,16 @@ __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
 #ifndef KCDC_HELP_GAP
 #define KCDC_HELP_GAP 2u
 #endif
+constexpr int64_t kHelpSplit = 2;     // sub-tiles per help task (lane segments lane_cap / 2, >= 256 B)
 constexpr int kHelpTiles = 128;          // regions of up to 128 tiles take help (every registered name)
 constexpr uint32_t kHelpMinTiles = 3;    // the owner's tile, its next one, and at least one more
 constexpr uint64_t kHelpWaitTicks = 20000;  // 200 us of s_memrealtime (a tile takes 15-40 us)
 __device__ __forceinline__ size_t help_params_off(uint32_t nw) { return 128ull * nw; }
 __device__ __forceinline__ size_t help_rows_off(uint32_t nw) { return 128ull * nw + 64ull * nw; }
+__device__ __forceinline__ size_t help_bits_off(uint32_t nw) { return help_rows_off(nw) + 8ull * kHelpTiles * nw; }
+__device__ __forceinline__ uint32_t* help_bits(const BatchArgs& a) {
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(a.help) + help_bits_off(a.help_waves));
+}
 __device__ __forceinline__ uint64_t* help_claim(const BatchArgs& a, uint32_t g) {
     return reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(a.help) + 128ull * g);
 }
@@ -1379,11 +1065,22 @@ __device__ void help_publish(const BatchArgs& a, int lane, uint32_t g, uint32_t 
         __builtin_amdgcn_raw_buffer_store_b128(pgranule(ep, static_cast<uint64_t>(hi), 0), r, base + 48, 0, 16);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store((gu64*)help_claim(a, g), hclaim(ep, K, 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) {
+        __hip_atomic_store((gu64*)help_claim(a, g), hclaim(ep, K, 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_or((gu32*)(help_bits(a) + (g >> 5)), 1u << (g & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
-// Owner: no more tiles of this slot's region for helpers (the region or the visit ended).
+// Owner: no more tiles of this slot's region for helpers (the region or the visit ended).  The
+// closed word carries the epoch with bit 23 set: claims of the open epoch fail, and a helper
+// still scanning one of its tiles sees the change (every 4th step) and stops.
+constexpr uint32_t kHelpClosed = 1u << 23;
 __device__ __forceinline__ void help_close(const BatchArgs& a, int lane, uint32_t g, uint32_t ep) {
-    if (lane == 0) __hip_atomic_store((gu64*)help_claim(a, g), hclaim(ep, 0, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) {
+        __hip_atomic_store((gu64*)help_claim(a, g), hclaim(ep | kHelpClosed, 0, 0), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_and((gu32*)(help_bits(a) + (g >> 5)), ~(1u << (g & 31u)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 // Owner: read its claim word back by LDS-DMA (sc1, past L1) into LDS at m0 (16 bytes per lane,
 // every lane the same granule: the word lands at m0).  The waitcnt pass does not see it (as the
@@ -1444,29 +1141,37 @@ __device__ int64_t help_wait(const BatchArgs& a, int lane, uint32_t g, uint32_t 
         __builtin_amdgcn_s_sleep(8);
     }
 }
-// Waiting wave: claim the top tile of the published region with the most unclaimed tiles
-// among 64 slots (a window that moves with every attempt).  On success `task` is a one-tile
-// help task: sid | kHelpBit, the stream's pointer and length, s = the owner's tile 0,
-// ct = the tile, aux = the region end, cb = slot, cnt = tile index, epoch.
+// Waiting wave: claim the top tile of an open region with many unclaimed tiles.  The bitmap
+// names the open slots; each lane takes one set bit of one bitmap word (words and bits start at
+// positions that rotate with the wave and the attempt, so waiting waves spread over the owners),
+// reads that slot's claim word, and the lane with the most unclaimed tiles (ties: rotated) tries
+// the compare-and-swap.  On success `task` is a one-tile help task: sid | kHelpBit, the stream's
+// pointer and length, s = the owner's tile 0, ct = the tile, aux = the tile's end, cb = slot,
+// cnt = tile index, epoch.
 __device__ bool help_find(const BatchArgs& a, int lane, uint32_t me, uint32_t attempt, PStream& task) {
-    const uint32_t nw = a.help_waves;
-    const uint32_t base = (me * 97u + attempt * static_cast<uint32_t>(kWave)) % nw;
-    const uint32_t g = (base + static_cast<uint32_t>(lane)) % nw;
-    const uint64_t c = lane < static_cast<int>(nw) ? ld_agent64(help_claim(a, g)) : 0ull;
+    const uint32_t nw = a.help_waves, nwords = (nw + 31u) >> 5;
+    const uint32_t rot = me * 7u + attempt * 13u;
+    const uint32_t wi = (static_cast<uint32_t>(lane) + rot) % nwords;
+    uint32_t bits = static_cast<uint32_t>(lane) < nwords ? ld_agent(help_bits(a) + wi) : 0u;
+    if (wi == (me >> 5)) bits &= ~(1u << (me & 31u));  // not our own slot
+    uint32_t g = 0xFFFFFFFFu;
+    if (bits) {
+        const uint32_t r = (rot >> 3) & 31u;
+        const uint32_t rb = (bits >> r) | (r ? bits << (32u - r) : 0u);  // rotate right by r
+        g = (wi << 5) + ((static_cast<uint32_t>(__builtin_ctz(rb)) + r) & 31u);
+    }
+    const uint64_t c = g < nw ? ld_agent64(help_claim(a, g)) : 0ull;
     const uint32_t ep = static_cast<uint32_t>(c >> 40), top = static_cast<uint32_t>(c >> 20) & 0xFFFFFu,
                    bot = static_cast<uint32_t>(c) & 0xFFFFFu;
-    // leave the owner its next tile: claim only tiles >= bottom + 1
-    uint32_t avail = ep != 0u && g != me && top >= bot + KCDC_HELP_GAP ? top - bot - (KCDC_HELP_GAP - 1u) : 0u;
-    uint32_t best = avail;
+    // leave the owner its next tile: claim only tiles >= bottom + KCDC_HELP_GAP - 1
+    const bool open = ep != 0u && !(ep & kHelpClosed) && top >= bot + KCDC_HELP_GAP;
+    const uint32_t key = open ? ((top - bot) << 6) | ((static_cast<uint32_t>(lane) + rot) & 63u) : 0u;
+    uint32_t best = key;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) best = max(best, static_cast<uint32_t>(__shfl_xor(static_cast<int>(best), d)));
     best = __builtin_amdgcn_readfirstlane(best);
-#if KCDC_TRACE  // header words kQStat + 0..4: attempts, empty windows, lost races, stale records, tasks
-    if (lane == 0) add_agent(a.queue + kQStat, 1u);
-    if (best == 0u && lane == 0) add_agent(a.queue + kQStat + 1, 1u);
-#endif
     if (best == 0u) return false;
-    const int f = __builtin_ctzll(__ballot(avail == best));
+    const int f = __builtin_ctzll(__ballot(key == best));
     const uint32_t gs = static_cast<uint32_t>(__builtin_amdgcn_readlane(g, f));
     const uint64_t cw = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(c >> 32), f)))
                          << 32) |
@@ -1475,25 +1180,12 @@ __device__ bool help_find(const BatchArgs& a, int lane, uint32_t me, uint32_t at
     if (lane == 0)
         __hip_atomic_compare_exchange_strong((gu64*)help_claim(a, gs), &old, cw - (1ull << 20), __ATOMIC_RELAXED,
                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (qht_value(static_cast<uint32_t>(old), static_cast<uint32_t>(old >> 32)) != cw) {  // lost the race
-#if KCDC_TRACE
-        if (lane == 0) add_agent(a.queue + kQStat + 2, 1u);
-#endif
-        return false;
-    }
+    if (qht_value(static_cast<uint32_t>(old), static_cast<uint32_t>(old >> 32)) != cw) return false;  // lost the race
     const uint32_t eps = static_cast<uint32_t>(cw >> 40);
     const uint32_t k = (static_cast<uint32_t>(cw >> 20) & 0xFFFFFu) - 1u;
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(help_params_rsrc(a), static_cast<int>(64u * gs) + 16 * (lane & 3),
                                                           0, 16 /* sc1 */);
-    if (__ballot(lane < 4 && v.x != eps) != 0) {  // the owner has moved on: nobody waits for this tile
-#if KCDC_TRACE
-        if (lane == 0) add_agent(a.queue + kQStat + 3, 1u);
-#endif
-        return false;
-    }
-#if KCDC_TRACE
-    if (lane == 0) add_agent(a.queue + kQStat + 4, 1u);
-#endif
+    if (__ballot(lane < 4 && v.x != eps) != 0) return false;  // the owner has moved on: nobody waits for this tile
     const uint64_t p = rl64(v, 0);
     task.sid = static_cast<uint32_t>(__builtin_amdgcn_readlane(v.w, 0)) | kHelpBit;
     task.off0 = static_cast<int64_t>(p & 15u);
@@ -1502,7 +1194,8 @@ __device__ bool help_find(const BatchArgs& a, int lane, uint32_t me, uint32_t at
     task.s = static_cast<int64_t>(rl64(v, 2));  // tile 0
     const int64_t T = static_cast<int64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(v.w, 2)));
     task.ct = task.s + static_cast<int64_t>(k) * T;
-    task.aux = static_cast<int64_t>(rl64(v, 3));
+    const int64_t rhi = static_cast<int64_t>(rl64(v, 3));
+    task.aux = task.ct + T - 1 < rhi ? task.ct + T - 1 : rhi;  // the tile's end
     task.cb = gs;
     task.cnt = k;
     task.cap = 0;
@@ -1665,6 +1358,10 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
 #endif
     const uint32_t lim = TOP ? a.buz_lim : 0u;
     const int64_t mx = static_cast<int64_t>(a.max_size);
+    // help sub-tiles halve the lane segments (>= 256 B): shift = sid's help bit & this (integer
+    // arithmetic: a select on a bool here became a VALU-materialised shift next to the DMAs)
+    const uint32_t help_shift = __builtin_amdgcn_readfirstlane(a.lane_cap >= 512u ? 1u : 0u);
+    static_assert(kHelpSplit == 2, "help sub-tiles: one halving");
 
     PStream cur;
     int64_t budget = kNoYield;
@@ -1767,10 +1464,13 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
 #endif
         int64_t lo, hi;
         pregion(a, cur, lo, hi);
-        const TileGeom g = tile_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n, a.lane_cap);
+        // A help task's tile (one owner tile, up to hi) goes in kHelpSplit sub-tiles: it stops at
+        // the first one with a candidate, or when its owner has closed the region meanwhile.
+        const int64_t lcap = static_cast<int64_t>(a.lane_cap >> ((cur.sid >> 31) & help_shift));
+        const TileGeom g = tile_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n, lcap);
         const int64_t ct = cur.ct, ct_next = ct + kWave * g.L;
-        const bool last_of_region = is_help || ct_next > hi;
-        if (!issued) ptile_issue(cur, hi, wl32, sl32, lane, a.lane_cap);
+        const bool last_of_region = ct_next > hi;
+        if (!issued) ptile_issue(cur, hi, wl32, sl32, lane, lcap);
         // A region new to this wave: publish it when it is long enough to share.
         if ((hs & kHsNeedPub) && !is_help) {
             const int64_t T = kWave * static_cast<int64_t>(a.lane_cap);  // bytes per full tile
@@ -1798,13 +1498,16 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         const bool claim_next = claim_next_r && !switching;  // a yielding owner claims nothing more
         uint64_t ht_raw = 0;
         if (switching) ht_raw = qht_add(a, lane, 1);  // the next stream's ticket
-        const int64_t c0 = ct + lane * g.L;
+        // Lane positions as 32-bit offsets from the tile start (a tile < 2^31 bytes): 64-bit
+        // per-lane values live across the hash loop cost VGPRs this kernel does not have.
+        const int32_t cl0 = lane * static_cast<int32_t>(g.L);
+        const int32_t hi_rel = static_cast<int32_t>(hi - ct < 0x7FFFFFFF ? hi - ct : 0x7FFFFFFF);
         uint32_t ht_lo = static_cast<uint32_t>(ht_raw), ht_hi = static_cast<uint32_t>(ht_raw >> 32);
         {
             uint32_t w16[16];
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_waitcnt vmcnt(0)" : "+v"(ht_lo), "+v"(ht_hi)::"memory");
-            read_piece(wl, lane, c0 - 64, cur.off0, w16);
+            read_piece(wl, lane, 1, cur.off0, w16);  // (the piece before coordinate 0 reads as zeros)
             hash.clear();
             hash.template block<kWarm>(w16);
         }
@@ -1821,7 +1524,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         PStream nx;
         nx.ct = -1;
         bool next_issued = false;
-        int64_t found = -1;
+        int32_t found = -1;  // offset from ct of this lane's first candidate
         const int poll_step = g.nb > 1 ? g.nb / 2 : 0;
         // The owner's claim on tile htile + 1: an atomic add on its slot's bottom in step 0 (no
         // return value: nothing stays live across the hashing), the word read back by an sc1
@@ -1836,15 +1539,16 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             claim_known = true;
         };
         for (int n = 0; n < g.nb; n++) {
-            const int64_t c = c0 + 128 * n;
+            const int32_t cl = cl0 + 128 * n;
             const uint32_t st0 = hash.save();
             uint32_t dw[32];
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            read_step128(sl, lane, c, cur.off0, dw);
+            read_step128h(sl, lane, ct == 0 && cl == 0, cur.off0, dw);
             if (claim_next && n >= 2 && n == g.nb - 1) claim_decode(*reinterpret_cast<const uint64_t*>(wl));
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot free: refill it
             __builtin_amdgcn_sched_barrier(0);
+
             if (reserve && n == g.nb - 1) {  // this stream's entry, reserved late
                 pe_raw = qht_add(a, lane, 1ull << 32);
                 res_issued = true;
@@ -1859,7 +1563,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             } else if (!switching && !last_of_region && claim_known && (!claim_next || claim_ok)) {
                 PStream t2 = cur;  // next tile of this region (ours)
                 t2.ct = ct_next;
-                ptile_issue(t2, hi, wl32, sl32, lane, a.lane_cap);
+                ptile_issue(t2, hi, wl32, sl32, lane, lcap);
                 next_issued = true;
             }
             if (claim_next && n == 0 && lane == 0)
@@ -1867,14 +1571,15 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             __builtin_amdgcn_sched_barrier(0);
             const uint32_t m = hash.template step128<TOP>(dw, 0u);
             __builtin_amdgcn_sched_barrier(0);
-            if (m <= lim && found < 0 && c <= hi) {  // rare: exact re-run from global memory
+            if (m <= lim && found < 0 && cl <= hi_rel) {  // rare: exact re-run from global memory
+                const int64_t c = ct + cl;
                 uint32_t prv[16], cur32[32];
                 g.ld.load(c - 64, prv);
                 g.ld.load(c, cur32);
                 const int64_t blo = lo - c, bhi = hi - c;
                 const uint32_t idx = hash.exact(st0, prv, cur32, blo < 0 ? 0 : static_cast<int>(blo),
                                                 bhi > 127 ? 127 : static_cast<int>(bhi));
-                if (idx < 128u) found = c + idx;
+                if (idx < 128u) found = cl + static_cast<int32_t>(idx);
                 // a wait the waitcnt pass sees: its scoreboard otherwise keeps these loads
                 // pending around the loop and waits for them in the hash loop (draining DMAs)
                 __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
@@ -1899,11 +1604,23 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         if (is_help) tr_help_t += __builtin_amdgcn_s_memrealtime() - tr_t0;
         else tr_own_end = __builtin_amdgcn_s_memrealtime();
 #endif
-        if (is_help) {  // post the tile's first candidate to its owner's row; back to the held ticket
-            int64_t f = -1;
-            if (hit) f = static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, __builtin_ctzll(hit)))));
-            help_post(a, lane, static_cast<uint32_t>(cur.cb), cur.epoch, static_cast<uint32_t>(cur.cnt), cur.s, f);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (is_help) {
+            bool done = true;
+            if (hit || last_of_region) {  // post the tile's first candidate to its owner's row
+                int64_t f = -1;
+                if (hit) f = ct + __builtin_amdgcn_readfirstlane(__shfl(found, __builtin_ctzll(hit)));
+                help_post(a, lane, static_cast<uint32_t>(cur.cb), cur.epoch, static_cast<uint32_t>(cur.cnt), cur.s, f);
+            } else {  // the next sub-tile (prefetched), unless the owner has closed the region
+                const uint64_t w = ld_agent64(help_claim(a, static_cast<uint32_t>(cur.cb)));
+                done = static_cast<uint32_t>(qht_value(static_cast<uint32_t>(w), static_cast<uint32_t>(w >> 32)) >> 40) !=
+                       cur.epoch;
+            }
+            if (!done) {
+                cur.ct = ct_next;
+                issued = next_issued;
+                continue;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the post, or a dropped prefetch
             need_take = true;
             take_t = static_cast<uint32_t>(cur.cap);
             take_backlog = 0;
@@ -1914,8 +1631,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         const int64_t forced = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;  // max-size cut / the end
         int64_t cut = -1;  // this region's cut, once known
         if (hit) {
-            const int first = __builtin_ctzll(hit);
-            const int64_t f = static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, first))));
+            const int64_t f = ct + __builtin_amdgcn_readfirstlane(__shfl(found, __builtin_ctzll(hit)));
             cut = f - cur.off0 + 1;
         } else if (last_of_region) {  // forced cut at max size (splitter_buzhash32.go:60-64) or the end
             cut = forced;
@@ -2045,15 +1761,10 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
 // bit-reversed once as they leave the step slot, so byte b of w sits bit-reversed in byte 3 - b),
 // lo' = one v_alignbit.  The reduction index (v's bits 45..52) is lo's bits 11..18, bit-reversed:
 // the tables are stored bit-reversed at bit-reversed rows.  8.9 -> ~7.9 VALU per byte.
-#ifndef KCDC_RK_MODREP
-#define KCDC_RK_MODREP 16  // mod[] replicas: 16 = 2-way conflicts, perm-addressed out[]; 32 = conflict-free mod[]
-                           // but a 2-op out[] address: 3.01 vs 2.80 ms on config 2 (issue-bound)
-#endif
-constexpr int kRkModRep = KCDC_RK_MODREP;
-#ifndef KCDC_RK_OUTREP
-#define KCDC_RK_OUTREP (48 - KCDC_RK_MODREP)  // out[] gets the rest of the 96 KiB
-#endif
-constexpr int kRkOutRep = KCDC_RK_OUTREP;
+// mod[] replicas: 16 = 2-way conflicts and a perm-addressed out[] (32 = conflict-free mod[] but a
+// 2-op out[] address: 3.01 vs 2.80 ms on config 2, issue-bound); out[] gets the rest of 96 KiB.
+constexpr int kRkModRep = 16;
+constexpr int kRkOutRep = 48 - kRkModRep;
 struct RkTables {
     uint64_t mod[256 * kRkModRep];  // row f (replicas at f*R + r): rev64(mod[rev8(f)]); first, so its
                                     // addresses fit the 16-bit ds offset
@@ -2082,17 +1793,14 @@ __device__ __forceinline__ void rk_read_step128(const uint8_t* slot, int lane, i
 __device__ __forceinline__ uint64_t rk_out(const RkCtx& k, uint32_t w, int b) {
     const int bb = 3 - b;
     uint32_t a;
-    if constexpr (kRkOutRep == 32) {  // row << 8 | lane8o: the replica address in one v_perm
-        a = __builtin_amdgcn_perm(w, k.lane8o, 0x0c0c0000u | ((4u + bb) << 8));
-    } else {  // 16 replicas, 128-byte stride: row << 7 | lane8o
-        a = ((bb == 0 ? (w << 7) : (w >> (8 * bb - 7))) & 0x7F80u) | k.lane8o;
-    }
+    static_assert(kRkOutRep == 32, "out[]: 32 replicas, the address in one v_perm");
+    a = __builtin_amdgcn_perm(w, k.lane8o, 0x0c0c0000u | ((4u + bb) << 8));  // row << 8 | lane8o
     return *reinterpret_cast<const uint64_t*>(k.outb + a);
 }
 // v << 8 | c, high word: [hi.b1, hi.b2, hi.b3, the entering byte (byte 3 - b of the reversed dword)]
 constexpr uint32_t rk_in_sel(int b) { return 0x00030201u | (static_cast<uint32_t>(7 - b) << 24); }
 __device__ __forceinline__ uint32_t rk_mod_addr(const RkCtx& k, uint32_t lo) {
-    return (__builtin_amdgcn_ubfe(lo, kRkIdxBit, 8) << (kRkModRep == 32 ? 8 : 7)) | k.lane8m;
+    return (__builtin_amdgcn_ubfe(lo, kRkIdxBit, 8) << 7) | k.lane8m;  // 16 replicas, 128-byte rows
 }
 // One roll with the leaving byte's out[] value already read: updates (hi, lo).
 // Linearity folds the leaving byte's removal into one table read that is off the chain:
@@ -2116,9 +1824,6 @@ __device__ __forceinline__ void rk_roll0(const RkCtx& k, uint32_t& hi, uint32_t&
     lo = tl ^ static_cast<uint32_t>(m);
 }
 
-#ifndef KCDC_RK_W
-#define KCDC_RK_W 2  // bytes per lookahead window: outx[] reads of both chains issued one window ahead (2: 2.58 ms, 4: 2.65)
-#endif
 // 64 bytes of chain A (in a / leaving pa) and of chain B (in b / leaving pb), interleaved
 // byte by byte; ma/mb: running min of hi over the piece's positions (a candidate iff < thr).
 // Software-pipelined across the chains: a chain's next mod[] read issues right after its own
@@ -2126,18 +1831,14 @@ __device__ __forceinline__ void rk_roll0(const RkCtx& k, uint32_t& hi, uint32_t&
 // not one latency + two rolls).  The outx[] reads of byte x + W follow each chain's mod[] read
 // (the in-order LDS return then never queues a chain's read behind a prefetch).
 // ACT_A/ACT_B: whether that chain's bytes are real (an idle chain is not rolled at all).
-#ifndef KCDC_RK_SWP
-#define KCDC_RK_SWP 1  // 0: both chains' mod[] reads issue together at the top of each byte
-#endif
 template <bool ACT_A, bool ACT_B>
 __device__ __forceinline__ void rk_step64(const RkCtx& k, uint32_t& ha, uint32_t& la, const uint32_t (&a)[16],
                                           const uint32_t (&pa)[16], uint32_t& hb, uint32_t& lb,
                                           const uint32_t (&b)[16], const uint32_t (&pb)[16], uint32_t& ma,
                                           uint32_t& mb) {
-    constexpr int W = KCDC_RK_W;
+    constexpr int W = 2;  // outx[] reads of both chains issued this many bytes ahead (2: 2.58 ms, 4: 2.65)
     uint64_t oa[64], ob[64];  // only W live at a time (unrolled: register renaming)
     uint64_t mA = 0, mB = 0;
-#if KCDC_RK_SWP
     if (ACT_A) mA = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, la));
 #pragma unroll
     for (int i = 0; i < W; i++)
@@ -2146,37 +1847,19 @@ __device__ __forceinline__ void rk_step64(const RkCtx& k, uint32_t& ha, uint32_t
 #pragma unroll
     for (int i = 0; i < W; i++)
         if (ACT_B) ob[i] = rk_out(k, pb[i >> 2], i & 3);
-#else
-#pragma unroll
-    for (int i = 0; i < W; i++) {
-        if (ACT_A) oa[i] = rk_out(k, pa[i >> 2], i & 3);
-        if (ACT_B) ob[i] = rk_out(k, pb[i >> 2], i & 3);
-    }
-#endif
     uint32_t pha = 0xFFFFFFFFu, phb = 0xFFFFFFFFu;  // the previous byte's hi (tested in pairs)
 #pragma unroll
     for (int x = 0; x < 64; x++) {
         __builtin_amdgcn_sched_barrier(0);
-#if !KCDC_RK_SWP
-        if (ACT_A) mA = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, la));
-        if (ACT_B) mB = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, lb));
-        if (x + W < 64) {
-            if (ACT_A) oa[x + W] = rk_out(k, pa[(x + W) >> 2], (x + W) & 3);
-            if (ACT_B) ob[x + W] = rk_out(k, pb[(x + W) >> 2], (x + W) & 3);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#endif
         if (ACT_A) {
             const uint32_t th = __builtin_amdgcn_perm(a[x >> 2], ha, rk_in_sel(x & 3));
             const uint32_t tl = __builtin_amdgcn_alignbit(ha, la, 8);
             ha = __builtin_amdgcn_bitop3_b32(th, static_cast<uint32_t>(mA >> 32), static_cast<uint32_t>(oa[x] >> 32), 0x96);
             la = __builtin_amdgcn_bitop3_b32(tl, static_cast<uint32_t>(mA), static_cast<uint32_t>(oa[x]), 0x96);
-#if KCDC_RK_SWP
             __builtin_amdgcn_sched_barrier(0);
             if (x + 1 < 64) mA = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, la));
             if (x + W < 64) oa[x + W] = rk_out(k, pa[(x + W) >> 2], (x + W) & 3);
             __builtin_amdgcn_sched_barrier(0);
-#endif
             if (x & 1) ma = min(ma, min(pha, ha));  // v_min3
             else pha = ha;
         }
@@ -2185,12 +1868,10 @@ __device__ __forceinline__ void rk_step64(const RkCtx& k, uint32_t& ha, uint32_t
             const uint32_t tl = __builtin_amdgcn_alignbit(hb, lb, 8);
             hb = __builtin_amdgcn_bitop3_b32(th, static_cast<uint32_t>(mB >> 32), static_cast<uint32_t>(ob[x] >> 32), 0x96);
             lb = __builtin_amdgcn_bitop3_b32(tl, static_cast<uint32_t>(mB), static_cast<uint32_t>(ob[x]), 0x96);
-#if KCDC_RK_SWP
             __builtin_amdgcn_sched_barrier(0);
             if (x + 1 < 64) mB = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, lb));
             if (x + W < 64) ob[x + W] = rk_out(k, pb[(x + W) >> 2], (x + W) & 3);
             __builtin_amdgcn_sched_barrier(0);
-#endif
             if (x & 1) mb = min(mb, min(phb, hb));
             else phb = hb;
         }
@@ -2292,9 +1973,6 @@ __device__ __forceinline__ RkGeom rk_geom(int64_t ct, int64_t hi, const uint8_t*
 // Warm fill: lane l's slot line = [64 B before c0 | 64 B before c0 + L/2] (16-byte granule j
 // of lane l at j ^ sw(l), as dma_step128).
 __device__ __forceinline__ void rk_dma_warm(const Loader& ld, uint32_t slot, int64_t ct, int64_t L, int lane) {
-#ifdef KCDC_EXP_COMPONLY
-    return;
-#endif
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         const int l = 8 * i + (lane >> 3);
@@ -2398,11 +2076,9 @@ __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int 
     }
 }
 
-#ifndef KCDC_RK_LMUL
-#define KCDC_RK_LMUL 2  // Rabin-Karp lane segments: this many times the buzhash cap (warm-up vs tile overshoot;
-                        // 2 vs 1: 4M 2.542 vs 2.554 ms, 128K 5.536 vs 5.643 ms, profiles/r03/rk/kbench_lmul_*.log)
-#endif
-constexpr int64_t kRkLaneMul = KCDC_RK_LMUL;
+// Rabin-Karp lane segments: twice the buzhash cap (warm-up vs tile overshoot; 2 vs 1: 4M 2.542 vs
+// 2.554 ms, 128K 5.536 vs 5.643 ms, profiles/r03/rk/kbench_lmul_*.log)
+constexpr int64_t kRkLaneMul = 2;
 __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk_kernel(BatchArgs a) {
     __shared__ RkTables smt;
     __shared__ RkSlots smslots;
@@ -2644,6 +2320,7 @@ __global__ void init_ring_kernel(BatchArgs a, uint32_t nslots, uint32_t nwaves, 
                                  uint32_t steal_spins) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (a.help && i < a.help_waves) *help_claim(a, i) = 0ull;  // help slot i: nothing published
+    if (a.help && i < (a.help_waves + 31u) / 32u) help_bits(a)[i] = 0u;
     if (i < kQHeaderBytes / 4)  // (workgroup flags kQFlags.. start at 0: none has started)
         a.queue[i] = i == static_cast<uint32_t>(kQHT) + 1u ? a.nstreams  // tail = n
                    : i == static_cast<uint32_t>(kQHT) ? (nwaves < a.nstreams ? nwaves : a.nstreams)
@@ -2745,9 +2422,6 @@ struct ServerMbox {
 };
 constexpr uint64_t kSrvIdle = 200000;     // 2 ms
 constexpr uint64_t kSrvLife = 20000000;   // 200 ms: every server kernel is bounded
-#ifndef KCDC_SRV_IN
-#define KCDC_SRV_IN 8  // 16-byte PCIe reads in flight per thread while copying a request's slice
-#endif
 constexpr int kSrvWaves = 8;  // 2 per SIMD: scan_region needs up to 219 VGPRs (1,024 threads spilled)
 
 template <int KIND>
@@ -2795,7 +2469,7 @@ __global__ __launch_bounds__(kSrvWaves * kWave) void scan_server_kernel(BatchArg
         // 8 loads in flight per thread (64 KiB per round over PCIe), then their stores: a
         // load-store loop left one 16-byte PCIe read per thread outstanding and cost ~2 us per 8 KiB
         const int64_t n16 = len >> 4;
-        constexpr int kIn = KCDC_SRV_IN;
+        constexpr int kIn = 8;  // 16-byte PCIe reads in flight per thread while copying a request's slice
         constexpr int64_t kT = kSrvWaves * kWave;
         const u32x4* s16 = reinterpret_cast<const u32x4*>(src);
         u32x4* d16 = reinterpret_cast<u32x4*>(scratch);
@@ -2945,9 +2619,6 @@ __global__ void fill_prng_kernel(uint8_t* data, uint64_t stride, uint64_t len, u
 // candidate it needs, it rescans that range with the same scan_region() the
 // batch kernel uses.  The cut set is therefore exactly the sequential one.
 constexpr int64_t kSegBytes = kWave * kLaneMax;  // 128 KiB
-#ifndef KCDC_LONG_DMA
-#define KCDC_LONG_DMA 1  // buzhash candidate scan: cand_scan_dma_kernel (0: cand_scan_kernel)
-#endif
 constexpr int kSegK = 8;
 constexpr uint64_t kTruncBit = 1ull << 63;
 
@@ -2992,79 +2663,10 @@ __device__ __forceinline__ uint32_t long_stream_of(const LongArgs& g, int64_t se
     return lo;
 }
 
-template <int KIND>
-__global__ __launch_bounds__(kScanWaves * kWave, 2) void cand_scan_kernel(BatchArgs a, LongArgs g) {
-    __shared__ HashSmem<KIND> sm;
-    fill_tables<KIND>(sm, a);
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const int64_t seg = static_cast<int64_t>(blockIdx.x) * kScanWaves + wave;
-    if (seg >= g.nseg) return;
-    auto hash = make_hash<KIND>(sm, a, lane);
-    const LongStream& S = g.streams[long_stream_of(g, seg)];
-    const int64_t off0 = static_cast<int64_t>(uni64(static_cast<uint64_t>(S.off0)));
-    const int64_t n = static_cast<int64_t>(uni64(static_cast<uint64_t>(S.n)));
-    const uint8_t* abase = reinterpret_cast<const uint8_t*>(uni64(reinterpret_cast<uint64_t>(S.abase)));
-    const int64_t seg0 = static_cast<int64_t>(uni64(static_cast<uint64_t>(S.seg0)));
-    // Segments tile COORDINATES (position + off0) so every lane sub-range is 16-byte aligned.
-    const int64_t cs = (seg - seg0) * kSegBytes;
-    const int64_t lo = cs > off0 ? cs : off0;                                           // first tested
-    const int64_t hi = (cs + kSegBytes < off0 + n ? cs + kSegBytes : off0 + n) - 1;  // inclusive
-    const int64_t tb = cs >= 64 ? cs - 64 : 0;
-    const Loader ld = make_loader(abase, off0, off0 + n, tb);
-    const int64_t c0 = cs + lane * kLaneMax;
-    uint32_t found[kSegK];
-    int nf = 0;  // candidates found by this lane (kSegK + 1 means "more than kSegK")
-    if (c0 <= hi) {
-        uint32_t cur[kNdw], nxt[kNdw];
-        {
-            uint32_t w[16];
-            hash.clear();
-            ld.load(c0 - 64, w);
-            hash.template block<kWarm>(w);
-        }
-        ld.load(c0, cur);
-        for (int k = 0; k < static_cast<int>(kLaneMax / kBlk) && nf <= kSegK; k++) {
-            const int64_t c = c0 + kBlk * k;
-            if (c > hi) break;
-            if (k + 1 < static_cast<int>(kLaneMax / kBlk)) ld.load(c + kBlk, nxt);
-            const typename decltype(hash)::State st0 = hash.save();
-            if (hash.template block<kFast>(cur) == 0) {
-                uint32_t prv[16];
-                ld.load(c - 64, prv);
-                const int bhi = hi - c > kBlk - 1 ? kBlk - 1 : static_cast<int>(hi - c);
-                int from = lo > c ? static_cast<int>(lo - c) : 0;
-                while (from <= bhi && nf <= kSegK) {
-                    const uint32_t idx = hash.exact(st0, prv, cur, from, bhi);
-                    if (idx >= static_cast<uint32_t>(kBlk)) break;
-                    if (nf < kSegK) found[nf] = static_cast<uint32_t>(c - cs) + idx;
-                    nf++;
-                    from = static_cast<int>(idx) + 1;
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < kNdw; i++) cur[i] = nxt[i];
-        }
-    }
-    // exclusive prefix of per-lane counts (segments are in lane order)
-    int incl = nf;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const int v = __shfl_up(incl, d);
-        if (lane >= d) incl += v;
-    }
-    const int tot = __shfl(incl, kWave - 1);
-    const int pre = incl - nf;
-    for (int j = 0; j < nf && j < kSegK; j++)
-        if (pre + j < kSegK) g.seg_cand[seg * kSegK + pre + j] = static_cast<uint64_t>(cs - off0) + found[j];
-    if (lane == 0)
-        g.seg_cnt[seg] = (tot > kSegK ? 0x80000000u : 0u) | static_cast<uint32_t>(tot < kSegK ? tot : kSegK);
-}
-
 // Rabin-Karp candidate scan of the long path on split_batch_rk_kernel's tile walk (two
 // chains per lane, alternating 128-byte line fills, outx[] folding): one 128 KiB segment per
 // tile, persistent grid-stride over the segments of every stream of the launch, the next
-// segment's warm fill issued during the drain step.  Records what cand_scan_kernel records.
+// segment's warm fill issued during the drain step.  Records what cand_scan_dma_kernel records.
 __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void cand_scan_rk_kernel(BatchArgs a, LongArgs g) {
     __shared__ RkTables smt;
     __shared__ RkSlots smslots;
@@ -3187,7 +2789,8 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void cand_scan_rk_k
 // (128 KiB of coordinates) is exactly one tile of 64 lane segments, streamed by LDS-DMA in
 // 128-byte steps with the next segment's warm piece and first step prefetched during the
 // last step; persistent grid (one workgroup of kDmaWaves waves per CU), grid-stride over
-// the segments of every stream of the launch.  Records what cand_scan_kernel records.
+// the segments of every stream of the launch.  Per segment it records the first kSegK
+// candidates (positions from the stream start) and a truncation flag.
 template <bool TOP>
 __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void cand_scan_dma_kernel(BatchArgs a, LongArgs g) {
     __shared__ BuzShared smtab;
@@ -3724,7 +3327,7 @@ dev::BatchArgs base_args(const Algo& algo, const DeviceTables& t) {
     // largest power of two <= avg / 256, within [256, kLaneMax]: tiles of ~avg/4 (1 MiB and
     // larger averages keep the full 2 KiB lane segments)
     uint64_t cap = dev::kLaneMax;
-    while (cap > 256 && cap * KCDC_TILE_DIV > algo.avg) cap >>= 1;
+    while (cap > 256 && cap * dev::kTileDiv > algo.avg) cap >>= 1;
     a.lane_cap = static_cast<uint32_t>(cap);
     return a;
 }
@@ -3760,18 +3363,9 @@ extern "C" int kcdc_debug_trace_copy(uint64_t* host, uint64_t nstreams) {
 }
 #endif
 
-// Experiment switches that make the batch kernels cut WRONG (timing ablations only); the
-// product build has none of them (kcdc_version, tests/test_lib_host.py).
-const char* ablations_kernels() {
-    return ""
-#ifdef KCDC_EXP_COMPONLY
-           "KCDC_EXP_COMPONLY,"
-#endif
-#ifdef KCDC_EXP_MEMONLY
-           "KCDC_EXP_MEMONLY,"
-#endif
-        ;
-}
+// Experiment switches that make the batch kernels cut WRONG: none are left in the source (round 4
+// moved the timing ablations out; kcdc_version, tests/test_lib_host.py).
+const char* ablations_kernels() { return ""; }
 
 const DeviceTables* device_tables(int device, int* err) {
     *err = 0;
@@ -3826,31 +3420,29 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
     a.resume = s.starts ? s.resume : nullptr;
     a.counts = s.counts;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (s.starts && (algo.kind == kFixed || !KCDC_DMA || (algo.kind == kRabinKarp && !KCDC_RK_PIPE)))
-        return set_error(-22, "per-stream starts need the pipelined batch kernels");
+    if (s.starts && algo.kind == kFixed) return set_error(-22, "per-stream starts need the pipelined batch kernels");
     if (algo.kind == kFixed) {
         hipLaunchKernelGGL(dev::split_fixed_kernel, dim3(s.nstreams), dim3(256), 0, st, a);
     } else {
         const unsigned cus = static_cast<unsigned>(t->cus);
-        const bool dma = (algo.kind == kBuzhash || (algo.kind == kRabinKarp && KCDC_RK_PIPE)) && KCDC_DMA;
-        if (algo.kind == kRabinKarp && dma && tables().rk_shift != 45)
+        if (algo.kind == kRabinKarp && tables().rk_shift != 45)
             return set_error(-22, "Rabin-Karp kernel: the polynomial must have degree 53");
-        const unsigned wg_waves = !dma ? dev::kBatchWaves : algo.kind == kRabinKarp ? dev::kRkWaves : dev::kDmaWaves;
+        const unsigned wg_waves = algo.kind == kRabinKarp ? dev::kRkWaves : dev::kDmaWaves;
         const unsigned need = (s.nstreams + wg_waves - 1) / wg_waves;
         // The buzhash pipe kernel takes the whole chip even for a few streams: the waves without
         // a stream help scan the owners' regions (help slots).
-        const bool helpers = dma && algo.kind == kBuzhash && !g_test.no_help;
+        const bool helpers = algo.kind == kBuzhash && !g_test.no_help;
         unsigned grid = helpers || need >= cus ? cus : need;
-        if (dma && grid > dev::kMaxPipeGrid) grid = dev::kMaxPipeGrid;  // one claim flag per workgroup
+        if (grid > dev::kMaxPipeGrid) grid = dev::kMaxPipeGrid;  // one claim flag per workgroup
         uint64_t ring = 1;
-        // every push (yields, probes, tombstones) takes a fresh slot; a launch pushes at most
+        // every push (yields, tombstones) takes a fresh slot; a launch pushes at most
         // a few entries per wave beyond the initial n: size the ring with ample margin
         const uint64_t live = static_cast<uint64_t>(s.nstreams) + 8ull * grid * wg_waves;
         while (ring <= live) ring <<= 1;
-        const size_t ring_bytes = dma ? static_cast<size_t>(dev::kPEntryStride) * ring : 0;
+        const size_t ring_bytes = static_cast<size_t>(dev::kPEntryStride) * ring;
         const size_t hdr = dev::kQHeaderBytes;
         const uint32_t hwaves = helpers ? grid * wg_waves : 0u;
-        const size_t help_bytes = static_cast<size_t>(hwaves) * (128u + 64u + 8u * dev::kHelpTiles);
+        const size_t help_bytes = static_cast<size_t>(hwaves) * (128u + 64u + 8u * dev::kHelpTiles) + 4u * ((hwaves + 31u) / 32u);
         const size_t bytes = hdr + ring_bytes + help_bytes;
         char* ws = nullptr;
         // The slot stays locked from its selection to its event record, so a later user of the
@@ -3927,23 +3519,20 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         a.trace = g_trace;
 #endif
         // header + ring zeroed per launch (the ring is also left empty by every finished launch)
-        if (dma) {
+        {
             const uint32_t slots = static_cast<uint32_t>(ring);
             const uint64_t threads = std::max<uint64_t>(std::max<uint64_t>(8ull * slots, dev::kQHeaderBytes / 4), hwaves);  // >= nstreams
             hipLaunchKernelGGL(dev::init_ring_kernel, dim3(static_cast<unsigned>((threads + 255) / 256)), dim3(256), 0, st, a,
                                slots, grid * wg_waves, g_test.spin_cap ? g_test.spin_cap : dev::kSpinCap,
                                g_test.no_steal ? 0u : dev::kStealSpins);
-        } else {
-            hipError_t e = hipMemsetAsync(ws, 0, hdr + ring_bytes, st);
-            if (e != hipSuccess) return hip_fail(e, "queue reset");
         }
         // persistent grid: one workgroup per CU, never more workgroups than the streams need
-        if (dma && algo.kind == kRabinKarp) {
+        if (algo.kind == kRabinKarp) {
             hipLaunchKernelGGL(dev::split_batch_rk_kernel, dim3(grid), dim3(dev::kRkWaves * dev::kWave), 0, st, a);
             if (g_test.force_error)
                 hipLaunchKernelGGL(dev::poison_counts_kernel, dim3(std::min<unsigned>((s.nstreams + 255) / 256, 256u)),
                                    dim3(256), 0, st, a);
-        } else if (dma) {
+        } else {
             const bool top = buz_frame(static_cast<uint32_t>(algo.mask())).top;
             if (top)
                 hipLaunchKernelGGL(dev::split_batch_pipe_kernel<true>, dim3(grid), dim3(dev::kDmaWaves * dev::kWave), 0,
@@ -3954,12 +3543,6 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
             if (g_test.force_error)  // test hook: report a failed launch (kcdc_test_set)
                 hipLaunchKernelGGL(dev::poison_counts_kernel, dim3(std::min<unsigned>((s.nstreams + 255) / 256, 256u)),
                                    dim3(256), 0, st, a);
-        } else {
-            const dim3 block(dev::kBatchWaves * dev::kWave);
-            if (algo.kind == kBuzhash)
-                hipLaunchKernelGGL(dev::split_batch_kernel<kBuzhash>, dim3(grid), block, 0, st, a);
-            else
-                hipLaunchKernelGGL(dev::split_batch_kernel<kRabinKarp>, dim3(grid), block, 0, st, a);
         }
         const hipError_t er = hipEventRecord(q.done, st);
         if (er != hipSuccess) return hip_fail(er, "queue workspace record");
@@ -4144,9 +3727,6 @@ int launch_fill_prng(uint8_t* d_data, uint64_t stride, uint64_t stream_len, uint
 }
 
 namespace {
-#ifndef KCDC_PAR_RESOLVE
-#define KCDC_PAR_RESOLVE 1  // resolve_par_kernel for streams with complete candidate lists
-#endif
 constexpr uint64_t kParNodeCap = uint64_t(1) << 20;  // parallel-resolver nodes per launch (<= 88 MB of tables)
 struct LongLayout {
     int64_t nseg;
@@ -4180,7 +3760,7 @@ LongLayout long_layout(int64_t nseg, uint32_t nstreams) {
     L.node_cap = 0;
     L.levels = 0;
     L.off_serial = L.off_forced = L.off_jump = o;
-    if (KCDC_PAR_RESOLVE) {
+    {  // resolve_par_kernel for streams with complete candidate lists
         L.node_cap = std::min<uint64_t>(static_cast<uint64_t>(ns) * dev::kSegK + 2ull * nstreams, kParNodeCap);
         L.levels = 1;
         while ((uint64_t(1) << L.levels) <= L.node_cap) L.levels++;
@@ -4244,7 +3824,7 @@ int launch_split_long_multi(const Algo& algo, uint32_t m, const uint8_t* const* 
     g.seg_off = reinterpret_cast<uint64_t*>(w + L.off_off);
     g.list = reinterpret_cast<uint64_t*>(w + L.off_list);
     g.total = reinterpret_cast<uint64_t*>(w + L.off_total);
-    if (KCDC_PAR_RESOLVE) {
+    {
         g.serial = reinterpret_cast<uint32_t*>(w + L.off_serial);
         g.forced = reinterpret_cast<uint32_t*>(w + L.off_forced);
         g.jump = reinterpret_cast<uint32_t*>(w + L.off_jump);
@@ -4256,23 +3836,17 @@ int launch_split_long_multi(const Algo& algo, uint32_t m, const uint8_t* const* 
     dev::BatchArgs a = base_args(algo, *t);
     const int64_t mn = static_cast<int64_t>(algo.min_size()), mx = static_cast<int64_t>(algo.max_size());
     if (nseg > 0) {
-        const dim3 grid(static_cast<unsigned>((nseg + dev::kScanWaves - 1) / dev::kScanWaves));
-        const dim3 block(dev::kScanWaves * dev::kWave);
-        if (algo.kind == kBuzhash && KCDC_LONG_DMA) {  // LDS-DMA fed, persistent: one workgroup per CU
+        if (algo.kind == kBuzhash) {  // LDS-DMA fed, persistent: one workgroup per CU
             const dim3 pgrid(static_cast<unsigned>(
                 std::min<int64_t>(t->cus, (nseg + dev::kDmaWaves - 1) / dev::kDmaWaves)));
             if (buz_frame(static_cast<uint32_t>(algo.mask())).top)
                 hipLaunchKernelGGL(dev::cand_scan_dma_kernel<true>, pgrid, dim3(dev::kDmaWaves * dev::kWave), 0, st, a, g);
             else
                 hipLaunchKernelGGL(dev::cand_scan_dma_kernel<false>, pgrid, dim3(dev::kDmaWaves * dev::kWave), 0, st, a, g);
-        } else if (algo.kind == kRabinKarp && KCDC_RK_PIPE) {  // two-chain LDS-DMA tiles, persistent
+        } else {  // Rabin-Karp: two-chain LDS-DMA tiles, persistent
             const dim3 pgrid(static_cast<unsigned>(
                 std::min<int64_t>(t->cus, (nseg + dev::kRkWaves - 1) / dev::kRkWaves)));
             hipLaunchKernelGGL(dev::cand_scan_rk_kernel, pgrid, dim3(dev::kRkWaves * dev::kWave), 0, st, a, g);
-        } else if (algo.kind == kBuzhash) {
-            hipLaunchKernelGGL(dev::cand_scan_kernel<kBuzhash>, grid, block, 0, st, a, g);
-        } else {
-            hipLaunchKernelGGL(dev::cand_scan_kernel<kRabinKarp>, grid, block, 0, st, a, g);
         }
         const unsigned nblk = static_cast<unsigned>((nseg + dev::kPrefixItems - 1) / dev::kPrefixItems);
         uint64_t* bsum = reinterpret_cast<uint64_t*>(w + L.off_bsum);

@@ -47,10 +47,7 @@ span = en_us.max()
 # waves still scanning a stream of their own at time x (the tail's shape)
 grid = np.linspace(0, span, 41)
 owners = [int((own_end >= x).sum()) for x in grid]
-hdr = np.zeros(2048, dtype=np.uint32)
-assert lib.kcdc_debug_queue_copy(hdr.ctypes.data_as(C.c_void_p)) == 0
-help_stats = dict(zip(["attempts", "empty_windows", "lost_races", "stale_records", "tasks"], hdr[1792:1797].tolist()))
-print(json.dumps({"waves": int(t.shape[0]), "span_us": round(span, 1), "help_find": help_stats,
+print(json.dumps({"waves": int(t.shape[0]), "span_us": round(span, 1),
                   "busy_frac": round(float((en_us - st_us).mean() / span), 4),
                   "blocking_take_us_per_wave": round(float(blk_us.mean()), 1),
                   "final_idle_us_pct": {p: round(float(np.percentile(en_us - (t[:, 3] - t0) / 100.0, p)), 1)
