@@ -74,6 +74,7 @@ struct CompArgs {
     uint32_t* span_bytes;  // [max_spans]: output bytes of each span's segments
     uint64_t* span_pos;    // [max_spans + 1]: their exclusive prefix over all chunks
     uint8_t* slots;     // [max_spans * 64 * kSlot]
+    uint32_t* desc;     // [max_spans * kDescWords]: deflate, each span's plan
     uint32_t n;
     uint32_t max_spans;
     uint32_t header_id;
@@ -122,6 +123,31 @@ __global__ __launch_bounds__(1024) void span_scan_kernel(uint32_t n, uint32_t* s
 
 // LDS dword index of staged word k: one pad dword per 128 words (a 512-byte segment).
 __device__ __forceinline__ uint32_t pw(uint32_t k) { return k + (k >> 7); }
+// Byte x / the 4 bytes at x of a span staged at byte offset d (the source's misalignment).
+__device__ __forceinline__ uint32_t st_byte(const uint32_t* L, uint32_t d, uint32_t x) {
+    const uint32_t q = x + d;
+    return reinterpret_cast<const uint8_t*>(L)[4u * pw(q >> 2) + (q & 3u)];
+}
+__device__ __forceinline__ uint32_t st_ld32(const uint32_t* L, uint32_t d, uint32_t x) {
+    const uint32_t q = x + d, k = q >> 2;
+    return __builtin_amdgcn_alignbit(L[pw(k + 1)], L[pw(k)], 8u * (q & 3u));
+}
+// Stage the span_len bytes at A into L: the 16-byte granules [A & ~15, ...) holding them, at
+// staged word pw(k); returns d = A & 15.
+__device__ __forceinline__ uint32_t stage_span(uint32_t* L, const uint8_t* A, uint32_t span_len, uint32_t lane) {
+    const uint32_t d = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(A) & 15u);
+    const uint4* G = reinterpret_cast<const uint4*>(A - d);
+    const uint32_t ng = (d + span_len + 15u) >> 4;
+    for (uint32_t g = lane; g < ng; g += 64u) {
+        const uint4 v = G[g];
+        const uint32_t k = 4u * g;
+        L[pw(k)] = v.x;
+        L[pw(k + 1)] = v.y;
+        L[pw(k + 2)] = v.z;
+        L[pw(k + 3)] = v.w;
+    }
+    return d;
+}
 
 // ---------------------------------------------------------------- Zstandard sequences (RFC 8878)
 // The sequences of a block go through FSE with the predefined distributions (Symbol_Compression_Modes
@@ -238,46 +264,606 @@ struct Bits {
 // Huffman codes go MSB-first into the LSB-first bit stream (RFC 1951 §3.1.1).
 __device__ __forceinline__ uint32_t rev(uint32_t code, uint32_t n) { return __builtin_bitreverse32(code) >> (32u - n); }
 
-// Fixed literal/length code (RFC 1951 §3.2.6).
-__device__ __forceinline__ void put_lit(Bits& w, uint32_t b) {
-    if (b < 144u)
-        w.put(rev(0x30u + b, 8), 8);
-    else
-        w.put(rev(0x190u + (b - 144u), 9), 9);
-}
-__device__ __forceinline__ void put_match(Bits& w, uint32_t len, uint32_t dist) {
-    uint32_t sym, eb = 0, ev = 0;
+// A deflate match's symbols (RFC 1951 §3.2.5): length symbol 257..285 with its extra bits,
+// distance symbol 0..29 with its extra bits.
+struct MatchSyms {
+    uint32_t ls, eb, ev, ds, deb, dev;
+};
+__device__ __forceinline__ MatchSyms match_syms(uint32_t len, uint32_t dist) {
+    MatchSyms m{0u, 0u, 0u, 0u, 0u, 0u};
     const uint32_t l = len - 3u;
     if (len == 258u) {
-        sym = 285u;
+        m.ls = 285u;
     } else if (l < 8u) {
-        sym = 257u + l;
+        m.ls = 257u + l;
     } else {
         const uint32_t nb = 31u - __builtin_clz(l);
-        eb = nb - 2u;
-        sym = 257u + 4u * (nb - 1u) + ((l >> eb) & 3u);
-        ev = l & ((1u << eb) - 1u);
+        m.eb = nb - 2u;
+        m.ls = 257u + 4u * (nb - 1u) + ((l >> m.eb) & 3u);
+        m.ev = l & ((1u << m.eb) - 1u);
     }
-    if (sym < 280u)
-        w.put(rev(sym - 256u, 7), 7);
-    else
-        w.put(rev(0xC0u + (sym - 280u), 8), 8);
-    if (eb) w.put(ev, eb);
     const uint32_t d = dist - 1u;
-    uint32_t dc = d, deb = 0, dev = 0;
+    m.ds = d;
     if (d >= 4u) {
         const uint32_t nb = 31u - __builtin_clz(d);
-        deb = nb - 1u;
-        dc = 2u * nb + ((d >> deb) & 1u);
-        dev = d & ((1u << deb) - 1u);
+        m.deb = nb - 1u;
+        m.ds = 2u * nb + ((d >> m.deb) & 1u);
+        m.dev = d & ((1u << m.deb) - 1u);
     }
-    w.put(rev(dc, 5), 5);
-    if (deb) w.put(dev, deb);
+    return m;
 }
+
+// ---------------------------------------------------------------- deflate blocks of a span
+// The parse (lz_spans_kernel<kFmtDeflate>) leaves each segment's matches as tokens in its slot
+// ((literal run << 23) | (length - 3) << 15 | (distance - 1): a segment holds <= 128) and marks
+// the segment stored when a fixed code would not beat a stored copy (random data).  The span's
+// coded segments then share ONE code: per maximal run of coded segments one Huffman block,
+// BTYPE 10 with a dynamic code built from the span's symbol counts (default and
+// best-compression) or BTYPE 01 with the fixed code (best-speed, or when smaller for the span);
+// per run of stored segments one stored block; a span whose coded form is not smaller than a
+// stored copy is one stored block.  A span ends byte aligned (a coded run last: an empty stored
+// block, zlib's sync flush), so spans concatenate by a byte prefix as before.  The plan (block
+// type, code lengths, header bits, every segment's bit offset) goes to the span's descriptor;
+// deflate_emit_kernel writes the bits straight to the chunk's place.
+// The reference's encoder (klauspost/compress/flate, compressor_deflate.go:14-16) chooses
+// between the same three block types per block; readers accept any valid RFC 1951 stream.
+constexpr uint32_t kNLit = 286, kNDist = 30, kNSym = kNLit + kNDist;
+constexpr uint32_t kHdrWords = 72;  // a dynamic header: <= 5 + 5 + 4 + 19 * 3 + 316 * 7 bits
+// Descriptor words per span: [0, 64) each segment's bit offset in the span's output; [64, 128)
+// its info (class 1 coded / 2 stored, bit 2 first of its run, bit 3 last of its run, bit 4 the
+// span's last segment, bits 16.. a stored run's length at its first segment); [128, 208) the code
+// lengths (bytes: 286 literal/length, 30 distance); [208, 280) the dynamic header's bits; [280]
+// the mode (0 one stored block, 1 fixed, 2 dynamic) | header bits << 8.
+constexpr uint32_t kDescOff = 0, kDescInfo = 64, kDescLens = 128, kDescHdr = 208, kDescMode = 280;
+constexpr uint32_t kDescWords = 288;
+static_assert(kDescHdr + kHdrWords <= kDescMode && kDescMode < kDescWords, "descriptor layout");
+constexpr uint32_t kModeStored = 0, kModeFixed = 1, kModeDynamic = 2;
+constexpr uint32_t kClsCoded = 1, kClsStored = 2;
+
+// Fixed code lengths (RFC 1951 §3.2.6); s >= 286: distance symbols.
+__device__ __forceinline__ uint32_t fixed_len(uint32_t s) {
+    return s < 144u ? 8u : s < 256u ? 9u : s < 280u ? 7u : s < kNLit ? 8u : 5u;
+}
+
+// Canonical codes (RFC 1951 §3.2.2) of the n code lengths len[] (LDS bytes), bit-reversed for the
+// LSB-first stream: out[s] = rev(code) | length << 16 (0 for unused symbols).  Wave-collective:
+// symbols in 64-wide groups, a symbol's rank among the equal lengths before it by ballot.
+__device__ void canon_codes(const uint8_t* len, uint32_t n, uint32_t* out, uint32_t lane) {
+    uint32_t cnt[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) cnt[j] = 0u;
+    for (uint32_t k = 0; k < n; k += 64u) {
+        const uint32_t l = k + lane < n ? len[k + lane] : 0u;
+#pragma unroll
+        for (int j = 1; j < 16; j++) cnt[j] += static_cast<uint32_t>(__popcll(__ballot(l == static_cast<uint32_t>(j))));
+    }
+    uint32_t next[16];
+    next[0] = 0u;
+    uint32_t code = 0u;
+#pragma unroll
+    for (int j = 1; j < 16; j++) {
+        code = (code + (j > 1 ? cnt[j - 1] : 0u)) << 1;
+        next[j] = code;
+    }
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (uint32_t k = 0; k < n; k += 64u) {
+        const uint32_t l = k + lane < n ? len[k + lane] : 0u;
+        uint32_t c = 0u;
+#pragma unroll
+        for (int j = 1; j < 16; j++) {
+            const uint64_t m = __ballot(l == static_cast<uint32_t>(j));
+            if (l == static_cast<uint32_t>(j)) c = next[j] + static_cast<uint32_t>(__popcll(m & lt));
+            next[j] += static_cast<uint32_t>(__popcll(m));
+        }
+        if (k + lane < n) out[k + lane] = l ? (rev(c, l) | (l << 16)) : 0u;
+    }
+}
+
+// Code lengths (<= maxb bits) of a minimum-redundancy code for the n counts cnt[] (LDS), into
+// len[] (LDS bytes); unused symbols get 0, a single used symbol 1.  The wave ranks the used
+// symbols by (count, symbol); lane 0 then runs Moffat and Katajainen's in-place construction
+// ("In-place calculation of minimum-redundancy codes", WADS 1995) over the sorted counts and, if
+// a depth exceeds maxb, clamps the depths and moves leaves down until the Kraft sum is exactly 1
+// (the zlib/miniz limiting heuristic).  Scratch (LDS): sa[n], ss[n], num[33].  Wave-collective.
+__device__ void huff_lengths(const uint32_t* cnt, uint32_t n, uint32_t maxb, uint8_t* len, uint32_t* sa, uint16_t* ss,
+                             uint32_t* num, uint32_t lane) {
+    uint32_t used = 0u;
+    for (uint32_t k = 0; k < n; k += 64u) {
+        const uint32_t s = k + lane;
+        const uint32_t c = s < n ? cnt[s] : 0u;
+        uint32_t r = 0u;
+        for (uint32_t t = 0; t < n; t++) {
+            const uint32_t ct = cnt[t];
+            r += (ct != 0u && (ct < c || (ct == c && t < s))) ? 1u : 0u;
+        }
+        if (s < n) len[s] = 0u;
+        if (c) {
+            sa[r] = c;
+            ss[r] = static_cast<uint16_t>(s);
+        }
+        used += static_cast<uint32_t>(__popcll(__ballot(c != 0u)));
+    }
+    __syncthreads();
+    if (lane == 0 && used == 1u) len[ss[0]] = 1u;
+    if (lane == 0 && used >= 2u) {
+        const int m = static_cast<int>(used);
+        uint32_t* A = sa;
+        A[0] += A[1];
+        int root = 0, leaf = 2;
+        for (int next = 1; next < m - 1; next++) {
+            if (leaf >= m || A[root] < A[leaf]) {
+                A[next] = A[root];
+                A[root++] = static_cast<uint32_t>(next);
+            } else {
+                A[next] = A[leaf++];
+            }
+            if (leaf >= m || (root < next && A[root] < A[leaf])) {
+                A[next] += A[root];
+                A[root++] = static_cast<uint32_t>(next);
+            } else {
+                A[next] += A[leaf++];
+            }
+        }
+        A[m - 2] = 0u;
+        for (int next = m - 3; next >= 0; next--) A[next] = A[A[next]] + 1u;
+        int avbl = 1, usedc = 0, dpth = 0, next = m - 1;
+        root = m - 2;
+        while (avbl > 0) {
+            while (root >= 0 && static_cast<int>(A[root]) == dpth) {
+                usedc++;
+                root--;
+            }
+            while (avbl > usedc) {
+                A[next--] = static_cast<uint32_t>(dpth);
+                avbl--;
+            }
+            avbl = 2 * usedc;
+            dpth++;
+            usedc = 0;
+        }
+        // A[i]: depth of the i-th least frequent symbol (non-increasing in i)
+        for (uint32_t l = 0; l <= 32u; l++) num[l] = 0u;
+        uint32_t maxd = 0u;
+        for (int i = 0; i < m; i++) {
+            const uint32_t dd = A[i] < 32u ? A[i] : 32u;
+            num[dd]++;
+            maxd = dd > maxd ? dd : maxd;
+        }
+        if (maxd > maxb) {
+            for (uint32_t l = maxb + 1u; l <= 32u; l++) {
+                num[maxb] += num[l];
+                num[l] = 0u;
+            }
+            uint32_t total = 0u;
+            for (uint32_t l = 1; l <= maxb; l++) total += num[l] << (maxb - l);
+            while (total != (1u << maxb)) {
+                num[maxb]--;
+                for (uint32_t l = maxb - 1u; l > 0u; l--)
+                    if (num[l]) {
+                        num[l]--;
+                        num[l + 1u] += 2u;
+                        break;
+                    }
+                total--;
+            }
+        }
+        int i = 0;
+        for (uint32_t l = maxb; l >= 1u; l--)
+            for (uint32_t k = num[l]; k > 0u; k--) len[ss[i++]] = static_cast<uint8_t>(l);
+    }
+    __syncthreads();
+}
+
+// The bit layout of a span's output for one code (hb = block header bits incl. the 3-bit BTYPE
+// header, eob = the end-of-block code's length): each segment's bit offset and info (see the
+// descriptor), the total in bits (a multiple of 8).  cls/bits/slen per segment, nseg segments.
+// One lane; deflate_emit_kernel writes exactly these bits.
+__device__ uint32_t deflate_layout(const uint32_t* cls, const uint32_t* bits, const uint32_t* slen, uint32_t nseg,
+                                   uint32_t hb, uint32_t eob, uint32_t* boff, uint32_t* info) {
+    uint32_t pos = 0u;
+    for (uint32_t j = 0; j < nseg; j++) {
+        const uint32_t c = cls[j];
+        const bool first = j == 0u || cls[j - 1u] != c, end = j + 1u == nseg, last = end || cls[j + 1u] != c;
+        uint32_t inf = c | (first ? 4u : 0u) | (last ? 8u : 0u) | (end ? 16u : 0u);
+        if (boff) boff[j] = pos;
+        if (c == kClsCoded) {
+            pos += (first ? hb : 0u) + bits[j] + (last ? eob : 0u);
+            if (end) pos = ((pos + 3u + 7u) & ~7u) + 32u;  // sync flush: 000, pad, 00 00 FF FF
+        } else {
+            if (first) {
+                uint32_t run = 0u;
+                for (uint32_t k = j; k < nseg && cls[k] == kClsStored; k++) run += slen[k];
+                inf |= run << 16;
+                pos = ((pos + 3u + 7u) & ~7u) + 32u;  // BFINAL 0, BTYPE 00, pad, LEN, NLEN
+            }
+            pos += 8u * slen[j];
+        }
+        if (info) info[j] = inf;
+    }
+    return pos;
+}
+
+__constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// The dynamic block header (RFC 1951 §3.2.7) for the code lengths len[0..316): HLIT, HDIST,
+// HCLEN, the code-length code's lengths in the permuted order, then the literal/length and
+// distance lengths (one sequence) run-length coded with 16 (the previous length 3-6 times), 17
+// (3-10 zeros) and 18 (11-138 zeros) through that code (lengths <= 7, at least two used symbols:
+// inflaters reject an incomplete code-length code).  Bits to hdr[] (LDS words); returns their
+// count.  Scratch (LDS): cl[316] (symbol | extra << 8), clcnt[19], cllen[20], clcode[19], misc[4]
+// and huff_lengths' sa/ss/num.  Wave-collective.
+__device__ uint32_t dyn_header(const uint8_t* len, uint32_t* hdr, uint16_t* cl, uint32_t* clcnt, uint8_t* cllen,
+                               uint32_t* clcode, uint32_t* sa, uint16_t* ss, uint32_t* num, uint32_t* misc,
+                               uint32_t lane) {
+    if (lane == 0) {
+        uint32_t hlit = kNLit, hdist = kNDist;
+        while (hlit > 257u && len[hlit - 1u] == 0u) hlit--;
+        while (hdist > 1u && len[kNLit + hdist - 1u] == 0u) hdist--;
+        for (uint32_t j = 0; j < 19u; j++) clcnt[j] = 0u;
+        const uint32_t nt = hlit + hdist;
+        auto at = [&](uint32_t i) -> uint32_t { return i < hlit ? len[i] : len[kNLit + i - hlit]; };
+        uint32_t ncl = 0;
+        auto sym = [&](uint32_t s, uint32_t x) {
+            cl[ncl++] = static_cast<uint16_t>(s | (x << 8));
+            clcnt[s]++;
+        };
+        for (uint32_t i = 0; i < nt;) {
+            const uint32_t v = at(i);
+            uint32_t r = 1;
+            while (i + r < nt && at(i + r) == v) r++;
+            i += r;
+            if (v == 0u) {
+                while (r >= 11u) {
+                    const uint32_t k = r < 138u ? r : 138u;
+                    sym(18u, k - 11u);
+                    r -= k;
+                }
+                if (r >= 3u) {
+                    sym(17u, r - 3u);
+                    r = 0u;
+                }
+            } else {
+                sym(v, 0u);
+                r--;
+                while (r >= 3u) {
+                    const uint32_t k = r < 6u ? r : 6u;
+                    sym(16u, k - 3u);
+                    r -= k;
+                }
+            }
+            for (; r > 0u; r--) sym(v, 0u);
+        }
+        uint32_t nz = 0;
+        for (uint32_t j = 0; j < 19u; j++) nz += clcnt[j] != 0u;
+        if (nz < 2u) {
+            if (clcnt[0] == 0u) clcnt[0] = 1u;
+            else clcnt[1] = 1u;
+        }
+        misc[0] = hlit;
+        misc[1] = hdist;
+        misc[2] = ncl;
+    }
+    __syncthreads();
+    huff_lengths(clcnt, 19u, 7u, cllen, sa, ss, num, lane);
+    canon_codes(cllen, 19u, clcode, lane);
+    __syncthreads();
+    if (lane == 0) {
+        uint32_t hclen = 19u;
+        while (hclen > 4u && cllen[kClOrder[hclen - 1u]] == 0u) hclen--;
+        Bits w{0ull, 0u, hdr};
+        w.put(misc[0] - 257u, 5);
+        w.put(misc[1] - 1u, 5);
+        w.put(hclen - 4u, 4);
+        for (uint32_t i = 0; i < hclen; i++) w.put(cllen[kClOrder[i]], 3);
+        const uint32_t ncl = misc[2];
+        for (uint32_t k = 0; k < ncl; k++) {
+            const uint32_t s = cl[k] & 31u, x = cl[k] >> 8, c = clcode[s];
+            w.put(c & 0xFFFFu, c >> 16);
+            if (s >= 16u) w.put(x, s == 16u ? 2u : s == 17u ? 3u : 7u);
+        }
+        const uint32_t hb = 32u * static_cast<uint32_t>(w.op - hdr) + w.nb;
+        if (w.nb) *w.op = static_cast<uint32_t>(w.bb);
+        misc[3] = hb;
+    }
+    __syncthreads();
+    return misc[3];
+}
+
+// Bits OR-ed into an LDS word buffer from any bit offset (neighbouring segments share words).
+struct OrBits {
+    uint64_t bb;
+    uint32_t nb;
+    uint32_t wa;
+    uint32_t* buf;
+    __device__ __forceinline__ void put(uint32_t v, uint32_t n) {
+        bb |= static_cast<uint64_t>(v) << nb;
+        nb += n;
+        if (nb >= 32u) {
+            atomicOr(&buf[wa++], static_cast<uint32_t>(bb));
+            bb >>= 32;
+            nb -= 32u;
+        }
+    }
+    __device__ __forceinline__ void pad() { put(0u, (8u - (nb & 7u)) & 7u); }
+    __device__ __forceinline__ void flush() {
+        if (nb) atomicOr(&buf[wa], static_cast<uint32_t>(bb));
+    }
+};
 
 // S2 framing header of span b: 0x00, 3-byte LE length of (CRC + block), then the masked CRC
 // (written by the copy kernel) and the block's uvarint uncompressed length.
 __device__ __forceinline__ uint32_t uvarint_len(uint32_t v) { return v < 128u ? 1u : v < 16384u ? 2u : 3u; }
+
+// The chunk of global span b: the last c with spans[c] <= b (empty chunks share their prefix
+// with the next).
+__device__ __forceinline__ uint32_t span_chunk(const CompArgs& a, uint32_t b) {
+    uint32_t lo = 0, hi = a.n;  // spans[lo] <= b < spans[hi]
+    while (hi - lo > 1u) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.spans[mid] <= b) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// Walk a coded segment's tokens: lit(x) per literal byte position, match(x, len, dist) per match.
+template <typename FL, typename FM>
+__device__ __forceinline__ void walk_tokens(const uint32_t* tok, uint32_t nm, uint32_t x0, uint32_t xe, FL lit, FM match) {
+    uint32_t x = x0;
+    for (uint32_t k = 0; k < nm; k++) {
+        const uint32_t t = tok[k];
+        for (const uint32_t e = x + (t >> 23); x < e; x++) lit(x);
+        const uint32_t n = ((t >> 15) & 255u) + 3u;
+        match(x, n, (t & 0x7FFFu) + 1u);
+        x += n;
+    }
+    for (; x < xe; x++) lit(x);
+}
+
+// The span's deflate plan (see "deflate blocks of a span"), after the parse: symbol counts of the
+// coded segments, the dynamic code and its header (effort >= 1), every segment's size under the
+// dynamic and the fixed code, the cheapest of dynamic / fixed / one stored block, and the layout
+// to the span's descriptor; span_bytes[b] = the span's output bytes.  S: 2048 words of LDS
+// scratch (the match tables, free once every lane's parse is done).
+__device__ __forceinline__ void deflate_plan(const CompArgs& a, uint32_t b, uint32_t lane, uint32_t span_len,
+                                             uint32_t x0, uint32_t word, uint32_t nm, uint32_t* hist, uint32_t* S,
+                                             const uint32_t* L, uint32_t d) {
+    __syncthreads();  // every lane's parse is done
+    uint32_t* sa = S;                                      // [0, 288)
+    uint16_t* ss = reinterpret_cast<uint16_t*>(S + 288);   // 286 u16
+    uint8_t* lens = reinterpret_cast<uint8_t*>(S + 432);   // 316 bytes
+    uint32_t* hdr = S + 512;                               // kHdrWords
+    uint32_t* clcnt = S + 584;                             // 19
+    uint8_t* cllen = reinterpret_cast<uint8_t*>(S + 604);  // 19 bytes
+    uint32_t* clcode = S + 612;                            // 19
+    uint16_t* cl = reinterpret_cast<uint16_t*>(S + 640);   // 316 u16
+    uint32_t *lcls = S + 800, *lbd = S + 864, *lbf = S + 928, *llen = S + 992;  // per segment
+    uint32_t *boff = S + 1056, *info = S + 1120;
+    uint32_t* num = S + 1184;                              // 33
+    uint32_t* misc = S + 1220;                             // 8
+    const uint32_t seg_len = x0 < span_len ? min(kSeg, span_len - x0) : 0u, xe = x0 + seg_len;
+    const bool coded = seg_len && !(word & kStored);
+    const uint32_t* tok = reinterpret_cast<const uint32_t*>(a.slots + (static_cast<uint64_t>(b) * 64u + lane) * kSlot);
+    const uint64_t cm = __ballot(coded);
+    const bool dynamic = cm != 0ull && a.effort >= 1u;
+    if (dynamic && coded)
+        walk_tokens(tok, nm, x0, xe, [&](uint32_t x) { atomicAdd(&hist[st_byte(L, d, x)], 1u); },
+                    [&](uint32_t, uint32_t n, uint32_t dist) {
+                        const MatchSyms m = match_syms(n, dist);
+                        atomicAdd(&hist[m.ls], 1u);
+                        atomicAdd(&hist[kNLit + m.ds], 1u);
+                    });
+    __syncthreads();
+    uint32_t hb = 0;
+    if (dynamic) {
+        if (lane == 0) {
+            hist[256] = 1u;  // end of block
+            uint32_t nz = 0;  // >= 2 distance codes: inflaters take no incomplete code but a single 1-bit one
+            for (uint32_t j = 0; j < kNDist; j++) nz += hist[kNLit + j] != 0u;
+            if (nz < 2u) {
+                if (hist[kNLit] == 0u) hist[kNLit] = 1u;
+                if (hist[kNLit + 1] == 0u) hist[kNLit + 1] = 1u;
+            }
+        }
+        __syncthreads();
+        huff_lengths(hist, kNLit, 15u, lens, sa, ss, num, lane);
+        huff_lengths(hist + kNLit, kNDist, 15u, lens + kNLit, sa, ss, num, lane);
+        hb = dyn_header(lens, hdr, cl, clcnt, cllen, clcode, sa, ss, num, misc, lane);
+    }
+    uint32_t bd = 0, bf = 0;  // the segment's bits under the dynamic / the fixed code
+    if (coded)
+        walk_tokens(tok, nm, x0, xe,
+                    [&](uint32_t x) {
+                        const uint32_t v = st_byte(L, d, x);
+                        if (dynamic) bd += lens[v];
+                        bf += fixed_len(v);
+                    },
+                    [&](uint32_t, uint32_t n, uint32_t dist) {
+                        const MatchSyms m = match_syms(n, dist);
+                        if (dynamic) bd += lens[m.ls] + lens[kNLit + m.ds] + m.eb + m.deb;
+                        bf += fixed_len(m.ls) + 5u + m.eb + m.deb;
+                    });
+    lcls[lane] = coded ? kClsCoded : seg_len ? kClsStored : 0u;
+    lbd[lane] = bd;
+    lbf[lane] = bf;
+    llen[lane] = seg_len;
+    __syncthreads();
+    const uint32_t nseg = (span_len + kSeg - 1u) / kSeg;
+    if (lane == 0) {
+        uint32_t mode = kModeStored, bits = 8u * (span_len + 5u);
+        if (cm) {
+            const uint32_t tf = deflate_layout(lcls, lbf, llen, nseg, 3u, 7u, nullptr, nullptr);
+            if (tf < bits) {
+                mode = kModeFixed;
+                bits = tf;
+            }
+            if (dynamic) {
+                const uint32_t td = deflate_layout(lcls, lbd, llen, nseg, 3u + hb, lens[256], nullptr, nullptr);
+                if (td < bits) {
+                    mode = kModeDynamic;
+                    bits = td;
+                }
+            }
+            if (mode == kModeDynamic)
+                deflate_layout(lcls, lbd, llen, nseg, 3u + hb, lens[256], boff, info);
+            else if (mode == kModeFixed)
+                deflate_layout(lcls, lbf, llen, nseg, 3u, 7u, boff, info);
+        }
+        misc[4] = mode;
+        misc[5] = bits;
+    }
+    __syncthreads();
+    const uint32_t mode = misc[4];
+    uint32_t* desc = a.desc + static_cast<uint64_t>(b) * kDescWords;
+    if (mode != kModeStored) {
+        a.seglen[b * 64u + lane] = nm;
+        desc[kDescOff + lane] = lane < nseg ? boff[lane] : 0u;
+        desc[kDescInfo + lane] = lane < nseg ? info[lane] : 0u;
+    }
+    if (mode == kModeDynamic) {
+        for (uint32_t k = lane; k < 80u; k += 64u) desc[kDescLens + k] = k < 79u ? S[432 + k] : 0u;
+        for (uint32_t k = lane; k < (hb + 31u) / 32u; k += 64u) desc[kDescHdr + k] = hdr[k];
+    }
+    if (lane == 0) {
+        desc[kDescMode] = mode | (hb << 8);
+        a.span_bytes[b] = misc[5] >> 3;
+    }
+}
+
+// zstd literals through one Huffman code per span (RFC 8878 §3.1.1.3.1, §4.2): after the parse
+// (each coded segment a Compressed_Block with Raw_Literals: block header at slot + 3, literals
+// header at + 6, the literals from + 8, the sequences section after them), the span's literal
+// counts give a code of <= 11 bits.  The first segment whose literals shrink with it, tree
+// description included, carries the tree (Compressed_Literals_Block, direct weights: the span's
+// largest literal must be <= 128); the later segments whose literals shrink reuse it
+// (Treeless_Literals_Block, the frame's previous table); the others keep raw literals.  Single
+// stream, 10-bit sizes (a segment has <= 512 literals); the stream holds the literals last to
+// first (the decoder reads it backwards), then a 1 bit.  Literal bytes come from the staged span;
+// the stream overwrites the raw literals (it is shorter) and the sequences section moves down
+// behind it.  Returns the segment's new length word.  S: LDS scratch (the match tables).
+// The reference's zstd encoder (klauspost/compress/zstd, compressor_zstd.go:15-18) Huffman-codes
+// literals the same way (one table per block, reused by later blocks when that is smaller).
+__device__ __forceinline__ uint32_t zstd_huff_literals(const CompArgs& a, uint32_t b, uint32_t lane, uint32_t span_len,
+                                                       uint32_t x0, uint32_t word, uint32_t nseq, uint32_t nlit,
+                                                       uint32_t* hist, uint32_t* S, const uint32_t* L, uint32_t d) {
+    __syncthreads();  // every lane's parse is done
+    uint32_t* sa = S;                                      // 256
+    uint16_t* ss = reinterpret_cast<uint16_t*>(S + 256);   // 256 u16
+    uint8_t* lens = reinterpret_cast<uint8_t*>(S + 384);   // 256 bytes
+    uint32_t* zc = S + 448;                                // 256: code | bits << 16
+    uint32_t* num = S + 704;                               // 33
+    uint32_t* misc = S + 740;                              // 8
+    const uint32_t seg_len = x0 < span_len ? min(kSeg, span_len - x0) : 0u, xe = x0 + seg_len;
+    const bool coded = seg_len && !(word & kStored);
+    uint8_t* sb8 = a.slots + (static_cast<uint64_t>(b) * 64u + lane) * kSlot;
+    const uint32_t* sq = reinterpret_cast<const uint32_t*>(sb8);  // sequence k at word 143 - k
+    auto seq_ll = [&](uint32_t k) { return sq[143u - k] >> 23; };
+    auto seq_ml = [&](uint32_t k) { return ((sq[143u - k] >> 15) & 255u) + 4u; };
+    if (coded) {
+        uint32_t x = x0;
+        for (uint32_t k = 0; k < nseq; k++) {
+            for (const uint32_t e = x + seq_ll(k); x < e; x++) atomicAdd(&hist[st_byte(L, d, x)], 1u);
+            x += seq_ml(k);
+        }
+        for (; x < xe; x++) atomicAdd(&hist[st_byte(L, d, x)], 1u);
+    }
+    __syncthreads();
+    uint32_t used = 0, top = 0;
+    for (uint32_t k = 0; k < 256u; k += 64u) {
+        const uint64_t m = __ballot(hist[k + lane] != 0u);
+        used += static_cast<uint32_t>(__popcll(m));
+        if (m) top = k + 63u - static_cast<uint32_t>(__builtin_clzll(m));
+    }
+    if (used < 2u || top > 128u) return word;  // one symbol (an RLE block's case) or no direct weights: raw
+    huff_lengths(hist, 256u, 11u, lens, sa, ss, num, lane);
+    if (lane == 0) {  // codes: by weight ascending (longest first), then symbol (RFC 8878 §4.2.1.4)
+        uint32_t maxb = 0;
+        for (uint32_t s = 0; s <= top; s++) maxb = lens[s] > maxb ? lens[s] : maxb;
+        for (uint32_t w = 0; w <= 12u; w++) num[w] = 0u;
+        for (uint32_t s = 0; s <= top; s++)
+            if (lens[s]) num[maxb + 1u - lens[s]]++;
+        uint32_t acc = 0;  // rank start (in 2^(w-1) cells), then the next code, per weight
+        for (uint32_t w = 1; w <= maxb; w++) {
+            const uint32_t c = num[w];
+            num[w] = acc >> (w - 1u);
+            acc += c << (w - 1u);
+        }
+        for (uint32_t s = 0; s <= top; s++) {
+            const uint32_t l = lens[s];
+            zc[s] = l ? (num[maxb + 1u - l]++ | (l << 16)) : 0u;
+        }
+        misc[0] = maxb;
+    }
+    __syncthreads();
+    const uint32_t maxb = misc[0];
+    const uint32_t tsz = 1u + (top + 1u) / 2u;  // header byte + 4-bit weights of symbols 0..top-1
+    uint32_t bits = 1u;                         // the end marker
+    auto for_lits = [&](auto f) {  // every literal of the segment, first to last
+        uint32_t x = x0;
+        for (uint32_t k = 0; k < nseq; k++) {
+            for (const uint32_t e = x + seq_ll(k); x < e; x++) f(x);
+            x += seq_ml(k);
+        }
+        for (; x < xe; x++) f(x);
+    };
+    if (coded && nlit) for_lits([&](uint32_t x) { bits += zc[st_byte(L, d, x)] >> 16; });
+    const uint32_t sbytes = (bits + 7u) / 8u;
+    const bool can_tree = coded && nlit && 3u + tsz + sbytes < 2u + nlit;
+    const uint64_t cm = __ballot(can_tree);
+    if (!cm) return word;
+    const uint32_t carrier = static_cast<uint32_t>(__builtin_ctzll(cm));
+    const uint32_t use = lane == carrier ? 2u : (lane > carrier && coded && nlit && 3u + sbytes < 2u + nlit) ? 3u : 0u;
+    if (!use) return word;
+    const uint32_t old_total = word;               // block header + content bytes, from slot + 3
+    const uint32_t qs = old_total - 5u - nlit;     // the sequences section, at slot + 8 + nlit
+    const uint32_t ts = use == 2u ? tsz : 0u;
+    uint8_t* op = sb8 + 9u + ts;
+    if (use == 2u) {  // direct weights: W = maxb + 1 - bits (0: unused), two per byte, high nibble first
+        sb8[9] = static_cast<uint8_t>(127u + top);
+        for (uint32_t j = 0; 2u * j < top; j++) {
+            const uint32_t l0 = lens[2u * j], l1 = 2u * j + 1u < top ? lens[2u * j + 1u] : 0u;
+            const uint32_t w0 = l0 ? maxb + 1u - l0 : 0u, w1 = l1 ? maxb + 1u - l1 : 0u;
+            sb8[10u + j] = static_cast<uint8_t>((w0 << 4) | w1);
+        }
+    }
+    // the stream: literals last to first, then the end marker
+    uint64_t bb = 0;
+    uint32_t nb = 0;
+    auto put = [&](uint32_t v, uint32_t n) {
+        bb |= static_cast<uint64_t>(v) << nb;
+        nb += n;
+        while (nb >= 8u) {
+            *op++ = static_cast<uint8_t>(bb);
+            bb >>= 8;
+            nb -= 8u;
+        }
+    };
+    auto lit = [&](uint32_t x) {
+        const uint32_t c = zc[st_byte(L, d, x)];
+        put(c & 0xFFFFu, c >> 16);
+    };
+    uint32_t xm = x0;
+    for (uint32_t k = 0; k < nseq; k++) xm += seq_ll(k) + seq_ml(k);
+    for (uint32_t x = xe; x > xm; x--) lit(x - 1u);
+    for (uint32_t k = nseq; k-- > 0u;) {
+        xm -= seq_ml(k);
+        for (uint32_t e = xm - seq_ll(k); xm > e; xm--) lit(xm - 1u);
+    }
+    put(1u, 1);
+    if (nb) put(0u, 8u - nb);
+    // literals header: type (2 compressed / 3 treeless), Size_Format 00, 10-bit sizes
+    const uint32_t lh = use | (nlit << 4) | ((ts + sbytes) << 14);
+    sb8[6] = static_cast<uint8_t>(lh);
+    sb8[7] = static_cast<uint8_t>(lh >> 8);
+    sb8[8] = static_cast<uint8_t>(lh >> 16);
+    const uint8_t* src = sb8 + 8u + nlit;
+    for (uint32_t i = 0; i < qs; i++) op[i] = src[i];  // the sequences section, moved down
+    const uint32_t total = 6u + ts + sbytes + qs;
+    const uint32_t hdr = ((total - 3u) << 3) | (2u << 1);  // Compressed_Block, not the last
+    sb8[3] = static_cast<uint8_t>(hdr);
+    sb8[4] = static_cast<uint8_t>(hdr >> 8);
+    sb8[5] = static_cast<uint8_t>(hdr >> 16);
+    return total;
+}
 
 // One wave per span: blockIdx.x = global span index.  FMT: kFmtDeflate or kFmtS2 (the parse is
 // shared; the emitters differ: fixed-Huffman bits closed by a sync flush, or Snappy tags).
@@ -286,37 +872,25 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
     __shared__ uint32_t L[kLdsWords];
     __shared__ uint16_t tab[(1u << kHashBits) * 64u];
     __shared__ uint32_t ftab[1u << kFirstBits];
+    __shared__ uint32_t hist[FMT == kFmtDeflate ? kNSym : FMT == kFmtZstd ? 256 : 1];  // the span's symbol counts
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
     const uint32_t total = a.spans[a.n];
     if (total > a.max_spans || b >= total) return;
-    // The chunk: the last c with spans[c] <= b (empty chunks share their prefix with the next).
-    uint32_t lo = 0, hi = a.n;  // spans[lo] <= b < spans[hi]
-    while (hi - lo > 1u) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (a.spans[mid] <= b) lo = mid; else hi = mid;
-    }
-    const uint32_t c = lo;
+    const uint32_t c = span_chunk(a, b);
     const uint32_t u = b - a.spans[c];
     const uint64_t len = a.in_lens[c];
     const uint64_t sb = static_cast<uint64_t>(u) * kSpan;
     const uint32_t span_len = static_cast<uint32_t>(len - sb < kSpan ? len - sb : kSpan);
     // Stage [A0, A0 + 16 ng) with A0 = A & ~15: every 16-byte granule holds a byte of the span.
-    const uint8_t* A = a.in + a.in_offs[c] + sb;
-    const uint32_t d = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(A) & 15u);
-    const uint4* G = reinterpret_cast<const uint4*>(A - d);
-    const uint32_t ng = (d + span_len + 15u) >> 4;
-    for (uint32_t g = lane; g < ng; g += 64u) {
-        const uint4 v = G[g];
-        const uint32_t k = 4u * g;
-        L[pw(k)] = v.x;
-        L[pw(k + 1)] = v.y;
-        L[pw(k + 2)] = v.z;
-        L[pw(k + 3)] = v.w;
-    }
+    const uint32_t d = stage_span(L, a.in + a.in_offs[c] + sb, span_len, lane);
     {
         uint64_t* t64 = reinterpret_cast<uint64_t*>(tab);
         for (uint32_t i = lane; i < (1u << kHashBits) * 16u; i += 64u) t64[i] = ~0ull;
         for (uint32_t i = lane; i < (1u << kFirstBits); i += 64u) ftab[i] = ~0u;
+        if constexpr (FMT == kFmtDeflate)
+            for (uint32_t i = lane; i < kNSym; i += 64u) hist[i] = 0u;
+        if constexpr (FMT == kFmtZstd)
+            for (uint32_t i = lane; i < 256u; i += 64u) hist[i] = 0u;
     }
     __syncthreads();
     const uint8_t* Lb = reinterpret_cast<const uint8_t*>(L);
@@ -339,6 +913,8 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
         __syncthreads();
     }
     uint32_t word = 0;  // the segment's length word (0: past the span's end)
+    uint32_t nm = 0;    // deflate: the segment's match tokens; zstd: its sequences
+    uint32_t zlit = 0;  // zstd: its literals
     if (x0 < span_len) word = [&]() -> uint32_t {
     const uint32_t xe = span_len - x0 < kSeg ? span_len : x0 + kSeg;
     const uint32_t seg_len = xe - x0;
@@ -350,7 +926,7 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
     Bits w{0ull, 0u, FMT == kFmtZstd ? base + 2 : base};
     bool over = false;
     uint32_t nseq = 0;
-    if constexpr (FMT == kFmtDeflate) w.put(2u, 3);  // BFINAL 0, BTYPE 01
+    uint32_t fb = 3;  // deflate: the segment's size as one fixed-code block (bits), the stored/coded test
     uint32_t x = x0, lit = x0;
     auto literals = [&](uint32_t e) {
         if constexpr (FMT == kFmtS2) {  // one literal element: tag (n-1) << 2 | 0, 60: +1 byte, 61: +2
@@ -366,11 +942,13 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
                 w.put(m, 16);
             }
         }
+        if constexpr (FMT == kFmtDeflate) {
+            for (uint32_t q = lit; q < e; q++) fb += byte(q) < 144u ? 8u : 9u;
+            over = fb > 8u * limit;
+            return;
+        }
         for (uint32_t q = lit; q < e; q++) {
-            if constexpr (FMT != kFmtDeflate)
-                w.put(byte(q), 8);
-            else
-                put_lit(w, byte(q));
+            w.put(byte(q), 8);
             if (4u * static_cast<uint32_t>(w.op - base) > limit) {
                 over = true;
                 break;
@@ -448,8 +1026,11 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
             } else if constexpr (FMT == kFmtZstd) {  // (literal length, match length - 4, offset)
                 base[143u - nseq] = ((x - lit) << 23) | ((n - 4u) << 15) | (x - cand);
                 nseq++;
-            } else {
-                put_match(w, n, x - cand);
+            } else {  // deflate token; the fixed code's cost
+                base[nm++] = ((x - lit) << 23) | ((n - 3u) << 15) | (x - cand - 1u);
+                const MatchSyms m = match_syms(n, x - cand);
+                fb += (m.ls < 280u ? 7u : 8u) + m.eb + 5u + m.deb;
+                if (fb > 8u * limit) over = true;
             }
             if (4u * static_cast<uint32_t>(w.op - base) > limit) {
                 over = true;
@@ -465,6 +1046,8 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
         if (!over) literals(xe);  // the block's last literals (no sequence)
         if (over) return kStored | seg_len;
         const uint32_t nlit = 4u * static_cast<uint32_t>(w.op - (base + 2)) + (w.nb >> 3);
+        nm = nseq;
+        zlit = nlit;
         if (w.nb) *w.op = static_cast<uint32_t>(w.bb);
         uint8_t* sb8 = reinterpret_cast<uint8_t*>(base);
         // Sequences section: Number_of_Sequences, Symbol_Compression_Modes = 0 (all Predefined), then
@@ -556,9 +1139,9 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
         return over ? (kStored | seg_len) : bytes;
     }
     if (!over) {
-        // The block's exact size with the pending literals, counted 4 bytes at a time (a fixed
-        // literal is 8 bits, 9 from 0x90): a segment that would not beat a stored copy (random
-        // data) is never emitted.
+        // The block's size with the pending literals, counted 4 bytes at a time (a fixed literal
+        // is 8 bits, 9 from 0x90): a segment that would not beat a stored copy (random data) is
+        // stored; the others share the span's code (deflate_plan).
         uint32_t a0 = lit, nine = 0;
         for (; a0 < xe && ((a0 + d) & 3u); a0++) nine += byte(a0) >= 144u;
         for (; a0 + 4u <= xe; a0 += 4u) {
@@ -566,23 +1149,18 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
             nine += __builtin_popcount(v & 0x80808080u & ((v << 1) | (v << 2) | (v << 3)));
         }
         for (; a0 < xe; a0++) nine += byte(a0) >= 144u;
-        const uint32_t bits = 32u * static_cast<uint32_t>(w.op - base) + w.nb + 8u * (xe - lit) + nine + 10u;
+        const uint32_t bits = fb + 8u * (xe - lit) + nine + 10u;
         if (((bits + 7u) >> 3) + 4u >= seg_len + 5u) over = true;
     }
-    if (!over) literals(xe);
-    uint32_t bytes = 0;
-    if (!over) {
-        w.put(0u, 7);  // end of block (256: seven zero bits)
-        w.put(0u, 3);  // empty stored block: BFINAL 0, BTYPE 00 ...
-        w.nb = (w.nb + 7u) & ~7u;  // ... padded to a byte
-        w.put(0x0000u, 16);
-        w.put(0xFFFFu, 16);
-        bytes = 4u * static_cast<uint32_t>(w.op - base) + (w.nb >> 3);
-        if (w.nb) *w.op = static_cast<uint32_t>(w.bb);
-        if (bytes >= seg_len + 5u) over = true;
-    }
-    return over ? (kStored | seg_len) : bytes;
+    return over ? (kStored | seg_len) : seg_len;
     }();
+    if constexpr (FMT == kFmtDeflate) {
+        deflate_plan(a, b, lane, span_len, x0, word, nm, hist, reinterpret_cast<uint32_t*>(tab), L, d);
+        return;
+    }
+    if constexpr (FMT == kFmtZstd)
+        if (a.effort >= 1u) word = zstd_huff_literals(a, b, lane, span_len, x0, word, nm, zlit, hist,
+                                                      reinterpret_cast<uint32_t*>(tab), L, d);
     a.seglen[slot] = word;
     // The span's output bytes (stored segments: 5 + n, S2: 3 + n; S2 adds the framing header).
     const uint32_t shdr = FMT == kFmtS2 ? kS2StoredHdr : FMT == kFmtZstd ? kZStoredHdr : 5u;
@@ -837,6 +1415,104 @@ __global__ __launch_bounds__(64) void deflate_copy_kernel(CompArgs a) {
     }
 }
 
+// One wave per span (deflate, gzip, pgzip): the span's blocks as its plan says (deflate_plan),
+// assembled in LDS (segments OR their bits in from their bit offsets), then copied to the
+// chunk's stream.  A stored span is copied from the input directly.
+constexpr uint32_t kOutWords = 8200;  // >= (32768 + 4) / 4 + 2: a coded span is smaller than stored
+__global__ __launch_bounds__(64) void deflate_emit_kernel(CompArgs a) {
+    __shared__ uint32_t L[kLdsWords];
+    __shared__ uint32_t ob[kOutWords];
+    __shared__ uint32_t ctab[kNSym];
+    __shared__ uint32_t lensw[80];
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    const uint32_t total = a.spans[a.n];
+    if (total > a.max_spans || b >= total) return;
+    const uint32_t c = span_chunk(a, b);
+    const uint32_t u = b - a.spans[c];
+    const uint64_t len = a.in_lens[c], sb = static_cast<uint64_t>(u) * kSpan;
+    const uint32_t span_len = static_cast<uint32_t>(len - sb < kSpan ? len - sb : kSpan);
+    uint8_t* dst = a.out + a.out_offs[c] + 4u + (a.gzip ? 10u : 0u) + (a.span_pos[b] - a.span_pos[a.spans[c]]);
+    const uint8_t* in = a.in + a.in_offs[c] + sb;
+    const uint32_t* desc = a.desc + static_cast<uint64_t>(b) * kDescWords;
+    const uint32_t mw = desc[kDescMode], mode = mw & 255u, hb = mw >> 8;
+    if (mode == kModeStored) {  // BFINAL 0, BTYPE 00, LEN, NLEN, the bytes
+        if (lane < 5u) {
+            const uint32_t m = span_len;
+            const uint32_t h = lane == 0 ? 0u : lane == 1 ? (m & 255u) : lane == 2 ? (m >> 8)
+                             : lane == 3 ? (~m & 255u) : ((~m >> 8) & 255u);
+            dst[lane] = static_cast<uint8_t>(h);
+        }
+        wave_copy(dst + 5, in, span_len, lane);
+        return;
+    }
+    const uint32_t nbytes = a.span_bytes[b];
+    const uint32_t d = stage_span(L, in, span_len, lane);
+    uint8_t* lens = reinterpret_cast<uint8_t*>(lensw);
+    for (uint32_t k = lane; k < 80u; k += 64u) lensw[k] = mode == kModeDynamic ? desc[kDescLens + k] : 0u;
+    for (uint32_t k = lane; k < (nbytes + 3u) / 4u + 2u; k += 64u) ob[k] = 0u;
+    __syncthreads();
+    if (mode == kModeFixed)
+        for (uint32_t s = lane; s < kNSym; s += 64u) lens[s] = static_cast<uint8_t>(fixed_len(s));
+    __syncthreads();
+    canon_codes(lens, kNLit, ctab, lane);
+    canon_codes(lens + kNLit, kNDist, ctab + kNLit, lane);
+    __syncthreads();
+    const uint32_t x0 = kSeg * lane;
+    if (x0 < span_len) {
+        const uint32_t xe = span_len - x0 < kSeg ? span_len : x0 + kSeg;
+        const uint32_t inf = desc[kDescInfo + lane], bo = desc[kDescOff + lane];
+        OrBits w{0ull, bo & 31u, bo >> 5, ob};
+        if ((inf & 3u) == kClsCoded) {
+            if (inf & 4u) {  // a run's first segment: the block header
+                w.put(mode == kModeDynamic ? 4u : 2u, 3);  // BFINAL 0, BTYPE 10 / 01
+                if (mode == kModeDynamic) {
+                    for (uint32_t k = 0; k < hb / 32u; k++) w.put(desc[kDescHdr + k], 32);
+                    if (hb & 31u) w.put(desc[kDescHdr + hb / 32u], hb & 31u);
+                }
+            }
+            const uint32_t* tok = reinterpret_cast<const uint32_t*>(a.slots + (static_cast<uint64_t>(b) * 64u + lane) * kSlot);
+            const uint32_t nm = a.seglen[b * 64u + lane];  // the segment's tokens
+            walk_tokens(tok, nm, x0, xe,
+                        [&](uint32_t x) {
+                            const uint32_t cw = ctab[st_byte(L, d, x)];
+                            w.put(cw & 0xFFFFu, cw >> 16);
+                        },
+                        [&](uint32_t, uint32_t n, uint32_t dist) {
+                            const MatchSyms m = match_syms(n, dist);
+                            const uint32_t cl = ctab[m.ls], cd = ctab[kNLit + m.ds];
+                            w.put(cl & 0xFFFFu, cl >> 16);
+                            w.put(m.ev, m.eb);
+                            w.put(cd & 0xFFFFu, cd >> 16);
+                            w.put(m.dev, m.deb);
+                        });
+            if (inf & 8u) {  // a run's last segment: end of block
+                const uint32_t ce = ctab[256];
+                w.put(ce & 0xFFFFu, ce >> 16);
+            }
+            if (inf & 16u) {  // the span's end: an empty stored block (sync flush)
+                w.put(0u, 3);
+                w.pad();
+                w.put(0u, 16);
+                w.put(0xFFFFu, 16);
+            }
+        } else {
+            if (inf & 4u) {  // a stored run: BFINAL 0, BTYPE 00, pad, LEN, NLEN
+                const uint32_t run = inf >> 16;
+                w.put(0u, 3);
+                w.pad();
+                w.put(run, 16);
+                w.put(~run & 0xFFFFu, 16);
+            }
+            uint32_t x = x0;
+            for (; x + 4u <= xe; x += 4u) w.put(st_ld32(L, d, x), 32);
+            for (; x < xe; x++) w.put(st_byte(L, d, x), 8);
+        }
+        w.flush();
+    }
+    __syncthreads();
+    wave_copy(dst, reinterpret_cast<const uint8_t*>(ob), nbytes, lane);
+}
+
 // One thread per chunk: header ID, the empty final block (03 00), the length and the ID kept.
 __global__ __launch_bounds__(256) void deflate_frame_kernel(CompArgs a) {
     const uint32_t c = blockIdx.x * 256u + threadIdx.x;
@@ -944,9 +1620,9 @@ const CompAlgo* find_comp(const char* name) {
 uint64_t align256c(uint64_t x) { return (x + 255u) & ~uint64_t(255); }
 
 struct CompWs {
-    uint64_t spans, crc, span_crc, seglen, span_bytes, span_pos, slots, total;
+    uint64_t spans, crc, span_crc, seglen, span_bytes, span_pos, slots, desc, total;
 };
-constexpr uint64_t kPerSpan = 64u * (compdev::kSlot + 4u) + 4u + 4u + 8u;
+constexpr uint64_t kPerSpan = 64u * (compdev::kSlot + 4u) + 4u + 4u + 8u + 4u * compdev::kDescWords;
 CompWs comp_ws(uint32_t n, uint64_t max_spans) {
     CompWs l{};
     l.spans = 0;
@@ -956,7 +1632,8 @@ CompWs comp_ws(uint32_t n, uint64_t max_spans) {
     l.span_bytes = align256c(l.seglen + max_spans * 64u * 4u);
     l.span_pos = align256c(l.span_bytes + max_spans * 4u);
     l.slots = align256c(l.span_pos + (max_spans + 1u) * 8u);
-    l.total = align256c(l.slots + max_spans * 64u * compdev::kSlot);
+    l.desc = align256c(l.slots + max_spans * 64u * compdev::kSlot);
+    l.total = align256c(l.desc + max_spans * 4u * compdev::kDescWords);
     return l;
 }
 
@@ -1015,6 +1692,7 @@ extern "C" int kcdc_compress_chunks_device(const char* name, const uint8_t* d_da
     a.span_bytes = reinterpret_cast<uint32_t*>(w + l.span_bytes);
     a.span_pos = reinterpret_cast<uint64_t*>(w + l.span_pos);
     a.slots = w + l.slots;
+    a.desc = reinterpret_cast<uint32_t*>(w + l.desc);
     a.n = nchunks;
     a.max_spans = static_cast<uint32_t>(max_spans);
     a.header_id = al->header_id;
@@ -1048,7 +1726,10 @@ extern "C" int kcdc_compress_chunks_device(const char* name, const uint8_t* d_da
             hipLaunchKernelGGL(compdev::lz_spans_kernel<compdev::kFmtDeflate>, grid, dim3(64), 0, st, a);
         }
         hipLaunchKernelGGL(compdev::span_pos_kernel, dim3(1), dim3(1024), 0, st, a);
-        hipLaunchKernelGGL(compdev::deflate_copy_kernel, grid, dim3(64), 0, st, a);
+        if (a.fmt == compdev::kFmtDeflate)
+            hipLaunchKernelGGL(compdev::deflate_emit_kernel, grid, dim3(64), 0, st, a);
+        else
+            hipLaunchKernelGGL(compdev::deflate_copy_kernel, grid, dim3(64), 0, st, a);
         if (a.gzip)
             hipLaunchKernelGGL(compdev::crc_spans_kernel<false>, cgrid, dim3(64 * compdev::kCrcWaves), 0, st, a);
     }

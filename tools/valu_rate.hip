@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <string>
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s\n", hipGetErrorString(e)); return 1; } } while (0)
 
 // One dependent step of chain `a` (b, c: loop-invariant operands).
@@ -89,12 +90,118 @@ int run_all(int cus, uint32_t* out, uint64_t* cyc, std::integer_sequence<int, K.
     return rc;
 }
 
-int main() {
+// The Rabin-Karp batch kernel's hot loop in isolation (a replica of rk_step64 in
+// kcdc_kernels.hip: two chains per lane interleaved byte by byte, 16 mod[] replicas and 32 out[]
+// replicas in LDS, bit-reversed state, the running v_min3 test, outx[] reads two bytes ahead),
+// fed from an LDS step slot (8 ds_read_b128 + 32 v_bfrev per 128 bytes, as the kernel's
+// rk_read_step128) instead of the DMA ring, at the kernel's occupancy (one 512-thread workgroup
+// per CU, 160 KiB LDS) over config 2's rolled bytes (4096 x 4 MiB).  Its wall time is the hot
+// loop's floor on config 2 without HBM, queue, warm-up or tile overheads.
+struct RkL {
+    uint64_t mod[256 * 16];
+    uint64_t out[256 * 32];
+    uint32_t slot[8][32][64];  // per wave: 32 dwords per lane, lane-minor (conflict free)
+};
+__device__ __forceinline__ uint64_t ld64(const char* base, uint32_t a) { return *reinterpret_cast<const uint64_t*>(base + a); }
+__global__ __launch_bounds__(512, 2) void rkloop_kernel(uint64_t steps, uint32_t seed, uint32_t* out) {
+    __shared__ RkL t;
+    for (uint32_t i = threadIdx.x; i < 256u * 16u; i += 512u) t.mod[i] = (i * 0x9E3779B97F4A7C15ull) ^ seed;
+    for (uint32_t i = threadIdx.x; i < 256u * 32u; i += 512u) t.out[i] = (i * 0xC2B2AE3D27D4EB4Full) ^ seed;
+    const uint32_t wv = threadIdx.x / 64u, lane = threadIdx.x % 64u;
+    for (uint32_t i = 0; i < 32u; i++) t.slot[wv][i][lane] = (lane + 1u) * 0x01000193u * (i + seed);
+    __syncthreads();
+    const char* modb = reinterpret_cast<const char*>(t.mod);
+    const char* outb = reinterpret_cast<const char*>(t.out);
+    const uint32_t l8o = (lane & 31u) * 8u, l8m = (lane & 15u) * 8u;
+    auto maddr = [&](uint32_t lo) { return (__builtin_amdgcn_ubfe(lo, 11, 8) << 7) | l8m; };
+    auto oaddr = [&](uint32_t w, int b) { return __builtin_amdgcn_perm(w, l8o, 0x0c0c0000u | ((4u + (3 - b)) << 8)); };
+    auto sel = [](int b) { return 0x00030201u | (static_cast<uint32_t>(7 - b) << 24); };
+    uint32_t ha = seed, la = seed * 3u, hb = seed * 5u, lb = seed * 7u, ma = ~0u, mb = ~0u;
+    uint32_t pa[16], pb[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) pa[i] = pb[i] = seed * (i + 1);
+    for (uint64_t s = 0; s < steps; s++) {
+        uint32_t a[16], b[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            a[i] = __builtin_bitreverse32(t.slot[wv][i][lane]);
+            b[i] = __builtin_bitreverse32(t.slot[wv][16 + i][lane]);
+        }
+        constexpr int W = 2;
+        uint64_t oa[64], ob[64];
+        uint64_t mA = ld64(modb, maddr(la)), mB;
+#pragma unroll
+        for (int i = 0; i < W; i++) oa[i] = ld64(outb, oaddr(pa[i >> 2], i & 3));
+        mB = ld64(modb, maddr(lb));
+#pragma unroll
+        for (int i = 0; i < W; i++) ob[i] = ld64(outb, oaddr(pb[i >> 2], i & 3));
+        uint32_t pha = ~0u, phb = ~0u;
+#pragma unroll
+        for (int x = 0; x < 64; x++) {
+            __builtin_amdgcn_sched_barrier(0);
+            {
+                const uint32_t th = __builtin_amdgcn_perm(a[x >> 2], ha, sel(x & 3));
+                const uint32_t tl = __builtin_amdgcn_alignbit(ha, la, 8);
+                ha = __builtin_amdgcn_bitop3_b32(th, static_cast<uint32_t>(mA >> 32), static_cast<uint32_t>(oa[x] >> 32), 0x96);
+                la = __builtin_amdgcn_bitop3_b32(tl, static_cast<uint32_t>(mA), static_cast<uint32_t>(oa[x]), 0x96);
+                __builtin_amdgcn_sched_barrier(0);
+                if (x + 1 < 64) mA = ld64(modb, maddr(la));
+                if (x + W < 64) oa[x + W] = ld64(outb, oaddr(pa[(x + W) >> 2], (x + W) & 3));
+                __builtin_amdgcn_sched_barrier(0);
+                if (x & 1) ma = min(ma, min(pha, ha));
+                else pha = ha;
+            }
+            {
+                const uint32_t th = __builtin_amdgcn_perm(b[x >> 2], hb, sel(x & 3));
+                const uint32_t tl = __builtin_amdgcn_alignbit(hb, lb, 8);
+                hb = __builtin_amdgcn_bitop3_b32(th, static_cast<uint32_t>(mB >> 32), static_cast<uint32_t>(ob[x] >> 32), 0x96);
+                lb = __builtin_amdgcn_bitop3_b32(tl, static_cast<uint32_t>(mB), static_cast<uint32_t>(ob[x]), 0x96);
+                __builtin_amdgcn_sched_barrier(0);
+                if (x + 1 < 64) mB = ld64(modb, maddr(lb));
+                if (x + W < 64) ob[x + W] = ld64(outb, oaddr(pb[(x + W) >> 2], (x + W) & 3));
+                __builtin_amdgcn_sched_barrier(0);
+                if (x & 1) mb = min(mb, min(phb, hb));
+                else phb = hb;
+            }
+            if ((x & 3) == 3) {
+                asm volatile("" : "+v"(ma));
+                asm volatile("" : "+v"(mb));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            pa[i] = a[i];
+            pb[i] = b[i];
+        }
+    }
+    if ((ma ^ mb ^ ha ^ la ^ hb ^ lb) == 0x12345678u) out[threadIdx.x] = ma;
+}
+
+int main(int argc, char** argv) {
     hipDeviceProp_t p;
     CK(hipGetDeviceProperties(&p, 0));
     uint32_t* out;
     uint64_t* cyc;
     CK(hipMalloc(&out, 4096 * 4));
     CK(hipMalloc(&cyc, 256 * 16 * 8));
+    if (argc > 1 && std::string(argv[1]) == "rk") {
+        const double bytes = 4096.0 * (4 << 20);  // config 2's rolled bytes
+        const int cus = p.multiProcessorCount;
+        const uint64_t steps = static_cast<uint64_t>(bytes / (cus * 512.0) / 128.0);  // 128 bytes per step per lane
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        for (int rep = 0; rep < 4; rep++) {
+            CK(hipEventRecord(e0, 0));
+            hipLaunchKernelGGL(rkloop_kernel, dim3(cus), dim3(512), 0, 0, steps, 7u, out);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            printf("rk hot loop alone: %.3f ms over config 2 (%.0f bytes, %llu 128-byte steps per lane, %d CUs)\n", ms,
+                   bytes, static_cast<unsigned long long>(steps), cus);
+        }
+        return 0;
+    }
     return run_all(p.multiProcessorCount, out, cyc, std::make_integer_sequence<int, 14>{});
 }
