@@ -66,3 +66,13 @@ variants:
 build/writer_bench: tools/writer_bench.cpp include/kcdc.h $(LIB)
 	@mkdir -p build
 	g++ -O2 -std=c++17 -pthread -Iinclude $< -Lkopia_amd -lkcdc -Wl,-rpath,'$$ORIGIN/../kopia_amd' -o $@
+
+# Microbenchmarks run by tools/gpu_session.sh (valu:, membench): standalone HIP programs
+build/valu_rate: tools/valu_rate.hip
+	@mkdir -p build
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) $< -o $@
+build/membench: tools/membench.hip
+	@mkdir -p build
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) $< -o $@
+tools: build/valu_rate build/membench build/writer_bench
+.PHONY: tools

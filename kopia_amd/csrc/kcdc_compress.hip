@@ -1451,11 +1451,17 @@ __global__ __launch_bounds__(64) void deflate_emit_kernel(CompArgs a) {
     for (uint32_t k = lane; k < 80u; k += 64u) lensw[k] = mode == kModeDynamic ? desc[kDescLens + k] : 0u;
     for (uint32_t k = lane; k < (nbytes + 3u) / 4u + 2u; k += 64u) ob[k] = 0u;
     __syncthreads();
+    // The fixed code is canonical over all 288 literal/length symbols (RFC 1951 §3.2.6: 286 and 287
+    // take part in the construction though never sent), so its 9-bit literals start at 0x190; the
+    // distance lengths then sit at byte 288 (ctab[286..287] are overwritten by the distance codes).
+    const uint32_t lit_n = mode == kModeFixed ? kNLit + 2u : kNLit;
+    uint8_t* dlens = lens + lit_n;
     if (mode == kModeFixed)
-        for (uint32_t s = lane; s < kNSym; s += 64u) lens[s] = static_cast<uint8_t>(fixed_len(s));
+        for (uint32_t s = lane; s < lit_n + kNDist; s += 64u)
+            lens[s] = static_cast<uint8_t>(s < lit_n ? (s < kNLit ? fixed_len(s) : 8u) : 5u);
     __syncthreads();
-    canon_codes(lens, kNLit, ctab, lane);
-    canon_codes(lens + kNLit, kNDist, ctab + kNLit, lane);
+    canon_codes(lens, lit_n, ctab, lane);
+    canon_codes(dlens, kNDist, ctab + kNLit, lane);
     __syncthreads();
     const uint32_t x0 = kSeg * lane;
     if (x0 < span_len) {
