@@ -1860,7 +1860,7 @@ __device__ __forceinline__ void rk_step64(const RkCtx& k, uint32_t& ha, uint32_t
             if (x + 1 < 64) mA = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, la));
             if (x + W < 64) oa[x + W] = rk_out(k, pa[(x + W) >> 2], (x + W) & 3);
             __builtin_amdgcn_sched_barrier(0);
-            if (x & 1) ma = min(ma, min(pha, ha));  // v_min3
+            if (x & 1) asm("v_min3_u32 %0, %1, %2, %3" : "=v"(ma) : "v"(ma), "v"(pha), "v"(ha));  // one op per two bytes
             else pha = ha;
         }
         if (ACT_B) {
@@ -1872,12 +1872,8 @@ __device__ __forceinline__ void rk_step64(const RkCtx& k, uint32_t& ha, uint32_t
             if (x + 1 < 64) mB = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, lb));
             if (x + W < 64) ob[x + W] = rk_out(k, pb[(x + W) >> 2], (x + W) & 3);
             __builtin_amdgcn_sched_barrier(0);
-            if (x & 1) mb = min(mb, min(phb, hb));
+            if (x & 1) asm("v_min3_u32 %0, %1, %2, %3" : "=v"(mb) : "v"(mb), "v"(phb), "v"(hb));
             else phb = hb;
-        }
-        if ((x & 3) == 3) {  // keep the running mins sequential (reassociated trees hold ~2 x 64 values)
-            if (ACT_A) asm volatile("" : "+v"(ma));
-            if (ACT_B) asm volatile("" : "+v"(mb));
         }
     }
 }
@@ -2088,9 +2084,18 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
     uint8_t* sl = smslots.b[wave][0];
     const uint32_t sl32 = lds_addr(sl);
     const int64_t mx = static_cast<int64_t>(a.max_size);
+    const uint32_t me = blockIdx.x * kRkWaves + wave;  // this wave's help slot
+    const int64_t rk_cap = kRkLaneMul * static_cast<int64_t>(a.lane_cap);  // lane bytes of an own tile (>= 512)
 
     PStream cur;
     int64_t budget = kNoYield;
+    // Intra-region help as in split_batch_pipe_kernel (hep, hs and the kHs* flags mean the same);
+    // tiles are T = 64 x rk_cap bytes, a help task scans one in two sub-tiles of rk_cap / 2 per lane.
+    uint32_t hep = 0, hs = 0;
+    constexpr uint32_t kHsPub = 1u << 16, kHsNeedPub = 1u << 17, kHsHelped = 1u << 18;
+    hs = kHsNeedPub;
+    auto hK = [&] { return hs & 0xFFu; };
+    auto htile = [&] { return (hs >> 8) & 0xFFu; };
     auto take_blocking = [&](uint32_t t, int64_t backlog_hint, uint32_t claim) -> bool {
         for (;;) {
             int64_t backlog = backlog_hint;
@@ -2100,8 +2105,13 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
                 backlog = static_cast<int64_t>(ht >> 32) - static_cast<int64_t>(t) - 1;
             }
             const uint32_t held = t;
-            const int r = presolve(a, lane, held, cur, kRkWaves, 0u, false);
+            const int r = presolve(a, lane, held, cur, kRkWaves, me, a.help != nullptr && claim == 0xFFFFFFFFu);
             if (r == 0) return false;
+            if (r == 3) {  // a help task; the ticket stays held (in cap, unused by help tasks)
+                cur.cap = held;
+                uniformize(cur);
+                return true;
+            }
             t = 0xFFFFFFFFu;
             if (claim != 0xFFFFFFFFu) {
                 const bool requeued = bcast(claim) == 2u;
@@ -2141,22 +2151,41 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             if (!take_blocking(take_t, take_backlog, take_claim)) return;
             need_take = false;
             issued = false;
+            hs |= kHsNeedPub;
         }
         uniformize(cur);
         if (!pcheck(a, lane, cur, 0xFFFFFFFFu, 5)) return;
+        const bool is_help = (cur.sid & kHelpBit) != 0;
         int64_t lo, hi;
         pregion(a, cur, lo, hi);
-        const RkGeom g = rk_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n, kRkLaneMul * a.lane_cap);
+        const int64_t lcap = is_help ? rk_cap / 2 : rk_cap;
+        const RkGeom g = rk_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n, lcap);
         const int64_t ct = cur.ct, ct_next = ct + kWave * g.L;
         const bool last_of_region = ct_next > hi;
-        const bool budget_out = budget - kWave * g.L <= 0;
+        // A region new to this wave: publish it when it is long enough to share.
+        if ((hs & kHsNeedPub) && !is_help) {
+            const int64_t T = kWave * rk_cap;
+            const uint32_t K = static_cast<uint32_t>((hi - ct + T) / T);
+            hs = 0;
+            if (a.help && K >= kHelpMinTiles && K <= static_cast<uint32_t>(kHelpTiles)) {
+                hep++;
+                hs = kHsPub | K;
+                help_publish(a, lane, me, hep, cur, ct, hi, K, T);
+            }
+        }
+        // The owner's claim on its next tile: an atomic add on its slot's bottom after fill 1's
+        // DMA, its value consumed at fill 2 (after that fill's vmcnt wait, before its DMA), so
+        // no compiler-visible load is in flight across a DMA.
+        const bool claim_next_r = (hs & kHsPub) && !is_help && !last_of_region && htile() + 1u < hK();
+        const bool budget_out = !is_help && !(hs & kHsHelped) && budget - kWave * g.L <= 0;
         bool ends_nocand = false;
-        if (last_of_region) {
+        if (!is_help && last_of_region) {
             const int64_t s2 = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;
             ends_nocand = s2 >= cur.n || s2 + static_cast<int64_t>(a.min_size) - 1 >= cur.n;
         }
-        const bool switching = budget_out || ends_nocand;
+        const bool switching = !is_help && (budget_out || ends_nocand);
         const bool reserve = budget_out && !ends_nocand;
+        const bool claim_next = claim_next_r && !switching;
         uint64_t ht_raw = 0;
         if (switching) ht_raw = qht_add(a, lane, 1);  // the next stream's ticket
         uint32_t ht_lo = static_cast<uint32_t>(ht_raw), ht_hi = static_cast<uint32_t>(ht_raw >> 32);
@@ -2184,6 +2213,15 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
         }
         uint64_t pe_raw = 0;
         bool res_issued = false, next_issued = false, entry_issued = false;
+        bool claim_ok = false, claim_known = !claim_next;
+        uint64_t claim_raw = 0;
+        auto claim_decode = [&]() {  // the claim word before this tile's add (+1 = after it)
+            const uint64_t cw = qht_value(static_cast<uint32_t>(claim_raw), static_cast<uint32_t>(claim_raw >> 32)) + 1ull;
+            const uint32_t top = static_cast<uint32_t>(cw >> 20) & 0xFFFFFu, bot = static_cast<uint32_t>(cw) & 0xFFFFFu;
+            claim_ok = static_cast<uint32_t>(cw >> 40) == hep && bot <= top;
+            if (top < hK()) hs |= kHsHelped;
+            claim_known = true;
+        };
         // After the tile's last fill: the next tile's warm fill, or the next stream's entry.
         auto refill_last = [&]() {
             if (reserve && !res_issued) {  // this stream's ring entry, reserved late
@@ -2193,8 +2231,8 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             if (switching) {
                 pentry_dma(a, lane, tk, sl32);
                 entry_issued = true;
-            } else if (!last_of_region) {  // the next tile has its own geometry
-                const RkGeom gn = rk_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n, kRkLaneMul * a.lane_cap);
+            } else if (!last_of_region && (!claim_next || claim_ok)) {  // the next tile has its own geometry
+                const RkGeom gn = rk_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n, lcap);
                 rk_dma_warm(gn.ld, sl32, ct_next, gn.L, lane);
                 next_issued = true;
             }
@@ -2203,10 +2241,14 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
         // After line fill f is read: issue what the slot takes next (fill f+1, or after the
         // last fill the next tile's warm fill / the next stream's queue entry).
         auto refill = [&](int f) {
+            if (claim_next && f == 2) claim_decode();
             if (f < 2 * g.K)
                 rk_dma_line(g.ld, sl32, ct, g.L, f + 1, lane);
             else
                 refill_last();
+            if (claim_next && f == 1 && lane == 0)
+                claim_raw = __hip_atomic_fetch_add((gu64*)help_claim(a, me), 1ull, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
         };
         // Hit check of one chain's 64 bytes at `rel` from its start (state before: h0/l0):
         // the chain's first candidate in [lo, hi].  The coordinate is formed only here, from
@@ -2234,31 +2276,77 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
         const int64_t c0 = ct + lane * g.L;
         const int64_t found = found_a >= 0 ? c0 + found_a : found_b >= 0 ? c0 + g.L / 2 + found_b : -1;
         // ---- end of tile
+        if (!claim_known) {  // one-line tiles (K = 1) consume the claim here
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            claim_decode();
+        }
         if (reserve && !res_issued) {
             pe_raw = qht_add(a, lane, 1ull << 32);
             res_issued = true;
         }
         const uint64_t hit = __ballot(found >= 0);
+        if (is_help) {
+            bool done = true;
+            if (hit || last_of_region) {  // post the tile's first candidate to its owner's row
+                int64_t f = -1;
+                if (hit) f = static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, __builtin_ctzll(hit)))));
+                help_post(a, lane, static_cast<uint32_t>(cur.cb), cur.epoch, static_cast<uint32_t>(cur.cnt), cur.s, f);
+            } else {  // the next sub-tile (prefetched), unless the owner has closed the region
+                const uint64_t w = ld_agent64(help_claim(a, static_cast<uint32_t>(cur.cb)));
+                done = static_cast<uint32_t>(qht_value(static_cast<uint32_t>(w), static_cast<uint32_t>(w >> 32)) >> 40) !=
+                       cur.epoch;
+            }
+            if (!done) {
+                cur.ct = ct_next;
+                issued = next_issued;
+                continue;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the post, or a dropped prefetch
+            need_take = true;
+            take_t = static_cast<uint32_t>(cur.cap);
+            take_backlog = 0;
+            take_claim = 0xFFFFFFFFu;
+            continue;
+        }
         bool region_changed = true;
-        bool live;
         const int64_t forced = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;
+        int64_t cut = -1;  // this region's cut, once known
         if (hit) {
             const int first = __builtin_ctzll(hit);
             const int64_t f = static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, first))));
-            const int64_t next = f - cur.off0 + 1;
-            emit_cut(a, cur, lane, next);
-            cur.s = next;
-            cur.ct = -1;
+            cut = f - cur.off0 + 1;
         } else if (last_of_region) {  // forced cut at max size (splitter_rabinkarp64.go:60-64) or the end
-            emit_cut(a, cur, lane, forced);
-            cur.s = forced;
-            cur.ct = -1;
+            cut = forced;
+        } else if (claim_next && !claim_ok) {  // the helpers hold the rest of the region
+            const int64_t T = kWave * rk_cap;
+            const int64_t ct0 = ct - static_cast<int64_t>(htile()) * T;  // the published tile 0
+            const int64_t r = help_wait(a, lane, me, hep, htile() + 1u, hK(), ct0);
+            if (r >= 0) {
+                cut = r - cur.off0 + 1;
+            } else if (r == -1) {
+                cut = forced;
+            } else {  // a tile still pending: scan on from it, unshared
+                cur.ct = ct0 + (-2 - r) * T;
+                help_close(a, lane, me, hep);
+                hs = 0;
+                region_changed = false;
+            }
         } else {
             cur.ct = ct_next;
+            hs += 1u << 8;  // htile++
             budget -= kWave * g.L;
             region_changed = false;
         }
-        live = pstream_region(a, cur, lane);
+        if (cut >= 0) {
+            emit_cut(a, cur, lane, cut);
+            cur.s = cut;
+            cur.ct = -1;
+        }
+        if (region_changed) {
+            if (hs & kHsPub) help_close(a, lane, me, hep);
+            hs = kHsNeedPub;
+        }
+        const bool live = pstream_region(a, cur, lane);
         if (!live && lane == 0) {
             a.counts[cur.sid] = cur.cnt;
             add_agent(a.queue + kQDone, 1u);
@@ -2268,6 +2356,8 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             if (next_issued && region_changed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stale prefetch
             continue;
         }
+        if (hs & kHsPub) help_close(a, lane, me, hep);  // a yielded region is not ours to share any more
+        hs = kHsNeedPub;
         if (reserve) {
             const uint32_t pe = static_cast<uint32_t>(
                 qht_value(static_cast<uint32_t>(pe_raw), static_cast<uint32_t>(pe_raw >> 32)) >> 32);
@@ -3431,7 +3521,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         const unsigned need = (s.nstreams + wg_waves - 1) / wg_waves;
         // The buzhash pipe kernel takes the whole chip even for a few streams: the waves without
         // a stream help scan the owners' regions (help slots).
-        const bool helpers = algo.kind == kBuzhash && !g_test.no_help;
+        const bool helpers = (algo.kind == kBuzhash || algo.kind == kRabinKarp) && !g_test.no_help;
         unsigned grid = helpers || need >= cus ? cus : need;
         if (grid > dev::kMaxPipeGrid) grid = dev::kMaxPipeGrid;  // one claim flag per workgroup
         uint64_t ring = 1;

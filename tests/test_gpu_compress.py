@@ -133,16 +133,19 @@ def test_splitter_chunks_of_mixed_stream(name, gpu):
 
 @pytest.mark.parametrize("name", ["deflate-default", "gzip"])
 def test_random_stream_is_stored(name, gpu):
-    """Config-2 bytes (uniform PRNG): every segment falls back to a stored block, the output is
-    the bound minus the unused trailer slack, and the ID is NoCompression."""
+    """Config-2 bytes (uniform PRNG): every 32 KiB span falls back to ONE stored block (5 + 32768
+    bytes: a span whose code would not beat a stored copy is stored whole), the stream is the header
+    ID, those blocks and the final empty block (plus the gzip member's 18 bytes), and the ID is
+    NoCompression."""
     host = coracle.gen_stream(0x6B6F706961, 0, 8 << 20)
     lens = [1 << 20] * 8
     offs = [i << 20 for i in range(8)]
     out, oo, ol, ids = _compress(name, host, offs, lens, gpu)
     _check(name, host, offs, lens, out, oo, ol, ids)
     assert not ids.any()
-    frame = 0 if name in GZIP else 18  # the bound leaves room for a gzip member's header and trailer
-    assert all(int(x) == kc.compress_bound(1 << 20) - frame for x in ol)
+    spans = (1 << 20) // 32768
+    want = 4 + spans * (5 + 32768) + 2 + (18 if name in GZIP else 0)
+    assert all(int(x) == want for x in ol), (want, ol)
 
 
 def test_workspace_too_small_writes_no_output(gpu):

@@ -17,6 +17,7 @@
 #   valu:ARGS        build/valu_rate ARGS (tools/valu_rate.hip: the VALU rate table, or "rk": the
 #                    Rabin-Karp hot loop alone over config 2's bytes)
 #   sq:TAG:ARGS      SQ counters (VALU/LDS/wait) of bench.py ARGS, one --pmc pass
+#   trace:ARGS       tools/trace_pipe.py build/libkcdc_trace.so ARGS (per-wave timeline of the batch kernel)
 #   compress:NAMES   tools/compress_bench.py --gib 4 for each compressor name (commas between names)
 set -u
 OUT=gpurun_out/${1:?usage: tools/gpu_session.sh OUT step...}
@@ -65,6 +66,10 @@ for step in "$@"; do
       a=$(args "${step#valu:}"); t=$(echo "$a" | tr -c 'A-Za-z0-9' '_')
       timeout -k 10 300 ./build/valu_rate $a > "$OUT/valu_$t.log" 2>&1 || exit $?
       tail -4 "$OUT/valu_$t.log" ;;
+    trace:*)
+      a=$(args "${step#trace:}"); t=$(echo "$a" | tr -c 'A-Za-z0-9' '_')
+      timeout -k 10 300 python -u tools/trace_pipe.py build/libkcdc_trace.so $a > "$OUT/trace_$t.log" 2>&1 || exit $?
+      tail -12 "$OUT/trace_$t.log" ;;
     compress:*)
       for nm in $(args "${step#compress:}"); do
         timeout -k 10 300 python -u tools/compress_bench.py --gib 4 --iters 3 --name "$nm" > "$OUT/compress_$nm.log" 2>&1 || exit $?

@@ -148,7 +148,7 @@ __global__ __launch_bounds__(512, 2) void rkloop_kernel(uint64_t steps, uint32_t
                 if (x + 1 < 64) mA = ld64(modb, maddr(la));
                 if (x + W < 64) oa[x + W] = ld64(outb, oaddr(pa[(x + W) >> 2], (x + W) & 3));
                 __builtin_amdgcn_sched_barrier(0);
-                if (x & 1) ma = min(ma, min(pha, ha));
+                if (x & 1) asm("v_min3_u32 %0, %1, %2, %3" : "=v"(ma) : "v"(ma), "v"(pha), "v"(ha));
                 else pha = ha;
             }
             {
@@ -160,12 +160,8 @@ __global__ __launch_bounds__(512, 2) void rkloop_kernel(uint64_t steps, uint32_t
                 if (x + 1 < 64) mB = ld64(modb, maddr(lb));
                 if (x + W < 64) ob[x + W] = ld64(outb, oaddr(pb[(x + W) >> 2], (x + W) & 3));
                 __builtin_amdgcn_sched_barrier(0);
-                if (x & 1) mb = min(mb, min(phb, hb));
+                if (x & 1) asm("v_min3_u32 %0, %1, %2, %3" : "=v"(mb) : "v"(mb), "v"(phb), "v"(hb));
                 else phb = hb;
-            }
-            if ((x & 3) == 3) {
-                asm volatile("" : "+v"(ma));
-                asm volatile("" : "+v"(mb));
             }
         }
 #pragma unroll
@@ -185,7 +181,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&out, 4096 * 4));
     CK(hipMalloc(&cyc, 256 * 16 * 8));
     if (argc > 1 && std::string(argv[1]) == "rk") {
-        const double bytes = 4096.0 * (4 << 20);  // config 2's rolled bytes
+        const double bytes = 6.7429e9;  // config 2's rolled bytes under 4M-RABINKARP
         const int cus = p.multiProcessorCount;
         const uint64_t steps = static_cast<uint64_t>(bytes / (cus * 512.0) / 128.0);  // 128 bytes per step per lane
         hipEvent_t e0, e1;
