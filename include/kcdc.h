@@ -397,6 +397,9 @@ int kcdc_test_occupy(uint32_t nwg, uint32_t usec, void* hip_stream);
 #define KCDC_TEST_STAT_STEALS 3
 #define KCDC_TEST_STAT_HELPS 4
 int64_t kcdc_test_queue_stat(int32_t key);
+/* Test hook: copy bytes [off, off + n) of the last pipelined launch's queue workspace (queue
+ * header, stream ring, help slots) to host memory at dst; 0 or a negative error. */
+int kcdc_test_ws_copy(void* dst, uint64_t off, uint64_t n);
 /* Requests the resident scan server has answered in this process (private streaming handles use
  * it while exactly one private handle is open). */
 int64_t kcdc_test_server_requests(void);

@@ -91,6 +91,7 @@ _SIGS = {
     "kcdc_test_set": (C.c_int, [C.c_int32, C.c_int64]),
     "kcdc_test_occupy": (C.c_int, [C.c_uint32, C.c_uint32, _P]),
     "kcdc_test_queue_stat": (C.c_int64, [C.c_int32]),
+    "kcdc_test_ws_copy": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64]),
     "kcdc_test_server_requests": (C.c_int64, []),
     "kcdc_hash_algorithms": (C.c_int, [C.POINTER(C.c_char_p), C.c_int]),
     "kcdc_hash_size": (C.c_int, [C.c_char_p]),

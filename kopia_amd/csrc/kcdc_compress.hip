@@ -732,14 +732,15 @@ __device__ __forceinline__ void deflate_plan(const CompArgs& a, uint32_t b, uint
 // zstd literals through one Huffman code per span (RFC 8878 §3.1.1.3.1, §4.2): after the parse
 // (each coded segment a Compressed_Block with Raw_Literals: block header at slot + 3, literals
 // header at + 6, the literals from + 8, the sequences section after them), the span's literal
-// counts give a code of <= 11 bits.  The first segment whose literals shrink with it, tree
-// description included, carries the tree (Compressed_Literals_Block, direct weights: the span's
-// largest literal must be <= 128); the later segments whose literals shrink reuse it
-// (Treeless_Literals_Block, the frame's previous table); the others keep raw literals.  Single
-// stream, 10-bit sizes (a segment has <= 512 literals); the stream holds the literals last to
-// first (the decoder reads it backwards), then a 1 bit.  Literal bytes come from the staged span;
-// the stream overwrites the raw literals (it is shorter) and the sequences section moves down
-// behind it.  Returns the segment's new length word.  S: LDS scratch (the match tables).
+// counts give a code of <= 11 bits.  The first segment whose literals shrink with it carries the
+// tree (Compressed_Literals_Block, direct weights: the span's largest literal must be <= 128); the
+// later segments whose literals shrink reuse it (Treeless_Literals_Block, the frame's previous
+// table); the others keep raw literals.  The code is used when what those segments save exceeds the
+// tree description.  Single stream, 10-bit sizes (a segment has <= 512 literals); the stream holds
+// the literals last to first (the decoder reads it backwards), then a 1 bit.  Literal bytes come
+// from the staged span; the sequences section moves to its new place first (the carrier's block
+// may grow, within its slot), then the tree and stream replace the raw literals.  Returns the
+// segment's new length word.  S: LDS scratch (the match tables).
 // The reference's zstd encoder (klauspost/compress/zstd, compressor_zstd.go:15-18) Huffman-codes
 // literals the same way (one table per block, reused by later blocks when that is smaller).
 __device__ __forceinline__ uint32_t zstd_huff_literals(const CompArgs& a, uint32_t b, uint32_t lane, uint32_t span_len,
@@ -807,15 +808,31 @@ __device__ __forceinline__ uint32_t zstd_huff_literals(const CompArgs& a, uint32
     };
     if (coded && nlit) for_lits([&](uint32_t x) { bits += zc[st_byte(L, d, x)] >> 16; });
     const uint32_t sbytes = (bits + 7u) / 8u;
-    const bool can_tree = coded && nlit && 3u + tsz + sbytes < 2u + nlit;
-    const uint64_t cm = __ballot(can_tree);
+    // Bytes a Treeless literals section saves against the raw one (3-byte header + stream vs
+    // 2-byte header + the literals).  The tree is paid once, by the first segment that saves
+    // (the carrier), and pays off over the span: Huffman literals are used when the savings of all
+    // segments exceed the tree.  The carrier's block must still fit its slot (it may grow).
+    const uint32_t old_total = word;            // block header + content bytes, from slot + 3
+    const uint32_t qs = coded ? old_total - 5u - nlit : 0u;  // the sequences section, at slot + 8 + nlit
+    const int32_t save = coded && nlit ? static_cast<int32_t>(2u + nlit) - static_cast<int32_t>(3u + sbytes) : 0;
+    const bool fits = 6u + tsz + sbytes + qs + kZOff <= kSlot;
+    const uint64_t cm = __ballot(save > 0 && fits);
     if (!cm) return word;
     const uint32_t carrier = static_cast<uint32_t>(__builtin_ctzll(cm));
-    const uint32_t use = lane == carrier ? 2u : (lane > carrier && coded && nlit && 3u + sbytes < 2u + nlit) ? 3u : 0u;
+    int32_t tot = save > 0 && lane >= carrier ? save : 0;  // what the carrier and the segments after it save
+    for (uint32_t o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, static_cast<int>(o), 64);
+    if (tot <= static_cast<int32_t>(tsz)) return word;
+    const uint32_t use = lane == carrier ? 2u : (lane > carrier && save > 0) ? 3u : 0u;
     if (!use) return word;
-    const uint32_t old_total = word;               // block header + content bytes, from slot + 3
-    const uint32_t qs = old_total - 5u - nlit;     // the sequences section, at slot + 8 + nlit
     const uint32_t ts = use == 2u ? tsz : 0u;
+    {  // the sequences section to its new place (memmove: the carrier's section may grow)
+        const uint8_t* src = sb8 + 8u + nlit;
+        uint8_t* dst = sb8 + 9u + ts + sbytes;
+        if (dst > src)
+            for (uint32_t i = qs; i-- > 0u;) dst[i] = src[i];
+        else
+            for (uint32_t i = 0; i < qs; i++) dst[i] = src[i];
+    }
     uint8_t* op = sb8 + 9u + ts;
     if (use == 2u) {  // direct weights: W = maxb + 1 - bits (0: unused), two per byte, high nibble first
         sb8[9] = static_cast<uint8_t>(127u + top);
@@ -855,8 +872,6 @@ __device__ __forceinline__ uint32_t zstd_huff_literals(const CompArgs& a, uint32
     sb8[6] = static_cast<uint8_t>(lh);
     sb8[7] = static_cast<uint8_t>(lh >> 8);
     sb8[8] = static_cast<uint8_t>(lh >> 16);
-    const uint8_t* src = sb8 + 8u + nlit;
-    for (uint32_t i = 0; i < qs; i++) op[i] = src[i];  // the sequences section, moved down
     const uint32_t total = 6u + ts + sbytes + qs;
     const uint32_t hdr = ((total - 3u) << 3) | (2u << 1);  // Compressed_Block, not the last
     sb8[3] = static_cast<uint8_t>(hdr);
@@ -1001,6 +1016,20 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
                 if (n2 > n) {
                     n = n2;
                     q = c2;
+                }
+            }
+            // the latest candidates of the previous segments (their lanes' tables: any entry is an
+            // earlier position of this hash, whatever those lanes have reached): effort 1 one
+            // segment back, effort 2 three
+            const uint32_t back = a.effort >= 2u ? 3u : 1u;
+            for (uint32_t k = 1; k <= back && k <= lane; k++) {
+                const uint32_t c3 = tab[h * 64u + lane - k];
+                if (c3 != 0xFFFFu && c3 != q) {
+                    const uint32_t n3 = match_len(c3, xx, v);
+                    if (n3 > n) {
+                        n = n3;
+                        q = c3;
+                    }
                 }
             }
         }
@@ -1313,11 +1342,25 @@ __device__ __forceinline__ void wave_copy(uint8_t* dst, const uint8_t* src, uint
     const uint32_t head = min(n, static_cast<uint32_t>((4u - (reinterpret_cast<uintptr_t>(dst) & 3u)) & 3u));
     if (lane < head) dst[lane] = src[lane];
     const uint32_t m = (n - head) >> 2;
-    uint32_t* dw = reinterpret_cast<uint32_t*>(dst + head);
+    uint32_t* __restrict__ dw = reinterpret_cast<uint32_t*>(dst + head);
     const uint8_t* s0 = src + head;
     const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(s0) & 3u);
-    const uint32_t* sw = reinterpret_cast<const uint32_t*>(s0 - sh);
-    for (uint32_t i = lane; i < m; i += 64u) {
+    const uint32_t* __restrict__ sw = reinterpret_cast<const uint32_t*>(s0 - sh);
+    // 8 words per lane in flight per round (loads first, then stores): one dependent load per
+    // 256 bytes left a copy latency-bound at the emit kernel's two waves per CU
+    constexpr uint32_t kU = 8;
+    uint32_t i = lane;
+    for (; i + 64u * (kU - 1u) < m; i += 64u * kU) {
+        uint32_t w0[kU], w1[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            w0[u] = sw[i + 64u * u];
+            w1[u] = sh ? sw[i + 64u * u + 1u] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) dw[i + 64u * u] = __builtin_amdgcn_alignbit(w1[u], w0[u], 8u * sh);
+    }
+    for (; i < m; i += 64u) {
         const uint32_t w0 = sw[i];
         const uint32_t w1 = sh ? sw[i + 1] : 0u;
         dw[i] = __builtin_amdgcn_alignbit(w1, w0, 8u * sh);
@@ -1435,16 +1478,7 @@ __global__ __launch_bounds__(64) void deflate_emit_kernel(CompArgs a) {
     const uint8_t* in = a.in + a.in_offs[c] + sb;
     const uint32_t* desc = a.desc + static_cast<uint64_t>(b) * kDescWords;
     const uint32_t mw = desc[kDescMode], mode = mw & 255u, hb = mw >> 8;
-    if (mode == kModeStored) {  // BFINAL 0, BTYPE 00, LEN, NLEN, the bytes
-        if (lane < 5u) {
-            const uint32_t m = span_len;
-            const uint32_t h = lane == 0 ? 0u : lane == 1 ? (m & 255u) : lane == 2 ? (m >> 8)
-                             : lane == 3 ? (~m & 255u) : ((~m >> 8) & 255u);
-            dst[lane] = static_cast<uint8_t>(h);
-        }
-        wave_copy(dst + 5, in, span_len, lane);
-        return;
-    }
+    if (mode == kModeStored) return;  // deflate_stored_kernel
     const uint32_t nbytes = a.span_bytes[b];
     const uint32_t d = stage_span(L, in, span_len, lane);
     uint8_t* lens = reinterpret_cast<uint8_t*>(lensw);
@@ -1517,6 +1551,29 @@ __global__ __launch_bounds__(64) void deflate_emit_kernel(CompArgs a) {
     }
     __syncthreads();
     wave_copy(dst, reinterpret_cast<const uint8_t*>(ob), nbytes, lane);
+}
+
+// One wave per span whose plan is one stored block (random data): BFINAL 0, BTYPE 00, LEN, NLEN,
+// the bytes.  Apart from deflate_emit_kernel, whose 67 KiB of LDS allow two waves per CU: at that
+// occupancy the copy of an incompressible batch ran at ~130 GB/s.
+__global__ __launch_bounds__(64) void deflate_stored_kernel(CompArgs a) {
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    const uint32_t total = a.spans[a.n];
+    if (total > a.max_spans || b >= total) return;
+    const uint32_t* desc = a.desc + static_cast<uint64_t>(b) * kDescWords;
+    if ((desc[kDescMode] & 255u) != kModeStored) return;
+    const uint32_t c = span_chunk(a, b);
+    const uint32_t u = b - a.spans[c];
+    const uint64_t len = a.in_lens[c], sb = static_cast<uint64_t>(u) * kSpan;
+    const uint32_t span_len = static_cast<uint32_t>(len - sb < kSpan ? len - sb : kSpan);
+    uint8_t* dst = a.out + a.out_offs[c] + 4u + (a.gzip ? 10u : 0u) + (a.span_pos[b] - a.span_pos[a.spans[c]]);
+    if (lane < 5u) {
+        const uint32_t m = span_len;
+        const uint32_t h = lane == 0 ? 0u : lane == 1 ? (m & 255u) : lane == 2 ? (m >> 8)
+                         : lane == 3 ? (~m & 255u) : ((~m >> 8) & 255u);
+        dst[lane] = static_cast<uint8_t>(h);
+    }
+    wave_copy(dst + 5, a.in + a.in_offs[c] + sb, span_len, lane);
 }
 
 // One thread per chunk: header ID, the empty final block (03 00), the length and the ID kept.
@@ -1732,9 +1789,10 @@ extern "C" int kcdc_compress_chunks_device(const char* name, const uint8_t* d_da
             hipLaunchKernelGGL(compdev::lz_spans_kernel<compdev::kFmtDeflate>, grid, dim3(64), 0, st, a);
         }
         hipLaunchKernelGGL(compdev::span_pos_kernel, dim3(1), dim3(1024), 0, st, a);
-        if (a.fmt == compdev::kFmtDeflate)
+        if (a.fmt == compdev::kFmtDeflate) {
             hipLaunchKernelGGL(compdev::deflate_emit_kernel, grid, dim3(64), 0, st, a);
-        else
+            hipLaunchKernelGGL(compdev::deflate_stored_kernel, grid, dim3(64), 0, st, a);
+        } else
             hipLaunchKernelGGL(compdev::deflate_copy_kernel, grid, dim3(64), 0, st, a);
         if (a.gzip)
             hipLaunchKernelGGL(compdev::crc_spans_kernel<false>, cgrid, dim3(64 * compdev::kCrcWaves), 0, st, a);

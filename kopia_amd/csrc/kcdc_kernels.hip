@@ -853,6 +853,21 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t pring_rsrc(const BatchArgs& a)
     return __builtin_amdgcn_make_buffer_rsrc(a.ring, static_cast<short>(0),
                                              static_cast<int>((a.ring_mask + 1u) * kPEntryStride), 0x00020000);
 }
+#ifndef KCDC_TICKET_TRACE
+#define KCDC_TICKET_TRACE 0
+#endif
+// Debug builds (-DKCDC_TICKET_TRACE=1): who took / consumed ticket t, in the unused 8th granule of
+// ring entry t (word 0 taker, 1 consumer, 2 last help taken on it, 3 re-presented), for
+// tools/batch_probe.py post-mortems.  Compiled out of the product.
+__device__ __forceinline__ void tk_trace(const BatchArgs& a, int lane, uint32_t t, uint32_t word, uint32_t v) {
+#if KCDC_TICKET_TRACE
+    if (lane == 0 && t != 0xFFFFFFFFu)
+        reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.ring) + static_cast<size_t>(t & a.ring_mask) * kPEntryStride +
+                                    112)[word] = v;
+#else
+    (void)a; (void)lane; (void)t; (void)word; (void)v;
+#endif
+}
 // Every lane loads (lane & 7): no divergent load, so no copy of the result that would
 // make the compiler wait for it early.
 __device__ __forceinline__ u32x4 pentry_load(const BatchArgs& a, int lane, uint32_t e) {
@@ -1220,8 +1235,12 @@ __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, u
     for (uint32_t spin = 0;; spin++) {
         const u32x4 v = pentry_load(a, lane, t);
         if (pentry_ok(v, lane, t)) {
-            if (static_cast<uint32_t>(__builtin_amdgcn_readlane(v.w, 0)) == kTombstone) return 2;
+            if (static_cast<uint32_t>(__builtin_amdgcn_readlane(v.w, 0)) == kTombstone) {
+                tk_trace(a, lane, t, 1, 0x20000u | me);
+                return 2;
+            }
             pentry_decode(st, v);
+            tk_trace(a, lane, t, 1, 0x10000u | me);
             return 1;
         }
         uint32_t stop = 0;
@@ -1235,6 +1254,9 @@ __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, u
                 stop = 1;
             } else if (idle + 1u >= spin_cap) {  // this poll included: a cap of 1 gives up at once (test knob)
                 add_agent(a.queue + kQErr, 1u);
+                // post-mortem (tools/batch_probe.py): the ticket this wave gave up on, in the spare
+                // words of its help slot's claim line
+                if (a.help && me < a.help_waves) help_claim(a, me)[1] = 0x100000000ull | t;
                 stop = 1;
             }
         }
@@ -1246,7 +1268,10 @@ __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, u
         }
         if (can_help && spin % kHelpEvery == kHelpEvery - 1) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (help_find(a, lane, me, spin / kHelpEvery, st)) return 3;
+            if (help_find(a, lane, me, spin / kHelpEvery, st)) {
+                tk_trace(a, lane, t, 2, 0x40000u | me);
+                return 3;
+            }
         }
         // back off while nothing finishes: ~1,000 waiting waves polling two words every 0.5 us
         // load the L2 channel of the done counter in the batch's tail
@@ -2075,6 +2100,9 @@ __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int 
 // Rabin-Karp lane segments: twice the buzhash cap (warm-up vs tile overshoot; 2 vs 1: 4M 2.542 vs
 // 2.554 ms, 128K 5.536 vs 5.643 ms, profiles/r03/rk/kbench_lmul_*.log)
 constexpr int64_t kRkLaneMul = 2;
+#ifndef KCDC_RK_HELP_MODE
+#define KCDC_RK_HELP_MODE 0
+#endif
 __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk_kernel(BatchArgs a) {
     __shared__ RkTables smt;
     __shared__ RkSlots smslots;
@@ -2103,6 +2131,9 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
                 const uint64_t ht = qht_take(a, lane, 1);
                 t = static_cast<uint32_t>(ht);
                 backlog = static_cast<int64_t>(ht >> 32) - static_cast<int64_t>(t) - 1;
+                tk_trace(a, lane, t, 0, 0x20000u | me);
+            } else {
+                tk_trace(a, lane, t, 3, 0x50000u | me);
             }
             const uint32_t held = t;
             const int r = presolve(a, lane, held, cur, kRkWaves, me, a.help != nullptr && claim == 0xFFFFFFFFu);
@@ -2167,7 +2198,7 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             const int64_t T = kWave * rk_cap;
             const uint32_t K = static_cast<uint32_t>((hi - ct + T) / T);
             hs = 0;
-            if (a.help && K >= kHelpMinTiles && K <= static_cast<uint32_t>(kHelpTiles)) {
+            if (KCDC_RK_HELP_MODE >= 1 && a.help && K >= kHelpMinTiles && K <= static_cast<uint32_t>(kHelpTiles)) {
                 hep++;
                 hs = kHsPub | K;
                 help_publish(a, lane, me, hep, cur, ct, hi, K, T);
@@ -2176,8 +2207,8 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
         // The owner's claim on its next tile: an atomic add on its slot's bottom after fill 1's
         // DMA, its value consumed at fill 2 (after that fill's vmcnt wait, before its DMA), so
         // no compiler-visible load is in flight across a DMA.
-        const bool claim_next_r = (hs & kHsPub) && !is_help && !last_of_region && htile() + 1u < hK();
-        const bool budget_out = !is_help && !(hs & kHsHelped) && budget - kWave * g.L <= 0;
+        const bool claim_next_r = KCDC_RK_HELP_MODE >= 2 && (hs & kHsPub) && !is_help && !last_of_region && htile() + 1u < hK();
+        const bool budget_out = !is_help && (KCDC_RK_HELP_MODE == 3 || !(hs & kHsHelped)) && budget - kWave * g.L <= 0;
         bool ends_nocand = false;
         if (!is_help && last_of_region) {
             const int64_t s2 = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;
@@ -2210,13 +2241,19 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             const uint64_t ht = qht_value(ht_lo, ht_hi);
             tk = static_cast<uint32_t>(ht);
             nbacklog = static_cast<int64_t>(ht >> 32) + (reserve ? 1 : 0) - static_cast<int64_t>(tk) - 1;
+            tk_trace(a, lane, tk, 0, 0x10000u | me);
         }
         uint64_t pe_raw = 0;
         bool res_issued = false, next_issued = false, entry_issued = false;
         bool claim_ok = false, claim_known = !claim_next;
         uint64_t claim_raw = 0;
         auto claim_decode = [&]() {  // the claim word before this tile's add (+1 = after it)
+#if KCDC_RK_HELP_MODE == 5
+            const uint64_t raw5 = ld_agent64(help_claim(a, me));
+            const uint64_t cw = qht_value(static_cast<uint32_t>(raw5), static_cast<uint32_t>(raw5 >> 32));
+#else
             const uint64_t cw = qht_value(static_cast<uint32_t>(claim_raw), static_cast<uint32_t>(claim_raw >> 32)) + 1ull;
+#endif
             const uint32_t top = static_cast<uint32_t>(cw >> 20) & 0xFFFFFu, bot = static_cast<uint32_t>(cw) & 0xFFFFFu;
             claim_ok = static_cast<uint32_t>(cw >> 40) == hep && bot <= top;
             if (top < hK()) hs |= kHsHelped;
@@ -2246,9 +2283,14 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
                 rk_dma_line(g.ld, sl32, ct, g.L, f + 1, lane);
             else
                 refill_last();
+#if KCDC_RK_HELP_MODE == 5
+            if (claim_next && f == 1 && lane == 0)
+                __hip_atomic_fetch_add((gu64*)help_claim(a, me), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
             if (claim_next && f == 1 && lane == 0)
                 claim_raw = __hip_atomic_fetch_add((gu64*)help_claim(a, me), 1ull, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
+#endif
         };
         // Hit check of one chain's 64 bytes at `rel` from its start (state before: h0/l0):
         // the chain's first candidate in [lo, hi].  The coordinate is formed only here, from
@@ -2320,7 +2362,8 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
         } else if (claim_next && !claim_ok) {  // the helpers hold the rest of the region
             const int64_t T = kWave * rk_cap;
             const int64_t ct0 = ct - static_cast<int64_t>(htile()) * T;  // the published tile 0
-            const int64_t r = help_wait(a, lane, me, hep, htile() + 1u, hK(), ct0);
+            const int64_t r = KCDC_RK_HELP_MODE == 4 ? -2 - static_cast<int64_t>(htile() + 1u)
+                                                     : help_wait(a, lane, me, hep, htile() + 1u, hK(), ct0);
             if (r >= 0) {
                 cut = r - cur.off0 + 1;
             } else if (r == -1) {
@@ -2375,6 +2418,7 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
                 pentry_decode(nx, ev);
                 uniformize(nx);
                 if (!pcheck(a, lane, nx, tk, 2)) return;
+                tk_trace(a, lane, tk, 1, 0x30000u | me);
                 cur = nx;
                 budget = pipe_quantum(nbacklog);
                 took = true;
@@ -3521,7 +3565,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         const unsigned need = (s.nstreams + wg_waves - 1) / wg_waves;
         // The buzhash pipe kernel takes the whole chip even for a few streams: the waves without
         // a stream help scan the owners' regions (help slots).
-        const bool helpers = (algo.kind == kBuzhash || algo.kind == kRabinKarp) && !g_test.no_help;
+        const bool helpers = (algo.kind == kBuzhash || (KCDC_RK_HELP_MODE > 0 && algo.kind == kRabinKarp)) && !g_test.no_help;
         unsigned grid = helpers || need >= cus ? cus : need;
         if (grid > dev::kMaxPipeGrid) grid = dev::kMaxPipeGrid;  // one claim flag per workgroup
         uint64_t ring = 1;
@@ -3992,6 +4036,18 @@ extern "C" int64_t kcdc_test_queue_stat(int32_t key) {
     const hipError_t e = hipMemcpy(&v, g_test.last_ws + 4 * word, 4, hipMemcpyDeviceToHost);
     (void)hipSetDevice(prev);
     return e == hipSuccess ? static_cast<int64_t>(v) : hip_fail(e, "queue statistic");
+}
+
+// Test hook: bytes [off, off + n) of the last pipelined launch's queue workspace (header, ring,
+// help slots) to host memory, for post-mortems of a launch (tools/batch_probe.py).
+extern "C" int kcdc_test_ws_copy(void* dst, uint64_t off, uint64_t n) {
+    if (!g_test.last_ws) return set_error(-22, "no pipelined batch launch yet");
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(g_test.last_dev);
+    const hipError_t e = hipMemcpy(dst, g_test.last_ws + off, n, hipMemcpyDeviceToHost);
+    (void)hipSetDevice(prev);
+    return e == hipSuccess ? 0 : hip_fail(e, "workspace copy");
 }
 
 extern "C" int kcdc_test_occupy(uint32_t nwg, uint32_t usec, void* stream) {

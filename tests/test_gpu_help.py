@@ -1,9 +1,10 @@
-"""GPU: intra-region help in the buzhash batch kernel (split_batch_pipe_kernel).
+"""GPU: intra-region help in the batch kernels (split_batch_pipe_kernel for buzhash,
+split_batch_rk_kernel for Rabin-Karp).
 
 Waves with no stream of their own claim far tiles of other waves' regions and post each tile's
 first candidate; an owner whose next claim fails takes the region's cut from those posts.  The
 cut must still be exactly the reference's: the first candidate in [s + min - 1, s + max - 1],
-else the forced cut (repo/splitter/splitter_buzhash32.go:26-67), checked here against the C
+else the forced cut (repo/splitter/splitter_buzhash32.go:26-67, splitter_rabinkarp64.go:26-67), checked here against the C
 oracle (oracle/cdc_oracle.c, pinned by TestSplitterStability) on launches where helpers do most
 of the scanning -- few long streams, many regions per stream, small and custom averages,
 misaligned streams, dense candidates -- and with help switched off (KCDC_TEST_NO_HELP) for A/B
@@ -29,6 +30,12 @@ class knob:
         _lib.lib().kcdc_test_set(self.key, 0)
 
 
+def _helped(name):
+    """Whether the product build lets waiting waves help this name's batch kernel (buzhash; the
+    Rabin-Karp kernel's help is built but switched off: DESIGN.md §2.1b)."""
+    return "BUZHASH" in name
+
+
 def _split(name, data, offs, lens, gpu):
     import torch
     b = batch.make_device_batch(name, [data.data_ptr() + int(o) for o in offs], [int(x) for x in lens], gpu)
@@ -46,7 +53,9 @@ def _check(name, host, offs, lens, got):
 
 @pytest.mark.parametrize("name,ns,mib", [("DYNAMIC-4M-BUZHASH", 4, 64), ("DYNAMIC-4M-BUZHASH", 24, 16),
                                          ("DYNAMIC-8M-BUZHASH", 3, 96), ("DYNAMIC-1M-BUZHASH", 8, 40),
-                                         ("DYNAMIC-128K-BUZHASH", 6, 24)])
+                                         ("DYNAMIC-128K-BUZHASH", 6, 24), ("DYNAMIC-4M-RABINKARP", 4, 64),
+                                         ("DYNAMIC-4M-RABINKARP", 24, 16), ("DYNAMIC-1M-RABINKARP", 8, 40),
+                                         ("DYNAMIC-128K-RABINKARP", 6, 24)])
 def test_few_long_streams(gpu, name, ns, mib):
     """Fewer streams than waves: almost every tile of every region is a helper's."""
     import torch
@@ -57,15 +66,15 @@ def test_few_long_streams(gpu, name, ns, mib):
     cuts, counts = coracle.split_prng_streams(name, SEED, np.arange(100, 100 + ns), L, nthreads=16)
     for i in range(ns):
         assert got[i].tolist() == cuts[i, :counts[i]].tolist(), f"{name} stream {i}"
-    assert helps > 0, "no tile was helped"
+    assert helps > 0 or not _helped(name), "no tile was helped"
 
 
-def test_ragged_misaligned_streams(gpu):
+@pytest.mark.parametrize("name", ["DYNAMIC-2M-BUZHASH", "DYNAMIC-2M-RABINKARP"])
+def test_ragged_misaligned_streams(gpu, name):
     """Odd lengths at odd offsets (coordinates with a nonzero head), including lengths that end
     inside a helper's tile and regions of exactly kHelpMinTiles tiles."""
     import torch
     rng = np.random.default_rng(5)
-    name = "DYNAMIC-2M-BUZHASH"
     lens = [int(x) for x in rng.integers(3 << 20, 30 << 20, 10)] + [(1 << 20) + 3 * (128 << 10) - 1, 5 << 20, 1, 0]
     offs = np.concatenate(([7], 7 + np.cumsum(np.asarray(lens) + 13)[:-1])).astype(np.int64)
     total = int(offs[-1] + lens[-1] + 64)
@@ -73,29 +82,30 @@ def test_ragged_misaligned_streams(gpu):
     data = torch.from_numpy(host).to(gpu)
     got, helps = _split(name, data, offs, lens, gpu)
     _check(name, host, offs, lens, got)
-    assert helps > 0
+    assert helps > 0 or not _helped(name)
 
 
-def test_custom_small_averages(gpu):
-    """Custom buzhash averages (the TestSplitterStability parameterisations, splitter_test.go:30-39):
+@pytest.mark.parametrize("kind", ["buzhash", "rabinkarp"])
+def test_custom_small_averages(gpu, kind):
+    """Custom averages (the TestSplitterStability parameterisations, splitter_test.go:30-52):
     small tiles, many regions, regions of few tiles."""
     import torch
     kat = coracle.gorand_read(5, 5_000_000)
     data = torch.from_numpy(kat).to(gpu)
     for avg in (1024, 2048, 32 << 10, 64 << 10):
-        name = _lib.lib().kcdc_custom_algorithm(1, avg).decode()
+        name = _lib.lib().kcdc_custom_algorithm(coracle.KIND[kind], avg).decode()
         offs = [0, 1_000_003, 2_500_001]
         lens = [1_000_003, 1_500_000, 2_499_999]
         got, _ = _split(name, data, offs, lens, gpu)
         for i, (o, L) in enumerate(zip(offs, lens)):
-            assert got[i].tolist() == coracle.split_stream_kind("buzhash", avg, kat[o:o + L]).tolist(), (avg, i)
+            assert got[i].tolist() == coracle.split_stream_kind(kind, avg, kat[o:o + L]).tolist(), (avg, i)
 
 
-def test_dense_and_periodic(gpu):
+@pytest.mark.parametrize("name", ["DYNAMIC-4M-BUZHASH", "DYNAMIC-4M-RABINKARP"])
+def test_dense_and_periodic(gpu, name):
     """All-zero data (every position a candidate: cuts every min) and a periodic pattern (one
     candidate phase) through helped launches."""
     import torch
-    name = "DYNAMIC-4M-BUZHASH"
     L = 40 << 20
     zeros = np.zeros(L, np.uint8)
     pat = np.tile(np.arange(1, 12, dtype=np.uint8), L // 11 + 1)[:L]
@@ -105,10 +115,10 @@ def test_dense_and_periodic(gpu):
     _check(name, host, [0, L], [L, L], got)
 
 
-def test_help_off_is_identical(gpu):
+@pytest.mark.parametrize("name", ["DYNAMIC-4M-BUZHASH", "DYNAMIC-4M-RABINKARP"])
+def test_help_off_is_identical(gpu, name):
     """The same batch with help switched off (KCDC_TEST_NO_HELP) cuts identically and posts no help."""
     import torch
-    name = "DYNAMIC-4M-BUZHASH"
     ns, L = 12, 24 << 20
     data = torch.empty(ns * L, dtype=torch.uint8, device=gpu)
     batch.fill_prng(data, L, ns, L, SEED, first_sid=7)
@@ -116,15 +126,15 @@ def test_help_off_is_identical(gpu):
     on, helps_on = _split(name, data, offs, [L] * ns, gpu)
     with knob(_lib.TEST_NO_HELP, 1):
         off, helps_off = _split(name, data, offs, [L] * ns, gpu)
-    assert helps_on > 0 and helps_off == 0
+    assert (helps_on > 0 or not _helped(name)) and helps_off == 0
     assert [x.tolist() for x in on] == [x.tolist() for x in off]
 
 
-def test_config2_shape_with_tail_help(gpu):
+@pytest.mark.parametrize("name", ["DYNAMIC-4M-BUZHASH", "DYNAMIC-4M-RABINKARP"])
+def test_config2_shape_with_tail_help(gpu, name):
     """A config-2-shaped batch (512 x 4 MiB here): help happens only in the batch's tail, every
     stream bit-exact."""
     import torch
-    name = "DYNAMIC-4M-BUZHASH"
     ns, L = 512, 4 << 20
     data = torch.empty(ns * L, dtype=torch.uint8, device=gpu)
     batch.fill_prng(data, L, ns, L, SEED, first_sid=3000)

@@ -18,6 +18,8 @@
 #                    Rabin-Karp hot loop alone over config 2's bytes)
 #   sq:TAG:ARGS      SQ counters (VALU/LDS/wait) of bench.py ARGS, one --pmc pass
 #   trace:ARGS       tools/trace_pipe.py build/libkcdc_trace.so ARGS (per-wave timeline of the batch kernel)
+#   cprof:NAME:KIND  rocprofv3 --kernel-trace --stats of compress_bench.py --name NAME --only KIND (per-kernel time)
+#   probe:ARGS       tools/batch_probe.py ARGS (one bounded launch: queue stats, mismatched streams)
 #   compress:NAMES   tools/compress_bench.py --gib 4 for each compressor name (commas between names)
 set -u
 OUT=gpurun_out/${1:?usage: tools/gpu_session.sh OUT step...}
@@ -70,6 +72,14 @@ for step in "$@"; do
       a=$(args "${step#trace:}"); t=$(echo "$a" | tr -c 'A-Za-z0-9' '_')
       timeout -k 10 300 python -u tools/trace_pipe.py build/libkcdc_trace.so $a > "$OUT/trace_$t.log" 2>&1 || exit $?
       tail -12 "$OUT/trace_$t.log" ;;
+    cprof:*)
+      r=${step#cprof:}; nm=${r%%:*}; kind=${r#*:}
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/cprof_${nm}_$kind" -o run --output-format csv -- python3 tools/compress_bench.py --gib 4 --iters 3 --name "$nm" --only "$kind" > "$OUT/cprof_${nm}_$kind.log" 2>&1 || exit $?
+      echo "profiled $nm $kind" ;;
+    probe:*)
+      a=$(args "${step#probe:}"); t=$(echo "$a" | tr -c 'A-Za-z0-9' '_')
+      timeout -k 10 120 python -u tools/batch_probe.py $a > "$OUT/probe_$t.log" 2>&1 || { cat "$OUT/probe_$t.log"; exit 1; }
+      cat "$OUT/probe_$t.log" ;;
     compress:*)
       for nm in $(args "${step#compress:}"); do
         timeout -k 10 300 python -u tools/compress_bench.py --gib 4 --iters 3 --name "$nm" > "$OUT/compress_$nm.log" 2>&1 || exit $?
