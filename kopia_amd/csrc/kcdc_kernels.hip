@@ -853,21 +853,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t pring_rsrc(const BatchArgs& a)
     return __builtin_amdgcn_make_buffer_rsrc(a.ring, static_cast<short>(0),
                                              static_cast<int>((a.ring_mask + 1u) * kPEntryStride), 0x00020000);
 }
-#ifndef KCDC_TICKET_TRACE
-#define KCDC_TICKET_TRACE 0
-#endif
-// Debug builds (-DKCDC_TICKET_TRACE=1): who took / consumed ticket t, in the unused 8th granule of
-// ring entry t (word 0 taker, 1 consumer, 2 last help taken on it, 3 re-presented), for
-// tools/batch_probe.py post-mortems.  Compiled out of the product.
-__device__ __forceinline__ void tk_trace(const BatchArgs& a, int lane, uint32_t t, uint32_t word, uint32_t v) {
-#if KCDC_TICKET_TRACE
-    if (lane == 0 && t != 0xFFFFFFFFu)
-        reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a.ring) + static_cast<size_t>(t & a.ring_mask) * kPEntryStride +
-                                    112)[word] = v;
-#else
-    (void)a; (void)lane; (void)t; (void)word; (void)v;
-#endif
-}
 // Every lane loads (lane & 7): no divergent load, so no copy of the result that would
 // make the compiler wait for it early.
 __device__ __forceinline__ u32x4 pentry_load(const BatchArgs& a, int lane, uint32_t e) {
@@ -1235,12 +1220,8 @@ __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, u
     for (uint32_t spin = 0;; spin++) {
         const u32x4 v = pentry_load(a, lane, t);
         if (pentry_ok(v, lane, t)) {
-            if (static_cast<uint32_t>(__builtin_amdgcn_readlane(v.w, 0)) == kTombstone) {
-                tk_trace(a, lane, t, 1, 0x20000u | me);
-                return 2;
-            }
+            if (static_cast<uint32_t>(__builtin_amdgcn_readlane(v.w, 0)) == kTombstone) return 2;
             pentry_decode(st, v);
-            tk_trace(a, lane, t, 1, 0x10000u | me);
             return 1;
         }
         uint32_t stop = 0;
@@ -1268,10 +1249,7 @@ __device__ int presolve(const BatchArgs& a, int lane, uint32_t t, PStream& st, u
         }
         if (can_help && spin % kHelpEvery == kHelpEvery - 1) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (help_find(a, lane, me, spin / kHelpEvery, st)) {
-                tk_trace(a, lane, t, 2, 0x40000u | me);
-                return 3;
-            }
+            if (help_find(a, lane, me, spin / kHelpEvery, st)) return 3;
         }
         // back off while nothing finishes: ~1,000 waiting waves polling two words every 0.5 us
         // load the L2 channel of the done counter in the batch's tail
@@ -2100,9 +2078,6 @@ __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int 
 // Rabin-Karp lane segments: twice the buzhash cap (warm-up vs tile overshoot; 2 vs 1: 4M 2.542 vs
 // 2.554 ms, 128K 5.536 vs 5.643 ms, profiles/r03/rk/kbench_lmul_*.log)
 constexpr int64_t kRkLaneMul = 2;
-#ifndef KCDC_RK_HELP_MODE
-#define KCDC_RK_HELP_MODE 0
-#endif
 __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk_kernel(BatchArgs a) {
     __shared__ RkTables smt;
     __shared__ RkSlots smslots;
@@ -2112,18 +2087,9 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
     uint8_t* sl = smslots.b[wave][0];
     const uint32_t sl32 = lds_addr(sl);
     const int64_t mx = static_cast<int64_t>(a.max_size);
-    const uint32_t me = blockIdx.x * kRkWaves + wave;  // this wave's help slot
-    const int64_t rk_cap = kRkLaneMul * static_cast<int64_t>(a.lane_cap);  // lane bytes of an own tile (>= 512)
 
     PStream cur;
     int64_t budget = kNoYield;
-    // Intra-region help as in split_batch_pipe_kernel (hep, hs and the kHs* flags mean the same);
-    // tiles are T = 64 x rk_cap bytes, a help task scans one in two sub-tiles of rk_cap / 2 per lane.
-    uint32_t hep = 0, hs = 0;
-    constexpr uint32_t kHsPub = 1u << 16, kHsNeedPub = 1u << 17, kHsHelped = 1u << 18;
-    hs = kHsNeedPub;
-    auto hK = [&] { return hs & 0xFFu; };
-    auto htile = [&] { return (hs >> 8) & 0xFFu; };
     auto take_blocking = [&](uint32_t t, int64_t backlog_hint, uint32_t claim) -> bool {
         for (;;) {
             int64_t backlog = backlog_hint;
@@ -2131,18 +2097,10 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
                 const uint64_t ht = qht_take(a, lane, 1);
                 t = static_cast<uint32_t>(ht);
                 backlog = static_cast<int64_t>(ht >> 32) - static_cast<int64_t>(t) - 1;
-                tk_trace(a, lane, t, 0, 0x20000u | me);
-            } else {
-                tk_trace(a, lane, t, 3, 0x50000u | me);
             }
             const uint32_t held = t;
-            const int r = presolve(a, lane, held, cur, kRkWaves, me, a.help != nullptr && claim == 0xFFFFFFFFu);
+            const int r = presolve(a, lane, held, cur, kRkWaves, 0u, false);
             if (r == 0) return false;
-            if (r == 3) {  // a help task; the ticket stays held (in cap, unused by help tasks)
-                cur.cap = held;
-                uniformize(cur);
-                return true;
-            }
             t = 0xFFFFFFFFu;
             if (claim != 0xFFFFFFFFu) {
                 const bool requeued = bcast(claim) == 2u;
@@ -2182,41 +2140,22 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             if (!take_blocking(take_t, take_backlog, take_claim)) return;
             need_take = false;
             issued = false;
-            hs |= kHsNeedPub;
         }
         uniformize(cur);
         if (!pcheck(a, lane, cur, 0xFFFFFFFFu, 5)) return;
-        const bool is_help = (cur.sid & kHelpBit) != 0;
         int64_t lo, hi;
         pregion(a, cur, lo, hi);
-        const int64_t lcap = is_help ? rk_cap / 2 : rk_cap;
-        const RkGeom g = rk_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n, lcap);
+        const RkGeom g = rk_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n, kRkLaneMul * a.lane_cap);
         const int64_t ct = cur.ct, ct_next = ct + kWave * g.L;
         const bool last_of_region = ct_next > hi;
-        // A region new to this wave: publish it when it is long enough to share.
-        if ((hs & kHsNeedPub) && !is_help) {
-            const int64_t T = kWave * rk_cap;
-            const uint32_t K = static_cast<uint32_t>((hi - ct + T) / T);
-            hs = 0;
-            if (KCDC_RK_HELP_MODE >= 1 && a.help && K >= kHelpMinTiles && K <= static_cast<uint32_t>(kHelpTiles)) {
-                hep++;
-                hs = kHsPub | K;
-                help_publish(a, lane, me, hep, cur, ct, hi, K, T);
-            }
-        }
-        // The owner's claim on its next tile: an atomic add on its slot's bottom after fill 1's
-        // DMA, its value consumed at fill 2 (after that fill's vmcnt wait, before its DMA), so
-        // no compiler-visible load is in flight across a DMA.
-        const bool claim_next_r = KCDC_RK_HELP_MODE >= 2 && (hs & kHsPub) && !is_help && !last_of_region && htile() + 1u < hK();
-        const bool budget_out = !is_help && (KCDC_RK_HELP_MODE == 3 || !(hs & kHsHelped)) && budget - kWave * g.L <= 0;
+        const bool budget_out = budget - kWave * g.L <= 0;
         bool ends_nocand = false;
-        if (!is_help && last_of_region) {
+        if (last_of_region) {
             const int64_t s2 = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;
             ends_nocand = s2 >= cur.n || s2 + static_cast<int64_t>(a.min_size) - 1 >= cur.n;
         }
-        const bool switching = !is_help && (budget_out || ends_nocand);
+        const bool switching = budget_out || ends_nocand;
         const bool reserve = budget_out && !ends_nocand;
-        const bool claim_next = claim_next_r && !switching;
         uint64_t ht_raw = 0;
         if (switching) ht_raw = qht_add(a, lane, 1);  // the next stream's ticket
         uint32_t ht_lo = static_cast<uint32_t>(ht_raw), ht_hi = static_cast<uint32_t>(ht_raw >> 32);
@@ -2241,24 +2180,9 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             const uint64_t ht = qht_value(ht_lo, ht_hi);
             tk = static_cast<uint32_t>(ht);
             nbacklog = static_cast<int64_t>(ht >> 32) + (reserve ? 1 : 0) - static_cast<int64_t>(tk) - 1;
-            tk_trace(a, lane, tk, 0, 0x10000u | me);
         }
         uint64_t pe_raw = 0;
         bool res_issued = false, next_issued = false, entry_issued = false;
-        bool claim_ok = false, claim_known = !claim_next;
-        uint64_t claim_raw = 0;
-        auto claim_decode = [&]() {  // the claim word before this tile's add (+1 = after it)
-#if KCDC_RK_HELP_MODE == 5
-            const uint64_t raw5 = ld_agent64(help_claim(a, me));
-            const uint64_t cw = qht_value(static_cast<uint32_t>(raw5), static_cast<uint32_t>(raw5 >> 32));
-#else
-            const uint64_t cw = qht_value(static_cast<uint32_t>(claim_raw), static_cast<uint32_t>(claim_raw >> 32)) + 1ull;
-#endif
-            const uint32_t top = static_cast<uint32_t>(cw >> 20) & 0xFFFFFu, bot = static_cast<uint32_t>(cw) & 0xFFFFFu;
-            claim_ok = static_cast<uint32_t>(cw >> 40) == hep && bot <= top;
-            if (top < hK()) hs |= kHsHelped;
-            claim_known = true;
-        };
         // After the tile's last fill: the next tile's warm fill, or the next stream's entry.
         auto refill_last = [&]() {
             if (reserve && !res_issued) {  // this stream's ring entry, reserved late
@@ -2268,8 +2192,8 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             if (switching) {
                 pentry_dma(a, lane, tk, sl32);
                 entry_issued = true;
-            } else if (!last_of_region && (!claim_next || claim_ok)) {  // the next tile has its own geometry
-                const RkGeom gn = rk_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n, lcap);
+            } else if (!last_of_region) {  // the next tile has its own geometry
+                const RkGeom gn = rk_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n, kRkLaneMul * a.lane_cap);
                 rk_dma_warm(gn.ld, sl32, ct_next, gn.L, lane);
                 next_issued = true;
             }
@@ -2278,19 +2202,10 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
         // After line fill f is read: issue what the slot takes next (fill f+1, or after the
         // last fill the next tile's warm fill / the next stream's queue entry).
         auto refill = [&](int f) {
-            if (claim_next && f == 2) claim_decode();
             if (f < 2 * g.K)
                 rk_dma_line(g.ld, sl32, ct, g.L, f + 1, lane);
             else
                 refill_last();
-#if KCDC_RK_HELP_MODE == 5
-            if (claim_next && f == 1 && lane == 0)
-                __hip_atomic_fetch_add((gu64*)help_claim(a, me), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-            if (claim_next && f == 1 && lane == 0)
-                claim_raw = __hip_atomic_fetch_add((gu64*)help_claim(a, me), 1ull, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-#endif
         };
         // Hit check of one chain's 64 bytes at `rel` from its start (state before: h0/l0):
         // the chain's first candidate in [lo, hi].  The coordinate is formed only here, from
@@ -2318,78 +2233,31 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
         const int64_t c0 = ct + lane * g.L;
         const int64_t found = found_a >= 0 ? c0 + found_a : found_b >= 0 ? c0 + g.L / 2 + found_b : -1;
         // ---- end of tile
-        if (!claim_known) {  // one-line tiles (K = 1) consume the claim here
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            claim_decode();
-        }
         if (reserve && !res_issued) {
             pe_raw = qht_add(a, lane, 1ull << 32);
             res_issued = true;
         }
         const uint64_t hit = __ballot(found >= 0);
-        if (is_help) {
-            bool done = true;
-            if (hit || last_of_region) {  // post the tile's first candidate to its owner's row
-                int64_t f = -1;
-                if (hit) f = static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, __builtin_ctzll(hit)))));
-                help_post(a, lane, static_cast<uint32_t>(cur.cb), cur.epoch, static_cast<uint32_t>(cur.cnt), cur.s, f);
-            } else {  // the next sub-tile (prefetched), unless the owner has closed the region
-                const uint64_t w = ld_agent64(help_claim(a, static_cast<uint32_t>(cur.cb)));
-                done = static_cast<uint32_t>(qht_value(static_cast<uint32_t>(w), static_cast<uint32_t>(w >> 32)) >> 40) !=
-                       cur.epoch;
-            }
-            if (!done) {
-                cur.ct = ct_next;
-                issued = next_issued;
-                continue;
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the post, or a dropped prefetch
-            need_take = true;
-            take_t = static_cast<uint32_t>(cur.cap);
-            take_backlog = 0;
-            take_claim = 0xFFFFFFFFu;
-            continue;
-        }
         bool region_changed = true;
+        bool live;
         const int64_t forced = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;
-        int64_t cut = -1;  // this region's cut, once known
         if (hit) {
             const int first = __builtin_ctzll(hit);
             const int64_t f = static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, first))));
-            cut = f - cur.off0 + 1;
+            const int64_t next = f - cur.off0 + 1;
+            emit_cut(a, cur, lane, next);
+            cur.s = next;
+            cur.ct = -1;
         } else if (last_of_region) {  // forced cut at max size (splitter_rabinkarp64.go:60-64) or the end
-            cut = forced;
-        } else if (claim_next && !claim_ok) {  // the helpers hold the rest of the region
-            const int64_t T = kWave * rk_cap;
-            const int64_t ct0 = ct - static_cast<int64_t>(htile()) * T;  // the published tile 0
-            const int64_t r = KCDC_RK_HELP_MODE == 4 ? -2 - static_cast<int64_t>(htile() + 1u)
-                                                     : help_wait(a, lane, me, hep, htile() + 1u, hK(), ct0);
-            if (r >= 0) {
-                cut = r - cur.off0 + 1;
-            } else if (r == -1) {
-                cut = forced;
-            } else {  // a tile still pending: scan on from it, unshared
-                cur.ct = ct0 + (-2 - r) * T;
-                help_close(a, lane, me, hep);
-                hs = 0;
-                region_changed = false;
-            }
+            emit_cut(a, cur, lane, forced);
+            cur.s = forced;
+            cur.ct = -1;
         } else {
             cur.ct = ct_next;
-            hs += 1u << 8;  // htile++
             budget -= kWave * g.L;
             region_changed = false;
         }
-        if (cut >= 0) {
-            emit_cut(a, cur, lane, cut);
-            cur.s = cut;
-            cur.ct = -1;
-        }
-        if (region_changed) {
-            if (hs & kHsPub) help_close(a, lane, me, hep);
-            hs = kHsNeedPub;
-        }
-        const bool live = pstream_region(a, cur, lane);
+        live = pstream_region(a, cur, lane);
         if (!live && lane == 0) {
             a.counts[cur.sid] = cur.cnt;
             add_agent(a.queue + kQDone, 1u);
@@ -2399,8 +2267,6 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             if (next_issued && region_changed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stale prefetch
             continue;
         }
-        if (hs & kHsPub) help_close(a, lane, me, hep);  // a yielded region is not ours to share any more
-        hs = kHsNeedPub;
         if (reserve) {
             const uint32_t pe = static_cast<uint32_t>(
                 qht_value(static_cast<uint32_t>(pe_raw), static_cast<uint32_t>(pe_raw >> 32)) >> 32);
@@ -2418,7 +2284,6 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
                 pentry_decode(nx, ev);
                 uniformize(nx);
                 if (!pcheck(a, lane, nx, tk, 2)) return;
-                tk_trace(a, lane, tk, 1, 0x30000u | me);
                 cur = nx;
                 budget = pipe_quantum(nbacklog);
                 took = true;
@@ -3565,7 +3430,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         const unsigned need = (s.nstreams + wg_waves - 1) / wg_waves;
         // The buzhash pipe kernel takes the whole chip even for a few streams: the waves without
         // a stream help scan the owners' regions (help slots).
-        const bool helpers = (algo.kind == kBuzhash || (KCDC_RK_HELP_MODE > 0 && algo.kind == kRabinKarp)) && !g_test.no_help;
+        const bool helpers = algo.kind == kBuzhash && !g_test.no_help;
         unsigned grid = helpers || need >= cus ? cus : need;
         if (grid > dev::kMaxPipeGrid) grid = dev::kMaxPipeGrid;  // one claim flag per workgroup
         uint64_t ring = 1;

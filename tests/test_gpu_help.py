@@ -31,8 +31,9 @@ class knob:
 
 
 def _helped(name):
-    """Whether the product build lets waiting waves help this name's batch kernel (buzhash; the
-    Rabin-Karp kernel's help is built but switched off: DESIGN.md §2.1b)."""
+    """Whether waiting waves help this name's batch kernel: buzhash only (the Rabin-Karp kernel's
+    port of the protocol lost streams under yields and is not in the product: DESIGN.md §2.1b).
+    The Rabin-Karp rows still check that few-stream, ragged and dense launches cut exactly."""
     return "BUZHASH" in name
 
 

@@ -97,12 +97,3 @@ if bad:
     hs = set(held)
     print("tickets in [tail, head) nobody holds:", [t for t in range(tail, head) if t not in hs][:40], flush=True)
     print("tickets below tail held:", [t for t in held if t < tail][:40], flush=True)
-    # ticket trace (builds with -DKCDC_TICKET_TRACE=1): granule 7 of entry t = taker, consumer,
-    # last help taken while holding it, re-presented (site << 16 | wave)
-    def dec(v):
-        v = int(v)
-        return f"{v >> 16}:{v & 0xFFFF}" if v else "-"
-    ab = [t for t in range(tail, head) if t not in hs]
-    for t in ab[:12] + [e for e in range(ns, tail) if int(ent[e % ring][3]) in lost]:
-        g = ent[t % ring][28:32]
-        print("ticket", t, "taken", dec(g[0]), "consumed", dec(g[1]), "help", dec(g[2]), "represented", dec(g[3]), flush=True)
