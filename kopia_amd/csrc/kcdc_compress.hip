@@ -729,6 +729,73 @@ __device__ __forceinline__ void deflate_plan(const CompArgs& a, uint32_t b, uint
     }
 }
 
+// The sequences section of a segment's zstd block at sb8 + o (RFC 8878 §3.1.1.3.2):
+// Number_of_Sequences, Symbol_Compression_Modes = 0 (all Predefined), then the FSE bitstream written
+// backwards from the last sequence (zstd's ZSTD_encodeSequences order), closed by the 1-bit end
+// marker.  The sequences are read from the slot's words 143 - k (the parse keeps them at the slot's
+// end); the writer must stay below the words not yet read and inside the segment's size, else
+// kZOver (rare: costly sequences).  write = false: the size only, nothing stored.
+constexpr uint32_t kZOver = 0xFFFFFFFFu;
+__device__ uint32_t zstd_seqs(uint8_t* sb8, uint32_t o, uint32_t nseq, uint32_t seg_len, bool write) {
+    const uint32_t* words = reinterpret_cast<const uint32_t*>(sb8);
+    uint32_t pos = o;
+    uint64_t bb = 0;
+    uint32_t nb = 0;
+    auto put = [&](uint32_t v, uint32_t n) {
+        bb |= static_cast<uint64_t>(v) << nb;
+        nb += n;
+        while (nb >= 8u) {
+            if (write) sb8[pos] = static_cast<uint8_t>(bb);
+            pos++;
+            bb >>= 8;
+            nb -= 8u;
+        }
+    };
+    if (nseq < 128u) {
+        put(nseq, 8);
+    } else {
+        put(128u + (nseq >> 8), 8);
+        put(nseq & 255u, 8);
+    }
+    if (nseq) {
+        put(0u, 8);  // Predefined_Mode x 3
+        uint32_t sLL = 0, sML = 0, sOF = 0;
+        for (int k = static_cast<int>(nseq) - 1; k >= 0; k--) {
+            if (pos + 8u > 4u * (144u - static_cast<uint32_t>(k) - 1u) || pos > seg_len + 2u) return kZOver;
+            const uint32_t v = words[143u - static_cast<uint32_t>(k)];
+            const uint32_t ll = v >> 23, ml = ((v >> 15) & 255u) + 4u, ov = (v & 0x7FFFu) + 3u;
+            uint32_t llc, llb, llx, mlc, mlb, mlx;
+            ll_code(ll, llc, llb, llx);
+            ml_code(ml, mlc, mlb, mlx);
+            const uint32_t ofc = 31u - __builtin_clz(ov), ofx = ov - (1u << ofc);
+            if (k == static_cast<int>(nseq) - 1) {
+                sLL = kFseLL.first[llc];
+                sML = kFseML.first[mlc];
+                sOF = kFseOF.first[ofc];
+            } else {  // the decoder's updates after sequence k: LL, ML, OF -> written OF, ML, LL
+                const uint32_t nOF = kFseOF.enc[ofc][sOF];
+                put(sOF - kFseOF.base[nOF], kFseOF.nb[nOF]);
+                sOF = nOF;
+                const uint32_t nML = kFseML.enc[mlc][sML];
+                put(sML - kFseML.base[nML], kFseML.nb[nML]);
+                sML = nML;
+                const uint32_t nLL = kFseLL.enc[llc][sLL];
+                put(sLL - kFseLL.base[nLL], kFseLL.nb[nLL]);
+                sLL = nLL;
+            }
+            put(llx, llb);  // the decoder reads offset, match length, literal length extras
+            put(mlx, mlb);
+            put(ofx, ofc);
+        }
+        put(sML, 6);  // initial states, read LL, OF, ML
+        put(sOF, 5);
+        put(sLL, 6);
+        put(1u, 1);  // end marker
+        if (nb) put(0u, 8u - nb);
+    }
+    return pos - o;
+}
+
 // zstd literals through one Huffman code per span (RFC 8878 §3.1.1.3.1, §4.2): after the parse
 // (each coded segment a Compressed_Block with Raw_Literals: block header at slot + 3, literals
 // header at + 6, the literals from + 8, the sequences section after them), the span's literal
@@ -759,6 +826,11 @@ __device__ __forceinline__ uint32_t zstd_huff_literals(const CompArgs& a, uint32
     const uint32_t* sq = reinterpret_cast<const uint32_t*>(sb8);  // sequence k at word 143 - k
     auto seq_ll = [&](uint32_t k) { return sq[143u - k] >> 23; };
     auto seq_ml = [&](uint32_t k) { return ((sq[143u - k] >> 15) & 255u) + 4u; };
+    // A segment that keeps raw literals: its sequences section after them (sized in the parse).
+    auto raw_tail = [&]() -> uint32_t {
+        if (coded && zstd_seqs(sb8, 8u + nlit, nseq, seg_len, true) == kZOver) return kStored | seg_len;
+        return word;
+    };
     if (coded) {
         uint32_t x = x0;
         for (uint32_t k = 0; k < nseq; k++) {
@@ -774,7 +846,7 @@ __device__ __forceinline__ uint32_t zstd_huff_literals(const CompArgs& a, uint32
         used += static_cast<uint32_t>(__popcll(m));
         if (m) top = k + 63u - static_cast<uint32_t>(__builtin_clzll(m));
     }
-    if (used < 2u || top > 128u) return word;  // one symbol (an RLE block's case) or no direct weights: raw
+    if (used < 2u || top > 128u) return raw_tail();  // one symbol (an RLE block's case) or no direct weights
     huff_lengths(hist, 256u, 11u, lens, sa, ss, num, lane);
     if (lane == 0) {  // codes: by weight ascending (longest first), then symbol (RFC 8878 §4.2.1.4)
         uint32_t maxb = 0;
@@ -812,27 +884,20 @@ __device__ __forceinline__ uint32_t zstd_huff_literals(const CompArgs& a, uint32
     // 2-byte header + the literals).  The tree is paid once, by the first segment that saves
     // (the carrier), and pays off over the span: Huffman literals are used when the savings of all
     // segments exceed the tree.  The carrier's block must still fit its slot (it may grow).
-    const uint32_t old_total = word;            // block header + content bytes, from slot + 3
-    const uint32_t qs = coded ? old_total - 5u - nlit : 0u;  // the sequences section, at slot + 8 + nlit
+    const uint32_t qs = coded ? word - 5u - nlit : 0u;  // the sequences section's size (the parse's block)
     const int32_t save = coded && nlit ? static_cast<int32_t>(2u + nlit) - static_cast<int32_t>(3u + sbytes) : 0;
-    const bool fits = 6u + tsz + sbytes + qs + kZOff <= kSlot;
+    // the carrier's block may grow: it must fit its slot, and its literal section and sequences
+    // must stay below the sequence words they are written from
+    const bool fits = 6u + tsz + sbytes + qs + kZOff <= kSlot && 9u + tsz + sbytes + qs + 8u <= 4u * (144u - nseq);
     const uint64_t cm = __ballot(save > 0 && fits);
-    if (!cm) return word;
+    if (!cm) return raw_tail();
     const uint32_t carrier = static_cast<uint32_t>(__builtin_ctzll(cm));
     int32_t tot = save > 0 && lane >= carrier ? save : 0;  // what the carrier and the segments after it save
     for (uint32_t o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, static_cast<int>(o), 64);
-    if (tot <= static_cast<int32_t>(tsz)) return word;
+    if (tot <= static_cast<int32_t>(tsz)) return raw_tail();
     const uint32_t use = lane == carrier ? 2u : (lane > carrier && save > 0) ? 3u : 0u;
-    if (!use) return word;
+    if (!use) return raw_tail();
     const uint32_t ts = use == 2u ? tsz : 0u;
-    {  // the sequences section to its new place (memmove: the carrier's section may grow)
-        const uint8_t* src = sb8 + 8u + nlit;
-        uint8_t* dst = sb8 + 9u + ts + sbytes;
-        if (dst > src)
-            for (uint32_t i = qs; i-- > 0u;) dst[i] = src[i];
-        else
-            for (uint32_t i = 0; i < qs; i++) dst[i] = src[i];
-    }
     uint8_t* op = sb8 + 9u + ts;
     if (use == 2u) {  // direct weights: W = maxb + 1 - bits (0: unused), two per byte, high nibble first
         sb8[9] = static_cast<uint8_t>(127u + top);
@@ -872,7 +937,11 @@ __device__ __forceinline__ uint32_t zstd_huff_literals(const CompArgs& a, uint32
     sb8[6] = static_cast<uint8_t>(lh);
     sb8[7] = static_cast<uint8_t>(lh >> 8);
     sb8[8] = static_cast<uint8_t>(lh >> 16);
-    const uint32_t total = 6u + ts + sbytes + qs;
+    // the sequences section after the stream (a treeless segment's may not fit below its sequence
+    // words: stored then, which keeps the frame's table for the segments after it)
+    const uint32_t q2 = zstd_seqs(sb8, 9u + ts + sbytes, nseq, seg_len, true);
+    if (q2 == kZOver) return kStored | seg_len;
+    const uint32_t total = 6u + ts + sbytes + q2;
     const uint32_t hdr = ((total - 3u) << 3) | (2u << 1);  // Compressed_Block, not the last
     sb8[3] = static_cast<uint8_t>(hdr);
     sb8[4] = static_cast<uint8_t>(hdr >> 8);
@@ -1078,69 +1147,12 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
         zlit = nlit;
         if (w.nb) *w.op = static_cast<uint32_t>(w.bb);
         uint8_t* sb8 = reinterpret_cast<uint8_t*>(base);
-        // Sequences section: Number_of_Sequences, Symbol_Compression_Modes = 0 (all Predefined), then
-        // the FSE bitstream written backwards from the last sequence (RFC 8878 §3.1.1.3.2;
-        // zstd's ZSTD_encodeSequences order), closed by the 1-bit end marker.
-        uint8_t* op = sb8 + 8 + nlit;
-        uint64_t bb = 0;
-        uint32_t nb = 0;
-        auto put = [&](uint32_t v, uint32_t n) {
-            bb |= static_cast<uint64_t>(v) << nb;
-            nb += n;
-            while (nb >= 8u) {
-                *op++ = static_cast<uint8_t>(bb);
-                bb >>= 8;
-                nb -= 8u;
-            }
-        };
-        if (nseq < 128u) {
-            put(nseq, 8);
-        } else {
-            put(128u + (nseq >> 8), 8);
-            put(nseq & 255u, 8);
-        }
-        if (nseq) {
-            put(0u, 8);  // Predefined_Mode x 3
-            uint32_t sLL = 0, sML = 0, sOF = 0;
-            for (int k = static_cast<int>(nseq) - 1; k >= 0; k--) {
-                // the writer must stay below the sequences not yet read (rare: costly sequences)
-                if (op + 8 > sb8 + 4u * (144u - static_cast<uint32_t>(k) - 1u) || op > sb8 + seg_len + 2u) {
-                    over = true;
-                    break;
-                }
-                const uint32_t v = base[143u - static_cast<uint32_t>(k)];
-                const uint32_t ll = v >> 23, ml = ((v >> 15) & 255u) + 4u, ov = (v & 0x7FFFu) + 3u;
-                uint32_t llc, llb, llx, mlc, mlb, mlx;
-                ll_code(ll, llc, llb, llx);
-                ml_code(ml, mlc, mlb, mlx);
-                const uint32_t ofc = 31u - __builtin_clz(ov), ofx = ov - (1u << ofc);
-                if (k == static_cast<int>(nseq) - 1) {
-                    sLL = kFseLL.first[llc];
-                    sML = kFseML.first[mlc];
-                    sOF = kFseOF.first[ofc];
-                } else {  // the decoder's updates after sequence k: LL, ML, OF -> written OF, ML, LL
-                    const uint32_t nOF = kFseOF.enc[ofc][sOF];
-                    put(sOF - kFseOF.base[nOF], kFseOF.nb[nOF]);
-                    sOF = nOF;
-                    const uint32_t nML = kFseML.enc[mlc][sML];
-                    put(sML - kFseML.base[nML], kFseML.nb[nML]);
-                    sML = nML;
-                    const uint32_t nLL = kFseLL.enc[llc][sLL];
-                    put(sLL - kFseLL.base[nLL], kFseLL.nb[nLL]);
-                    sLL = nLL;
-                }
-                put(llx, llb);  // the decoder reads offset, match length, literal length extras
-                put(mlx, mlb);
-                put(ofx, ofc);
-            }
-            put(sML, 6);  // initial states, read LL, OF, ML
-            put(sOF, 5);
-            put(sLL, 6);
-            put(1u, 1);  // end marker
-            if (nb) put(0u, 8u - nb);
-        }
-        if (over) return kStored | seg_len;
-        const uint32_t total = static_cast<uint32_t>(op - sb8) - kZOff;  // block header + content
+        // The sequences section follows the raw literals.  With the span's Huffman pass to come
+        // (effort >= 1) only its size is taken here: zstd_huff_literals reads the sequence words
+        // again (literal positions) and writes the section after the literal section it chooses.
+        const uint32_t qs = zstd_seqs(sb8, 8u + nlit, nseq, seg_len, a.effort == 0u);
+        if (qs == kZOver) return kStored | seg_len;
+        const uint32_t total = 5u + nlit + qs;  // block header + literals section + sequences section
         if (total >= seg_len + kZStoredHdr) return kStored | seg_len;
         const uint32_t hdr = ((total - 3u) << 3) | (2u << 1);  // Compressed_Block, not the last
         sb8[3] = static_cast<uint8_t>(hdr);
