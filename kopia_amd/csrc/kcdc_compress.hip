@@ -79,8 +79,8 @@ struct CompArgs {
     uint32_t max_spans;
     uint32_t header_id;
     uint32_t skip;      // literal-run skip shift of the match search (level)
-    uint32_t effort;    // 0: the lane's own table only; 1: + the span-wide first-occurrence table;
-                        // 2: + one-step lazy matching (compression levels)
+    uint32_t effort;    // 0: the lane's own table only; 1: + the span-wide first-occurrence table,
+                        // previous segments' tables, lazy matching of short matches; 2: lazy < 32 B
     uint32_t gzip;      // 1: the stream sits in a gzip member (RFC 1952): gzip, pgzip
     uint32_t fmt;       // kFmtDeflate or kFmtS2
     uint32_t* crc;      // [n]: per chunk, XOR of its spans' shifted raw CRC-32s (atomic)
@@ -1106,7 +1106,9 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
     while (!over && x + 4u <= xe) {
         uint32_t cand;
         uint32_t n = best_at(x, cand);
-        if (n && a.effort >= 2u && n < 32u && x + 5u <= xe) {  // lazy: a longer match one byte later wins
+        // lazy: a longer match one byte later wins (default: for matches under 8 bytes, the short
+        // word repeats of text; best-compression: under 32)
+        if (n && a.effort >= 1u && n < (a.effort >= 2u ? 32u : 8u) && x + 5u <= xe) {
             uint32_t c2;
             const uint32_t n2 = best_at(x + 1u, c2);
             if (n2 > n + 1u) {
@@ -1658,8 +1660,9 @@ struct CompAlgo {
 // compressor_deflate.go:14-16, compressor_gzip.go:15-17, compressor_pgzip.go:16-18 (sorted names).
 // pgzip's writer splits its input into independently compressed blocks; gzip and pgzip readers
 // accept any valid member, so both families carry the same device stream.  The levels differ in
-// search effort: best-speed = the lane's own table, default = + the span's first occurrences,
-// best-compression = + lazy matching and no literal-run skipping to speak of.
+// search effort: best-speed = the lane's own table; default = + the span's first occurrences, the
+// three previous segments' tables and lazy matching of matches under 8 bytes; best-compression =
+// lazy matching under 32 bytes and no literal-run skipping to speak of.
 constexpr CompAlgo kCompAlgos[] = {
     {"deflate-best-compression", 0x1502u, 8u, 2u, 0u},
     {"deflate-best-speed", 0x1501u, 4u, 0u, 0u},

@@ -1017,8 +1017,8 @@ __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
 #ifndef KCDC_HELP_EVERY
 #define KCDC_HELP_EVERY 2
 #endif
-#ifndef KCDC_HELP_GAP
-#define KCDC_HELP_GAP 2u
+#ifndef KCDC_HELP_GAP  // a region is open to helpers while top >= bottom + GAP (1 vs 2: 1.295 vs
+#define KCDC_HELP_GAP 1u  // 1.332 ms on config 2, same-process A/B, profiles/r04/third/)
 #endif
 constexpr int64_t kHelpSplit = 2;     // sub-tiles per help task (lane segments lane_cap / 2, >= 256 B)
 constexpr int kHelpTiles = 128;          // regions of up to 128 tiles take help (every registered name)
@@ -1163,7 +1163,8 @@ __device__ bool help_find(const BatchArgs& a, int lane, uint32_t me, uint32_t at
     const uint64_t c = g < nw ? ld_agent64(help_claim(a, g)) : 0ull;
     const uint32_t ep = static_cast<uint32_t>(c >> 40), top = static_cast<uint32_t>(c >> 20) & 0xFFFFFu,
                    bot = static_cast<uint32_t>(c) & 0xFFFFFu;
-    // leave the owner its next tile: claim only tiles >= bottom + KCDC_HELP_GAP - 1
+    // claim only tiles >= bottom + KCDC_HELP_GAP - 1 (GAP 1: up to the owner's next tile, which the
+    // owner then takes from the row instead of scanning it)
     const bool open = ep != 0u && !(ep & kHelpClosed) && top >= bot + KCDC_HELP_GAP;
     const uint32_t key = open ? ((top - bot) << 6) | ((static_cast<uint32_t>(lane) + rot) & 63u) : 0u;
     uint32_t best = key;

@@ -22,14 +22,10 @@
 // whole object, however the bytes were sliced (tests/test_gpu_writer.py).
 #include <hip/hip_runtime.h>
 
-#include <sched.h>
-
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
-#include <cstdio>
-#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -125,57 +121,6 @@ int64_t now_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
         .count();
 }
-
-// CPUs this process may run on at once: its affinity mask, capped by a cgroup CPU quota (v2
-// cpu.max, v1 cfs_quota_us / cfs_period_us).  A pod may see hundreds of CPUs and own 16.
-int usable_cpus() {
-    cpu_set_t set;
-    int n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 0;
-    if (n <= 0) n = static_cast<int>(std::thread::hardware_concurrency());
-    long quota = -1, period = 0;
-    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
-        char q[32] = {0};
-        if (std::fscanf(f, "%31s %ld", q, &period) == 2 && std::strcmp(q, "max") != 0) quota = std::atol(q);
-        std::fclose(f);
-    } else if (FILE* fq = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
-        if (std::fscanf(fq, "%ld", &quota) != 1) quota = -1;
-        std::fclose(fq);
-        if (FILE* fp = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
-            if (std::fscanf(fp, "%ld", &period) != 1) period = 0;
-            std::fclose(fp);
-        }
-    }
-    if (quota > 0 && period > 0) n = std::min<int>(n, static_cast<int>((quota + period - 1) / period));
-    return std::max(1, n);
-}
-
-// Writers copying into their staging blocks at once: the usable CPUs less one.  Uploads run a
-// writer per CPU (upload.go:777 sizes the pool by runtime.NumCPU(), which sees the whole machine
-// in a container), so without a gate the copies oversubscribe a CPU quota, the quota throttles
-// every thread of the process, the round threads with them, and a writer preempted inside its
-// copy stalls the round's collection (measured: 64 writers 29 GiB/s, 16 writers 43 GiB/s).
-class CopyGate {
-  public:
-    void enter() {
-        std::unique_lock<std::mutex> lk(mu_);
-        if (tokens_ < 0) tokens_ = std::max(1, usable_cpus() - 1);
-        cv_.wait(lk, [&] { return tokens_ > 0; });
-        tokens_--;
-    }
-    void leave() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            tokens_++;
-        }
-        cv_.notify_one();
-    }
-
-  private:
-    std::mutex mu_;
-    std::condition_variable cv_;
-    int tokens_ = -1;
-};
-CopyGate g_copy_gate;
 
 }  // namespace
 
@@ -860,19 +805,9 @@ extern "C" int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len) {
             nb.pos = w->written;
             w->blocks.push_back(nb);
         }
-        // copy outside the writer's mutex (the round thread's collection takes it), behind the gate;
-        // only this thread appends to or fills the last block, and a block that is not full and
-        // last is never retired, so it is still blocks.back() afterwards
-        uint8_t* const blk = w->blocks.back().p;
-        const uint32_t at = w->blocks.back().end;
-        const size_t k = std::min<size_t>(len, kBlock - at);
-        wl.unlock();
-        g_copy_gate.enter();
-        std::memcpy(blk + at, p, k);
-        g_copy_gate.leave();
-        wl.lock();
         Blk& bk = w->blocks.back();
-        if (bk.p != blk || bk.end != at) return set_error(KCDC_EINVAL, "concurrent writes to one writer");
+        const size_t k = std::min<size_t>(len, kBlock - bk.end);
+        std::memcpy(bk.p + bk.end, p, k);
         bk.end += static_cast<uint32_t>(k);
         w->written += k;
         if (w->written > w->counted) {  // bytes beyond the size hint count toward the device's load
