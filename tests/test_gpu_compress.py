@@ -207,9 +207,13 @@ def test_tiny_chunks_frame(name, gpu):
 
 
 def test_mixed_ratio_does_not_regress(gpu):
-    """Pins the device encoders' ratio on text-like data (DESIGN.md §2.7 measures 0.37-0.40; zlib
-    -6: 0.30): the levels order as their search effort, and no name falls past 0.42."""
+    """Pins the device encoders' ratio on text-like data against zlib level 6 on the same 1 MiB
+    chunks (DESIGN.md §2.7, round 4 on the bench's mixed data: deflate-default 0.329 = 1.09 x
+    zlib-6, best-compression 0.328, s2 0.367, zstd 0.370 = 1.23 x): the levels order as their search
+    effort, and each family stays within its margin."""
+    import zlib
     host = _mixed(8 << 20, 31)
+    z6 = sum(len(zlib.compress(host[i << 20:(i + 1) << 20].tobytes(), 6)) for i in range(8)) / host.size
     offs, lens = [i << 20 for i in range(8)], [1 << 20] * 8
     ratio = {}
     for name in ["deflate-best-speed", "deflate-default", "deflate-best-compression", "s2-default", "zstd"]:
@@ -218,4 +222,5 @@ def test_mixed_ratio_does_not_regress(gpu):
         ratio[name] = float(ol.sum()) / host.size
     assert ratio["deflate-default"] <= ratio["deflate-best-speed"], ratio
     assert ratio["deflate-best-compression"] <= ratio["deflate-default"] + 1e-3, ratio
-    assert max(ratio.values()) < 0.42, ratio
+    assert ratio["deflate-default"] <= 1.12 * z6, (ratio, z6)
+    assert ratio["s2-default"] <= 1.25 * z6 and ratio["zstd"] <= 1.26 * z6, (ratio, z6)
