@@ -1319,7 +1319,14 @@ __device__ __forceinline__ void ptile_issue(const PStream& st, int64_t hi, uint3
 // Visit quantum from the number of streams queued behind the taken ticket: none waiting ->
 // run to completion; otherwise 768 KiB (short tail quanta measured no gain, and helpers now
 // split the tail's regions).
-__device__ __forceinline__ int64_t pipe_quantum(int64_t backlog) { return backlog <= 0 ? kNoYield : kPipeYield; }
+__device__ __forceinline__ int64_t pipe_quantum(int64_t backlog, int64_t q = kPipeYield) { return backlog <= 0 ? kNoYield : q; }
+// The buzhash kernel's quantum in tiles: 6 full tiles, at least 512 KiB (4M and larger averages: 6 x
+// 128 KiB = 768 KiB as before; 128K: 512 KiB instead of 768: 3.42 vs 3.63 ms, while 512 KiB at 4M
+// cost 1.334 vs 1.286 ms; profiles/r04/third/kbench_quantum_*.log; against the constant in one process: 128K 3.415 vs 3.639, 256K 2.697 vs 2.843, 4M 1.296 vs 1.309 ms, ab_quantum_tiles_*.log)
+__device__ __forceinline__ int64_t pipe_quantum_tiles(int64_t backlog, uint32_t lane_cap) {
+    const int64_t q = 6 * kWave * static_cast<int64_t>(lane_cap);
+    return pipe_quantum(backlog, q > (512 << 10) ? q : (512 << 10));
+}
 
 template <bool TOP>
 __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_pipe_kernel(BatchArgs a) {
@@ -1421,7 +1428,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             if (r == 2) continue;  // tombstone
             uniformize(cur);
             if (!pcheck(a, lane, cur, held, 1)) return false;
-            budget = pipe_quantum(backlog);
+            budget = pipe_quantum_tiles(backlog, a.lane_cap);
             if (pstream_region(a, cur, lane)) return true;
             if (lane == 0) {  // nothing left to scan
                 a.counts[cur.sid] = cur.cnt;
@@ -1711,7 +1718,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         if (nstate >= 2) {
             cur = nx;
             issued = nstate == 3;
-            budget = pipe_quantum(nbacklog);
+            budget = pipe_quantum_tiles(nbacklog, a.lane_cap);
             if (pstream_region(a, cur, lane)) continue;
             if (lane == 0) {  // nothing left to scan in it
                 a.counts[cur.sid] = cur.cnt;
