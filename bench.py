@@ -165,20 +165,23 @@ def roofline(kernel: str, config: str, kern_ms: float, rolled: int, stream_bytes
             "stream_gbs": round(stream_bytes / kern_s / 1e9, 1)} | valu_note(kernel, config)
 
 
-# Rabin-Karp's limiter is VALU issue, not HBM: SQ_INSTS_VALU per config-2
-# launch (profiles/r03/rk/sq1_counter_collection.csv, 7 launches) at 4 cycles per wave64
-# instruction on each of the 1,024 SIMDs gives the launch's VALU floor at the measured clock.
-RK_VALU_PER_LAUNCH = {"config2-rk": 1.0146e9}
-SIMDS, VALU_CYCLES, CLOCK_HZ = 1024, 4, 2.13e9
+# Rabin-Karp's limiter is neither HBM nor VALU issue: with every
+# instruction class measured (tools/valu_rate.hip, profiles/r04/rk/valu_rate.log), the hot roll is
+# ~26 SIMD cycles per wave-roll (perm/alignbit/and_or/min3 at ~4.2, bitop3/lshr at ~2.3 with two
+# waves per SIMD), a VALU floor of ~1.1 ms for config 2; the hot loop alone (the kernel's rk_step64
+# replica fed from LDS, `valu_rate rk`, profiles/r04/rk/valu_rk_hotloop.log) takes 2.02 ms: the
+# per-byte chain through the mod[] table read is LDS-latency bound at four chains per SIMD.
+RK_HOT_LOOP_MS = {"config2-rk": 2.021}
+RK_VALU_FLOOR_MS = {"config2-rk": 1.1}
 
 
 def valu_note(kernel: str, config: str) -> dict:
-    n = RK_VALU_PER_LAUNCH.get(config)
-    if not n:
+    hot = RK_HOT_LOOP_MS.get(config)
+    if not hot:
         return {}
-    floor_ms = n * VALU_CYCLES / SIMDS / CLOCK_HZ * 1e3
-    return {"limited_by": "VALU", "valu_insts_per_launch": n, "valu_floor_ms": round(floor_ms, 3),
-            "valu_source": "profiles/r03/rk/sq1_counter_collection.csv (SQ_INSTS_VALU)"}
+    return {"limited_by": "LDS latency of the per-byte table chain", "hot_loop_alone_ms": hot,
+            "valu_floor_ms": RK_VALU_FLOOR_MS[config],
+            "hot_loop_source": "profiles/r04/rk/valu_rk_hotloop.log (tools/valu_rate.hip rk)"}
 
 
 def h2d_rates(host: np.ndarray, dev) -> dict:
@@ -368,8 +371,8 @@ def bench_batch(args, comm: Comm):
         "per_gpu_gib_s": agg["per_gpu_gib_s"],
     }
     out["roofline"] = roofline(BATCH_KERNEL[int(info.kind)], cfg, kern_ms, rolled, ns * L)
-    if "valu_floor_ms" in out["roofline"]:
-        out["roofline"]["valu_busy"] = round(out["roofline"]["valu_floor_ms"] / kern_ms, 3)
+    if "hot_loop_alone_ms" in out["roofline"]:
+        out["roofline"]["hot_loop_frac"] = round(out["roofline"]["hot_loop_alone_ms"] / kern_ms, 3)
     out["cut_stats"] = {"chunks": int(sum(c.size for c in cuts)), "rolled_fraction": round(rolled / (ns * L), 4)}
 
     if args.hash and rank == 0 and world == 1:

@@ -1320,9 +1320,10 @@ __device__ __forceinline__ void ptile_issue(const PStream& st, int64_t hi, uint3
 // run to completion; otherwise 768 KiB (short tail quanta measured no gain, and helpers now
 // split the tail's regions).
 __device__ __forceinline__ int64_t pipe_quantum(int64_t backlog, int64_t q = kPipeYield) { return backlog <= 0 ? kNoYield : q; }
-// The buzhash kernel's quantum in tiles: 6 full tiles, at least 512 KiB (4M and larger averages: 6 x
-// 128 KiB = 768 KiB as before; 128K: 512 KiB instead of 768: 3.42 vs 3.63 ms, while 512 KiB at 4M
-// cost 1.334 vs 1.286 ms; profiles/r04/third/kbench_quantum_*.log; against the constant in one process: 128K 3.415 vs 3.639, 256K 2.697 vs 2.843, 4M 1.296 vs 1.309 ms, ab_quantum_tiles_*.log)
+// The buzhash kernel's quantum in tiles: 6 full tiles, at least 512 KiB.  4M and larger averages
+// keep 6 x 128 KiB = 768 KiB (512 KiB there: 1.334 vs 1.286 ms); 128K and 256K get 512 KiB.  Against
+// the constant 768 KiB in one process (profiles/r04/third/ab_quantum_tiles_*.log): 128K 3.415 vs
+// 3.639 ms, 256K 2.697 vs 2.843, 4M 1.296 vs 1.309; all bit-exact.
 __device__ __forceinline__ int64_t pipe_quantum_tiles(int64_t backlog, uint32_t lane_cap) {
     const int64_t q = 6 * kWave * static_cast<int64_t>(lane_cap);
     return pipe_quantum(backlog, q > (512 << 10) ? q : (512 << 10));
