@@ -179,7 +179,9 @@ int64_t kcdc_bw_rounds(const kcdc_bw_batcher* b); /* rounds shipped so far (test
  * launch, cut lists out), from HIP events, then the device span of all rounds and the seconds of
  * it in which a gather or a split ran, then the round thread's seconds per phase (collecting the
  * writers' blocks, placing them in the arenas, issuing the gather, waiting for the previous round,
- * issuing the split).  Returns 13. */
+ * issuing the split), then the round thread's seconds waiting for a round's worth of staged bytes,
+ * and the writers' seconds (summed over writers) blocked on their staging cap and getting a pinned
+ * staging block.  Returns 16. */
 int kcdc_bw_stats(kcdc_bw_batcher* b, double* out, int n);
 
 /* ------------------------------------------------------ batch (hot path)

@@ -171,6 +171,9 @@ struct BwDev {
     double t_seg[5] = {0, 0, 0, 0, 0};  // host seconds per round phase: collect, place, gather issue, wait, launch
     hipEvent_t ev_ref = nullptr;                   // recorded once: the origin of the intervals below
     std::vector<std::pair<float, float>> busy;     // device intervals (ms after ev_ref) of gathers and splits
+    double t_idle = 0;                             // round thread: waiting for a round's worth of bytes
+    std::atomic<int64_t> w_capped_ns{0};           // writers: blocked on their staging cap (summed)
+    std::atomic<int64_t> w_block_ns{0};            // writers: getting a pinned block (summed)
 
     ~BwDev() {
         if (algo->kind == kFixed) return;
@@ -326,6 +329,7 @@ void BwDev::loop() {
         // the round in flight as soon as the device has finished it (its writers may be waiting
         // for cuts) -- but do not block on it: the next round's gather should start while it splits.
         bool timed_out = false;
+        const auto idle0 = std::chrono::steady_clock::now();
         while (!work() && !timed_out) {
             if (inflight.live) {
                 if (hipEventQuery(meta[inflight.m].done) == hipSuccess) {
@@ -353,6 +357,7 @@ void BwDev::loop() {
                 cv_round.wait_for(lk, std::chrono::milliseconds(1), [&] { return work() || staged.load() > 0; });
             }
         }
+        t_idle += std::chrono::duration<double>(std::chrono::steady_clock::now() - idle0).count();
         if (error) break;
         if (staged.load() == 0 && finish_pending.load() == 0) {
             if (stop) break;
@@ -784,19 +789,23 @@ extern "C" int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len) {
         // backpressure: at most writer_cap unshipped bytes (a capped writer asks for a round at
         // once: with few writers `staged` may never reach round_bytes)
         if (w->written - w->shipped >= b->writer_cap) {
+            const int64_t c0 = now_ns();
             b->capped++;
             b->cv_round.notify_one();
             w->cv.wait(wl, [&] { return b->error || w->written - w->shipped < b->writer_cap; });
             b->capped--;
+            b->w_capped_ns += now_ns() - c0;
             continue;
         }
         if (w->blocks.empty() || w->blocks.back().end == kBlock) {
             wl.unlock();  // lock order: the batcher's mutex is never taken under a writer's
+            const int64_t g0 = now_ns();
             uint8_t* blk;
             {
                 std::lock_guard<std::mutex> lk(b->mu);
                 blk = b->get_block();
             }
+            b->w_block_ns += now_ns() - g0;
             wl.lock();
             if (!blk) return set_error(KCDC_ENOMEM, "pinned staging block");
             Blk nb;
@@ -907,7 +916,7 @@ extern "C" int kcdc_bw_stats(kcdc_bw_batcher* t, double* out, int n) {
     // per device: the device span from its first round's start to its last one's end, and the
     // part of it in which a gather or a split ran (their union: overlapped rounds count once);
     // over devices: counts and host seconds add up, spans and busy times are the maximum
-    double v[13] = {0};
+    double v[16] = {0};
     for (BwDev* b : t->devs) {
         std::lock_guard<std::mutex> lk(b->mu);
         std::vector<std::pair<float, float>> iv = b->busy;
@@ -928,11 +937,12 @@ extern "C" int kcdc_bw_stats(kcdc_bw_batcher* t, double* out, int n) {
             busy += e0 - s0;
             span = hi - iv[0].first;
         }
-        const double d[13] = {static_cast<double>(b->rounds), static_cast<double>(b->shipped_bytes), b->t_submit,
+        const double d[16] = {static_cast<double>(b->rounds), static_cast<double>(b->shipped_bytes), b->t_submit,
                               b->t_wait, b->t_gather, b->t_kernel, span * 1e-3, busy * 1e-3,
-                              b->t_seg[0], b->t_seg[1], b->t_seg[2], b->t_seg[3], b->t_seg[4]};
-        for (int i = 0; i < 13; i++) v[i] = (i == 6 || i == 7) ? std::max(v[i], d[i]) : v[i] + d[i];
+                              b->t_seg[0], b->t_seg[1], b->t_seg[2], b->t_seg[3], b->t_seg[4],
+                              b->t_idle, b->w_capped_ns.load() * 1e-9, b->w_block_ns.load() * 1e-9};
+        for (int i = 0; i < 16; i++) v[i] = (i == 6 || i == 7) ? std::max(v[i], d[i]) : v[i] + d[i];
     }
-    for (int i = 0; i < n && i < 13; i++) out[i] = v[i];
-    return 13;
+    for (int i = 0; i < n && i < 16; i++) out[i] = v[i];
+    return 16;
 }
