@@ -181,7 +181,8 @@ int64_t kcdc_bw_rounds(const kcdc_bw_batcher* b); /* rounds shipped so far (test
  * writers' blocks, placing them in the arenas, issuing the gather, waiting for the previous round,
  * issuing the split), then the round thread's seconds waiting for a round's worth of staged bytes,
  * and the writers' seconds (summed over writers) blocked on their staging cap and getting a pinned
- * staging block.  Returns 16. */
+ * staging block, then the pinned blocks allocated because the pool was empty and the round
+ * thread's seconds acquiring the batcher's mutex to apply a finished round.  Returns 18. */
 int kcdc_bw_stats(kcdc_bw_batcher* b, double* out, int n);
 
 /* ------------------------------------------------------ batch (hot path)

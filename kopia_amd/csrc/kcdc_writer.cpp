@@ -144,6 +144,12 @@ struct BwDev {
     std::condition_variable cv_done;   // finishing writers: a round completed
     std::vector<kcdc_bw*> open;        // writers not yet freed
     std::vector<uint8_t*> pool;        // free pinned blocks
+    // arenas of freed writers (arena, spare), reused by the next kcdc_bw_open: an uploader opens a
+    // writer per object, and hipMalloc/hipFree of two arenas per object would serialise on the device
+    std::vector<std::pair<uint8_t*, uint8_t*>> arenas;
+    size_t keep_arenas() const {  // at least 64 writers' worth, or up to 32 GiB of HBM
+        return std::max<size_t>(64, (32ull << 30) / (2 * arena_cap));
+    }
     std::atomic<uint64_t> staged{0};   // unshipped bytes over all writers
     std::atomic<int64_t> since{0};     // when `staged` last became nonzero (steady ns)
     std::atomic<uint32_t> capped{0};   // writers blocked on their staging cap (a round is due)
@@ -174,11 +180,17 @@ struct BwDev {
     double t_idle = 0;                             // round thread: waiting for a round's worth of bytes
     std::atomic<int64_t> w_capped_ns{0};           // writers: blocked on their staging cap (summed)
     std::atomic<int64_t> w_block_ns{0};            // writers: getting a pinned block (summed)
+    std::atomic<uint64_t> pool_misses{0};          // pinned blocks allocated (the pool was empty)
+    double t_lock = 0;                             // round thread: acquiring mu to apply a round
 
     ~BwDev() {
         if (algo->kind == kFixed) return;
         Guard g(device);
         for (uint8_t* b : pool) (void)hipHostFree(b);
+        for (auto& a : arenas) {
+            (void)hipFree(a.first);
+            (void)hipFree(a.second);
+        }
         for (Meta& m : meta) {
             if (m.d) (void)hipFree(m.d);
             if (m.h) (void)hipHostFree(m.h);
@@ -191,12 +203,16 @@ struct BwDev {
         if (copy) (void)hipStreamDestroy(copy);
         if (stream) (void)hipStreamDestroy(stream);
     }
-    uint8_t* get_block() {  // mu held
-        if (!pool.empty()) {
-            uint8_t* b = pool.back();
-            pool.pop_back();
-            return b;
+    uint8_t* get_block() {  // mu not held: a new pinned block is allocated outside it
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!pool.empty()) {
+                uint8_t* b = pool.back();
+                pool.pop_back();
+                return b;
+            }
         }
+        pool_misses++;
         void* p = nullptr;
         Guard g(device);
         return hipHostMalloc(&p, kBlock, hipHostMallocDefault) == hipSuccess ? static_cast<uint8_t*>(p) : nullptr;
@@ -234,6 +250,9 @@ struct kcdc_bw {
     bool final_sent = false;     // the finishing region is issued
     std::vector<uint64_t> ready; // final cuts not taken yet (batcher mu)
     size_t ready_head = 0;
+    // cuts ever pushed to / taken from `ready` (written under the batcher mu): kcdc_bw_cuts returns
+    // without that mutex when they are equal, so polling writers do not contend with the round thread
+    std::atomic<uint64_t> ready_pushed{0}, ready_taken{0};
     bool done = false;           // (batcher mu)
     uint64_t fixed_next = 0;     // FIXED names: the next cut (no data is read)
 };
@@ -257,6 +276,7 @@ struct Round {
     std::vector<uint64_t> cbase;
     uint64_t fresh = 0;
     bool live = false;
+    bool recycled = false;  // its retired blocks are back in the pool
 };
 }  // namespace
 
@@ -296,7 +316,9 @@ void BwDev::loop() {
         }
         const uint32_t n = r.n;
         const uint64_t* hp = M.h;
+        const auto l0 = std::chrono::steady_clock::now();
         std::lock_guard<std::mutex> lk(mu);
+        t_lock += std::chrono::duration<double>(std::chrono::steady_clock::now() - l0).count();
         shipped_bytes += r.fresh;
         for (uint32_t k = 0; k < n; k++) {
             Job& j = r.jobs[k];
@@ -309,6 +331,7 @@ void BwDev::loop() {
             const uint64_t* c = hp + 6 * n + r.cbase[k];
             const uint64_t fin = j.finishing ? cnt : (cnt ? cnt - 1 : 0);
             for (uint64_t t = 0; t < fin; t++) w->ready.push_back(w->tail_pos + c[t]);
+            w->ready_pushed.fetch_add(fin, std::memory_order_release);
             if (fin) w->frontier = w->tail_pos + c[fin - 1];
             w->launched_to = j.to;
             w->tail_pos = w->frontier >= kHist ? w->frontier - kHist : 0;
@@ -318,6 +341,16 @@ void BwDev::loop() {
         return KCDC_OK;
     };
 
+    // The round in flight's pinned blocks go back to the pool once its gather has copied them (the
+    // split reads the arenas), not when its cuts arrive.  mu held.
+    auto recycle = [&](Round& r) {
+        if (!r.live || r.recycled || hipEventQuery(meta[r.m].gathered) != hipSuccess) return;
+        for (Job& j : r.jobs) {
+            for (uint8_t* blk : j.retire) pool.push_back(blk);
+            j.retire.clear();
+        }
+        r.recycled = true;
+    };
     std::unique_lock<std::mutex> lk(mu);
     auto last = std::chrono::steady_clock::now();
     for (;;) {
@@ -331,6 +364,7 @@ void BwDev::loop() {
         bool timed_out = false;
         const auto idle0 = std::chrono::steady_clock::now();
         while (!work() && !timed_out) {
+            recycle(inflight);
             if (inflight.live) {
                 if (hipEventQuery(meta[inflight.m].done) == hipSuccess) {
                     lk.unlock();
@@ -363,6 +397,7 @@ void BwDev::loop() {
             if (stop) break;
             continue;
         }
+        recycle(inflight);
         // ---- collect round R: every writer's staged bytes (writers keep writing meanwhile)
         const auto t0 = std::chrono::steady_clock::now();
         Round R;
@@ -739,8 +774,17 @@ extern "C" kcdc_bw* kcdc_bw_open_hint(kcdc_bw_batcher* t, uint64_t size_hint) {
     if (b->algo->kind != kFixed) {
         Guard g(b->device);
         void *p = nullptr, *q = nullptr;
-        hipError_t e = hipMalloc(&p, b->arena_cap);
-        if (e == hipSuccess) e = hipMalloc(&q, b->arena_cap);
+        {
+            std::lock_guard<std::mutex> lk(b->mu);
+            if (!b->arenas.empty()) {
+                p = b->arenas.back().first;
+                q = b->arenas.back().second;
+                b->arenas.pop_back();
+            }
+        }
+        hipError_t e = hipSuccess;
+        if (!p) e = hipMalloc(&p, b->arena_cap);
+        if (e == hipSuccess && !q) e = hipMalloc(&q, b->arena_cap);
         if (e != hipSuccess) {
             if (p) (void)hipFree(p);
             b->load -= size_hint;
@@ -778,6 +822,7 @@ extern "C" int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len) {
         }
         while (w->fixed_next <= w->written) {
             w->ready.push_back(w->fixed_next);
+            w->ready_pushed.fetch_add(1, std::memory_order_release);
             w->fixed_next += b->algo->avg;
         }
         return KCDC_OK;
@@ -800,11 +845,7 @@ extern "C" int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len) {
         if (w->blocks.empty() || w->blocks.back().end == kBlock) {
             wl.unlock();  // lock order: the batcher's mutex is never taken under a writer's
             const int64_t g0 = now_ns();
-            uint8_t* blk;
-            {
-                std::lock_guard<std::mutex> lk(b->mu);
-                blk = b->get_block();
-            }
+            uint8_t* blk = b->get_block();
             b->w_block_ns += now_ns() - g0;
             wl.lock();
             if (!blk) return set_error(KCDC_ENOMEM, "pinned staging block");
@@ -837,11 +878,15 @@ extern "C" int64_t kcdc_bw_cuts(kcdc_bw* w, uint64_t* out, uint64_t cap) {
     Inside in(w->top);
     if (!in.ok) return set_error(KCDC_EINVAL, "writer batcher closed");
     BwDev* b = w->b;
+    if (w->ready_pushed.load(std::memory_order_acquire) == w->ready_taken.load(std::memory_order_relaxed) &&
+        !b->error)
+        return 0;
     std::lock_guard<std::mutex> lk(b->mu);
     const uint64_t avail = w->ready.size() - w->ready_head;
     const uint64_t k = std::min<uint64_t>(avail, cap);
     if (k) std::memcpy(out, w->ready.data() + w->ready_head, k * 8);
     w->ready_head += k;
+    w->ready_taken.fetch_add(k, std::memory_order_relaxed);
     if (w->ready_head == w->ready.size()) {
         w->ready.clear();
         w->ready_head = 0;
@@ -859,7 +904,10 @@ extern "C" int kcdc_bw_finish(kcdc_bw* w) {
         std::lock_guard<std::mutex> lk(b->mu);
         if (w->finishing) return KCDC_OK;
         const uint64_t last = w->ready.empty() ? w->fixed_next - b->algo->avg : w->ready.back();
-        if (w->written > last) w->ready.push_back(w->written);  // the trailing chunk
+        if (w->written > last) {  // the trailing chunk
+            w->ready.push_back(w->written);
+            w->ready_pushed.fetch_add(1, std::memory_order_release);
+        }
         w->finishing = w->done = true;
         return KCDC_OK;
     }
@@ -889,7 +937,11 @@ extern "C" void kcdc_bw_free(kcdc_bw* w) {
         b->load -= std::min<uint64_t>(b->load.load(), w->counted);
         for (Blk& bk : w->blocks) b->pool.push_back(bk.p);
         b->open.erase(std::find(b->open.begin(), b->open.end(), w));
-        if (w->arena) {
+        if (w->arena && w->done && !b->error && b->arenas.size() < b->keep_arenas()) {
+            // its last round has completed (finish waited for it), so no gather, compaction or
+            // split still touches these arenas
+            b->arenas.emplace_back(w->arena, w->spare);
+        } else if (w->arena) {
             Guard g(b->device);
             (void)hipStreamSynchronize(b->copy);
             (void)hipStreamSynchronize(b->stream);
@@ -916,7 +968,7 @@ extern "C" int kcdc_bw_stats(kcdc_bw_batcher* t, double* out, int n) {
     // per device: the device span from its first round's start to its last one's end, and the
     // part of it in which a gather or a split ran (their union: overlapped rounds count once);
     // over devices: counts and host seconds add up, spans and busy times are the maximum
-    double v[16] = {0};
+    double v[18] = {0};
     for (BwDev* b : t->devs) {
         std::lock_guard<std::mutex> lk(b->mu);
         std::vector<std::pair<float, float>> iv = b->busy;
@@ -937,12 +989,13 @@ extern "C" int kcdc_bw_stats(kcdc_bw_batcher* t, double* out, int n) {
             busy += e0 - s0;
             span = hi - iv[0].first;
         }
-        const double d[16] = {static_cast<double>(b->rounds), static_cast<double>(b->shipped_bytes), b->t_submit,
+        const double d[18] = {static_cast<double>(b->rounds), static_cast<double>(b->shipped_bytes), b->t_submit,
                               b->t_wait, b->t_gather, b->t_kernel, span * 1e-3, busy * 1e-3,
                               b->t_seg[0], b->t_seg[1], b->t_seg[2], b->t_seg[3], b->t_seg[4],
-                              b->t_idle, b->w_capped_ns.load() * 1e-9, b->w_block_ns.load() * 1e-9};
-        for (int i = 0; i < 16; i++) v[i] = (i == 6 || i == 7) ? std::max(v[i], d[i]) : v[i] + d[i];
+                              b->t_idle, b->w_capped_ns.load() * 1e-9, b->w_block_ns.load() * 1e-9,
+                              static_cast<double>(b->pool_misses.load()), b->t_lock};
+        for (int i = 0; i < 18; i++) v[i] = (i == 6 || i == 7) ? std::max(v[i], d[i]) : v[i] + d[i];
     }
-    for (int i = 0; i < n && i < 16; i++) out[i] = v[i];
-    return 16;
+    for (int i = 0; i < n && i < 18; i++) out[i] = v[i];
+    return 18;
 }

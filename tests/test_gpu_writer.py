@@ -85,6 +85,25 @@ def test_sixty_four_writers_64k_slices(gpu):
     assert rounds >= 4
 
 
+@pytest.mark.parametrize("name", ["DYNAMIC-1M-BUZHASH", "DYNAMIC-1M-RABINKARP"])
+def test_objects_one_after_another_reuse_arenas(gpu, name):
+    """An uploader opens a writer per object: a freed writer's arenas go to the next one
+    (kcdc_bw_free/kcdc_bw_open).  Long objects first, then short ones whose arena still holds the
+    previous object's bytes beyond their end, then long again: every object's cuts exact."""
+    b = WriterBatcher(name, round_bytes=8 << 20)
+    sizes = [9 << 20, 7 << 20, 3000, 0, 65, 1 << 20, (1 << 20) + 17, 5 << 20, 200_000, 11 << 20]
+    try:
+        for rep in range(2):
+            for i, n in enumerate(sizes):
+                d = coracle.gen_stream(SEED, 500 + 16 * rep + i, n)
+                w = b.open()
+                got = _feed(w, d, ["64k", "rand", "whole"][i % 3], np.random.default_rng(i))
+                w.close()
+                assert got == coracle.split_stream(name, d).tolist(), f"object {rep}/{i} ({n} B)"
+    finally:
+        b.close()
+
+
 def test_device_set_two_logical_devices(gpu):
     """kcdc_bw_batcher_new_devices over [0, 0]: two device batchers (own round threads, streams
     and arenas) on the one GPU, 64 writers with size hints spread over both, every object's cuts

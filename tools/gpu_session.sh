@@ -14,6 +14,7 @@
 #   prof:TAG:ARGS    the same for bench.py ARGS (commas for spaces), files named TAG_*
 #   kbench:ARGS      tools/kbench.py ARGS (same-process A/B of build/variants/*.so)
 #   writer:ARGS      build/writer_bench ARGS (commas for spaces)
+#   writerpin:CPUS:ARGS  the same under taskset -c CPUS (threads confined to the CPU quota)
 #   valu:ARGS        build/valu_rate ARGS (tools/valu_rate.hip: the VALU rate table, or "rk": the
 #                    Rabin-Karp hot loop alone over config 2's bytes)
 #   sq:TAG:ARGS      SQ counters (VALU/LDS/wait) of bench.py ARGS, one --pmc pass
@@ -64,6 +65,10 @@ for step in "$@"; do
       a=$(args "${step#writer:}"); t=$(echo "$a" | tr -c 'A-Za-z0-9' '_')
       timeout -k 10 300 ./build/writer_bench $a > "$OUT/writer_$t.json" 2> "$OUT/writer_$t.err" || exit $?
       cat "$OUT/writer_$t.json" ;;
+    writerpin:*)
+      r=${step#writerpin:}; cpus=${r%%:*}; a=$(args "${r#*:}"); t=$(echo "$cpus $a" | tr -c 'A-Za-z0-9' '_')
+      timeout -k 10 300 taskset -c "$cpus" ./build/writer_bench $a > "$OUT/writerpin_$t.json" 2> "$OUT/writerpin_$t.err" || exit $?
+      cat "$OUT/writerpin_$t.json" ;;
     valu:*)
       a=$(args "${step#valu:}"); t=$(echo "$a" | tr -c 'A-Za-z0-9' '_')
       timeout -k 10 300 ./build/valu_rate $a > "$OUT/valu_$t.log" 2>&1 || exit $?
