@@ -40,6 +40,7 @@ using namespace kcdc;
 namespace {
 
 constexpr size_t kBlock = 4u << 20;    // pinned staging block
+constexpr size_t kSlabBlocks = 8;      // blocks per pinned allocation
 constexpr uint64_t kHist = 64;         // window history kept before a writer's last final cut
 constexpr uint32_t kTask = 64u << 10;  // gather: bytes per workgroup
 
@@ -143,7 +144,8 @@ struct BwDev {
     std::condition_variable cv_round;  // round thread: work arrived
     std::condition_variable cv_done;   // finishing writers: a round completed
     std::vector<kcdc_bw*> open;        // writers not yet freed
-    std::vector<uint8_t*> pool;        // free pinned blocks
+    std::vector<uint8_t*> pool;        // free pinned blocks (carved from slabs)
+    std::vector<uint8_t*> slabs;       // pinned allocations of kSlabBlocks blocks each
     // arenas of freed writers (arena, spare), reused by the next kcdc_bw_open: an uploader opens a
     // writer per object, and hipMalloc/hipFree of two arenas per object would serialise on the device
     std::vector<std::pair<uint8_t*, uint8_t*>> arenas;
@@ -180,13 +182,13 @@ struct BwDev {
     double t_idle = 0;                             // round thread: waiting for a round's worth of bytes
     std::atomic<int64_t> w_capped_ns{0};           // writers: blocked on their staging cap (summed)
     std::atomic<int64_t> w_block_ns{0};            // writers: getting a pinned block (summed)
-    std::atomic<uint64_t> pool_misses{0};          // pinned blocks allocated (the pool was empty)
+    std::atomic<uint64_t> pool_misses{0};          // pinned slabs allocated (the pool was empty)
     double t_lock = 0;                             // round thread: acquiring mu to apply a round
 
     ~BwDev() {
         if (algo->kind == kFixed) return;
         Guard g(device);
-        for (uint8_t* b : pool) (void)hipHostFree(b);
+        for (uint8_t* s : slabs) (void)hipHostFree(s);
         for (auto& a : arenas) {
             (void)hipFree(a.first);
             (void)hipFree(a.second);
@@ -203,7 +205,7 @@ struct BwDev {
         if (copy) (void)hipStreamDestroy(copy);
         if (stream) (void)hipStreamDestroy(stream);
     }
-    uint8_t* get_block() {  // mu not held: a new pinned block is allocated outside it
+    uint8_t* get_block() {  // mu not held: new pinned blocks are allocated outside it
         {
             std::lock_guard<std::mutex> lk(mu);
             if (!pool.empty()) {
@@ -212,10 +214,17 @@ struct BwDev {
                 return b;
             }
         }
+        // a slab of kSlabBlocks at once: a hipHostMalloc costs milliseconds under load, and the
+        // staging peak grows in steps of many blocks when many writers are open
         pool_misses++;
         void* p = nullptr;
         Guard g(device);
-        return hipHostMalloc(&p, kBlock, hipHostMallocDefault) == hipSuccess ? static_cast<uint8_t*>(p) : nullptr;
+        if (hipHostMalloc(&p, kSlabBlocks * kBlock, hipHostMallocDefault) != hipSuccess) return nullptr;
+        uint8_t* s = static_cast<uint8_t*>(p);
+        std::lock_guard<std::mutex> lk(mu);
+        slabs.push_back(s);
+        for (size_t i = 1; i < kSlabBlocks; i++) pool.push_back(s + i * kBlock);
+        return s;
     }
     void loop();
 };
