@@ -697,6 +697,11 @@ constexpr uint32_t kMaxPipeGrid = 256;
 constexpr size_t kQHeaderBytes = 8192;
 // Header words 1792.. : debug-build failure record (pcheck, KCDC_DEBUG_CHECKS).
 [[maybe_unused]] constexpr int kQStat = 1792;
+// Header words 1664.. : held-ticket audit (help tasks) -- [0] help tasks whose ticket register
+// disagreed with the ticket's memory copy, [1] [2] the first such pair (register, memory);
+// diagnostic builds (KCDC_HELP_DIAG) also [3] a bitmask of wave-uniform control values seen
+// lane-divergent at the loop top and [4] the count of such observations.
+constexpr int kQDiag = 1664;
 // A waiting wave gives up (error word; a stream it held a ticket for is then reported failed)
 // only after this many polls with no stream finishing: a bug guard that keeps the kernel
 // bounded, >= 60 s; no correct launch waits that long (one wave scans >= 6 GB/s).
@@ -1107,6 +1112,42 @@ __device__ __forceinline__ void help_post(const BatchArgs& a, int lane, uint32_t
         add_agent(a.queue + kQHelp, 1u);
     }
 }
+// The ticket a wave holds while it runs help tasks: kept in memory (word 2 of its help slot's
+// claim line) from the moment the help task is taken, and taken back from there when the task
+// ends, besides the copy in the task's cap field.  held_get audits the two (header words kQDiag..).
+#ifndef KCDC_HELP_MIRROR
+#define KCDC_HELP_MIRROR 1
+#endif
+__device__ __forceinline__ void held_put(const BatchArgs& a, int lane, uint32_t me, uint32_t t) {
+    if (lane == 0)
+        __hip_atomic_store((gu64*)(help_claim(a, me) + 2), 0x100000000ull | t, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t held_get(const BatchArgs& a, int lane, uint32_t me, uint32_t reg) {
+    const uint64_t raw = ld_agent64(help_claim(a, me) + 2);
+    const uint32_t t = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(raw), 0));
+    if (t != reg && lane == 0) {
+        if (atomicAdd(a.queue + kQDiag, 1u) == 0) {
+            a.queue[kQDiag + 1] = reg;
+            a.queue[kQDiag + 2] = t;
+        }
+    }
+    return KCDC_HELP_MIRROR ? t : reg;
+}
+#ifndef KCDC_HELP_DIAG
+#define KCDC_HELP_DIAG 0
+#endif
+// Diagnostic builds: bit `bit` when v is not the same in every lane (a wave-uniform control value
+// held lane-divergent).
+__device__ __forceinline__ uint32_t divergent_bit(uint32_t v, int bit) {
+    return __ballot(v != static_cast<uint32_t>(__shfl(static_cast<int>(v), 0))) != 0 ? 1u << bit : 0u;
+}
+__device__ __forceinline__ void diag_record(const BatchArgs& a, int lane, uint32_t bits) {
+    if (bits && lane == 0) {
+        atomicOr(a.queue + kQDiag + 3, bits);
+        atomicAdd(a.queue + kQDiag + 4, 1u);
+    }
+}
 // Owner whose claim failed: the helpers hold tiles [k0, K).  Returns the region's first
 // candidate (coordinate) among them, -1 if they have none, or -2 - k when tile k is still
 // pending after kHelpWaitTicks (the owner then scans from tile k itself).
@@ -1415,7 +1456,8 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             const uint32_t held = t;
             const int r = presolve(a, lane, held, cur, kDmaWaves, me, a.help != nullptr && claim == 0xFFFFFFFFu);
             if (r == 0) return false;
-            if (r == 3) {  // a help task; the ticket stays held (in cap, unused by help tasks)
+            if (r == 3) {  // a help task; the ticket stays held (in cap, unused by help tasks, and in memory)
+                held_put(a, lane, me, held);
                 cur.cap = held;
                 uniformize(cur);
                 return true;
@@ -1459,6 +1501,9 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
     }
     bool issued = false;  // this tile's warm piece + step 0 are in flight
     for (;;) {
+#if KCDC_HELP_DIAG
+        diag_record(a, lane, divergent_bit(need_take, 0) | divergent_bit(take_t, 1) | divergent_bit(issued, 2));
+#endif
         // The one blocking take site (inlined once: presolve and try_steal are large).
         if (need_take) {
             if (!take_blocking(take_t, take_backlog, take_claim)) KCDC_PRET;
@@ -1466,6 +1511,12 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             issued = false;
             hs |= kHsNeedPub;
         }
+#if KCDC_HELP_DIAG
+        diag_record(a, lane, divergent_bit(hs, 3) | divergent_bit(hep, 4) | divergent_bit(cur.sid, 5) |
+                                 divergent_bit(static_cast<uint32_t>(cur.cap), 6) |
+                                 divergent_bit(static_cast<uint32_t>(cur.ct), 7) |
+                                 divergent_bit(static_cast<uint32_t>(budget), 8));
+#endif
         uniformize(cur);
         if (!pcheck(a, lane, cur, 0xFFFFFFFFu, 5)) return;
         const bool is_help = (cur.sid & kHelpBit) != 0;
@@ -1634,7 +1685,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the post, or a dropped prefetch
             need_take = true;
-            take_t = static_cast<uint32_t>(cur.cap);
+            take_t = held_get(a, lane, me, static_cast<uint32_t>(cur.cap));
             take_backlog = 0;
             take_claim = 0xFFFFFFFFu;
             continue;
@@ -2087,6 +2138,9 @@ __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int 
 // Rabin-Karp lane segments: twice the buzhash cap (warm-up vs tile overshoot; 2 vs 1: 4M 2.542 vs
 // 2.554 ms, 128K 5.536 vs 5.643 ms, profiles/r03/rk/kbench_lmul_*.log)
 constexpr int64_t kRkLaneMul = 2;
+// Intra-region help as in split_batch_pipe_kernel (the same help slots, claim words and rows; hep,
+// hs and the kHs* flags mean the same).  An own tile is T = 64 x rk_cap bytes; a help task scans
+// one in two sub-tiles of rk_cap / 2 bytes per lane.
 __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk_kernel(BatchArgs a) {
     __shared__ RkTables smt;
     __shared__ RkSlots smslots;
@@ -2096,9 +2150,16 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
     uint8_t* sl = smslots.b[wave][0];
     const uint32_t sl32 = lds_addr(sl);
     const int64_t mx = static_cast<int64_t>(a.max_size);
+    const uint32_t me = blockIdx.x * kRkWaves + wave;  // this wave's help slot
+    const int64_t rk_cap = kRkLaneMul * static_cast<int64_t>(a.lane_cap);  // lane bytes of an own tile (>= 512)
 
     PStream cur;
     int64_t budget = kNoYield;
+    uint32_t hep = 0, hs = 0;
+    constexpr uint32_t kHsPub = 1u << 16, kHsNeedPub = 1u << 17, kHsHelped = 1u << 18;
+    hs = kHsNeedPub;
+    auto hK = [&] { return hs & 0xFFu; };
+    auto htile = [&] { return (hs >> 8) & 0xFFu; };
     auto take_blocking = [&](uint32_t t, int64_t backlog_hint, uint32_t claim) -> bool {
         for (;;) {
             int64_t backlog = backlog_hint;
@@ -2108,8 +2169,14 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
                 backlog = static_cast<int64_t>(ht >> 32) - static_cast<int64_t>(t) - 1;
             }
             const uint32_t held = t;
-            const int r = presolve(a, lane, held, cur, kRkWaves, 0u, false);
+            const int r = presolve(a, lane, held, cur, kRkWaves, me, a.help != nullptr && claim == 0xFFFFFFFFu);
             if (r == 0) return false;
+            if (r == 3) {  // a help task; the ticket stays held (in cap, unused by help tasks, and in memory)
+                held_put(a, lane, me, held);
+                cur.cap = held;
+                uniformize(cur);
+                return true;
+            }
             t = 0xFFFFFFFFu;
             if (claim != 0xFFFFFFFFu) {
                 const bool requeued = bcast(claim) == 2u;
@@ -2145,26 +2212,54 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
     }
     bool issued = false;  // this tile's warm fill is in flight
     for (;;) {
+#if KCDC_HELP_DIAG
+        diag_record(a, lane, divergent_bit(need_take, 0) | divergent_bit(take_t, 1) | divergent_bit(issued, 2));
+#endif
         if (need_take) {
             if (!take_blocking(take_t, take_backlog, take_claim)) return;
             need_take = false;
             issued = false;
+            hs |= kHsNeedPub;
         }
+#if KCDC_HELP_DIAG
+        diag_record(a, lane, divergent_bit(hs, 3) | divergent_bit(hep, 4) | divergent_bit(cur.sid, 5) |
+                                 divergent_bit(static_cast<uint32_t>(cur.cap), 6) |
+                                 divergent_bit(static_cast<uint32_t>(cur.ct), 7) |
+                                 divergent_bit(static_cast<uint32_t>(budget), 8));
+#endif
         uniformize(cur);
         if (!pcheck(a, lane, cur, 0xFFFFFFFFu, 5)) return;
+        const bool is_help = (cur.sid & kHelpBit) != 0;
         int64_t lo, hi;
         pregion(a, cur, lo, hi);
-        const RkGeom g = rk_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n, kRkLaneMul * a.lane_cap);
+        const int64_t lcap = is_help ? rk_cap / 2 : rk_cap;
+        const RkGeom g = rk_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n, lcap);
         const int64_t ct = cur.ct, ct_next = ct + kWave * g.L;
         const bool last_of_region = ct_next > hi;
-        const bool budget_out = budget - kWave * g.L <= 0;
+        // A region new to this wave: publish it when it is long enough to share.
+        if ((hs & kHsNeedPub) && !is_help) {
+            const int64_t T = kWave * rk_cap;
+            const uint32_t K = static_cast<uint32_t>((hi - ct + T) / T);
+            hs = 0;
+            if (a.help && K >= kHelpMinTiles && K <= static_cast<uint32_t>(kHelpTiles)) {
+                hep++;
+                hs = kHsPub | K;
+                help_publish(a, lane, me, hep, cur, ct, hi, K, T);
+            }
+        }
+        // The owner's claim on its next tile: an atomic add on its slot's bottom after fill 1's
+        // DMA, its value consumed at fill 2 (after that fill's vmcnt wait, before its DMA), so
+        // no compiler-visible load is in flight across a DMA.
+        const bool claim_next_r = (hs & kHsPub) && !is_help && !last_of_region && htile() + 1u < hK();
+        const bool budget_out = !is_help && !(hs & kHsHelped) && budget - kWave * g.L <= 0;
         bool ends_nocand = false;
-        if (last_of_region) {
+        if (!is_help && last_of_region) {
             const int64_t s2 = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;
             ends_nocand = s2 >= cur.n || s2 + static_cast<int64_t>(a.min_size) - 1 >= cur.n;
         }
-        const bool switching = budget_out || ends_nocand;
+        const bool switching = !is_help && (budget_out || ends_nocand);
         const bool reserve = budget_out && !ends_nocand;
+        const bool claim_next = claim_next_r && !switching;
         uint64_t ht_raw = 0;
         if (switching) ht_raw = qht_add(a, lane, 1);  // the next stream's ticket
         uint32_t ht_lo = static_cast<uint32_t>(ht_raw), ht_hi = static_cast<uint32_t>(ht_raw >> 32);
@@ -2192,6 +2287,15 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
         }
         uint64_t pe_raw = 0;
         bool res_issued = false, next_issued = false, entry_issued = false;
+        bool claim_ok = false, claim_known = !claim_next;
+        uint64_t claim_raw = 0;
+        auto claim_decode = [&]() {  // the claim word before this tile's add (+1 = after it)
+            const uint64_t cw = qht_value(static_cast<uint32_t>(claim_raw), static_cast<uint32_t>(claim_raw >> 32)) + 1ull;
+            const uint32_t top = static_cast<uint32_t>(cw >> 20) & 0xFFFFFu, bot = static_cast<uint32_t>(cw) & 0xFFFFFu;
+            claim_ok = static_cast<uint32_t>(cw >> 40) == hep && bot <= top;
+            if (top < hK()) hs |= kHsHelped;
+            claim_known = true;
+        };
         // After the tile's last fill: the next tile's warm fill, or the next stream's entry.
         auto refill_last = [&]() {
             if (reserve && !res_issued) {  // this stream's ring entry, reserved late
@@ -2201,8 +2305,8 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             if (switching) {
                 pentry_dma(a, lane, tk, sl32);
                 entry_issued = true;
-            } else if (!last_of_region) {  // the next tile has its own geometry
-                const RkGeom gn = rk_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n, kRkLaneMul * a.lane_cap);
+            } else if (!last_of_region && (!claim_next || claim_ok)) {  // the next tile has its own geometry
+                const RkGeom gn = rk_geom(ct_next, hi, cur.abase, cur.off0, cur.off0 + cur.n, lcap);
                 rk_dma_warm(gn.ld, sl32, ct_next, gn.L, lane);
                 next_issued = true;
             }
@@ -2211,10 +2315,14 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
         // After line fill f is read: issue what the slot takes next (fill f+1, or after the
         // last fill the next tile's warm fill / the next stream's queue entry).
         auto refill = [&](int f) {
+            if (claim_next && f == 2) claim_decode();
             if (f < 2 * g.K)
                 rk_dma_line(g.ld, sl32, ct, g.L, f + 1, lane);
             else
                 refill_last();
+            if (claim_next && f == 1 && lane == 0)
+                claim_raw = __hip_atomic_fetch_add((gu64*)help_claim(a, me), 1ull, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
         };
         // Hit check of one chain's 64 bytes at `rel` from its start (state before: h0/l0):
         // the chain's first candidate in [lo, hi].  The coordinate is formed only here, from
@@ -2242,31 +2350,77 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
         const int64_t c0 = ct + lane * g.L;
         const int64_t found = found_a >= 0 ? c0 + found_a : found_b >= 0 ? c0 + g.L / 2 + found_b : -1;
         // ---- end of tile
+        if (!claim_known) {  // one-line tiles (K = 1) consume the claim here
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            claim_decode();
+        }
         if (reserve && !res_issued) {
             pe_raw = qht_add(a, lane, 1ull << 32);
             res_issued = true;
         }
         const uint64_t hit = __ballot(found >= 0);
+        if (is_help) {
+            bool done = true;
+            if (hit || last_of_region) {  // post the tile's first candidate to its owner's row
+                int64_t f = -1;
+                if (hit) f = static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, __builtin_ctzll(hit)))));
+                help_post(a, lane, static_cast<uint32_t>(cur.cb), cur.epoch, static_cast<uint32_t>(cur.cnt), cur.s, f);
+            } else {  // the next sub-tile (prefetched), unless the owner has closed the region
+                const uint64_t w = ld_agent64(help_claim(a, static_cast<uint32_t>(cur.cb)));
+                done = static_cast<uint32_t>(qht_value(static_cast<uint32_t>(w), static_cast<uint32_t>(w >> 32)) >> 40) !=
+                       cur.epoch;
+            }
+            if (!done) {
+                cur.ct = ct_next;
+                issued = next_issued;
+                continue;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the post, or a dropped prefetch
+            need_take = true;
+            take_t = held_get(a, lane, me, static_cast<uint32_t>(cur.cap));
+            take_backlog = 0;
+            take_claim = 0xFFFFFFFFu;
+            continue;
+        }
         bool region_changed = true;
-        bool live;
         const int64_t forced = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;
+        int64_t cut = -1;  // this region's cut, once known
         if (hit) {
             const int first = __builtin_ctzll(hit);
             const int64_t f = static_cast<int64_t>(uni64(static_cast<uint64_t>(__shfl(found, first))));
-            const int64_t next = f - cur.off0 + 1;
-            emit_cut(a, cur, lane, next);
-            cur.s = next;
-            cur.ct = -1;
+            cut = f - cur.off0 + 1;
         } else if (last_of_region) {  // forced cut at max size (splitter_rabinkarp64.go:60-64) or the end
-            emit_cut(a, cur, lane, forced);
-            cur.s = forced;
-            cur.ct = -1;
+            cut = forced;
+        } else if (claim_next && !claim_ok) {  // the helpers hold the rest of the region
+            const int64_t T = kWave * rk_cap;
+            const int64_t ct0 = ct - static_cast<int64_t>(htile()) * T;  // the published tile 0
+            const int64_t r = help_wait(a, lane, me, hep, htile() + 1u, hK(), ct0);
+            if (r >= 0) {
+                cut = r - cur.off0 + 1;
+            } else if (r == -1) {
+                cut = forced;
+            } else {  // a tile still pending: scan on from it, unshared
+                cur.ct = ct0 + (-2 - r) * T;
+                help_close(a, lane, me, hep);
+                hs = 0;
+                region_changed = false;
+            }
         } else {
             cur.ct = ct_next;
+            hs += 1u << 8;  // htile++
             budget -= kWave * g.L;
             region_changed = false;
         }
-        live = pstream_region(a, cur, lane);
+        if (cut >= 0) {
+            emit_cut(a, cur, lane, cut);
+            cur.s = cut;
+            cur.ct = -1;
+        }
+        if (region_changed) {
+            if (hs & kHsPub) help_close(a, lane, me, hep);
+            hs = kHsNeedPub;
+        }
+        const bool live = pstream_region(a, cur, lane);
         if (!live && lane == 0) {
             a.counts[cur.sid] = cur.cnt;
             add_agent(a.queue + kQDone, 1u);
@@ -2276,6 +2430,8 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             if (next_issued && region_changed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stale prefetch
             continue;
         }
+        if (hs & kHsPub) help_close(a, lane, me, hep);  // a yielded region is not ours to share any more
+        hs = kHsNeedPub;
         if (reserve) {
             const uint32_t pe = static_cast<uint32_t>(
                 qht_value(static_cast<uint32_t>(pe_raw), static_cast<uint32_t>(pe_raw >> 32)) >> 32);
@@ -3439,7 +3595,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         const unsigned need = (s.nstreams + wg_waves - 1) / wg_waves;
         // The buzhash pipe kernel takes the whole chip even for a few streams: the waves without
         // a stream help scan the owners' regions (help slots).
-        const bool helpers = algo.kind == kBuzhash && !g_test.no_help;
+        const bool helpers = (algo.kind == kBuzhash || algo.kind == kRabinKarp) && !g_test.no_help;
         unsigned grid = helpers || need >= cus ? cus : need;
         if (grid > dev::kMaxPipeGrid) grid = dev::kMaxPipeGrid;  // one claim flag per workgroup
         uint64_t ring = 1;
@@ -3900,7 +4056,8 @@ extern "C" int kcdc_test_set(int32_t key, int64_t value) {
 }
 
 extern "C" int64_t kcdc_test_queue_stat(int32_t key) {
-    const int word = key == 1 ? dev::kQErr : key == 2 ? dev::kQDone : key == 3 ? dev::kQSteal : key == 4 ? dev::kQHelp : -1;
+    const int word = key == 1 ? dev::kQErr : key == 2 ? dev::kQDone : key == 3 ? dev::kQSteal : key == 4 ? dev::kQHelp
+                   : key >= 5 && key <= 9 ? dev::kQDiag + (key - 5) : -1;
     if (word < 0) return set_error(-22, "unknown queue statistic");
     if (!g_test.last_ws) return set_error(-22, "no pipelined batch launch yet");
     int prev = 0;

@@ -179,3 +179,29 @@ def test_gcm_tables_read_from_lds(xasm):
             seen += 1
             assert len(re.findall(r"^\s*ds_read", body, re.M)) >= 256, f"{name}: table lookups not in LDS"
     assert seen == 4
+
+
+# ---- the ticket a wave holds while it helps
+# Round 4's Rabin-Karp port lost streams because the backend (AMD clang 22.0.0git roc-7.2.0) placed
+# the loop-carried `take_t = cur.cap` copy on only one of the help task's two ending paths: a task
+# that ended because its owner closed the region re-entered the blocking take with the previous
+# take_t (~0, "take a fresh ticket") and its held ticket was never presented again.  Both batch
+# kernels now take the ticket back from memory (held_get) in the help task's end block; the load's
+# value is defined after the paths join, so no per-path copy can carry a stale one.
+HELD_KERNELS = ["_ZN4kcdc3dev23split_batch_pipe_kernelILb1EEEvNS0_9BatchArgsE",
+                "_ZN4kcdc3dev23split_batch_pipe_kernelILb0EEEvNS0_9BatchArgsE",
+                "_ZN4kcdc3dev21split_batch_rk_kernelENS0_9BatchArgsE"]
+
+
+@pytest.mark.parametrize("kernel", HELD_KERNELS)
+def test_help_end_reads_held_ticket_from_memory(dma_asm, kernel):
+    asm, _ = dma_asm
+    sites = []
+    for label, ins in _blocks(asm, kernel):
+        for k, i in enumerate(ins):
+            if i.startswith("global_load_dwordx2") and i.endswith("offset:16 sc1"):
+                dst = i.split()[1].rstrip(",")
+                lo = dst[2:-1].split(":")[0] if dst.startswith("v[") else dst[1:]
+                sites.append((label, any(j.startswith("v_readlane_b32") and f", v{lo}, 0" in j for j in ins[k:])))
+    assert len(sites) == 1, f"expected one held-ticket load in {kernel}, found {sites}"
+    assert sites[0][1], f"the held-ticket load's value is not read back in its own block ({sites[0][0]})"

@@ -31,10 +31,9 @@ class knob:
 
 
 def _helped(name):
-    """Whether waiting waves help this name's batch kernel: buzhash only (the Rabin-Karp kernel's
-    port of the protocol lost streams under yields and is not in the product: DESIGN.md §2.1b).
-    The Rabin-Karp rows still check that few-stream, ragged and dense launches cut exactly."""
-    return "BUZHASH" in name
+    """Whether waiting waves help this name's batch kernel: every dynamic name (buzhash and, since
+    round 5, Rabin-Karp: DESIGN.md §2.1c)."""
+    return "BUZHASH" in name or "RABINKARP" in name
 
 
 def _split(name, data, offs, lens, gpu):
@@ -141,5 +140,28 @@ def test_config2_shape_with_tail_help(gpu, name):
     batch.fill_prng(data, L, ns, L, SEED, first_sid=3000)
     got, helps = _split(name, data, [i * L for i in range(ns)], [L] * ns, gpu)
     cuts, counts = coracle.split_prng_streams(name, SEED, np.arange(3000, 3000 + ns), L, nthreads=16)
+    bad = [i for i in range(ns) if got[i].tolist() != cuts[i, :counts[i]].tolist()]
+    assert not bad, bad[:8]
+
+
+@pytest.mark.parametrize("name", ["DYNAMIC-4M-BUZHASH", "DYNAMIC-4M-RABINKARP"])
+@pytest.mark.parametrize("ns", [2304, 4096])
+def test_many_streams_with_yields(gpu, name, ns):
+    """More streams than launch waves (2,048): visits yield, waves wait on tickets and take help
+    tasks while they hold them.  Round 4's Rabin-Karp port lost streams exactly here (a held ticket
+    never re-presented after a help task: DESIGN.md §2.1c).  Every stream must come back exact, no
+    wave may give up, help must happen, and the held-ticket audit (the ticket's register copy
+    against its memory copy at the end of every help task) must be clean."""
+    import torch
+    L = 4 << 20
+    data = torch.empty(ns * L, dtype=torch.uint8, device=gpu)
+    batch.fill_prng(data, L, ns, L, SEED, first_sid=0)
+    got, helps = _split(name, data, [i * L for i in range(ns)], [L] * ns, gpu)
+    lib = _lib.lib()
+    assert lib.kcdc_test_queue_stat(_lib.STAT_GIVEUPS) == 0
+    assert lib.kcdc_test_queue_stat(_lib.STAT_DONE) == ns
+    assert lib.kcdc_test_queue_stat(_lib.STAT_TICKET_AUDIT) == 0
+    assert helps > 0
+    cuts, counts = coracle.split_prng_streams(name, SEED, np.arange(ns), L, nthreads=16)
     bad = [i for i in range(ns) if got[i].tolist() != cuts[i, :counts[i]].tolist()]
     assert not bad, bad[:8]

@@ -35,7 +35,10 @@ for rep in range(reps):  # until a launch loses a stream (a race shows in some l
         rc = 0
     except Exception as e:  # noqa: BLE001
         rc = repr(e)
-    print("launch", rep, rc, "%.3f s" % (time.time() - t), flush=True)
+    # held-ticket audit and (KCDC_HELP_DIAG builds) lane-divergence record, header words kQDiag..
+    diag = [int(lib.kcdc_test_queue_stat(k)) for k in range(5, 10)]
+    print("launch", rep, rc, "%.3f s" % (time.time() - t), "helps", int(lib.kcdc_test_queue_stat(_lib.STAT_HELPS)),
+          "ticket audit [mismatches, reg, mem]", diag[:3], "divergent [bits, count]", [hex(diag[3]), diag[4]], flush=True)
     if int(lib.kcdc_test_queue_stat(_lib.STAT_DONE)) < ns:
         break
 st = {k: int(lib.kcdc_test_queue_stat(v)) for k, v in (("giveups", _lib.STAT_GIVEUPS), ("done", _lib.STAT_DONE),

@@ -20,7 +20,9 @@
 #   sq:TAG:ARGS      SQ counters (VALU/LDS/wait) of bench.py ARGS, one --pmc pass
 #   trace:ARGS       tools/trace_pipe.py build/libkcdc_trace.so ARGS (per-wave timeline of the batch kernel)
 #   cprof:NAME:KIND  rocprofv3 --kernel-trace --stats of compress_bench.py --name NAME --only KIND (per-kernel time)
-#   probe:ARGS       tools/batch_probe.py ARGS (one bounded launch: queue stats, mismatched streams)
+#   probe:ARGS       tools/batch_probe.py ARGS (one bounded launch: queue stats, mismatched streams;
+#                    PROBE_REPS=n repeats the launch until one loses a stream)
+#   vprobe:V:ARGS    the same with build/variants/libkcdc_V.so
 #   compress:NAMES   tools/compress_bench.py --gib 4 for each compressor name (commas between names)
 set -u
 OUT=gpurun_out/${1:?usage: tools/gpu_session.sh OUT step...}
@@ -81,9 +83,13 @@ for step in "$@"; do
       r=${step#cprof:}; nm=${r%%:*}; kind=${r#*:}
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/cprof_${nm}_$kind" -o run --output-format csv -- python3 tools/compress_bench.py --gib 4 --iters 3 --name "$nm" --only "$kind" > "$OUT/cprof_${nm}_$kind.log" 2>&1 || exit $?
       echo "profiled $nm $kind" ;;
+    vprobe:*)
+      r=${step#vprobe:}; v=${r%%:*}; a=$(args "${r#*:}"); t=$(echo "$v $a" | tr -c 'A-Za-z0-9' '_')
+      KCDC_ALLOW_VARIANT_LIB=1 KCDC_LIB=build/variants/libkcdc_$v.so timeout -k 10 240 python -u tools/batch_probe.py $a > "$OUT/vprobe_$t.log" 2>&1 || { cat "$OUT/vprobe_$t.log"; exit 1; }
+      cat "$OUT/vprobe_$t.log" ;;
     probe:*)
       a=$(args "${step#probe:}"); t=$(echo "$a" | tr -c 'A-Za-z0-9' '_')
-      timeout -k 10 120 python -u tools/batch_probe.py $a > "$OUT/probe_$t.log" 2>&1 || { cat "$OUT/probe_$t.log"; exit 1; }
+      timeout -k 10 240 python -u tools/batch_probe.py $a > "$OUT/probe_$t.log" 2>&1 || { cat "$OUT/probe_$t.log"; exit 1; }
       cat "$OUT/probe_$t.log" ;;
     compress:*)
       for nm in $(args "${step#compress:}"); do
