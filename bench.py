@@ -244,6 +244,13 @@ def _time_passes(fn, min_seconds: float) -> tuple[int, float]:
     return passes, time.perf_counter() - t0
 
 
+def ref_loop(name: str) -> str:
+    """The reference loop a name's CPU baseline restates."""
+    return ("repo/splitter/splitter_rabinkarp64.go:26-67" if "RABINKARP" in name
+            else "repo/splitter/splitter_fixed.go:15-26" if name.startswith("FIXED")
+            else "repo/splitter/splitter_buzhash32.go:26-67")
+
+
 def cpu_baseline(name: str, ns: int, L: int, gpu_cuts: list) -> dict:
     """Rank 0, N=1: the C restatement of the reference Go loop (oracle/cdc_oracle.c, "port")
     timed on this host with 1 thread and with every usable thread, on disjoint streams of
@@ -266,12 +273,12 @@ def cpu_baseline(name: str, ns: int, L: int, gpu_cuts: list) -> dict:
     pa, da = _time_passes(lambda: coracle.split_batch(name, streams, nthreads=nt), 8.0)
     r1 = p1 * len(one) * L / GiB / d1
     ra = pa * ns * L / GiB / da
-    return {"value": round(ra, 3), "unit": "GiB/s", "cores": info["logical_cores"], "kind": "port",
-            "threads_1": round(r1, 3), "threads_all": round(ra, 3), "threads_all_n": nt,
+    return {"value": round(ra, 3), "unit": "GiB/s", "cores": nt, "logical_cores": info["logical_cores"],
+            "kind": "port", "threads_1": round(r1, 3), "threads_all": round(ra, 3), "threads_all_n": nt,
             "cpu_model": info["cpu_model"], "affinity_cpus": info["affinity_cpus"],
             "cgroup_cpu_quota": info["cgroup_cpu_quota"],
             "sample": f"{ns} x {L >> 20} MiB counter-PRNG streams (ids 0..{ns - 1}, the GPU's bytes), {name}; "
-                      f"C restatement of repo/splitter/splitter_buzhash32.go:26-67 (oracle/cdc_oracle.c); "
+                      f"C restatement of {ref_loop(name)} (oracle/cdc_oracle.c); "
                       f"1 thread: {len(one)} streams x {p1} passes in {d1:.1f}s; {nt} threads (every usable CPU of "
                       f"this process): {pa} passes in {da:.1f}s",
             "sample_parity_mismatches": mism, "gen_seconds": round(gen_s, 2)}
@@ -742,7 +749,8 @@ def bench_long(args, comm: Comm):
         want, split_s = coracle.split_prng_stream_blocks(name, SEED, 0, L)
         out["oracle_parity"] = bool(np.array_equal(got, want))
         out["cpu_baseline"] = {"value": round(L / GiB / split_s, 3), "unit": "GiB/s",
-                               "cores": host_cpu_info()["logical_cores"], "cpu_model": host_cpu_info()["cpu_model"],
+                               "cores": 1, "logical_cores": host_cpu_info()["logical_cores"],
+                               "cpu_model": host_cpu_info()["cpu_model"],
                                "kind": "port", "threads_1": round(L / GiB / split_s, 3),
                                "sample": f"the whole {args.long_gib} GiB stream, one sequential NextSplitPoint pass of "
                                          f"oracle/cdc_oracle.c over 256 MiB slices (bytes generated ahead on other "
@@ -779,21 +787,28 @@ def bench_files(args, comm: Comm):
     ptrs = [data.data_ptr() + int(o) for o in offs]
     stream = torch.cuda.current_stream(dev)
 
+    ev = {}
+
     def run(name, steps, warmup):
         warm_up(lambda: batch.split_files_device(name, ptrs, lens, dev, stream), warmup, args.warmup_min_s, dev)
         comm.barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         res = None
+        e0.record(stream)
         for _ in range(steps):
             res = batch.split_files_device(name, ptrs, lens, dev, stream)
+        e1.record(stream)
         torch.cuda.synchronize(dev)
         own = time.perf_counter() - t0
+        ev["step_ms"] = e0.elapsed_time(e1) / steps
         comm.barrier()
         return time.perf_counter() - t0, own, res
 
     name = args.splitter
     steps = max(1, min(args.steps, 10))
     elapsed, own, res = run(name, steps, max(1, min(args.warmup, 2)))
+    step_ms = ev["step_ms"]
     agg = aggregate(comm.gather({"bytes_per_step": total, "elapsed_s": elapsed, "own_s": own}), steps)
     out = {"metric": METRIC, "value": agg["value"], "unit": "GiB/s", "n_gpus": world, "steps": steps,
            "warmup": max(1, min(args.warmup, 2)), "ms_per_step": agg["ms_per_step"], "higher_is_better": True,
@@ -804,11 +819,22 @@ def bench_files(args, comm: Comm):
                       "largest_file": max(lens) if lens else 0,
                       "parallelism": f"LPT file sharding x{world}, no data-path collectives"},
            "per_gpu_gib_s": agg["per_gpu_gib_s"]}
+    got = batch.read_files(*res)
+    info = ks.lookup(name)
+    if int(info.kind) != 0:  # FIXED names read no data: no roofline
+        # The step's kernels (batch kernel for the small files, the long path's scan/prefix/resolve
+        # for the large ones, kcdc_split_files_device) timed together with one event pair on the
+        # launch stream: rolled bytes R summed over every file's cut list / the step's device time.
+        rolled = sum(rolled_bytes(c, int(info.min_size)) for c in got)
+        out["roofline"] = roofline("kcdc_split_files_device step (batch + long-path kernels)",
+                                   "config5" + ("-rk" if int(info.kind) == 2 else ""), step_ms, rolled, total)
+        out["roofline"]["kernel_def"] = ("every kernel of one kcdc_split_files_device call, one HIP event pair around "
+                                         "the K steps on the launch stream")
+        out["cut_stats"] = {"chunks": int(sum(c.size for c in got)), "rolled_fraction": round(rolled / max(total, 1), 4)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # cpu_baseline leg: the oracle's C restatement on a sample of this rank's files
         # (the 64 smallest, every 8th and the 2 largest), which also checks their GPU cuts
         from oracle import coracle
-        got = batch.read_files(*res)
         pick = sorted(set(range(min(64, len(lens)))) | set(range(0, len(lens), 8)) |
                       set(range(max(0, len(lens) - 2), len(lens))))
         host = [data[int(offs[i]):int(offs[i]) + lens[i]].cpu().numpy() for i in pick]
@@ -818,8 +844,8 @@ def bench_files(args, comm: Comm):
         dt = time.perf_counter() - t0
         sb = sum(lens[i] for i in pick)
         out["cpu_baseline"] = {
-            "value": round(sb / GiB / dt, 3), "unit": "GiB/s", "cores": host_cpu_info()["logical_cores"],
-            "kind": "port", "threads_all_n": nt,
+            "value": round(sb / GiB / dt, 3), "unit": "GiB/s", "cores": nt,
+            "logical_cores": host_cpu_info()["logical_cores"], "kind": "port", "threads_all_n": nt,
             "sample": f"{len(pick)} files of this rank (64 smallest, every 8th, 2 largest; {sb >> 20} MiB), {name}, "
                       f"oracle/cdc_oracle.c, {nt} threads, {dt:.2f}s wall",
             "sample_parity_mismatches": sum(1 for j, i in enumerate(pick) if not np.array_equal(got[i], want[j]))}

@@ -154,9 +154,14 @@ void kcdc_group_free(kcdc_group* g);
  * Device memory: every open writer holds two arenas of about max_size + 4 x (round_bytes / 8 +
  * 4 MiB) bytes each (152 MiB at the defaults); kcdc_bw_open fails with KCDC_ENOMEM when the
  * device cannot hold them.
+ * A freed writer's arenas are kept for the next kcdc_bw_open (hipMalloc/hipFree per object would
+ * serialise on the device): at most as many pairs as writers were open at once, all given back
+ * when a kcdc_bw_open would otherwise fail with KCDC_ENOMEM, and at kcdc_bw_batcher_free.
  * kcdc_bw_batcher_free ships what is staged, then fails every writer call still blocked in it
  * (KCDC_EINVAL) and waits for those calls to return; writers not freed before it stay valid for
- * kcdc_bw_free only. */
+ * kcdc_bw_free only.  No writer call may *start* concurrently with kcdc_bw_batcher_free (the
+ * uploader frees the batcher after its writers' last calls, as it closes the repository after
+ * its object writers). */
 typedef struct kcdc_bw_batcher kcdc_bw_batcher;
 typedef struct kcdc_bw kcdc_bw;
 kcdc_bw_batcher* kcdc_bw_batcher_new(const char* name, int device, uint64_t round_bytes, uint32_t max_wait_us);

@@ -886,9 +886,12 @@ __device__ __forceinline__ uint32_t zstd_huff_literals(const CompArgs& a, uint32
     // segments exceed the tree.  The carrier's block must still fit its slot (it may grow).
     const uint32_t qs = coded ? word - 5u - nlit : 0u;  // the sequences section's size (the parse's block)
     const int32_t save = coded && nlit ? static_cast<int32_t>(2u + nlit) - static_cast<int32_t>(3u + sbytes) : 0;
-    // the carrier's block may grow: it must fit its slot, and its literal section and sequences
-    // must stay below the sequence words they are written from
-    const bool fits = 6u + tsz + sbytes + qs + kZOff <= kSlot && 9u + tsz + sbytes + qs + 8u <= 4u * (144u - nseq);
+    // the carrier's block may grow: it must fit its slot, its literal section and sequences must
+    // stay below the sequence words they are written from, and its sequences section must end
+    // within zstd_seqs' seg_len + 2 bound (else the carrier would be stored and the treeless
+    // segments after it would name a tree the frame never holds: ADVICE r4)
+    const bool fits = 6u + tsz + sbytes + qs + kZOff <= kSlot && 9u + tsz + sbytes + qs + 8u <= 4u * (144u - nseq) &&
+                      9u + tsz + sbytes + qs <= seg_len + 2u;
     const uint64_t cm = __ballot(save > 0 && fits);
     if (!cm) return raw_tail();
     const uint32_t carrier = static_cast<uint32_t>(__builtin_ctzll(cm));
@@ -940,7 +943,10 @@ __device__ __forceinline__ uint32_t zstd_huff_literals(const CompArgs& a, uint32
     // the sequences section after the stream (a treeless segment's may not fit below its sequence
     // words: stored then, which keeps the frame's table for the segments after it)
     const uint32_t q2 = zstd_seqs(sb8, 9u + ts + sbytes, nseq, seg_len, true);
-    if (q2 == kZOver) return kStored | seg_len;
+    // (defence in depth) a carrier that still could not be written leaves the segments after it
+    // without their table: they are stored too (a stored block depends on no table)
+    const bool carrier_lost = __ballot(use == 2u && q2 == kZOver) != 0;
+    if (q2 == kZOver || carrier_lost) return kStored | seg_len;
     const uint32_t total = 6u + ts + sbytes + q2;
     const uint32_t hdr = ((total - 3u) << 3) | (2u << 1);  // Compressed_Block, not the last
     sb8[3] = static_cast<uint8_t>(hdr);

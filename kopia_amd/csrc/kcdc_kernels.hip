@@ -3593,9 +3593,17 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
             return set_error(-22, "Rabin-Karp kernel: the polynomial must have degree 53");
         const unsigned wg_waves = algo.kind == kRabinKarp ? dev::kRkWaves : dev::kDmaWaves;
         const unsigned need = (s.nstreams + wg_waves - 1) / wg_waves;
-        // The buzhash pipe kernel takes the whole chip even for a few streams: the waves without
-        // a stream help scan the owners' regions (help slots).
-        const bool helpers = (algo.kind == kBuzhash || algo.kind == kRabinKarp) && !g_test.no_help;
+        // With helpers the batch kernels take the whole chip even for a few streams: the waves
+        // without a stream help scan the owners' regions (help slots).  Help pays when a chunk's
+        // test region spans many tiles: averages of 1 MiB and up (12+ buzhash tiles, 6+ Rabin-Karp
+        // tiles per region).  Below that, the claims, row waits and helpers' polling cost more than
+        // the tail they remove (same-process A/B, 4096 x 4 MiB: 128K-BUZHASH 3.42 vs 3.13 ms with
+        // help off, 512K 2.37 vs 2.27; 64 x 64 MiB 128K-BUZHASH 27.5 vs 22.2 ms), except for the
+        // Rabin-Karp kernel in launches with fewer streams than waves (64 x 64 MiB 128K-RABINKARP
+        // 30.1 vs 38.0 ms); DESIGN.md §2.1d, profiles/r05/help_policy/.
+        const bool helpers = !g_test.no_help &&
+                             (algo.avg >= (1ull << 20) ||
+                              (algo.kind == kRabinKarp && s.nstreams < static_cast<uint64_t>(cus) * wg_waves));
         unsigned grid = helpers || need >= cus ? cus : need;
         if (grid > dev::kMaxPipeGrid) grid = dev::kMaxPipeGrid;  // one claim flag per workgroup
         uint64_t ring = 1;

@@ -147,10 +147,21 @@ struct BwDev {
     std::vector<uint8_t*> pool;        // free pinned blocks (carved from slabs)
     std::vector<uint8_t*> slabs;       // pinned allocations of kSlabBlocks blocks each
     // arenas of freed writers (arena, spare), reused by the next kcdc_bw_open: an uploader opens a
-    // writer per object, and hipMalloc/hipFree of two arenas per object would serialise on the device
+    // writer per object, and hipMalloc/hipFree of two arenas per object would serialise on the device.
+    // The cache holds at most as many pairs as writers were open at once since it was last trimmed
+    // (a freed writer's pair waits for the next open; the device never holds more arena memory than
+    // that peak needed), and kcdc_bw_open frees it before it reports KCDC_ENOMEM.
     std::vector<std::pair<uint8_t*, uint8_t*>> arenas;
-    size_t keep_arenas() const {  // at least 64 writers' worth, or up to 32 GiB of HBM
-        return std::max<size_t>(64, (32ull << 30) / (2 * arena_cap));
+    size_t peak_open = 0;  // (mu) most writers open at once since the cache was last trimmed
+    size_t keep_arenas() const { return peak_open; }
+    void trim_arenas() {  // mu held; the cached pairs are idle (their writers' rounds completed)
+        Guard g(device);
+        for (auto& ar : arenas) {
+            (void)hipFree(ar.first);
+            (void)hipFree(ar.second);
+        }
+        arenas.clear();
+        peak_open = open.size();
     }
     std::atomic<uint64_t> staged{0};   // unshipped bytes over all writers
     std::atomic<int64_t> since{0};     // when `staged` last became nonzero (steady ns)
@@ -794,6 +805,15 @@ extern "C" kcdc_bw* kcdc_bw_open_hint(kcdc_bw_batcher* t, uint64_t size_hint) {
         hipError_t e = hipSuccess;
         if (!p) e = hipMalloc(&p, b->arena_cap);
         if (e == hipSuccess && !q) e = hipMalloc(&q, b->arena_cap);
+        if (e != hipSuccess) {  // give back the cached pairs (another device user may need the memory), retry once
+            {
+                std::lock_guard<std::mutex> lk(b->mu);
+                b->trim_arenas();
+            }
+            e = hipSuccess;
+            if (!p) e = hipMalloc(&p, b->arena_cap);
+            if (e == hipSuccess && !q) e = hipMalloc(&q, b->arena_cap);
+        }
         if (e != hipSuccess) {
             if (p) (void)hipFree(p);
             b->load -= size_hint;
@@ -807,6 +827,7 @@ extern "C" kcdc_bw* kcdc_bw_open_hint(kcdc_bw_batcher* t, uint64_t size_hint) {
     }
     std::lock_guard<std::mutex> lk(b->mu);
     b->open.push_back(w);
+    b->peak_open = std::max(b->peak_open, b->open.size());
     return w;
 }
 

@@ -30,10 +30,12 @@ class knob:
         _lib.lib().kcdc_test_set(self.key, 0)
 
 
-def _helped(name):
-    """Whether waiting waves help this name's batch kernel: every dynamic name (buzhash and, since
-    round 5, Rabin-Karp: DESIGN.md §2.1c)."""
-    return "BUZHASH" in name or "RABINKARP" in name
+def _helped(name, ns=4096):
+    """Whether waiting waves help this launch (launch_split_batch's policy):
+    averages of 1 MiB and up for both kinds, and Rabin-Karp launches with fewer streams than the
+    grid's waves (2,048 on MI355X)."""
+    avg = _lib.lib().kcdc_max_segment_size(name.encode()) // 2  # max = 2 x avg (splitter_buzhash32.go:73-86)
+    return avg >= (1 << 20) or ("RABINKARP" in name and ns < 2048)
 
 
 def _split(name, data, offs, lens, gpu):
@@ -66,7 +68,7 @@ def test_few_long_streams(gpu, name, ns, mib):
     cuts, counts = coracle.split_prng_streams(name, SEED, np.arange(100, 100 + ns), L, nthreads=16)
     for i in range(ns):
         assert got[i].tolist() == cuts[i, :counts[i]].tolist(), f"{name} stream {i}"
-    assert helps > 0 or not _helped(name), "no tile was helped"
+    assert helps > 0 or not _helped(name, ns), "no tile was helped"
 
 
 @pytest.mark.parametrize("name", ["DYNAMIC-2M-BUZHASH", "DYNAMIC-2M-RABINKARP"])
@@ -82,7 +84,7 @@ def test_ragged_misaligned_streams(gpu, name):
     data = torch.from_numpy(host).to(gpu)
     got, helps = _split(name, data, offs, lens, gpu)
     _check(name, host, offs, lens, got)
-    assert helps > 0 or not _helped(name)
+    assert helps > 0 or not _helped(name, len(lens))
 
 
 @pytest.mark.parametrize("kind", ["buzhash", "rabinkarp"])
@@ -126,7 +128,7 @@ def test_help_off_is_identical(gpu, name):
     on, helps_on = _split(name, data, offs, [L] * ns, gpu)
     with knob(_lib.TEST_NO_HELP, 1):
         off, helps_off = _split(name, data, offs, [L] * ns, gpu)
-    assert (helps_on > 0 or not _helped(name)) and helps_off == 0
+    assert (helps_on > 0 or not _helped(name, ns)) and helps_off == 0
     assert [x.tolist() for x in on] == [x.tolist() for x in off]
 
 
