@@ -176,6 +176,20 @@ int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len);
 int64_t kcdc_bw_cuts(kcdc_bw* w, uint64_t* out, uint64_t cap); /* final cuts taken (<= cap), or KCDC_E* */
 int kcdc_bw_finish(kcdc_bw* w);
 void kcdc_bw_free(kcdc_bw* w);
+/* Content IDs (round 5): name every final chunk on the device, from the bytes the rounds already
+ * hold, as the content manager does after the object writer flushes it
+ * (repo/object/object_writer.go:186-227 -> repo/content/content_manager.go:812, hashData):
+ * kcdc_bw_batcher_hash selects a registered hash name (kcdc_hash_algorithms; the repository's
+ * hasher, hashing.go:51 defaults to BLAKE2B-256-128) and its HMAC secret, before the first writer
+ * opens.  Then kcdc_bw_cuts_ids replaces kcdc_bw_cuts: it returns up to cap final cuts in order, each
+ * with its chunk's digest (kcdc_hash_size bytes at ids + i * id_stride), as soon as the digests of
+ * every chunk up to it are known; kcdc_bw_finish also waits for the last chunk's digest.  BLAKE2
+ * names hash in slices of 256 KiB per chunk per step (a chunk is one chain of compressions), the
+ * others whole chunks per step.  Device memory: an ID ring of max(16 x round_bytes, 1 GiB) per
+ * device holds the chunks until they are named.  FIXED names: KCDC_EINVAL (their writers stage no
+ * bytes on the device). */
+int kcdc_bw_batcher_hash(kcdc_bw_batcher* b, const char* hash_name, const uint8_t* key, uint32_t key_len);
+int64_t kcdc_bw_cuts_ids(kcdc_bw* w, uint64_t* cuts, uint8_t* ids, uint32_t id_stride, uint64_t cap);
 int64_t kcdc_bw_rounds(const kcdc_bw_batcher* b); /* rounds shipped so far (test hook) */
 /* Observability (summed over the batcher's devices; the span and busy seconds are the largest
  * device's): out[0..n) = rounds, bytes shipped, seconds the round thread spent building and
@@ -187,7 +201,8 @@ int64_t kcdc_bw_rounds(const kcdc_bw_batcher* b); /* rounds shipped so far (test
  * issuing the split), then the round thread's seconds waiting for a round's worth of staged bytes,
  * and the writers' seconds (summed over writers) blocked on their staging cap and getting a pinned
  * staging block, then the pinned blocks allocated because the pool was empty and the round
- * thread's seconds acquiring the batcher's mutex to apply a finished round.  Returns 18. */
+ * thread's seconds acquiring the batcher's mutex to apply a finished round, then (content IDs)
+ * the chunks named, the hash steps issued and their device seconds.  Returns 21. */
 int kcdc_bw_stats(kcdc_bw_batcher* b, double* out, int n);
 
 /* ------------------------------------------------------ batch (hot path)

@@ -84,6 +84,8 @@ _SIGS = {
     "kcdc_bw_device": (C.c_int, [_P]),
     "kcdc_bw_write": (C.c_int, [_P, _P, C.c_size_t]),
     "kcdc_bw_cuts": (C.c_int64, [_P, _P, C.c_uint64]),
+    "kcdc_bw_cuts_ids": (C.c_int64, [_P, _P, _P, C.c_uint32, C.c_uint64]),
+    "kcdc_bw_batcher_hash": (C.c_int, [_P, C.c_char_p, _P, C.c_uint32]),
     "kcdc_bw_finish": (C.c_int, [_P]),
     "kcdc_bw_free": (None, [_P]),
     "kcdc_bw_rounds": (C.c_int64, [_P]),

@@ -392,22 +392,186 @@ __global__ __launch_bounds__(256) void blake2_chunks_x4_kernel(const uint8_t* da
         wave_lds_fence();
     }
     const uint64_t nblk = !live ? 0 : len ? (len + BB - 1) / BB : (key.kk ? 0 : 1);
-    for (uint64_t blk = 0; blk < nblk; blk++) {
+    // this lane's quarter of block blk: bytes [4 PER q, 4 PER q + 4 PER)
+    auto take_of = [&](uint64_t blk) -> uint32_t {
         const uint64_t rem = len - BB * blk;
-        const uint32_t take = rem < BB ? static_cast<uint32_t>(rem) : BB;
-        // this lane's quarter of the block: bytes [4 PER q, 4 PER q + 4 PER)
-        const int32_t part = static_cast<int32_t>(take) - static_cast<int32_t>(4 * PER * q);
-        uint32_t w[PER];
+        return rem < BB ? static_cast<uint32_t>(rem) : BB;
+    };
+    auto load_quarter = [&](uint64_t blk, uint32_t (&w)[PER]) {
+        const int32_t part = static_cast<int32_t>(take_of(blk)) - static_cast<int32_t>(4 * PER * q);
         load_block<PER>(p + BB * blk + 4 * PER * q, part <= 0 ? 0u : static_cast<uint32_t>(part), w);
+    };
+    // Block blk+1's quarter is loaded while block blk is compressed (round 5): the chain no longer
+    // waits a global-memory round trip per block.
+    uint32_t w[PER], wn[PER];
+    if (nblk) load_quarter(0, w);
+    for (uint64_t blk = 0; blk < nblk; blk++) {
+        if (blk + 1 < nblk) load_quarter(blk + 1, wn);
 #pragma unroll
         for (int j = 0; j < PER; j++) M[PER * q + j] = w[j];
         wave_lds_fence();
-        t += take;
+        t += take_of(blk);
         compress(t, blk + 1 == nblk);
         wave_lds_fence();
+#pragma unroll
+        for (int j = 0; j < PER; j++) w[j] = wn[j];
     }
     if (!live) return;
     uint32_t* o = reinterpret_cast<uint32_t*>(out + static_cast<uint64_t>(c) * out_stride);
+    constexpr uint32_t WB = sizeof(W);
+    if (WB * q < out_len) {
+        o[(WB / 4) * q] = static_cast<uint32_t>(h0);
+        if constexpr (B64) o[2 * q + 1] = static_cast<uint32_t>(static_cast<uint64_t>(h0) >> 32);
+    }
+    if (WB * (4 + q) < out_len) {
+        o[(WB / 4) * (4 + q)] = static_cast<uint32_t>(h1);
+        if constexpr (B64) o[2 * (4 + q) + 1] = static_cast<uint32_t>(static_cast<uint64_t>(h1) >> 32);
+    }
+}
+
+// ------------------------------------------------------------------ resumable chains (writers)
+// The batching object writers (kcdc_bw_*, kcdc_writer.cpp) name every final chunk as it is cut.
+// A BLAKE2 chunk is one chain of dependent compressions (~32,768 for a 4 MiB chunk), far longer
+// than a writer round, so the chains advance in slices: each launch moves every active chain by
+// at most max_blocks blocks, from its state in device memory (HashChain), one quad of lanes per
+// chain as in blake2_chunks_x4_kernel.  A chain's first slice also runs the key block; its last
+// writes the digest to slot `out`.  Chunks stay where the writer copied them until their chain ends.
+template <bool B64>
+__global__ __launch_bounds__(256) void blake2_chain_step_kernel(HashChain* chains, const uint32_t* active, uint32_t n,
+                                                                uint64_t max_blocks, HashKey key, uint32_t nn,
+                                                                uint32_t out_len, uint32_t out_stride, uint8_t* out) {
+    using W = typename std::conditional<B64, uint64_t, uint32_t>::type;
+    constexpr int R = B64 ? 12 : 10;
+    constexpr uint32_t BB = B64 ? 128 : 64;
+    constexpr int NW = BB / 4;
+    constexpr int PER = NW / 4;
+    __shared__ __attribute__((aligned(16))) uint32_t msg[4][16][NW];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, q = lane & 3u;
+    uint32_t* M = msg[wv][lane >> 2];
+    const uint32_t gi = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;
+    const bool live = gi < n;
+    HashChain* ch = chains + (live ? active[gi] : 0u);
+    const uint64_t len = live ? ch->len : 0u;
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(live ? ch->src : 0u);
+    const uint64_t next0 = live ? ch->next : 0u;
+    uint32_t sidx[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const uint8_t* sg = kSig[r];
+        const uint32_t v0 = sg[0] | (sg[1] << 4) | (sg[8] << 8) | (sg[9] << 12);
+        const uint32_t v1 = sg[2] | (sg[3] << 4) | (sg[10] << 8) | (sg[11] << 12);
+        const uint32_t v2 = sg[4] | (sg[5] << 4) | (sg[12] << 8) | (sg[13] << 12);
+        const uint32_t v3 = sg[6] | (sg[7] << 4) | (sg[14] << 8) | (sg[15] << 12);
+        sidx[r] = q == 0 ? v0 : q == 1 ? v1 : q == 2 ? v2 : v3;
+    }
+    auto iv = [](uint32_t i) -> W {
+        if constexpr (B64)
+            return i == 0 ? kIV64[0] : i == 1 ? kIV64[1] : i == 2 ? kIV64[2] : i == 3 ? kIV64[3]
+                 : i == 4 ? kIV64[4] : i == 5 ? kIV64[5] : i == 6 ? kIV64[6] : kIV64[7];
+        else return i == 0 ? kIV32[0] : i == 1 ? kIV32[1] : i == 2 ? kIV32[2] : i == 3 ? kIV32[3]
+                   : i == 4 ? kIV32[4] : i == 5 ? kIV32[5] : i == 6 ? kIV32[6] : kIV32[7];
+    };
+    auto mword = [&](uint32_t k) -> W {
+        if constexpr (B64) {
+            const uint2 v = *reinterpret_cast<const uint2*>(M + 2 * k);
+            return static_cast<uint64_t>(v.x) | (static_cast<uint64_t>(v.y) << 32);
+        } else {
+            return M[k];
+        }
+    };
+    auto g = [](W& a, W& b, W& cc, W& d, W x, W y) {
+        if constexpr (B64) g64(a, b, cc, d, x, y);
+        else g32(a, b, cc, d, x, y);
+    };
+    const W ivq = iv(q), ivq4 = iv(4 + q);
+    W h0, h1;
+    auto compress = [&](uint64_t t, bool last) {
+        W a = h0, b = h1, cc = ivq, d = ivq4;
+        if (q == 0) d ^= static_cast<W>(t);
+        if constexpr (!B64) {
+            if (q == 1) d ^= static_cast<W>(t >> 32);
+        }
+        if (q == 2 && last) d = ~d;
+        W mx = mword(sidx[0] & 15u), my = mword((sidx[0] >> 4) & 15u);
+        W dx = mword((sidx[0] >> 8) & 15u), dy = mword(sidx[0] >> 12);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            W nmx = mx, nmy = my, ndx = dx, ndy = dy;
+            if (r + 1 < R) {
+                const uint32_t sn = sidx[r + 1];
+                nmx = mword(sn & 15u);
+                nmy = mword((sn >> 4) & 15u);
+                ndx = mword((sn >> 8) & 15u);
+                ndy = mword(sn >> 12);
+            }
+            g(a, b, cc, d, mx, my);
+            b = qperm<kQRot1>(b);
+            cc = qperm<kQRot2>(cc);
+            d = qperm<kQRot3>(d);
+            g(a, b, cc, d, dx, dy);
+            b = qperm<kQRot3>(b);
+            cc = qperm<kQRot2>(cc);
+            d = qperm<kQRot1>(d);
+            mx = nmx;
+            my = nmy;
+            dx = ndx;
+            dy = ndy;
+        }
+        h0 ^= a ^ cc;
+        h1 ^= b ^ d;
+    };
+    const uint64_t nblk = len ? (len + BB - 1) / BB : (key.kk ? 0 : 1);
+    uint64_t next = next0;
+    if (next == ~0ull) {  // a new chain: the parameter block, then the key block (RFC 7693 §3.3)
+        h0 = ivq;
+        h1 = ivq4;
+        if (q == 0) h0 ^= static_cast<W>(0x01010000u ^ (key.kk << 8) ^ nn);
+        if (live && key.kk) {
+            if (q == 0) {
+#pragma unroll
+                for (int j = 0; j < NW; j++) M[j] = j < 16 ? key.w[j] : 0u;
+            }
+            wave_lds_fence();
+            compress(BB, len == 0);
+            wave_lds_fence();
+        }
+        next = 0;
+    } else {
+        h0 = static_cast<W>(live ? ch->h[q] : 0u);
+        h1 = static_cast<W>(live ? ch->h[4 + q] : 0u);
+    }
+    const uint64_t end = !live ? next : nblk - next < max_blocks ? nblk : next + max_blocks;
+    auto take_of = [&](uint64_t blk) -> uint32_t {
+        const uint64_t rem = len - BB * blk;
+        return rem < BB ? static_cast<uint32_t>(rem) : BB;
+    };
+    auto load_quarter = [&](uint64_t blk, uint32_t (&w)[PER]) {
+        const int32_t part = static_cast<int32_t>(take_of(blk)) - static_cast<int32_t>(4 * PER * q);
+        load_block<PER>(p + BB * blk + 4 * PER * q, part <= 0 ? 0u : static_cast<uint32_t>(part), w);
+    };
+    uint64_t t = (key.kk ? BB : 0) + (next * BB < len ? next * BB : len);
+    uint32_t w[PER], wn[PER];
+    if (next < end) load_quarter(next, w);
+    for (uint64_t blk = next; blk < end; blk++) {
+        if (blk + 1 < end) load_quarter(blk + 1, wn);
+#pragma unroll
+        for (int j = 0; j < PER; j++) M[PER * q + j] = w[j];
+        wave_lds_fence();
+        t += take_of(blk);
+        compress(t, blk + 1 == nblk);
+        wave_lds_fence();
+#pragma unroll
+        for (int j = 0; j < PER; j++) w[j] = wn[j];
+    }
+    if (!live) return;
+    if (end < nblk) {  // the chain goes on in a later slice
+        ch->h[q] = static_cast<uint64_t>(h0);
+        ch->h[4 + q] = static_cast<uint64_t>(h1);
+        if (q == 0) ch->next = end;
+        return;
+    }
+    if (q == 0) ch->next = nblk;
+    uint32_t* o = reinterpret_cast<uint32_t*>(out + static_cast<uint64_t>(ch->out) * out_stride);
     constexpr uint32_t WB = sizeof(W);
     if (WB * q < out_len) {
         o[(WB / 4) * q] = static_cast<uint32_t>(h0);
@@ -1151,3 +1315,36 @@ extern "C" int kcdc_hash_chunks_device(const char* name, const uint8_t* d_data, 
                            k, h->nn, h->out, out_stride, d_out);
     return launched();
 }
+
+namespace kcdc {
+int hash_chain_kind(const char* name, uint32_t* out_len) {
+    const HashAlgo* h = find_hash(name);
+    if (!h) return set_error(-2, std::string("unknown hash: ") + (name ? name : "(null)"));
+    if (out_len) *out_len = h->out;
+    return h->kind == HashKind::Blake2b ? 1 : h->kind == HashKind::Blake2s ? 2 : 3;
+}
+
+int launch_hash_chains(const char* name, const uint8_t* key, uint32_t key_len, HashChain* d_chains,
+                       const uint32_t* d_active, uint32_t nactive, uint64_t max_blocks, uint8_t* d_digests,
+                       uint32_t digest_stride, void* stream) {
+    const HashAlgo* h = find_hash(name);
+    if (!h || (h->kind != HashKind::Blake2b && h->kind != HashKind::Blake2s))
+        return set_error(-22, "resumable chains: BLAKE2 names only");
+    if (key_len > (h->kind == HashKind::Blake2b ? 64u : 32u)) return set_error(-22, "hash key too long");
+    if (h->kind == HashKind::Blake2s && h->nn == 16 && key_len == 0) return set_error(-22, "BLAKE2S-128 requires a key");
+    if (nactive == 0) return 0;
+    hashdev::HashKey k{};
+    k.kk = key_len;
+    for (uint32_t i = 0; i < key_len; i++) k.w[i / 4] |= static_cast<uint32_t>(key[i]) << (8 * (i % 4));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const dim3 block(256), grid((4ull * nactive + 255) / 256);
+    if (h->kind == HashKind::Blake2b)
+        hipLaunchKernelGGL(hashdev::blake2_chain_step_kernel<true>, grid, block, 0, st, d_chains, d_active, nactive,
+                           max_blocks, k, h->nn, h->out, digest_stride, d_digests);
+    else
+        hipLaunchKernelGGL(hashdev::blake2_chain_step_kernel<false>, grid, block, 0, st, d_chains, d_active, nactive,
+                           max_blocks, k, h->nn, h->out, digest_stride, d_digests);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : set_error(-5, std::string("hash chain launch: ") + hipGetErrorString(e));
+}
+}  // namespace kcdc

@@ -102,4 +102,22 @@ int launch_split_long_multi(const Algo& algo, uint32_t m, const uint8_t* const* 
 int launch_split_long(const Algo& algo, const uint8_t* d_data, uint64_t len, uint64_t* d_cuts, uint64_t cuts_cap,
                       uint64_t* d_count, void* ws, size_t ws_bytes, int device, void* stream);
 
+// ---- resumable content hashes (kcdc_hash.hip), for the batching writers
+struct HashChain {       // one chunk's keyed BLAKE2 chain, in device memory (128 bytes)
+    uint64_t h[8];       // the state (BLAKE2s: the low words)
+    uint64_t src;        // the chunk's bytes (device address)
+    uint64_t len;        // its length
+    uint64_t next;       // message blocks compressed so far; ~0: not started (parameter and key blocks next)
+    uint32_t out;        // digest slot
+    uint32_t pad[9];
+};
+static_assert(sizeof(HashChain) == 128, "HashChain is 128 bytes");
+// 1 BLAKE2b, 2 BLAKE2s (resumable), 3 another registered name (whole chunks), < 0 unknown; *out_len = digest bytes.
+int hash_chain_kind(const char* name, uint32_t* out_len);
+// Advance chains d_chains[d_active[0..n)] by at most max_blocks message blocks each; a chain that ends
+// writes its digest to d_digests + out * digest_stride.
+int launch_hash_chains(const char* name, const uint8_t* key, uint32_t key_len, HashChain* d_chains,
+                       const uint32_t* d_active, uint32_t nactive, uint64_t max_blocks, uint8_t* d_digests,
+                       uint32_t digest_stride, void* stream);
+
 }  // namespace kcdc

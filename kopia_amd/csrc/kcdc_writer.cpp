@@ -27,6 +27,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -196,6 +197,58 @@ struct BwDev {
     std::atomic<uint64_t> pool_misses{0};          // pinned slabs allocated (the pool was empty)
     double t_lock = 0;                             // round thread: acquiring mu to apply a round
 
+    // ---- content IDs (kcdc_bw_batcher_hash): every final chunk's keyed hash, computed on the
+    // device from the bytes the round already holds (content_manager.go:812 hashes each chunk the
+    // object writer flushes).  At a round's completion each new final chunk is copied from the
+    // writer's arena into the ID ring (copy stream, ordered after that round's compactions) and
+    // gets a chain; the chains advance in slices on their own stream (one step in flight at a
+    // time, every pending chain moved by at most step_blocks blocks), since a BLAKE2 chunk is one
+    // long dependent chain.  Ring bytes and chain slots are reused first in, first out.
+    struct IdCfg {
+        bool on = false;
+        std::string name;
+        std::vector<uint8_t> key;
+        uint32_t out = 0;  // digest bytes
+        int kind = 0;      // 1 BLAKE2b, 2 BLAKE2s (sliced chains), 3 other names (whole chunks per step)
+    } ids;
+    struct Chain {
+        kcdc_bw* w;            // null once its writer was freed
+        uint64_t wseq;         // the writer's ID entry
+        uint64_t ring_at;      // bytes in the ring (monotonic offset; position = ring_at % ring_cap)
+        uint64_t ring_end;     // the ring's monotonic offset after this chain (its bytes and any wrap skip)
+        uint64_t len, nblk, done;  // chunk bytes; message blocks; blocks done after the steps issued
+        bool fin = false;      // its digest has been delivered
+    };
+    struct NewChunk {
+        kcdc_bw* w;
+        uint64_t wseq, pos, len;
+    };
+    std::vector<NewChunk> newc;        // final chunks of the last completed round (round thread)
+    hipStream_t hstream = nullptr;
+    uint8_t* ring = nullptr;
+    uint64_t ring_cap = 0, ring_head = 0, ring_tail = 0;  // monotonic byte offsets
+    HashChain* d_chains = nullptr;
+    HashChain* h_chains = nullptr;     // pinned: new chains' records, by slot
+    uint32_t chain_cap = 0;
+    uint64_t chain_head = 0, chain_tail = 0, uploaded = 0;  // monotonic chain numbers
+    std::deque<Chain> chains;          // chains [chain_tail, chain_head)
+    uint8_t* d_dig = nullptr;          // digests: by slot (kinds 1, 2) or by position in the step (kind 3)
+    uint8_t* h_dig = nullptr;
+    uint32_t* d_act = nullptr;         // a step's active chain slots
+    uint32_t* h_act = nullptr;
+    uint64_t* d_ol = nullptr;          // kind 3: ring offsets, then lengths
+    uint64_t* h_ol = nullptr;
+    hipEvent_t copy_ev = nullptr, step_ev = nullptr, step_t0 = nullptr;
+    bool step_live = false;
+    std::vector<std::pair<uint64_t, uint32_t>> step_done;  // (chain number, digest row) ending in the live step
+    uint64_t step_blocks = 0;
+    uint64_t id_chains = 0, id_steps = 0;
+    double t_hash = 0;                 // device seconds of the hash steps
+    int ids_enable(const char* name, const uint8_t* key, uint32_t key_len);
+    int id_create();                   // round thread, mu not held: newc -> chains (ring copies)
+    int id_pump(bool block);           // round thread, mu not held: deliver a finished step, issue the next
+    bool id_busy() const { return step_live || chain_tail != chain_head; }
+
     ~BwDev() {
         if (algo->kind == kFixed) return;
         Guard g(device);
@@ -213,6 +266,18 @@ struct BwDev {
                 if (e) (void)hipEventDestroy(e);
         }
         if (ev_ref) (void)hipEventDestroy(ev_ref);
+        for (hipEvent_t e : {copy_ev, step_ev, step_t0})
+            if (e) (void)hipEventDestroy(e);
+        if (ring) (void)hipFree(ring);
+        if (d_chains) (void)hipFree(d_chains);
+        if (h_chains) (void)hipHostFree(h_chains);
+        if (d_dig) (void)hipFree(d_dig);
+        if (h_dig) (void)hipHostFree(h_dig);
+        if (d_act) (void)hipFree(d_act);
+        if (h_act) (void)hipHostFree(h_act);
+        if (d_ol) (void)hipFree(d_ol);
+        if (h_ol) (void)hipHostFree(h_ol);
+        if (hstream) (void)hipStreamDestroy(hstream);
         if (copy) (void)hipStreamDestroy(copy);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -275,6 +340,17 @@ struct kcdc_bw {
     std::atomic<uint64_t> ready_pushed{0}, ready_taken{0};
     bool done = false;           // (batcher mu)
     uint64_t fixed_next = 0;     // FIXED names: the next cut (no data is read)
+    // content IDs (batcher mu): entry wseq = ids_base + i, in cut order; taken as a ready prefix
+    struct IdEntry {
+        uint64_t cut;
+        bool ready;
+        uint8_t id[32];
+    };
+    std::deque<IdEntry> ids;
+    uint64_t ids_base = 0;       // wseq of ids.front()
+    uint64_t ids_made = 0;       // entries ever created
+    uint64_t ids_ready = 0;      // entries whose digest has arrived
+    uint64_t id_from = 0;        // start of the next final chunk
 };
 
 namespace {
@@ -350,8 +426,17 @@ void BwDev::loop() {
                 return set_error(KCDC_EIO, "writer round: the device lost a stream");
             const uint64_t* c = hp + 6 * n + r.cbase[k];
             const uint64_t fin = j.finishing ? cnt : (cnt ? cnt - 1 : 0);
-            for (uint64_t t = 0; t < fin; t++) w->ready.push_back(w->tail_pos + c[t]);
-            w->ready_pushed.fetch_add(fin, std::memory_order_release);
+            if (ids.on) {  // every final chunk [id_from, cut) gets an ID entry and, in id_create, a chain
+                for (uint64_t t = 0; t < fin; t++) {
+                    const uint64_t cut = w->tail_pos + c[t];
+                    w->ids.push_back(kcdc_bw::IdEntry{cut, false, {}});
+                    newc.push_back(NewChunk{w, w->ids_made++, w->id_from, cut - w->id_from});
+                    w->id_from = cut;
+                }
+            } else {
+                for (uint64_t t = 0; t < fin; t++) w->ready.push_back(w->tail_pos + c[t]);
+                w->ready_pushed.fetch_add(fin, std::memory_order_release);
+            }
             if (fin) w->frontier = w->tail_pos + c[fin - 1];
             w->launched_to = j.to;
             w->tail_pos = w->frontier >= kHist ? w->frontier - kHist : 0;
@@ -385,10 +470,22 @@ void BwDev::loop() {
         const auto idle0 = std::chrono::steady_clock::now();
         while (!work() && !timed_out) {
             recycle(inflight);
+            if (ids.on && id_busy()) {
+                lk.unlock();
+                const int rc = id_pump(false);
+                lk.lock();
+                if (rc != KCDC_OK) {
+                    lk.unlock();
+                    fail(rc);
+                    lk.lock();
+                    break;
+                }
+            }
             if (inflight.live) {
                 if (hipEventQuery(meta[inflight.m].done) == hipSuccess) {
                     lk.unlock();
-                    const int rc = complete(inflight);
+                    int rc = complete(inflight);
+                    if (rc == KCDC_OK && ids.on) rc = id_create();
                     lk.lock();
                     if (rc != KCDC_OK) {
                         lk.unlock();
@@ -398,6 +495,10 @@ void BwDev::loop() {
                 } else {
                     cv_round.wait_for(lk, std::chrono::microseconds(100), work);
                 }
+                continue;
+            }
+            if (ids.on && id_busy()) {  // hash steps in flight: poll them as a round in flight
+                cv_round.wait_for(lk, std::chrono::microseconds(100), work);
                 continue;
             }
             if (staged.load() > 0) {
@@ -414,7 +515,7 @@ void BwDev::loop() {
         t_idle += std::chrono::duration<double>(std::chrono::steady_clock::now() - idle0).count();
         if (error) break;
         if (staged.load() == 0 && finish_pending.load() == 0) {
-            if (stop) break;
+            if (stop && !(ids.on && id_busy() && !error)) break;
             continue;
         }
         recycle(inflight);
@@ -522,7 +623,12 @@ void BwDev::loop() {
         }
         lap(2);
         // round k's cuts are round k+1's chunk starts
-        if (rc == KCDC_OK && inflight.live) rc = complete(inflight);
+        if (rc == KCDC_OK && inflight.live) {
+            rc = complete(inflight);
+            // its final chunks' ring copies queue on the copy stream behind this round's compactions
+            if (rc == KCDC_OK && ids.on) rc = id_create();
+        }
+        if (rc == KCDC_OK && ids.on) rc = id_pump(false);
         lap(3);
         // ---- launch R over every job's region [tail_pos, to)
         if (rc == KCDC_OK) {
@@ -602,11 +708,187 @@ void BwDev::loop() {
     }
     lk.unlock();
     if (inflight.live && !error) {
-        const int rc = complete(inflight);
+        int rc = complete(inflight);
+        if (rc == KCDC_OK && ids.on) rc = id_create();
+        if (rc != KCDC_OK) fail(rc);
+    }
+    while (ids.on && id_busy() && !error) {  // drain the chains of the last rounds
+        const int rc = id_pump(true);
         if (rc != KCDC_OK) fail(rc);
     }
     lk.lock();
     cv_done.notify_all();
+}
+
+// ---------------------------------------------------------------- content IDs
+int BwDev::ids_enable(const char* name, const uint8_t* key, uint32_t key_len) {
+    uint32_t out = 0;
+    const int kind = hash_chain_kind(name, &out);
+    if (kind < 0) return kind;
+    if (key_len && !key) return set_error(KCDC_EINVAL, "null key");
+    ids.name = name;
+    ids.key.assign(key, key + key_len);
+    ids.out = out;
+    ids.kind = kind;
+    // slices of 256 KiB per chain per step: a 4 MiB chunk is named after ~16 steps
+    step_blocks = kind == 1 ? 2048 : 4096;
+    ring_cap = std::max<uint64_t>(16 * round_bytes, 1ull << 30);
+    chain_cap = 16384;
+    Guard g(device);
+    hipError_t e = hipStreamCreateWithFlags(&hstream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&ring, ring_cap);
+    if (e == hipSuccess) e = hipMalloc(&d_chains, sizeof(HashChain) * chain_cap);
+    if (e == hipSuccess) e = hipHostMalloc(&h_chains, sizeof(HashChain) * chain_cap, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc(&d_dig, 32ull * chain_cap);
+    if (e == hipSuccess) e = hipHostMalloc(&h_dig, 32ull * chain_cap, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc(&d_act, 4ull * chain_cap);
+    if (e == hipSuccess) e = hipHostMalloc(&h_act, 4ull * chain_cap, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc(&d_ol, 16ull * chain_cap);
+    if (e == hipSuccess) e = hipHostMalloc(&h_ol, 16ull * chain_cap, hipHostMallocDefault);
+    for (hipEvent_t* ev : {&copy_ev, &step_ev, &step_t0})
+        if (e == hipSuccess) e = hipEventCreate(ev);
+    if (e != hipSuccess) return hip_err(e, "writer content IDs: device memory");
+    ids.on = true;
+    return KCDC_OK;
+}
+
+// The last completed round's final chunks (newc) become chains: ring space and a slot each (waiting
+// for steps to free them when the ring is full), and a copy from the writer's arena into the ring.
+// Called right after complete(): the arena pointers are those of the compactions queued before it
+// on the copy stream, and the copies queue behind them, before any later compaction.
+int BwDev::id_create() {
+    if (newc.empty()) return KCDC_OK;
+    Guard g(device);
+    bool copied = false;
+    for (const NewChunk& nc : newc) {
+        const uint64_t need = (nc.len + 15) & ~uint64_t(15);
+        if (need > ring_cap) return set_error(KCDC_EIO, "writer content IDs: chunk larger than the ID ring");
+        uint64_t at = ring_head;
+        for (;;) {
+            at = ring_head;
+            if (at % ring_cap + need > ring_cap) at += ring_cap - at % ring_cap;  // no chunk wraps
+            if (at + need - ring_tail <= ring_cap && chain_head - chain_tail < chain_cap) break;
+            if (copied) {  // the chains waiting for space may read bytes just copied: order the copies first
+                hipError_t e = hipEventRecord(copy_ev, copy);
+                if (e != hipSuccess) return hip_err(e, "writer content IDs: copy event");
+            }
+            const int rc = id_pump(true);
+            if (rc != KCDC_OK) return rc;
+            if (!id_busy() && !(at + need - ring_tail <= ring_cap && chain_head - chain_tail < chain_cap))
+                return set_error(KCDC_EIO, "writer content IDs: ring full with no chain in flight");
+        }
+        const uint32_t slot = static_cast<uint32_t>(chain_head % chain_cap);
+        uint8_t* dst = ring + at % ring_cap;
+        if (nc.len) {
+            hipError_t e = hipMemcpyAsync(dst, nc.w->arena + (nc.pos - nc.w->origin), nc.len, hipMemcpyDeviceToDevice, copy);
+            if (e != hipSuccess) return hip_err(e, "writer content IDs: ring copy");
+            copied = true;
+        }
+        HashChain& hc = h_chains[slot];
+        std::memset(&hc, 0, sizeof(hc));
+        hc.src = reinterpret_cast<uint64_t>(dst);
+        hc.len = nc.len;
+        hc.next = ~0ull;
+        hc.out = slot;
+        const uint64_t bb = ids.kind == 2 ? 64 : 128;
+        const uint64_t nblk = ids.kind == 3 ? 1 : nc.len ? (nc.len + bb - 1) / bb : 1;
+        std::lock_guard<std::mutex> lk(mu);
+        chains.push_back(Chain{nc.w, nc.wseq, at, at + need, nc.len, nblk, 0, false});
+        chain_head++;
+        ring_head = at + need;
+        id_chains++;
+    }
+    newc.clear();
+    if (copied) {
+        hipError_t e = hipEventRecord(copy_ev, copy);
+        if (e != hipSuccess) return hip_err(e, "writer content IDs: copy event");
+    }
+    return KCDC_OK;
+}
+
+// Deliver the step in flight once it has finished (block: wait for it), then issue the next one
+// over every chain not yet named.
+int BwDev::id_pump(bool block) {
+    Guard g(device);
+    if (step_live) {
+        const hipError_t q = block ? hipEventSynchronize(step_ev) : hipEventQuery(step_ev);
+        if (q == hipErrorNotReady) return KCDC_OK;
+        if (q != hipSuccess) return hip_err(q, "writer content IDs: hash step");
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, step_t0, step_ev) == hipSuccess) t_hash += ms * 1e-3;
+        std::lock_guard<std::mutex> lk(mu);
+        for (const auto& d : step_done) {
+            Chain& c = chains[d.first - chain_tail];
+            c.fin = true;
+            if (!c.w) continue;  // its writer was freed
+            kcdc_bw::IdEntry& en = c.w->ids[c.wseq - c.w->ids_base];
+            std::memcpy(en.id, h_dig + 32ull * d.second, ids.out);
+            en.ready = true;
+            c.w->ids_ready++;
+        }
+        step_done.clear();
+        while (!chains.empty() && chains.front().fin) {
+            ring_tail = chains.front().ring_end;
+            chains.pop_front();
+            chain_tail++;
+        }
+        step_live = false;
+        cv_done.notify_all();
+    }
+    if (chain_head == chain_tail) return KCDC_OK;
+    // ---- the next step: new chains' records up, then every pending chain advanced
+    hipError_t e = hipStreamWaitEvent(hstream, copy_ev, 0);
+    for (uint64_t c0 = uploaded; e == hipSuccess && c0 < chain_head;) {  // slots [uploaded, chain_head) mod cap
+        const uint32_t s0 = static_cast<uint32_t>(c0 % chain_cap);
+        const uint64_t run = std::min<uint64_t>(chain_head - c0, chain_cap - s0);
+        e = hipMemcpyAsync(d_chains + s0, h_chains + s0, run * sizeof(HashChain), hipMemcpyHostToDevice, hstream);
+        c0 += run;
+    }
+    uploaded = chain_head;
+    if (e == hipSuccess) e = hipEventRecord(step_t0, hstream);
+    if (e != hipSuccess) return hip_err(e, "writer content IDs: chain upload");
+    uint32_t n = 0;
+    int rc = KCDC_OK;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (uint64_t k = 0; k < chains.size(); k++) {
+            Chain& c = chains[k];
+            if (c.fin || c.done >= c.nblk) continue;
+            const uint64_t cn = chain_tail + k;
+            if (ids.kind == 3) {  // whole chunks, in this step's order
+                h_ol[n] = c.ring_at % ring_cap;
+                h_ol[chain_cap + n] = c.len;
+                c.done = c.nblk;
+                step_done.emplace_back(cn, n);
+            } else {
+                h_act[n] = static_cast<uint32_t>(cn % chain_cap);
+                c.done = std::min(c.nblk, c.done + step_blocks);
+                if (c.done == c.nblk) step_done.emplace_back(cn, static_cast<uint32_t>(cn % chain_cap));
+            }
+            n++;
+        }
+    }
+    if (n == 0) return KCDC_OK;
+    if (ids.kind == 3) {
+        e = hipMemcpyAsync(d_ol, h_ol, 8ull * n, hipMemcpyHostToDevice, hstream);
+        if (e == hipSuccess) e = hipMemcpyAsync(d_ol + chain_cap, h_ol + chain_cap, 8ull * n, hipMemcpyHostToDevice, hstream);
+        if (e != hipSuccess) return hip_err(e, "writer content IDs: chunk list");
+        rc = kcdc_hash_chunks_device(ids.name.c_str(), ring, d_ol, d_ol + chain_cap, nullptr, n, ids.key.data(),
+                                     static_cast<uint32_t>(ids.key.size()), d_dig, 32, hstream);
+        if (rc == KCDC_OK) e = hipMemcpyAsync(h_dig, d_dig, 32ull * n, hipMemcpyDeviceToHost, hstream);
+    } else {
+        e = hipMemcpyAsync(d_act, h_act, 4ull * n, hipMemcpyHostToDevice, hstream);
+        if (e != hipSuccess) return hip_err(e, "writer content IDs: active list");
+        rc = launch_hash_chains(ids.name.c_str(), ids.key.data(), static_cast<uint32_t>(ids.key.size()), d_chains, d_act,
+                                n, step_blocks, d_dig, 32, hstream);
+        if (rc == KCDC_OK) e = hipMemcpyAsync(h_dig, d_dig, 32ull * chain_cap, hipMemcpyDeviceToHost, hstream);
+    }
+    if (rc != KCDC_OK) return rc;
+    if (e == hipSuccess) e = hipEventRecord(step_ev, hstream);
+    if (e != hipSuccess) return hip_err(e, "writer content IDs: hash step");
+    step_live = true;
+    id_steps++;
+    return KCDC_OK;
 }
 
 namespace {
@@ -908,6 +1190,7 @@ extern "C" int64_t kcdc_bw_cuts(kcdc_bw* w, uint64_t* out, uint64_t cap) {
     Inside in(w->top);
     if (!in.ok) return set_error(KCDC_EINVAL, "writer batcher closed");
     BwDev* b = w->b;
+    if (b->ids.on) return set_error(KCDC_EINVAL, "content IDs are on: take cuts with kcdc_bw_cuts_ids");
     if (w->ready_pushed.load(std::memory_order_acquire) == w->ready_taken.load(std::memory_order_relaxed) &&
         !b->error)
         return 0;
@@ -953,8 +1236,46 @@ extern "C" int kcdc_bw_finish(kcdc_bw* w) {
         b->cv_round.notify_one();
     }
     std::unique_lock<std::mutex> lk(b->mu);
-    b->cv_done.wait(lk, [&] { return w->done || b->error; });
-    return b->error && !w->done ? dev_error(b) : KCDC_OK;
+    // with content IDs, Result() also waits for the last chunk's name
+    b->cv_done.wait(lk, [&] { return (w->done && w->ids_ready == w->ids_made) || b->error; });
+    return b->error && !(w->done && w->ids_ready == w->ids_made) ? dev_error(b) : KCDC_OK;
+}
+
+extern "C" int64_t kcdc_bw_cuts_ids(kcdc_bw* w, uint64_t* cuts, uint8_t* ids, uint32_t id_stride, uint64_t cap) {
+    if (!w || !w->b) return set_error(KCDC_EINVAL, "writer not open");
+    Inside in(w->top);
+    if (!in.ok) return set_error(KCDC_EINVAL, "writer batcher closed");
+    BwDev* b = w->b;
+    if (!b->ids.on) return set_error(KCDC_EINVAL, "content IDs are off (kcdc_bw_batcher_hash)");
+    if (id_stride < b->ids.out || (cap && (!cuts || !ids))) return set_error(KCDC_EINVAL, "bad ID buffer");
+    std::lock_guard<std::mutex> lk(b->mu);
+    uint64_t k = 0;
+    while (k < cap && !w->ids.empty() && w->ids.front().ready) {
+        const kcdc_bw::IdEntry& en = w->ids.front();
+        cuts[k] = en.cut;
+        std::memcpy(ids + k * id_stride, en.id, b->ids.out);
+        w->ids.pop_front();
+        w->ids_base++;
+        k++;
+    }
+    if (b->error && k == 0) return dev_error(b);
+    return static_cast<int64_t>(k);
+}
+
+extern "C" int kcdc_bw_batcher_hash(kcdc_bw_batcher* t, const char* hash_name, const uint8_t* key, uint32_t key_len) {
+    if (!t) return set_error(KCDC_EINVAL, "null batcher");
+    if (t->algo->kind == kFixed) return set_error(KCDC_EINVAL, "content IDs: FIXED writers stage no bytes on the device");
+    std::lock_guard<std::mutex> lk(t->mu);
+    for (BwDev* b : t->devs) {
+        std::lock_guard<std::mutex> dl(b->mu);
+        if (!b->open.empty() || b->rounds) return set_error(KCDC_EINVAL, "content IDs: enable before the first writer opens");
+        if (b->ids.on) return set_error(KCDC_EINVAL, "content IDs are already on");
+    }
+    for (BwDev* b : t->devs) {
+        const int rc = b->ids_enable(hash_name, key, key_len);
+        if (rc != KCDC_OK) return rc;
+    }
+    return KCDC_OK;
 }
 
 extern "C" void kcdc_bw_free(kcdc_bw* w) {
@@ -964,6 +1285,8 @@ extern "C" void kcdc_bw_free(kcdc_bw* w) {
         // an abandoned object: split (and drop) what it staged, so no round still reads its arena
         if (b->algo->kind != kFixed && !b->error) (void)kcdc_bw_finish(w);
         std::lock_guard<std::mutex> lk(b->mu);
+        for (BwDev::Chain& c : b->chains)  // (an error left chains of this writer unnamed)
+            if (c.w == w) c.w = nullptr;
         b->load -= std::min<uint64_t>(b->load.load(), w->counted);
         for (Blk& bk : w->blocks) b->pool.push_back(bk.p);
         b->open.erase(std::find(b->open.begin(), b->open.end(), w));
@@ -998,7 +1321,7 @@ extern "C" int kcdc_bw_stats(kcdc_bw_batcher* t, double* out, int n) {
     // per device: the device span from its first round's start to its last one's end, and the
     // part of it in which a gather or a split ran (their union: overlapped rounds count once);
     // over devices: counts and host seconds add up, spans and busy times are the maximum
-    double v[18] = {0};
+    double v[21] = {0};
     for (BwDev* b : t->devs) {
         std::lock_guard<std::mutex> lk(b->mu);
         std::vector<std::pair<float, float>> iv = b->busy;
@@ -1019,13 +1342,14 @@ extern "C" int kcdc_bw_stats(kcdc_bw_batcher* t, double* out, int n) {
             busy += e0 - s0;
             span = hi - iv[0].first;
         }
-        const double d[18] = {static_cast<double>(b->rounds), static_cast<double>(b->shipped_bytes), b->t_submit,
+        const double d[21] = {static_cast<double>(b->rounds), static_cast<double>(b->shipped_bytes), b->t_submit,
                               b->t_wait, b->t_gather, b->t_kernel, span * 1e-3, busy * 1e-3,
                               b->t_seg[0], b->t_seg[1], b->t_seg[2], b->t_seg[3], b->t_seg[4],
                               b->t_idle, b->w_capped_ns.load() * 1e-9, b->w_block_ns.load() * 1e-9,
-                              static_cast<double>(b->pool_misses.load()), b->t_lock};
-        for (int i = 0; i < 18; i++) v[i] = (i == 6 || i == 7) ? std::max(v[i], d[i]) : v[i] + d[i];
+                              static_cast<double>(b->pool_misses.load()), b->t_lock,
+                              static_cast<double>(b->id_chains), static_cast<double>(b->id_steps), b->t_hash};
+        for (int i = 0; i < 21; i++) v[i] = (i == 6 || i == 7) ? std::max(v[i], d[i]) : v[i] + d[i];
     }
-    for (int i = 0; i < n && i < 18; i++) out[i] = v[i];
-    return 18;
+    for (int i = 0; i < n && i < 21; i++) out[i] = v[i];
+    return 21;
 }

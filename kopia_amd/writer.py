@@ -52,10 +52,30 @@ class BatchedWriter:
             if k < self._buf.size:
                 return out
 
+    def cuts_ids(self) -> list[tuple[int, bytes]]:
+        """Final cuts found since the last call with their chunks' content hashes (batchers built
+        with hash=...): (cut, digest) in cut order, non-blocking."""
+        n = self._buf.size
+        ids = np.zeros(n * 32, dtype=np.uint8)
+        size = self._b.hash_size
+        out: list[tuple[int, bytes]] = []
+        while True:
+            k = _lib.lib().kcdc_bw_cuts_ids(self._h, self._buf.ctypes.data, ids.ctypes.data, 32, n)
+            if k < 0:
+                _lib.check(int(k))
+            out.extend((int(self._buf[i]), ids[32 * i:32 * i + size].tobytes()) for i in range(k))
+            if k < n:
+                return out
+
     def finish(self) -> list[int]:
         """Split the rest (blocks) and return the remaining cuts, the last one = the object size."""
         _lib.check(_lib.lib().kcdc_bw_finish(self._h))
         return self.cuts()
+
+    def finish_ids(self) -> list[tuple[int, bytes]]:
+        """finish() for batchers with content IDs: the remaining (cut, digest) pairs."""
+        _lib.check(_lib.lib().kcdc_bw_finish(self._h))
+        return self.cuts_ids()
 
     def close(self) -> None:
         if self._h:
@@ -75,9 +95,10 @@ class WriterBatcher:
     (`devices`: device indices, repeats allowed; [] = every device)."""
 
     def __init__(self, name: str, device: int = 0, round_bytes: int = 0, max_wait_us: int = 0,
-                 devices: list[int] | None = None):
+                 devices: list[int] | None = None, hash: str | None = None, key: bytes = b""):
         import weakref
         self.name = name
+        self.hash_size = 0
         self._writers = weakref.WeakSet()
         if devices is None:
             self._h = _lib.lib().kcdc_bw_batcher_new(name.encode(), device, round_bytes, max_wait_us)
@@ -87,6 +108,14 @@ class WriterBatcher:
                                                             round_bytes, max_wait_us)
         if not self._h:
             raise _lib.KcdcError(_lib.KCDC_ENODEV, _lib.last_error())
+        if hash is not None:
+            kb = (C.c_uint8 * max(len(key), 1)).from_buffer_copy(key or b"\0")
+            rc = _lib.lib().kcdc_bw_batcher_hash(self._h, hash.encode(), kb, len(key))
+            if rc != 0:
+                _lib.lib().kcdc_bw_batcher_free(self._h)
+                self._h = None
+                _lib.check(rc)
+            self.hash_size = int(_lib.check(_lib.lib().kcdc_hash_size(hash.encode())))
 
     def open(self, size_hint: int = 0) -> BatchedWriter:
         return BatchedWriter(self, size_hint)

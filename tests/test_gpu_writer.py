@@ -212,3 +212,110 @@ def test_errors(gpu):
     b.close()
     with pytest.raises(_lib.KcdcError):
         WriterBatcher("NO-SUCH-SPLITTER")
+
+
+# ---- content IDs (kcdc_bw_batcher_hash / kcdc_bw_cuts_ids): every final chunk named on the device
+# as the content manager names what the object writer flushes (object_writer.go:186-227 ->
+# content_manager.go:812, hashing.go:78-101), checked against hashlib / the hash oracle.
+KEY = bytes(range(7, 39))  # a 32-byte repository HMAC secret
+
+
+def _feed_ids(w, data, mode, rng):
+    got = []
+    pos = 0
+    while pos < data.size:
+        k = 64 << 10 if mode == "64k" else int(rng.integers(1, 1001)) if mode == "rand" else data.size
+        w.write(data[pos:pos + k])
+        pos += k
+        if rng.random() < 0.05:
+            got.extend(w.cuts_ids())
+    got.extend(w.finish_ids())
+    return got
+
+
+def _run_ids(name, sizes, modes, hash_name="BLAKE2B-256-128", key=KEY, round_bytes=0, sid0=0):
+    from oracle import hashes
+    b = WriterBatcher(name, round_bytes=round_bytes, hash=hash_name, key=key)
+    datas = [coracle.gen_stream(SEED, sid0 + i, int(n)) for i, n in enumerate(sizes)]
+    got = [None] * len(sizes)
+    errs = []
+
+    def work(i):
+        try:
+            w = b.open()
+            got[i] = _feed_ids(w, datas[i], modes[i % len(modes)], np.random.default_rng(i))
+            w.close()
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(len(sizes))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    rounds = b.rounds()
+    b.close()
+    assert not errs, errs
+    for i, d in enumerate(datas):
+        want = coracle.split_stream(name, d).tolist()
+        assert [c for c, _ in got[i]] == want, f"writer {i}: cuts"
+        prev = 0
+        for c, h in got[i]:
+            assert h == hashes.kopia_hash(hash_name, key, d[prev:c].tobytes()), f"writer {i}: chunk [{prev}, {c})"
+            prev = c
+    return rounds
+
+
+def test_ids_sixty_four_writers(gpu):
+    """The uploader's shape with content IDs on: 64 writers in 64 KiB slices, BLAKE2B-256-128 (the
+    repository default), every chunk's ID equal to hashlib's keyed BLAKE2b truncated to 16 bytes."""
+    rounds = _run_ids("DYNAMIC-4M-BUZHASH", [12 << 20] * 48 + [int(x) for x in range(1 << 20, 17 << 20, 1 << 20)],
+                      ["64k", "64k", "64k", "rand"], round_bytes=64 << 20)
+    assert rounds >= 4
+
+
+@pytest.mark.parametrize("hash_name", ["BLAKE2B-256", "BLAKE2S-128", "BLAKE2S-256", "BLAKE3-256-128",
+                                       "HMAC-SHA256-128"])
+def test_ids_every_kind(gpu, hash_name):
+    """Sliced chains (BLAKE2b, BLAKE2s) and whole-chunk steps (BLAKE3, HMAC-SHA256), with empty,
+    tiny and block-edge objects."""
+    rng = np.random.default_rng(31)
+    sizes = [int(x) for x in rng.integers(0, 5 << 20, 6)] + [0, 1, 127, 128, 129, 64 << 10]
+    _run_ids("DYNAMIC-1M-BUZHASH", sizes, ["64k", "rand", "whole"], hash_name=hash_name, round_bytes=8 << 20)
+
+
+def test_ids_kat_rows_and_rabinkarp(gpu):
+    """The KAT parameterisations' many small chunks (TestSplitterStability, splitter_test.go:30-39)
+    and a Rabin-Karp name, with an unkeyed and a 64-byte key."""
+    kat = coracle.gorand_read(5, 5_000_000)
+    from oracle import hashes
+    for kind, avg, key in [(1, 2048, b""), (2, 1024, bytes(range(64)))]:
+        name = _lib.lib().kcdc_custom_algorithm(kind, avg).decode()
+        b = WriterBatcher(name, round_bytes=1 << 20, max_wait_us=100, hash="BLAKE2B-256-128", key=key)
+        w = b.open()
+        got = _feed_ids(w, kat, "rand", np.random.default_rng(avg))
+        w.close()
+        b.close()
+        want = coracle.split_stream_kind("buzhash" if kind == 1 else "rabinkarp", avg, kat).tolist()
+        assert [c for c, _ in got] == want
+        prev = 0
+        for c, h in got:
+            assert h == hashes.kopia_hash("BLAKE2B-256-128", key, kat[prev:c].tobytes())
+            prev = c
+
+
+def test_ids_errors(gpu):
+    b = WriterBatcher("DYNAMIC-4M-BUZHASH", hash="BLAKE2B-256-128", key=KEY)
+    w = b.open()
+    w.write(bytes(1000))
+    with pytest.raises(_lib.KcdcError):
+        w.cuts()  # cuts come with their IDs when IDs are on
+    assert [c for c, _ in w.finish_ids()] == [1000]
+    w.close()
+    with pytest.raises(_lib.KcdcError):  # IDs must be chosen before the first writer opens
+        _lib.check(_lib.lib().kcdc_bw_batcher_hash(b._h, b"BLAKE2B-256-128", None, 0))
+    b.close()
+    with pytest.raises(_lib.KcdcError):
+        WriterBatcher("FIXED-4M", hash="BLAKE2B-256-128", key=KEY)
+    with pytest.raises(_lib.KcdcError):
+        WriterBatcher("DYNAMIC-4M-BUZHASH", hash="NO-SUCH-HASH", key=KEY)

@@ -5,7 +5,9 @@
 // final cut lists (PCIe included).  The cuts are checked against kcdc_split_batch_host on the
 // same objects (the whole-stream path, itself checked against the oracle by the GPU tests).
 // Prints one JSON line.
-//   build/writer_bench [writers=64] [MiB per writer=64] [slice KiB=64] [name] [round MiB=256] [reps=3]
+//   build/writer_bench [writers=64] [MiB per writer=64] [slice KiB=64] [name] [round MiB=256] [reps=3] [hash=none]
+// hash: a content-hash name (kcdc_bw_batcher_hash with a 32-byte secret): every final chunk is also
+// named on the device and the rate counts host bytes to (cut, ID) pairs.
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -24,6 +26,8 @@ int main(int argc, char** argv) {
     const std::string name = argc > 4 ? argv[4] : "DYNAMIC-4M-BUZHASH";
     const uint64_t round = (argc > 5 ? std::strtoull(argv[5], nullptr, 10) : 256) << 20;
     const int reps = argc > 6 ? std::atoi(argv[6]) : 3;
+    const std::string hash = argc > 7 ? argv[7] : "none";
+    const bool ids = hash != "none";
     if (kcdc_device_count() < 1) {
         std::fprintf(stderr, "no gfx950 device: %s\n", kcdc_last_error());
         return 1;
@@ -63,8 +67,16 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "kcdc_bw_batcher_new: %s\n", kcdc_last_error());
         return 1;
     }
+    if (ids) {
+        uint8_t key[32];
+        for (int i = 0; i < 32; i++) key[i] = static_cast<uint8_t>(7 + i);
+        if (kcdc_bw_batcher_hash(b, hash.c_str(), key, 32)) {
+            std::fprintf(stderr, "kcdc_bw_batcher_hash: %s\n", kcdc_last_error());
+            return 1;
+        }
+    }
     std::vector<double> rates;
-    double st0[18] = {0};  // the stats after the warm-up rep: the steady-state pool misses are the rest
+    double st0[21] = {0};  // the stats after the warm-up rep: the steady-state pool misses are the rest
     bool ok = true;
     for (int r = 0; r < reps + 1; r++) {  // rep 0 warms the pinned pool and device buffers
         std::vector<std::vector<uint64_t>> got(W);
@@ -75,6 +87,15 @@ int main(int argc, char** argv) {
             th.emplace_back([&, i] {
                 kcdc_bw* w = kcdc_bw_open(b);
                 uint64_t buf[256];
+                static thread_local uint8_t idbuf[256 * 32];
+                auto take = [&] {
+                    if (ids) {
+                        for (int64_t n; (n = kcdc_bw_cuts_ids(w, buf, idbuf, 32, 256)) > 0;)
+                            got[i].insert(got[i].end(), buf, buf + n);
+                    } else {
+                        for (int64_t n; (n = kcdc_bw_cuts(w, buf, 256)) > 0;) got[i].insert(got[i].end(), buf, buf + n);
+                    }
+                };
                 ready++;
                 while (!go.load()) std::this_thread::yield();
                 size_t pos = 0, calls = 0;
@@ -85,14 +106,13 @@ int main(int argc, char** argv) {
                         std::exit(1);
                     }
                     pos += k;
-                    if (++calls % 16 == 0)
-                        for (int64_t n; (n = kcdc_bw_cuts(w, buf, 256)) > 0;) got[i].insert(got[i].end(), buf, buf + n);
+                    if (++calls % 16 == 0) take();
                 }
                 if (kcdc_bw_finish(w)) {
                     std::fprintf(stderr, "kcdc_bw_finish: %s\n", kcdc_last_error());
                     std::exit(1);
                 }
-                for (int64_t n; (n = kcdc_bw_cuts(w, buf, 256)) > 0;) got[i].insert(got[i].end(), buf, buf + n);
+                take();
                 kcdc_bw_free(w);
             });
         while (ready.load() < W) std::this_thread::yield();
@@ -101,13 +121,13 @@ int main(int argc, char** argv) {
         for (auto& t : th) t.join();
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         if (r > 0) rates.push_back(static_cast<double>(W) * L / s / (1ull << 30));
-        if (r == 0) kcdc_bw_stats(b, st0, 18);
+        if (r == 0) kcdc_bw_stats(b, st0, 21);
         for (int i = 0; i < W; i++)
             ok = ok && got[i] == std::vector<uint64_t>(ref.begin() + base[i], ref.begin() + base[i] + counts[i]);
     }
     const int64_t rounds = kcdc_bw_rounds(b);
-    double st[18] = {0};
-    kcdc_bw_stats(b, st, 18);
+    double st[21] = {0};
+    kcdc_bw_stats(b, st, 21);
     kcdc_bw_batcher_free(b);
     // the host-side ceiling: the same W threads only copying their slices into 4 MiB buffers
     double copy_rate = 0;
@@ -142,9 +162,9 @@ int main(int argc, char** argv) {
                 "\"round_wait_s\": %.3f, \"dev_gather_s\": %.3f, \"dev_split_s\": %.3f, \"dev_span_s\": %.3f, "
                 "\"dev_busy_s\": %.3f, \"host_s\": [%.3f, %.3f, %.3f, %.3f, %.3f], "
                 "\"round_idle_s\": %.3f, \"writer_capped_s\": %.3f, \"writer_block_s\": %.3f, \"pool_misses\": %.0f, \"pool_misses_after_warmup\": %.0f, \"writer_block_s_after_warmup\": %.3f, \"round_lock_s\": %.3f, "
-                "\"memcpy_only_gib_s\": %.2f, \"parity_ok\": %s}\n",
+                "\"memcpy_only_gib_s\": %.2f, \"hash\": \"%s\", \"ids_named\": %.0f, \"hash_steps\": %.0f, \"hash_dev_s\": %.3f, \"parity_ok\": %s}\n",
                 W, L >> 20, S >> 10, name.c_str(), static_cast<unsigned long long>(round >> 20),
                 rates.empty() ? 0.0 : sum / rates.size(), best, static_cast<long long>(rounds), st[2], st[3], st[4], st[5], st[6], st[7], st[8], st[9], st[10], st[11], st[12], st[13], st[14], st[15], st[16], st[16] - st0[16], st[15] - st0[15], st[17], copy_rate,
-                ok ? "true" : "false");
+                hash.c_str(), st[18], st[19], st[20], ok ? "true" : "false");
     return ok ? 0 : 2;
 }
