@@ -399,8 +399,10 @@ int kcdc_compress_chunks_device(const char* algorithm, const uint8_t* d_data, co
  *                         chunks, else 1), 1 or 4
  *   KCDC_TEST_NO_SERVER   1: private streaming handles launch one scan per call instead of using
  *                         the device's resident scan server
- *   KCDC_TEST_NO_HELP     1: buzhash batch launches without intra-region help (each region is
- *                         scanned by the wave that owns its stream only)
+ *   KCDC_TEST_NO_HELP     1: batch launches without intra-region help (each region is scanned by
+ *                         the wave that owns its stream only); 2: help on whatever the average
+ *                         (0, the default: help for averages of 1 MiB and up, and for Rabin-Karp
+ *                         launches with fewer streams than waves)
  * kcdc_test_occupy: occupy `nwg` CUs (one workgroup with all of the CU's LDS each) for
  * `usec` microseconds on `hip_stream`, e.g. to run a batch beside a kernel that holds CUs.
  * kcdc_test_queue_stat: after the last pipelined batch launch has finished (synchronise

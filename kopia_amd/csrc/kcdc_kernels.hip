@@ -3448,7 +3448,7 @@ struct TestKnobs {
     uint32_t spin_cap = 0;     // 0: dev::kSpinCap
     bool no_steal = false;     // disable try_steal
     bool force_error = false;  // mark every pipelined launch as failed
-    bool no_help = false;      // buzhash batches without help slots (A/B, tests)
+    int help = 0;              // intra-region help: 0 the policy below, 1 off, 2 on (A/B, tests)
     char* last_ws = nullptr;   // queue header of the last pipelined launch (kcdc_test_queue_stat)
     int last_dev = 0;
 };
@@ -3601,9 +3601,10 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         // help off, 512K 2.37 vs 2.27; 64 x 64 MiB 128K-BUZHASH 27.5 vs 22.2 ms), except for the
         // Rabin-Karp kernel in launches with fewer streams than waves (64 x 64 MiB 128K-RABINKARP
         // 30.1 vs 38.0 ms); DESIGN.md §2.1d, profiles/r05/help_policy/.
-        const bool helpers = !g_test.no_help &&
-                             (algo.avg >= (1ull << 20) ||
-                              (algo.kind == kRabinKarp && s.nstreams < static_cast<uint64_t>(cus) * wg_waves));
+        const bool helpers = g_test.help == 2 ||
+                             (g_test.help == 0 &&
+                              (algo.avg >= (1ull << 20) ||
+                               (algo.kind == kRabinKarp && s.nstreams < static_cast<uint64_t>(cus) * wg_waves)));
         unsigned grid = helpers || need >= cus ? cus : need;
         if (grid > dev::kMaxPipeGrid) grid = dev::kMaxPipeGrid;  // one claim flag per workgroup
         uint64_t ring = 1;
@@ -4058,7 +4059,7 @@ extern "C" int kcdc_test_set(int32_t key, int64_t value) {
         case 3: g_test.force_error = value != 0; return 0;                  // KCDC_TEST_FORCE_ERROR
         case 4: test_hash_lanes() = static_cast<int>(value); return 0;     // KCDC_TEST_HASH_LANES
         case 5: set_scan_server_off(value != 0); return 0;                 // KCDC_TEST_NO_SERVER
-        case 6: g_test.no_help = value != 0; return 0;                      // KCDC_TEST_NO_HELP
+        case 6: g_test.help = value == 2 ? 2 : value != 0; return 0;       // KCDC_TEST_NO_HELP (2: force help on)
         default: return set_error(-22, "unknown test knob");
     }
 }

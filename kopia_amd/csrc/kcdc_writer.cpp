@@ -141,7 +141,8 @@ struct BwDev {
     std::chrono::microseconds wait{0};
     hipStream_t stream = nullptr, copy = nullptr;
 
-    std::mutex mu;                     // open list, pool, writer cut state (lock order: mu, then a writer's mu)
+    std::mutex mu;                     // open list, writer cut state (lock order: mu, then a writer's mu, then pool_mu)
+    std::mutex pool_mu;                // the pinned block pool (writers take blocks without the round thread's mutex)
     std::condition_variable cv_round;  // round thread: work arrived
     std::condition_variable cv_done;   // finishing writers: a round completed
     std::vector<kcdc_bw*> open;        // writers not yet freed
@@ -281,9 +282,9 @@ struct BwDev {
         if (copy) (void)hipStreamDestroy(copy);
         if (stream) (void)hipStreamDestroy(stream);
     }
-    uint8_t* get_block() {  // mu not held: new pinned blocks are allocated outside it
+    uint8_t* get_block() {  // pool_mu not held: new pinned blocks are allocated outside it
         {
-            std::lock_guard<std::mutex> lk(mu);
+            std::lock_guard<std::mutex> lk(pool_mu);
             if (!pool.empty()) {
                 uint8_t* b = pool.back();
                 pool.pop_back();
@@ -297,7 +298,7 @@ struct BwDev {
         Guard g(device);
         if (hipHostMalloc(&p, kSlabBlocks * kBlock, hipHostMallocDefault) != hipSuccess) return nullptr;
         uint8_t* s = static_cast<uint8_t*>(p);
-        std::lock_guard<std::mutex> lk(mu);
+        std::lock_guard<std::mutex> lk(pool_mu);
         slabs.push_back(s);
         for (size_t i = 1; i < kSlabBlocks; i++) pool.push_back(s + i * kBlock);
         return s;
@@ -350,6 +351,8 @@ struct kcdc_bw {
     uint64_t ids_base = 0;       // wseq of ids.front()
     uint64_t ids_made = 0;       // entries ever created
     uint64_t ids_ready = 0;      // entries whose digest has arrived
+    // entries ready at the front / taken (kcdc_bw_cuts_ids answers "nothing new" without the mutex)
+    std::atomic<uint64_t> ids_pub{0}, ids_taken{0};
     uint64_t id_from = 0;        // start of the next final chunk
 };
 
@@ -419,7 +422,10 @@ void BwDev::loop() {
         for (uint32_t k = 0; k < n; k++) {
             Job& j = r.jobs[k];
             kcdc_bw* w = j.w;
-            for (uint8_t* blk : j.retire) pool.push_back(blk);
+            if (!j.retire.empty()) {
+                std::lock_guard<std::mutex> pl(pool_mu);
+                for (uint8_t* blk : j.retire) pool.push_back(blk);
+            }
             const uint64_t len = j.to - w->tail_pos;
             const uint64_t cnt = hp[5 * n + k];
             if (cnt == ~0ull || cnt > len / algo->min_size() + 2)
@@ -450,6 +456,7 @@ void BwDev::loop() {
     // split reads the arenas), not when its cuts arrive.  mu held.
     auto recycle = [&](Round& r) {
         if (!r.live || r.recycled || hipEventQuery(meta[r.m].gathered) != hipSuccess) return;
+        std::lock_guard<std::mutex> pl(pool_mu);
         for (Job& j : r.jobs) {
             for (uint8_t* blk : j.retire) pool.push_back(blk);
             j.retire.clear();
@@ -826,6 +833,15 @@ int BwDev::id_pump(bool block) {
             en.ready = true;
             c.w->ids_ready++;
         }
+        // publish each touched writer's ready prefix (digests arrive out of order across chains)
+        for (const auto& d : step_done) {
+            Chain& c = chains[d.first - chain_tail];
+            if (!c.w) continue;
+            kcdc_bw* w = c.w;
+            uint64_t k = w->ids_pub.load(std::memory_order_relaxed);
+            while (k - w->ids_base < w->ids.size() && w->ids[k - w->ids_base].ready) k++;
+            w->ids_pub.store(k, std::memory_order_release);
+        }
         step_done.clear();
         while (!chains.empty() && chains.front().fin) {
             ring_tail = chains.front().ring_end;
@@ -1167,9 +1183,16 @@ extern "C" int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len) {
             nb.pos = w->written;
             w->blocks.push_back(nb);
         }
+        // Copy without the writer's mutex: a writer preempted inside a 64 KiB copy (more writer
+        // threads than CPUs) would hold up the round thread's collection, and with it every writer
+        // waiting on the batcher.  Only this thread appends blocks or moves `end`; the round thread
+        // never retires the last block while it is partial, so the block stays the last one.
+        const size_t k = std::min<size_t>(len, kBlock - w->blocks.back().end);
+        uint8_t* dst = w->blocks.back().p + w->blocks.back().end;
+        wl.unlock();
+        std::memcpy(dst, p, k);
+        wl.lock();
         Blk& bk = w->blocks.back();
-        const size_t k = std::min<size_t>(len, kBlock - bk.end);
-        std::memcpy(bk.p + bk.end, p, k);
         bk.end += static_cast<uint32_t>(k);
         w->written += k;
         if (w->written > w->counted) {  // bytes beyond the size hint count toward the device's load
@@ -1248,6 +1271,8 @@ extern "C" int64_t kcdc_bw_cuts_ids(kcdc_bw* w, uint64_t* cuts, uint8_t* ids, ui
     BwDev* b = w->b;
     if (!b->ids.on) return set_error(KCDC_EINVAL, "content IDs are off (kcdc_bw_batcher_hash)");
     if (id_stride < b->ids.out || (cap && (!cuts || !ids))) return set_error(KCDC_EINVAL, "bad ID buffer");
+    if (w->ids_pub.load(std::memory_order_acquire) == w->ids_taken.load(std::memory_order_relaxed) && !b->error)
+        return 0;
     std::lock_guard<std::mutex> lk(b->mu);
     uint64_t k = 0;
     while (k < cap && !w->ids.empty() && w->ids.front().ready) {
@@ -1258,6 +1283,7 @@ extern "C" int64_t kcdc_bw_cuts_ids(kcdc_bw* w, uint64_t* cuts, uint8_t* ids, ui
         w->ids_base++;
         k++;
     }
+    w->ids_taken.fetch_add(k, std::memory_order_relaxed);
     if (b->error && k == 0) return dev_error(b);
     return static_cast<int64_t>(k);
 }
@@ -1288,7 +1314,10 @@ extern "C" void kcdc_bw_free(kcdc_bw* w) {
         for (BwDev::Chain& c : b->chains)  // (an error left chains of this writer unnamed)
             if (c.w == w) c.w = nullptr;
         b->load -= std::min<uint64_t>(b->load.load(), w->counted);
-        for (Blk& bk : w->blocks) b->pool.push_back(bk.p);
+        {
+            std::lock_guard<std::mutex> pl(b->pool_mu);
+            for (Blk& bk : w->blocks) b->pool.push_back(bk.p);
+        }
         b->open.erase(std::find(b->open.begin(), b->open.end(), w));
         if (w->arena && w->done && !b->error && b->arenas.size() < b->keep_arenas()) {
             // its last round has completed (finish waited for it), so no gather, compaction or

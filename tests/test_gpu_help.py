@@ -167,3 +167,21 @@ def test_many_streams_with_yields(gpu, name, ns):
     cuts, counts = coracle.split_prng_streams(name, SEED, np.arange(ns), L, nthreads=16)
     bad = [i for i in range(ns) if got[i].tolist() != cuts[i, :counts[i]].tolist()]
     assert not bad, bad[:8]
+
+
+@pytest.mark.parametrize("name", ["DYNAMIC-128K-BUZHASH", "DYNAMIC-512K-RABINKARP"])
+def test_forced_help_below_policy(gpu, name):
+    """Below 1 MiB the policy keeps help off; forced on (KCDC_TEST_NO_HELP = 2)
+    the protocol must still cut exactly: small averages mean many regions per tile and owners
+    closing regions while helpers scan them."""
+    import torch
+    ns, L = 2304, 1 << 20
+    data = torch.empty(ns * L, dtype=torch.uint8, device=gpu)
+    batch.fill_prng(data, L, ns, L, SEED, first_sid=11)
+    with knob(_lib.TEST_NO_HELP, 2):
+        got, helps = _split(name, data, [i * L for i in range(ns)], [L] * ns, gpu)
+        giveups = _lib.lib().kcdc_test_queue_stat(_lib.STAT_GIVEUPS)
+    assert helps > 0 and giveups == 0
+    cuts, counts = coracle.split_prng_streams(name, SEED, np.arange(11, 11 + ns), L, nthreads=16)
+    bad = [i for i in range(ns) if got[i].tolist() != cuts[i, :counts[i]].tolist()]
+    assert not bad, bad[:8]
