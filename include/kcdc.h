@@ -185,9 +185,10 @@ void kcdc_bw_free(kcdc_bw* w);
  * with its chunk's digest (kcdc_hash_size bytes at ids + i * id_stride), as soon as the digests of
  * every chunk up to it are known; kcdc_bw_finish also waits for the last chunk's digest.  BLAKE2
  * names hash in slices of 256 KiB per chunk per step (a chunk is one chain of compressions), the
- * others whole chunks per step.  Device memory: an ID ring of max(16 x round_bytes, 1 GiB) per
- * device holds the chunks until they are named.  FIXED names: KCDC_EINVAL (their writers stage no
- * bytes on the device). */
+ * others whole chunks per step, on a hash thread of their own.  Device memory: an ID ring of
+ * max(32 x round_bytes, 1 GiB) per device holds the chunks until they are named (a chunk is one
+ * dependent chain, so the naming rate grows with the chunks in flight).  FIXED names: KCDC_EINVAL
+ * (their writers stage no bytes on the device). */
 int kcdc_bw_batcher_hash(kcdc_bw_batcher* b, const char* hash_name, const uint8_t* key, uint32_t key_len);
 int64_t kcdc_bw_cuts_ids(kcdc_bw* w, uint64_t* cuts, uint8_t* ids, uint32_t id_stride, uint64_t cap);
 int64_t kcdc_bw_rounds(const kcdc_bw_batcher* b); /* rounds shipped so far (test hook) */

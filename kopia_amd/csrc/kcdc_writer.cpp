@@ -200,11 +200,12 @@ struct BwDev {
 
     // ---- content IDs (kcdc_bw_batcher_hash): every final chunk's keyed hash, computed on the
     // device from the bytes the round already holds (content_manager.go:812 hashes each chunk the
-    // object writer flushes).  At a round's completion each new final chunk is copied from the
-    // writer's arena into the ID ring (copy stream, ordered after that round's compactions) and
-    // gets a chain; the chains advance in slices on their own stream (one step in flight at a
-    // time, every pending chain moved by at most step_blocks blocks), since a BLAKE2 chunk is one
-    // long dependent chain.  Ring bytes and chain slots are reused first in, first out.
+    // object writer flushes).  At a round's completion the round thread copies each new final chunk
+    // from the writer's arena into the ID ring (copy stream, ordered after that round's compactions)
+    // and publishes a chain for it.  A hash thread of its own advances the chains in slices on the
+    // hash stream, two steps in flight so the stream never idles between them (a BLAKE2 chunk is one
+    // long dependent chain: throughput = chains in flight x one chain's rate, so the ring must stay
+    // full and the steps back to back).  Ring bytes and chain slots are reused first in, first out.
     struct IdCfg {
         bool on = false;
         std::string name;
@@ -224,33 +225,52 @@ struct BwDev {
         kcdc_bw* w;
         uint64_t wseq, pos, len;
     };
+    struct Step {  // one hash step's host-side buffers (two steps may be in flight)
+        hipEvent_t t0 = nullptr, ev = nullptr;
+        uint8_t* h_dig = nullptr;  // digests: by slot (kinds 1, 2) or by position in the step (kind 3)
+        uint32_t* h_act = nullptr; // active chain slots
+        uint64_t* h_ol = nullptr;  // kind 3: ring offsets, then lengths
+        std::vector<std::pair<uint64_t, uint32_t>> done;  // (chain number, digest row) ending in this step
+    } steps[2];
     std::vector<NewChunk> newc;        // final chunks of the last completed round (round thread)
     hipStream_t hstream = nullptr;
     uint8_t* ring = nullptr;
-    uint64_t ring_cap = 0, ring_head = 0, ring_tail = 0;  // monotonic byte offsets
+    // monotonic byte offsets; ring_head: round thread (reservations), ring_tail: hash thread (mu)
+    uint64_t ring_cap = 0, ring_head = 0, ring_tail = 0;
     HashChain* d_chains = nullptr;
-    HashChain* h_chains = nullptr;     // pinned: new chains' records, by slot
+    HashChain* h_chains = nullptr;     // pinned: new chains' records, by slot (round thread writes, hash thread uploads)
     uint32_t chain_cap = 0;
-    uint64_t chain_head = 0, chain_tail = 0, uploaded = 0;  // monotonic chain numbers
+    // monotonic chain numbers (mu): [chain_tail, chain_head) published, [.., uploaded) uploaded
+    uint64_t chain_head = 0, chain_tail = 0, uploaded = 0;
+    uint64_t undone = 0;               // (mu) published chains with blocks not yet issued
     std::deque<Chain> chains;          // chains [chain_tail, chain_head)
-    uint8_t* d_dig = nullptr;          // digests: by slot (kinds 1, 2) or by position in the step (kind 3)
-    uint8_t* h_dig = nullptr;
-    uint32_t* d_act = nullptr;         // a step's active chain slots
-    uint32_t* h_act = nullptr;
-    uint64_t* d_ol = nullptr;          // kind 3: ring offsets, then lengths
-    uint64_t* h_ol = nullptr;
-    hipEvent_t copy_ev = nullptr, step_ev = nullptr, step_t0 = nullptr;
-    bool step_live = false;
-    std::vector<std::pair<uint64_t, uint32_t>> step_done;  // (chain number, digest row) ending in the live step
+    uint8_t* d_dig = nullptr;
+    uint32_t* d_act = nullptr;
+    uint64_t* d_ol = nullptr;
+    hipEvent_t copy_ev = nullptr;      // the ring copies of the chains published so far
     uint64_t step_blocks = 0;
     uint64_t id_chains = 0, id_steps = 0;
     double t_hash = 0;                 // device seconds of the hash steps
+    std::condition_variable cv_hash;   // hash thread: chains published, or stop
+    std::condition_variable cv_space;  // round thread: ring space or chain slots freed
+    bool hstop = false;                // (mu) the round thread has published its last chains
+    std::thread hth;
     int ids_enable(const char* name, const uint8_t* key, uint32_t key_len);
     int id_create();                   // round thread, mu not held: newc -> chains (ring copies)
-    int id_pump(bool block);           // round thread, mu not held: deliver a finished step, issue the next
-    bool id_busy() const { return step_live || chain_tail != chain_head; }
+    int id_issue(Step& st, bool& issued);  // hash thread, mu not held
+    int id_deliver(Step& st);          // hash thread, mu not held
+    void hash_loop();
+    void fail(int rc);                 // mu not held: record the first error, wake everyone
 
     ~BwDev() {
+        if (hth.joinable()) {  // (a batcher whose round thread never started it cleanly)
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                hstop = true;
+            }
+            cv_hash.notify_all();
+            hth.join();
+        }
         if (algo->kind == kFixed) return;
         Guard g(device);
         for (uint8_t* s : slabs) (void)hipHostFree(s);
@@ -267,17 +287,20 @@ struct BwDev {
                 if (e) (void)hipEventDestroy(e);
         }
         if (ev_ref) (void)hipEventDestroy(ev_ref);
-        for (hipEvent_t e : {copy_ev, step_ev, step_t0})
-            if (e) (void)hipEventDestroy(e);
+        if (copy_ev) (void)hipEventDestroy(copy_ev);
+        for (Step& st : steps) {
+            for (hipEvent_t e : {st.t0, st.ev})
+                if (e) (void)hipEventDestroy(e);
+            if (st.h_dig) (void)hipHostFree(st.h_dig);
+            if (st.h_act) (void)hipHostFree(st.h_act);
+            if (st.h_ol) (void)hipHostFree(st.h_ol);
+        }
         if (ring) (void)hipFree(ring);
         if (d_chains) (void)hipFree(d_chains);
         if (h_chains) (void)hipHostFree(h_chains);
         if (d_dig) (void)hipFree(d_dig);
-        if (h_dig) (void)hipHostFree(h_dig);
         if (d_act) (void)hipFree(d_act);
-        if (h_act) (void)hipHostFree(h_act);
         if (d_ol) (void)hipFree(d_ol);
-        if (h_ol) (void)hipHostFree(h_ol);
         if (hstream) (void)hipStreamDestroy(hstream);
         if (copy) (void)hipStreamDestroy(copy);
         if (stream) (void)hipStreamDestroy(stream);
@@ -383,18 +406,6 @@ void BwDev::loop() {
     Guard g(device);
     Round inflight;
     int next_meta = 0;
-    auto fail = [&](int rc) {
-        std::lock_guard<std::mutex> lk(mu);
-        if (!error) {
-            errmsg = kcdc_last_error();
-            error = rc;
-        }
-        cv_done.notify_all();
-        for (kcdc_bw* w : open) {
-            std::lock_guard<std::mutex> wl(w->mu);
-            w->cv.notify_all();
-        }
-    };
     // Wait for round r's cuts and apply them (final cuts, frontier, tail position).  mu not held.
     auto complete = [&](Round& r) -> int {
         if (!r.live) return KCDC_OK;
@@ -477,17 +488,6 @@ void BwDev::loop() {
         const auto idle0 = std::chrono::steady_clock::now();
         while (!work() && !timed_out) {
             recycle(inflight);
-            if (ids.on && id_busy()) {
-                lk.unlock();
-                const int rc = id_pump(false);
-                lk.lock();
-                if (rc != KCDC_OK) {
-                    lk.unlock();
-                    fail(rc);
-                    lk.lock();
-                    break;
-                }
-            }
             if (inflight.live) {
                 if (hipEventQuery(meta[inflight.m].done) == hipSuccess) {
                     lk.unlock();
@@ -504,10 +504,6 @@ void BwDev::loop() {
                 }
                 continue;
             }
-            if (ids.on && id_busy()) {  // hash steps in flight: poll them as a round in flight
-                cv_round.wait_for(lk, std::chrono::microseconds(100), work);
-                continue;
-            }
             if (staged.load() > 0) {
                 const auto since_tp = std::chrono::steady_clock::time_point(std::chrono::nanoseconds(since.load()));
                 const auto due = std::max(last, since_tp) + wait;
@@ -522,7 +518,7 @@ void BwDev::loop() {
         t_idle += std::chrono::duration<double>(std::chrono::steady_clock::now() - idle0).count();
         if (error) break;
         if (staged.load() == 0 && finish_pending.load() == 0) {
-            if (stop && !(ids.on && id_busy() && !error)) break;
+            if (stop) break;
             continue;
         }
         recycle(inflight);
@@ -635,7 +631,6 @@ void BwDev::loop() {
             // its final chunks' ring copies queue on the copy stream behind this round's compactions
             if (rc == KCDC_OK && ids.on) rc = id_create();
         }
-        if (rc == KCDC_OK && ids.on) rc = id_pump(false);
         lap(3);
         // ---- launch R over every job's region [tail_pos, to)
         if (rc == KCDC_OK) {
@@ -719,12 +714,31 @@ void BwDev::loop() {
         if (rc == KCDC_OK && ids.on) rc = id_create();
         if (rc != KCDC_OK) fail(rc);
     }
-    while (ids.on && id_busy() && !error) {  // drain the chains of the last rounds
-        const int rc = id_pump(true);
-        if (rc != KCDC_OK) fail(rc);
-    }
     lk.lock();
     cv_done.notify_all();
+    if (ids.on) {  // the hash thread names the chains of the last rounds, then ends
+        hstop = true;
+        cv_hash.notify_all();
+        lk.unlock();
+        if (hth.joinable()) hth.join();
+        lk.lock();
+        cv_done.notify_all();
+    }
+}
+
+void BwDev::fail(int rc) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!error) {
+        errmsg = kcdc_last_error();
+        error = rc;
+    }
+    cv_done.notify_all();
+    cv_space.notify_all();
+    cv_hash.notify_all();
+    for (kcdc_bw* w : open) {
+        std::lock_guard<std::mutex> wl(w->mu);
+        w->cv.notify_all();
+    }
 }
 
 // ---------------------------------------------------------------- content IDs
@@ -739,7 +753,9 @@ int BwDev::ids_enable(const char* name, const uint8_t* key, uint32_t key_len) {
     ids.kind = kind;
     // slices of 256 KiB per chain per step: a 4 MiB chunk is named after ~16 steps
     step_blocks = kind == 1 ? 2048 : 4096;
-    ring_cap = std::max<uint64_t>(16 * round_bytes, 1ull << 30);
+    // chains in flight set the naming rate (one chain: ~55 MB/s of BLAKE2b), so the ring holds 32
+    // rounds: ~2,000 chunks of 4 MiB at the default 256 MiB rounds
+    ring_cap = std::max<uint64_t>(32 * round_bytes, 1ull << 30);
     chain_cap = 16384;
     Guard g(device);
     hipError_t e = hipStreamCreateWithFlags(&hstream, hipStreamNonBlocking);
@@ -747,49 +763,75 @@ int BwDev::ids_enable(const char* name, const uint8_t* key, uint32_t key_len) {
     if (e == hipSuccess) e = hipMalloc(&d_chains, sizeof(HashChain) * chain_cap);
     if (e == hipSuccess) e = hipHostMalloc(&h_chains, sizeof(HashChain) * chain_cap, hipHostMallocDefault);
     if (e == hipSuccess) e = hipMalloc(&d_dig, 32ull * chain_cap);
-    if (e == hipSuccess) e = hipHostMalloc(&h_dig, 32ull * chain_cap, hipHostMallocDefault);
     if (e == hipSuccess) e = hipMalloc(&d_act, 4ull * chain_cap);
-    if (e == hipSuccess) e = hipHostMalloc(&h_act, 4ull * chain_cap, hipHostMallocDefault);
     if (e == hipSuccess) e = hipMalloc(&d_ol, 16ull * chain_cap);
-    if (e == hipSuccess) e = hipHostMalloc(&h_ol, 16ull * chain_cap, hipHostMallocDefault);
-    for (hipEvent_t* ev : {&copy_ev, &step_ev, &step_t0})
-        if (e == hipSuccess) e = hipEventCreate(ev);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&copy_ev, hipEventDisableTiming);
+    for (Step& st : steps) {
+        if (e == hipSuccess) e = hipHostMalloc(&st.h_dig, 32ull * chain_cap, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipHostMalloc(&st.h_act, 4ull * chain_cap, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipHostMalloc(&st.h_ol, 16ull * chain_cap, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipEventCreate(&st.t0);
+        // the hash thread sleeps in hipEventSynchronize instead of spinning beside the writers
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&st.ev, hipEventBlockingSync);
+    }
     if (e != hipSuccess) return hip_err(e, "writer content IDs: device memory");
     ids.on = true;
+    hth = std::thread([this] { hash_loop(); });
     return KCDC_OK;
 }
 
-// The last completed round's final chunks (newc) become chains: ring space and a slot each (waiting
-// for steps to free them when the ring is full), and a copy from the writer's arena into the ring.
-// Called right after complete(): the arena pointers are those of the compactions queued before it
-// on the copy stream, and the copies queue behind them, before any later compaction.
+// The last completed round's final chunks (newc) become chains: ring space and a slot each, a
+// copy from the writer's arena into the ring, then (after an event on the copy stream) the chain
+// is published to the hash thread.  Called right after complete(): the arena pointers are those of
+// the compactions queued before it on the copy stream, and the copies queue behind them, before
+// any later compaction.  When the ring is full it publishes what it has copied and waits for the
+// hash thread to free space.
 int BwDev::id_create() {
     if (newc.empty()) return KCDC_OK;
     Guard g(device);
-    bool copied = false;
+    std::vector<Chain> made;
+    auto publish = [&]() -> int {
+        if (made.empty()) return KCDC_OK;
+        hipError_t e = hipEventRecord(copy_ev, copy);  // before the chains are visible (hash thread waits on it)
+        if (e != hipSuccess) return hip_err(e, "writer content IDs: copy event");
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            for (const Chain& c : made) chains.push_back(c);
+            chain_head += made.size();
+            undone += made.size();
+            id_chains += made.size();
+        }
+        made.clear();
+        cv_hash.notify_one();
+        return KCDC_OK;
+    };
     for (const NewChunk& nc : newc) {
         const uint64_t need = (nc.len + 15) & ~uint64_t(15);
         if (need > ring_cap) return set_error(KCDC_EIO, "writer content IDs: chunk larger than the ID ring");
-        uint64_t at = ring_head;
+        uint64_t at = 0;
         for (;;) {
-            at = ring_head;
-            if (at % ring_cap + need > ring_cap) at += ring_cap - at % ring_cap;  // no chunk wraps
-            if (at + need - ring_tail <= ring_cap && chain_head - chain_tail < chain_cap) break;
-            if (copied) {  // the chains waiting for space may read bytes just copied: order the copies first
-                hipError_t e = hipEventRecord(copy_ev, copy);
-                if (e != hipSuccess) return hip_err(e, "writer content IDs: copy event");
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                if (error) return error;
+                at = ring_head;
+                if (at % ring_cap + need > ring_cap) at += ring_cap - at % ring_cap;  // no chunk wraps
+                if (at + need - ring_tail <= ring_cap && chain_head + made.size() - chain_tail < chain_cap) break;
+                if (made.empty()) {
+                    if (chain_tail == chain_head)
+                        return set_error(KCDC_EIO, "writer content IDs: ring full with no chain in flight");
+                    cv_space.wait_for(lk, std::chrono::milliseconds(2));
+                    continue;
+                }
             }
-            const int rc = id_pump(true);
+            const int rc = publish();  // the waiting chains may need the bytes just copied
             if (rc != KCDC_OK) return rc;
-            if (!id_busy() && !(at + need - ring_tail <= ring_cap && chain_head - chain_tail < chain_cap))
-                return set_error(KCDC_EIO, "writer content IDs: ring full with no chain in flight");
         }
-        const uint32_t slot = static_cast<uint32_t>(chain_head % chain_cap);
+        const uint64_t cn = chain_head + made.size();  // (only this thread grows chain_head)
+        const uint32_t slot = static_cast<uint32_t>(cn % chain_cap);
         uint8_t* dst = ring + at % ring_cap;
         if (nc.len) {
             hipError_t e = hipMemcpyAsync(dst, nc.w->arena + (nc.pos - nc.w->origin), nc.len, hipMemcpyDeviceToDevice, copy);
             if (e != hipSuccess) return hip_err(e, "writer content IDs: ring copy");
-            copied = true;
         }
         HashChain& hc = h_chains[slot];
         std::memset(&hc, 0, sizeof(hc));
@@ -799,112 +841,144 @@ int BwDev::id_create() {
         hc.out = slot;
         const uint64_t bb = ids.kind == 2 ? 64 : 128;
         const uint64_t nblk = ids.kind == 3 ? 1 : nc.len ? (nc.len + bb - 1) / bb : 1;
-        std::lock_guard<std::mutex> lk(mu);
-        chains.push_back(Chain{nc.w, nc.wseq, at, at + need, nc.len, nblk, 0, false});
-        chain_head++;
+        made.push_back(Chain{nc.w, nc.wseq, at, at + need, nc.len, nblk, 0, false});
         ring_head = at + need;
-        id_chains++;
     }
     newc.clear();
-    if (copied) {
-        hipError_t e = hipEventRecord(copy_ev, copy);
-        if (e != hipSuccess) return hip_err(e, "writer content IDs: copy event");
-    }
-    return KCDC_OK;
+    return publish();
 }
 
-// Deliver the step in flight once it has finished (block: wait for it), then issue the next one
-// over every chain not yet named.
-int BwDev::id_pump(bool block) {
-    Guard g(device);
-    if (step_live) {
-        const hipError_t q = block ? hipEventSynchronize(step_ev) : hipEventQuery(step_ev);
-        if (q == hipErrorNotReady) return KCDC_OK;
-        if (q != hipSuccess) return hip_err(q, "writer content IDs: hash step");
-        float ms = 0;
-        if (hipEventElapsedTime(&ms, step_t0, step_ev) == hipSuccess) t_hash += ms * 1e-3;
-        std::lock_guard<std::mutex> lk(mu);
-        for (const auto& d : step_done) {
-            Chain& c = chains[d.first - chain_tail];
-            c.fin = true;
-            if (!c.w) continue;  // its writer was freed
-            kcdc_bw::IdEntry& en = c.w->ids[c.wseq - c.w->ids_base];
-            std::memcpy(en.id, h_dig + 32ull * d.second, ids.out);
-            en.ready = true;
-            c.w->ids_ready++;
-        }
-        // publish each touched writer's ready prefix (digests arrive out of order across chains)
-        for (const auto& d : step_done) {
-            Chain& c = chains[d.first - chain_tail];
-            if (!c.w) continue;
-            kcdc_bw* w = c.w;
-            uint64_t k = w->ids_pub.load(std::memory_order_relaxed);
-            while (k - w->ids_base < w->ids.size() && w->ids[k - w->ids_base].ready) k++;
-            w->ids_pub.store(k, std::memory_order_release);
-        }
-        step_done.clear();
-        while (!chains.empty() && chains.front().fin) {
-            ring_tail = chains.front().ring_end;
-            chains.pop_front();
-            chain_tail++;
-        }
-        step_live = false;
-        cv_done.notify_all();
-    }
-    if (chain_head == chain_tail) return KCDC_OK;
-    // ---- the next step: new chains' records up, then every pending chain advanced
-    hipError_t e = hipStreamWaitEvent(hstream, copy_ev, 0);
-    for (uint64_t c0 = uploaded; e == hipSuccess && c0 < chain_head;) {  // slots [uploaded, chain_head) mod cap
-        const uint32_t s0 = static_cast<uint32_t>(c0 % chain_cap);
-        const uint64_t run = std::min<uint64_t>(chain_head - c0, chain_cap - s0);
-        e = hipMemcpyAsync(d_chains + s0, h_chains + s0, run * sizeof(HashChain), hipMemcpyHostToDevice, hstream);
-        c0 += run;
-    }
-    uploaded = chain_head;
-    if (e == hipSuccess) e = hipEventRecord(step_t0, hstream);
-    if (e != hipSuccess) return hip_err(e, "writer content IDs: chain upload");
+// Issue one step over every published chain with blocks left (issued = false: none).
+int BwDev::id_issue(Step& st, bool& issued) {
+    issued = false;
     uint32_t n = 0;
-    int rc = KCDC_OK;
+    uint64_t up0 = 0, up1 = 0;
+    st.done.clear();
     {
         std::lock_guard<std::mutex> lk(mu);
+        if (undone == 0) return KCDC_OK;
+        up0 = uploaded;
+        up1 = uploaded = chain_head;
         for (uint64_t k = 0; k < chains.size(); k++) {
             Chain& c = chains[k];
             if (c.fin || c.done >= c.nblk) continue;
             const uint64_t cn = chain_tail + k;
             if (ids.kind == 3) {  // whole chunks, in this step's order
-                h_ol[n] = c.ring_at % ring_cap;
-                h_ol[chain_cap + n] = c.len;
+                st.h_ol[n] = c.ring_at % ring_cap;
+                st.h_ol[chain_cap + n] = c.len;
                 c.done = c.nblk;
-                step_done.emplace_back(cn, n);
+                st.done.emplace_back(cn, n);
             } else {
-                h_act[n] = static_cast<uint32_t>(cn % chain_cap);
+                st.h_act[n] = static_cast<uint32_t>(cn % chain_cap);
                 c.done = std::min(c.nblk, c.done + step_blocks);
-                if (c.done == c.nblk) step_done.emplace_back(cn, static_cast<uint32_t>(cn % chain_cap));
+                if (c.done == c.nblk) st.done.emplace_back(cn, static_cast<uint32_t>(cn % chain_cap));
             }
+            if (c.done == c.nblk) undone--;
             n++;
         }
     }
     if (n == 0) return KCDC_OK;
+    // the ring copies of every chain published so far, then the new chains' records
+    hipError_t e = hipStreamWaitEvent(hstream, copy_ev, 0);
+    for (uint64_t c0 = up0; e == hipSuccess && c0 < up1;) {  // slots [up0, up1) mod cap
+        const uint32_t s0 = static_cast<uint32_t>(c0 % chain_cap);
+        const uint64_t run = std::min<uint64_t>(up1 - c0, chain_cap - s0);
+        e = hipMemcpyAsync(d_chains + s0, h_chains + s0, run * sizeof(HashChain), hipMemcpyHostToDevice, hstream);
+        c0 += run;
+    }
+    if (e == hipSuccess) e = hipEventRecord(st.t0, hstream);
+    if (e != hipSuccess) return hip_err(e, "writer content IDs: chain upload");
+    int rc = KCDC_OK;
     if (ids.kind == 3) {
-        e = hipMemcpyAsync(d_ol, h_ol, 8ull * n, hipMemcpyHostToDevice, hstream);
-        if (e == hipSuccess) e = hipMemcpyAsync(d_ol + chain_cap, h_ol + chain_cap, 8ull * n, hipMemcpyHostToDevice, hstream);
+        e = hipMemcpyAsync(d_ol, st.h_ol, 8ull * n, hipMemcpyHostToDevice, hstream);
+        if (e == hipSuccess) e = hipMemcpyAsync(d_ol + chain_cap, st.h_ol + chain_cap, 8ull * n, hipMemcpyHostToDevice, hstream);
         if (e != hipSuccess) return hip_err(e, "writer content IDs: chunk list");
         rc = kcdc_hash_chunks_device(ids.name.c_str(), ring, d_ol, d_ol + chain_cap, nullptr, n, ids.key.data(),
                                      static_cast<uint32_t>(ids.key.size()), d_dig, 32, hstream);
-        if (rc == KCDC_OK) e = hipMemcpyAsync(h_dig, d_dig, 32ull * n, hipMemcpyDeviceToHost, hstream);
+        if (rc == KCDC_OK) e = hipMemcpyAsync(st.h_dig, d_dig, 32ull * n, hipMemcpyDeviceToHost, hstream);
     } else {
-        e = hipMemcpyAsync(d_act, h_act, 4ull * n, hipMemcpyHostToDevice, hstream);
+        e = hipMemcpyAsync(d_act, st.h_act, 4ull * n, hipMemcpyHostToDevice, hstream);
         if (e != hipSuccess) return hip_err(e, "writer content IDs: active list");
         rc = launch_hash_chains(ids.name.c_str(), ids.key.data(), static_cast<uint32_t>(ids.key.size()), d_chains, d_act,
                                 n, step_blocks, d_dig, 32, hstream);
-        if (rc == KCDC_OK) e = hipMemcpyAsync(h_dig, d_dig, 32ull * chain_cap, hipMemcpyDeviceToHost, hstream);
+        if (rc == KCDC_OK) e = hipMemcpyAsync(st.h_dig, d_dig, 32ull * chain_cap, hipMemcpyDeviceToHost, hstream);
     }
     if (rc != KCDC_OK) return rc;
-    if (e == hipSuccess) e = hipEventRecord(step_ev, hstream);
+    if (e == hipSuccess) e = hipEventRecord(st.ev, hstream);
     if (e != hipSuccess) return hip_err(e, "writer content IDs: hash step");
-    step_live = true;
-    id_steps++;
+    issued = true;
     return KCDC_OK;
+}
+
+// Wait for a step, then hand its finished digests to their writers and free the ring's head.
+int BwDev::id_deliver(Step& st) {
+    const hipError_t q = hipEventSynchronize(st.ev);
+    if (q != hipSuccess) return hip_err(q, "writer content IDs: hash step");
+    float ms = 0;
+    const bool timed = hipEventElapsedTime(&ms, st.t0, st.ev) == hipSuccess;
+    std::lock_guard<std::mutex> lk(mu);
+    if (timed) t_hash += ms * 1e-3;
+    id_steps++;
+    for (const auto& d : st.done) {
+        Chain& c = chains[d.first - chain_tail];
+        c.fin = true;
+        if (!c.w) continue;  // its writer was freed
+        kcdc_bw::IdEntry& en = c.w->ids[c.wseq - c.w->ids_base];
+        std::memcpy(en.id, st.h_dig + 32ull * d.second, ids.out);
+        en.ready = true;
+        c.w->ids_ready++;
+    }
+    // publish each touched writer's ready prefix (digests arrive out of order across chains)
+    for (const auto& d : st.done) {
+        Chain& c = chains[d.first - chain_tail];
+        if (!c.w) continue;
+        kcdc_bw* w = c.w;
+        uint64_t k = w->ids_pub.load(std::memory_order_relaxed);
+        while (k - w->ids_base < w->ids.size() && w->ids[k - w->ids_base].ready) k++;
+        w->ids_pub.store(k, std::memory_order_release);
+    }
+    st.done.clear();
+    bool freed = false;
+    while (!chains.empty() && chains.front().fin) {
+        ring_tail = chains.front().ring_end;
+        chains.pop_front();
+        chain_tail++;
+        freed = true;
+    }
+    cv_done.notify_all();
+    if (freed) cv_space.notify_all();
+    return KCDC_OK;
+}
+
+// The hash thread: keep two steps in flight while chains have blocks left; end once the round
+// thread has stopped and every chain is named (or on an error).
+void BwDev::hash_loop() {
+    Guard g(device);
+    std::deque<int> live;  // steps in flight, in issue order
+    int next = 0;
+    for (;;) {
+        int rc = KCDC_OK;
+        while (rc == KCDC_OK && live.size() < 2) {
+            bool issued = false;
+            rc = id_issue(steps[next], issued);
+            if (!issued) break;
+            live.push_back(next);
+            next ^= 1;
+        }
+        if (rc == KCDC_OK && !live.empty()) {
+            rc = id_deliver(steps[live.front()]);
+            live.pop_front();
+        }
+        if (rc != KCDC_OK) {
+            fail(rc);
+            break;
+        }
+        if (!live.empty()) continue;
+        std::unique_lock<std::mutex> lk(mu);
+        if (error || (hstop && chain_tail == chain_head)) break;
+        if (undone == 0) cv_hash.wait_for(lk, std::chrono::milliseconds(5), [&] { return error || hstop || undone > 0; });
+    }
+    for (int i : live) (void)hipEventSynchronize(steps[i].ev);  // (after an error: nothing reads the buffers after this)
 }
 
 namespace {
