@@ -203,7 +203,9 @@ int64_t kcdc_bw_rounds(const kcdc_bw_batcher* b); /* rounds shipped so far (test
  * and the writers' seconds (summed over writers) blocked on their staging cap and getting a pinned
  * staging block, then the pinned blocks allocated because the pool was empty and the round
  * thread's seconds acquiring the batcher's mutex to apply a finished round, then (content IDs)
- * the chunks named, the hash steps issued and their device seconds.  Returns 21. */
+ * the chunks named, the hash steps issued and their device seconds, the round thread's seconds
+ * waiting for ID ring space, the hash thread's seconds with no step to issue, and the chains
+ * advanced summed over steps.  Returns 24. */
 int kcdc_bw_stats(kcdc_bw_batcher* b, double* out, int n);
 
 /* ------------------------------------------------------ batch (hot path)

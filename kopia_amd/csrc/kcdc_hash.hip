@@ -436,8 +436,20 @@ __global__ __launch_bounds__(256) void blake2_chunks_x4_kernel(const uint8_t* da
 // at most max_blocks blocks, from its state in device memory (HashChain), one quad of lanes per
 // chain as in blake2_chunks_x4_kernel.  A chain's first slice also runs the key block; its last
 // writes the digest to slot `out`.  Chunks stay where the writer copied them until their chain ends.
+// A step is one launch and no copies: the active list may be host-mapped pinned memory, an entry
+// with kChainNew set takes its record (src, len, out) from `fresh` (host-mapped: the host wrote it)
+// and stores it into `chains` for the later slices, and `out` may be host-mapped too.  (One small
+// hipMemcpyAsync each way per step queued behind the writers' PCIe gathers on the copy engines.)
+// The message words' LDS addresses are the same for every block (lane and round only): computed
+// once, 48 VGPRs (recomputing them was 144 of the block's 928 instructions).
+// Workgroups of 4 waves, one per SIMD: a wave issues ~800 instructions per block for its 16 chains
+// and runs alone at ~7 cycles per instruction; three waves per SIMD (12-wave workgroups) measured
+// 8.2 ms per 2,048-block step against 5.1 (profiles/r05/writer_ids/), so the SIMD's issue, not the
+// chain's latency, is what a second wave would share.
+constexpr int kChainWaves = 4;
 template <bool B64>
-__global__ __launch_bounds__(256) void blake2_chain_step_kernel(HashChain* chains, const uint32_t* active, uint32_t n,
+__global__ __launch_bounds__(kChainWaves * 64) void blake2_chain_step_kernel(HashChain* chains, const HashChain* fresh,
+                                                                const uint32_t* active, uint32_t n,
                                                                 uint64_t max_blocks, HashKey key, uint32_t nn,
                                                                 uint32_t out_len, uint32_t out_stride, uint8_t* out) {
     using W = typename std::conditional<B64, uint64_t, uint32_t>::type;
@@ -445,15 +457,25 @@ __global__ __launch_bounds__(256) void blake2_chain_step_kernel(HashChain* chain
     constexpr uint32_t BB = B64 ? 128 : 64;
     constexpr int NW = BB / 4;
     constexpr int PER = NW / 4;
-    __shared__ __attribute__((aligned(16))) uint32_t msg[4][16][NW];
+    __shared__ __attribute__((aligned(16))) uint32_t msg[kChainWaves][16][NW];
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, q = lane & 3u;
     uint32_t* M = msg[wv][lane >> 2];
     const uint32_t gi = (blockIdx.x * blockDim.x + threadIdx.x) >> 2;
     const bool live = gi < n;
-    HashChain* ch = chains + (live ? active[gi] : 0u);
-    const uint64_t len = live ? ch->len : 0u;
-    const uint8_t* p = reinterpret_cast<const uint8_t*>(live ? ch->src : 0u);
-    const uint64_t next0 = live ? ch->next : 0u;
+    const uint32_t ent = live ? active[gi] : 0u;
+    const bool is_new = (ent & kChainNew) != 0u;
+    const uint32_t slot = ent & ~kChainNew;
+    HashChain* ch = chains + slot;
+    const HashChain* rec = is_new ? fresh + slot : ch;
+    const uint64_t len = live ? rec->len : 0u;
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(live ? rec->src : 0u);
+    const uint64_t next0 = !live ? 0u : is_new ? ~0ull : ch->next;
+    const uint32_t oslot = live ? rec->out : 0u;
+    if (live && is_new && q == 0) {  // the record, for the chain's later slices
+        ch->src = reinterpret_cast<uint64_t>(p);
+        ch->len = len;
+        ch->out = oslot;
+    }
     uint32_t sidx[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
@@ -471,12 +493,24 @@ __global__ __launch_bounds__(256) void blake2_chain_step_kernel(HashChain* chain
         else return i == 0 ? kIV32[0] : i == 1 ? kIV32[1] : i == 2 ? kIV32[2] : i == 3 ? kIV32[3]
                    : i == 4 ? kIV32[4] : i == 5 ? kIV32[5] : i == 6 ? kIV32[6] : kIV32[7];
     };
-    auto mword = [&](uint32_t k) -> W {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    typedef __attribute__((address_space(3))) const u32x2 lds_u2;
+    typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+    const uint32_t mbase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint32_t*)(M)));
+    uint32_t maddr[R][4];  // byte addresses of the 4 words this lane reads in round r
+#pragma unroll
+    for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            maddr[r][j] = mbase + (B64 ? 8u : 4u) * ((sidx[r] >> (4 * j)) & 15u);
+            asm volatile("" : "+v"(maddr[r][j]));  // opaque: kept in a register, not recomputed per block
+        }
+    auto mword = [&](uint32_t addr) -> W {
         if constexpr (B64) {
-            const uint2 v = *reinterpret_cast<const uint2*>(M + 2 * k);
+            const u32x2 v = *reinterpret_cast<lds_u2*>(addr);
             return static_cast<uint64_t>(v.x) | (static_cast<uint64_t>(v.y) << 32);
         } else {
-            return M[k];
+            return *reinterpret_cast<lds_u32*>(addr);
         }
     };
     auto g = [](W& a, W& b, W& cc, W& d, W x, W y) {
@@ -492,17 +526,16 @@ __global__ __launch_bounds__(256) void blake2_chain_step_kernel(HashChain* chain
             if (q == 1) d ^= static_cast<W>(t >> 32);
         }
         if (q == 2 && last) d = ~d;
-        W mx = mword(sidx[0] & 15u), my = mword((sidx[0] >> 4) & 15u);
-        W dx = mword((sidx[0] >> 8) & 15u), dy = mword(sidx[0] >> 12);
+        W mx = mword(maddr[0][0]), my = mword(maddr[0][1]);
+        W dx = mword(maddr[0][2]), dy = mword(maddr[0][3]);
 #pragma unroll
         for (int r = 0; r < R; r++) {
             W nmx = mx, nmy = my, ndx = dx, ndy = dy;
             if (r + 1 < R) {
-                const uint32_t sn = sidx[r + 1];
-                nmx = mword(sn & 15u);
-                nmy = mword((sn >> 4) & 15u);
-                ndx = mword((sn >> 8) & 15u);
-                ndy = mword(sn >> 12);
+                nmx = mword(maddr[r + 1][0]);
+                nmy = mword(maddr[r + 1][1]);
+                ndx = mword(maddr[r + 1][2]);
+                ndy = mword(maddr[r + 1][3]);
             }
             g(a, b, cc, d, mx, my);
             b = qperm<kQRot1>(b);
@@ -571,7 +604,7 @@ __global__ __launch_bounds__(256) void blake2_chain_step_kernel(HashChain* chain
         return;
     }
     if (q == 0) ch->next = nblk;
-    uint32_t* o = reinterpret_cast<uint32_t*>(out + static_cast<uint64_t>(ch->out) * out_stride);
+    uint32_t* o = reinterpret_cast<uint32_t*>(out + static_cast<uint64_t>(oslot) * out_stride);
     constexpr uint32_t WB = sizeof(W);
     if (WB * q < out_len) {
         o[(WB / 4) * q] = static_cast<uint32_t>(h0);
@@ -1325,8 +1358,8 @@ int hash_chain_kind(const char* name, uint32_t* out_len) {
 }
 
 int launch_hash_chains(const char* name, const uint8_t* key, uint32_t key_len, HashChain* d_chains,
-                       const uint32_t* d_active, uint32_t nactive, uint64_t max_blocks, uint8_t* d_digests,
-                       uint32_t digest_stride, void* stream) {
+                       const HashChain* fresh, const uint32_t* d_active, uint32_t nactive, uint64_t max_blocks,
+                       uint8_t* d_digests, uint32_t digest_stride, void* stream) {
     const HashAlgo* h = find_hash(name);
     if (!h || (h->kind != HashKind::Blake2b && h->kind != HashKind::Blake2s))
         return set_error(-22, "resumable chains: BLAKE2 names only");
@@ -1337,12 +1370,13 @@ int launch_hash_chains(const char* name, const uint8_t* key, uint32_t key_len, H
     k.kk = key_len;
     for (uint32_t i = 0; i < key_len; i++) k.w[i / 4] |= static_cast<uint32_t>(key[i]) << (8 * (i % 4));
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const dim3 block(256), grid((4ull * nactive + 255) / 256);
+    constexpr unsigned kT = hashdev::kChainWaves * 64;
+    const dim3 block(kT), grid(static_cast<unsigned>((4ull * nactive + kT - 1) / kT));
     if (h->kind == HashKind::Blake2b)
-        hipLaunchKernelGGL(hashdev::blake2_chain_step_kernel<true>, grid, block, 0, st, d_chains, d_active, nactive,
+        hipLaunchKernelGGL(hashdev::blake2_chain_step_kernel<true>, grid, block, 0, st, d_chains, fresh, d_active, nactive,
                            max_blocks, k, h->nn, h->out, digest_stride, d_digests);
     else
-        hipLaunchKernelGGL(hashdev::blake2_chain_step_kernel<false>, grid, block, 0, st, d_chains, d_active, nactive,
+        hipLaunchKernelGGL(hashdev::blake2_chain_step_kernel<false>, grid, block, 0, st, d_chains, fresh, d_active, nactive,
                            max_blocks, k, h->nn, h->out, digest_stride, d_digests);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : set_error(-5, std::string("hash chain launch: ") + hipGetErrorString(e));

@@ -115,9 +115,12 @@ static_assert(sizeof(HashChain) == 128, "HashChain is 128 bytes");
 // 1 BLAKE2b, 2 BLAKE2s (resumable), 3 another registered name (whole chunks), < 0 unknown; *out_len = digest bytes.
 int hash_chain_kind(const char* name, uint32_t* out_len);
 // Advance chains d_chains[d_active[0..n)] by at most max_blocks message blocks each; a chain that ends
-// writes its digest to d_digests + out * digest_stride.
+// writes its digest to d_digests + out * digest_stride.  An entry with kChainNew set starts its chain
+// from the record fresh[slot] (src, len, out; may be host-mapped pinned memory, as may d_active and
+// d_digests).
+constexpr uint32_t kChainNew = 0x80000000u;
 int launch_hash_chains(const char* name, const uint8_t* key, uint32_t key_len, HashChain* d_chains,
-                       const uint32_t* d_active, uint32_t nactive, uint64_t max_blocks, uint8_t* d_digests,
-                       uint32_t digest_stride, void* stream);
+                       const HashChain* fresh, const uint32_t* d_active, uint32_t nactive, uint64_t max_blocks,
+                       uint8_t* d_digests, uint32_t digest_stride, void* stream);
 
 }  // namespace kcdc

@@ -220,6 +220,7 @@ struct BwDev {
         uint64_t ring_end;     // the ring's monotonic offset after this chain (its bytes and any wrap skip)
         uint64_t len, nblk, done;  // chunk bytes; message blocks; blocks done after the steps issued
         bool fin = false;      // its digest has been delivered
+        uint64_t pub = 0;      // its publish (a step takes it once that publish's ring copies are done)
     };
     struct NewChunk {
         kcdc_bw* w;
@@ -247,10 +248,28 @@ struct BwDev {
     uint8_t* d_dig = nullptr;
     uint32_t* d_act = nullptr;
     uint64_t* d_ol = nullptr;
-    hipEvent_t copy_ev = nullptr;      // the ring copies of the chains published so far
+    // Ring copies run on their own stream (idcopy): behind the compactions of the last collected
+    // round (compacted_ev, recorded on the copy stream before that round's gather), not behind the
+    // gather itself, so hash steps never wait for PCIe.  Compactions in turn wait for the ring
+    // copies issued so far (copy_ev): a compaction may overwrite an arena the copies read.
+    hipStream_t idcopy = nullptr;
+    hipEvent_t copy_ev = nullptr;      // the ring copies of the chains published so far (idcopy)
+    hipEvent_t compacted_ev = nullptr; // the compactions of the last collected round (copy stream)
+    // One event per publish (a ring of kPubEv): a step takes only chains whose copies are known
+    // done, so the hash stream never waits on the copies (they wait on compactions, which sit
+    // behind a gather on the copy stream).
+    static constexpr uint64_t kPubEv = 64;
+    static constexpr uint64_t kPubPieces = 1024;  // chunks per publish (one copy launch each)
+    hipEvent_t pub_ev[kPubEv] = {};
+    Piece* h_rp = nullptr;             // pinned: publish seq's copy pieces at slot seq % kPubEv
+    Piece* d_rp = nullptr;
+    uint64_t pub_seq = 0, pub_done = 0;  // (mu) publishes issued; [0, pub_done) known complete
     uint64_t step_blocks = 0;
     uint64_t id_chains = 0, id_steps = 0;
     double t_hash = 0;                 // device seconds of the hash steps
+    double t_space = 0;                // round thread: seconds waiting for ring space / chain slots
+    double t_hidle = 0;                // hash thread: seconds with no step in flight
+    uint64_t chain_steps = 0;          // chains advanced, summed over steps (/ id_steps: chains per step)
     std::condition_variable cv_hash;   // hash thread: chains published, or stop
     std::condition_variable cv_space;  // round thread: ring space or chain slots freed
     bool hstop = false;                // (mu) the round thread has published its last chains
@@ -288,6 +307,12 @@ struct BwDev {
         }
         if (ev_ref) (void)hipEventDestroy(ev_ref);
         if (copy_ev) (void)hipEventDestroy(copy_ev);
+        if (h_rp) (void)hipHostFree(h_rp);
+        if (d_rp) (void)hipFree(d_rp);
+        for (hipEvent_t ev : pub_ev)
+            if (ev) (void)hipEventDestroy(ev);
+        if (compacted_ev) (void)hipEventDestroy(compacted_ev);
+        if (idcopy) (void)hipStreamDestroy(idcopy);
         for (Step& st : steps) {
             for (hipEvent_t e : {st.t0, st.ev})
                 if (e) (void)hipEventDestroy(e);
@@ -583,13 +608,21 @@ void BwDev::loop() {
         };
         t_seg[0] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         int rc = overflow ? set_error(KCDC_EIO, "writer arena overflow") : KCDC_OK;
-        for (const Move& mv : compact) {
-            if (rc != KCDC_OK || !mv.len) continue;
-            hipError_t e = hipMemcpyAsync(mv.dst, mv.src, mv.len, hipMemcpyDeviceToDevice, copy);
-            if (e != hipSuccess) rc = hip_err(e, "writer arena compaction");
+        if (rc == KCDC_OK && ids.on && !compact.empty()) {  // the ring copies may still read these arenas
+            hipError_t e = hipStreamWaitEvent(copy, copy_ev, 0);
+            if (e != hipSuccess) rc = hip_err(e, "writer compaction wait");
         }
+        // Compactions ride in the gather launch: their destinations (the live bytes below this
+        // round's new bytes, in the new arena) and the new bytes' are disjoint, their sources (the
+        // old arena) were last written by an earlier gather on this stream.  (One hipMemcpyAsync
+        // each was a blit kernel each.)
         std::vector<Piece> pieces;
         uint64_t tasks = 0;
+        for (const Move& mv : compact) {
+            if (!mv.len) continue;
+            pieces.push_back(Piece{mv.src, mv.dst, mv.len, tasks});
+            tasks += (mv.len + kTask - 1) / kTask;
+        }
         for (Job& j : R.jobs) {
             for (const SrcPiece& sp : j.pcs) {
                 pieces.push_back(Piece{sp.src, j.w->arena + (sp.pos - j.w->origin), sp.len, tasks});
@@ -622,6 +655,7 @@ void BwDev::loop() {
                 }
             }
             if (e == hipSuccess) e = hipEventRecord(M.gathered, copy);
+            if (e == hipSuccess && ids.on) e = hipEventRecord(compacted_ev, copy);
             if (e != hipSuccess) rc = hip_err(e, "writer gather");
         }
         lap(2);
@@ -759,6 +793,9 @@ int BwDev::ids_enable(const char* name, const uint8_t* key, uint32_t key_len) {
     chain_cap = 16384;
     Guard g(device);
     hipError_t e = hipStreamCreateWithFlags(&hstream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&idcopy, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&compacted_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(compacted_ev, copy);
     if (e == hipSuccess) e = hipMalloc(&ring, ring_cap);
     if (e == hipSuccess) e = hipMalloc(&d_chains, sizeof(HashChain) * chain_cap);
     if (e == hipSuccess) e = hipHostMalloc(&h_chains, sizeof(HashChain) * chain_cap, hipHostMallocDefault);
@@ -766,13 +803,17 @@ int BwDev::ids_enable(const char* name, const uint8_t* key, uint32_t key_len) {
     if (e == hipSuccess) e = hipMalloc(&d_act, 4ull * chain_cap);
     if (e == hipSuccess) e = hipMalloc(&d_ol, 16ull * chain_cap);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&copy_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(copy_ev, idcopy);
+    for (hipEvent_t& ev : pub_ev)
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipHostMalloc(&h_rp, sizeof(Piece) * kPubEv * kPubPieces, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc(&d_rp, sizeof(Piece) * kPubEv * kPubPieces);
     for (Step& st : steps) {
         if (e == hipSuccess) e = hipHostMalloc(&st.h_dig, 32ull * chain_cap, hipHostMallocDefault);
         if (e == hipSuccess) e = hipHostMalloc(&st.h_act, 4ull * chain_cap, hipHostMallocDefault);
         if (e == hipSuccess) e = hipHostMalloc(&st.h_ol, 16ull * chain_cap, hipHostMallocDefault);
         if (e == hipSuccess) e = hipEventCreate(&st.t0);
-        // the hash thread sleeps in hipEventSynchronize instead of spinning beside the writers
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&st.ev, hipEventBlockingSync);
+        if (e == hipSuccess) e = hipEventCreate(&st.ev);
     }
     if (e != hipSuccess) return hip_err(e, "writer content IDs: device memory");
     ids.on = true;
@@ -783,20 +824,53 @@ int BwDev::ids_enable(const char* name, const uint8_t* key, uint32_t key_len) {
 // The last completed round's final chunks (newc) become chains: ring space and a slot each, a
 // copy from the writer's arena into the ring, then (after an event on the copy stream) the chain
 // is published to the hash thread.  Called right after complete(): the arena pointers are those of
-// the compactions queued before it on the copy stream, and the copies queue behind them, before
-// any later compaction.  When the ring is full it publishes what it has copied and waits for the
+// the compactions of the last collected round, and the copies (idcopy stream) wait for those
+// (compacted_ev); any later compaction waits for the copies (copy_ev).  When the ring is full it publishes what it has copied and waits for the
 // hash thread to free space.
 int BwDev::id_create() {
     if (newc.empty()) return KCDC_OK;
     Guard g(device);
+    {
+        const hipError_t e = hipStreamWaitEvent(idcopy, compacted_ev, 0);
+        if (e != hipSuccess) return hip_err(e, "writer content IDs: compaction wait");
+    }
     std::vector<Chain> made;
+    std::vector<Piece> pcs;  // the made chains' ring copies (source and ring congruent mod 16)
+    uint64_t ptasks = 0;
     auto publish = [&]() -> int {
         if (made.empty()) return KCDC_OK;
-        hipError_t e = hipEventRecord(copy_ev, copy);  // before the chains are visible (hash thread waits on it)
+        uint64_t seq;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            seq = pub_seq;
+        }
+        // the slot of publish seq - kPubEv (event, pinned pieces) must be complete before reuse
+        hipError_t e = hipSuccess;
+        if (seq >= kPubEv) e = hipEventSynchronize(pub_ev[seq % kPubEv]);
+        if (e == hipSuccess && !pcs.empty()) {  // one copy launch for the whole publish
+            Piece* hp = h_rp + (seq % kPubEv) * kPubPieces;
+            Piece* dp = d_rp + (seq % kPubEv) * kPubPieces;
+            std::memcpy(hp, pcs.data(), pcs.size() * sizeof(Piece));
+            e = hipMemcpyAsync(dp, hp, pcs.size() * sizeof(Piece), hipMemcpyHostToDevice, idcopy);
+            if (e == hipSuccess) {
+                const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(ptasks, 2 * kGatherWGs));
+                hipLaunchKernelGGL(bw_gather_kernel, dim3(grid), dim3(256), 0, idcopy, dp,
+                                   static_cast<uint32_t>(pcs.size()), ptasks);
+                e = hipGetLastError();
+            }
+        }
+        pcs.clear();
+        ptasks = 0;
+        if (e == hipSuccess) e = hipEventRecord(pub_ev[seq % kPubEv], idcopy);
+        if (e == hipSuccess) e = hipEventRecord(copy_ev, idcopy);  // (later compactions wait on it)
         if (e != hipSuccess) return hip_err(e, "writer content IDs: copy event");
         {
             std::lock_guard<std::mutex> lk(mu);
-            for (const Chain& c : made) chains.push_back(c);
+            pub_seq = seq + 1;
+            for (Chain& c : made) {
+                c.pub = seq;
+                chains.push_back(c);
+            }
             chain_head += made.size();
             undone += made.size();
             id_chains += made.size();
@@ -807,19 +881,27 @@ int BwDev::id_create() {
     };
     for (const NewChunk& nc : newc) {
         const uint64_t need = (nc.len + 15) & ~uint64_t(15);
-        if (need > ring_cap) return set_error(KCDC_EIO, "writer content IDs: chunk larger than the ID ring");
+        if (need + 32 > ring_cap) return set_error(KCDC_EIO, "writer content IDs: chunk larger than the ID ring");
+        const uint8_t* src = nc.w->arena + (nc.pos - nc.w->origin);
+        const uint64_t cong = reinterpret_cast<uintptr_t>(src) & 15u;  // the ring (256-aligned) copy starts congruent
         uint64_t at = 0;
+        if (made.size() >= kPubPieces) {
+            const int rc = publish();
+            if (rc != KCDC_OK) return rc;
+        }
         for (;;) {
             {
                 std::unique_lock<std::mutex> lk(mu);
                 if (error) return error;
-                at = ring_head;
-                if (at % ring_cap + need > ring_cap) at += ring_cap - at % ring_cap;  // no chunk wraps
+                at = ring_head + ((cong - ring_head) & 15u);
+                if (at % ring_cap + need + 16 > ring_cap) at += ring_cap - at % ring_cap + cong;  // no chunk wraps
                 if (at + need - ring_tail <= ring_cap && chain_head + made.size() - chain_tail < chain_cap) break;
                 if (made.empty()) {
                     if (chain_tail == chain_head)
                         return set_error(KCDC_EIO, "writer content IDs: ring full with no chain in flight");
+                    const auto w0 = std::chrono::steady_clock::now();
                     cv_space.wait_for(lk, std::chrono::milliseconds(2));
+                    t_space += std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
                     continue;
                 }
             }
@@ -830,8 +912,8 @@ int BwDev::id_create() {
         const uint32_t slot = static_cast<uint32_t>(cn % chain_cap);
         uint8_t* dst = ring + at % ring_cap;
         if (nc.len) {
-            hipError_t e = hipMemcpyAsync(dst, nc.w->arena + (nc.pos - nc.w->origin), nc.len, hipMemcpyDeviceToDevice, copy);
-            if (e != hipSuccess) return hip_err(e, "writer content IDs: ring copy");
+            pcs.push_back(Piece{src, dst, nc.len, ptasks});
+            ptasks += (nc.len + kTask - 1) / kTask;
         }
         HashChain& hc = h_chains[slot];
         std::memset(&hc, 0, sizeof(hc));
@@ -857,30 +939,35 @@ int BwDev::id_issue(Step& st, bool& issued) {
     {
         std::lock_guard<std::mutex> lk(mu);
         if (undone == 0) return KCDC_OK;
+        while (pub_done < pub_seq && hipEventQuery(pub_ev[pub_done % kPubEv]) == hipSuccess) pub_done++;
         up0 = uploaded;
-        up1 = uploaded = chain_head;
+        up1 = chain_head;
         for (uint64_t k = 0; k < chains.size(); k++) {
             Chain& c = chains[k];
             if (c.fin || c.done >= c.nblk) continue;
+            if (c.pub >= pub_done) break;  // its ring copy (and every later chain's) is not done yet
             const uint64_t cn = chain_tail + k;
             if (ids.kind == 3) {  // whole chunks, in this step's order
                 st.h_ol[n] = c.ring_at % ring_cap;
                 st.h_ol[chain_cap + n] = c.len;
                 c.done = c.nblk;
                 st.done.emplace_back(cn, n);
-            } else {
-                st.h_act[n] = static_cast<uint32_t>(cn % chain_cap);
+            } else {  // (a chain's first step takes its record from h_chains)
+                st.h_act[n] = static_cast<uint32_t>(cn % chain_cap) | (c.done == 0 ? kChainNew : 0u);
                 c.done = std::min(c.nblk, c.done + step_blocks);
                 if (c.done == c.nblk) st.done.emplace_back(cn, static_cast<uint32_t>(cn % chain_cap));
             }
             if (c.done == c.nblk) undone--;
             n++;
         }
+        chain_steps += n;
+        if (n && ids.kind == 3) uploaded = up1;  // (a step that issues nothing uploads nothing either)
     }
     if (n == 0) return KCDC_OK;
-    // the ring copies of every chain published so far, then the new chains' records
-    hipError_t e = hipStreamWaitEvent(hstream, copy_ev, 0);
-    for (uint64_t c0 = up0; e == hipSuccess && c0 < up1;) {  // slots [up0, up1) mod cap
+    // kind 3: the new chains' records (their ring copies are done: see pub_done); the BLAKE2 kinds
+    // read them, the active list and their digests through host-mapped memory (one launch, no copies)
+    hipError_t e = hipSuccess;
+    for (uint64_t c0 = up0; ids.kind == 3 && e == hipSuccess && c0 < up1;) {  // slots [up0, up1) mod cap
         const uint32_t s0 = static_cast<uint32_t>(c0 % chain_cap);
         const uint64_t run = std::min<uint64_t>(up1 - c0, chain_cap - s0);
         e = hipMemcpyAsync(d_chains + s0, h_chains + s0, run * sizeof(HashChain), hipMemcpyHostToDevice, hstream);
@@ -897,11 +984,8 @@ int BwDev::id_issue(Step& st, bool& issued) {
                                      static_cast<uint32_t>(ids.key.size()), d_dig, 32, hstream);
         if (rc == KCDC_OK) e = hipMemcpyAsync(st.h_dig, d_dig, 32ull * n, hipMemcpyDeviceToHost, hstream);
     } else {
-        e = hipMemcpyAsync(d_act, st.h_act, 4ull * n, hipMemcpyHostToDevice, hstream);
-        if (e != hipSuccess) return hip_err(e, "writer content IDs: active list");
-        rc = launch_hash_chains(ids.name.c_str(), ids.key.data(), static_cast<uint32_t>(ids.key.size()), d_chains, d_act,
-                                n, step_blocks, d_dig, 32, hstream);
-        if (rc == KCDC_OK) e = hipMemcpyAsync(st.h_dig, d_dig, 32ull * chain_cap, hipMemcpyDeviceToHost, hstream);
+        rc = launch_hash_chains(ids.name.c_str(), ids.key.data(), static_cast<uint32_t>(ids.key.size()), d_chains,
+                                h_chains, st.h_act, n, step_blocks, st.h_dig, 32, hstream);
     }
     if (rc != KCDC_OK) return rc;
     if (e == hipSuccess) e = hipEventRecord(st.ev, hstream);
@@ -912,7 +996,10 @@ int BwDev::id_issue(Step& st, bool& issued) {
 
 // Wait for a step, then hand its finished digests to their writers and free the ring's head.
 int BwDev::id_deliver(Step& st) {
-    const hipError_t q = hipEventSynchronize(st.ev);
+    // polled with sleeps: a hash thread parked in hipEventSynchronize for a 5 ms step held up the
+    // round thread's HIP calls (its round waits doubled and the device idled half the time)
+    hipError_t q;
+    while ((q = hipEventQuery(st.ev)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(200));
     if (q != hipSuccess) return hip_err(q, "writer content IDs: hash step");
     float ms = 0;
     const bool timed = hipEventElapsedTime(&ms, st.t0, st.ev) == hipSuccess;
@@ -976,7 +1063,12 @@ void BwDev::hash_loop() {
         if (!live.empty()) continue;
         std::unique_lock<std::mutex> lk(mu);
         if (error || (hstop && chain_tail == chain_head)) break;
-        if (undone == 0) cv_hash.wait_for(lk, std::chrono::milliseconds(5), [&] { return error || hstop || undone > 0; });
+        const auto w0 = std::chrono::steady_clock::now();
+        if (undone == 0)
+            cv_hash.wait_for(lk, std::chrono::milliseconds(5), [&] { return error || hstop || undone > 0; });
+        else  // chains waiting for their ring copies
+            cv_hash.wait_for(lk, std::chrono::microseconds(200));
+        t_hidle += std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
     }
     for (int i : live) (void)hipEventSynchronize(steps[i].ev);  // (after an error: nothing reads the buffers after this)
 }
@@ -1424,7 +1516,7 @@ extern "C" int kcdc_bw_stats(kcdc_bw_batcher* t, double* out, int n) {
     // per device: the device span from its first round's start to its last one's end, and the
     // part of it in which a gather or a split ran (their union: overlapped rounds count once);
     // over devices: counts and host seconds add up, spans and busy times are the maximum
-    double v[21] = {0};
+    double v[24] = {0};
     for (BwDev* b : t->devs) {
         std::lock_guard<std::mutex> lk(b->mu);
         std::vector<std::pair<float, float>> iv = b->busy;
@@ -1445,14 +1537,15 @@ extern "C" int kcdc_bw_stats(kcdc_bw_batcher* t, double* out, int n) {
             busy += e0 - s0;
             span = hi - iv[0].first;
         }
-        const double d[21] = {static_cast<double>(b->rounds), static_cast<double>(b->shipped_bytes), b->t_submit,
+        const double d[24] = {static_cast<double>(b->rounds), static_cast<double>(b->shipped_bytes), b->t_submit,
                               b->t_wait, b->t_gather, b->t_kernel, span * 1e-3, busy * 1e-3,
                               b->t_seg[0], b->t_seg[1], b->t_seg[2], b->t_seg[3], b->t_seg[4],
                               b->t_idle, b->w_capped_ns.load() * 1e-9, b->w_block_ns.load() * 1e-9,
                               static_cast<double>(b->pool_misses.load()), b->t_lock,
-                              static_cast<double>(b->id_chains), static_cast<double>(b->id_steps), b->t_hash};
-        for (int i = 0; i < 21; i++) v[i] = (i == 6 || i == 7) ? std::max(v[i], d[i]) : v[i] + d[i];
+                              static_cast<double>(b->id_chains), static_cast<double>(b->id_steps), b->t_hash,
+                              b->t_space, b->t_hidle, static_cast<double>(b->chain_steps)};
+        for (int i = 0; i < 24; i++) v[i] = (i == 6 || i == 7) ? std::max(v[i], d[i]) : v[i] + d[i];
     }
-    for (int i = 0; i < n && i < 21; i++) out[i] = v[i];
-    return 21;
+    for (int i = 0; i < n && i < 24; i++) out[i] = v[i];
+    return 24;
 }

@@ -76,7 +76,7 @@ int main(int argc, char** argv) {
         }
     }
     std::vector<double> rates;
-    double st0[21] = {0};  // the stats after the warm-up rep: the steady-state pool misses are the rest
+    double st0[24] = {0};  // the stats after the warm-up rep: the steady-state pool misses are the rest
     bool ok = true;
     for (int r = 0; r < reps + 1; r++) {  // rep 0 warms the pinned pool and device buffers
         std::vector<std::vector<uint64_t>> got(W);
@@ -121,13 +121,13 @@ int main(int argc, char** argv) {
         for (auto& t : th) t.join();
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         if (r > 0) rates.push_back(static_cast<double>(W) * L / s / (1ull << 30));
-        if (r == 0) kcdc_bw_stats(b, st0, 21);
+        if (r == 0) kcdc_bw_stats(b, st0, 24);
         for (int i = 0; i < W; i++)
             ok = ok && got[i] == std::vector<uint64_t>(ref.begin() + base[i], ref.begin() + base[i] + counts[i]);
     }
     const int64_t rounds = kcdc_bw_rounds(b);
-    double st[21] = {0};
-    kcdc_bw_stats(b, st, 21);
+    double st[24] = {0};
+    kcdc_bw_stats(b, st, 24);
     kcdc_bw_batcher_free(b);
     // the host-side ceiling: the same W threads only copying their slices into 4 MiB buffers
     double copy_rate = 0;
@@ -162,9 +162,9 @@ int main(int argc, char** argv) {
                 "\"round_wait_s\": %.3f, \"dev_gather_s\": %.3f, \"dev_split_s\": %.3f, \"dev_span_s\": %.3f, "
                 "\"dev_busy_s\": %.3f, \"host_s\": [%.3f, %.3f, %.3f, %.3f, %.3f], "
                 "\"round_idle_s\": %.3f, \"writer_capped_s\": %.3f, \"writer_block_s\": %.3f, \"pool_misses\": %.0f, \"pool_misses_after_warmup\": %.0f, \"writer_block_s_after_warmup\": %.3f, \"round_lock_s\": %.3f, "
-                "\"memcpy_only_gib_s\": %.2f, \"hash\": \"%s\", \"ids_named\": %.0f, \"hash_steps\": %.0f, \"hash_dev_s\": %.3f, \"parity_ok\": %s}\n",
+                "\"memcpy_only_gib_s\": %.2f, \"hash\": \"%s\", \"ids_named\": %.0f, \"hash_steps\": %.0f, \"hash_dev_s\": %.3f, \"id_space_wait_s\": %.3f, \"hash_idle_s\": %.3f, \"chains_per_step\": %.0f, \"parity_ok\": %s}\n",
                 W, L >> 20, S >> 10, name.c_str(), static_cast<unsigned long long>(round >> 20),
                 rates.empty() ? 0.0 : sum / rates.size(), best, static_cast<long long>(rounds), st[2], st[3], st[4], st[5], st[6], st[7], st[8], st[9], st[10], st[11], st[12], st[13], st[14], st[15], st[16], st[16] - st0[16], st[15] - st0[15], st[17], copy_rate,
-                hash.c_str(), st[18], st[19], st[20], ok ? "true" : "false");
+                hash.c_str(), st[18], st[19], st[20], st[21], st[22], st[19] > 0 ? st[23] / st[19] : 0.0, ok ? "true" : "false");
     return ok ? 0 : 2;
 }
