@@ -186,7 +186,7 @@ void kcdc_bw_free(kcdc_bw* w);
  * every chunk up to it are known; kcdc_bw_finish also waits for the last chunk's digest.  BLAKE2
  * names hash in slices of 256 KiB per chunk per step (a chunk is one chain of compressions), the
  * others whole chunks per step, on a hash thread of their own.  Device memory: an ID ring of
- * max(32 x round_bytes, 1 GiB) per device holds the chunks until they are named (a chunk is one
+ * max(64 x round_bytes, 1 GiB) per device holds the chunks until they are named (a chunk is one
  * dependent chain, so the naming rate grows with the chunks in flight).  FIXED names: KCDC_EINVAL
  * (their writers stage no bytes on the device). */
 int kcdc_bw_batcher_hash(kcdc_bw_batcher* b, const char* hash_name, const uint8_t* key, uint32_t key_len);

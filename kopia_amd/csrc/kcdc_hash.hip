@@ -98,6 +98,39 @@ __device__ __forceinline__ void load_block(const uint8_t* p, uint32_t take, uint
     }
 }
 
+// Prefetch for 16-byte aligned chunks (the resumable chains): a lane's quarter of a block is
+// issued as dwordx4 loads and only masked when its block is used, so the loads stay in flight
+// while earlier blocks compress.  (load_block consumes its loads at once: the "next block"
+// prefetch of round 5's first chain kernel waited a memory round trip every block, ~2.5 us.)
+// Loads are unconditional (a conditional load leaves the waitcnt pass unsure at the join, and it
+// waits for everything there): a vector with no bytes of the chunk reads the chunk's first 16
+// bytes instead (`safe`), which the mask discards.
+template <int NW>
+__device__ __forceinline__ void load_aligned(const uint8_t* p, uint32_t take, const uint8_t* safe, uint32_t (&x)[NW]) {
+    static_assert(NW % 4 == 0, "whole dwordx4 vectors");
+    typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+    typedef const __attribute__((address_space(1))) u32x4v gu32x4;
+#pragma unroll
+    for (int v = 0; v < NW / 4; v++) {
+        const uint8_t* a = take > 16u * v ? p + 16 * v : safe;
+        const u32x4v r = *reinterpret_cast<gu32x4*>(reinterpret_cast<uintptr_t>(a));
+        x[4 * v] = r.x;
+        x[4 * v + 1] = r.y;
+        x[4 * v + 2] = r.z;
+        x[4 * v + 3] = r.w;
+    }
+}
+template <int NW>
+__device__ __forceinline__ void mask_take(uint32_t take, uint32_t (&d)[NW]) {
+    if (take < 4u * NW) {
+#pragma unroll
+        for (int i = 0; i < NW; i++) {
+            const int32_t keep = static_cast<int32_t>(take) - 4 * i;
+            d[i] &= keep >= 4 ? 0xFFFFFFFFu : keep <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * keep));
+        }
+    }
+}
+
 // ------------------------------------------------------------------ BLAKE2b
 __device__ __forceinline__ void g64(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, uint64_t x, uint64_t y) {
     a = a + b + x;
@@ -578,23 +611,48 @@ __global__ __launch_bounds__(kChainWaves * 64) void blake2_chain_step_kernel(Has
         const uint64_t rem = len - BB * blk;
         return rem < BB ? static_cast<uint32_t>(rem) : BB;
     };
-    auto load_quarter = [&](uint64_t blk, uint32_t (&w)[PER]) {
-        const int32_t part = static_cast<int32_t>(take_of(blk)) - static_cast<int32_t>(4 * PER * q);
-        load_block<PER>(p + BB * blk + 4 * PER * q, part <= 0 ? 0u : static_cast<uint32_t>(part), w);
-    };
     uint64_t t = (key.kk ? BB : 0) + (next * BB < len ? next * BB : len);
-    uint32_t w[PER], wn[PER];
-    if (next < end) load_quarter(next, w);
-    for (uint64_t blk = next; blk < end; blk++) {
-        if (blk + 1 < end) load_quarter(blk + 1, wn);
+    // Blocks blk+1 and blk+2 are in flight (unmasked) while block blk is compressed: beside the
+    // writers' gathers and splits a load takes about as long as one compression.  The chunk
+    // starts 16-byte aligned (launch_hash_chains' contract; the writers' ring copies realign).
+    constexpr int kAhead = 3;
+    auto part_of = [&](uint64_t blk) -> uint32_t {
+        const int32_t part = static_cast<int32_t>(take_of(blk)) - static_cast<int32_t>(4 * PER * q);
+        return part <= 0 ? 0u : static_cast<uint32_t>(part);
+    };
+    uint32_t w[kAhead][PER];
+    // block indices past the slice's end load the slice's last block again (never used)
+    auto pre = [&](uint64_t b, uint32_t (&r)[PER]) {
+        const uint64_t bb = b < end ? b : end - 1;
+        load_aligned<PER>(p + BB * bb + 4 * PER * q, part_of(bb), p, r);
+    };
+    static_assert(kAhead == 3, "the block loop below is unrolled over three buffers");
+    // one block: prefetch blk + 2 into `fill`, compress blk from `use` (the buffers rotate by
+    // unrolling, not by copies: a register copy of an in-flight load waits for it)
+    auto step = [&](uint32_t (&use)[PER], uint32_t (&fill)[PER], uint64_t blk) {
+        pre(blk + kAhead - 1, fill);
+        uint32_t cur[PER];
 #pragma unroll
-        for (int j = 0; j < PER; j++) M[PER * q + j] = w[j];
+        for (int j = 0; j < PER; j++) cur[j] = use[j];
+        mask_take<PER>(part_of(blk), cur);
+#pragma unroll
+        for (int j = 0; j < PER; j++) M[PER * q + j] = cur[j];
         wave_lds_fence();
         t += take_of(blk);
         compress(t, blk + 1 == nblk);
         wave_lds_fence();
-#pragma unroll
-        for (int j = 0; j < PER; j++) w[j] = wn[j];
+    };
+    if (next < end) {
+        pre(next, w[0]);
+        pre(next + 1, w[1]);
+    }
+    for (uint64_t blk = next; blk < end;) {
+        step(w[0], w[2], blk);
+        if (++blk >= end) break;
+        step(w[1], w[0], blk);
+        if (++blk >= end) break;
+        step(w[2], w[1], blk);
+        ++blk;
     }
     if (!live) return;
     if (end < nblk) {  // the chain goes on in a later slice

@@ -117,7 +117,8 @@ int hash_chain_kind(const char* name, uint32_t* out_len);
 // Advance chains d_chains[d_active[0..n)] by at most max_blocks message blocks each; a chain that ends
 // writes its digest to d_digests + out * digest_stride.  An entry with kChainNew set starts its chain
 // from the record fresh[slot] (src, len, out; may be host-mapped pinned memory, as may d_active and
-// d_digests).
+// d_digests).  Every chunk must start 16-byte aligned and be readable up to its length rounded up
+// to 16.
 constexpr uint32_t kChainNew = 0x80000000u;
 int launch_hash_chains(const char* name, const uint8_t* key, uint32_t key_len, HashChain* d_chains,
                        const HashChain* fresh, const uint32_t* d_active, uint32_t nactive, uint64_t max_blocks,

@@ -113,6 +113,44 @@ __global__ __launch_bounds__(256) void bw_gather_kernel(const Piece* pieces, uin
     }
 }
 
+// The content IDs' ring copies: chunk bytes from any source address to a 16-byte aligned ring
+// slot (the chain kernel loads whole aligned vectors).  Per thread 16 destination bytes from five
+// aligned source words (never past the source's last word: the next word may not be mapped);
+// the last vector of a chunk may write up to 15 bytes past its end, inside the slot (the ring
+// reserves each chunk's length rounded up to 16).
+__global__ __launch_bounds__(256) void bw_realign_kernel(const Piece* pieces, uint32_t npieces, uint64_t ntasks) {
+    for (uint64_t task = blockIdx.x; task < ntasks; task += gridDim.x) {
+        uint32_t lo = 0, hi = npieces;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pieces[mid].task0 <= task) lo = mid;
+            else hi = mid;
+        }
+        const Piece pc = pieces[lo];
+        const uint64_t off = (task - pc.task0) * kTask;
+        if (off >= pc.len) continue;
+        const uint64_t len = pc.len - off < kTask ? pc.len - off : kTask;
+        const uintptr_t sa = reinterpret_cast<uintptr_t>(pc.src) + off;
+        const uint32_t mis = static_cast<uint32_t>(sa & 3u);
+        const __attribute__((address_space(1))) uint32_t* sw =
+            reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(sa - mis);
+        gv4u* dv = reinterpret_cast<gv4u*>(reinterpret_cast<uintptr_t>(pc.dst) + off);
+        const uint64_t lw = (len + mis - 1) >> 2;  // the last source word holding a chunk byte
+        const uint64_t nv = (len + 15) >> 4;
+        for (uint64_t i = threadIdx.x; i < nv; i += 256) {
+            uint32_t x[5];
+#pragma unroll
+            for (int k = 0; k < 5; k++) x[k] = sw[4 * i + k < lw ? 4 * i + k : lw];
+            v4u o;
+            o.x = mis ? __builtin_amdgcn_alignbit(x[1], x[0], 8 * mis) : x[0];
+            o.y = mis ? __builtin_amdgcn_alignbit(x[2], x[1], 8 * mis) : x[1];
+            o.z = mis ? __builtin_amdgcn_alignbit(x[3], x[2], 8 * mis) : x[2];
+            o.w = mis ? __builtin_amdgcn_alignbit(x[4], x[3], 8 * mis) : x[3];
+            dv[i] = o;
+        }
+    }
+}
+
 struct Blk {  // a pinned block: bytes [start, end) are stream bytes [pos, pos + end - start)
     uint8_t* p = nullptr;
     uint32_t start = 0, end = 0;
@@ -612,17 +650,17 @@ void BwDev::loop() {
             hipError_t e = hipStreamWaitEvent(copy, copy_ev, 0);
             if (e != hipSuccess) rc = hip_err(e, "writer compaction wait");
         }
-        // Compactions ride in the gather launch: their destinations (the live bytes below this
-        // round's new bytes, in the new arena) and the new bytes' are disjoint, their sources (the
-        // old arena) were last written by an earlier gather on this stream.  (One hipMemcpyAsync
-        // each was a blit kernel each.)
+        // Compactions: one copy launch for all of them (one hipMemcpyAsync each was a blit kernel
+        // each), before the gather; their pieces lead the round's piece list.  The ring copies of
+        // the content IDs wait for them (compacted_ev), not for the gather.
         std::vector<Piece> pieces;
-        uint64_t tasks = 0;
+        uint64_t tasks = 0, ctasks = 0;
         for (const Move& mv : compact) {
             if (!mv.len) continue;
-            pieces.push_back(Piece{mv.src, mv.dst, mv.len, tasks});
-            tasks += (mv.len + kTask - 1) / kTask;
+            pieces.push_back(Piece{mv.src, mv.dst, mv.len, ctasks});
+            ctasks += (mv.len + kTask - 1) / kTask;
         }
+        const size_t ncp = pieces.size();
         for (Job& j : R.jobs) {
             for (const SrcPiece& sp : j.pcs) {
                 pieces.push_back(Piece{sp.src, j.w->arena + (sp.pos - j.w->origin), sp.len, tasks});
@@ -647,15 +685,21 @@ void BwDev::loop() {
             if (e == hipSuccess && !pieces.empty()) {
                 std::memcpy(M.hp, pieces.data(), pieces.size() * sizeof(Piece));
                 e = hipMemcpyAsync(M.dp, M.hp, pieces.size() * sizeof(Piece), hipMemcpyHostToDevice, copy);
-                if (e == hipSuccess) {
-                    const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(tasks, kGatherWGs));
-                    hipLaunchKernelGGL(bw_gather_kernel, dim3(grid), dim3(256), 0, copy, M.dp,
-                                       static_cast<uint32_t>(pieces.size()), tasks);
+                if (e == hipSuccess && ncp) {
+                    const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(ctasks, 2 * kGatherWGs));
+                    hipLaunchKernelGGL(bw_gather_kernel, dim3(grid), dim3(256), 0, copy, M.dp, static_cast<uint32_t>(ncp),
+                                       ctasks);
                     e = hipGetLastError();
                 }
             }
-            if (e == hipSuccess) e = hipEventRecord(M.gathered, copy);
             if (e == hipSuccess && ids.on) e = hipEventRecord(compacted_ev, copy);
+            if (e == hipSuccess && pieces.size() > ncp) {
+                const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(tasks, kGatherWGs));
+                hipLaunchKernelGGL(bw_gather_kernel, dim3(grid), dim3(256), 0, copy, M.dp + ncp,
+                                   static_cast<uint32_t>(pieces.size() - ncp), tasks);
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess) e = hipEventRecord(M.gathered, copy);
             if (e != hipSuccess) rc = hip_err(e, "writer gather");
         }
         lap(2);
@@ -787,9 +831,9 @@ int BwDev::ids_enable(const char* name, const uint8_t* key, uint32_t key_len) {
     ids.kind = kind;
     // slices of 256 KiB per chain per step: a 4 MiB chunk is named after ~16 steps
     step_blocks = kind == 1 ? 2048 : 4096;
-    // chains in flight set the naming rate (one chain: ~55 MB/s of BLAKE2b), so the ring holds 32
-    // rounds: ~2,000 chunks of 4 MiB at the default 256 MiB rounds
-    ring_cap = std::max<uint64_t>(32 * round_bytes, 1ull << 30);
+    // chains in flight set the naming rate (one chain: ~50 MB/s of BLAKE2b), so the ring holds 64
+    // rounds: 16 GiB, ~3,000 chunks of 4-5 MiB at the default 256 MiB rounds (of 288 GB of HBM)
+    ring_cap = std::max<uint64_t>(64 * round_bytes, 1ull << 30);
     chain_cap = 16384;
     Guard g(device);
     hipError_t e = hipStreamCreateWithFlags(&hstream, hipStreamNonBlocking);
@@ -835,7 +879,7 @@ int BwDev::id_create() {
         if (e != hipSuccess) return hip_err(e, "writer content IDs: compaction wait");
     }
     std::vector<Chain> made;
-    std::vector<Piece> pcs;  // the made chains' ring copies (source and ring congruent mod 16)
+    std::vector<Piece> pcs;  // the made chains' ring copies (to 16-byte aligned ring slots)
     uint64_t ptasks = 0;
     auto publish = [&]() -> int {
         if (made.empty()) return KCDC_OK;
@@ -854,7 +898,7 @@ int BwDev::id_create() {
             e = hipMemcpyAsync(dp, hp, pcs.size() * sizeof(Piece), hipMemcpyHostToDevice, idcopy);
             if (e == hipSuccess) {
                 const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(ptasks, 2 * kGatherWGs));
-                hipLaunchKernelGGL(bw_gather_kernel, dim3(grid), dim3(256), 0, idcopy, dp,
+                hipLaunchKernelGGL(bw_realign_kernel, dim3(grid), dim3(256), 0, idcopy, dp,
                                    static_cast<uint32_t>(pcs.size()), ptasks);
                 e = hipGetLastError();
             }
@@ -881,9 +925,8 @@ int BwDev::id_create() {
     };
     for (const NewChunk& nc : newc) {
         const uint64_t need = (nc.len + 15) & ~uint64_t(15);
-        if (need + 32 > ring_cap) return set_error(KCDC_EIO, "writer content IDs: chunk larger than the ID ring");
+        if (need > ring_cap) return set_error(KCDC_EIO, "writer content IDs: chunk larger than the ID ring");
         const uint8_t* src = nc.w->arena + (nc.pos - nc.w->origin);
-        const uint64_t cong = reinterpret_cast<uintptr_t>(src) & 15u;  // the ring (256-aligned) copy starts congruent
         uint64_t at = 0;
         if (made.size() >= kPubPieces) {
             const int rc = publish();
@@ -893,8 +936,8 @@ int BwDev::id_create() {
             {
                 std::unique_lock<std::mutex> lk(mu);
                 if (error) return error;
-                at = ring_head + ((cong - ring_head) & 15u);
-                if (at % ring_cap + need + 16 > ring_cap) at += ring_cap - at % ring_cap + cong;  // no chunk wraps
+                at = ring_head;  // (a multiple of 16)
+                if (at % ring_cap + need > ring_cap) at += ring_cap - at % ring_cap;  // no chunk wraps
                 if (at + need - ring_tail <= ring_cap && chain_head + made.size() - chain_tail < chain_cap) break;
                 if (made.empty()) {
                     if (chain_tail == chain_head)
