@@ -49,7 +49,10 @@ constexpr int kWave = 64;
 constexpr int kBlk = 128;               // bytes per lane per step (one cache line)
 constexpr int kNdw = kBlk / 4;          // dwords per lane per step
 constexpr int64_t kLaneMax = 2048;      // max bytes per lane segment (tile = 64 x kLaneMax)
-constexpr uint64_t kTileDiv = 256;      // batch lane segments <= avg / kTileDiv (tiles ~ avg / 4), >= 256 B
+#ifndef KCDC_TILE_DIV
+#define KCDC_TILE_DIV 256
+#endif
+constexpr uint64_t kTileDiv = KCDC_TILE_DIV;  // batch lane segments <= avg / kTileDiv (tiles ~ avg / 4), >= 256 B
 constexpr int kSchedWindow = 16;        // bytes per scheduling window in the warm-up / exact loops
 constexpr int kLookahead = 16;          // 128-byte steps: table reads issued this many bytes ahead (VGPR bound)
 
@@ -1623,7 +1626,11 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             if (claim_next && n == 1) help_claim_dma(a, lane, me, wl32);
             if (n + 1 < g.nb) {
                 dma_step128(g.ld, g.ld.tb, sl32, ct, g.L, n + 1, lane);
-            } else if (!switching && !last_of_region && claim_known && (!claim_next || claim_ok)) {
+            } else if (!switching && !last_of_region && claim_known && (!claim_next || claim_ok) &&
+                       __ballot(found >= 0) == 0) {
+                // (a candidate in an earlier step means the region's cut is in this tile: the
+                // next tile would be a stale prefetch, 12 KiB of HBM traffic per chunk wasted --
+                // 9 % of R at 128K, where chunks span ~4 tiles)
                 PStream t2 = cur;  // next tile of this region (ours)
                 t2.ct = ct_next;
                 ptile_issue(t2, hi, wl32, sl32, lane, lcap);

@@ -21,7 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from oracle import coracle  # noqa: E402  (test/measurement infrastructure only)
 
-WAVE, LANE_MAX, TILE_DIV, SEED = 64, 2048, 256, 0x6B6F706961
+WAVE, LANE_MAX, SEED = 64, 2048, 0x6B6F706961
+TILE_DIV = int(os.environ.get("KCDC_TILE_DIV", "256"))  # kcdc_kernels.hip kTileDiv
 
 
 def lane_cap(avg):
