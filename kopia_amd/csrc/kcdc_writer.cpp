@@ -21,6 +21,7 @@
 // growing), unless the writer is finishing.  So the cuts equal one NextSplitPoint pass over the
 // whole object, however the bytes were sliced (tests/test_gpu_writer.py).
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -156,6 +157,37 @@ struct Blk {  // a pinned block: bytes [start, end) are stream bytes [pos, pos +
     uint32_t start = 0, end = 0;
     uint64_t pos = 0;
 };
+
+// Staging copy of a writer's slice into its pinned block.  Non-temporal stores write the block
+// without first reading its lines (a plain memcpy's stores read each destination line for
+// ownership: three memory passes instead of two), and the block is read next by the GPU, not the
+// CPU.  With more writer threads than cores the copies are what the host's memory bandwidth goes
+// to.  The stores are weakly ordered: the sfence makes them visible before the writer publishes
+// the bytes (under its mutex) to the round thread, whose gather reads them over PCIe.
+__attribute__((target("avx2"))) void copy_nt_avx2(uint8_t* d, const uint8_t* s, size_t n) {
+    const size_t h = std::min<size_t>(n, (32 - (reinterpret_cast<uintptr_t>(d) & 31)) & 31);
+    std::memcpy(d, s, h);
+    d += h;
+    s += h;
+    n -= h;
+    for (; n >= 128; n -= 128, d += 128, s += 128) {
+        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s));
+        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + 32));
+        const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + 64));
+        const __m256i e = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + 96));
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(d), a);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(d + 32), b);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(d + 64), c);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(d + 96), e);
+    }
+    std::memcpy(d, s, n);
+    _mm_sfence();
+}
+const bool g_have_avx2 = __builtin_cpu_supports("avx2");
+void stage_copy(uint8_t* d, const uint8_t* s, size_t n) {
+    if (g_have_avx2 && n >= 4096) copy_nt_avx2(d, s, n);
+    else std::memcpy(d, s, n);
+}
 
 int64_t now_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
@@ -1399,7 +1431,7 @@ extern "C" int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len) {
         const size_t k = std::min<size_t>(len, kBlock - w->blocks.back().end);
         uint8_t* dst = w->blocks.back().p + w->blocks.back().end;
         wl.unlock();
-        std::memcpy(dst, p, k);
+        stage_copy(dst, p, k);
         wl.lock();
         Blk& bk = w->blocks.back();
         bk.end += static_cast<uint32_t>(k);

@@ -17,7 +17,20 @@
 #include <thread>
 #include <vector>
 
+#include <immintrin.h>
+#include <algorithm>
+
 #include "kcdc.h"
+
+__attribute__((target("avx2"))) static void nt_copy(uint8_t* d, const uint8_t* s, size_t n) {
+    const size_t h = std::min<size_t>(n, (32 - (reinterpret_cast<uintptr_t>(d) & 31)) & 31);
+    std::memcpy(d, s, h);
+    d += h, s += h, n -= h;
+    for (; n >= 32; n -= 32, d += 32, s += 32)
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(d), _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s)));
+    std::memcpy(d, s, n);
+    _mm_sfence();
+}
 
 int main(int argc, char** argv) {
     const int W = argc > 1 ? std::atoi(argv[1]) : 64;
@@ -152,6 +165,31 @@ int main(int argc, char** argv) {
         copy_rate = static_cast<double>(W) * L / std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() /
                     (1ull << 30);
     }
+    // the same, with non-temporal stores (what the batcher's staging copy uses on AVX2 hosts)
+    double copy_nt_rate = 0;
+    if (__builtin_cpu_supports("avx2")) {
+        std::vector<uint8_t*> stage(W);
+        for (auto& p : stage) p = static_cast<uint8_t*>(std::aligned_alloc(64, 4u << 20));
+        std::vector<std::thread> th;
+        std::atomic<bool> go{false};
+        for (int i = 0; i < W; i++)
+            th.emplace_back([&, i] {
+                while (!go.load()) std::this_thread::yield();
+                size_t at = 0;
+                for (size_t pos = 0; pos < L; pos += S) {
+                    const size_t k = S < L - pos ? S : L - pos;
+                    if (at + k > (4u << 20)) at = 0;
+                    nt_copy(stage[i] + at, data[i].data() + pos, k);
+                    at += k;
+                }
+            });
+        const auto t0 = std::chrono::steady_clock::now();
+        go = true;
+        for (auto& t : th) t.join();
+        copy_nt_rate = static_cast<double>(W) * L / std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() /
+                       (1ull << 30);
+        for (auto& p : stage) std::free(p);
+    }
     double best = 0, sum = 0;
     for (double x : rates) {
         best = x > best ? x : best;
@@ -162,9 +200,9 @@ int main(int argc, char** argv) {
                 "\"round_wait_s\": %.3f, \"dev_gather_s\": %.3f, \"dev_split_s\": %.3f, \"dev_span_s\": %.3f, "
                 "\"dev_busy_s\": %.3f, \"host_s\": [%.3f, %.3f, %.3f, %.3f, %.3f], "
                 "\"round_idle_s\": %.3f, \"writer_capped_s\": %.3f, \"writer_block_s\": %.3f, \"pool_misses\": %.0f, \"pool_misses_after_warmup\": %.0f, \"writer_block_s_after_warmup\": %.3f, \"round_lock_s\": %.3f, "
-                "\"memcpy_only_gib_s\": %.2f, \"hash\": \"%s\", \"ids_named\": %.0f, \"hash_steps\": %.0f, \"hash_dev_s\": %.3f, \"id_space_wait_s\": %.3f, \"hash_idle_s\": %.3f, \"chains_per_step\": %.0f, \"parity_ok\": %s}\n",
+                "\"memcpy_only_gib_s\": %.2f, \"memcpy_nt_only_gib_s\": %.2f, \"hash\": \"%s\", \"ids_named\": %.0f, \"hash_steps\": %.0f, \"hash_dev_s\": %.3f, \"id_space_wait_s\": %.3f, \"hash_idle_s\": %.3f, \"chains_per_step\": %.0f, \"parity_ok\": %s}\n",
                 W, L >> 20, S >> 10, name.c_str(), static_cast<unsigned long long>(round >> 20),
-                rates.empty() ? 0.0 : sum / rates.size(), best, static_cast<long long>(rounds), st[2], st[3], st[4], st[5], st[6], st[7], st[8], st[9], st[10], st[11], st[12], st[13], st[14], st[15], st[16], st[16] - st0[16], st[15] - st0[15], st[17], copy_rate,
+                rates.empty() ? 0.0 : sum / rates.size(), best, static_cast<long long>(rounds), st[2], st[3], st[4], st[5], st[6], st[7], st[8], st[9], st[10], st[11], st[12], st[13], st[14], st[15], st[16], st[16] - st0[16], st[15] - st0[15], st[17], copy_rate, copy_nt_rate,
                 hash.c_str(), st[18], st[19], st[20], st[21], st[22], st[19] > 0 ? st[23] / st[19] : 0.0, ok ? "true" : "false");
     return ok ? 0 : 2;
 }
