@@ -12,20 +12,28 @@
 // any valid RFC 1951 stream, so what must match is the format, not the encoder's choices.
 //
 // Device layout: a chunk is cut into 32 KiB spans (one 64-lane wave each) and a span into
-// 512-byte segments (one lane each).  The wave stages its span in LDS (segment l at a
-// 516-byte stride, so lanes at equal offsets hit distinct banks), and every lane runs a
-// greedy LZ77 over its own segment with a 128-entry hash table of its own (lane-minor u16
-// columns: conflict free).  A lane emits one fixed-Huffman block (BTYPE 01) for its segment
-// and ends it with an empty stored block (zlib's sync flush: 3 bits, pad, 00 00 FF FF), so
-// every segment's output is a whole number of bytes and segments concatenate by a byte
-// prefix sum.  A segment whose block is not smaller than a stored copy becomes a stored
-// block (5 + n bytes, copied from the input by the finish kernel).  The stream ends with an
-// empty final fixed block (03 00).
-//
-// Kernels, in stream order: span_count (spans per chunk), span_scan (prefix), deflate_spans
-// (LZ77 + bits; output bytes per span), span_pos (their prefix), deflate_copy (one wave per
-// span: segments to their places, dword stores), deflate_frame (per chunk: header ID, final
-// block, length, the ID kept).
+// 512-byte segments (one lane each).  The wave stages its span in LDS (segment l at a 516-byte
+// stride, so lanes at equal offsets hit distinct banks) and every lane runs a greedy LZ77 parse
+// over its own segment (lz_spans_kernel<FMT>).  Candidates per position: the lane's 64-entry hash
+// table (lane-minor u16 columns); with effort >= 1 also the previous match's distance (a repeat
+// candidate), the 32 nearest distances at the segment's first position, the three previous lanes'
+// latest entries and the span's first occurrence of the hash (a table built by LDS atomic min);
+// among equally long matches the nearest wins; the default level adds one-step lazy matching.
+// How a segment's matches are written depends on the format:
+//   deflate  the parse leaves tokens; deflate_plan builds one plan per span (literal/length and
+//            distance histograms, code lengths <= 15 bits, the dynamic header, every segment's
+//            exact size under the dynamic and the fixed code) and picks stored / fixed / dynamic
+//            blocks; deflate_emit_kernel writes each segment's bits at its planned bit offset, a
+//            span ends byte-aligned (deflate_stored_kernel copies stored spans);
+//   S2       Snappy elements (literal runs, copy-1/copy-2) in S2's framing format, one framed
+//            chunk per span with the masked CRC-32C of its bytes (crc_spans_kernel<true>);
+//   zstd     one Compressed_Block per segment: literals Huffman-coded with one code per span
+//            (the first saving segment carries the tree, later ones are Treeless) or raw, the
+//            sequences through the predefined FSE tables, written backwards (zstd_seqs).
+// A segment that would not beat a stored copy is stored.  Segments join by a byte prefix sum
+// (span_pos), deflate_copy_kernel places them, deflate_frame_kernel writes the header ID, the
+// format's frame (gzip member with CRC-32 and ISIZE, zstd frame header, final empty block) and
+// the kept-or-dropped ID (NoCompression when the output is not smaller).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -1075,37 +1083,68 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
         return n;
     };
     // Best match at xx: the lane table's latest candidate (inside the segment) and, with effort
-    // >= 1, the span's first occurrence (anywhere earlier in the span).  Updates the lane table.
+    // >= 1, the span's first occurrence (anywhere earlier in the span), the previous lanes' latest
+    // entries and the previous match's distance (a repeat candidate, zstd's repcode idea: periodic
+    // and structured data repeat their distances).  Among equally long matches the nearest wins
+    // (fewer distance extra bits).  Updates the lane table.
+    uint32_t last_d = 0;  // the previous match's distance (0: none yet)
     auto best_at = [&](uint32_t xx, uint32_t& q) -> uint32_t {
         const uint32_t v = ld32(xx);
         const uint32_t hv = v * kMul;
         const uint32_t h = hv >> (32u - kHashBits);
         const uint32_t c1 = tab[h * 64u + lane];
         tab[h * 64u + lane] = static_cast<uint16_t>(xx);
-        uint32_t n = c1 >= x0 ? match_len(c1, xx, v) : 0u;
+        uint32_t n = 0;
         q = c1;
+        // effort >= 1: the repeat distance first (periodic data: nearest, and usually full length)
+        if (a.effort >= 1u && last_d && last_d <= xx) {
+            n = match_len(xx - last_d, xx, v);
+            if (n) q = xx - last_d;
+        }
+        if (c1 >= x0 && (n == 0u || c1 != q)) {
+            const uint32_t m = match_len(c1, xx, v);
+            if (m > n || (m == n && m && c1 > q)) {
+                n = m;
+                q = c1;
+            }
+        }
         if (a.effort >= 1u) {
-            const uint32_t c2 = ftab[hv >> (32u - kFirstBits)];
-            if (c2 != c1) {
-                const uint32_t n2 = match_len(c2, xx, v);
-                if (n2 > n) {
-                    n = n2;
-                    q = c2;
+            // candidates nearest first; none is tried once a match reaches the longest possible
+            const uint32_t full = min(xe - xx, FMT == kFmtS2 ? kSeg : 258u);
+            auto offer = [&](uint32_t c) {  // longer, or as long and nearer
+                if (n >= full) return;
+                const uint32_t m = match_len(c, xx, v);
+                if (m > n || (m == n && m && c > q)) {
+                    n = m;
+                    q = c;
                 }
+            };
+            // a segment's first position: its own table is empty, so probe the 32 nearest
+            // distances (a period up to 32 then costs its distance, not one to a far occurrence);
+            // the 32 bytes before it are read once and compared from registers
+            if (xx == x0 && xx >= 32u && n < full) {
+                uint32_t w[9];
+#pragma unroll
+                for (int i = 0; i < 9; i++) w[i] = ld32(xx - 32u + 4u * i);  // bytes xx-32 .. xx+3
+                uint32_t kmin = 0;  // the nearest distance whose 4 bytes agree (then one match_len)
+#pragma unroll
+                for (uint32_t k = 32; k >= 1u; k--) {
+                    const uint32_t o = 32u - k;  // byte offset of xx - k in w
+                    const uint32_t cv = (o & 3u) ? __builtin_amdgcn_alignbit(w[(o >> 2) + 1], w[o >> 2], 8u * (o & 3u))
+                                                 : w[o >> 2];
+                    kmin = cv == v ? k : kmin;
+                }
+                if (kmin) offer(xx - kmin);
             }
             // the latest candidates of the three previous segments (their lanes' tables: any entry
             // is an earlier position of this hash, whatever those lanes have reached; a host model
             // of the parse on the mixed bench data: 1 segment back -0.7 % bytes, 3 back -1.4 %)
             for (uint32_t k = 1; k <= 3u && k <= lane; k++) {
                 const uint32_t c3 = tab[h * 64u + lane - k];
-                if (c3 != 0xFFFFu && c3 != q) {
-                    const uint32_t n3 = match_len(c3, xx, v);
-                    if (n3 > n) {
-                        n = n3;
-                        q = c3;
-                    }
-                }
+                if (c3 != 0xFFFFu && c3 != q) offer(c3);
             }
+            const uint32_t c2 = ftab[hv >> (32u - kFirstBits)];  // the span's first occurrence: farthest
+            if (c2 != c1) offer(c2);
         }
         return n;
     };
@@ -1141,6 +1180,7 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
                 over = true;
                 break;
             }
+            last_d = x - cand;
             x += n;
             lit = x;
         } else {
