@@ -271,9 +271,15 @@ struct BuzRing {
         }
         return min(m, m0 | hmask);
     }
+    // The rare exact re-run of a step whose running test passed: the first position in [lo, hi]
+    // that is a candidate, else 4N.  16-byte windows (the arrays shift by four dwords per window),
+    // done as soon as every lane running it has found its candidate.  (Round 5: the arrays shifted
+    // by one dword every 4 bytes, ~3,800 VALU per re-run, and at 128K averages 6 % of wave-steps
+    // re-run.  Fully unrolled instead, the long-path scan kernel spilled.)
     template <int N>
     __device__ __forceinline__ uint32_t exact(State st0, const uint32_t (&prv)[16], const uint32_t (&dw)[N], int lo,
                                               int hi) const {
+        static_assert(N % 4 == 0, "16-byte windows");
         uint32_t e[N], o[N];
 #pragma unroll
         for (int j = 0; j < N; j++) {
@@ -282,17 +288,18 @@ struct BuzRing {
         }
         uint32_t hh = st0, first = 4 * N;
 #pragma unroll 1
-        for (int j = 0; j < N; j++) {
+        for (int w = 0; w < N / 4; w++) {
 #pragma unroll
-            for (int b = 0; b < 4; b++) {
-                hh = rotl1(hh) ^ look(o[0], b) ^ look(e[0], b);
-                const int i = 4 * j + b;
+            for (int b = 0; b < 16; b++) {
+                hh = rotl1(hh) ^ look(o[b >> 2], b & 3) ^ look(e[b >> 2], b & 3);
+                const int i = 16 * w + b;
                 if (first == 4 * N && (hh & mask) == 0 && i >= lo && i <= hi) first = static_cast<uint32_t>(i);
             }
+            if (__ballot(first == 4 * N) == 0) break;
 #pragma unroll
-            for (int k = 0; k < N - 1; k++) {
-                e[k] = e[k + 1];
-                o[k] = o[k + 1];
+            for (int k = 0; k < N - 4; k++) {
+                e[k] = e[k + 4];
+                o[k] = o[k + 4];
             }
         }
         return first;
@@ -1952,6 +1959,8 @@ __device__ __forceinline__ void rk_step64(const RkCtx& k, uint32_t& ha, uint32_t
 // that is a candidate, else 64.
 __device__ uint32_t rk_exact64(const RkCtx& k, uint32_t hi, uint32_t lo, const uint32_t (&in)[16],
                                const uint32_t (&prv)[16], int lo_i, int hi_i) {
+    // 16-byte windows (the arrays shift by four dwords per window, not one per 4 bytes), done
+    // once every lane running it has found its candidate
     uint32_t e[16], o[16];
 #pragma unroll
     for (int j = 0; j < 16; j++) {
@@ -1960,17 +1969,18 @@ __device__ uint32_t rk_exact64(const RkCtx& k, uint32_t hi, uint32_t lo, const u
     }
     uint32_t first = 64;
 #pragma unroll 1
-    for (int j = 0; j < 16; j++) {
+    for (int w = 0; w < 4; w++) {
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
-            rk_roll(k, hi, lo, rk_out(k, o[0], b), e[0], b);
-            const int i = 4 * j + b;
+        for (int b = 0; b < 16; b++) {
+            rk_roll(k, hi, lo, rk_out(k, o[b >> 2], b & 3), e[b >> 2], b & 3);
+            const int i = 16 * w + b;
             if (first == 64 && hi < k.thr && i >= lo_i && i <= hi_i) first = static_cast<uint32_t>(i);
         }
+        if (__ballot(first == 64) == 0) break;
 #pragma unroll
-        for (int q = 0; q < 15; q++) {
-            e[q] = e[q + 1];
-            o[q] = o[q + 1];
+        for (int q = 0; q < 12; q++) {
+            e[q] = e[q + 4];
+            o[q] = o[q + 4];
         }
     }
     return first;
