@@ -173,6 +173,84 @@ __global__ __launch_bounds__(512, 2) void rkloop_kernel(uint64_t steps, uint32_t
     if ((ma ^ mb ^ ha ^ la ^ hb ^ lb) == 0x12345678u) out[threadIdx.x] = ma;
 }
 
+// Round 5: the same hot loop at 12 waves per CU (three per SIMD: six chains per SIMD instead of
+// four).  12 step slots of 8 KiB leave 64 KiB for the tables, so both go to 16 replicas in one
+// table of 256-byte rows: mod[] in bytes 0..127 of row r (address: bfe + lshl_or, as now) and
+// out[] in bytes 128..255 (address: one v_perm with 128 + lane%16 * 8 as its low byte).  Same
+// instruction mix per byte; what changes is the chains in flight per SIMD (and out[]'s 16-replica
+// bank conflicts).  "rk12": this variant; "rk": the production layout at 8 waves.
+struct RkL12 {
+    uint64_t tab[256 * 32];        // row r: mod replicas 0..15, then out replicas 0..15
+    uint32_t slot[12][32][64];
+};
+__global__ __launch_bounds__(768, 1) void rkloop12_kernel(uint64_t steps, uint32_t seed, uint32_t* out) {
+    __shared__ RkL12 t;
+    for (uint32_t i = threadIdx.x; i < 256u * 32u; i += 768u) t.tab[i] = (i * 0x9E3779B97F4A7C15ull) ^ seed;
+    const uint32_t wv = threadIdx.x / 64u, lane = threadIdx.x % 64u;
+    for (uint32_t i = 0; i < 32u; i++) t.slot[wv][i][lane] = (lane + 1u) * 0x01000193u * (i + seed);
+    __syncthreads();
+    const char* tb = reinterpret_cast<const char*>(t.tab);
+    const uint32_t l8o = 128u + (lane & 15u) * 8u, l8m = (lane & 15u) * 8u;
+    auto maddr = [&](uint32_t lo) { return (__builtin_amdgcn_ubfe(lo, 11, 8) << 8) | l8m; };
+    auto oaddr = [&](uint32_t w, int b) { return __builtin_amdgcn_perm(w, l8o, 0x0c0c0000u | ((4u + (3 - b)) << 8)); };
+    auto sel = [](int b) { return 0x00030201u | (static_cast<uint32_t>(7 - b) << 24); };
+    uint32_t ha = seed, la = seed * 3u, hb = seed * 5u, lb = seed * 7u, ma = ~0u, mb = ~0u;
+    uint32_t pa[16], pb[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) pa[i] = pb[i] = seed * (i + 1);
+    for (uint64_t s = 0; s < steps; s++) {
+        uint32_t a[16], b[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            a[i] = __builtin_bitreverse32(t.slot[wv][i][lane]);
+            b[i] = __builtin_bitreverse32(t.slot[wv][16 + i][lane]);
+        }
+        constexpr int W = 2;
+        uint64_t oa[64], ob[64];
+        uint64_t mA = ld64(tb, maddr(la)), mB;
+#pragma unroll
+        for (int i = 0; i < W; i++) oa[i] = ld64(tb, oaddr(pa[i >> 2], i & 3));
+        mB = ld64(tb, maddr(lb));
+#pragma unroll
+        for (int i = 0; i < W; i++) ob[i] = ld64(tb, oaddr(pb[i >> 2], i & 3));
+        uint32_t pha = ~0u, phb = ~0u;
+#pragma unroll
+        for (int x = 0; x < 64; x++) {
+            __builtin_amdgcn_sched_barrier(0);
+            {
+                const uint32_t th = __builtin_amdgcn_perm(a[x >> 2], ha, sel(x & 3));
+                const uint32_t tl = __builtin_amdgcn_alignbit(ha, la, 8);
+                ha = __builtin_amdgcn_bitop3_b32(th, static_cast<uint32_t>(mA >> 32), static_cast<uint32_t>(oa[x] >> 32), 0x96);
+                la = __builtin_amdgcn_bitop3_b32(tl, static_cast<uint32_t>(mA), static_cast<uint32_t>(oa[x]), 0x96);
+                __builtin_amdgcn_sched_barrier(0);
+                if (x + 1 < 64) mA = ld64(tb, maddr(la));
+                if (x + W < 64) oa[x + W] = ld64(tb, oaddr(pa[(x + W) >> 2], (x + W) & 3));
+                __builtin_amdgcn_sched_barrier(0);
+                if (x & 1) asm("v_min3_u32 %0, %1, %2, %3" : "=v"(ma) : "v"(ma), "v"(pha), "v"(ha));
+                else pha = ha;
+            }
+            {
+                const uint32_t th = __builtin_amdgcn_perm(b[x >> 2], hb, sel(x & 3));
+                const uint32_t tl = __builtin_amdgcn_alignbit(hb, lb, 8);
+                hb = __builtin_amdgcn_bitop3_b32(th, static_cast<uint32_t>(mB >> 32), static_cast<uint32_t>(ob[x] >> 32), 0x96);
+                lb = __builtin_amdgcn_bitop3_b32(tl, static_cast<uint32_t>(mB), static_cast<uint32_t>(ob[x]), 0x96);
+                __builtin_amdgcn_sched_barrier(0);
+                if (x + 1 < 64) mB = ld64(tb, maddr(lb));
+                if (x + W < 64) ob[x + W] = ld64(tb, oaddr(pb[(x + W) >> 2], (x + W) & 3));
+                __builtin_amdgcn_sched_barrier(0);
+                if (x & 1) asm("v_min3_u32 %0, %1, %2, %3" : "=v"(mb) : "v"(mb), "v"(phb), "v"(hb));
+                else phb = hb;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            pa[i] = a[i];
+            pb[i] = b[i];
+        }
+    }
+    if ((ma ^ mb ^ ha ^ la ^ hb ^ lb) == 0x12345678u) out[threadIdx.x] = ma;
+}
+
 int main(int argc, char** argv) {
     hipDeviceProp_t p;
     CK(hipGetDeviceProperties(&p, 0));
@@ -180,6 +258,25 @@ int main(int argc, char** argv) {
     uint64_t* cyc;
     CK(hipMalloc(&out, 4096 * 4));
     CK(hipMalloc(&cyc, 256 * 16 * 8));
+    if (argc > 1 && std::string(argv[1]) == "rk12") {
+        const double bytes = 6.7429e9;
+        const int cus = p.multiProcessorCount;
+        const uint64_t steps = static_cast<uint64_t>(bytes / (cus * 768.0) / 128.0);
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        for (int rep = 0; rep < 4; rep++) {
+            CK(hipEventRecord(e0, 0));
+            hipLaunchKernelGGL(rkloop12_kernel, dim3(cus), dim3(768), 0, 0, steps, 7u, out);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            printf("rk hot loop, 12 waves/CU, 64 KiB combined tables: %.3f ms over config 2 (%llu 128-byte steps per lane)\n", ms,
+                   static_cast<unsigned long long>(steps));
+        }
+        return 0;
+    }
     if (argc > 1 && std::string(argv[1]) == "rk") {
         const double bytes = 6.7429e9;  // config 2's rolled bytes under 4M-RABINKARP
         const int cus = p.multiProcessorCount;
