@@ -406,6 +406,8 @@ int kcdc_compress_chunks_device(const char* algorithm, const uint8_t* d_data, co
  *                         the wave that owns its stream only); 2: help on whatever the average
  *                         (0, the default: help for averages of 1 MiB and up, and for Rabin-Karp
  *                         launches with fewer streams than waves)
+ *   KCDC_TEST_ID_RING     bytes of the writers' content-ID ring for batchers created from now on
+ *                         (0: the default; small values exercise wrap-around and backpressure)
  * kcdc_test_occupy: occupy `nwg` CUs (one workgroup with all of the CU's LDS each) for
  * `usec` microseconds on `hip_stream`, e.g. to run a batch beside a kernel that holds CUs.
  * kcdc_test_queue_stat: after the last pipelined batch launch has finished (synchronise
@@ -418,6 +420,7 @@ int kcdc_compress_chunks_device(const char* algorithm, const uint8_t* d_data, co
 #define KCDC_TEST_HASH_LANES 4
 #define KCDC_TEST_NO_SERVER 5
 #define KCDC_TEST_NO_HELP 6
+#define KCDC_TEST_ID_RING 7
 int kcdc_test_set(int32_t key, int64_t value);
 int kcdc_test_occupy(uint32_t nwg, uint32_t usec, void* hip_stream);
 #define KCDC_TEST_STAT_GIVEUPS 1

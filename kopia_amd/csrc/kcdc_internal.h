@@ -41,6 +41,7 @@ const Algo& algo_at(int i);  // sorted by name
 
 // Test knob: lanes per chunk of the content-hash kernels (0 auto, 1, 4).
 int& test_hash_lanes();
+uint64_t& test_id_ring_bytes();  // kcdc_test_set(KCDC_TEST_ID_RING): the writers' ID ring size (0: default)
 
 // Wrong-output experiment switches compiled into this build (comma-terminated names; "" in
 // the product): kcdc_kernels.hip, kcdc_crypt.hip.

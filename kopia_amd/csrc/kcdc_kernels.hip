@@ -4077,6 +4077,7 @@ extern "C" int kcdc_test_set(int32_t key, int64_t value) {
         case 4: test_hash_lanes() = static_cast<int>(value); return 0;     // KCDC_TEST_HASH_LANES
         case 5: set_scan_server_off(value != 0); return 0;                 // KCDC_TEST_NO_SERVER
         case 6: g_test.help = value == 2 ? 2 : value != 0; return 0;       // KCDC_TEST_NO_HELP (2: force help on)
+        case 7: test_id_ring_bytes() = static_cast<uint64_t>(value); return 0;  // KCDC_TEST_ID_RING
         default: return set_error(-22, "unknown test knob");
     }
 }

@@ -866,6 +866,7 @@ int BwDev::ids_enable(const char* name, const uint8_t* key, uint32_t key_len) {
     // chains in flight set the naming rate (one chain: ~50 MB/s of BLAKE2b), so the ring holds 64
     // rounds: 16 GiB, ~3,000 chunks of 4-5 MiB at the default 256 MiB rounds (of 288 GB of HBM)
     ring_cap = std::max<uint64_t>(64 * round_bytes, 1ull << 30);
+    if (test_id_ring_bytes()) ring_cap = std::max<uint64_t>(test_id_ring_bytes(), 16) & ~uint64_t(15);  // tests: wrap and backpressure
     chain_cap = 16384;
     Guard g(device);
     hipError_t e = hipStreamCreateWithFlags(&hstream, hipStreamNonBlocking);
@@ -1146,6 +1147,11 @@ void BwDev::hash_loop() {
         t_hidle += std::chrono::duration<double>(std::chrono::steady_clock::now() - w0).count();
     }
     for (int i : live) (void)hipEventSynchronize(steps[i].ev);  // (after an error: nothing reads the buffers after this)
+}
+
+uint64_t& kcdc::test_id_ring_bytes() {
+    static uint64_t v = 0;
+    return v;
 }
 
 namespace {

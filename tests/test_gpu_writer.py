@@ -319,3 +319,18 @@ def test_ids_errors(gpu):
         WriterBatcher("FIXED-4M", hash="BLAKE2B-256-128", key=KEY)
     with pytest.raises(_lib.KcdcError):
         WriterBatcher("DYNAMIC-4M-BUZHASH", hash="NO-SUCH-HASH", key=KEY)
+
+
+@pytest.mark.parametrize("hash_name", ["BLAKE2B-256-128", "BLAKE3-256-128"])
+def test_ids_ring_wraps_under_backpressure(gpu, hash_name):
+    """An ID ring far smaller than the data (KCDC_TEST_ID_RING = 24 MiB): chunks wrap around its
+    end, rounds wait for ring space while the hash thread names the chains ahead of them, and chain
+    slots are reused; every ID must still match hashlib's, in order.  Small averages (many chunks,
+    many publishes) and one long object whose chunks reach the 2 MiB maximum."""
+    lib = _lib.lib()
+    assert lib.kcdc_test_set(_lib.TEST_ID_RING, 24 << 20) == 0
+    try:
+        sizes = [24 << 20] * 6 + [int(x) for x in np.random.default_rng(3).integers(1, 8 << 20, 10)]
+        _run_ids("DYNAMIC-1M-BUZHASH", sizes, ["64k", "rand"], hash_name=hash_name, round_bytes=4 << 20, sid0=900)
+    finally:
+        lib.kcdc_test_set(_lib.TEST_ID_RING, 0)
