@@ -1574,6 +1574,7 @@ extern "C" void kcdc_bw_free(kcdc_bw* w) {
             Guard g(b->device);
             (void)hipStreamSynchronize(b->copy);
             (void)hipStreamSynchronize(b->stream);
+            if (b->idcopy) (void)hipStreamSynchronize(b->idcopy);  // (after an error: ring copies may read it)
             (void)hipFree(w->arena);
             (void)hipFree(w->spare);
         }
