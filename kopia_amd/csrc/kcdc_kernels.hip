@@ -585,11 +585,13 @@ __device__ __forceinline__ void dma_piece(const Loader& ld, int64_t tb, uint32_t
                                           int64_t L, int64_t piece, int lane) {
     // descriptor offsets in 32 bits (ct - tb <= 64, a tile < 2^31 bytes): no per-lane 64-bit values
     const int32_t base = static_cast<int32_t>(ct - tb) + 64 * static_cast<int32_t>(piece), Li = static_cast<int32_t>(L);
+    uint32_t sl = slot;  // opaque per call (as dma_step128): the m0 values are scalar adds, not spills
+    asm volatile("" : "+s"(sl));
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const int l = 16 * i + (lane >> 2);
         const int jj = (lane & 3) ^ ((l >> 2) & 3);
-        dma_lds16(ld.d, slot + 1024u * i, base + l * Li + 16 * jj);
+        dma_lds16(ld.d, sl + 1024u * i, base + l * Li + 16 * jj);
     }
 }
 
@@ -621,11 +623,15 @@ __device__ __forceinline__ void read_piece(const uint8_t* slot, int lane, int64_
 __device__ __forceinline__ void dma_step128(const Loader& ld, int64_t tb, uint32_t slot, int64_t ct,
                                             int64_t L, int64_t n, int lane) {
     const int32_t base = static_cast<int32_t>(ct - tb) + 128 * static_cast<int32_t>(n), Li = static_cast<int32_t>(L);
+    // the slot address made opaque per call: its eight m0 values are then one scalar add each,
+    // not eight values kept across the hash loop (they were SGPR spills, a v_readlane per DMA)
+    uint32_t sl = slot;
+    asm volatile("" : "+s"(sl));
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         const int l = 8 * i + (lane >> 3);
         const int jj = (lane & 7) ^ ((l >> 1) & 7);
-        dma_lds16(ld.d, slot + 1024u * i, base + l * Li + 16 * jj);
+        dma_lds16(ld.d, sl + 1024u * i, base + l * Li + 16 * jj);
     }
 }
 
