@@ -2055,13 +2055,15 @@ __device__ __forceinline__ RkGeom rk_geom(int64_t ct, int64_t hi, const uint8_t*
 // Warm fill: lane l's slot line = [64 B before c0 | 64 B before c0 + L/2] (16-byte granule j
 // of lane l at j ^ sw(l), as dma_step128).
 __device__ __forceinline__ void rk_dma_warm(const Loader& ld, uint32_t slot, int64_t ct, int64_t L, int lane) {
+    uint32_t sl = slot;  // opaque per call (as dma_step128)
+    asm volatile("" : "+s"(sl));
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         const int l = 8 * i + (lane >> 3);
         const int jj = (lane & 7) ^ ((l >> 1) & 7);
         const int64_t c0 = ct + l * L + (jj < 4 ? 0 : L / 2);
         const int64_t coord = c0 - 64 + 16 * (jj & 3);
-        dma_lds16(ld.d, slot + 1024u * i, static_cast<int32_t>(coord - ld.tb));
+        dma_lds16(ld.d, sl + 1024u * i, static_cast<int32_t>(coord - ld.tb));
     }
 }
 // Line fill f (1..2K): odd f = line (f-1)/2 of chain A, even f = line f/2 - 1 of chain B.
