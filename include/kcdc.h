@@ -408,12 +408,20 @@ int kcdc_compress_chunks_device(const char* algorithm, const uint8_t* d_data, co
  *                         launches with fewer streams than waves)
  *   KCDC_TEST_ID_RING     bytes of the writers' content-ID ring for batchers created from now on
  *                         (0: the default; small values exercise wrap-around and backpressure)
+ *   KCDC_TEST_LANE_CAP    buzhash batch launches: bytes per lane segment (a tile is 64 of them),
+ *                         a power of two in [256, 4096]; 0: the default (avg / 256 within
+ *                         [256, 2048]).  Other tile geometries for the same cuts.
  * kcdc_test_occupy: occupy `nwg` CUs (one workgroup with all of the CU's LDS each) for
  * `usec` microseconds on `hip_stream`, e.g. to run a batch beside a kernel that holds CUs.
  * kcdc_test_queue_stat: after the last pipelined batch launch has finished (synchronise
  * first), read one word of its queue header: KCDC_TEST_STAT_GIVEUPS (waves that gave up
  * waiting), KCDC_TEST_STAT_DONE (streams finished), KCDC_TEST_STAT_STEALS (requeued
- * workgroups), KCDC_TEST_STAT_HELPS (tiles scanned by waves that helped another wave's region).  Synchronous copy; returns the word, or a negative KCDC_E* code. */
+ * workgroups), KCDC_TEST_STAT_HELPS (tiles scanned by waves that helped another wave's region),
+ * KCDC_TEST_STAT_TICKETS / KCDC_TEST_STAT_ENTRIES (the ring's ticket and entry counters) and
+ * KCDC_TEST_STAT_WAVES (the launch's waves).  Every wave exits holding one ticket and every
+ * reserved entry is written, so TICKETS - ENTRIES is WAVES (WAVES - 1 when the last stream's
+ * final entry is a tombstone nobody waited for).  Synchronous copy; returns the word, or a
+ * negative KCDC_E* code. */
 #define KCDC_TEST_SPIN_CAP 1
 #define KCDC_TEST_NO_STEAL 2
 #define KCDC_TEST_FORCE_ERROR 3
@@ -421,12 +429,16 @@ int kcdc_compress_chunks_device(const char* algorithm, const uint8_t* d_data, co
 #define KCDC_TEST_NO_SERVER 5
 #define KCDC_TEST_NO_HELP 6
 #define KCDC_TEST_ID_RING 7
+#define KCDC_TEST_LANE_CAP 8
 int kcdc_test_set(int32_t key, int64_t value);
 int kcdc_test_occupy(uint32_t nwg, uint32_t usec, void* hip_stream);
 #define KCDC_TEST_STAT_GIVEUPS 1
 #define KCDC_TEST_STAT_DONE 2
 #define KCDC_TEST_STAT_STEALS 3
 #define KCDC_TEST_STAT_HELPS 4
+#define KCDC_TEST_STAT_TICKETS 10
+#define KCDC_TEST_STAT_ENTRIES 11
+#define KCDC_TEST_STAT_WAVES 12
 int64_t kcdc_test_queue_stat(int32_t key);
 /* Test hook: copy bytes [off, off + n) of the last pipelined launch's queue workspace (queue
  * header, stream ring, help slots) to host memory at dst; 0 or a negative error. */

@@ -33,7 +33,9 @@ KIND_FIXED, KIND_BUZHASH, KIND_RABINKARP = 0, 1, 2
 COUNT_FAILED = (1 << 64) - 1  # KCDC_COUNT_FAILED: the batch launch failed on the device
 TEST_SPIN_CAP, TEST_NO_STEAL, TEST_FORCE_ERROR, TEST_HASH_LANES, TEST_NO_SERVER, TEST_NO_HELP = 1, 2, 3, 4, 5, 6
 TEST_ID_RING = 7
+TEST_LANE_CAP = 8
 STAT_GIVEUPS, STAT_DONE, STAT_STEALS, STAT_HELPS, STAT_TICKET_AUDIT = 1, 2, 3, 4, 5
+STAT_TICKETS, STAT_ENTRIES, STAT_WAVES = 10, 11, 12
 
 
 class KcdcError(RuntimeError):

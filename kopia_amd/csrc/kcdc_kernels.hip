@@ -53,6 +53,10 @@ constexpr int64_t kLaneMax = 2048;      // max bytes per lane segment (tile = 64
 #define KCDC_TILE_DIV 256
 #endif
 constexpr uint64_t kTileDiv = KCDC_TILE_DIV;  // batch lane segments <= avg / kTileDiv (tiles ~ avg / 4), >= 256 B
+#ifndef KCDC_BUZ_LANE_MAX
+#define KCDC_BUZ_LANE_MAX 2048
+#endif
+constexpr uint64_t kBuzLaneMax = KCDC_BUZ_LANE_MAX;  // the buzhash batch kernel's lane segment cap
 constexpr int kSchedWindow = 16;        // bytes per scheduling window in the warm-up / exact loops
 constexpr int kLookahead = 16;          // 128-byte steps: table reads issued this many bytes ahead (VGPR bound)
 
@@ -954,6 +958,9 @@ __device__ __forceinline__ uint64_t qht_add(const BatchArgs& a, int lane, uint64
     if (lane == 0)
         v = __hip_atomic_fetch_add((gu64*)(reinterpret_cast<uint64_t*>(a.queue + kQHT)), inc, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
+#if KCDC_DEBUG_CHECKS  // entries reserved (kQStat+32)
+    if (lane == 0 && (inc >> 32)) add_agent(a.queue + kQStat + 32, static_cast<uint32_t>(inc >> 32));
+#endif
     return v;  // lane 0's register
 }
 __device__ __forceinline__ uint64_t qht_value(uint32_t lo_raw, uint32_t hi_raw) {
@@ -1324,6 +1331,19 @@ __device__ __forceinline__ void pwrite(const BatchArgs& a, int lane, uint32_t e,
     const uint64_t p = reinterpret_cast<uint64_t>(st.abase) + static_cast<uint64_t>(st.off0);
     const __amdgpu_buffer_rsrc_t r = pring_rsrc(a);
     const int base = static_cast<int>((e & a.ring_mask) * kPEntryStride);
+#if KCDC_DEBUG_CHECKS  // entry writes (kQStat+33), and a slot written twice under one tag (code 9)
+    if (lane == 0) {
+        add_agent(a.queue + kQStat + 33, 1u);
+        const u32x4 old = __builtin_amdgcn_raw_buffer_load_b128(r, base, 0, 16);
+        const uint32_t ht_tail = ld_agent(a.queue + kQHT + 1);
+        if ((old.x == tag || e >= ht_tail) && atomicAdd(a.queue + kQErr, 1u) == 0) {
+            a.queue[kQStat + 16] = old.x == tag ? 9u : 10u;
+            a.queue[kQStat + 17] = st.sid;
+            a.queue[kQStat + 18] = e;
+            a.queue[kQStat + 19] = ht_tail;
+        }
+    }
+#endif
     if (lane == 0) {
         __builtin_amdgcn_raw_buffer_store_b128(pgranule(tag, st.cnt, tomb ? kTombstone : st.sid), r, base + 0, 0,
                                                16 /* sc1 */);
@@ -1383,7 +1403,7 @@ __device__ __forceinline__ int64_t pipe_quantum(int64_t backlog, int64_t q = kPi
 // 3.639 ms, 256K 2.697 vs 2.843, 4M 1.296 vs 1.309; all bit-exact.
 __device__ __forceinline__ int64_t pipe_quantum_tiles(int64_t backlog, uint32_t lane_cap) {
     const int64_t q = 6 * kWave * static_cast<int64_t>(lane_cap);
-    return pipe_quantum(backlog, q > (512 << 10) ? q : (512 << 10));
+    return pipe_quantum(backlog, q < (512 << 10) ? (512 << 10) : q > (768 << 10) ? (768 << 10) : q);
 }
 
 template <bool TOP>
@@ -1564,7 +1584,9 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         // The owner's claim on its next tile (atomic add on its slot's bottom), issued in step 0
         // behind the refill DMA and read in step 2 (or at the tile end for one- and two-step tiles).
         const bool claim_next_r = (hs & kHsPub) && !is_help && !last_of_region && htile() + 1u < hK();
-        const bool budget_out = !(hs & kHsHelped) && budget - kWave * g.L <= 0;  // (with helpers: no yield)
+        // (a help task never yields: its wave's budget is the last own visit's leftover, and a
+        // reservation made here would never be written -- its ticket's taker would wait to the end)
+        const bool budget_out = !is_help && !(hs & kHsHelped) && budget - kWave * g.L <= 0;  // (with helpers: no yield)
         bool ends_nocand = false;  // no candidate in this tile => the stream is finished
         if (!is_help && last_of_region) {
             const int64_t s2 = cur.s + mx - 1 <= cur.n - 1 ? cur.s + mx : cur.n;
@@ -3474,8 +3496,10 @@ struct TestKnobs {
     bool no_steal = false;     // disable try_steal
     bool force_error = false;  // mark every pipelined launch as failed
     int help = 0;              // intra-region help: 0 the policy below, 1 off, 2 on (A/B, tests)
+    uint32_t lane_cap = 0;     // buzhash batch lane segment cap (256..4096, a power of two); 0: base_args' rule
     char* last_ws = nullptr;   // queue header of the last pipelined launch (kcdc_test_queue_stat)
     int last_dev = 0;
+    uint32_t last_waves = 0;   // launch waves of that launch (kcdc_test_queue_stat key 12)
 };
 TestKnobs g_test;
 
@@ -3515,9 +3539,9 @@ dev::BatchArgs base_args(const Algo& algo, const DeviceTables& t) {
     a.rk_shift = static_cast<uint32_t>(tables().rk_shift);
     // largest power of two <= avg / 256, within [256, kLaneMax]: tiles of ~avg/4 (1 MiB and
     // larger averages keep the full 2 KiB lane segments)
-    uint64_t cap = dev::kLaneMax;
+    uint64_t cap = algo.kind == kBuzhash ? dev::kBuzLaneMax : dev::kLaneMax;
     while (cap > 256 && cap * dev::kTileDiv > algo.avg) cap >>= 1;
-    a.lane_cap = static_cast<uint32_t>(cap);
+    a.lane_cap = algo.kind == kBuzhash && g_test.lane_cap ? g_test.lane_cap : static_cast<uint32_t>(cap);
     return a;
 }
 #if KCDC_TRACE || KCDC_DEBUG_CHECKS
@@ -3704,6 +3728,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         a.queue = reinterpret_cast<uint32_t*>(ws);
         g_test.last_ws = ws;
         g_test.last_dev = device;
+        g_test.last_waves = grid * wg_waves;
 #if KCDC_TRACE || KCDC_DEBUG_CHECKS
         g_last_ws = ws;
 #endif
@@ -4086,13 +4111,20 @@ extern "C" int kcdc_test_set(int32_t key, int64_t value) {
         case 5: set_scan_server_off(value != 0); return 0;                 // KCDC_TEST_NO_SERVER
         case 6: g_test.help = value == 2 ? 2 : value != 0; return 0;       // KCDC_TEST_NO_HELP (2: force help on)
         case 7: test_id_ring_bytes() = static_cast<uint64_t>(value); return 0;  // KCDC_TEST_ID_RING
+        case 8:                                                            // KCDC_TEST_LANE_CAP
+            if (value != 0 && (value < 256 || value > 4096 || (value & (value - 1)) != 0))
+                return set_error(-22, "lane cap: 0, or a power of two in [256, 4096]");
+            g_test.lane_cap = static_cast<uint32_t>(value);
+            return 0;
         default: return set_error(-22, "unknown test knob");
     }
 }
 
 extern "C" int64_t kcdc_test_queue_stat(int32_t key) {
+    if (key == 12) return g_test.last_ws ? static_cast<int64_t>(g_test.last_waves) : set_error(-22, "no pipelined batch launch yet");
     const int word = key == 1 ? dev::kQErr : key == 2 ? dev::kQDone : key == 3 ? dev::kQSteal : key == 4 ? dev::kQHelp
-                   : key >= 5 && key <= 9 ? dev::kQDiag + (key - 5) : -1;
+                   : key >= 5 && key <= 9 ? dev::kQDiag + (key - 5)
+                   : key == 10 ? dev::kQHT : key == 11 ? dev::kQHT + 1 : -1;
     if (word < 0) return set_error(-22, "unknown queue statistic");
     if (!g_test.last_ws) return set_error(-22, "no pipelined batch launch yet");
     int prev = 0;

@@ -185,3 +185,42 @@ def test_forced_help_below_policy(gpu, name):
     cuts, counts = coracle.split_prng_streams(name, SEED, np.arange(11, 11 + ns), L, nthreads=16)
     bad = [i for i in range(ns) if got[i].tolist() != cuts[i, :counts[i]].tolist()]
     assert not bad, bad[:8]
+
+
+def _ring_balance():
+    lib = _lib.lib()
+    tickets = _lib.check(lib.kcdc_test_queue_stat(_lib.STAT_TICKETS))
+    entries = _lib.check(lib.kcdc_test_queue_stat(_lib.STAT_ENTRIES))
+    waves = _lib.check(lib.kcdc_test_queue_stat(_lib.STAT_WAVES))
+    return tickets, entries, waves
+
+
+@pytest.mark.parametrize("name,lane_cap", [("DYNAMIC-4M-BUZHASH", 0), ("DYNAMIC-2M-BUZHASH", 0),
+                                           ("DYNAMIC-2M-BUZHASH", 1024), ("DYNAMIC-4M-RABINKARP", 0)])
+def test_every_reserved_entry_is_written(gpu, name, lane_cap):
+    """Round-5 regression: a HELP task whose wave had spent its own visit's budget reserved a ring
+    entry (the yield path's atomic) and never wrote it, so the wave that took that entry's ticket
+    waited to the end of the launch -- ~1,200 of 2,048 waves per config-2 launch at 2M.  With
+    1 KiB lanes at 2M (regions of 49 tiles, yields every 8) the orphans outnumbered the waves:
+    every wave ended up holding an orphan ticket, the real entries behind them were never taken,
+    and the launch lost the streams still queued (profiles/r05/orphan_entries/).  Now every wave
+    exits holding exactly one ticket no entry was written for (the last stream's tombstone may
+    leave one fewer), and the 1 KiB geometry splits bit-exact launch after launch, each launch
+    bounded by a small spin cap so a regression fails fast instead of spinning."""
+    import torch
+    ns, L = 4096, 4 << 20
+    data = torch.empty(ns * L, dtype=torch.uint8, device=gpu)
+    batch.fill_prng(data, L, ns, L, SEED, 0)
+    b = batch.make_device_batch(name, [data.data_ptr() + i * L for i in range(ns)], [L] * ns, gpu)
+    cuts, counts = coracle.split_prng_streams(name, SEED, np.arange(ns), L, nthreads=16)
+    want = [cuts[i, :counts[i]].tolist() for i in range(ns)]
+    with knob(_lib.TEST_LANE_CAP, lane_cap), knob(_lib.TEST_SPIN_CAP, 200000):
+        for launch in range(6):
+            batch.split_batch_device(name, b)
+            torch.cuda.synchronize()
+            tickets, entries, waves = _ring_balance()
+            assert waves - 1 <= tickets - entries <= waves, (launch, tickets, entries, waves)
+            assert _lib.check(_lib.lib().kcdc_test_queue_stat(_lib.STAT_GIVEUPS)) == 0, launch
+            got = batch.read_cuts(b)
+            bad = [i for i in range(ns) if got[i].tolist() != want[i]]
+            assert not bad, f"launch {launch}: {len(bad)} streams differ, first {bad[:5]}"

@@ -44,6 +44,12 @@ for rep in range(reps):  # until a launch loses a stream (a race shows in some l
 st = {k: int(lib.kcdc_test_queue_stat(v)) for k, v in (("giveups", _lib.STAT_GIVEUPS), ("done", _lib.STAT_DONE),
                                                         ("steals", _lib.STAT_STEALS), ("helps", _lib.STAT_HELPS))}
 print(st, flush=True)
+import ctypes as C  # noqa: E402
+_h = np.zeros(2048, np.uint32)
+assert lib.kcdc_test_ws_copy(_h.ctypes.data_as(C.c_void_p), 0, 8192) == 0
+# debug builds (KCDC_DEBUG_CHECKS): entries reserved / entries written (every reservation is written once)
+print("head", int(_h[0]), "tail", int(_h[1]), "reserved (debug)", int(_h[1792 + 32]), "written (debug)", int(_h[1792 + 33]),
+      "first check failure", _h[1792 + 16:1792 + 24].tolist(), flush=True)
 counts = b.counts.cpu().numpy()[:ns].astype(np.int64)
 print("failed counts", int((counts == -1).sum()), "max count", int(counts.max()), flush=True)
 cuts, cnt = coracle.split_prng_streams(name, SEED, np.arange(ns), L, nthreads=16)

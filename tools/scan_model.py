@@ -21,7 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from oracle import coracle  # noqa: E402  (test/measurement infrastructure only)
 
-WAVE, LANE_MAX, SEED = 64, 2048, 0x6B6F706961
+WAVE, SEED = 64, 0x6B6F706961
+LANE_MAX = int(os.environ.get("KCDC_LANE_MAX", "2048"))  # kcdc_kernels.hip kLaneMax
 TILE_DIV = int(os.environ.get("KCDC_TILE_DIV", "256"))  # kcdc_kernels.hip kTileDiv
 
 
