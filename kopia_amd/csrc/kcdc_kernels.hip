@@ -1048,6 +1048,17 @@ __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
 #ifndef KCDC_HELP_GAP  // a region is open to helpers while top >= bottom + GAP (1 vs 2: 1.295 vs
 #define KCDC_HELP_GAP 1u  // 1.332 ms on config 2, same-process A/B, profiles/r04/third/)
 #endif
+// Publish only in visits that began with no stream waiting (budget kNoYield): only then can a
+// wave be waiting for a ticket, i.e. free to help (KCDC_HELP_TAIL_ONLY; 0 publishes every region).
+#ifndef KCDC_HELP_MIN_AVG  // launch_split_batch's help policy: averages from here up (1 MiB)
+#define KCDC_HELP_MIN_AVG (1ull << 20)
+#endif
+#ifndef KCDC_HELP_TAIL_ONLY
+#define KCDC_HELP_TAIL_ONLY 0
+#endif
+__device__ __forceinline__ bool help_phase(int64_t budget) {
+    return !KCDC_HELP_TAIL_ONLY || budget > (int64_t(1) << 61);
+}
 constexpr int64_t kHelpSplit = 2;     // sub-tiles per help task (lane segments lane_cap / 2, >= 256 B)
 constexpr int kHelpTiles = 128;          // regions of up to 128 tiles take help (every registered name)
 constexpr uint32_t kHelpMinTiles = 3;    // the owner's tile, its next one, and at least one more
@@ -1575,7 +1586,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             const int64_t T = kWave * static_cast<int64_t>(a.lane_cap);  // bytes per full tile
             const uint32_t K = static_cast<uint32_t>((hi - ct + T) / T);
             hs = 0;
-            if (a.help && K >= kHelpMinTiles && K <= static_cast<uint32_t>(kHelpTiles)) {
+            if (a.help && help_phase(budget) && K >= kHelpMinTiles && K <= static_cast<uint32_t>(kHelpTiles)) {
                 hep++;
                 hs = kHsPub | K;
                 help_publish(a, lane, me, hep, cur, ct, hi, K, T);
@@ -2288,7 +2299,7 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             const int64_t T = kWave * rk_cap;
             const uint32_t K = static_cast<uint32_t>((hi - ct + T) / T);
             hs = 0;
-            if (a.help && K >= kHelpMinTiles && K <= static_cast<uint32_t>(kHelpTiles)) {
+            if (a.help && help_phase(budget) && K >= kHelpMinTiles && K <= static_cast<uint32_t>(kHelpTiles)) {
                 hep++;
                 hs = kHsPub | K;
                 help_publish(a, lane, me, hep, cur, ct, hi, K, T);
@@ -3652,7 +3663,7 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         // 30.1 vs 38.0 ms); DESIGN.md §2.1d, profiles/r05/help_policy/.
         const bool helpers = g_test.help == 2 ||
                              (g_test.help == 0 &&
-                              (algo.avg >= (1ull << 20) ||
+                              (algo.avg >= KCDC_HELP_MIN_AVG ||
                                (algo.kind == kRabinKarp && s.nstreams < static_cast<uint64_t>(cus) * wg_waves)));
         unsigned grid = helpers || need >= cus ? cus : need;
         if (grid > dev::kMaxPipeGrid) grid = dev::kMaxPipeGrid;  // one claim flag per workgroup
