@@ -1061,7 +1061,10 @@ __device__ __forceinline__ bool help_phase(int64_t budget) {
 }
 constexpr int64_t kHelpSplit = 2;     // sub-tiles per help task (lane segments lane_cap / 2, >= 256 B)
 constexpr int kHelpTiles = 128;          // regions of up to 128 tiles take help (every registered name)
-constexpr uint32_t kHelpMinTiles = 3;    // the owner's tile, its next one, and at least one more
+#ifndef KCDC_HELP_MIN_TILES
+#define KCDC_HELP_MIN_TILES 3u
+#endif
+constexpr uint32_t kHelpMinTiles = KCDC_HELP_MIN_TILES;  // the owner's tile, its next one, and at least one more
 constexpr uint64_t kHelpWaitTicks = 20000;  // 200 us of s_memrealtime (a tile takes 15-40 us)
 __device__ __forceinline__ size_t help_params_off(uint32_t nw) { return 128ull * nw; }
 __device__ __forceinline__ size_t help_rows_off(uint32_t nw) { return 128ull * nw + 64ull * nw; }

@@ -224,3 +224,28 @@ def test_every_reserved_entry_is_written(gpu, name, lane_cap):
             got = batch.read_cuts(b)
             bad = [i for i in range(ns) if got[i].tolist() != want[i]]
             assert not bad, f"launch {launch}: {len(bad)} streams differ, first {bad[:5]}"
+
+
+@pytest.mark.parametrize("name,lane_cap", [("DYNAMIC-128K-BUZHASH", 256), ("DYNAMIC-128K-BUZHASH", 4096),
+                                           ("DYNAMIC-2M-BUZHASH", 256), ("DYNAMIC-2M-BUZHASH", 4096)])
+def test_forced_help_in_other_geometries(gpu, name, lane_cap):
+    """Help forced on in tile geometries the default rule never picks (KCDC_TEST_LANE_CAP): 16 KiB
+    tiles give 128K regions of ~8 tiles and 2M regions of ~190; 256 KiB tiles leave 128K regions
+    too short to publish.  Every stream exact and the ring balanced, launch after launch
+    (tools/geometry_sweep.py runs the full grid: profiles/r05/geometry_sweep/)."""
+    import torch
+    ns, L = 4096, 4 << 20
+    data = torch.empty(ns * L, dtype=torch.uint8, device=gpu)
+    batch.fill_prng(data, L, ns, L, SEED, 0)
+    b = batch.make_device_batch(name, [data.data_ptr() + i * L for i in range(ns)], [L] * ns, gpu)
+    cuts, counts = coracle.split_prng_streams(name, SEED, np.arange(ns), L, nthreads=16)
+    want = [cuts[i, :counts[i]].tolist() for i in range(ns)]
+    with knob(_lib.TEST_LANE_CAP, lane_cap), knob(_lib.TEST_NO_HELP, 2), knob(_lib.TEST_SPIN_CAP, 200000):
+        for launch in range(3):
+            batch.split_batch_device(name, b)
+            torch.cuda.synchronize()
+            tickets, entries, waves = _ring_balance()
+            assert waves - 1 <= tickets - entries <= waves, (launch, tickets, entries, waves)
+            got = batch.read_cuts(b)
+            bad = [i for i in range(ns) if got[i].tolist() != want[i]]
+            assert not bad, f"launch {launch}: {len(bad)} streams differ, first {bad[:5]}"
