@@ -230,8 +230,8 @@ def test_every_reserved_entry_is_written(gpu, name, lane_cap):
                                            ("DYNAMIC-2M-BUZHASH", 256), ("DYNAMIC-2M-BUZHASH", 4096)])
 def test_forced_help_in_other_geometries(gpu, name, lane_cap):
     """Help forced on in tile geometries the default rule never picks (KCDC_TEST_LANE_CAP): 16 KiB
-    tiles give 128K regions of ~8 tiles and 2M regions of ~190; 256 KiB tiles leave 128K regions
-    too short to publish.  Every stream exact and the ring balanced, launch after launch
+    tiles give 128K regions of ~8 tiles and 2M regions of up to ~190 (only those of <= 128 tiles
+    take help); 256 KiB tiles leave 128K regions too short to publish.  Every stream exact and the ring balanced, launch after launch
     (tools/geometry_sweep.py runs the full grid: profiles/r05/geometry_sweep/)."""
     import torch
     ns, L = 4096, 4 << 20
