@@ -1415,9 +1415,13 @@ __device__ __forceinline__ int64_t pipe_quantum(int64_t backlog, int64_t q = kPi
 // keep 6 x 128 KiB = 768 KiB (512 KiB there: 1.334 vs 1.286 ms); 128K and 256K get 512 KiB.  Against
 // the constant 768 KiB in one process (profiles/r04/third/ab_quantum_tiles_*.log): 128K 3.415 vs
 // 3.639 ms, 256K 2.697 vs 2.843, 4M 1.296 vs 1.309; all bit-exact.
+#ifndef KCDC_QUANTUM_TILES
+#define KCDC_QUANTUM_TILES 6
+#endif
 __device__ __forceinline__ int64_t pipe_quantum_tiles(int64_t backlog, uint32_t lane_cap) {
-    const int64_t q = 6 * kWave * static_cast<int64_t>(lane_cap);
-    return pipe_quantum(backlog, q < (512 << 10) ? (512 << 10) : q > (768 << 10) ? (768 << 10) : q);
+    constexpr int64_t kTiles = KCDC_QUANTUM_TILES, kMax = kTiles * kWave * 2048;  // (2 KiB lanes: 768 KiB)
+    const int64_t q = kTiles * kWave * static_cast<int64_t>(lane_cap);
+    return pipe_quantum(backlog, q < (512 << 10) ? (512 << 10) : q > kMax ? kMax : q);
 }
 
 template <bool TOP>
