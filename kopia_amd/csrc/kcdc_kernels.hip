@@ -1048,11 +1048,12 @@ __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
 #ifndef KCDC_HELP_GAP  // a region is open to helpers while top >= bottom + GAP (1 vs 2: 1.295 vs
 #define KCDC_HELP_GAP 1u  // 1.332 ms on config 2, same-process A/B, profiles/r04/third/)
 #endif
-// Publish only in visits that began with no stream waiting (budget kNoYield): only then can a
-// wave be waiting for a ticket, i.e. free to help (KCDC_HELP_TAIL_ONLY; 0 publishes every region).
 #ifndef KCDC_HELP_MIN_AVG  // launch_split_batch's help policy: averages from here up (1 MiB)
 #define KCDC_HELP_MIN_AVG (1ull << 20)
 #endif
+// KCDC_HELP_TAIL_ONLY: publish only in visits that began with no stream waiting (budget
+// kNoYield).  0 (the product) publishes every region: the tail-only variant lost 2-10 % at
+// 1M-4M (profiles/r05/help_tail_only/).
 #ifndef KCDC_HELP_TAIL_ONLY
 #define KCDC_HELP_TAIL_ONLY 0
 #endif
