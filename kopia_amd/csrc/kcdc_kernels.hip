@@ -1066,7 +1066,10 @@ constexpr int kHelpTiles = 128;          // regions of up to 128 tiles take help
 #define KCDC_HELP_MIN_TILES 3u
 #endif
 constexpr uint32_t kHelpMinTiles = KCDC_HELP_MIN_TILES;  // the owner's tile, its next one, and at least one more
-constexpr uint64_t kHelpWaitTicks = 20000;  // 200 us of s_memrealtime (a tile takes 15-40 us)
+#ifndef KCDC_HELP_WAIT_TICKS
+#define KCDC_HELP_WAIT_TICKS 20000
+#endif
+constexpr uint64_t kHelpWaitTicks = KCDC_HELP_WAIT_TICKS;  // 200 us of s_memrealtime (a tile takes 15-40 us)
 __device__ __forceinline__ size_t help_params_off(uint32_t nw) { return 128ull * nw; }
 __device__ __forceinline__ size_t help_rows_off(uint32_t nw) { return 128ull * nw + 64ull * nw; }
 __device__ __forceinline__ size_t help_bits_off(uint32_t nw) { return help_rows_off(nw) + 8ull * kHelpTiles * nw; }
