@@ -1051,14 +1051,11 @@ __device__ bool try_steal(const BatchArgs& a, int lane, uint32_t wg_waves) {
 #ifndef KCDC_HELP_MIN_AVG  // launch_split_batch's help policy: averages from here up (1 MiB)
 #define KCDC_HELP_MIN_AVG (1ull << 20)
 #endif
-// KCDC_HELP_TAIL_ONLY: publish only in visits that began with no stream waiting (budget
-// kNoYield).  0 (the product) publishes every region: the tail-only variant lost 2-10 % at
-// 1M-4M (profiles/r05/help_tail_only/).
-#ifndef KCDC_HELP_TAIL_ONLY
-#define KCDC_HELP_TAIL_ONLY 0
-#endif
+// Every region is published (a tail-only policy -- publish only in visits that began with no
+// stream waiting -- lost 2-10 % at 1M-4M; DESIGN.md §2.1, profiles/r05/help_tail_only/).
 __device__ __forceinline__ bool help_phase(int64_t budget) {
-    return !KCDC_HELP_TAIL_ONLY || budget > (int64_t(1) << 61);
+    (void)budget;
+    return true;
 }
 constexpr int64_t kHelpSplit = 2;     // sub-tiles per help task (lane segments lane_cap / 2, >= 256 B)
 constexpr int kHelpTiles = 128;          // regions of up to 128 tiles take help (every registered name)
@@ -1156,9 +1153,6 @@ __device__ __forceinline__ void help_post(const BatchArgs& a, int lane, uint32_t
 // The ticket a wave holds while it runs help tasks: kept in memory (word 2 of its help slot's
 // claim line) from the moment the help task is taken, and taken back from there when the task
 // ends, besides the copy in the task's cap field.  held_get audits the two (header words kQDiag..).
-#ifndef KCDC_HELP_MIRROR
-#define KCDC_HELP_MIRROR 1
-#endif
 __device__ __forceinline__ void held_put(const BatchArgs& a, int lane, uint32_t me, uint32_t t) {
     if (lane == 0)
         __hip_atomic_store((gu64*)(help_claim(a, me) + 2), 0x100000000ull | t, __ATOMIC_RELAXED,
@@ -1173,7 +1167,7 @@ __device__ __forceinline__ uint32_t held_get(const BatchArgs& a, int lane, uint3
             a.queue[kQDiag + 2] = t;
         }
     }
-    return KCDC_HELP_MIRROR ? t : reg;
+    return t;  // always memory's copy: the register copy is only audited
 }
 #ifndef KCDC_HELP_DIAG
 #define KCDC_HELP_DIAG 0
@@ -1890,25 +1884,12 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
 // the tables are stored bit-reversed at bit-reversed rows.  8.9 -> ~7.9 VALU per byte.
 // mod[] replicas: 16 = 2-way conflicts and a perm-addressed out[] (32 = conflict-free mod[] but a
 // 2-op out[] address: 3.01 vs 2.80 ms on config 2, issue-bound); out[] gets the rest of 96 KiB.
-#ifndef KCDC_RK_2BYTE
-#define KCDC_RK_2BYTE 0
-#endif
-#if KCDC_RK_2BYTE
-// Two-byte rolls (rk_step64 below): 16-byte entries, {mod, A} by the reduction index and
-// {outx, OX2} by the leaving byte; 128-byte mod rows (8 replicas) and 256-byte out rows (16), so
-// rk_mod_addr and rk_out address the first halves exactly as the one-byte layout does.
-constexpr int kRkModRep = 8;
-constexpr int kRkOutRep = 16;
-constexpr int kRkEntryWords = 2;
-#else
 constexpr int kRkModRep = 16;
 constexpr int kRkOutRep = 48 - kRkModRep;
-constexpr int kRkEntryWords = 1;
-#endif
 struct RkTables {
-    uint64_t mod[256 * kRkModRep * kRkEntryWords];  // row f (replicas at f*R + r): rev64(mod[rev8(f)]); first, so its
+    uint64_t mod[256 * kRkModRep];  // row f (replicas at f*R + r): rev64(mod[rev8(f)]); first, so its
                                                     // addresses fit the 16-bit ds offset
-    uint64_t out[256 * kRkOutRep * kRkEntryWords];  // row f: rev64(outx[rev8(f)]) (outx[] pre-shifted and pre-reduced)
+    uint64_t out[256 * kRkOutRep];  // row f: rev64(outx[rev8(f)]) (outx[] pre-shifted and pre-reduced)
 };
 static_assert(sizeof(RkTables) + sizeof(RkSlots) <= 160 * 1024, "Rabin-Karp tables + step slots exceed LDS");
 constexpr uint32_t kRkIdxBit = 11;  // the reduction index (v >> 45, bit-reversed) = lo bits 11..18
@@ -1933,14 +1914,29 @@ __device__ __forceinline__ void rk_read_step128(const uint8_t* slot, int lane, i
 __device__ __forceinline__ uint64_t rk_out(const RkCtx& k, uint32_t w, int b) {
     const int bb = 3 - b;
     uint32_t a;
-    static_assert(kRkOutRep * 8 * kRkEntryWords == 256, "out[]: 256-byte rows, the address in one v_perm");
+    static_assert(kRkOutRep * 8 == 256, "out[]: 256-byte rows, the address in one v_perm");
     a = __builtin_amdgcn_perm(w, k.lane8o, 0x0c0c0000u | ((4u + bb) << 8));  // row << 8 | lane8o
     return *reinterpret_cast<const uint64_t*>(k.outb + a);
 }
 // v << 8 | c, high word: [hi.b1, hi.b2, hi.b3, the entering byte (byte 3 - b of the reversed dword)]
 constexpr uint32_t rk_in_sel(int b) { return 0x00030201u | (static_cast<uint32_t>(7 - b) << 24); }
+// mod[] address (16 replicas, 128-byte rows): ((lo >> 4) & 0x7F80) | lane8m as v_lshrrev + one
+// v_bitop3 -- both issue every ~2.2-2.4 cycles at two waves per SIMD, where the v_bfe/v_lshl_or or
+// v_and_or pairs the compiler picks take ~4.3 each (tools/valu_rate.hip; round 6: the hot loop
+// alone 1.728 -> 1.586 ms, tools/rk_loop.hip).
 __device__ __forceinline__ uint32_t rk_mod_addr(const RkCtx& k, uint32_t lo) {
-    return (__builtin_amdgcn_ubfe(lo, kRkIdxBit, 8) << 7) | k.lane8m;  // 16 replicas, 128-byte rows
+    static_assert(kRkModRep == 16, "128-byte mod[] rows");
+    return __builtin_amdgcn_bitop3_b32(lo >> (kRkIdxBit - 7), 0xFFu << 7, k.lane8m, 0xEA);  // (x & m) | lane8m
+}
+// out[] address of the leaving byte b of a (bit-reversed) dword, as rk_out, by one SDWA v_mov that
+// writes the byte into byte 1 of `a` and keeps the rest: `a` holds lane8o in byte 0 for good.
+__device__ __forceinline__ uint32_t rk_out_sdwa(uint32_t& a, uint32_t w, int b) {
+    const int pos = 3 - b;
+    if (pos == 0) asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0" : "+v"(a) : "v"(w));
+    else if (pos == 1) asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1" : "+v"(a) : "v"(w));
+    else if (pos == 2) asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(a) : "v"(w));
+    else asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_3" : "+v"(a) : "v"(w));
+    return a;
 }
 // One roll with the leaving byte's out[] value already read: updates (hi, lo).
 // Linearity folds the leaving byte's removal into one table read that is off the chain:
@@ -1971,90 +1967,6 @@ __device__ __forceinline__ void rk_roll0(const RkCtx& k, uint32_t& hi, uint32_t&
 // not one latency + two rolls).  The outx[] reads of byte x + W follow each chain's mod[] read
 // (the in-order LDS return then never queues a chain's read behind a prefetch).
 // ACT_A/ACT_B: whether that chain's bytes are real (an idle chain is not rolled at all).
-#if KCDC_RK_2BYTE
-// Two bytes per chain step.  With c1, c2 entering and l1, l2 leaving, linearity gives
-//   v'' = (v << 16 | c1 << 8 | c2) ^ A[idx(v)] ^ mod[idx2(v)] ^ OX2[l1] ^ outx[l2]
-// (idx(v) = v's bits 45..52, idx2(v) = bits 37..44; every bit above 52 cancels, mod 2^64 too),
-// and the intermediate v' = (v << 8 | c1) ^ mod[idx(v)] ^ outx[l1] is needed only for the cut
-// test.  Both chain reads ({mod, A} at idx, mod at idx2) depend on v alone: one LDS latency per
-// two bytes instead of two.
-__device__ __forceinline__ uint32_t rk_out_addr(const RkCtx& k, uint32_t w, int b) {
-    return __builtin_amdgcn_perm(w, k.lane8o, 0x0c0c0000u | ((4u + static_cast<uint32_t>(3 - b)) << 8));
-}
-__device__ __forceinline__ uint32_t rk_mod2_addr(const RkCtx& k, uint32_t lo) {
-    return (__builtin_amdgcn_ubfe(lo, kRkIdxBit + 8, 8) << 7) | k.lane8m;
-}
-// v << 16 | c1 << 8 | c2, high word: [hi.b2, hi.b3, c1, c2] (bytes b, b + 1 of the reversed dword)
-constexpr uint32_t rk_in_sel2(int b) {
-    return 0x00000302u | (static_cast<uint32_t>(7 - b) << 16) | (static_cast<uint32_t>(6 - b) << 24);
-}
-template <bool ACT_A, bool ACT_B>
-__device__ __forceinline__ void rk_step64(const RkCtx& k, uint32_t& ha, uint32_t& la, const uint32_t (&a)[16],
-                                          const uint32_t (&pa)[16], uint32_t& hb, uint32_t& lb,
-                                          const uint32_t (&b)[16], const uint32_t (&pb)[16], uint32_t& ma,
-                                          uint32_t& mb) {
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    auto ld128 = [](const char* p) { return *reinterpret_cast<const v4u*>(p); };
-    auto ld64 = [](const char* p) { return *reinterpret_cast<const uint64_t*>(p); };
-    v4u qA = {0, 0, 0, 0}, qB = {0, 0, 0, 0}, eA[32], eB[32];  // (unrolled: one pair live at a time)
-    uint64_t rA = 0, rB = 0, fA[32], fB[32];
-    if (ACT_A) {
-        qA = ld128(k.modb + rk_mod_addr(k, la));
-        rA = ld64(k.modb + rk_mod2_addr(k, la));
-        eA[0] = ld128(k.outb + rk_out_addr(k, pa[0], 0));
-        fA[0] = ld64(k.outb + rk_out_addr(k, pa[0], 1));
-    }
-    if (ACT_B) {
-        qB = ld128(k.modb + rk_mod_addr(k, lb));
-        rB = ld64(k.modb + rk_mod2_addr(k, lb));
-        eB[0] = ld128(k.outb + rk_out_addr(k, pb[0], 0));
-        fB[0] = ld64(k.outb + rk_out_addr(k, pb[0], 1));
-    }
-#pragma unroll
-    for (int p = 0; p < 32; p++) {
-        const int x = 2 * p, bi = x & 3;
-        __builtin_amdgcn_sched_barrier(0);
-        if (ACT_A) {
-            const uint32_t w = a[x >> 2];
-            const uint32_t h1 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(w, ha, rk_in_sel(bi)), qA.y, eA[p].y, 0x96);
-            const uint32_t th = __builtin_amdgcn_perm(w, ha, rk_in_sel2(bi));
-            const uint32_t tl = __builtin_amdgcn_alignbit(ha, la, 16);
-            const uint32_t nh = __builtin_amdgcn_bitop3_b32(th, qA.w, static_cast<uint32_t>(rA >> 32), 0x96);
-            const uint32_t nl = __builtin_amdgcn_bitop3_b32(tl, qA.z, static_cast<uint32_t>(rA), 0x96);
-            ha = __builtin_amdgcn_bitop3_b32(nh, eA[p].w, static_cast<uint32_t>(fA[p] >> 32), 0x96);
-            la = __builtin_amdgcn_bitop3_b32(nl, eA[p].z, static_cast<uint32_t>(fA[p]), 0x96);
-            __builtin_amdgcn_sched_barrier(0);
-            if (p + 1 < 32) {
-                qA = ld128(k.modb + rk_mod_addr(k, la));
-                rA = ld64(k.modb + rk_mod2_addr(k, la));
-                eA[p + 1] = ld128(k.outb + rk_out_addr(k, pa[(x + 2) >> 2], (x + 2) & 3));
-                fA[p + 1] = ld64(k.outb + rk_out_addr(k, pa[(x + 3) >> 2], (x + 3) & 3));
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            asm("v_min3_u32 %0, %1, %2, %3" : "=v"(ma) : "v"(ma), "v"(h1), "v"(ha));
-        }
-        if (ACT_B) {
-            const uint32_t w = b[x >> 2];
-            const uint32_t h1 = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(w, hb, rk_in_sel(bi)), qB.y, eB[p].y, 0x96);
-            const uint32_t th = __builtin_amdgcn_perm(w, hb, rk_in_sel2(bi));
-            const uint32_t tl = __builtin_amdgcn_alignbit(hb, lb, 16);
-            const uint32_t nh = __builtin_amdgcn_bitop3_b32(th, qB.w, static_cast<uint32_t>(rB >> 32), 0x96);
-            const uint32_t nl = __builtin_amdgcn_bitop3_b32(tl, qB.z, static_cast<uint32_t>(rB), 0x96);
-            hb = __builtin_amdgcn_bitop3_b32(nh, eB[p].w, static_cast<uint32_t>(fB[p] >> 32), 0x96);
-            lb = __builtin_amdgcn_bitop3_b32(nl, eB[p].z, static_cast<uint32_t>(fB[p]), 0x96);
-            __builtin_amdgcn_sched_barrier(0);
-            if (p + 1 < 32) {
-                qB = ld128(k.modb + rk_mod_addr(k, lb));
-                rB = ld64(k.modb + rk_mod2_addr(k, lb));
-                eB[p + 1] = ld128(k.outb + rk_out_addr(k, pb[(x + 2) >> 2], (x + 2) & 3));
-                fB[p + 1] = ld64(k.outb + rk_out_addr(k, pb[(x + 3) >> 2], (x + 3) & 3));
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            asm("v_min3_u32 %0, %1, %2, %3" : "=v"(mb) : "v"(mb), "v"(h1), "v"(hb));
-        }
-    }
-}
-#else
 template <bool ACT_A, bool ACT_B>
 __device__ __forceinline__ void rk_step64(const RkCtx& k, uint32_t& ha, uint32_t& la, const uint32_t (&a)[16],
                                           const uint32_t (&pa)[16], uint32_t& hb, uint32_t& lb,
@@ -2062,15 +1974,21 @@ __device__ __forceinline__ void rk_step64(const RkCtx& k, uint32_t& ha, uint32_t
                                           uint32_t& mb) {
     constexpr int W = 2;  // outx[] reads of both chains issued this many bytes ahead (2: 2.58 ms, 4: 2.65)
     uint64_t oa[64], ob[64];  // only W live at a time (unrolled: register renaming)
+    uint32_t xa[W], xb[W];    // out[] address registers (rk_out_sdwa), one per read in flight
+#pragma unroll
+    for (int i = 0; i < W; i++) xa[i] = xb[i] = k.lane8o;
+    auto ld_out = [&](uint32_t& x, uint32_t w, int b) {
+        return *reinterpret_cast<const uint64_t*>(k.outb + rk_out_sdwa(x, w, b));
+    };
     uint64_t mA = 0, mB = 0;
     if (ACT_A) mA = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, la));
 #pragma unroll
     for (int i = 0; i < W; i++)
-        if (ACT_A) oa[i] = rk_out(k, pa[i >> 2], i & 3);
+        if (ACT_A) oa[i] = ld_out(xa[i], pa[i >> 2], i & 3);
     if (ACT_B) mB = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, lb));
 #pragma unroll
     for (int i = 0; i < W; i++)
-        if (ACT_B) ob[i] = rk_out(k, pb[i >> 2], i & 3);
+        if (ACT_B) ob[i] = ld_out(xb[i], pb[i >> 2], i & 3);
     uint32_t pha = 0xFFFFFFFFu, phb = 0xFFFFFFFFu;  // the previous byte's hi (tested in pairs)
 #pragma unroll
     for (int x = 0; x < 64; x++) {
@@ -2082,7 +2000,7 @@ __device__ __forceinline__ void rk_step64(const RkCtx& k, uint32_t& ha, uint32_t
             la = __builtin_amdgcn_bitop3_b32(tl, static_cast<uint32_t>(mA), static_cast<uint32_t>(oa[x]), 0x96);
             __builtin_amdgcn_sched_barrier(0);
             if (x + 1 < 64) mA = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, la));
-            if (x + W < 64) oa[x + W] = rk_out(k, pa[(x + W) >> 2], (x + W) & 3);
+            if (x + W < 64) oa[x + W] = ld_out(xa[(x + W) % W], pa[(x + W) >> 2], (x + W) & 3);
             __builtin_amdgcn_sched_barrier(0);
             if (x & 1) asm("v_min3_u32 %0, %1, %2, %3" : "=v"(ma) : "v"(ma), "v"(pha), "v"(ha));  // one op per two bytes
             else pha = ha;
@@ -2094,7 +2012,7 @@ __device__ __forceinline__ void rk_step64(const RkCtx& k, uint32_t& ha, uint32_t
             lb = __builtin_amdgcn_bitop3_b32(tl, static_cast<uint32_t>(mB), static_cast<uint32_t>(ob[x]), 0x96);
             __builtin_amdgcn_sched_barrier(0);
             if (x + 1 < 64) mB = *reinterpret_cast<const uint64_t*>(k.modb + rk_mod_addr(k, lb));
-            if (x + W < 64) ob[x + W] = rk_out(k, pb[(x + W) >> 2], (x + W) & 3);
+            if (x + W < 64) ob[x + W] = ld_out(xb[(x + W) % W], pb[(x + W) >> 2], (x + W) & 3);
             __builtin_amdgcn_sched_barrier(0);
             if (x & 1) asm("v_min3_u32 %0, %1, %2, %3" : "=v"(mb) : "v"(mb), "v"(phb), "v"(hb));
             else phb = hb;
@@ -2102,7 +2020,6 @@ __device__ __forceinline__ void rk_step64(const RkCtx& k, uint32_t& ha, uint32_t
     }
 }
 
-#endif
 // Exact re-run of one chain's 64 bytes from (hi, lo) (rare): first index in [lo_i, hi_i]
 // that is a candidate, else 64.
 __device__ uint32_t rk_exact64(const RkCtx& k, uint32_t hi, uint32_t lo, const uint32_t (&in)[16],
@@ -2152,33 +2069,18 @@ __device__ __forceinline__ void rk_warm(const RkCtx& kx, const uint32_t (&dw)[32
 }
 __device__ __forceinline__ RkCtx rk_setup(RkTables& smt, const BatchArgs& a, int lane) {
     auto rev8 = [](uint32_t f) { return __builtin_bitreverse32(f) >> 24; };
-#if KCDC_RK_2BYTE
-    // A[j] = (mod[j] << 8) ^ mod[idx(mod[j])], OX2[l] = (outx[l] << 8) ^ mod[idx(outx[l])] (rk_step64)
-    auto red = [&](uint64_t x) { return (x << 8) ^ a.rk_mod[(x >> 45) & 0xFFu]; };
-    for (uint32_t i = threadIdx.x; i < 256u * kRkModRep; i += blockDim.x) {
-        const uint64_t m = a.rk_mod[rev8(i / kRkModRep)];
-        smt.mod[2 * i] = __builtin_bitreverse64(m);
-        smt.mod[2 * i + 1] = __builtin_bitreverse64(red(m));
-    }
-    for (uint32_t i = threadIdx.x; i < 256u * kRkOutRep; i += blockDim.x) {
-        const uint64_t ox = red(a.rk_out[rev8(i / kRkOutRep)]);
-        smt.out[2 * i] = __builtin_bitreverse64(ox);
-        smt.out[2 * i + 1] = __builtin_bitreverse64(red(ox));
-    }
-#else
     for (uint32_t i = threadIdx.x; i < 256u * kRkModRep; i += blockDim.x)
         smt.mod[i] = __builtin_bitreverse64(a.rk_mod[rev8(i / kRkModRep)]);
     for (uint32_t i = threadIdx.x; i < 256u * kRkOutRep; i += blockDim.x) {  // outx[] (rk_roll)
         const uint64_t o = a.rk_out[rev8(i / kRkOutRep)];
         smt.out[i] = __builtin_bitreverse64((o << 8) ^ a.rk_mod[(o >> 45) & 0xFFu]);
     }
-#endif
     __syncthreads();
     RkCtx kx;
     kx.modb = reinterpret_cast<const char*>(smt.mod);
     kx.outb = reinterpret_cast<const char*>(smt.out);
-    kx.lane8o = static_cast<uint32_t>(lane & (kRkOutRep - 1)) * 8u * kRkEntryWords;
-    kx.lane8m = static_cast<uint32_t>(lane & (kRkModRep - 1)) * 8u * kRkEntryWords;
+    kx.lane8o = static_cast<uint32_t>(lane & (kRkOutRep - 1)) * 8u;
+    kx.lane8m = static_cast<uint32_t>(lane & (kRkModRep - 1)) * 8u;
     kx.thr = 1u << (32 - __builtin_popcount(a.mask));  // mask = avg - 1, avg a power of two in [2, 2^31]
     return kx;
 }

@@ -27,11 +27,23 @@
     X(10, "v_lshl_add_u32 %0, %0, 2, %1")                        \
     X(11, "v_mov_b32 %0, %1")                                    \
     X(12, "v_fma_f32 %0, %0, %1, %2")                            \
-    X(13, "v_lshrrev_b32 %0, 8, %0")
+    X(13, "v_lshrrev_b32 %0, 8, %0")                              \
+    X(14, "v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2") \
+    X(15, "v_xor_b32_sdwa %0, %1, %0 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1 src1_sel:BYTE_3") \
+    X(16, "v_and_or_b32 %0, %0, %1, %2")                         \
+    X(17, "v_min_u32 %0, %0, %1")                                \
+    X(18, "v_or3_b32 %0, %0, %1, %2")                            \
+    X(19, "v_xor_b32_sdwa %0, %1, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD") \
+    X(20, "v_bfrev_b32 %0, %0")                                  \
+    X(21, "v_lshlrev_b32 %0, %1, %0")                            \
+    X(22, "v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PAD src0_sel:BYTE_2") \
+    X(23, "v_lshrrev_b32 %0, %1, %0")
 
 static const char* kNames[] = {"v_xor_b32",  "v_and_b32",   "v_add_u32",  "v_lshlrev_b32", "v_lshl_or_b32",
                                "v_min3_u32", "v_perm_b32",  "v_bitop3_b32", "v_alignbit_b32", "v_bfe_u32",
-                               "v_lshl_add_u32", "v_mov_b32",   "v_fma_f32",  "v_lshrrev_b32"};
+                               "v_lshl_add_u32", "v_mov_b32",   "v_fma_f32",  "v_lshrrev_b32",
+                               "v_mov_sdwa_pres", "v_xor_sdwa_pres", "v_and_or_b32", "v_min_u32", "v_or3_b32",
+                               "v_xor_sdwa_src", "v_bfrev_b32", "v_lshlrev_reg", "v_mov_sdwa_pad", "v_lshrrev_reg"};
 
 template <int KIND>
 __device__ __forceinline__ void step(uint32_t& a, uint32_t b, uint32_t c) {
@@ -296,5 +308,5 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
-    return run_all(p.multiProcessorCount, out, cyc, std::make_integer_sequence<int, 14>{});
+    return run_all(p.multiProcessorCount, out, cyc, std::make_integer_sequence<int, 24>{});
 }
