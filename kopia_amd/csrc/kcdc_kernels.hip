@@ -2148,10 +2148,23 @@ __device__ __forceinline__ void rk_mask_head(uint32_t (&dw)[16], int64_t c, int6
 // state before, bytes, history) after each chain's 64 bytes.  Coordinates stay out of the
 // walk (64-bit per-lane values live across it spilled, and every reload's vmcnt wait drained
 // the line DMA): `head` says whether lane 0's chain A starts at coordinate 0.
+// KCDC_TRACE builds time every line fill's DMA wait (s_memtime, shader cycles) into `dmaw`.
+#if KCDC_TRACE
+#define RK_VMWAIT(acc)                                                  \
+    do {                                                                \
+        const uint64_t t0_ = __builtin_amdgcn_s_memtime();              \
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                \
+        acc += __builtin_amdgcn_s_memtime() - t0_;                      \
+    } while (0)
+#else
+#define RK_VMWAIT(acc) asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#endif
 template <class Refill, class Check>
 __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int lane, bool head,
                                         int64_t off0, int K, uint32_t& ha, uint32_t& la, uint32_t& hb, uint32_t& lb,
-                                        uint32_t (&pa)[16], uint32_t (&pb)[16], Refill&& refill, Check&& check) {
+                                        uint32_t (&pa)[16], uint32_t (&pb)[16], Refill&& refill, Check&& check,
+                                        uint64_t& dmaw) {
+    (void)dmaw;
     uint32_t bf[16];  // the second half of the line that arrived last step
 #pragma unroll
     for (int i = 0; i < 16; i++) bf[i] = 0;
@@ -2160,7 +2173,7 @@ __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int 
         {
             uint32_t dw[32], na[16];
             __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            RK_VMWAIT(dmaw);
             rk_read_step128(sl, lane, head && j == 0 ? 0 : 1, off0, dw);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
@@ -2189,7 +2202,7 @@ __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int 
         {
             uint32_t dw[32], nb[16];
             __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            RK_VMWAIT(dmaw);
             rk_read_step128(sl, lane, 1, off0, dw);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
@@ -2237,6 +2250,31 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
     const uint32_t me = blockIdx.x * kRkWaves + wave;  // this wave's help slot
     const int64_t rk_cap = kRkLaneMul * static_cast<int64_t>(a.lane_cap);  // lane bytes of an own tile (>= 512)
 
+#if KCDC_TRACE  // per wave at trace[8 * global wave]: start, end, ticks in blocking takes, the last take's
+                // start (s_memrealtime); help tiles | own tiles << 32; shader cycles in line-fill DMA
+                // waits, in the walks, in the warm fills (s_memtime)
+    const uint32_t gw = blockIdx.x * kRkWaves + wave;
+    uint64_t tr_block = 0, tr_last = 0, tr_tiles = 0, tr_dma = 0, tr_walk = 0, tr_warm = 0;
+    const uint64_t tr_mt0 = __builtin_amdgcn_s_memtime();  // span in shader cycles after the records
+    if (lane == 0) a.trace[8 * gw] = __builtin_amdgcn_s_memrealtime();
+#define KCDC_RKRET                                                                \
+    do {                                                                          \
+        if (lane == 0) {                                                          \
+            a.trace[8 * gw + 1] = __builtin_amdgcn_s_memrealtime();                \
+            a.trace[8 * gw + 2] = tr_block;                                       \
+            a.trace[8 * gw + 3] = tr_last;                                        \
+            a.trace[8 * gw + 4] = tr_tiles;                                       \
+            a.trace[8 * gw + 5] = tr_dma;                                         \
+            a.trace[8 * gw + 6] = tr_walk;                                        \
+            a.trace[8 * gw + 7] = tr_warm;                                        \
+            a.trace[8ull * gridDim.x * kRkWaves + gw] = __builtin_amdgcn_s_memtime() - tr_mt0; \
+        }                                                                         \
+        return;                                                                   \
+    } while (0)
+#else
+    uint64_t tr_dma = 0;
+#define KCDC_RKRET return
+#endif
     PStream cur;
     int64_t budget = kNoYield;
     uint32_t hep = 0, hs = 0;
@@ -2245,6 +2283,14 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
     auto hK = [&] { return hs & 0xFFu; };
     auto htile = [&] { return (hs >> 8) & 0xFFu; };
     auto take_blocking = [&](uint32_t t, int64_t backlog_hint, uint32_t claim) -> bool {
+#if KCDC_TRACE
+        const uint64_t tb0 = __builtin_amdgcn_s_memrealtime();
+        tr_last = tb0;
+        struct Acc {
+            uint64_t t0, &sum;
+            __device__ ~Acc() { sum += __builtin_amdgcn_s_memrealtime() - t0; }
+        } acc{tb0, tr_block};
+#endif
         for (;;) {
             int64_t backlog = backlog_hint;
             if (t == 0xFFFFFFFFu) {
@@ -2300,7 +2346,7 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
         diag_record(a, lane, divergent_bit(need_take, 0) | divergent_bit(take_t, 1) | divergent_bit(issued, 2));
 #endif
         if (need_take) {
-            if (!take_blocking(take_t, take_backlog, take_claim)) return;
+            if (!take_blocking(take_t, take_backlog, take_claim)) KCDC_RKRET;
             need_take = false;
             issued = false;
             hs |= kHsNeedPub;
@@ -2312,8 +2358,12 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
                                  divergent_bit(static_cast<uint32_t>(budget), 8));
 #endif
         uniformize(cur);
-        if (!pcheck(a, lane, cur, 0xFFFFFFFFu, 5)) return;
+        if (!pcheck(a, lane, cur, 0xFFFFFFFFu, 5)) KCDC_RKRET;
         const bool is_help = (cur.sid & kHelpBit) != 0;
+#if KCDC_TRACE
+        tr_tiles += is_help ? 1ull : (1ull << 32);
+        const uint64_t tr_t0 = __builtin_amdgcn_s_memtime();
+#endif
         int64_t lo, hi;
         pregion(a, cur, lo, hi);
         const int64_t lcap = is_help ? rk_cap / 2 : rk_cap;
@@ -2362,6 +2412,10 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             __builtin_amdgcn_sched_barrier(0);
             rk_warm(kx, dw, ha, la, hb, lb, pa, pb);
         }
+#if KCDC_TRACE
+        const uint64_t tr_t1 = __builtin_amdgcn_s_memtime();
+        tr_warm += tr_t1 - tr_t0;
+#endif
         uint32_t tk = 0;
         int64_t nbacklog = 0;
         if (switching) {
@@ -2430,7 +2484,10 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
                 }
             }
         };
-        rk_walk(kx, sl, lane, ct == 0 && lane == 0, cur.off0, g.K, ha, la, hb, lb, pa, pb, refill, check);
+        rk_walk(kx, sl, lane, ct == 0 && lane == 0, cur.off0, g.K, ha, la, hb, lb, pa, pb, refill, check, tr_dma);
+#if KCDC_TRACE
+        tr_walk += __builtin_amdgcn_s_memtime() - tr_t1;
+#endif
         const int64_t c0 = ct + lane * g.L;
         const int64_t found = found_a >= 0 ? c0 + found_a : found_b >= 0 ? c0 + g.L / 2 + found_b : -1;
         // ---- end of tile
@@ -2532,7 +2589,7 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
                 PStream nx;
                 pentry_decode(nx, ev);
                 uniformize(nx);
-                if (!pcheck(a, lane, nx, tk, 2)) return;
+                if (!pcheck(a, lane, nx, tk, 2)) KCDC_RKRET;
                 cur = nx;
                 budget = pipe_quantum(nbacklog);
                 took = true;
@@ -3000,7 +3057,8 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void cand_scan_rk_k
                 }
             }
         };
-        rk_walk(kx, sl, lane, q.cs == 0 && lane == 0, q.off0, t.K, ha, la, hb, lb, pa, pb, refill, check);
+        uint64_t dmaw = 0;
+        rk_walk(kx, sl, lane, q.cs == 0 && lane == 0, q.off0, t.K, ha, la, hb, lb, pa, pb, refill, check, dmaw);
         const int64_t c0 = q.cs + lane * t.L, c0b = c0 + t.L / 2;
         // this lane's candidates in position order: chain A's, then chain B's
         const int nas = na < kSegK ? na : kSegK;
