@@ -29,6 +29,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -240,6 +241,14 @@ struct BwDev {
     std::atomic<uint32_t> capped{0};   // writers blocked on their staging cap (a round is due)
     std::atomic<uint32_t> finish_pending{0};  // finishing writers whose last region is not issued
     uint64_t rounds = 0;
+    // (mu) the round thread holds writer pointers outside mu: a round being collected and issued,
+    // or id_create reading arenas.  kcdc_bw_free of a writer that may still be in such a round (its
+    // last round did not complete: an error) waits until this is 0 before it frees the writer.
+    int writer_refs = 0;
+    void unref_writers() {  // mu held
+        writer_refs--;
+        cv_done.notify_all();
+    }
     bool stop = false;
     std::atomic<int> error{0};
     std::string errmsg;
@@ -311,8 +320,8 @@ struct BwDev {
     HashChain* d_chains = nullptr;
     HashChain* h_chains = nullptr;     // pinned: new chains' records, by slot (round thread writes, hash thread uploads)
     uint32_t chain_cap = 0;
-    // monotonic chain numbers (mu): [chain_tail, chain_head) published, [.., uploaded) uploaded
-    uint64_t chain_head = 0, chain_tail = 0, uploaded = 0;
+    // monotonic chain numbers (mu): [chain_tail, chain_head) published
+    uint64_t chain_head = 0, chain_tail = 0;
     uint64_t undone = 0;               // (mu) published chains with blocks not yet issued
     std::deque<Chain> chains;          // chains [chain_tail, chain_head)
     uint8_t* d_dig = nullptr;
@@ -345,6 +354,7 @@ struct BwDev {
     bool hstop = false;                // (mu) the round thread has published its last chains
     std::thread hth;
     int ids_enable(const char* name, const uint8_t* key, uint32_t key_len);
+    void ids_disable();                // undo ids_enable (no writer has opened yet)
     int id_create();                   // round thread, mu not held: newc -> chains (ring copies)
     int id_issue(Step& st, bool& issued);  // hash thread, mu not held
     int id_deliver(Step& st);          // hash thread, mu not held
@@ -424,17 +434,25 @@ struct BwDev {
     void loop();
 };
 
+// The batcher's lifetime state, shared by the batcher and every writer it opened (refcounted): a
+// writer call that starts while or after kcdc_bw_batcher_free runs sees `closing` here -- memory
+// that outlives the batcher -- and returns KCDC_EINVAL without touching the freed device state.
+struct BwCtl {
+    std::atomic<int> inside{0};        // threads inside a writer call (batcher_free waits for them)
+    std::atomic<bool> closing{false};  // kcdc_bw_batcher_free has started
+    std::atomic<bool> detached{false}; // ... and has detached every open writer (w->b = null)
+};
+
 struct kcdc_bw_batcher {
     const Algo* algo = nullptr;
     std::vector<BwDev*> devs;
     std::mutex mu;                   // writer assignment
-    std::atomic<int> inside{0};      // threads inside a writer call (batcher_free waits for them)
-    std::atomic<bool> closing{false};
+    std::shared_ptr<BwCtl> ctl = std::make_shared<BwCtl>();
 };
 
 struct kcdc_bw {
     BwDev* b = nullptr;              // the device batcher this writer ships through (null once freed)
-    kcdc_bw_batcher* top = nullptr;
+    std::shared_ptr<BwCtl> ctl;      // the batcher's lifetime state (outlives the batcher)
     int device = 0;                  // HIP device of the arenas
     uint64_t hint = 0;               // expected object size (0: unknown)
     uint64_t counted = 0;            // this writer's share of b->load
@@ -524,6 +542,9 @@ void BwDev::loop() {
         const auto l0 = std::chrono::steady_clock::now();
         std::lock_guard<std::mutex> lk(mu);
         t_lock += std::chrono::duration<double>(std::chrono::steady_clock::now() - l0).count();
+        // after an error a writer of this round may already be freed (kcdc_bw_free does not wait
+        // for rounds then): touch none of them
+        if (error) return error;
         shipped_bytes += r.fresh;
         for (uint32_t k = 0; k < n; k++) {
             Job& j = r.jobs[k];
@@ -619,6 +640,7 @@ void BwDev::loop() {
         recycle(inflight);
         // ---- collect round R: every writer's staged bytes (writers keep writing meanwhile)
         const auto t0 = std::chrono::steady_clock::now();
+        writer_refs++;  // until R is issued (unref_writers below)
         Round R;
         R.m = next_meta;
         struct Move {
@@ -811,12 +833,14 @@ void BwDev::loop() {
         if (rc != KCDC_OK) {
             fail(rc);
             lk.lock();
+            unref_writers();
             break;
         }
         R.live = true;
         inflight = std::move(R);
         next_meta ^= 1;
         lk.lock();
+        unref_writers();
     }
     lk.unlock();
     if (inflight.live && !error) {
@@ -898,6 +922,41 @@ int BwDev::ids_enable(const char* name, const uint8_t* key, uint32_t key_len) {
     return KCDC_OK;
 }
 
+// Undo ids_enable on a device whose batcher could not enable content IDs on every device (no writer
+// has opened, so no chain exists): stop the hash thread, free what ids_enable allocated.
+void BwDev::ids_disable() {
+    if (hth.joinable()) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            hstop = true;
+        }
+        cv_hash.notify_all();
+        hth.join();
+    }
+    Guard g(device);
+    for (hipEvent_t* ev : {&compacted_ev, &copy_ev})
+        if (*ev) (void)hipEventDestroy(*ev), *ev = nullptr;
+    for (hipEvent_t& ev : pub_ev)
+        if (ev) (void)hipEventDestroy(ev), ev = nullptr;
+    for (Step& st : steps) {
+        for (hipEvent_t* ev : {&st.t0, &st.ev})
+            if (*ev) (void)hipEventDestroy(*ev), *ev = nullptr;
+        for (void** p : {reinterpret_cast<void**>(&st.h_dig), reinterpret_cast<void**>(&st.h_act),
+                         reinterpret_cast<void**>(&st.h_ol)})
+            if (*p) (void)hipHostFree(*p), *p = nullptr;
+    }
+    for (void** p : {reinterpret_cast<void**>(&h_rp), reinterpret_cast<void**>(&h_chains)})
+        if (*p) (void)hipHostFree(*p), *p = nullptr;
+    for (void** p : {reinterpret_cast<void**>(&d_rp), reinterpret_cast<void**>(&ring), reinterpret_cast<void**>(&d_chains),
+                     reinterpret_cast<void**>(&d_dig), reinterpret_cast<void**>(&d_act), reinterpret_cast<void**>(&d_ol)})
+        if (*p) (void)hipFree(*p), *p = nullptr;
+    for (hipStream_t* st : {&hstream, &idcopy})
+        if (*st) (void)hipStreamDestroy(*st), *st = nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    ids = IdCfg{};
+    hstop = false;
+}
+
 // The last completed round's final chunks (newc) become chains: ring space and a slot each, a
 // copy from the writer's arena into the ring, then (after an event on the copy stream) the chain
 // is published to the hash thread.  Called right after complete(): the arena pointers are those of
@@ -905,7 +964,24 @@ int BwDev::ids_enable(const char* name, const uint8_t* key, uint32_t key_len) {
 // (compacted_ev); any later compaction waits for the copies (copy_ev).  When the ring is full it publishes what it has copied and waits for the
 // hash thread to free space.
 int BwDev::id_create() {
-    if (newc.empty()) return KCDC_OK;
+    std::vector<NewChunk> work;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (error) {  // a writer of these chunks may already be freed (kcdc_bw_free after an error)
+            newc.clear();
+            return error;
+        }
+        if (newc.empty()) return KCDC_OK;
+        work.swap(newc);
+        writer_refs++;  // the arenas read below stay allocated until this returns
+    }
+    struct Unref {
+        BwDev* b;
+        ~Unref() {
+            std::lock_guard<std::mutex> lk(b->mu);
+            b->unref_writers();
+        }
+    } unref{this};
     Guard g(device);
     {
         const hipError_t e = hipStreamWaitEvent(idcopy, compacted_ev, 0);
@@ -919,6 +995,11 @@ int BwDev::id_create() {
         uint64_t seq;
         {
             std::lock_guard<std::mutex> lk(mu);
+            if (error) {  // no copies for chains that will never be named
+                made.clear();
+                pcs.clear();
+                return error;
+            }
             seq = pub_seq;
         }
         // the slot of publish seq - kPubEv (event, pinned pieces) must be complete before reuse
@@ -956,7 +1037,7 @@ int BwDev::id_create() {
         cv_hash.notify_one();
         return KCDC_OK;
     };
-    for (const NewChunk& nc : newc) {
+    for (const NewChunk& nc : work) {
         const uint64_t need = (nc.len + 15) & ~uint64_t(15);
         if (need > ring_cap) return set_error(KCDC_EIO, "writer content IDs: chunk larger than the ID ring");
         const uint8_t* src = nc.w->arena + (nc.pos - nc.w->origin);
@@ -969,6 +1050,11 @@ int BwDev::id_create() {
             {
                 std::unique_lock<std::mutex> lk(mu);
                 if (error) return error;
+                if (chain_tail == chain_head && made.empty()) {
+                    // the ring is empty: restart at a ring boundary, so a chunk larger than what is
+                    // left before the wrap does not wait for space nothing will free
+                    ring_head = ring_tail = (ring_head + ring_cap - 1) / ring_cap * ring_cap;
+                }
                 at = ring_head;  // (a multiple of 16)
                 if (at % ring_cap + need > ring_cap) at += ring_cap - at % ring_cap;  // no chunk wraps
                 if (at + need - ring_tail <= ring_cap && chain_head + made.size() - chain_tail < chain_cap) break;
@@ -1002,7 +1088,6 @@ int BwDev::id_create() {
         made.push_back(Chain{nc.w, nc.wseq, at, at + need, nc.len, nblk, 0, false});
         ring_head = at + need;
     }
-    newc.clear();
     return publish();
 }
 
@@ -1010,14 +1095,11 @@ int BwDev::id_create() {
 int BwDev::id_issue(Step& st, bool& issued) {
     issued = false;
     uint32_t n = 0;
-    uint64_t up0 = 0, up1 = 0;
     st.done.clear();
     {
         std::lock_guard<std::mutex> lk(mu);
         if (undone == 0) return KCDC_OK;
         while (pub_done < pub_seq && hipEventQuery(pub_ev[pub_done % kPubEv]) == hipSuccess) pub_done++;
-        up0 = uploaded;
-        up1 = chain_head;
         for (uint64_t k = 0; k < chains.size(); k++) {
             Chain& c = chains[k];
             if (c.fin || c.done >= c.nblk) continue;
@@ -1037,19 +1119,11 @@ int BwDev::id_issue(Step& st, bool& issued) {
             n++;
         }
         chain_steps += n;
-        if (n && ids.kind == 3) uploaded = up1;  // (a step that issues nothing uploads nothing either)
     }
     if (n == 0) return KCDC_OK;
-    // kind 3: the new chains' records (their ring copies are done: see pub_done); the BLAKE2 kinds
-    // read them, the active list and their digests through host-mapped memory (one launch, no copies)
-    hipError_t e = hipSuccess;
-    for (uint64_t c0 = up0; ids.kind == 3 && e == hipSuccess && c0 < up1;) {  // slots [up0, up1) mod cap
-        const uint32_t s0 = static_cast<uint32_t>(c0 % chain_cap);
-        const uint64_t run = std::min<uint64_t>(up1 - c0, chain_cap - s0);
-        e = hipMemcpyAsync(d_chains + s0, h_chains + s0, run * sizeof(HashChain), hipMemcpyHostToDevice, hstream);
-        c0 += run;
-    }
-    if (e == hipSuccess) e = hipEventRecord(st.t0, hstream);
+    // the BLAKE2 kinds read new chains' records, the active list and their digests through
+    // host-mapped memory (one launch, no copies); kind 3 hashes whole chunks from the step's list
+    hipError_t e = hipEventRecord(st.t0, hstream);
     if (e != hipSuccess) return hip_err(e, "writer content IDs: chain upload");
     int rc = KCDC_OK;
     if (ids.kind == 3) {
@@ -1155,16 +1229,17 @@ uint64_t& kcdc::test_id_ring_bytes() {
 }
 
 namespace {
-// A writer call in progress on batcher t (batcher_free waits until none is left); false when
-// the batcher is closing (the caller must not touch it).
+// A writer call in progress (batcher_free waits until none is left); ok is false when the batcher
+// is closing or gone (the caller must not touch w->b).  The count is taken before `closing` is
+// read: either batcher_free sees this call and waits for it, or this call sees `closing`.
 struct Inside {
-    kcdc_bw_batcher* t;
+    BwCtl* c;
     bool ok;
-    explicit Inside(kcdc_bw_batcher* top) : t(top) {
-        t->inside++;
-        ok = !t->closing.load();
+    explicit Inside(BwCtl* ctl) : c(ctl) {
+        c->inside++;
+        ok = !c->closing.load();
     }
-    ~Inside() { t->inside--; }
+    ~Inside() { c->inside--; }
 };
 
 int dev_error(BwDev* b) { return set_error(b->error, b->errmsg); }  // errmsg is set before error
@@ -1291,13 +1366,13 @@ extern "C" int kcdc_bw_batcher_devices(const kcdc_bw_batcher* t) {
 
 extern "C" void kcdc_bw_batcher_free(kcdc_bw_batcher* t) {
     if (!t) return;
-    t->closing = true;
+    t->ctl->closing = true;
     for (BwDev* b : t->devs) dev_stop(b);
-    while (t->inside.load() > 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    while (t->ctl->inside.load() > 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
     for (BwDev* b : t->devs) {
-        for (kcdc_bw* w : b->open) {  // writers not freed: unusable from now on (kcdc_bw_free frees their arenas)
-            w->b = nullptr;
-            w->top = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(b->mu);
+            for (kcdc_bw* w : b->open) w->b = nullptr;  // writers not freed: kcdc_bw_free frees their arenas
         }
         if (b->algo->kind != kFixed) {
             Guard g(b->device);
@@ -1306,6 +1381,7 @@ extern "C" void kcdc_bw_batcher_free(kcdc_bw_batcher* t) {
         }
         delete b;
     }
+    t->ctl->detached = true;
     delete t;
 }
 
@@ -1314,7 +1390,7 @@ extern "C" kcdc_bw* kcdc_bw_open_hint(kcdc_bw_batcher* t, uint64_t size_hint) {
         set_error(KCDC_EINVAL, "null batcher");
         return nullptr;
     }
-    Inside in(t);
+    Inside in(t->ctl.get());
     if (!in.ok) {
         set_error(KCDC_EINVAL, "writer batcher closed");
         return nullptr;
@@ -1331,7 +1407,7 @@ extern "C" kcdc_bw* kcdc_bw_open_hint(kcdc_bw_batcher* t, uint64_t size_hint) {
     }
     auto* w = new kcdc_bw();
     w->b = b;
-    w->top = t;
+    w->ctl = t->ctl;
     w->device = b->device;
     w->hint = size_hint;
     w->counted = size_hint;
@@ -1351,6 +1427,7 @@ extern "C" kcdc_bw* kcdc_bw_open_hint(kcdc_bw_batcher* t, uint64_t size_hint) {
         if (!p) e = hipMalloc(&p, b->arena_cap);
         if (e == hipSuccess && !q) e = hipMalloc(&q, b->arena_cap);
         if (e != hipSuccess) {  // give back the cached pairs (another device user may need the memory), retry once
+            (void)hipGetLastError();  // (the failed allocation's error is not this call's result)
             {
                 std::lock_guard<std::mutex> lk(b->mu);
                 b->trim_arenas();
@@ -1383,9 +1460,10 @@ extern "C" int kcdc_bw_device(const kcdc_bw* w) {
 }
 
 extern "C" int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len) {
-    if (!w || !w->b) return set_error(KCDC_EINVAL, "writer not open");
-    Inside in(w->top);
+    if (!w) return set_error(KCDC_EINVAL, "writer not open");
+    Inside in(w->ctl.get());
     if (!in.ok) return set_error(KCDC_EINVAL, "writer batcher closed");
+    if (!w->b) return set_error(KCDC_EINVAL, "writer not open");
     BwDev* b = w->b;
     if (b->algo->kind == kFixed) {  // splitter_fixed.go:15-26: no data is read
         std::lock_guard<std::mutex> lk(b->mu);
@@ -1456,9 +1534,10 @@ extern "C" int kcdc_bw_write(kcdc_bw* w, const uint8_t* p, size_t len) {
 }
 
 extern "C" int64_t kcdc_bw_cuts(kcdc_bw* w, uint64_t* out, uint64_t cap) {
-    if (!w || !w->b) return set_error(KCDC_EINVAL, "writer not open");
-    Inside in(w->top);
+    if (!w) return set_error(KCDC_EINVAL, "writer not open");
+    Inside in(w->ctl.get());
     if (!in.ok) return set_error(KCDC_EINVAL, "writer batcher closed");
+    if (!w->b) return set_error(KCDC_EINVAL, "writer not open");
     BwDev* b = w->b;
     if (b->ids.on) return set_error(KCDC_EINVAL, "content IDs are on: take cuts with kcdc_bw_cuts_ids");
     if (w->ready_pushed.load(std::memory_order_acquire) == w->ready_taken.load(std::memory_order_relaxed) &&
@@ -1479,9 +1558,10 @@ extern "C" int64_t kcdc_bw_cuts(kcdc_bw* w, uint64_t* out, uint64_t cap) {
 }
 
 extern "C" int kcdc_bw_finish(kcdc_bw* w) {
-    if (!w || !w->b) return set_error(KCDC_EINVAL, "writer not open");
-    Inside in(w->top);
+    if (!w) return set_error(KCDC_EINVAL, "writer not open");
+    Inside in(w->ctl.get());
     if (!in.ok) return set_error(KCDC_EINVAL, "writer batcher closed");
+    if (!w->b) return set_error(KCDC_EINVAL, "writer not open");
     BwDev* b = w->b;
     if (b->algo->kind == kFixed) {
         std::lock_guard<std::mutex> lk(b->mu);
@@ -1512,9 +1592,10 @@ extern "C" int kcdc_bw_finish(kcdc_bw* w) {
 }
 
 extern "C" int64_t kcdc_bw_cuts_ids(kcdc_bw* w, uint64_t* cuts, uint8_t* ids, uint32_t id_stride, uint64_t cap) {
-    if (!w || !w->b) return set_error(KCDC_EINVAL, "writer not open");
-    Inside in(w->top);
+    if (!w) return set_error(KCDC_EINVAL, "writer not open");
+    Inside in(w->ctl.get());
     if (!in.ok) return set_error(KCDC_EINVAL, "writer batcher closed");
+    if (!w->b) return set_error(KCDC_EINVAL, "writer not open");
     BwDev* b = w->b;
     if (!b->ids.on) return set_error(KCDC_EINVAL, "content IDs are off (kcdc_bw_batcher_hash)");
     if (id_stride < b->ids.out || (cap && (!cuts || !ids))) return set_error(KCDC_EINVAL, "bad ID buffer");
@@ -1544,20 +1625,39 @@ extern "C" int kcdc_bw_batcher_hash(kcdc_bw_batcher* t, const char* hash_name, c
         if (!b->open.empty() || b->rounds) return set_error(KCDC_EINVAL, "content IDs: enable before the first writer opens");
         if (b->ids.on) return set_error(KCDC_EINVAL, "content IDs are already on");
     }
-    for (BwDev* b : t->devs) {
-        const int rc = b->ids_enable(hash_name, key, key_len);
-        if (rc != KCDC_OK) return rc;
+    for (size_t i = 0; i < t->devs.size(); i++) {
+        const int rc = t->devs[i]->ids_enable(hash_name, key, key_len);
+        if (rc != KCDC_OK) {  // all or nothing: the devices enabled so far go back to plain cuts
+            const std::string msg = kcdc_last_error();
+            for (size_t k = 0; k <= i; k++) t->devs[k]->ids_disable();
+            return set_error(rc, msg);
+        }
     }
     return KCDC_OK;
 }
 
 extern "C" void kcdc_bw_free(kcdc_bw* w) {
     if (!w) return;
+    const std::shared_ptr<BwCtl> ctl = w->ctl;  // (outlives `in`: w and the batcher may hold the last references)
+    Inside in(ctl.get());
+    if (!in.ok) {  // the batcher is closing: once it has detached this writer, free what is left
+        while (!ctl->detached.load()) std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (w->arena) {
+            Guard g(w->device);
+            (void)hipFree(w->arena);
+            (void)hipFree(w->spare);
+        }
+        delete w;
+        return;
+    }
     BwDev* b = w->b;
     if (b) {
         // an abandoned object: split (and drop) what it staged, so no round still reads its arena
         if (b->algo->kind != kFixed && !b->error) (void)kcdc_bw_finish(w);
-        std::lock_guard<std::mutex> lk(b->mu);
+        std::unique_lock<std::mutex> lk(b->mu);
+        // a writer whose last round did not complete (an error) may still be in a round the round
+        // thread is issuing, or in id_create: wait until it holds no writer pointers
+        if (!w->done) b->cv_done.wait(lk, [&] { return b->writer_refs == 0; });
         for (BwDev::Chain& c : b->chains)  // (an error left chains of this writer unnamed)
             if (c.w == w) c.w = nullptr;
         b->load -= std::min<uint64_t>(b->load.load(), w->counted);

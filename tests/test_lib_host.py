@@ -203,3 +203,53 @@ def test_writer_batcher_free_fails_late_calls():
     b._h = None
     assert lib.kcdc_bw_write(h, b"y", 1) == _lib.KCDC_EINVAL
     lib.kcdc_bw_free(h)
+
+
+def test_writer_calls_racing_batcher_free():
+    """A writer call that races kcdc_bw_batcher_free returns KCDC_OK or KCDC_EINVAL and never touches
+    the freed batcher: the batcher's lifetime state is refcounted by its writers (kcdc_writer.cpp
+    BwCtl), so a call starting during or after the free sees `closing` in memory that outlives the
+    batcher.  Threads hammer write / cuts / finish on FIXED writers (host logic, no GPU) while the
+    batcher is freed; every writer is freed after."""
+    import threading
+    from kopia_amd.writer import WriterBatcher
+    lib = _lib.lib()
+    for rep in range(20):
+        b = WriterBatcher("FIXED-128K")
+        hs = [lib.kcdc_bw_open(b._h) for _ in range(6)]
+        assert all(hs)
+        codes, stop = [], threading.Event()
+        buf = b"z" * 5000
+        out = (C.c_uint64 * 64)()
+
+        def hammer(h, k):
+            got = []
+            i = 0
+            while not stop.is_set() and i < 4000:
+                op = (i + k) % 3
+                if op == 0:
+                    rc = lib.kcdc_bw_write(h, buf, len(buf))
+                elif op == 1:
+                    rc = lib.kcdc_bw_cuts(h, out, 64)
+                    rc = 0 if rc >= 0 else rc
+                else:
+                    rc = lib.kcdc_bw_device(h)
+                    rc = 0 if rc >= 0 else rc
+                got.append(rc)
+                i += 1
+            codes.append(got)
+
+        th = [threading.Thread(target=hammer, args=(h, k)) for k, h in enumerate(hs)]
+        for t in th:
+            t.start()
+        lib.kcdc_bw_batcher_free(b._h)
+        b._h = None
+        stop.set()
+        for t in th:
+            t.join()
+        for h in hs:
+            assert lib.kcdc_bw_write(h, b"y", 1) == _lib.KCDC_EINVAL
+            assert lib.kcdc_bw_finish(h) == _lib.KCDC_EINVAL
+            lib.kcdc_bw_free(h)
+        flat = [c for g in codes for c in g]
+        assert set(flat) <= {0, _lib.KCDC_EINVAL}, set(flat)

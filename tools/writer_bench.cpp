@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -89,6 +90,8 @@ int main(int argc, char** argv) {
         }
     }
     std::vector<double> rates;
+    std::vector<double> fin_ms;  // per object: kcdc_bw_finish's latency (what Result() waits on), timed reps
+    std::mutex fin_mu;
     double st0[24] = {0};  // the stats after the warm-up rep: the steady-state pool misses are the rest
     bool ok = true;
     for (int r = 0; r < reps + 1; r++) {  // rep 0 warms the pinned pool and device buffers
@@ -121,9 +124,15 @@ int main(int argc, char** argv) {
                     pos += k;
                     if (++calls % 16 == 0) take();
                 }
+                const auto f0 = std::chrono::steady_clock::now();
                 if (kcdc_bw_finish(w)) {
                     std::fprintf(stderr, "kcdc_bw_finish: %s\n", kcdc_last_error());
                     std::exit(1);
+                }
+                if (r > 0) {
+                    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - f0).count();
+                    std::lock_guard<std::mutex> fl(fin_mu);
+                    fin_ms.push_back(ms);
                 }
                 take();
                 kcdc_bw_free(w);
@@ -190,6 +199,8 @@ int main(int argc, char** argv) {
                        (1ull << 30);
         for (auto& p : stage) std::free(p);
     }
+    std::sort(fin_ms.begin(), fin_ms.end());
+    auto pct = [&](double q) { return fin_ms.empty() ? 0.0 : fin_ms[std::min(fin_ms.size() - 1, static_cast<size_t>(q * fin_ms.size()))]; };
     double best = 0, sum = 0;
     for (double x : rates) {
         best = x > best ? x : best;
@@ -200,9 +211,9 @@ int main(int argc, char** argv) {
                 "\"round_wait_s\": %.3f, \"dev_gather_s\": %.3f, \"dev_split_s\": %.3f, \"dev_span_s\": %.3f, "
                 "\"dev_busy_s\": %.3f, \"host_s\": [%.3f, %.3f, %.3f, %.3f, %.3f], "
                 "\"round_idle_s\": %.3f, \"writer_capped_s\": %.3f, \"writer_block_s\": %.3f, \"pool_misses\": %.0f, \"pool_misses_after_warmup\": %.0f, \"writer_block_s_after_warmup\": %.3f, \"round_lock_s\": %.3f, "
-                "\"memcpy_only_gib_s\": %.2f, \"memcpy_nt_only_gib_s\": %.2f, \"hash\": \"%s\", \"ids_named\": %.0f, \"hash_steps\": %.0f, \"hash_dev_s\": %.3f, \"id_space_wait_s\": %.3f, \"hash_idle_s\": %.3f, \"chains_per_step\": %.0f, \"parity_ok\": %s}\n",
+                "\"memcpy_only_gib_s\": %.2f, \"memcpy_nt_only_gib_s\": %.2f, \"hash\": \"%s\", \"ids_named\": %.0f, \"hash_steps\": %.0f, \"hash_dev_s\": %.3f, \"id_space_wait_s\": %.3f, \"hash_idle_s\": %.3f, \"chains_per_step\": %.0f, \"finish_ms_p50\": %.2f, \"finish_ms_p99\": %.2f, \"finish_ms_max\": %.2f, \"parity_ok\": %s}\n",
                 W, L >> 20, S >> 10, name.c_str(), static_cast<unsigned long long>(round >> 20),
                 rates.empty() ? 0.0 : sum / rates.size(), best, static_cast<long long>(rounds), st[2], st[3], st[4], st[5], st[6], st[7], st[8], st[9], st[10], st[11], st[12], st[13], st[14], st[15], st[16], st[16] - st0[16], st[15] - st0[15], st[17], copy_rate, copy_nt_rate,
-                hash.c_str(), st[18], st[19], st[20], st[21], st[22], st[19] > 0 ? st[23] / st[19] : 0.0, ok ? "true" : "false");
+                hash.c_str(), st[18], st[19], st[20], st[21], st[22], st[19] > 0 ? st[23] / st[19] : 0.0, pct(0.5), pct(0.99), fin_ms.empty() ? 0.0 : fin_ms.back(), ok ? "true" : "false");
     return ok ? 0 : 2;
 }
