@@ -1058,16 +1058,6 @@ __device__ __forceinline__ bool help_phase(int64_t budget) {
     return true;
 }
 constexpr int64_t kHelpSplit = 2;     // sub-tiles per help task (lane segments lane_cap / 2, >= 256 B)
-// Tail tiles (round 6): a region whose visit began with no stream waiting (the batch's tail, or a
-// launch with fewer streams than waves) is walked in tiles of half the lane segment, so helpers
-// split the last regions twice as finely.  The published tile grid carries its lane bytes to the
-// helpers (help_find: task.cnt's high word).
-#ifndef KCDC_TAIL_SMALL
-#define KCDC_TAIL_SMALL 1
-#endif
-__device__ __forceinline__ bool tail_small(int64_t budget, int64_t own_cap, int64_t min_cap) {
-    return KCDC_TAIL_SMALL && budget > (int64_t(1) << 61) && own_cap >= 2 * min_cap;
-}
 constexpr int kHelpTiles = 128;          // regions of up to 128 tiles take help (every registered name)
 #ifndef KCDC_HELP_MIN_TILES
 #define KCDC_HELP_MIN_TILES 3u
@@ -1284,7 +1274,7 @@ __device__ bool help_find(const BatchArgs& a, int lane, uint32_t me, uint32_t at
     const int64_t rhi = static_cast<int64_t>(rl64(v, 3));
     task.aux = task.ct + T - 1 < rhi ? task.ct + T - 1 : rhi;  // the tile's end
     task.cb = gs;
-    task.cnt = k | (static_cast<uint64_t>(T / kWave) << 32);  // tile index | the region's lane bytes per tile
+    task.cnt = k;
     task.cap = 0;
     task.epoch = eps;
     return true;
@@ -1475,6 +1465,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
     const int64_t mx = static_cast<int64_t>(a.max_size);
     // help sub-tiles halve the lane segments (>= 256 B): shift = sid's help bit & this (integer
     // arithmetic: a select on a bool here became a VALU-materialised shift next to the DMAs)
+    const uint32_t help_shift = __builtin_amdgcn_readfirstlane(a.lane_cap >= 512u ? 1u : 0u);
     static_assert(kHelpSplit == 2, "help sub-tiles: one halving");
 
     PStream cur;
@@ -1486,7 +1477,6 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
     constexpr uint32_t kHsPub = 1u << 16;     // the current region is published (claims are on)
     constexpr uint32_t kHsNeedPub = 1u << 17; // the region at cur.ct is new to this wave
     constexpr uint32_t kHsHelped = 1u << 18;  // the last claim saw helpers on the region: no yield
-    constexpr uint32_t kHsSmall = 1u << 19;   // this region's own tiles have half lane segments (tail_small)
     hs = kHsNeedPub;
     auto hK = [&] { return hs & 0xFFu; };
     auto htile = [&] { return (hs >> 8) & 0xFFu; };
@@ -1589,23 +1579,18 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
 #endif
         int64_t lo, hi;
         pregion(a, cur, lo, hi);
-        if ((hs & kHsNeedPub) && !is_help)  // a new region: its tile size (the prefetch below used the same rule)
-            hs = (hs & ~kHsSmall) | (tail_small(budget, a.lane_cap, 512) ? kHsSmall : 0u);
-        const int64_t own_cap = static_cast<int64_t>(a.lane_cap >> ((hs >> 19) & 1u));
-        // A help task's tile (one owner tile, up to hi) goes in kHelpSplit sub-tiles (lane segments of
-        // half its own tile's, >= 256 B): it stops at the first one with a candidate, or when its
-        // owner has closed the region meanwhile.
-        const int64_t task_cap = static_cast<int64_t>(cur.cnt >> 32);
-        const int64_t lcap = is_help ? (task_cap >= 512 ? task_cap / 2 : task_cap) : own_cap;
+        // A help task's tile (one owner tile, up to hi) goes in kHelpSplit sub-tiles: it stops at
+        // the first one with a candidate, or when its owner has closed the region meanwhile.
+        const int64_t lcap = static_cast<int64_t>(a.lane_cap >> ((cur.sid >> 31) & help_shift));
         const TileGeom g = tile_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n, lcap);
         const int64_t ct = cur.ct, ct_next = ct + kWave * g.L;
         const bool last_of_region = ct_next > hi;
         if (!issued) ptile_issue(cur, hi, wl32, sl32, lane, lcap);
         // A region new to this wave: publish it when it is long enough to share.
         if ((hs & kHsNeedPub) && !is_help) {
-            const int64_t T = kWave * own_cap;  // bytes per full tile
+            const int64_t T = kWave * static_cast<int64_t>(a.lane_cap);  // bytes per full tile
             const uint32_t K = static_cast<uint32_t>((hi - ct + T) / T);
-            hs &= kHsSmall;
+            hs = 0;
             if (a.help && help_phase(budget) && K >= kHelpMinTiles && K <= static_cast<uint32_t>(kHelpTiles)) {
                 hep++;
                 hs = kHsPub | K;
@@ -1772,7 +1757,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
         } else if (last_of_region) {  // forced cut at max size (splitter_buzhash32.go:60-64) or the end
             cut = forced;
         } else if (claim_next && !claim_ok) {  // the helpers hold the rest of the region
-            const int64_t T = kWave * own_cap;
+            const int64_t T = kWave * static_cast<int64_t>(a.lane_cap);
             const int64_t ct0 = ct - static_cast<int64_t>(htile()) * T;  // the published tile 0
             const int64_t r = help_wait(a, lane, me, hep, htile() + 1u, hK(), ct0);
             if (r >= 0) {
@@ -1782,7 +1767,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             } else {  // a tile still pending: scan on from it, unshared
                 cur.ct = ct0 + (-2 - r) * T;
                 help_close(a, lane, me, hep);
-                hs &= kHsSmall;
+                hs = 0;
                 region_changed = false;
             }
         } else {
@@ -1835,9 +1820,7 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
                     int64_t nlo, nhi;
                     pregion(a, nx, nlo, nhi);
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // entry read before the slot refill
-                    // the tile size its first region will pick (tail_small with the budget it gets below)
-                    const bool nsmall = tail_small(pipe_quantum_tiles(nbacklog, a.lane_cap), a.lane_cap, 512);
-                    ptile_issue(nx, nhi, wl32, sl32, lane, static_cast<int64_t>(a.lane_cap >> (nsmall ? 1 : 0)));
+                    ptile_issue(nx, nhi, wl32, sl32, lane, a.lane_cap);
                     nstate = 3;
                 }
             }
@@ -2251,10 +2234,7 @@ __device__ __forceinline__ void rk_walk(const RkCtx& kx, const uint8_t* sl, int 
 
 // Rabin-Karp lane segments: twice the buzhash cap (warm-up vs tile overshoot; 2 vs 1: 4M 2.542 vs
 // 2.554 ms, 128K 5.536 vs 5.643 ms, profiles/r03/rk/kbench_lmul_*.log)
-#ifndef KCDC_RK_LANE_MUL
-#define KCDC_RK_LANE_MUL 2
-#endif
-constexpr int64_t kRkLaneMul = KCDC_RK_LANE_MUL;
+constexpr int64_t kRkLaneMul = 2;
 // Intra-region help as in split_batch_pipe_kernel (the same help slots, claim words and rows; hep,
 // hs and the kHs* flags mean the same).  An own tile is T = 64 x rk_cap bytes; a help task scans
 // one in two sub-tiles of rk_cap / 2 bytes per lane.
@@ -2298,7 +2278,7 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
     PStream cur;
     int64_t budget = kNoYield;
     uint32_t hep = 0, hs = 0;
-    constexpr uint32_t kHsPub = 1u << 16, kHsNeedPub = 1u << 17, kHsHelped = 1u << 18, kHsSmall = 1u << 19;
+    constexpr uint32_t kHsPub = 1u << 16, kHsNeedPub = 1u << 17, kHsHelped = 1u << 18;
     hs = kHsNeedPub;
     auto hK = [&] { return hs & 0xFFu; };
     auto htile = [&] { return (hs >> 8) & 0xFFu; };
@@ -2386,19 +2366,15 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
 #endif
         int64_t lo, hi;
         pregion(a, cur, lo, hi);
-        if ((hs & kHsNeedPub) && !is_help)  // a new region: its tile size
-            hs = (hs & ~kHsSmall) | (tail_small(budget, rk_cap, 512) ? kHsSmall : 0u);
-        const int64_t own_cap = (hs & kHsSmall) ? rk_cap / 2 : rk_cap;
-        // a help task scans its owner's tile in two sub-tiles of half its lane bytes (>= 256 B)
-        const int64_t lcap = is_help ? static_cast<int64_t>(cur.cnt >> 32) / 2 : own_cap;
+        const int64_t lcap = is_help ? rk_cap / 2 : rk_cap;
         const RkGeom g = rk_geom(cur.ct, hi, cur.abase, cur.off0, cur.off0 + cur.n, lcap);
         const int64_t ct = cur.ct, ct_next = ct + kWave * g.L;
         const bool last_of_region = ct_next > hi;
         // A region new to this wave: publish it when it is long enough to share.
         if ((hs & kHsNeedPub) && !is_help) {
-            const int64_t T = kWave * own_cap;
+            const int64_t T = kWave * rk_cap;
             const uint32_t K = static_cast<uint32_t>((hi - ct + T) / T);
-            hs &= kHsSmall;
+            hs = 0;
             if (a.help && help_phase(budget) && K >= kHelpMinTiles && K <= static_cast<uint32_t>(kHelpTiles)) {
                 hep++;
                 hs = kHsPub | K;
@@ -2557,7 +2533,7 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
         } else if (last_of_region) {  // forced cut at max size (splitter_rabinkarp64.go:60-64) or the end
             cut = forced;
         } else if (claim_next && !claim_ok) {  // the helpers hold the rest of the region
-            const int64_t T = kWave * own_cap;
+            const int64_t T = kWave * rk_cap;
             const int64_t ct0 = ct - static_cast<int64_t>(htile()) * T;  // the published tile 0
             const int64_t r = help_wait(a, lane, me, hep, htile() + 1u, hK(), ct0);
             if (r >= 0) {
@@ -2567,7 +2543,7 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             } else {  // a tile still pending: scan on from it, unshared
                 cur.ct = ct0 + (-2 - r) * T;
                 help_close(a, lane, me, hep);
-                hs &= kHsSmall;
+                hs = 0;
                 region_changed = false;
             }
         } else {
