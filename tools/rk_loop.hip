@@ -15,6 +15,8 @@
 //                          that keeps lane%32*8 in byte 0, instead of a v_perm)
 //                  kB64   (the shift as one v_lshrrev_b64 and the entering byte XORed into byte 3 of hi
 //                          by one SDWA v_xor after the xor3s, instead of v_perm + v_alignbit)
+//                  kRegData (no step slot: the bytes come from registers, one v_add per dword, so the
+//                          tables may take all of LDS -- the layout a feed by global loads would allow)
 //
 // Bytes per variant are the same, so the times compare directly.  The output only defeats DCE.
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/rk_loop.hip -o build/rk_loop
@@ -24,7 +26,7 @@
 #include <string>
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s\n", hipGetErrorString(e)); return 1; } } while (0)
 
-constexpr int kNoOut = 1, kIndep = 2, kBitop = 4, kSdwa = 8, kB64 = 16;
+constexpr int kNoOut = 1, kIndep = 2, kBitop = 4, kSdwa = 8, kB64 = 16, kRegData = 32;
 
 template <int MODREP, int OUTREP, int NSLOT>
 struct Lds {
@@ -36,9 +38,10 @@ struct Lds {
 template <int NCH, int MODREP, int OUTREP, int WAVES, int FL>
 struct V {
     static constexpr int kTab = 256 * 8 * (MODREP + OUTREP);
-    static constexpr int kSlots = (160 * 1024 - kTab) / 8192 < WAVES ? (160 * 1024 - kTab) / 8192 : WAVES;
-    static_assert(kSlots >= 1, "no room for a step slot");
-    using L = Lds<MODREP, OUTREP, kSlots>;
+    static constexpr int kFree = (160 * 1024 - kTab) / 8192;
+    static constexpr int kSlots = (FL & kRegData) ? 1 : kFree < WAVES ? kFree : WAVES;
+    static_assert((FL & kRegData) || kSlots >= 1, "no room for a step slot");
+    using L = Lds<MODREP, OUTREP, (FL & kRegData) ? 0 : kSlots>;
 };
 
 __device__ __forceinline__ uint64_t ld64(const char* base, uint32_t a) { return *reinterpret_cast<const uint64_t*>(base + a); }
@@ -51,8 +54,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void rk_loop_kernel(uint64_t steps, 
     for (uint32_t i = threadIdx.x; i < 256u * OUTREP; i += blockDim.x) t.out[i] = (i * 0xC2B2AE3D27D4EB4Full) ^ seed;
     const uint32_t wv = threadIdx.x / 64u, lane = threadIdx.x % 64u;
     const uint32_t sv = wv % Vv::kSlots;
-    if (wv < Vv::kSlots)
-        for (uint32_t i = 0; i < 32u; i++) t.slot[sv][i][lane] = (lane + 1u) * 0x01000193u * (i + seed);
+    if constexpr ((FL & kRegData) == 0)
+        if (wv < Vv::kSlots)
+            for (uint32_t i = 0; i < 32u; i++) t.slot[sv][i][lane] = (lane + 1u) * 0x01000193u * (i + seed);
     __syncthreads();
     const char* modb = reinterpret_cast<const char*>(t.mod);
     const char* outb = reinterpret_cast<const char*>(t.out);
@@ -109,7 +113,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void rk_loop_kernel(uint64_t steps, 
         for (int c = 0; c < NCH; c++)
 #pragma unroll
             for (int i = 0; i < 16; i++) {
-                const uint32_t v = t.slot[sv][(16 * c + i) & 31][lane];
+                uint32_t v;
+                if constexpr ((FL & kRegData) != 0) v = static_cast<uint32_t>(s) * 0x9E3779B9u + (lane * 16u + i) * 0x01000193u + c;
+                else v = t.slot[sv][(16 * c + i) & 31][lane];
                 d[c][i] = c < 2 ? __builtin_bitreverse32(v) : __builtin_bitreverse32(v ^ 0x5A5A5A5Au);
             }
         constexpr int W = 2;
@@ -223,8 +229,10 @@ int main(int argc, char** argv) {
     run<4, 16, 32, 8, 0>("4 chains/lane", cus, out, reps);
     run<4, 32, 16, 8, 0>("4 chains/lane, mod conflict-free", cus, out, reps);
     run<2, 16, 32, 8, kBitop | kSdwa>("bitop3 mod addr + sdwa out addr", cus, out, reps);
+    run<2, 16, 32, 8, kBitop | kSdwa | kRegData>("... data from registers", cus, out, reps);
+    run<2, 32, 32, 8, kBitop | kSdwa | kRegData>("... + mod conflict-free (128 KiB tables)", cus, out, reps);
+    run<2, 32, 32, 12, kBitop | kSdwa | kRegData>("... + 12 waves/CU", cus, out, reps);
     run<2, 16, 32, 8, kBitop | kB64>("bitop3 mod addr + b64 shift", cus, out, reps);
-    run<2, 16, 32, 8, kBitop | kSdwa | kB64>("bitop3 + sdwa + b64", cus, out, reps);
     run<2, 16, 32, 8, kBitop | kNoOut>("bitop3 mod addr, no out[]", cus, out, reps);
     run<2, 16, 32, 8, 0>("production replica (again)", cus, out, reps);
     return 0;
