@@ -159,9 +159,9 @@ void kcdc_group_free(kcdc_group* g);
  * when a kcdc_bw_open would otherwise fail with KCDC_ENOMEM, and at kcdc_bw_batcher_free.
  * kcdc_bw_batcher_free ships what is staged, then fails every writer call still blocked in it
  * (KCDC_EINVAL) and waits for those calls to return; writers not freed before it stay valid for
- * kcdc_bw_free only.  No writer call may *start* concurrently with kcdc_bw_batcher_free (the
- * uploader frees the batcher after its writers' last calls, as it closes the repository after
- * its object writers). */
+ * kcdc_bw_free only.  A writer call that starts while or after kcdc_bw_batcher_free runs returns
+ * KCDC_EINVAL without touching the freed batcher (its lifetime state is refcounted by its
+ * writers), and kcdc_bw_free of such a writer waits until the batcher has let it go. */
 typedef struct kcdc_bw_batcher kcdc_bw_batcher;
 typedef struct kcdc_bw kcdc_bw;
 kcdc_bw_batcher* kcdc_bw_batcher_new(const char* name, int device, uint64_t round_bytes, uint32_t max_wait_us);
