@@ -142,11 +142,12 @@ __device__ __forceinline__ uint32_t st_ld32(const uint32_t* L, uint32_t d, uint3
 }
 // Stage the span_len bytes at A into L: the 16-byte granules [A & ~15, ...) holding them, at
 // staged word pw(k); returns d = A & 15.
-__device__ __forceinline__ uint32_t stage_span(uint32_t* L, const uint8_t* A, uint32_t span_len, uint32_t lane) {
+__device__ __forceinline__ uint32_t stage_span(uint32_t* L, const uint8_t* A, uint32_t span_len, uint32_t lane,
+                                                uint32_t nt = 64u) {
     const uint32_t d = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(A) & 15u);
     const uint4* G = reinterpret_cast<const uint4*>(A - d);
     const uint32_t ng = (d + span_len + 15u) >> 4;
-    for (uint32_t g = lane; g < ng; g += 64u) {
+    for (uint32_t g = lane; g < ng; g += nt) {
         const uint4 v = G[g];
         const uint32_t k = 4u * g;
         L[pw(k)] = v.x;
@@ -211,44 +212,47 @@ __device__ const FseTab<36, 6> kFseLL(kLLNorm);
 __device__ const FseTab<53, 6> kFseML(kMLNorm);
 __device__ const FseTab<29, 5> kFseOF(kOFNorm);
 
-// Literal length -> (code, extra bits, extra value); RFC 8878 Literals_Length_Code table.
+// Literal length -> (code, extra bits, extra value); RFC 8878 Literals_Length_Code table: codes
+// 16..24 cover 16..63 in groups of 1, 2, 3, 4 extra bits (bases 16, 24, 32, 48), from 64 the
+// code is 19 + log2.  Branch-free within each range (the FSE writer's serial loop runs it).
 __device__ __forceinline__ void ll_code(uint32_t ll, uint32_t& code, uint32_t& nbx, uint32_t& x) {
-    constexpr uint8_t base[20] = {16, 18, 20, 22, 24, 28, 32, 40, 48, 64, 128, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    constexpr uint8_t bits[20] = {1, 1, 1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+    const uint32_t g = ll >> 3;
+    const uint32_t nb = g == 2u ? 1u : g == 3u ? 2u : g < 6u ? 3u : 4u;
+    const uint32_t base = nb == 1u ? 16u : nb == 2u ? 24u : nb == 3u ? 32u : 48u;
+    const uint32_t c0 = nb == 1u ? 16u : nb == 2u ? 20u : nb == 3u ? 22u : 24u;
+    const uint32_t h = 31u - static_cast<uint32_t>(__builtin_clz(ll | 1u));
     if (ll < 16u) {
         code = ll;
         nbx = 0;
         x = 0;
     } else if (ll < 64u) {
-        uint32_t c = 0;
-        while (c + 1u < 9u && base[c + 1] <= ll) c++;
-        code = 16u + c;
-        nbx = bits[c];
-        x = ll - base[c];
+        code = c0 + ((ll - base) >> nb);
+        nbx = nb;
+        x = (ll - base) & ((1u << nb) - 1u);
     } else {
-        const uint32_t h = 31u - __builtin_clz(ll);  // 64 -> 6
         code = h + 19u;
         nbx = h;
         x = ll - (1u << h);
     }
 }
-// Match length (>= 3) -> (code, extra bits, extra value); Match_Length_Code table.
+// Match length (>= 3) -> (code, extra bits, extra value); Match_Length_Code table: m = ml - 3,
+// codes 32..42 cover m 32..127 in groups of 1..5 extra bits (bases 32, 40, 48, 64, 96), from 128
+// the code is 36 + log2.
 __device__ __forceinline__ void ml_code(uint32_t ml, uint32_t& code, uint32_t& nbx, uint32_t& x) {
-    constexpr uint8_t base[11] = {35, 37, 39, 41, 43, 47, 51, 59, 67, 83, 99};
-    constexpr uint8_t bits[11] = {1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5};
-    const uint32_t m = ml - 3u;
+    const uint32_t m = ml - 3u, g = m >> 3;
+    const uint32_t nb = g == 4u ? 1u : g == 5u ? 2u : g < 8u ? 3u : g < 12u ? 4u : 5u;
+    const uint32_t base = nb == 1u ? 32u : nb == 2u ? 40u : nb == 3u ? 48u : nb == 4u ? 64u : 96u;
+    const uint32_t c0 = nb == 1u ? 32u : nb == 2u ? 36u : nb == 3u ? 38u : nb == 4u ? 40u : 42u;
+    const uint32_t h = 31u - static_cast<uint32_t>(__builtin_clz(m | 1u));
     if (m < 32u) {
         code = m;
         nbx = 0;
         x = 0;
-    } else if (ml < 131u) {
-        uint32_t c = 0;
-        while (c + 1u < 11u && base[c + 1] <= ml) c++;
-        code = 32u + c;
-        nbx = bits[c];
-        x = ml - base[c];
+    } else if (m < 128u) {
+        code = c0 + ((m - base) >> nb);
+        nbx = nb;
+        x = (m - base) & ((1u << nb) - 1u);
     } else {
-        const uint32_t h = 31u - __builtin_clz(m);  // 128 -> 7: code 43, baseline 131
         code = h + 36u;
         nbx = h;
         x = m - (1u << h);
@@ -333,6 +337,14 @@ __device__ __forceinline__ uint32_t fixed_len(uint32_t s) {
     return s < 144u ? 8u : s < 256u ? 9u : s < 280u ? 7u : s < kNLit ? 8u : 5u;
 }
 
+// Orders one wave's LDS accesses across its lanes (a wave's LDS instructions complete in order):
+// the barrier for wave-collective helpers that also run inside multi-wave workgroups.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Canonical codes (RFC 1951 §3.2.2) of the n code lengths len[] (LDS bytes), bit-reversed for the
 // LSB-first stream: out[s] = rev(code) | length << 16 (0 for unused symbols).  Wave-collective:
 // symbols in 64-wide groups, a symbol's rank among the equal lengths before it by ballot.
@@ -391,7 +403,7 @@ __device__ void huff_lengths(const uint32_t* cnt, uint32_t n, uint32_t maxb, uin
         }
         used += static_cast<uint32_t>(__popcll(__ballot(c != 0u)));
     }
-    __syncthreads();
+    wave_sync();
     if (lane == 0 && used == 1u) len[ss[0]] = 1u;
     if (lane == 0 && used >= 2u) {
         const int m = static_cast<int>(used);
@@ -459,7 +471,7 @@ __device__ void huff_lengths(const uint32_t* cnt, uint32_t n, uint32_t maxb, uin
         for (uint32_t l = maxb; l >= 1u; l--)
             for (uint32_t k = num[l]; k > 0u; k--) len[ss[i++]] = static_cast<uint8_t>(l);
     }
-    __syncthreads();
+    wave_sync();
 }
 
 // The bit layout of a span's output for one code (hb = block header bits incl. the 3-bit BTYPE
@@ -737,6 +749,24 @@ __device__ __forceinline__ void deflate_plan(const CompArgs& a, uint32_t b, uint
     }
 }
 
+// A zstd sequence word: literal length, match length (4..512) and distance (15 bits) in 32 bits.
+// Inside a 512-byte segment ll + (ml - 4) <= 508, so the pair fits a 9-bit field A and an 8-bit
+// field B: ml - 4 < 256 as (A, B) = (ll, ml - 4); a longer match (then ll <= 252) as
+// (508 - ll, 511 - (ml - 4)), told apart by A + B > 508 (no short pair sums past 508).
+__device__ __forceinline__ uint32_t zseq_word(uint32_t ll, uint32_t ml, uint32_t dist) {
+    const uint32_t t = ml - 4u;
+    const bool lng = t >= 256u;
+    return ((lng ? 508u - ll : ll) << 23) | ((lng ? 511u - t : t) << 15) | dist;
+}
+__device__ __forceinline__ uint32_t zseq_ll(uint32_t v) {
+    const uint32_t A = v >> 23, B = (v >> 15) & 255u;
+    return A + B > 508u ? 508u - A : A;
+}
+__device__ __forceinline__ uint32_t zseq_ml(uint32_t v) {
+    const uint32_t A = v >> 23, B = (v >> 15) & 255u;
+    return (A + B > 508u ? 511u - B : B) + 4u;
+}
+
 // The sequences section of a segment's zstd block at sb8 + o (RFC 8878 §3.1.1.3.2):
 // Number_of_Sequences, Symbol_Compression_Modes = 0 (all Predefined), then the FSE bitstream written
 // backwards from the last sequence (zstd's ZSTD_encodeSequences order), closed by the 1-bit end
@@ -771,7 +801,7 @@ __device__ uint32_t zstd_seqs(uint8_t* sb8, uint32_t o, uint32_t nseq, uint32_t 
         for (int k = static_cast<int>(nseq) - 1; k >= 0; k--) {
             if (pos + 8u > 4u * (144u - static_cast<uint32_t>(k) - 1u) || pos > seg_len + 2u) return kZOver;
             const uint32_t v = words[143u - static_cast<uint32_t>(k)];
-            const uint32_t ll = v >> 23, ml = ((v >> 15) & 255u) + 4u, ov = (v & 0x7FFFu) + 3u;
+            const uint32_t ll = zseq_ll(v), ml = zseq_ml(v), ov = (v & 0x7FFFu) + 3u;
             uint32_t llc, llb, llx, mlc, mlb, mlx;
             ll_code(ll, llc, llb, llx);
             ml_code(ml, mlc, mlb, mlx);
@@ -804,163 +834,869 @@ __device__ uint32_t zstd_seqs(uint8_t* sb8, uint32_t o, uint32_t nseq, uint32_t 
     return pos - o;
 }
 
-// zstd literals through one Huffman code per span (RFC 8878 §3.1.1.3.1, §4.2): after the parse
-// (each coded segment a Compressed_Block with Raw_Literals: block header at slot + 3, literals
-// header at + 6, the literals from + 8, the sequences section after them), the span's literal
-// counts give a code of <= 11 bits.  The first segment whose literals shrink with it carries the
-// tree (Compressed_Literals_Block, direct weights: the span's largest literal must be <= 128); the
-// later segments whose literals shrink reuse it (Treeless_Literals_Block, the frame's previous
-// table); the others keep raw literals.  The code is used when what those segments save exceeds the
-// tree description.  Single stream, 10-bit sizes (a segment has <= 512 literals); the stream holds
-// the literals last to first (the decoder reads it backwards), then a 1 bit.  Literal bytes come
-// from the staged span; the sequences section moves to its new place first (the carrier's block
-// may grow, within its slot), then the tree and stream replace the raw literals.  Returns the
-// segment's new length word.  S: LDS scratch (the match tables).
-// The reference's zstd encoder (klauspost/compress/zstd, compressor_zstd.go:15-18) Huffman-codes
-// literals the same way (one table per block, reused by later blocks when that is smaller).
-__device__ __forceinline__ uint32_t zstd_huff_literals(const CompArgs& a, uint32_t b, uint32_t lane, uint32_t span_len,
-                                                       uint32_t x0, uint32_t word, uint32_t nseq, uint32_t nlit,
-                                                       uint32_t* hist, uint32_t* S, const uint32_t* L, uint32_t d) {
-    __syncthreads();  // every lane's parse is done
-    uint32_t* sa = S;                                      // 256
-    uint16_t* ss = reinterpret_cast<uint16_t*>(S + 256);   // 256 u16
-    uint8_t* lens = reinterpret_cast<uint8_t*>(S + 384);   // 256 bytes
-    uint32_t* zc = S + 448;                                // 256: code | bits << 16
-    uint32_t* num = S + 704;                               // 33
-    uint32_t* misc = S + 740;                              // 8
-    const uint32_t seg_len = x0 < span_len ? min(kSeg, span_len - x0) : 0u, xe = x0 + seg_len;
-    const bool coded = seg_len && !(word & kStored);
-    uint8_t* sb8 = a.slots + (static_cast<uint64_t>(b) * 64u + lane) * kSlot;
-    const uint32_t* sq = reinterpret_cast<const uint32_t*>(sb8);  // sequence k at word 143 - k
-    auto seq_ll = [&](uint32_t k) { return sq[143u - k] >> 23; };
-    auto seq_ml = [&](uint32_t k) { return ((sq[143u - k] >> 15) & 255u) + 4u; };
-    // A segment that keeps raw literals: its sequences section after them (sized in the parse).
-    auto raw_tail = [&]() -> uint32_t {
-        if (coded && zstd_seqs(sb8, 8u + nlit, nseq, seg_len, true) == kZOver) return kStored | seg_len;
-        return word;
-    };
-    if (coded) {
-        uint32_t x = x0;
-        for (uint32_t k = 0; k < nseq; k++) {
-            for (const uint32_t e = x + seq_ll(k); x < e; x++) atomicAdd(&hist[st_byte(L, d, x)], 1u);
-            x += seq_ml(k);
-        }
-        for (; x < xe; x++) atomicAdd(&hist[st_byte(L, d, x)], 1u);
-    }
-    __syncthreads();
-    uint32_t used = 0, top = 0;
-    for (uint32_t k = 0; k < 256u; k += 64u) {
-        const uint64_t m = __ballot(hist[k + lane] != 0u);
-        used += static_cast<uint32_t>(__popcll(m));
-        if (m) top = k + 63u - static_cast<uint32_t>(__builtin_clzll(m));
-    }
-    if (used < 2u || top > 128u) return raw_tail();  // one symbol (an RLE block's case) or no direct weights
-    huff_lengths(hist, 256u, 11u, lens, sa, ss, num, lane);
-    if (lane == 0) {  // codes: by weight ascending (longest first), then symbol (RFC 8878 §4.2.1.4)
-        uint32_t maxb = 0;
-        for (uint32_t s = 0; s <= top; s++) maxb = lens[s] > maxb ? lens[s] : maxb;
-        for (uint32_t w = 0; w <= 12u; w++) num[w] = 0u;
-        for (uint32_t s = 0; s <= top; s++)
-            if (lens[s]) num[maxb + 1u - lens[s]]++;
-        uint32_t acc = 0;  // rank start (in 2^(w-1) cells), then the next code, per weight
-        for (uint32_t w = 1; w <= maxb; w++) {
-            const uint32_t c = num[w];
-            num[w] = acc >> (w - 1u);
-            acc += c << (w - 1u);
-        }
-        for (uint32_t s = 0; s <= top; s++) {
-            const uint32_t l = lens[s];
-            zc[s] = l ? (num[maxb + 1u - l]++ | (l << 16)) : 0u;
-        }
-        misc[0] = maxb;
-    }
-    __syncthreads();
-    const uint32_t maxb = misc[0];
-    const uint32_t tsz = 1u + (top + 1u) / 2u;  // header byte + 4-bit weights of symbols 0..top-1
-    uint32_t bits = 1u;                         // the end marker
-    auto for_lits = [&](auto f) {  // every literal of the segment, first to last
-        uint32_t x = x0;
-        for (uint32_t k = 0; k < nseq; k++) {
-            for (const uint32_t e = x + seq_ll(k); x < e; x++) f(x);
-            x += seq_ml(k);
-        }
-        for (; x < xe; x++) f(x);
-    };
-    if (coded && nlit) for_lits([&](uint32_t x) { bits += zc[st_byte(L, d, x)] >> 16; });
-    const uint32_t sbytes = (bits + 7u) / 8u;
-    // Bytes a Treeless literals section saves against the raw one (3-byte header + stream vs
-    // 2-byte header + the literals).  The tree is paid once, by the first segment that saves
-    // (the carrier), and pays off over the span: Huffman literals are used when the savings of all
-    // segments exceed the tree.  The carrier's block must still fit its slot (it may grow).
-    const uint32_t qs = coded ? word - 5u - nlit : 0u;  // the sequences section's size (the parse's block)
-    const int32_t save = coded && nlit ? static_cast<int32_t>(2u + nlit) - static_cast<int32_t>(3u + sbytes) : 0;
-    // the carrier's block may grow: it must fit its slot, its literal section and sequences must
-    // stay below the sequence words they are written from, and its sequences section must end
-    // within zstd_seqs' seg_len + 2 bound (else the carrier would be stored and the treeless
-    // segments after it would name a tree the frame never holds: ADVICE r4)
-    const bool fits = 6u + tsz + sbytes + qs + kZOff <= kSlot && 9u + tsz + sbytes + qs + 8u <= 4u * (144u - nseq) &&
-                      9u + tsz + sbytes + qs <= seg_len + 2u;
-    const uint64_t cm = __ballot(save > 0 && fits);
-    if (!cm) return raw_tail();
-    const uint32_t carrier = static_cast<uint32_t>(__builtin_ctzll(cm));
-    int32_t tot = save > 0 && lane >= carrier ? save : 0;  // what the carrier and the segments after it save
-    for (uint32_t o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, static_cast<int>(o), 64);
-    if (tot <= static_cast<int32_t>(tsz)) return raw_tail();
-    const uint32_t use = lane == carrier ? 2u : (lane > carrier && save > 0) ? 3u : 0u;
-    if (!use) return raw_tail();
-    const uint32_t ts = use == 2u ? tsz : 0u;
-    uint8_t* op = sb8 + 9u + ts;
-    if (use == 2u) {  // direct weights: W = maxb + 1 - bits (0: unused), two per byte, high nibble first
-        sb8[9] = static_cast<uint8_t>(127u + top);
-        for (uint32_t j = 0; 2u * j < top; j++) {
-            const uint32_t l0 = lens[2u * j], l1 = 2u * j + 1u < top ? lens[2u * j + 1u] : 0u;
-            const uint32_t w0 = l0 ? maxb + 1u - l0 : 0u, w1 = l1 ? maxb + 1u - l1 : 0u;
-            sb8[10u + j] = static_cast<uint8_t>((w0 << 4) | w1);
+// ---------------------------------------------------------------- zstd: span-level blocks (effort >= 1)
+// The parse leaves each segment's sequences in its slot (word 143 - k: literal length << 23 |
+// (match length - 4) << 15 | distance) and their count in the span's descriptor.  zstd_emit_kernel
+// (one wave per span) then writes the span as kZBlks Compressed_Blocks of kZBlkSegs segments
+// (RFC 8878 §3.1.1.2), all sharing the span's codes:
+//   literals   one Huffman code for the span (<= 11 bits, direct weights: the largest literal
+//              must be <= 128), its tree carried by the span's first compressed block that uses it
+//              (Compressed_Literals_Block), the later ones Treeless; 1 stream up to 1023 literals,
+//              else 4 (jump table); a block whose raw literals are smaller keeps them raw;
+//   sequences  three FSE tables (literal length, offset, match length codes) normalized from the
+//              span's code counts and described once (Symbol_Compression_Mode 2, the first
+//              compressed block with sequences), Repeat_Mode (3) in the later blocks; offset
+//              value 1 (repeat offset 1) for a match at the previous sequence's distance in the
+//              same block (a block's first sequence names its offset: a Raw_Block before it
+//              leaves the decoder's repeat offsets at the last compressed block's);
+//   fallback   a block whose body is not smaller than its bytes is a Raw_Block (it carries no
+//              table: the next compressed block does).
+// Segments are the parse's unit, blocks the coding unit: a segment's literals before its first
+// sequence join the previous sequence's (the block's carry).  Literal streams are written by all
+// lanes at once (each lane its literals' bits at its offset in the stream; bytes shared by two
+// lanes go through per-lane edge records merged by the block's leader); the sequences bitstream
+// by the block's leader lane, backwards (ZSTD_encodeSequences order), after a counting pass (the
+// raw-or-compressed choice needs the exact size first).  Block k goes to the slots of its first
+// segment (16 x kSlot bytes, >= any compressed body); its seglen word is its size, 0 for the
+// other segments (deflate_copy_kernel skips them).  tools/zstd_span_model.py is the host model of
+// this layout (libzstd-decoded; mixed data 0.327 per-segment -> 0.281 span-level).
+// The reference (klauspost/compress/zstd, compressor_zstd.go:15-18) writes the same block types
+// (Huffman literals with table reuse, FSE-compressed or repeated sequence tables, raw fallback).
+constexpr uint32_t kZBlkSegs = 16;                 // segments per block
+constexpr uint32_t kZBlks = 64 / kZBlkSegs;        // blocks per span
+constexpr uint32_t kZMaxSeq = kSpan / 4;           // a sequence covers >= 4 bytes
+constexpr uint32_t kZDesc = 80;                    // a table description: <= 53 x 10 bits + 4 + 2 bytes
+constexpr uint32_t kZRegion = kZBlkSegs * kSlot - kZOff;  // a block's bytes: from its first slot + 3
+constexpr uint32_t kZNone = 0xFFFFFFFFu;
+
+struct ZTab {          // FSE encoding table (RFC 8878 §4.1; zstd's FSE_buildCTable formulation)
+    uint16_t st[512];  // next state, by (state >> bits) + dfs; states in [size, 2 size)
+    uint2 dd[53];      // per symbol: x = dnb = (bits << 16) - (count << bits) (output bits =
+                       // (state + dnb) >> 16), y = dfs = cumulative count before s - count of s
+    uint32_t al;       // Accuracy_Log
+};
+
+// One field's table from the span's code counts (total nseq).  Wave-collective, lane = symbol:
+// Accuracy_Log from the sequence count (5..maxlog, >= used + 1 cells); counts rounded to 2^al with
+// every used symbol >= 1 (the rounding surplus to the largest entry, a deficit taken from the
+// largest one at a time); the encoding table (the RFC's spread puts cumulative cell j at
+// j * step mod size, so each symbol's lane walks the states in order and keeps those whose
+// j = state * step^-1 is one of its cells); lane 0 writes the description (RFC 8878 §4.1.1, as
+// zstd's FSE_writeNCount) into desc and returns its bytes.  norm: nsym shorts of LDS.
+__device__ uint32_t zstd_table(const uint32_t* cnt, uint32_t nsym, uint32_t maxlog, uint32_t nseq, uint16_t* tst,
+                               uint2* tdd, uint32_t* tal, int16_t* norm, uint8_t* desc, uint32_t lane) {
+    const uint32_t cs = lane < nsym ? cnt[lane] : 0u;
+    const uint64_t um = __ballot(cs != 0u);
+    const uint32_t used = static_cast<uint32_t>(__popcll(um));
+    const uint32_t last = 63u - static_cast<uint32_t>(__builtin_clzll(um));
+    uint32_t al = 31u - static_cast<uint32_t>(__builtin_clz(nseq));
+    al = al < 5u ? 5u : al > maxlog ? maxlog : al;
+    while ((1u << al) < used + 1u && al < maxlog) al++;
+    const uint32_t size = 1u << al;
+    uint32_t v = cs ? (cs * size + nseq / 2u) / nseq : 0u;
+    if (cs && v == 0u) v = 1u;
+    uint32_t sum = v;
+    for (uint32_t o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, static_cast<int>(o), 64);
+    int32_t diff = static_cast<int32_t>(size) - static_cast<int32_t>(sum);
+    while (diff != 0) {  // size >= used + 1: while the sum is over, the largest entry is > 1
+        uint32_t mx = v;
+        for (uint32_t o = 32; o > 0; o >>= 1) mx = max(mx, static_cast<uint32_t>(__shfl_xor(mx, static_cast<int>(o), 64)));
+        const uint32_t am = static_cast<uint32_t>(__builtin_ctzll(__ballot(v == mx)));
+        if (diff > 0) {
+            if (lane == am) v += static_cast<uint32_t>(diff);
+            diff = 0;
+        } else {
+            if (lane == am) v--;
+            diff++;
         }
     }
-    // the stream: literals last to first, then the end marker
+    if (lane < nsym) norm[lane] = static_cast<int16_t>(v);
+    uint32_t incl = v;
+    for (uint32_t o = 1; o < 64u; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const uint32_t cum = incl - v;
+    if (lane < nsym) {
+        uint2 e;
+        if (v == 0u) {
+            e = make_uint2(((al + 1u) << 16) - size, 0u);
+        } else if (v == 1u) {
+            e = make_uint2((al << 16) - size, cum - 1u);
+        } else {
+            const uint32_t mbo = al - (31u - static_cast<uint32_t>(__builtin_clz(v - 1u)));
+            e = make_uint2((mbo << 16) - (v << mbo), cum - v);
+        }
+        tdd[lane] = e;
+    }
+    const uint32_t step = (size >> 1) + (size >> 3) + 3u, mask = size - 1u;  // step is odd
+    uint32_t inv = step;  // Newton: step * inv == 1 (mod 2^32)
+    for (int i = 0; i < 5; i++) inv *= 2u - step * inv;
+    if (v) {
+        uint32_t r = cum;
+        for (uint32_t u = 0; u < size; u++)
+            if (((u * inv) & mask) - cum < v) tst[r++] = static_cast<uint16_t>(size + u);
+    }
+    if (lane == 0) *tal = al;
+    wave_sync();
+    if (lane != 0) return 0u;
+    // description: Accuracy_Log - 5, then each count + 1 in a variable number of bits, runs of
+    // zero counts after a zero as 2-bit repeat flags (16 bits = 24 zeros)
     uint64_t bb = 0;
-    uint32_t nb = 0;
-    auto put = [&](uint32_t v, uint32_t n) {
-        bb |= static_cast<uint64_t>(v) << nb;
+    uint32_t nb = 0, o = 0;
+    auto put = [&](uint32_t x, uint32_t n) {
+        bb |= static_cast<uint64_t>(x) << nb;
         nb += n;
         while (nb >= 8u) {
-            *op++ = static_cast<uint8_t>(bb);
+            desc[o++] = static_cast<uint8_t>(bb);
             bb >>= 8;
             nb -= 8u;
         }
     };
-    auto lit = [&](uint32_t x) {
-        const uint32_t c = zc[st_byte(L, d, x)];
-        put(c & 0xFFFFu, c >> 16);
-    };
-    uint32_t xm = x0;
-    for (uint32_t k = 0; k < nseq; k++) xm += seq_ll(k) + seq_ml(k);
-    for (uint32_t x = xe; x > xm; x--) lit(x - 1u);
-    for (uint32_t k = nseq; k-- > 0u;) {
-        xm -= seq_ml(k);
-        for (uint32_t e = xm - seq_ll(k); xm > e; xm--) lit(xm - 1u);
+    put(al - 5u, 4);
+    int32_t remaining = static_cast<int32_t>(size) + 1;
+    int32_t threshold = static_cast<int32_t>(size);
+    uint32_t nbits = al + 1u, sym = 0;
+    bool prev0 = false;
+    while (sym <= last && remaining > 1) {
+        if (prev0) {
+            uint32_t start = sym;
+            while (sym <= last && norm[sym] == 0) sym++;
+            while (sym >= start + 24u) {
+                start += 24u;
+                put(0xFFFFu, 16);
+            }
+            while (sym >= start + 3u) {
+                start += 3u;
+                put(3u, 2);
+            }
+            put(sym - start, 2);
+        }
+        int32_t count = norm[sym++];
+        const int32_t mx = (2 * threshold - 1) - remaining;
+        remaining -= count;
+        count += 1;
+        if (count >= threshold) count += mx;
+        put(static_cast<uint32_t>(count), count < mx ? nbits - 1u : nbits);
+        prev0 = count == 1;
+        while (remaining < threshold) {
+            nbits--;
+            threshold >>= 1;
+        }
     }
-    put(1u, 1);
     if (nb) put(0u, 8u - nb);
-    // literals header: type (2 compressed / 3 treeless), Size_Format 00, 10-bit sizes
-    const uint32_t lh = use | (nlit << 4) | ((ts + sbytes) << 14);
-    sb8[6] = static_cast<uint8_t>(lh);
-    sb8[7] = static_cast<uint8_t>(lh >> 8);
-    sb8[8] = static_cast<uint8_t>(lh >> 16);
-    // the sequences section after the stream (a treeless segment's may not fit below its sequence
-    // words: stored then, which keeps the frame's table for the segments after it)
-    const uint32_t q2 = zstd_seqs(sb8, 9u + ts + sbytes, nseq, seg_len, true);
-    // (defence in depth) a carrier that still could not be written leaves the segments after it
-    // without their table: they are stored too (a stored block depends on no table)
-    const bool carrier_lost = __ballot(use == 2u && q2 == kZOver) != 0;
-    if (q2 == kZOver || carrier_lost) return kStored | seg_len;
-    const uint32_t total = 6u + ts + sbytes + q2;
-    const uint32_t hdr = ((total - 3u) << 3) | (2u << 1);  // Compressed_Block, not the last
-    sb8[3] = static_cast<uint8_t>(hdr);
-    sb8[4] = static_cast<uint8_t>(hdr >> 8);
-    sb8[5] = static_cast<uint8_t>(hdr >> 16);
-    return total;
+    return o;
+}
+__device__ __forceinline__ uint32_t zstd_table(const uint32_t* cnt, uint32_t nsym, uint32_t maxlog, uint32_t nseq,
+                                               ZTab& t, int16_t* norm, uint8_t* desc, uint32_t lane) {
+    return zstd_table(cnt, nsym, maxlog, nseq, t.st, t.dd, &t.al, norm, desc, lane);
+}
+
+// A block of the span: [3-byte header][literals section][sequences section]; offsets from the block.
+struct ZBlk {
+    uint32_t raw;        // input bytes
+    uint32_t nl, ns;     // literals, sequences
+    uint32_t q;          // literals per Huffman stream (the last takes the rest)
+    uint32_t nstr;       // Huffman streams: 1 or 4
+    uint32_t fbits;      // the sequences bitstream's bits (with the end marker); kZNone: too long
+    uint32_t fscr;       // where the bitstream was written first (16-byte aligned address)
+    uint32_t sbits[4];   // each Huffman stream's bits (with the end marker)
+    uint32_t role;       // kZr*
+    uint32_t body;       // bytes after the block header
+    uint32_t lh;         // the literals header's bytes
+    uint32_t lit0;       // where the raw literals / the first Huffman stream start
+    uint32_t soff[4];    // where each Huffman stream starts
+    uint32_t seq0;       // where the sequences section starts
+    uint32_t sh;         // the sequences section's header bytes (count, modes, descriptions)
+};
+constexpr uint32_t kZrCoded = 1, kZrHuff = 2, kZrTree = 4, kZrTables = 8;
+
+// KCDC_TRACE builds (tools/ztrace.py): thread 0's s_memtime at the phase ends, descriptor words 64..
+#ifdef KCDC_TRACE
+#define KCDC_ZSTAMP(i)                                                                                  \
+    do {                                                                                              \
+        if (tid == 0)                                                                                 \
+            reinterpret_cast<uint64_t*>(a.desc + static_cast<uint64_t>(b) * kDescWords + 64u)[i] =   \
+                __builtin_amdgcn_s_memtime();                                                         \
+    } while (0)
+#else
+#define KCDC_ZSTAMP(i) \
+    do {               \
+    } while (0)
+#endif
+
+// One workgroup of 4 waves per span (zstd, effort >= 1), after lz_spans_kernel<kFmtZstd>.  Wave 0
+// does the per-segment work (lane = segment); waves 1..3 build the three FSE tables while wave 0
+// builds the Huffman code; each wave's lane 0 writes one block's sequences bitstream (the serial
+// part: four SIMDs instead of one).
+__global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
+    __shared__ uint32_t L[kLdsWords];
+    __shared__ uint32_t seqw[kZMaxSeq];
+    // H: the literal counts and the Huffman scratch, then the literal streams' edge records (per
+    // lane and stream: its first / last shared byte, index << 8 | bits)
+    __shared__ uint32_t H[256 + 256 + 128];
+    uint32_t* hist = H;
+    uint32_t* sa = H + 256;
+    uint16_t* ss = reinterpret_cast<uint16_t*>(H + 512);
+    uint32_t* rec = H;                     // 64 x 8
+    __shared__ uint32_t zc[256];           // Huffman code | bits << 16
+    __shared__ uint8_t lens[256];
+    __shared__ uint32_t num[40];
+    __shared__ uint32_t fcnt[36 + 53 + 32];  // LL, ML, OF code counts
+    __shared__ ZTab tab[3];                  // LL, OF, ML (the description's order)
+    __shared__ int16_t fnorm[3][64];
+    __shared__ uint8_t fdesc[3][kZDesc];
+    __shared__ uint32_t fdlen[3];
+    __shared__ uint32_t ln_off[65], ln_nseq[64], ln_len[64], ln_nlit[64], ln_carry[64], ln_p[64], ln_prev[64];
+    __shared__ uint32_t ln_bits[64 * 4];
+    __shared__ ZBlk blk[kZBlks];
+    __shared__ uint32_t misc[2];             // [0]: the tree description's bytes (0: no Huffman), [1]: longest code
+    __shared__ uint8_t hdesc[128];           // the Huffman tree description (RFC 8878 §4.2.1)
+    __shared__ uint32_t llut[64], mlut[128];  // code | extra bits << 8 | baseline << 16 (ml: of ml - 3)
+    const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    const bool w0 = wv == 0u;
+    const uint32_t total = a.spans[a.n];
+    if (total > a.max_spans || b >= total) return;
+    const uint32_t c = span_chunk(a, b);
+    const uint32_t u = b - a.spans[c];
+    const uint64_t len = a.in_lens[c];
+    const uint64_t sb = static_cast<uint64_t>(u) * kSpan;
+    const uint32_t span_len = static_cast<uint32_t>(len - sb < kSpan ? len - sb : kSpan);
+    KCDC_ZSTAMP(0);
+    const uint32_t d = stage_span(L, a.in + a.in_offs[c] + sb, span_len, tid, 256u);
+    const uint32_t x0 = kSeg * lane;
+    const uint32_t seg_len = x0 < span_len ? min(kSeg, span_len - x0) : 0u, xe = x0 + seg_len;
+    const uint32_t nseq = seg_len && w0 ? a.desc[static_cast<uint64_t>(b) * kDescWords + lane] : 0u;
+    const uint32_t k = lane / kZBlkSegs, lead = k * kZBlkSegs;  // the lane's block, its first lane
+    hist[tid] = 0u;
+    if (tid < 36u + 53u + 32u) fcnt[tid] = 0u;
+    if (w0) {
+        uint32_t cc, nn, xx;
+        ll_code(lane, cc, nn, xx);
+        llut[lane] = cc | (nn << 8) | ((lane - xx) << 16);
+        for (uint32_t m = lane; m < 128u; m += 64u) {
+            ml_code(m + 3u, cc, nn, xx);
+            mlut[m] = cc | (nn << 8) | ((m - xx) << 16);
+        }
+    }
+    // the span's sequences in order (lane-major), each lane's literal count and trailing literals
+    uint32_t incl = nseq;
+    for (uint32_t o = 1; o < 64u; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const uint32_t off = incl - nseq;
+    const uint32_t* sq = reinterpret_cast<const uint32_t*>(a.slots + (static_cast<uint64_t>(b) * 64u + lane) * kSlot);
+    uint32_t covered = 0, matched = 0;
+    for (uint32_t j = 0; j < nseq; j++) {  // (wave 0 only: nseq is 0 in the others)
+        const uint32_t v = sq[143u - j];
+        seqw[off + j] = v;
+        const uint32_t ml = zseq_ml(v);
+        covered += zseq_ll(v) + ml;
+        matched += ml;
+    }
+    const uint32_t nlit = seg_len - matched, tail = seg_len - covered;
+    // the lane's first literal's index in its block
+    uint32_t pin = nlit;
+    for (uint32_t o = 1; o < kZBlkSegs; o <<= 1) {
+        const uint32_t y = __shfl_up(pin, o, 64);
+        if (lane - lead >= o) pin += y;
+    }
+    // the nearest earlier segment with sequences (0 if none: never followed past a block's first)
+    const uint64_t nz = __ballot(nseq != 0u) & ((1ull << lane) - 1ull);
+    if (w0) {
+        ln_off[lane] = off;
+        if (lane == 63u) ln_off[64] = incl;
+        ln_nseq[lane] = nseq;
+        ln_prev[lane] = nz ? 63u - static_cast<uint32_t>(__builtin_clzll(nz)) : 0u;
+        ln_len[lane] = seg_len;
+        ln_nlit[lane] = nlit;
+        ln_carry[lane] = tail;  // (becomes the carry below)
+        ln_p[lane] = pin - nlit;
+    }
+    __syncthreads();
+    if (tid == 0) {  // literals pending before each segment's first sequence, within its block
+        uint32_t cy = 0;
+        for (uint32_t j = 0; j < 64u; j++) {
+            if (j % kZBlkSegs == 0u) cy = 0u;
+            const uint32_t t = ln_carry[j];
+            ln_carry[j] = cy;
+            cy = ln_nseq[j] ? t : cy + ln_len[j];
+        }
+    }
+    __syncthreads();
+    KCDC_ZSTAMP(1);
+    // the lane's literals, first to last, as byte values: runs read 4 bytes at a time
+    auto lits_fwd = [&](auto f) {
+        auto run = [&](uint32_t x, uint32_t e) {
+            for (; x + 4u <= e; x += 4u) {
+                const uint32_t w = st_ld32(L, d, x);
+                f(w & 255u);
+                f((w >> 8) & 255u);
+                f((w >> 16) & 255u);
+                f(w >> 24);
+            }
+            for (; x < e; x++) f(st_byte(L, d, x));
+        };
+        uint32_t x = x0;
+        for (uint32_t j = 0; j < nseq; j++) {
+            const uint32_t v = seqw[off + j], ll = zseq_ll(v);
+            run(x, x + ll);
+            x += ll + zseq_ml(v);
+        }
+        run(x, xe);
+    };
+    // the codes of the lane's sequences: the carry joins the first literal length; offset value 1
+    // for the previous sequence's distance (same block, literal length > 0), else distance + 3
+    if (w0) {
+        lits_fwd([&](uint32_t v) { atomicAdd(&hist[v], 1u); });
+        const uint32_t blk0 = ln_off[lead];
+        const uint32_t cy = ln_carry[lane];
+        for (uint32_t j = 0; j < nseq; j++) {
+            const uint32_t i = off + j, v = seqw[i];
+            const uint32_t ll = zseq_ll(v) + (j == 0u ? cy : 0u), dist = v & 0x7FFFu;
+            const bool rep = i > blk0 && ll > 0u && (seqw[i - 1u] & 0x7FFFu) == dist;
+            uint32_t llc, llb, llx, mlc, mlb, mlx;
+            ll_code(ll, llc, llb, llx);
+            ml_code(zseq_ml(v), mlc, mlb, mlx);
+            atomicAdd(&fcnt[llc], 1u);
+            atomicAdd(&fcnt[36u + mlc], 1u);
+            atomicAdd(&fcnt[89u + (rep ? 0u : 31u - static_cast<uint32_t>(__builtin_clz(dist + 3u)))], 1u);
+        }
+    }
+    __syncthreads();
+    KCDC_ZSTAMP(2);
+    // The span's Huffman code and its description (RFC 8878 §4.2.1): the weights of symbols
+    // 0..top-1 (the last one's is implied) FSE-compressed (zstd's HUF_compressWeights: one table,
+    // two interleaved states) when that is smaller or when top > 128, else direct 4-bit weights.
+    // No Huffman literals when neither applies (e.g. all weights equal: random bytes).
+    uint32_t used = 0, top = 0;
+    for (uint32_t i = 0; i < 256u; i += 64u) {
+        const uint64_t m = __ballot(hist[i + lane] != 0u);
+        used += static_cast<uint32_t>(__popcll(m));
+        if (m) top = i + 63u - static_cast<uint32_t>(__builtin_clzll(m));
+    }
+    // Worth a code at all?  The literals' order-0 entropy against 8 bits each: a span whose
+    // literals are near-uniform (random data) would save less than a description costs.
+    float ent = 0.f;
+    uint32_t nl_span = 0;
+    for (uint32_t i = lane; i < 256u; i += 64u) {
+        const uint32_t cv = hist[i];
+        nl_span += cv;
+        ent += cv ? static_cast<float>(cv) * __log2f(static_cast<float>(cv)) : 0.f;
+    }
+    for (uint32_t o = 32; o > 0; o >>= 1) {
+        nl_span += static_cast<uint32_t>(__shfl_xor(nl_span, static_cast<int>(o), 64));
+        ent += __shfl_xor(ent, static_cast<int>(o), 64);
+    }
+    // bits = N log2 N - sum c log2 c; a Huffman code is within ~3 % of it here
+    const float hbits = nl_span ? static_cast<float>(nl_span) * __log2f(static_cast<float>(nl_span)) - ent : 0.f;
+    const bool try_huff = used >= 2u && 1.02f * hbits / 8.f + 40.f < static_cast<float>(nl_span);
+    const uint32_t nseq_span = ln_off[64];
+    __syncthreads();  // every wave has read the counts (wave 0 reuses their space below)
+    if (w0 && try_huff) {
+        huff_lengths(hist, 256u, 11u, lens, sa, ss, num, lane);
+        // codes: by weight ascending (longest first), then symbol (RFC 8878 §4.2.1.4); each
+        // weight's codes start where the lighter weights' end, ranks within a weight by ballot
+        uint32_t maxb = 0;
+        for (uint32_t i = lane; i <= top; i += 64u) maxb = max(maxb, static_cast<uint32_t>(lens[i]));
+        for (uint32_t o = 32; o > 0; o >>= 1) maxb = max(maxb, static_cast<uint32_t>(__shfl_xor(maxb, static_cast<int>(o), 64)));
+        uint32_t start[12];
+        {
+            uint32_t acc = 0;  // in 2^(w-1) cells
+#pragma unroll
+            for (uint32_t w = 1; w < 12u; w++) {
+                uint32_t cw = 0;
+                for (uint32_t i = 0; i <= top; i += 64u) {
+                    const uint32_t l = i + lane <= top ? lens[i + lane] : 0u;
+                    cw += static_cast<uint32_t>(__popcll(__ballot(l && maxb + 1u - l == w)));
+                }
+                start[w] = w <= maxb ? acc >> (w - 1u) : 0u;
+                acc += w <= maxb ? cw << (w - 1u) : 0u;
+            }
+        }
+        const uint64_t lt = (1ull << lane) - 1ull;
+        for (uint32_t i = 0; i <= top; i += 64u) {
+            const uint32_t sy = i + lane, l = sy <= top ? lens[sy] : 0u, w = l ? maxb + 1u - l : 0u;
+            uint32_t code = 0;
+#pragma unroll
+            for (uint32_t j = 1; j < 12u; j++) {
+                const uint64_t m = __ballot(w == j);
+                if (w == j) code = start[j] + static_cast<uint32_t>(__popcll(m & lt));
+                start[j] += static_cast<uint32_t>(__popcll(m));
+            }
+            if (sy <= top) zc[sy] = l ? (code | (l << 16)) : 0u;
+        }
+        if (lane == 0) misc[1] = maxb;
+        // the weights' table in H (the counts there are spent): 32 states, 12 symbols
+        uint16_t* wst = reinterpret_cast<uint16_t*>(H);
+        uint2* wdd = reinterpret_cast<uint2*>(H + 16);
+        uint32_t* wal = H + 40;
+        int16_t* wnorm = reinterpret_cast<int16_t*>(H + 48);
+        uint32_t* wcnt = H + 64;
+        if (lane < 16u) wcnt[lane] = 0u;
+        wave_sync();
+        auto wt = [&](uint32_t sy) -> uint32_t { return lens[sy] ? maxb + 1u - lens[sy] : 0u; };
+        for (uint32_t sy = lane; sy < top; sy += 64u) atomicAdd(&wcnt[wt(sy)], 1u);
+        wave_sync();
+        uint32_t wmax = lane < 12u ? wcnt[lane] : 0u;
+        for (uint32_t o = 32; o > 0; o >>= 1) wmax = max(wmax, static_cast<uint32_t>(__shfl_xor(wmax, static_cast<int>(o), 64)));
+        const bool fse_ok = top >= 3u && wmax < top;  // >= 2 distinct weights (one value: an RLE case)
+        const uint32_t nc = fse_ok ? zstd_table(wcnt, 12u, 5u, top, wst, wdd, wal, wnorm, hdesc + 1, lane) : 0u;
+        if (lane == 0) {
+            const uint32_t direct = top <= 128u ? 1u + (top + 1u) / 2u : 0u;
+            uint32_t fsz = 0;
+            if (fse_ok) {  // backwards, two states (FSE_compress_usingCTable): the decoder reads state 1 first
+                uint64_t bb = 0;
+                uint32_t nb = 0, o = 1u + nc;
+                auto put = [&](uint32_t x, uint32_t n) {
+                    bb |= static_cast<uint64_t>(x) << nb;
+                    nb += n;
+                    while (nb >= 8u) {
+                        if (o < 128u) hdesc[o] = static_cast<uint8_t>(bb);
+                        o++;
+                        bb >>= 8;
+                        nb -= 8u;
+                    }
+                };
+                auto initw = [&](uint32_t sy) -> uint32_t {
+                    const uint2 e = wdd[sy];
+                    const uint32_t nbo = (e.x + (1u << 15)) >> 16;
+                    const uint32_t s0 = (nbo << 16) - e.x;
+                    return wst[(s0 >> nbo) + e.y];
+                };
+                auto encw = [&](uint32_t& st, uint32_t sy) {
+                    const uint2 e = wdd[sy];
+                    const uint32_t nbo = (st + e.x) >> 16;
+                    put(st & ((1u << nbo) - 1u), nbo);
+                    st = wst[(st >> nbo) + e.y];
+                };
+                uint32_t i = top, s1, s2;
+                if (top & 1u) {
+                    s1 = initw(wt(--i));
+                    s2 = initw(wt(--i));
+                    encw(s1, wt(--i));
+                } else {
+                    s2 = initw(wt(--i));
+                    s1 = initw(wt(--i));
+                }
+                for (bool two = true; i > 0u; two = !two) encw(two ? s2 : s1, wt(--i));
+                const uint32_t wa = *wal;
+                put(s2 & ((1u << wa) - 1u), wa);
+                put(s1 & ((1u << wa) - 1u), wa);
+                put(1u, 1);  // end marker
+                if (nb) put(0u, 8u - nb);
+                if (o < 128u) fsz = o;
+            }
+            uint32_t tsz = 0;
+            if (fsz && (!direct || fsz < direct)) {
+                hdesc[0] = static_cast<uint8_t>(fsz - 1u);  // < 128: FSE-compressed weights of that size
+                tsz = fsz;
+            } else if (direct) {  // direct weights: W = maxb + 1 - bits (0: unused), high nibble first
+                hdesc[0] = static_cast<uint8_t>(127u + top);
+                for (uint32_t j = 0; 2u * j < top; j++)
+                    hdesc[1u + j] = static_cast<uint8_t>((wt(2u * j) << 4) | (2u * j + 1u < top ? wt(2u * j + 1u) : 0u));
+                tsz = direct;
+            }
+            misc[0] = tsz;
+        }
+    }
+    if (!w0 && nseq_span) {  // the LL, OF, ML tables, one per wave (at the same time as the Huffman code)
+        const uint32_t t = wv - 1u;
+        const uint32_t r = zstd_table(fcnt + (t == 0u ? 0u : t == 1u ? 89u : 36u), t == 0u ? 36u : t == 1u ? 32u : 53u,
+                                      t == 1u ? 8u : 9u, nseq_span, tab[t], fnorm[t], fdesc[t], lane);
+        if (lane == 0) fdlen[t] = r;
+    }
+    __syncthreads();
+    KCDC_ZSTAMP(3);
+    KCDC_ZSTAMP(4);
+    const uint32_t tsz = try_huff ? misc[0] : 0u;  // the tree description's bytes
+    const bool huff = tsz != 0u;
+    rec[tid] = kZNone;
+    rec[tid + 256u] = kZNone;
+    // literal streams: each lane's bits per stream of its block
+    const uint32_t p = ln_p[lane];
+    uint32_t nl_blk = 0;
+    for (uint32_t j = lead; j < lead + kZBlkSegs; j++) nl_blk += ln_nlit[j];
+    const uint32_t nstr = nl_blk > 1023u ? 4u : 1u;
+    const uint32_t qn = nstr == 4u ? (nl_blk + 3u) / 4u : (nl_blk ? nl_blk : 1u);
+    uint32_t bits[4] = {0u, 0u, 0u, 0u};
+    if (w0 && huff && nlit) {
+        uint32_t idx = p, q = p / qn, nextb = (q + 1u) * qn;
+        lits_fwd([&](uint32_t v) {
+            if (idx == nextb && q < 3u) {
+                q++;
+                nextb += qn;
+            }
+            bits[q] += zc[v] >> 16;
+            idx++;
+        });
+    }
+    if (w0)
+        for (uint32_t q = 0; q < 4u; q++) ln_bits[lane * 4u + q] = bits[q];
+    __syncthreads();
+    KCDC_ZSTAMP(5);
+    const uint32_t ns_blk = ln_off[lead + kZBlkSegs] - ln_off[lead];
+    const uint32_t tdesc = nseq_span ? fdlen[0] + fdlen[1] + fdlen[2] : 0u;
+    uint8_t* R = a.slots + (static_cast<uint64_t>(b) * 64u + lead) * kSlot + kZOff;  // the block's bytes
+    if (w0 && lane == lead) {
+        ZBlk& B = blk[k];
+        uint32_t raw = 0;
+        for (uint32_t j = lead; j < lead + kZBlkSegs; j++) raw += ln_len[j];
+        B.raw = raw;
+        B.nl = nl_blk;
+        B.ns = ns_blk;
+        B.q = qn;
+        B.nstr = nstr;
+        uint32_t lit = (nl_blk < 32u ? 1u : nl_blk < 4096u ? 2u : 3u) + nl_blk;  // raw literals
+        for (uint32_t q = 0; q < 4u; q++) {
+            uint32_t s = 0;
+            for (uint32_t j = lead; j < lead + kZBlkSegs; j++) s += ln_bits[j * 4u + q];
+            B.sbits[q] = s + 1u;
+        }
+        if (huff && nl_blk) {  // the Huffman section with the tree: a bound on any literals section chosen
+            uint32_t cs = tsz + (nstr == 4u ? 6u : 0u);
+            for (uint32_t q = 0; q < nstr; q++) cs += (B.sbits[q] + 7u) / 8u;
+            lit = min(lit, 5u + cs);
+        }
+        // The bitstream goes first to a scratch place above any layout the choices below can
+        // give (then moves down); a stream that would not fit the block's bytes from there makes
+        // the block raw: it exceeds the block's own size (the literals bound above is at most the
+        // tree's bytes over the section chosen).
+        B.fscr = ((3u + 3u + lit + 3u + tdesc + kZOff + 15u) & ~15u) - kZOff;
+        B.fbits = 0u;
+    }
+    __syncthreads();
+    if (lane == 0 && blk[wv].ns) {  // wave wv: block wv's sequences bitstream
+        ZBlk& B = blk[wv];
+        const uint32_t lead = wv * kZBlkSegs, fs = B.fscr;
+        uint8_t* R = a.slots + (static_cast<uint64_t>(b) * 64u + lead) * kSlot + kZOff;
+        {
+            uint32_t* dst = reinterpret_cast<uint32_t*>(R + fs);
+            const uint32_t lim = (kZRegion - fs - 40u) / 4u;  // words (the loop stops within 7 of it)
+            uint64_t bb = 0;
+            uint32_t nb = 0, o = 0, tb = 0;
+            // x < 2^n; the current word is stored every time (no branch), and kept once full
+            auto put = [&](uint32_t x, uint32_t n) {
+                tb += n;
+                bb |= static_cast<uint64_t>(x) << nb;
+                nb += n;
+                dst[o] = static_cast<uint32_t>(bb);
+                const bool full = nb >= 32u;
+                o += full ? 1u : 0u;
+                bb = full ? bb >> 32 : bb;
+                nb -= full ? 32u : 0u;
+            };
+            const ZTab &tLL = tab[0], &tOF = tab[1], &tML = tab[2];
+            // Sequence ii's codes and table entries: literal length (with its segment's carry when
+            // it is the segment's first), match length, offset value; extras x1 = ll | ml << llb,
+            // x2 = of.  Independent of the states: computed one sequence ahead, so the loop's
+            // critical path is the state chain (one LDS read per field and sequence).
+            struct ZC {
+                uint32_t ofc, x1, n1, x2;
+                uint2 eLL, eML, eOF;
+            };
+            const uint32_t i0 = ln_off[lead];
+            auto mk = [&](uint32_t ii, uint32_t v, uint32_t pv, uint32_t cy) -> ZC {
+                const uint32_t ll = zseq_ll(v) + cy, dist = v & 0x7FFFu, m = zseq_ml(v) - 3u;
+                const uint32_t ov = ii > i0 && ll > 0u && (pv & 0x7FFFu) == dist ? 1u : dist + 3u;
+                const uint32_t tl = llut[min(ll, 63u)], hl = 31u - static_cast<uint32_t>(__builtin_clz(ll | 1u));
+                const uint32_t tm = mlut[min(m, 127u)], hm = 31u - static_cast<uint32_t>(__builtin_clz(m));
+                const bool bl = ll >= 64u, bm = m >= 128u;
+                const uint32_t llc = bl ? hl + 19u : (tl & 255u);
+                const uint32_t llb = bl ? hl : ((tl >> 8) & 255u);
+                const uint32_t llx = ll - (bl ? (1u << hl) : (tl >> 16));
+                const uint32_t mlc = bm ? hm + 36u : (tm & 255u);
+                const uint32_t mlb = bm ? hm : ((tm >> 8) & 255u);
+                const uint32_t mlx = m - (bm ? (1u << hm) : (tm >> 16));
+                const uint32_t ofc = 31u - static_cast<uint32_t>(__builtin_clz(ov));
+                return ZC{ofc, llx | (mlx << llb), llb + mlb, ov - (1u << ofc), tLL.dd[llc], tML.dd[mlc], tOF.dd[ofc]};
+            };
+            // the segment of sequence ii (called for ii descending by one): its first sequence's
+            // index lo; a step below it goes to the previous segment with sequences
+            uint32_t l = lead + kZBlkSegs - 1u;
+            if (ln_nseq[l] == 0u) l = ln_prev[l];
+            uint32_t lo = ln_off[l];
+            auto seg_of = [&](uint32_t ii) {
+                if (ii < lo) {
+                    l = ln_prev[l];
+                    lo = ln_off[l];
+                }
+            };
+            uint32_t i = ln_off[lead + kZBlkSegs] - 1u;
+            uint32_t w1 = seqw[i > i0 ? i - 1u : i0];       // sequence i - 1's word
+            ZC c = mk(i, seqw[i], w1, i == lo ? ln_carry[l] : 0u);
+            // the block's last sequence: the initial states
+            auto init = [&](const ZTab& t, uint2 e) -> uint32_t {
+                const uint32_t nbo = (e.x + (1u << 15)) >> 16;
+                const uint32_t s0 = (nbo << 16) - e.x;
+                return t.st[(s0 >> nbo) + e.y];
+            };
+            uint32_t sML = init(tML, c.eML);
+            uint32_t sOF = init(tOF, c.eOF);
+            uint32_t sLL = init(tLL, c.eLL);
+            put(c.x1, c.n1);  // the decoder reads offset, match length, literal length extras
+            put(c.x2, c.ofc);
+            uint32_t jn = i > i0 ? i - 1u : i0;  // the next sequence
+            seg_of(jn);
+            uint32_t w2 = seqw[jn > i0 ? jn - 1u : i0];
+            ZC n = mk(jn, w1, w2, jn == lo ? ln_carry[l] : 0u);
+            bool over = false;
+            // backwards (ZSTD_encodeSequences order): each earlier sequence's state bits (the
+            // decoder's updates after it: LL, ML, OF -> written OF, ML, LL), then its extras
+            while (i > i0) {
+                i--;
+                c = n;
+                const uint32_t nOF = (sOF + c.eOF.x) >> 16, nML = (sML + c.eML.x) >> 16, nLL = (sLL + c.eLL.x) >> 16;
+                const uint32_t bits = (sOF & ((1u << nOF) - 1u)) | ((sML & ((1u << nML) - 1u)) << nOF) |
+                                      ((sLL & ((1u << nLL) - 1u)) << (nOF + nML));
+                sOF = tOF.st[(sOF >> nOF) + c.eOF.y];
+                sML = tML.st[(sML >> nML) + c.eML.y];
+                sLL = tLL.st[(sLL >> nLL) + c.eLL.y];
+                jn = i > i0 ? i - 1u : i0;
+                seg_of(jn);
+                w1 = w2;
+                w2 = seqw[jn > i0 ? jn - 1u : i0];
+                n = mk(jn, w1, w2, jn == lo ? ln_carry[l] : 0u);
+                put(bits, nOF + nML + nLL);
+                put(c.x1, c.n1);
+                put(c.x2, c.ofc);
+                if (o > lim) {
+                    over = true;
+                    break;
+                }
+            }
+            const uint32_t am = tML.al, ao = tOF.al, ala = tLL.al;  // initial states, read LL, OF, ML
+            put((sML & ((1u << am) - 1u)) | ((sOF & ((1u << ao) - 1u)) << am), am + ao);
+            put(sLL & ((1u << ala) - 1u), ala);
+            put(1u, 1);  // end marker
+            B.fbits = over ? kZNone : tb;
+        }
+    }
+    __syncthreads();
+    KCDC_ZSTAMP(6);
+    if (tid == 0) {  // each block: raw or compressed, which carries the tree / the tables; sizes
+        bool tree_sent = false, tables_sent = false;
+        uint32_t bytes = 0;
+        for (uint32_t kb = 0; kb < kZBlks; kb++) {
+            ZBlk& B = blk[kb];
+            B.role = 0u;
+            B.body = 0u;
+            if (B.raw == 0u) continue;
+            const uint32_t n = B.nl;
+            const uint32_t rawlh = n < 32u ? 1u : n < 4096u ? 2u : 3u;
+            uint32_t lit = rawlh + n, lh = rawlh, use = 0u;
+            if (huff && n) {
+                uint32_t cs = (tree_sent ? 0u : tsz) + (B.nstr == 4u ? 6u : 0u);
+                for (uint32_t q = 0; q < B.nstr; q++) cs += (B.sbits[q] + 7u) / 8u;
+                const uint32_t hlh = B.nstr == 1u ? (cs <= 1023u ? 3u : 0u) : (n <= 16383u && cs <= 16383u ? 4u : 5u);
+                if (hlh && hlh + cs < lit) {
+                    lit = hlh + cs;
+                    lh = hlh;
+                    use = kZrHuff | (tree_sent ? 0u : kZrTree);
+                }
+            }
+            const bool tables = B.ns && !tables_sent;
+            const uint32_t sh = B.ns == 0u ? 1u : (B.ns < 128u ? 1u : 2u) + 1u + (tables ? tdesc : 0u);
+            const uint32_t body = B.fbits == kZNone ? kZNone : lit + sh + (B.fbits + 7u) / 8u;
+            if (body < B.raw) {
+                B.role = kZrCoded | use | (tables ? kZrTables : 0u);
+                B.body = body;
+                B.lh = lh;
+                B.sh = sh;
+                uint32_t o = 3u + lh + ((use & kZrTree) ? tsz : 0u);
+                if ((use & kZrHuff) && B.nstr == 4u) o += 6u;
+                B.lit0 = o;
+                if (use & kZrHuff) {
+                    for (uint32_t q = 0; q < B.nstr; q++) {
+                        B.soff[q] = o;
+                        o += (B.sbits[q] + 7u) / 8u;
+                    }
+                } else {
+                    o += n;
+                }
+                B.seq0 = o;
+                if (use & kZrHuff) tree_sent = true;
+                if (B.ns) tables_sent = true;
+                bytes += 3u + body;
+            } else {
+                bytes += kZStoredHdr + B.raw;
+            }
+        }
+        a.span_bytes[b] = bytes;
+#ifdef KCDC_TRACE
+        {  // the span's byte budget (tools/ztrace.py): words 84.. of its descriptor
+            uint32_t* tw = a.desc + static_cast<uint64_t>(b) * kDescWords + 84u;
+            uint32_t st[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};  // raw blocks' bytes, literal sections,
+            // sequence bitstreams, table descriptions, trees, headers (block + literals + sequences), literals, sequences
+            for (uint32_t kb = 0; kb < kZBlks; kb++) {
+                const ZBlk& B = blk[kb];
+                if (B.raw == 0u) continue;
+                if (!(B.role & kZrCoded)) {
+                    st[0] += B.raw + 3u;
+                    continue;
+                }
+                st[1] += B.seq0 - 3u - B.lh - ((B.role & kZrTree) ? tsz : 0u);
+                st[2] += B.ns ? (B.fbits + 7u) / 8u : 0u;
+                st[3] += (B.role & kZrTables) ? tdesc : 0u;
+                st[4] += (B.role & kZrTree) ? tsz : 0u;
+                st[5] += 3u + B.lh + (B.ns ? B.sh - ((B.role & kZrTables) ? tdesc : 0u) : 1u);
+                st[6] += B.nl;
+                st[7] += B.ns;
+            }
+            for (uint32_t i = 0; i < 8u; i++) tw[i] = st[i];
+        }
+#endif
+    }
+    __syncthreads();
+    KCDC_ZSTAMP(7);
+    const ZBlk& B = blk[k];
+    if (w0 && (B.role & kZrCoded)) {
+        if (!(B.role & kZrHuff)) {  // raw literals at their index
+            uint32_t idx = B.lit0 + p;
+            lits_fwd([&](uint32_t v) { R[idx++] = static_cast<uint8_t>(v); });
+        } else if (nlit) {
+            // each stream holds its literals last to first: this lane's part of stream q starts
+            // after the bits of the block's later lanes; bytes it shares go to edge records
+            uint32_t bo[4];
+            for (uint32_t q = 0; q < 4u; q++) {
+                uint32_t s = 0;
+                for (uint32_t j = lane + 1u; j < lead + kZBlkSegs; j++) s += ln_bits[j * 4u + q];
+                bo[q] = s;
+            }
+            uint32_t idx = p + nlit, q = 4u;
+            uint64_t bb = 0;
+            uint32_t nb = 0, bi = 0, b0 = 0;
+            auto close = [&]() {  // the part's last byte, when partial
+                if (q < 4u && nb) rec[lane * 8u + q * 2u + 1u] = (bi << 8) | static_cast<uint32_t>(bb & 255u);
+            };
+            auto lit = [&](uint32_t x) {
+                idx--;
+                const uint32_t qq = B.nstr == 1u ? 0u : min(idx / B.q, 3u);
+                if (qq != q) {
+                    close();
+                    q = qq;
+                    b0 = bo[q];
+                    bi = b0 >> 3;
+                    nb = b0 & 7u;
+                    bb = 0;
+                }
+                const uint32_t cw = zc[st_byte(L, d, x)];
+                bb |= static_cast<uint64_t>(cw & 0xFFFFu) << nb;
+                nb += cw >> 16;
+                while (nb >= 8u) {
+                    const uint8_t v = static_cast<uint8_t>(bb);
+                    if (bi == (b0 >> 3) && (b0 & 7u))
+                        rec[lane * 8u + q * 2u] = (bi << 8) | v;  // shared with the part before
+                    else
+                        R[B.soff[q] + bi] = v;
+                    bi++;
+                    bb >>= 8;
+                    nb -= 8u;
+                }
+            };
+            // backwards: trailing literals, then each sequence's literals
+            uint32_t xm = x0;
+            for (uint32_t j = 0; j < nseq; j++) {
+                const uint32_t v = seqw[off + j];
+                xm += zseq_ll(v) + zseq_ml(v);
+            }
+            for (uint32_t x = xe; x > xm; x--) lit(x - 1u);
+            for (uint32_t j = nseq; j-- > 0u;) {
+                const uint32_t v = seqw[off + j];
+                xm -= zseq_ml(v);
+                for (const uint32_t e = xm - zseq_ll(v); xm > e; xm--) lit(xm - 1u);
+            }
+            close();
+        }
+        // the sequences bitstream down to its place (dst <= src: 256-byte steps, each read before
+        // it is written, never overlap an unread byte)
+        if (B.ns) {
+            const uint32_t n = (B.fbits + 7u) / 8u;
+            const uint8_t* src = R + B.fscr;
+            uint8_t* dst = R + B.seq0 + B.sh;
+            const uint32_t t = (lane - lead) * 16u;
+            for (uint32_t o = 0; o < n; o += 256u) {
+                const uint4 w = *reinterpret_cast<const uint4*>(src + o + t);
+                const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (uint32_t j = 0; j < 16u; j++)
+                    if (o + t + j < n) dst[o + t + j] = static_cast<uint8_t>(wv[j >> 2] >> (8u * (j & 3u)));
+            }
+        }
+    }
+    __syncthreads();
+    KCDC_ZSTAMP(8);
+    if (w0 && lane == lead && (B.role & kZrCoded)) {
+        const uint32_t hdr = (B.body << 3) | (2u << 1);  // Compressed_Block, not the last
+        R[0] = static_cast<uint8_t>(hdr);
+        R[1] = static_cast<uint8_t>(hdr >> 8);
+        R[2] = static_cast<uint8_t>(hdr >> 16);
+        const uint32_t n = B.nl;
+        if (B.role & kZrHuff) {
+            const uint32_t typ = (B.role & kZrTree) ? 2u : 3u;  // Compressed / Treeless_Literals_Block
+            const uint64_t cs = B.seq0 - 3u - B.lh, nn = n;
+            const uint64_t lh = B.nstr == 1u ? (typ | (nn << 4) | (cs << 14))
+                               : B.lh == 4u ? (typ | (2u << 2) | (nn << 4) | (cs << 18))
+                                            : (typ | (3u << 2) | (nn << 4) | (cs << 22));
+            for (uint32_t i = 0; i < B.lh; i++) R[3u + i] = static_cast<uint8_t>(lh >> (8u * i));
+            uint32_t o = 3u + B.lh;
+            if (B.role & kZrTree)
+                for (uint32_t i = 0; i < tsz; i++) R[o++] = hdesc[i];
+            if (B.nstr == 4u)
+                for (uint32_t q = 0; q < 3u; q++) {
+                    const uint32_t sz = (B.sbits[q] + 7u) / 8u;
+                    R[o++] = static_cast<uint8_t>(sz);
+                    R[o++] = static_cast<uint8_t>(sz >> 8);
+                }
+            // the shared bytes: every lane's edge records in bit order, OR-ed, then each stream's
+            // end marker (its highest bit) and zero padding
+            for (uint32_t q = 0; q < B.nstr; q++) {
+                uint32_t cur = kZNone, val = 0;
+                auto flush = [&]() {
+                    if (cur != kZNone) R[B.soff[q] + cur] = static_cast<uint8_t>(val);
+                };
+                auto add = [&](uint32_t r) {
+                    if (r == kZNone) return;
+                    if ((r >> 8) != cur) {
+                        flush();
+                        cur = r >> 8;
+                        val = 0;
+                    }
+                    val |= r & 255u;
+                };
+                for (uint32_t l = lead + kZBlkSegs; l-- > lead;) {
+                    add(rec[l * 8u + q * 2u]);
+                    add(rec[l * 8u + q * 2u + 1u]);
+                }
+                const uint32_t mb = B.sbits[q] - 1u;  // the marker's bit
+                add(((mb >> 3) << 8) | (1u << (mb & 7u)));
+                flush();
+            }
+        } else {
+            const uint32_t rh = n < 32u ? (n << 3) : n < 4096u ? (0x4u | (n << 4)) : (0xCu | (n << 4));
+            for (uint32_t i = 0; i < B.lh; i++) R[3u + i] = static_cast<uint8_t>(rh >> (8u * i));
+        }
+        uint32_t o = B.seq0;
+        const uint32_t ns = B.ns;
+        if (ns < 128u) {
+            R[o++] = static_cast<uint8_t>(ns);
+        } else {
+            R[o++] = static_cast<uint8_t>(128u + (ns >> 8));
+            R[o++] = static_cast<uint8_t>(ns);
+        }
+        if (ns) {
+            const uint32_t m = (B.role & kZrTables) ? 2u : 3u;  // FSE_Compressed_Mode / Repeat_Mode
+            R[o++] = static_cast<uint8_t>((m << 6) | (m << 4) | (m << 2));
+            if (B.role & kZrTables)
+                for (uint32_t t = 0; t < 3u; t++)
+                    for (uint32_t i = 0; i < fdlen[t]; i++) R[o++] = fdesc[t][i];
+        }
+    }
+    if (w0)
+        a.seglen[b * 64u + lane] = lane != lead || B.raw == 0u ? 0u : (B.role & kZrCoded) ? 3u + B.body : (kStored | B.raw);
+    __syncthreads();
+    KCDC_ZSTAMP(9);
 }
 
 // One wave per span: blockIdx.x = global span index.  FMT: kFmtDeflate or kFmtS2 (the parse is
@@ -970,7 +1706,7 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
     __shared__ uint32_t L[kLdsWords];
     __shared__ uint16_t tab[(1u << kHashBits) * 64u];
     __shared__ uint32_t ftab[1u << kFirstBits];
-    __shared__ uint32_t hist[FMT == kFmtDeflate ? kNSym : FMT == kFmtZstd ? 256 : 1];  // the span's symbol counts
+    __shared__ uint32_t hist[FMT == kFmtDeflate ? kNSym : 1];  // deflate: the span's symbol counts
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
     const uint32_t total = a.spans[a.n];
     if (total > a.max_spans || b >= total) return;
@@ -987,8 +1723,6 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
         for (uint32_t i = lane; i < (1u << kFirstBits); i += 64u) ftab[i] = ~0u;
         if constexpr (FMT == kFmtDeflate)
             for (uint32_t i = lane; i < kNSym; i += 64u) hist[i] = 0u;
-        if constexpr (FMT == kFmtZstd)
-            for (uint32_t i = lane; i < 256u; i += 64u) hist[i] = 0u;
     }
     __syncthreads();
     const uint8_t* Lb = reinterpret_cast<const uint8_t*>(L);
@@ -1012,7 +1746,6 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
     }
     uint32_t word = 0;  // the segment's length word (0: past the span's end)
     uint32_t nm = 0;    // deflate: the segment's match tokens; zstd: its sequences
-    uint32_t zlit = 0;  // zstd: its literals
     if (x0 < span_len) word = [&]() -> uint32_t {
     const uint32_t xe = span_len - x0 < kSeg ? span_len : x0 + kSeg;
     const uint32_t seg_len = xe - x0;
@@ -1027,6 +1760,8 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
     uint32_t fb = 3;  // deflate: the segment's size as one fixed-code block (bits), the stored/coded test
     uint32_t x = x0, lit = x0;
     auto literals = [&](uint32_t e) {
+        if constexpr (FMT == kFmtZstd)
+            if (a.effort >= 1u) return;  // zstd_emit_kernel takes the literals from the input
         if constexpr (FMT == kFmtS2) {  // one literal element: tag (n-1) << 2 | 0, 60: +1 byte, 61: +2
             if (e == lit) return;
             const uint32_t m = e - lit - 1u;
@@ -1071,7 +1806,7 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
     // Length of the match of x against an earlier q (>= 4 when the first 4 bytes agree), <= maxlen.
     auto match_len = [&](uint32_t q, uint32_t xx, uint32_t v) -> uint32_t {
         if (q >= xx || ld32(q) != v) return 0u;
-        const uint32_t cap = FMT == kFmtS2 ? kSeg : 258u;  // S2 copies have no length limit
+        const uint32_t cap = FMT == kFmtDeflate ? 258u : kSeg;  // S2 copies and zstd matches: the segment
         const uint32_t maxlen = xe - xx < cap ? xe - xx : cap;
         uint32_t n = 4;
         while (n + 4u <= maxlen) {
@@ -1110,7 +1845,7 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
         }
         if (a.effort >= 1u) {
             // candidates nearest first; none is tried once a match reaches the longest possible
-            const uint32_t full = min(xe - xx, FMT == kFmtS2 ? kSeg : 258u);
+            const uint32_t full = min(xe - xx, FMT == kFmtDeflate ? 258u : kSeg);
             auto offer = [&](uint32_t c) {  // longer, or as long and nearer
                 if (n >= full) return;
                 const uint32_t m = match_len(c, xx, v);
@@ -1168,7 +1903,7 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
             if constexpr (FMT == kFmtS2) {
                 s2_copy(n, x - cand);
             } else if constexpr (FMT == kFmtZstd) {  // (literal length, match length - 4, offset)
-                base[143u - nseq] = ((x - lit) << 23) | ((n - 4u) << 15) | (x - cand);
+                base[143u - nseq] = zseq_word(x - lit, n, x - cand);
                 nseq++;
             } else {  // deflate token; the fixed code's cost
                 base[nm++] = ((x - lit) << 23) | ((n - 3u) << 15) | (x - cand - 1u);
@@ -1188,17 +1923,17 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
         }
     }
     if constexpr (FMT == kFmtZstd) {
+        if (a.effort >= 1u) {  // zstd_emit_kernel codes the span (the sequences stay in the slot)
+            nm = nseq;
+            return seg_len;
+        }
         if (!over) literals(xe);  // the block's last literals (no sequence)
         if (over) return kStored | seg_len;
         const uint32_t nlit = 4u * static_cast<uint32_t>(w.op - (base + 2)) + (w.nb >> 3);
-        nm = nseq;
-        zlit = nlit;
         if (w.nb) *w.op = static_cast<uint32_t>(w.bb);
         uint8_t* sb8 = reinterpret_cast<uint8_t*>(base);
-        // The sequences section follows the raw literals.  With the span's Huffman pass to come
-        // (effort >= 1) only its size is taken here: zstd_huff_literals reads the sequence words
-        // again (literal positions) and writes the section after the literal section it chooses.
-        const uint32_t qs = zstd_seqs(sb8, 8u + nlit, nseq, seg_len, a.effort == 0u);
+        // zstd-fastest: one block per segment, the sequences section after the raw literals
+        const uint32_t qs = zstd_seqs(sb8, 8u + nlit, nseq, seg_len, true);
         if (qs == kZOver) return kStored | seg_len;
         const uint32_t total = 5u + nlit + qs;  // block header + literals section + sequences section
         if (total >= seg_len + kZStoredHdr) return kStored | seg_len;
@@ -1247,8 +1982,10 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
         return;
     }
     if constexpr (FMT == kFmtZstd)
-        if (a.effort >= 1u) word = zstd_huff_literals(a, b, lane, span_len, x0, word, nm, zlit, hist,
-                                                      reinterpret_cast<uint32_t*>(tab), L, d);
+        if (a.effort >= 1u) {
+            a.desc[static_cast<uint64_t>(b) * kDescWords + lane] = nm;
+            return;
+        }
     a.seglen[slot] = word;
     // The span's output bytes (stored segments: 5 + n, S2: 3 + n; S2 adds the framing header).
     const uint32_t shdr = FMT == kFmtS2 ? kS2StoredHdr : FMT == kFmtZstd ? kZStoredHdr : 5u;
@@ -1492,7 +2229,7 @@ __global__ __launch_bounds__(64) void deflate_copy_kernel(CompArgs a) {
     const uint32_t pos = incl - eff;
     for (uint32_t j = 0; j < 64u; j++) {
         const uint32_t wj = __shfl(word, j, 64), pj = __shfl(pos, j, 64);
-        if (wj == 0u) break;  // the rest of the span is past the chunk's end
+        if (wj == 0u) continue;  // past the chunk's end, or inside a zstd block of segments
         uint8_t* o = dst + pj;
         if ((wj & kStored) && zs) {  // Raw_Block: header (size << 3 | 0), then the bytes
             const uint32_t m = wj & ~kStored;
@@ -1845,6 +2582,7 @@ extern "C" int kcdc_compress_chunks_device(const char* name, const uint8_t* d_da
             hipLaunchKernelGGL(compdev::crc_spans_kernel<true>, cgrid, dim3(64 * compdev::kCrcWaves), 0, st, a);
         } else if (a.fmt == compdev::kFmtZstd) {
             hipLaunchKernelGGL(compdev::lz_spans_kernel<compdev::kFmtZstd>, grid, dim3(64), 0, st, a);
+            if (a.effort >= 1u) hipLaunchKernelGGL(compdev::zstd_emit_kernel, grid, dim3(256), 0, st, a);
         } else {
             hipLaunchKernelGGL(compdev::lz_spans_kernel<compdev::kFmtDeflate>, grid, dim3(64), 0, st, a);
         }

@@ -186,14 +186,15 @@ def test_s2_random_stream_is_stored(gpu):
 
 def test_zstd_random_stream_is_stored(gpu):
     """Config-2 bytes through zstd: one frame per chunk (magic, descriptor, 4-byte content size),
-    every 512-byte segment a Raw_Block (3-byte header), a final empty Raw_Block; ID NoCompression."""
+    every 8 KiB block of 16 segments a Raw_Block (3-byte header), a final empty Raw_Block; ID
+    NoCompression."""
     host = coracle.gen_stream(0x6B6F706961, 0, 8 << 20)
     lens = [1 << 20] * 8
     offs = [i << 20 for i in range(8)]
     out, oo, ol, ids = _compress("zstd", host, offs, lens, gpu)
     _check("zstd", host, offs, lens, out, oo, ol, ids)
     assert not ids.any()
-    assert all(int(x) == 4 + 9 + 2048 * (3 + 512) + 3 for x in ol)
+    assert all(int(x) == 4 + 9 + 128 * (3 + 8192) + 3 for x in ol)
 
 
 @pytest.mark.parametrize("name", ["s2-default", "zstd"])
@@ -224,3 +225,38 @@ def test_mixed_ratio_does_not_regress(gpu):
     assert ratio["deflate-best-compression"] <= ratio["deflate-default"] + 1e-3, ratio
     assert ratio["deflate-default"] <= 1.12 * z6, (ratio, z6)
     assert ratio["s2-default"] <= 1.25 * z6 and ratio["zstd"] <= 1.26 * z6, (ratio, z6)
+
+
+@pytest.mark.parametrize("name", ["zstd", "zstd-best-compression"])
+def test_zstd_table_carriers(name, gpu):
+    """Spans whose blocks (16 segments each) mix Raw_Blocks with compressed ones: the Huffman tree
+    and the FSE tables must ride on the first COMPRESSED block that uses them (a raw block 0, a
+    raw block between compressed ones, a literal-free block 0), later blocks reuse them (Treeless
+    literals, Repeat_Mode tables), and repeat offsets never reach back across a raw block.  Text
+    with literals above 128 takes the FSE-compressed weights description (RFC 8878 §4.2.1.2)."""
+    rng = np.random.default_rng(77)
+    rnd = lambda n: rng.integers(0, 256, n, dtype=np.uint8)
+    text = lambda n: _mixed(n, int(rng.integers(1 << 30)))[:n]
+    words = lambda n: np.frombuffer((b"kopia snapshot content chunk " * (n // 29 + 1))[:n], np.uint8)
+    per = np.frombuffer((bytes(range(7, 40)) * (1 + (1 << 16) // 33))[:1 << 16], np.uint8)
+    latin = [w.encode("latin-1") for w in ("été", "çà", "über", "naïve", "señor", "ÿ", "æther", " ", "\n")]
+    hitext = lambda n: np.frombuffer(b"".join(latin[int(i)] for i in rng.integers(0, len(latin), n))[:n], np.uint8)
+    parts = [
+        [rnd(8192), words(24576)],                             # block 0 raw, block 1 carries
+        [words(8192), rnd(8192), words(16384)],                # a raw block between
+        [np.zeros(8192, np.uint8), words(24576)],              # block 0: sequences, few literals
+        [rnd(8192), rnd(8192), rnd(8192), words(8192)],        # only the last block compresses
+        [per[:32768]],                                         # periodic: repeat offsets
+        [words(3000), rnd(5192), words(24576 + 777)],          # ragged last span
+        [text(70000)],
+        [np.zeros(32768, np.uint8)],                           # one literal symbol: no Huffman
+        [hitext(40000)],                                       # literals > 128: FSE-compressed weights
+        [rnd(3000), hitext(30000), rnd(100)],                  # every byte value in the span's code
+    ]
+    chunks = [np.concatenate(p) for p in parts]
+    host = np.concatenate(chunks)
+    lens = [c.size for c in chunks]
+    offs = list(np.cumsum([0] + lens[:-1]))
+    out, oo, ol, ids = _compress(name, host, [int(o) for o in offs], lens, gpu)
+    _check(name, host, [int(o) for o in offs], lens, out, oo, ol, ids)
+    assert (ids != 0).all(), ol

@@ -365,7 +365,7 @@ def main():
         print(f"blocks of {G:2d} segments, repeat offsets {'on ' if rep else 'off'}: ratio {tot / len(data):.4f}")
 
 
-if __name__ == "__main__" and len(sys.argv) <= 2:
+if __name__ == "__main__" and len(sys.argv) <= 2 and (len(sys.argv) < 2 or sys.argv[1] != "fseweights"):
     main()
 
 
@@ -637,9 +637,10 @@ def encode_chunk_t(data, G):
         if t:
             codes, desc = t
         blocks = []
-        prev_off = None
         for g0 in range(0, len(segs), G):
-            lits, seqs, carry = [], [], 0
+            # a block's first sequence names its offset: the block before it may become a
+            # Raw_Block, which leaves the decoder's repeat offsets where the last compressed one did
+            lits, seqs, carry, prev_off = [], [], 0, None
             for i in range(g0, min(g0 + G, len(segs))):
                 sq, tail = segs[i]
                 lits += seg_lits[i]
@@ -686,3 +687,99 @@ def main_t(mib):
 
 if __name__ == "__main__" and len(sys.argv) > 2 and sys.argv[2] == "tables":
     main_t(float(sys.argv[1]))
+
+
+# ---------------------------------------------------------------- FSE-compressed Huffman weights (round 6)
+def huff_desc_fse(lens):
+    """The tree description with FSE-compressed weights (RFC 8878 §4.2.1.2), as zstd's
+    HUF_compressWeights: weights of symbols 0..top-1 (the last one's is implied), one table
+    (accuracy log 5), two interleaved states written backwards; None when it does not apply."""
+    top = max(s for s in range(256) if lens[s])
+    maxb = max(lens)
+    w = [maxb + 1 - lens[s] if lens[s] else 0 for s in range(top)]
+    cnt = [0] * 12
+    for x in w:
+        cnt[x] += 1
+    if top < 3 or max(cnt) == top:
+        return None
+    norm = normalize(cnt, 5)
+    last = max(s for s in range(12) if norm[s])
+    nc = write_ncount(norm[:last + 1], 5)
+    t = CTable(norm, 5)
+    bw = BitW()
+    i = top
+    if top & 1:
+        i -= 1; s1 = t.init(w[i])
+        i -= 1; s2 = t.init(w[i])
+        i -= 1; s1 = t.enc(bw, s1, w[i])
+    else:
+        i -= 1; s2 = t.init(w[i])
+        i -= 1; s1 = t.init(w[i])
+    two = True
+    while i > 0:
+        i -= 1
+        if two:
+            s2 = t.enc(bw, s2, w[i])
+        else:
+            s1 = t.enc(bw, s1, w[i])
+        two = not two
+    bw.put(s2, 5)
+    bw.put(s1, 5)
+    body = nc + bw.close()
+    if len(body) >= 128:
+        return None
+    return bytes([len(body)]) + body
+
+
+def check_fse_weights(seed=3):
+    """Literal-only blocks whose code has literals above 128 (no direct weights possible), each
+    frame decoded by libzstd."""
+    import random
+    rnd = random.Random(seed)
+    for trial in range(200):
+        nsym = rnd.randint(3, 256)
+        syms = rnd.sample(range(256), nsym)
+        lits = [rnd.choice(syms) for _ in range(rnd.randint(50, 1000))]
+        lits += [max(syms)]
+        freq = [0] * 256
+        for c in lits:
+            freq[c] += 1
+        lens = huff_lengths(freq)
+        if lens is None:
+            continue
+        desc = huff_desc_fse(lens)
+        if desc is None:
+            continue
+        codes, _ = huff_table_any(lens)
+        ls = literals_section(lits, codes, desc)
+        if ls is None:
+            continue
+        body = ls + bytes([0])
+        blob = frame_header(len(lits)) + ((len(body) << 3) | (2 << 1) | 1).to_bytes(3, "little") + body
+        assert zstd_decode(blob) == bytes(lits), trial
+    print("fse weights: ok")
+
+
+def huff_table_any(lens):
+    """huff_table's codes without its top <= 128 limit."""
+    top = max(s for s in range(256) if lens[s])
+    maxb = max(lens)
+    w = [maxb + 1 - lens[s] if lens[s] else 0 for s in range(256)]
+    num = [0] * (maxb + 2)
+    for s in range(top + 1):
+        if w[s]:
+            num[w[s]] += 1
+    start, acc = [0] * (maxb + 2), 0
+    for wt in range(1, maxb + 1):
+        start[wt] = acc >> (wt - 1)
+        acc += num[wt] << (wt - 1)
+    codes = {}
+    for s in range(top + 1):
+        if w[s]:
+            codes[s] = (start[w[s]], lens[s])
+            start[w[s]] += 1
+    return codes, None
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "fseweights":
+    check_fse_weights()
