@@ -165,23 +165,25 @@ def roofline(kernel: str, config: str, kern_ms: float, rolled: int, stream_bytes
             "stream_gbs": round(stream_bytes / kern_s / 1e9, 1)} | valu_note(kernel, config)
 
 
-# Rabin-Karp's limiter is neither HBM nor VALU issue: with every
-# instruction class measured (tools/valu_rate.hip, profiles/r04/rk/valu_rate.log), the hot roll is
-# ~26 SIMD cycles per wave-roll (perm/alignbit/and_or/min3 at ~4.2, bitop3/lshr at ~2.3 with two
-# waves per SIMD), a VALU floor of ~1.1 ms for config 2; the hot loop alone (the kernel's rk_step64
-# replica fed from LDS, `valu_rate rk`, profiles/r04/rk/valu_rk_hotloop.log) takes 2.02 ms: the
-# per-byte chain through the mod[] table read is LDS-latency bound at four chains per SIMD.
-RK_HOT_LOOP_MS = {"config2-rk": 2.021}
-RK_VALU_FLOOR_MS = {"config2-rk": 1.1}
+# Rabin-Karp's limiter: the hot loop is throughput-bound on VALU issue
+# and the LDS array together, neither saturated (profiles/r06/rk_counters, rk_final: LDS array busy
+# 58.5 % of the CU's cycles, VALU ~64 % of each SIMD's at the measured per-class issue costs of
+# tools/valu_rate.hip), the per-byte chain's latency a 5 % term (ablations of the hot loop alone,
+# tools/rk_loop.hip, profiles/r06/rk_loop/rk_loop2.log: 1.555 ms for config 2's rolled bytes with
+# the round-6 address forms).  The floors are the busy fractions times the kernel's 2.15 ms.
+RK_HOT_LOOP_MS = {"config2-rk": 1.555}
+RK_VALU_FLOOR_MS = {"config2-rk": 1.38}
+RK_LDS_FLOOR_MS = {"config2-rk": 1.26}
 
 
 def valu_note(kernel: str, config: str) -> dict:
     hot = RK_HOT_LOOP_MS.get(config)
     if not hot:
         return {}
-    return {"limited_by": "LDS latency of the per-byte table chain", "hot_loop_alone_ms": hot,
-            "valu_floor_ms": RK_VALU_FLOOR_MS[config],
-            "hot_loop_source": "profiles/r04/rk/valu_rk_hotloop.log (tools/valu_rate.hip rk)"}
+    return {"limited_by": "VALU issue and the LDS array together (co-bound; chain latency ~5 %)",
+            "hot_loop_alone_ms": hot, "valu_floor_ms": RK_VALU_FLOOR_MS[config],
+            "lds_floor_ms": RK_LDS_FLOOR_MS[config],
+            "hot_loop_source": "profiles/r06/rk_loop/rk_loop2.log (tools/rk_loop.hip, round-6 replica)"}
 
 
 def h2d_rates(host: np.ndarray, dev) -> dict:

@@ -877,7 +877,8 @@ struct ZTab {          // FSE encoding table (RFC 8878 §4.1; zstd's FSE_buildCT
 };
 
 // One field's table from the span's code counts (total nseq).  Wave-collective, lane = symbol:
-// Accuracy_Log from the sequence count (5..maxlog, >= used + 1 cells); counts rounded to 2^al with
+// Accuracy_Log from the sequence count (log2 - 2 as zstd's FSE_optimalTableLog, 5..maxlog, >= used
+// + 1 cells); counts rounded to 2^al with
 // every used symbol >= 1 (the rounding surplus to the largest entry, a deficit taken from the
 // largest one at a time); the encoding table (the RFC's spread puts cumulative cell j at
 // j * step mod size, so each symbol's lane walks the states in order and keeps those whose
@@ -889,7 +890,7 @@ __device__ uint32_t zstd_table(const uint32_t* cnt, uint32_t nsym, uint32_t maxl
     const uint64_t um = __ballot(cs != 0u);
     const uint32_t used = static_cast<uint32_t>(__popcll(um));
     const uint32_t last = 63u - static_cast<uint32_t>(__builtin_clzll(um));
-    uint32_t al = 31u - static_cast<uint32_t>(__builtin_clz(nseq));
+    uint32_t al = nseq > 4u ? 29u - static_cast<uint32_t>(__builtin_clz(nseq - 1u)) : 0u;  // log2(n) - 2, as zstd
     al = al < 5u ? 5u : al > maxlog ? maxlog : al;
     while ((1u << al) < used + 1u && al < maxlog) al++;
     const uint32_t size = 1u << al;
@@ -992,6 +993,66 @@ __device__ __forceinline__ uint32_t zstd_table(const uint32_t* cnt, uint32_t nsy
     return zstd_table(cnt, nsym, maxlog, nseq, t.st, t.dd, &t.al, norm, desc, lane);
 }
 
+// The predefined distribution of field f (0 LL, 1 OF, 2 ML; RFC 8878 §3.1.1.3.2.2) as an encoding
+// table: the "less than 1" symbols (-1) take one cell each at the top, the others are spread with
+// the RFC's step skipping those cells.  One lane; tsym: 64 bytes of scratch.
+__device__ int32_t zstd_pre_norm(uint32_t f, uint32_t s) {
+    return f == 0u ? (s < 36u ? kLLNorm[s] : 0) : f == 1u ? (s < 29u ? kOFNorm[s] : 0) : (s < 53u ? kMLNorm[s] : 0);
+}
+__device__ void zstd_pre_table(uint32_t f, ZTab& t, uint8_t* tsym) {
+    const uint32_t al = f == 1u ? 5u : 6u, size = 1u << al, n = f == 0u ? 36u : f == 1u ? 29u : 53u;
+    uint32_t high = size - 1u;
+    for (uint32_t s = 0; s < n; s++)
+        if (zstd_pre_norm(f, s) == -1) tsym[high--] = static_cast<uint8_t>(s);
+    const uint32_t step = (size >> 1) + (size >> 3) + 3u, mask = size - 1u;
+    uint32_t pos = 0;
+    for (uint32_t s = 0; s < n; s++)
+        for (int32_t i = 0; i < zstd_pre_norm(f, s); i++) {
+            tsym[pos] = static_cast<uint8_t>(s);
+            do pos = (pos + step) & mask;
+            while (pos > high);
+        }
+    uint32_t total = 0;
+    for (uint32_t s = 0; s < n; s++) {  // running slots in dd[].x first
+        t.dd[s].x = total;
+        const int32_t v = zstd_pre_norm(f, s);
+        total += v == -1 ? 1u : static_cast<uint32_t>(v);
+    }
+    for (uint32_t u = 0; u < size; u++) t.st[t.dd[tsym[u]].x++] = static_cast<uint16_t>(size + u);
+    total = 0;
+    for (uint32_t s = 0; s < 53u; s++) {
+        const int32_t v = zstd_pre_norm(f, s);
+        if (v == 0) {
+            t.dd[s] = make_uint2(((al + 1u) << 16) - size, 0u);
+        } else if (v == -1 || v == 1) {
+            t.dd[s] = make_uint2((al << 16) - size, total - 1u);
+            total += 1u;
+        } else {
+            const uint32_t fv = static_cast<uint32_t>(v);
+            const uint32_t mbo = al - (31u - static_cast<uint32_t>(__builtin_clz(fv - 1u)));
+            t.dd[s] = make_uint2((mbo << 16) - (fv << mbo), total - fv);
+            total += fv;
+        }
+    }
+    t.al = al;
+}
+
+// Sequence i's offset value (RFC 8878 §3.1.2.5) from its word v, the two before it (pv, ppv), its
+// literal length ll and the previous one's llp (both with carries); blk0: the block's first sequence.
+// Repeat offset 1 is always the previous sequence's distance: offset value 1 when ll > 0.  With
+// ll = 0, offset value 1 names repeat offset 2, which is this distance when the previous two
+// sequences had it and the previous one had ll = 0 (then it was either explicit, pushing the one
+// before it to second place, or itself repeat offset 2, which swaps the first two).  A block's
+// first sequences name their offsets: the history before the block is not known here.
+__device__ __forceinline__ uint32_t zstd_ov(uint32_t i, uint32_t blk0, uint32_t v, uint32_t pv, uint32_t ppv,
+                                            uint32_t ll, uint32_t llp) {
+    const uint32_t dist = v & 0x7FFFu;
+    const bool same1 = i > blk0 && (pv & 0x7FFFu) == dist;
+    if (same1 && ll > 0u) return 1u;
+    if (same1 && ll == 0u && llp == 0u && i >= blk0 + 2u && (ppv & 0x7FFFu) == dist) return 1u;
+    return dist + 3u;
+}
+
 // A block of the span: [3-byte header][literals section][sequences section]; offsets from the block.
 struct ZBlk {
     uint32_t raw;        // input bytes
@@ -1047,6 +1108,7 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     __shared__ int16_t fnorm[3][64];
     __shared__ uint8_t fdesc[3][kZDesc];
     __shared__ uint32_t fdlen[3];
+    __shared__ uint32_t fmode[3];            // each field's Symbol_Compression_Mode in the carrier block
     __shared__ uint32_t ln_off[65], ln_nseq[64], ln_len[64], ln_nlit[64], ln_carry[64], ln_p[64], ln_prev[64];
     __shared__ uint32_t ln_bits[64 * 4];
     __shared__ ZBlk blk[kZBlks];
@@ -1066,9 +1128,10 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     const uint32_t d = stage_span(L, a.in + a.in_offs[c] + sb, span_len, tid, 256u);
     const uint32_t x0 = kSeg * lane;
     const uint32_t seg_len = x0 < span_len ? min(kSeg, span_len - x0) : 0u, xe = x0 + seg_len;
-    const uint32_t nseq = seg_len && w0 ? a.desc[static_cast<uint64_t>(b) * kDescWords + lane] : 0u;
+    const uint32_t nseq = seg_len ? a.desc[static_cast<uint64_t>(b) * kDescWords + lane] : 0u;
     const uint32_t k = lane / kZBlkSegs, lead = k * kZBlkSegs;  // the lane's block, its first lane
     hist[tid] = 0u;
+    ln_bits[tid] = 0u;
     if (tid < 36u + 53u + 32u) fcnt[tid] = 0u;
     if (w0) {
         uint32_t cc, nn, xx;
@@ -1088,7 +1151,7 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     const uint32_t off = incl - nseq;
     const uint32_t* sq = reinterpret_cast<const uint32_t*>(a.slots + (static_cast<uint64_t>(b) * 64u + lane) * kSlot);
     uint32_t covered = 0, matched = 0;
-    for (uint32_t j = 0; j < nseq; j++) {  // (wave 0 only: nseq is 0 in the others)
+    for (uint32_t j = 0; j < (w0 ? nseq : 0u); j++) {  // (wave 0: the others use the LDS copies)
         const uint32_t v = sq[143u - j];
         seqw[off + j] = v;
         const uint32_t ml = zseq_ml(v);
@@ -1146,22 +1209,55 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
         }
         run(x, xe);
     };
+    // The four waves share the counting passes: wave w takes the lane's literals at bytes
+    // [x0 + 128 w, x0 + 128 (w + 1)) of its segment (lits_part: f(value, index in the block)) and
+    // its sequences j = w mod 4.
+    const uint32_t plo = x0 + 128u * wv, phi = plo + 128u;
+    auto lits_part = [&](auto f) {
+        uint32_t idx = ln_p[lane];  // the block index of the first literal at or after plo
+        auto run = [&](uint32_t x, uint32_t e) {
+            const uint32_t a0 = max(x, plo), e0 = min(e, phi);
+            idx += (a0 > x ? min(a0, e) - x : 0u);
+            if (a0 >= e0) return;
+            uint32_t y = a0;
+            for (; y + 4u <= e0; y += 4u) {
+                const uint32_t w = st_ld32(L, d, y);
+                f(w & 255u, idx);
+                f((w >> 8) & 255u, idx + 1u);
+                f((w >> 16) & 255u, idx + 2u);
+                f(w >> 24, idx + 3u);
+                idx += 4u;
+            }
+            for (; y < e0; y++) f(st_byte(L, d, y), idx++);
+            idx += e > e0 ? e - e0 : 0u;
+        };
+        uint32_t x = x0;
+        for (uint32_t j = 0; j < nseq && x < phi; j++) {
+            const uint32_t v = seqw[off + j], ll = zseq_ll(v);
+            run(x, x + ll);
+            x += ll + zseq_ml(v);
+        }
+        if (x < phi) run(x, xe);
+    };
     // the codes of the lane's sequences: the carry joins the first literal length; offset value 1
     // for the previous sequence's distance (same block, literal length > 0), else distance + 3
-    if (w0) {
-        lits_fwd([&](uint32_t v) { atomicAdd(&hist[v], 1u); });
+    {
+        lits_part([&](uint32_t v, uint32_t) { atomicAdd(&hist[v], 1u); });
         const uint32_t blk0 = ln_off[lead];
         const uint32_t cy = ln_carry[lane];
-        for (uint32_t j = 0; j < nseq; j++) {
+        for (uint32_t j = wv; j < nseq; j += 4u) {
             const uint32_t i = off + j, v = seqw[i];
-            const uint32_t ll = zseq_ll(v) + (j == 0u ? cy : 0u), dist = v & 0x7FFFu;
-            const bool rep = i > blk0 && ll > 0u && (seqw[i - 1u] & 0x7FFFu) == dist;
+            const uint32_t ll = zseq_ll(v) + (j == 0u ? cy : 0u);
+            const uint32_t pv = seqw[i > blk0 ? i - 1u : i], ppv = seqw[i > blk0 + 1u ? i - 2u : i];
+            const uint32_t lp = j ? lane : ln_prev[lane];  // the segment of sequence i - 1
+            const uint32_t llp = zseq_ll(pv) + (i > blk0 && i - 1u == ln_off[lp] ? ln_carry[lp] : 0u);
+            const uint32_t ov = zstd_ov(i, blk0, v, pv, ppv, ll, llp);
             uint32_t llc, llb, llx, mlc, mlb, mlx;
             ll_code(ll, llc, llb, llx);
             ml_code(zseq_ml(v), mlc, mlb, mlx);
             atomicAdd(&fcnt[llc], 1u);
             atomicAdd(&fcnt[36u + mlc], 1u);
-            atomicAdd(&fcnt[89u + (rep ? 0u : 31u - static_cast<uint32_t>(__builtin_clz(dist + 3u)))], 1u);
+            atomicAdd(&fcnt[89u + 31u - static_cast<uint32_t>(__builtin_clz(ov))], 1u);
         }
     }
     __syncthreads();
@@ -1191,7 +1287,7 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     }
     // bits = N log2 N - sum c log2 c; a Huffman code is within ~3 % of it here
     const float hbits = nl_span ? static_cast<float>(nl_span) * __log2f(static_cast<float>(nl_span)) - ent : 0.f;
-    const bool try_huff = used >= 2u && 1.02f * hbits / 8.f + 40.f < static_cast<float>(nl_span);
+    const bool try_huff = used >= 2u && 1.02f * hbits / 8.f + 24.f < static_cast<float>(nl_span);
     const uint32_t nseq_span = ln_off[64];
     __syncthreads();  // every wave has read the counts (wave 0 reuses their space below)
     if (w0 && try_huff) {
@@ -1303,9 +1399,43 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     }
     if (!w0 && nseq_span) {  // the LL, OF, ML tables, one per wave (at the same time as the Huffman code)
         const uint32_t t = wv - 1u;
-        const uint32_t r = zstd_table(fcnt + (t == 0u ? 0u : t == 1u ? 89u : 36u), t == 0u ? 36u : t == 1u ? 32u : 53u,
-                                      t == 1u ? 8u : 9u, nseq_span, tab[t], fnorm[t], fdesc[t], lane);
-        if (lane == 0) fdlen[t] = r;
+        const uint32_t* cn = fcnt + (t == 0u ? 0u : t == 1u ? 89u : 36u);
+        const uint32_t ns = t == 0u ? 36u : t == 1u ? 32u : 53u;
+        const uint32_t r = zstd_table(cn, ns, t == 1u ? 8u : 9u, nseq_span, tab[t], fnorm[t], fdesc[t], lane);
+        // The mode of least estimated cost (the FSE cost of a symbol ~ log2(size / count)):
+        // Compressed (the table above and its description), Predefined (no description) or RLE
+        // (one symbol: one byte, no state bits).
+        const uint32_t cs = lane < ns ? cn[lane] : 0u;
+        const int32_t pn = static_cast<int32_t>(zstd_pre_norm(t, lane));
+        const float alc = static_cast<float>(tab[t].al), alp = t == 1u ? 5.f : 6.f;
+        float cc = cs ? static_cast<float>(cs) * (alc - __log2f(static_cast<float>(fnorm[t][lane]))) : 0.f;
+        float cp = cs ? (pn == 0 ? 1e30f : static_cast<float>(cs) * (alp - __log2f(pn == -1 ? 1.f : static_cast<float>(pn)))) : 0.f;
+        for (uint32_t o = 32; o > 0; o >>= 1) {
+            cc += __shfl_xor(cc, static_cast<int>(o), 64);
+            cp += __shfl_xor(cp, static_cast<int>(o), 64);
+        }
+        const uint64_t um = __ballot(cs != 0u);
+        const uint32_t rb = static_cast<uint32_t>(__shfl(static_cast<int>(r), 0, 64));
+        if (lane == 0) {
+            uint32_t mode = 2u;
+            if (__popcll(um) == 1) {  // RLE: state 1 forever, no bits
+                const uint32_t sy = static_cast<uint32_t>(__builtin_ctzll(um));
+                tab[t].st[0] = 1u;
+                tab[t].st[1] = 1u;
+                tab[t].dd[sy] = make_uint2(0u, 0u);
+                tab[t].al = 0u;
+                fdesc[t][0] = static_cast<uint8_t>(sy);
+                fdlen[t] = 1u;
+                mode = 1u;
+            } else if (cp <= cc + 8.f * static_cast<float>(rb)) {
+                zstd_pre_table(t, tab[t], fdesc[t]);
+                fdlen[t] = 0u;
+                mode = 0u;
+            } else {
+                fdlen[t] = r;
+            }
+            fmode[t] = mode;
+        }
     }
     __syncthreads();
     KCDC_ZSTAMP(3);
@@ -1320,20 +1450,27 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     for (uint32_t j = lead; j < lead + kZBlkSegs; j++) nl_blk += ln_nlit[j];
     const uint32_t nstr = nl_blk > 1023u ? 4u : 1u;
     const uint32_t qn = nstr == 4u ? (nl_blk + 3u) / 4u : (nl_blk ? nl_blk : 1u);
-    uint32_t bits[4] = {0u, 0u, 0u, 0u};
-    if (w0 && huff && nlit) {
-        uint32_t idx = p, q = p / qn, nextb = (q + 1u) * qn;
-        lits_fwd([&](uint32_t v) {
+    if (huff && ln_nlit[lane]) {  // (the four waves, each its part of the lane's literals)
+        uint32_t bits[4] = {0u, 0u, 0u, 0u};
+        uint32_t q = 4u, nextb = 0u;  // the stream of the part's first literal, then by boundary
+        lits_part([&](uint32_t v, uint32_t idx) {
+            if (q == 4u) {
+                q = nstr == 1u ? 0u : min(idx / qn, 3u);
+                nextb = nstr == 1u ? kZNone : (q + 1u) * qn;
+            }
             if (idx == nextb && q < 3u) {
                 q++;
                 nextb += qn;
             }
-            bits[q] += zc[v] >> 16;
-            idx++;
+            const uint32_t nbq = zc[v] >> 16;
+            bits[0] += q == 0u ? nbq : 0u;
+            bits[1] += q == 1u ? nbq : 0u;
+            bits[2] += q == 2u ? nbq : 0u;
+            bits[3] += q == 3u ? nbq : 0u;
         });
+        for (uint32_t q = 0; q < 4u; q++)
+            if (bits[q]) atomicAdd(&ln_bits[lane * 4u + q], bits[q]);
     }
-    if (w0)
-        for (uint32_t q = 0; q < 4u; q++) ln_bits[lane * 4u + q] = bits[q];
     __syncthreads();
     KCDC_ZSTAMP(5);
     const uint32_t ns_blk = ln_off[lead + kZBlkSegs] - ln_off[lead];
@@ -1367,110 +1504,110 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
         B.fbits = 0u;
     }
     __syncthreads();
-    if (lane == 0 && blk[wv].ns) {  // wave wv: block wv's sequences bitstream
+    if (blk[wv].ns) {  // wave wv: block wv's sequences bitstream
+        // Backwards from the block's last sequence (ZSTD_encodeSequences order), 64 at a time: the
+        // wave's lanes derive 64 sequences' codes, extras and table entries at once (independent
+        // of the states), then lane 0 runs the state chain over them, reading each lane's values
+        // with readlane: per sequence the chain is the three state steps and the bit packing.
         ZBlk& B = blk[wv];
         const uint32_t lead = wv * kZBlkSegs, fs = B.fscr;
         uint8_t* R = a.slots + (static_cast<uint64_t>(b) * 64u + lead) * kSlot + kZOff;
-        {
-            uint32_t* dst = reinterpret_cast<uint32_t*>(R + fs);
-            const uint32_t lim = (kZRegion - fs - 40u) / 4u;  // words (the loop stops within 7 of it)
-            uint64_t bb = 0;
-            uint32_t nb = 0, o = 0, tb = 0;
-            // x < 2^n; the current word is stored every time (no branch), and kept once full
-            auto put = [&](uint32_t x, uint32_t n) {
-                tb += n;
-                bb |= static_cast<uint64_t>(x) << nb;
-                nb += n;
-                dst[o] = static_cast<uint32_t>(bb);
-                const bool full = nb >= 32u;
-                o += full ? 1u : 0u;
-                bb = full ? bb >> 32 : bb;
-                nb -= full ? 32u : 0u;
-            };
-            const ZTab &tLL = tab[0], &tOF = tab[1], &tML = tab[2];
-            // Sequence ii's codes and table entries: literal length (with its segment's carry when
-            // it is the segment's first), match length, offset value; extras x1 = ll | ml << llb,
-            // x2 = of.  Independent of the states: computed one sequence ahead, so the loop's
-            // critical path is the state chain (one LDS read per field and sequence).
-            struct ZC {
-                uint32_t ofc, x1, n1, x2;
-                uint2 eLL, eML, eOF;
-            };
-            const uint32_t i0 = ln_off[lead];
-            auto mk = [&](uint32_t ii, uint32_t v, uint32_t pv, uint32_t cy) -> ZC {
-                const uint32_t ll = zseq_ll(v) + cy, dist = v & 0x7FFFu, m = zseq_ml(v) - 3u;
-                const uint32_t ov = ii > i0 && ll > 0u && (pv & 0x7FFFu) == dist ? 1u : dist + 3u;
-                const uint32_t tl = llut[min(ll, 63u)], hl = 31u - static_cast<uint32_t>(__builtin_clz(ll | 1u));
-                const uint32_t tm = mlut[min(m, 127u)], hm = 31u - static_cast<uint32_t>(__builtin_clz(m));
-                const bool bl = ll >= 64u, bm = m >= 128u;
-                const uint32_t llc = bl ? hl + 19u : (tl & 255u);
-                const uint32_t llb = bl ? hl : ((tl >> 8) & 255u);
-                const uint32_t llx = ll - (bl ? (1u << hl) : (tl >> 16));
-                const uint32_t mlc = bm ? hm + 36u : (tm & 255u);
-                const uint32_t mlb = bm ? hm : ((tm >> 8) & 255u);
-                const uint32_t mlx = m - (bm ? (1u << hm) : (tm >> 16));
-                const uint32_t ofc = 31u - static_cast<uint32_t>(__builtin_clz(ov));
-                return ZC{ofc, llx | (mlx << llb), llb + mlb, ov - (1u << ofc), tLL.dd[llc], tML.dd[mlc], tOF.dd[ofc]};
-            };
-            // the segment of sequence ii (called for ii descending by one): its first sequence's
-            // index lo; a step below it goes to the previous segment with sequences
-            uint32_t l = lead + kZBlkSegs - 1u;
-            if (ln_nseq[l] == 0u) l = ln_prev[l];
-            uint32_t lo = ln_off[l];
-            auto seg_of = [&](uint32_t ii) {
-                if (ii < lo) {
-                    l = ln_prev[l];
-                    lo = ln_off[l];
+        uint32_t* dst = reinterpret_cast<uint32_t*>(R + fs);
+        const uint32_t lim = (kZRegion - fs - 40u) / 4u;  // words (the chain stops within 7 of it)
+        const ZTab &tLL = tab[0], &tOF = tab[1], &tML = tab[2];
+        const uint32_t i0 = ln_off[lead], i1 = ln_off[lead + kZBlkSegs];
+        uint64_t bb = 0;       // lane 0: the bit writer
+        uint32_t nb = 0, o = 0;
+        uint32_t sLL = 0, sML = 0, sOF = 0;  // lane 0: the states
+        bool over = false;
+        auto put = [&](uint32_t x, uint32_t n) {  // x < 2^n; the current word is stored every time
+            bb |= static_cast<uint64_t>(x) << nb;
+            nb += n;
+            dst[o] = static_cast<uint32_t>(bb);
+            const bool full = nb >= 32u;
+            o += full ? 1u : 0u;
+            bb = full ? bb >> 32 : bb;
+            nb -= full ? 32u : 0u;
+        };
+        for (uint32_t hi = i1; hi > i0 && !over; hi = hi > i0 + 64u ? hi - 64u : i0) {
+            const uint32_t cnt = min(64u, hi - i0);
+            // lane t: sequence hi - 1 - t
+            const uint32_t idx = hi - 1u - min(lane, cnt - 1u);
+            uint32_t cy = 0, cyp = 0;  // its (and the previous one's) segment's carry when it is the segment's first
+            for (uint32_t sg = lead; sg < lead + kZBlkSegs; sg++) {
+                const uint32_t lo = ln_off[sg], hs = ln_off[sg + 1u];
+                if (lo < hs && idx == lo) cy = ln_carry[sg];
+                if (lo < hs && idx > i0 && idx - 1u == lo) cyp = ln_carry[sg];
+            }
+            const uint32_t v = seqw[idx], pv = seqw[idx > i0 ? idx - 1u : idx];
+            const uint32_t ppv = seqw[idx > i0 + 1u ? idx - 2u : idx];
+            const uint32_t ll = zseq_ll(v) + cy, m = zseq_ml(v) - 3u;
+            const uint32_t ov = zstd_ov(idx, i0, v, pv, ppv, ll, zseq_ll(pv) + cyp);
+            const uint32_t tl = llut[min(ll, 63u)], hl = 31u - static_cast<uint32_t>(__builtin_clz(ll | 1u));
+            const uint32_t tm = mlut[min(m, 127u)], hm = 31u - static_cast<uint32_t>(__builtin_clz(m));
+            const bool bl = ll >= 64u, bm = m >= 128u;
+            const uint32_t llc = bl ? hl + 19u : (tl & 255u);
+            const uint32_t llb = bl ? hl : ((tl >> 8) & 255u);
+            const uint32_t llx = ll - (bl ? (1u << hl) : (tl >> 16));
+            const uint32_t mlc = bm ? hm + 36u : (tm & 255u);
+            const uint32_t mlb = bm ? hm : ((tm >> 8) & 255u);
+            const uint32_t mlx = m - (bm ? (1u << hm) : (tm >> 16));
+            const uint32_t ofc = 31u - static_cast<uint32_t>(__builtin_clz(ov));
+            const uint32_t x1 = llx | (mlx << llb), n1 = llb + mlb, x2 = ov - (1u << ofc);
+            const uint2 eLL = tLL.dd[llc], eML = tML.dd[mlc], eOF = tOF.dd[ofc];
+            // packed for the chain: dnb (< 2^20) | (dfs + 512) << 20; x1 (< 2^21) | n1 << 21; x2 | ofc << 16
+            uint32_t pLL = eLL.x | ((eLL.y + 512u) << 20), pML = eML.x | ((eML.y + 512u) << 20);
+            uint32_t pOF = eOF.x | ((eOF.y + 512u) << 20), xa = x1 | (n1 << 21), xb = x2 | (ofc << 16);
+            // every lane's values are read across lanes below: keep them computed here, by all
+            asm volatile("" : "+v"(pLL), "+v"(pML), "+v"(pOF), "+v"(xa), "+v"(xb));
+            if (lane == 0) {
+                uint32_t t = 0;
+                if (hi == i1) {  // the block's last sequence: the initial states
+                    auto init = [&](const ZTab& tb, uint2 e) -> uint32_t {
+                        const uint32_t nbo = (e.x + (1u << 15)) >> 16;
+                        const uint32_t s0 = (nbo << 16) - e.x;
+                        return tb.st[(s0 >> nbo) + e.y];
+                    };
+                    sML = init(tML, eML);
+                    sOF = init(tOF, eOF);
+                    sLL = init(tLL, eLL);
+                    put(x1, n1);  // the decoder reads offset, match length, literal length extras
+                    put(x2, ofc);
+                    t = 1;
                 }
-            };
-            uint32_t i = ln_off[lead + kZBlkSegs] - 1u;
-            uint32_t w1 = seqw[i > i0 ? i - 1u : i0];       // sequence i - 1's word
-            ZC c = mk(i, seqw[i], w1, i == lo ? ln_carry[l] : 0u);
-            // the block's last sequence: the initial states
-            auto init = [&](const ZTab& t, uint2 e) -> uint32_t {
-                const uint32_t nbo = (e.x + (1u << 15)) >> 16;
-                const uint32_t s0 = (nbo << 16) - e.x;
-                return t.st[(s0 >> nbo) + e.y];
-            };
-            uint32_t sML = init(tML, c.eML);
-            uint32_t sOF = init(tOF, c.eOF);
-            uint32_t sLL = init(tLL, c.eLL);
-            put(c.x1, c.n1);  // the decoder reads offset, match length, literal length extras
-            put(c.x2, c.ofc);
-            uint32_t jn = i > i0 ? i - 1u : i0;  // the next sequence
-            seg_of(jn);
-            uint32_t w2 = seqw[jn > i0 ? jn - 1u : i0];
-            ZC n = mk(jn, w1, w2, jn == lo ? ln_carry[l] : 0u);
-            bool over = false;
-            // backwards (ZSTD_encodeSequences order): each earlier sequence's state bits (the
-            // decoder's updates after it: LL, ML, OF -> written OF, ML, LL), then its extras
-            while (i > i0) {
-                i--;
-                c = n;
-                const uint32_t nOF = (sOF + c.eOF.x) >> 16, nML = (sML + c.eML.x) >> 16, nLL = (sLL + c.eLL.x) >> 16;
-                const uint32_t bits = (sOF & ((1u << nOF) - 1u)) | ((sML & ((1u << nML) - 1u)) << nOF) |
-                                      ((sLL & ((1u << nLL) - 1u)) << (nOF + nML));
-                sOF = tOF.st[(sOF >> nOF) + c.eOF.y];
-                sML = tML.st[(sML >> nML) + c.eML.y];
-                sLL = tLL.st[(sLL >> nLL) + c.eLL.y];
-                jn = i > i0 ? i - 1u : i0;
-                seg_of(jn);
-                w1 = w2;
-                w2 = seqw[jn > i0 ? jn - 1u : i0];
-                n = mk(jn, w1, w2, jn == lo ? ln_carry[l] : 0u);
-                put(bits, nOF + nML + nLL);
-                put(c.x1, c.n1);
-                put(c.x2, c.ofc);
-                if (o > lim) {
-                    over = true;
-                    break;
+                for (; t < cnt; t++) {  // each earlier sequence: state bits (OF, ML, LL), extras
+                    const int tt = static_cast<int>(t);
+                    const uint32_t qOF = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(pOF), tt));
+                    const uint32_t qML = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(pML), tt));
+                    const uint32_t qLL = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(pLL), tt));
+                    const uint32_t ya = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(xa), tt));
+                    const uint32_t yb = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(xb), tt));
+                    const uint32_t dOF = qOF & 0xFFFFFu, fOF = (qOF >> 20) - 512u;
+                    const uint32_t dML = qML & 0xFFFFFu, fML = (qML >> 20) - 512u;
+                    const uint32_t dLL = qLL & 0xFFFFFu, fLL = (qLL >> 20) - 512u;
+                    const uint32_t nOF = (sOF + dOF) >> 16, nML = (sML + dML) >> 16, nLL = (sLL + dLL) >> 16;
+                    const uint32_t bits = (sOF & ((1u << nOF) - 1u)) | ((sML & ((1u << nML) - 1u)) << nOF) |
+                                          ((sLL & ((1u << nLL) - 1u)) << (nOF + nML));
+                    sOF = tOF.st[(sOF >> nOF) + fOF];
+                    sML = tML.st[(sML >> nML) + fML];
+                    sLL = tLL.st[(sLL >> nLL) + fLL];
+                    put(bits, nOF + nML + nLL);
+                    put(ya & 0x1FFFFFu, ya >> 21);
+                    put(yb & 0xFFFFu, yb >> 16);
+                    if (o > lim) {
+                        over = true;
+                        break;
+                    }
                 }
             }
+            over = __builtin_amdgcn_readfirstlane(over ? 1 : 0) != 0;
+        }
+        if (lane == 0) {
             const uint32_t am = tML.al, ao = tOF.al, ala = tLL.al;  // initial states, read LL, OF, ML
             put((sML & ((1u << am) - 1u)) | ((sOF & ((1u << ao) - 1u)) << am), am + ao);
             put(sLL & ((1u << ala) - 1u), ala);
             put(1u, 1);  // end marker
-            B.fbits = over ? kZNone : tb;
+            B.fbits = over ? kZNone : 32u * o + nb;
         }
     }
     __syncthreads();
@@ -1686,8 +1823,10 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
             R[o++] = static_cast<uint8_t>(ns);
         }
         if (ns) {
-            const uint32_t m = (B.role & kZrTables) ? 2u : 3u;  // FSE_Compressed_Mode / Repeat_Mode
-            R[o++] = static_cast<uint8_t>((m << 6) | (m << 4) | (m << 2));
+            // each field's mode in the carrier (0 Predefined, 1 RLE, 2 FSE_Compressed), else Repeat_Mode
+            const bool tb = (B.role & kZrTables) != 0u;
+            R[o++] = static_cast<uint8_t>(((tb ? fmode[0] : 3u) << 6) | ((tb ? fmode[1] : 3u) << 4) |
+                                          ((tb ? fmode[2] : 3u) << 2));
             if (B.role & kZrTables)
                 for (uint32_t t = 0; t < 3u; t++)
                     for (uint32_t i = 0; i < fdlen[t]; i++) R[o++] = fdesc[t][i];
