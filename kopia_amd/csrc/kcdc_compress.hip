@@ -1520,6 +1520,18 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
         uint32_t nb = 0, o = 0;
         uint32_t sLL = 0, sML = 0, sOF = 0;  // lane 0: the states
         bool over = false;
+        // val < 2^n, n <= 62, with nb < 32 before: both words of the low 64 bits are stored, the
+        // cursor moves by the full words, the rest stays (bits past 64 come from the high part)
+        auto put64 = [&](uint64_t val, uint32_t n) {
+            const uint64_t low = bb | (val << nb);
+            const uint64_t high = nb ? (val >> (64u - nb)) : 0ull;
+            const uint32_t tot = nb + n;
+            dst[o] = static_cast<uint32_t>(low);
+            dst[o + 1u] = static_cast<uint32_t>(low >> 32);
+            o += tot >> 5;
+            bb = tot >= 64u ? high : tot >= 32u ? (low >> 32) : low;
+            nb = tot & 31u;
+        };
         auto put = [&](uint32_t x, uint32_t n) {  // x < 2^n; the current word is stored every time
             bb |= static_cast<uint64_t>(x) << nb;
             nb += n;
@@ -1591,9 +1603,11 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
                     sOF = tOF.st[(sOF >> nOF) + fOF];
                     sML = tML.st[(sML >> nML) + fML];
                     sLL = tLL.st[(sLL >> nLL) + fLL];
-                    put(bits, nOF + nML + nLL);
-                    put(ya & 0x1FFFFFu, ya >> 21);
-                    put(yb & 0xFFFFu, yb >> 16);
+                    // the sequence's <= 62 bits (states <= 26, extras <= 21 + 15) as one value
+                    const uint32_t ns = nOF + nML + nLL, n1s = ya >> 21;
+                    const uint64_t val = static_cast<uint64_t>(bits) | (static_cast<uint64_t>(ya & 0x1FFFFFu) << ns) |
+                                         (static_cast<uint64_t>(yb & 0xFFFFu) << (ns + n1s));
+                    put64(val, ns + n1s + (yb >> 16));
                     if (o > lim) {
                         over = true;
                         break;

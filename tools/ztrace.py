@@ -76,6 +76,12 @@ def main():
         res[name] = {"mean": round(float(dt[:, i].mean()), 1), "p90": float(np.percentile(dt[:, i], 90))}
     seqs = desc[:, :64].astype(np.int64).sum(axis=1)
     res["sequences_per_span_mean"] = float(seqs.mean())
+    # the FSE phase against the longest block's sequence count: cycles per chained sequence
+    mx = desc[:, :64].astype(np.int64).reshape(spans, 4, 16).sum(axis=2).max(axis=1)
+    fse = dt[:, PHASES.index("fse pass")].astype(np.float64)
+    a, b0 = np.polyfit(mx.astype(np.float64), fse, 1)
+    res["fse_cycles_per_sequence_fit"] = {"slope": round(float(a), 1), "intercept": round(float(b0), 1),
+                                          "longest_block_mean": float(mx.mean())}
     bud = desc[:, 84:92].astype(np.int64).sum(axis=0)
     names = ["raw_blocks", "literal_sections", "sequence_bitstreams", "table_descriptions", "huffman_trees",
              "headers", "coded_literals", "coded_sequences"]
