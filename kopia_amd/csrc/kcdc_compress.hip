@@ -1093,13 +1093,11 @@ constexpr uint32_t kZrCoded = 1, kZrHuff = 2, kZrTree = 4, kZrTables = 8;
 __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     __shared__ uint32_t L[kLdsWords];
     __shared__ uint32_t seqw[kZMaxSeq];
-    // H: the literal counts and the Huffman scratch, then the literal streams' edge records (per
-    // lane and stream: its first / last shared byte, index << 8 | bits)
+    // H: the literal counts and the Huffman scratch, then the weights' FSE table
     __shared__ uint32_t H[256 + 256 + 128];
     uint32_t* hist = H;
     uint32_t* sa = H + 256;
     uint16_t* ss = reinterpret_cast<uint16_t*>(H + 512);
-    uint32_t* rec = H;                     // 64 x 8
     __shared__ uint32_t zc[256];           // Huffman code | bits << 16
     __shared__ uint8_t lens[256];
     __shared__ uint32_t num[40];
@@ -1111,6 +1109,7 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     __shared__ uint32_t fmode[3];            // each field's Symbol_Compression_Mode in the carrier block
     __shared__ uint32_t ln_off[65], ln_nseq[64], ln_len[64], ln_nlit[64], ln_carry[64], ln_p[64], ln_prev[64];
     __shared__ uint32_t ln_bits[64 * 4];
+    __shared__ uint16_t pbits[64 * 4 * 4];   // per lane, part (wave) and stream: the part's literal bits
     __shared__ ZBlk blk[kZBlks];
     __shared__ uint32_t misc[2];             // [0]: the tree description's bytes (0: no Huffman), [1]: longest code
     __shared__ uint8_t hdesc[128];           // the Huffman tree description (RFC 8878 §4.2.1)
@@ -1442,8 +1441,6 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     KCDC_ZSTAMP(4);
     const uint32_t tsz = try_huff ? misc[0] : 0u;  // the tree description's bytes
     const bool huff = tsz != 0u;
-    rec[tid] = kZNone;
-    rec[tid + 256u] = kZNone;
     // literal streams: each lane's bits per stream of its block
     const uint32_t p = ln_p[lane];
     uint32_t nl_blk = 0;
@@ -1470,6 +1467,9 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
         });
         for (uint32_t q = 0; q < 4u; q++)
             if (bits[q]) atomicAdd(&ln_bits[lane * 4u + q], bits[q]);
+        for (uint32_t q = 0; q < 4u; q++) pbits[(lane * 4u + wv) * 4u + q] = static_cast<uint16_t>(bits[q]);
+    } else {
+        for (uint32_t q = 0; q < 4u; q++) pbits[(lane * 4u + wv) * 4u + q] = 0u;
     }
     __syncthreads();
     KCDC_ZSTAMP(5);
@@ -1702,77 +1702,111 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     __syncthreads();
     KCDC_ZSTAMP(7);
     const ZBlk& B = blk[k];
-    if (w0 && (B.role & kZrCoded)) {
-        if (!(B.role & kZrHuff)) {  // raw literals at their index
-            uint32_t idx = B.lit0 + p;
-            lits_fwd([&](uint32_t v) { R[idx++] = static_cast<uint8_t>(v); });
-        } else if (nlit) {
-            // each stream holds its literals last to first: this lane's part of stream q starts
-            // after the bits of the block's later lanes; bytes it shares go to edge records
+    // Huffman streams are OR-ed together where parts share a byte: their bytes start at zero
+    for (uint32_t kb = 0; kb < kZBlks; kb++) {
+        const ZBlk& Z = blk[kb];
+        if ((Z.role & (kZrCoded | kZrHuff)) != (kZrCoded | kZrHuff)) continue;
+        uint8_t* Rk = a.slots + (static_cast<uint64_t>(b) * 64u + kb * kZBlkSegs) * kSlot + kZOff;
+        uint32_t* w0p = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(Rk + Z.soff[0]) & ~uintptr_t(3));
+        uint32_t* w1p = reinterpret_cast<uint32_t*>((reinterpret_cast<uintptr_t>(Rk + Z.seq0) + 3u) & ~uintptr_t(3));
+        for (uint32_t* wp = w0p + tid; wp < w1p; wp += 256u) *wp = 0u;
+    }
+    __syncthreads();
+    // The literals, each wave its part of every lane's literals (bytes [x0 + 128 w, + 128) of the
+    // segment): raw at their index, or Huffman bits at their offset in their stream (each stream
+    // holds its literals last to first: a part starts after the bits of the block's later lanes
+    // and of its lane's later parts).  Bytes a part fully covers are stored; its partial first
+    // and last bytes are OR-ed in (global atomics on the dword), as are the streams' end markers.
+    if (B.role & kZrCoded) {
+        if (!(B.role & kZrHuff)) {
+            lits_part([&](uint32_t v, uint32_t idx) { R[B.lit0 + idx] = static_cast<uint8_t>(v); });
+        } else if (ln_nlit[lane]) {
             uint32_t bo[4];
             for (uint32_t q = 0; q < 4u; q++) {
-                uint32_t s = 0;
-                for (uint32_t j = lane + 1u; j < lead + kZBlkSegs; j++) s += ln_bits[j * 4u + q];
-                bo[q] = s;
+                uint32_t sum = 0;
+                for (uint32_t j = lane + 1u; j < lead + kZBlkSegs; j++) sum += ln_bits[j * 4u + q];
+                for (uint32_t w = wv + 1u; w < 4u; w++) sum += pbits[(lane * 4u + w) * 4u + q];
+                bo[q] = sum;
             }
-            uint32_t idx = p + nlit, q = 4u;
+            auto or_byte = [&](uint32_t q, uint32_t bi, uint32_t v) {
+                uint8_t* p8 = R + B.soff[q] + bi;
+                const uintptr_t ad = reinterpret_cast<uintptr_t>(p8);
+                atomicOr(reinterpret_cast<uint32_t*>(ad & ~uintptr_t(3)), v << (8u * static_cast<uint32_t>(ad & 3u)));
+            };
+            uint32_t idx = ln_p[lane] + ln_nlit[lane], q = 4u, qlo = 0u;  // idx: one past the next literal back
             uint64_t bb = 0;
             uint32_t nb = 0, bi = 0, b0 = 0;
-            auto close = [&]() {  // the part's last byte, when partial
-                if (q < 4u && nb) rec[lane * 8u + q * 2u + 1u] = (bi << 8) | static_cast<uint32_t>(bb & 255u);
+            auto close = [&]() {  // the part's last byte in stream q, when partial
+                if (q < 4u && nb) or_byte(q, bi, static_cast<uint32_t>(bb & 255u));
             };
-            auto lit = [&](uint32_t x) {
+            auto lit = [&](uint32_t y) {  // the literal at byte y, block index idx - 1
                 idx--;
-                const uint32_t qq = B.nstr == 1u ? 0u : min(idx / B.q, 3u);
-                if (qq != q) {
+                if (q == 4u || idx < qlo) {
                     close();
-                    q = qq;
+                    q = B.nstr == 1u ? 0u : min(idx / B.q, 3u);
+                    qlo = B.nstr == 1u ? 0u : q * B.q;
                     b0 = bo[q];
                     bi = b0 >> 3;
                     nb = b0 & 7u;
                     bb = 0;
                 }
-                const uint32_t cw = zc[st_byte(L, d, x)];
+                const uint32_t cw = zc[st_byte(L, d, y)];
                 bb |= static_cast<uint64_t>(cw & 0xFFFFu) << nb;
                 nb += cw >> 16;
                 while (nb >= 8u) {
-                    const uint8_t v = static_cast<uint8_t>(bb);
+                    const uint32_t v = static_cast<uint32_t>(bb & 255u);
                     if (bi == (b0 >> 3) && (b0 & 7u))
-                        rec[lane * 8u + q * 2u] = (bi << 8) | v;  // shared with the part before
+                        or_byte(q, bi, v);  // shared with the part before
                     else
-                        R[B.soff[q] + bi] = v;
+                        R[B.soff[q] + bi] = static_cast<uint8_t>(v);
                     bi++;
                     bb >>= 8;
                     nb -= 8u;
                 }
             };
-            // backwards: trailing literals, then each sequence's literals
+            auto run_back = [&](uint32_t x, uint32_t e) {  // the run [x, e), last to first
+                if (e > phi) idx -= e - max(x, phi);
+                for (uint32_t y = min(e, phi); y > max(x, plo); y--) lit(y - 1u);
+                if (x < plo) idx -= min(e, plo) - x;
+            };
             uint32_t xm = x0;
             for (uint32_t j = 0; j < nseq; j++) {
                 const uint32_t v = seqw[off + j];
                 xm += zseq_ll(v) + zseq_ml(v);
             }
-            for (uint32_t x = xe; x > xm; x--) lit(x - 1u);
-            for (uint32_t j = nseq; j-- > 0u;) {
+            run_back(xm, xe);  // the trailing literals, then each sequence's, backwards
+            for (uint32_t j = nseq; j-- > 0u && xm > plo;) {
                 const uint32_t v = seqw[off + j];
                 xm -= zseq_ml(v);
-                for (const uint32_t e = xm - zseq_ll(v); xm > e; xm--) lit(xm - 1u);
+                const uint32_t ll = zseq_ll(v);
+                run_back(xm - ll, xm);
+                xm -= ll;
             }
             close();
         }
+        if (w0 && lane == lead && (B.role & kZrHuff))
+            for (uint32_t q = 0; q < B.nstr; q++) {
+                const uint32_t mb = B.sbits[q] - 1u;  // the end marker: the stream's highest bit
+                {
+                    uint8_t* p8 = R + B.soff[q] + (mb >> 3);
+                    const uintptr_t ad = reinterpret_cast<uintptr_t>(p8);
+                    atomicOr(reinterpret_cast<uint32_t*>(ad & ~uintptr_t(3)),
+                             (1u << (mb & 7u)) << (8u * static_cast<uint32_t>(ad & 3u)));
+                }
+            }
         // the sequences bitstream down to its place (dst <= src: 256-byte steps, each read before
         // it is written, never overlap an unread byte)
-        if (B.ns) {
+        if (w0 && B.ns) {
             const uint32_t n = (B.fbits + 7u) / 8u;
             const uint8_t* src = R + B.fscr;
             uint8_t* dst = R + B.seq0 + B.sh;
             const uint32_t t = (lane - lead) * 16u;
             for (uint32_t o = 0; o < n; o += 256u) {
                 const uint4 w = *reinterpret_cast<const uint4*>(src + o + t);
-                const uint32_t wv[4] = {w.x, w.y, w.z, w.w};
+                const uint32_t wv4[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
                 for (uint32_t j = 0; j < 16u; j++)
-                    if (o + t + j < n) dst[o + t + j] = static_cast<uint8_t>(wv[j >> 2] >> (8u * (j & 3u)));
+                    if (o + t + j < n) dst[o + t + j] = static_cast<uint8_t>(wv4[j >> 2] >> (8u * (j & 3u)));
             }
         }
     }
@@ -1800,30 +1834,6 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
                     R[o++] = static_cast<uint8_t>(sz);
                     R[o++] = static_cast<uint8_t>(sz >> 8);
                 }
-            // the shared bytes: every lane's edge records in bit order, OR-ed, then each stream's
-            // end marker (its highest bit) and zero padding
-            for (uint32_t q = 0; q < B.nstr; q++) {
-                uint32_t cur = kZNone, val = 0;
-                auto flush = [&]() {
-                    if (cur != kZNone) R[B.soff[q] + cur] = static_cast<uint8_t>(val);
-                };
-                auto add = [&](uint32_t r) {
-                    if (r == kZNone) return;
-                    if ((r >> 8) != cur) {
-                        flush();
-                        cur = r >> 8;
-                        val = 0;
-                    }
-                    val |= r & 255u;
-                };
-                for (uint32_t l = lead + kZBlkSegs; l-- > lead;) {
-                    add(rec[l * 8u + q * 2u]);
-                    add(rec[l * 8u + q * 2u + 1u]);
-                }
-                const uint32_t mb = B.sbits[q] - 1u;  // the marker's bit
-                add(((mb >> 3) << 8) | (1u << (mb & 7u)));
-                flush();
-            }
         } else {
             const uint32_t rh = n < 32u ? (n << 3) : n < 4096u ? (0x4u | (n << 4)) : (0xCu | (n << 4));
             for (uint32_t i = 0; i < B.lh; i++) R[3u + i] = static_cast<uint8_t>(rh >> (8u * i));
