@@ -1291,6 +1291,7 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     __syncthreads();  // every wave has read the counts (wave 0 reuses their space below)
     if (w0 && try_huff) {
         huff_lengths(hist, 256u, 11u, lens, sa, ss, num, lane);
+        KCDC_ZSTAMP(14);
         // codes: by weight ascending (longest first), then symbol (RFC 8878 §4.2.1.4); each
         // weight's codes start where the lighter weights' end, ranks within a weight by ballot
         uint32_t maxb = 0;
@@ -1338,6 +1339,7 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
         for (uint32_t o = 32; o > 0; o >>= 1) wmax = max(wmax, static_cast<uint32_t>(__shfl_xor(wmax, static_cast<int>(o), 64)));
         const bool fse_ok = top >= 3u && wmax < top;  // >= 2 distinct weights (one value: an RLE case)
         const uint32_t nc = fse_ok ? zstd_table(wcnt, 12u, 5u, top, wst, wdd, wal, wnorm, hdesc + 1, lane) : 0u;
+        KCDC_ZSTAMP(15);
         if (lane == 0) {
             const uint32_t direct = top <= 128u ? 1u + (top + 1u) / 2u : 0u;
             uint32_t fsz = 0;

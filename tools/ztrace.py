@@ -82,6 +82,13 @@ def main():
     a, b0 = np.polyfit(mx.astype(np.float64), fse, 1)
     res["fse_cycles_per_sequence_fit"] = {"slope": round(float(a), 1), "intercept": round(float(b0), 1),
                                           "longest_block_mean": float(mx.mean())}
+    sub = desc[:, 92:96].copy().view(np.uint64).astype(np.int64)  # huffman: lengths done, weights table done
+    hs = sub[:, 0] > 0
+    if hs.any():
+        res["huffman_split"] = {"spans_with_code": int(hs.sum()),
+                                "lengths": round(float((sub[hs, 0] - st[hs, 2]).mean()), 1),
+                                "codes+weights_table": round(float((sub[hs, 1] - sub[hs, 0]).mean()), 1),
+                                "weights_encode": round(float((st[hs, 3] - sub[hs, 1]).mean()), 1)}
     bud = desc[:, 84:92].astype(np.int64).sum(axis=0)
     names = ["raw_blocks", "literal_sections", "sequence_bitstreams", "table_descriptions", "huffman_trees",
              "headers", "coded_literals", "coded_sequences"]
