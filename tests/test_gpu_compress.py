@@ -260,3 +260,33 @@ def test_zstd_table_carriers(name, gpu):
     out, oo, ol, ids = _compress(name, host, [int(o) for o in offs], lens, gpu)
     _check(name, host, [int(o) for o in offs], lens, out, oo, ol, ids)
     assert (ids != 0).all(), ol
+
+
+@pytest.mark.parametrize("name", ["zstd", "zstd-best-compression", "zstd-fastest"])
+def test_zstd_adversarial_spans(name, gpu):
+    """Spans at the edges of the span writer's limits, each frame decoded by libzstd: the most
+    sequences a span can hold (4-byte matches everywhere: up to 8,192 per span, 2,048 per block),
+    the longest carries (a block's literals before its first sequence), matches reaching 32 KiB
+    back, long matches across whole segments, skewed literals over all 256 byte values, and
+    sequences whose offsets alternate (repeat-offset candidates that must not be taken)."""
+    rng = np.random.default_rng(2024)
+    vocab = [rng.integers(0, 256, 4, dtype=np.uint8).tobytes() for _ in range(12)]
+    tokens = np.frombuffer(b"".join(vocab[int(i)] for i in rng.integers(0, 12, 40000)), np.uint8)
+    head = rng.integers(0, 256, 7000, dtype=np.uint8)
+    far = np.concatenate([head[:2000], rng.integers(0, 256, 28000, dtype=np.uint8), head[:2768]])
+    skew = np.minimum(rng.geometric(0.02, 70000), 255).astype(np.uint8)
+    alt = np.tile(np.frombuffer(b"xyzw1234" * 3 + b"ABCD", np.uint8), 4000)
+    parts = [
+        tokens[:32768 * 3],                                                 # many 4-byte matches
+        np.concatenate([head, head[:500], rng.integers(0, 256, 9000, dtype=np.uint8), head]),  # long carries
+        far,                                                                # distances near 32 KiB
+        np.tile(np.frombuffer(b"0123456789abcdef" * 64, np.uint8), 70),     # long matches
+        skew,                                                               # all byte values, skewed
+        alt,                                                                # alternating offsets
+        np.concatenate([tokens[:5000], skew[:20000], tokens[5000:30000]]),
+    ]
+    host = np.concatenate(parts)
+    lens = [p.size for p in parts]
+    offs = [int(x) for x in np.cumsum([0] + lens[:-1])]
+    out, oo, ol, ids = _compress(name, host, offs, lens, gpu)
+    _check(name, host, offs, lens, out, oo, ol, ids)
