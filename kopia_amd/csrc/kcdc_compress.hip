@@ -505,90 +505,6 @@ __device__ uint32_t deflate_layout(const uint32_t* cls, const uint32_t* bits, co
 
 __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-// The dynamic block header (RFC 1951 §3.2.7) for the code lengths len[0..316): HLIT, HDIST,
-// HCLEN, the code-length code's lengths in the permuted order, then the literal/length and
-// distance lengths (one sequence) run-length coded with 16 (the previous length 3-6 times), 17
-// (3-10 zeros) and 18 (11-138 zeros) through that code (lengths <= 7, at least two used symbols:
-// inflaters reject an incomplete code-length code).  Bits to hdr[] (LDS words); returns their
-// count.  Scratch (LDS): cl[316] (symbol | extra << 8), clcnt[19], cllen[20], clcode[19], misc[4]
-// and huff_lengths' sa/ss/num.  Wave-collective.
-__device__ uint32_t dyn_header(const uint8_t* len, uint32_t* hdr, uint16_t* cl, uint32_t* clcnt, uint8_t* cllen,
-                               uint32_t* clcode, uint32_t* sa, uint16_t* ss, uint32_t* num, uint32_t* misc,
-                               uint32_t lane) {
-    if (lane == 0) {
-        uint32_t hlit = kNLit, hdist = kNDist;
-        while (hlit > 257u && len[hlit - 1u] == 0u) hlit--;
-        while (hdist > 1u && len[kNLit + hdist - 1u] == 0u) hdist--;
-        for (uint32_t j = 0; j < 19u; j++) clcnt[j] = 0u;
-        const uint32_t nt = hlit + hdist;
-        auto at = [&](uint32_t i) -> uint32_t { return i < hlit ? len[i] : len[kNLit + i - hlit]; };
-        uint32_t ncl = 0;
-        auto sym = [&](uint32_t s, uint32_t x) {
-            cl[ncl++] = static_cast<uint16_t>(s | (x << 8));
-            clcnt[s]++;
-        };
-        for (uint32_t i = 0; i < nt;) {
-            const uint32_t v = at(i);
-            uint32_t r = 1;
-            while (i + r < nt && at(i + r) == v) r++;
-            i += r;
-            if (v == 0u) {
-                while (r >= 11u) {
-                    const uint32_t k = r < 138u ? r : 138u;
-                    sym(18u, k - 11u);
-                    r -= k;
-                }
-                if (r >= 3u) {
-                    sym(17u, r - 3u);
-                    r = 0u;
-                }
-            } else {
-                sym(v, 0u);
-                r--;
-                while (r >= 3u) {
-                    const uint32_t k = r < 6u ? r : 6u;
-                    sym(16u, k - 3u);
-                    r -= k;
-                }
-            }
-            for (; r > 0u; r--) sym(v, 0u);
-        }
-        uint32_t nz = 0;
-        for (uint32_t j = 0; j < 19u; j++) nz += clcnt[j] != 0u;
-        if (nz < 2u) {
-            if (clcnt[0] == 0u) clcnt[0] = 1u;
-            else clcnt[1] = 1u;
-        }
-        misc[0] = hlit;
-        misc[1] = hdist;
-        misc[2] = ncl;
-    }
-    __syncthreads();
-    huff_lengths(clcnt, 19u, 7u, cllen, sa, ss, num, lane);
-    canon_codes(cllen, 19u, clcode, lane);
-    __syncthreads();
-    if (lane == 0) {
-        uint32_t hclen = 19u;
-        while (hclen > 4u && cllen[kClOrder[hclen - 1u]] == 0u) hclen--;
-        Bits w{0ull, 0u, hdr};
-        w.put(misc[0] - 257u, 5);
-        w.put(misc[1] - 1u, 5);
-        w.put(hclen - 4u, 4);
-        for (uint32_t i = 0; i < hclen; i++) w.put(cllen[kClOrder[i]], 3);
-        const uint32_t ncl = misc[2];
-        for (uint32_t k = 0; k < ncl; k++) {
-            const uint32_t s = cl[k] & 31u, x = cl[k] >> 8, c = clcode[s];
-            w.put(c & 0xFFFFu, c >> 16);
-            if (s >= 16u) w.put(x, s == 16u ? 2u : s == 17u ? 3u : 7u);
-        }
-        const uint32_t hb = 32u * static_cast<uint32_t>(w.op - hdr) + w.nb;
-        if (w.nb) *w.op = static_cast<uint32_t>(w.bb);
-        misc[3] = hb;
-    }
-    __syncthreads();
-    return misc[3];
-}
-
 // Bits OR-ed into an LDS word buffer from any bit offset (neighbouring segments share words).
 struct OrBits {
     uint64_t bb;
@@ -609,6 +525,154 @@ struct OrBits {
         if (nb) atomicOr(&buf[wa], static_cast<uint32_t>(bb));
     }
 };
+
+// The dynamic block header (RFC 1951 §3.2.7) for the code lengths len[0..316): HLIT, HDIST,
+// HCLEN, the code-length code's lengths in the permuted order, then the literal/length and
+// distance lengths (one sequence) run-length coded with 16 (the previous length 3-6 times), 17
+// (3-10 zeros) and 18 (11-138 zeros) through that code (lengths <= 7, at least two used symbols:
+// inflaters reject an incomplete code-length code).  Bits to hdr[] (LDS words); returns their
+// count.  Wave-parallel: the runs start where a length differs from the one before (a ballot per
+// 64 positions), each run's lane emits its symbols at its offset (a prefix over the runs in order),
+// and every symbol's code goes to its bit offset (a prefix over the symbols), OR-ed into hdr.
+// Scratch (LDS): cl[316] (symbol | extra << 8), clcnt[19], cllen[20], clcode[19], misc[4] and
+// huff_lengths' sa/ss/num.  Wave-collective.
+__device__ uint32_t dyn_header(const uint8_t* len, uint32_t* hdr, uint16_t* cl, uint32_t* clcnt, uint8_t* cllen,
+                               uint32_t* clcode, uint32_t* sa, uint16_t* ss, uint32_t* num, uint32_t* misc,
+                               uint32_t lane) {
+    uint32_t hlit = 257u, hdist = 1u;  // the last used literal/length and distance codes
+    for (uint32_t k = 0; k < kNLit; k += 64u) {
+        const uint64_t m = __ballot(k + lane < kNLit && len[k + lane] != 0u);
+        if (m) hlit = max(hlit, k + 64u - static_cast<uint32_t>(__builtin_clzll(m)));
+    }
+    {
+        const uint64_t m = __ballot(lane < kNDist && len[kNLit + lane] != 0u);
+        if (m) hdist = max(hdist, 64u - static_cast<uint32_t>(__builtin_clzll(m)));
+    }
+    const uint32_t nt = hlit + hdist;
+    auto at = [&](uint32_t i) -> uint32_t { return i < hlit ? len[i] : len[kNLit + i - hlit]; };
+    if (lane < 19u) clcnt[lane] = 0u;
+    for (uint32_t j = lane; j < kHdrWords; j += 64u) hdr[j] = 0u;
+    uint64_t S[5];  // run starts, per 64 positions
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+        const uint32_t i = 64u * static_cast<uint32_t>(c) + lane;
+        S[c] = __ballot(i < nt && (i == 0u || at(i) != at(i - 1u)));
+    }
+    wave_sync();
+    auto emit = [&](uint32_t v, uint32_t r, auto f) {  // the symbols of a run of r lengths v
+        if (v == 0u) {
+            while (r >= 11u) {
+                const uint32_t k = r < 138u ? r : 138u;
+                f(18u, k - 11u);
+                r -= k;
+            }
+            if (r >= 3u) {
+                f(17u, r - 3u);
+                r = 0u;
+            }
+        } else {
+            f(v, 0u);
+            r--;
+            while (r >= 3u) {
+                const uint32_t k = r < 6u ? r : 6u;
+                f(16u, k - 3u);
+                r -= k;
+            }
+        }
+        for (; r > 0u; r--) f(v, 0u);
+    };
+    uint32_t base = 0;  // symbols of the runs before this group of positions
+#pragma unroll
+    for (int c = 0; c < 5; c++) {
+        const uint32_t i = 64u * static_cast<uint32_t>(c) + lane;
+        const bool st = (S[c] >> lane) & 1ull;
+        uint32_t r = 0, v = 0, cnt = 0;
+        if (st) {
+            uint32_t nx = nt;  // the next run's start
+            const uint64_t above = lane < 63u ? (S[c] >> (lane + 1u)) << (lane + 1u) : 0ull;
+            if (above) {
+                nx = 64u * static_cast<uint32_t>(c) + static_cast<uint32_t>(__builtin_ctzll(above));
+            } else {
+                for (int c2 = c + 1; c2 < 5; c2++)
+                    if (S[c2]) {
+                        nx = 64u * static_cast<uint32_t>(c2) + static_cast<uint32_t>(__builtin_ctzll(S[c2]));
+                        break;
+                    }
+            }
+            r = nx - i;
+            v = at(i);
+            emit(v, r, [&](uint32_t, uint32_t) { cnt++; });
+        }
+        uint32_t incl = cnt;
+        for (uint32_t o = 1; o < 64u; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (st) {
+            uint32_t o = base + incl - cnt;
+            emit(v, r, [&](uint32_t sy, uint32_t x) {
+                cl[o++] = static_cast<uint16_t>(sy | (x << 8));
+                atomicAdd(&clcnt[sy], 1u);
+            });
+        }
+        base += static_cast<uint32_t>(__shfl(incl, 63, 64));
+    }
+    const uint32_t ncl = base;
+    wave_sync();
+    if (lane == 0) {
+        uint32_t nz = 0;
+        for (uint32_t j = 0; j < 19u; j++) nz += clcnt[j] != 0u;
+        if (nz < 2u) {
+            if (clcnt[0] == 0u) clcnt[0] = 1u;
+            else clcnt[1] = 1u;
+        }
+    }
+    wave_sync();
+    huff_lengths(clcnt, 19u, 7u, cllen, sa, ss, num, lane);
+    canon_codes(cllen, 19u, clcode, lane);
+    wave_sync();
+    uint32_t hclen = 19u;
+    {
+        const uint32_t l = lane < 19u ? cllen[kClOrder[lane]] : 0u;
+        const uint64_t m = __ballot(l != 0u);
+        hclen = m ? 64u - static_cast<uint32_t>(__builtin_clzll(m)) : 0u;
+        hclen = hclen < 4u ? 4u : hclen;
+    }
+    if (lane == 0) {
+        OrBits w{0ull, 0u, 0u, hdr};
+        w.put(hlit - 257u, 5);
+        w.put(hdist - 1u, 5);
+        w.put(hclen - 4u, 4);
+        for (uint32_t i = 0; i < hclen; i++) w.put(cllen[kClOrder[i]], 3);
+        w.flush();
+    }
+    uint32_t pos = 14u + 3u * hclen;
+    for (uint32_t k0 = 0; k0 < ncl; k0 += 64u) {  // each symbol's code (and extra bits) at its offset
+        const uint32_t k = k0 + lane;
+        uint32_t sy = 0, x = 0, c = 0, nbits = 0;
+        if (k < ncl) {
+            sy = cl[k] & 31u;
+            x = cl[k] >> 8;
+            c = clcode[sy];
+            nbits = (c >> 16) + (sy == 16u ? 2u : sy == 17u ? 3u : sy == 18u ? 7u : 0u);
+        }
+        uint32_t incl = nbits;
+        for (uint32_t o = 1; o < 64u; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (k < ncl) {
+            const uint32_t p0 = pos + incl - nbits;
+            OrBits w{0ull, p0 & 31u, p0 >> 5, hdr};
+            w.put(c & 0xFFFFu, c >> 16);
+            if (sy >= 16u) w.put(x, sy == 16u ? 2u : sy == 17u ? 3u : 7u);
+            w.flush();
+        }
+        pos += static_cast<uint32_t>(__shfl(incl, 63, 64));
+    }
+    wave_sync();
+    return pos;
+}
 
 // S2 framing header of span b: 0x00, 3-byte LE length of (CRC + block), then the masked CRC
 // (written by the copy kernel) and the block's uvarint uncompressed length.
@@ -638,6 +702,21 @@ __device__ __forceinline__ void walk_tokens(const uint32_t* tok, uint32_t nm, ui
     }
     for (; x < xe; x++) lit(x);
 }
+
+// KCDC_TRACE builds (tools/ztrace.py with a deflate name): lane 0's s_memtime (low 32 bits) at the
+// deflate span's phase ends, descriptor words 281.. (after the plan's mode word)
+#ifdef KCDC_TRACE
+#define KCDC_DSTAMP(i)                                                                              \
+    do {                                                                                          \
+        if (threadIdx.x == 0)                                                                     \
+            a.desc[static_cast<uint64_t>(blockIdx.x) * kDescWords + 281u + (i)] =                  \
+                static_cast<uint32_t>(__builtin_amdgcn_s_memtime());                              \
+    } while (0)
+#else
+#define KCDC_DSTAMP(i) \
+    do {               \
+    } while (0)
+#endif
 
 // The span's deflate plan (see "deflate blocks of a span"), after the parse: symbol counts of the
 // coded segments, the dynamic code and its header (effort >= 1), every segment's size under the
@@ -673,6 +752,7 @@ __device__ __forceinline__ void deflate_plan(const CompArgs& a, uint32_t b, uint
                         atomicAdd(&hist[kNLit + m.ds], 1u);
                     });
     __syncthreads();
+    KCDC_DSTAMP(2);
     uint32_t hb = 0;
     if (dynamic) {
         if (lane == 0) {
@@ -687,8 +767,10 @@ __device__ __forceinline__ void deflate_plan(const CompArgs& a, uint32_t b, uint
         __syncthreads();
         huff_lengths(hist, kNLit, 15u, lens, sa, ss, num, lane);
         huff_lengths(hist + kNLit, kNDist, 15u, lens + kNLit, sa, ss, num, lane);
+        KCDC_DSTAMP(3);
         hb = dyn_header(lens, hdr, cl, clcnt, cllen, clcode, sa, ss, num, misc, lane);
     }
+    KCDC_DSTAMP(4);
     uint32_t bd = 0, bf = 0;  // the segment's bits under the dynamic / the fixed code
     if (coded)
         walk_tokens(tok, nm, x0, xe,
@@ -707,6 +789,7 @@ __device__ __forceinline__ void deflate_plan(const CompArgs& a, uint32_t b, uint
     lbf[lane] = bf;
     llen[lane] = seg_len;
     __syncthreads();
+    KCDC_DSTAMP(5);
     const uint32_t nseg = (span_len + kSeg - 1u) / kSeg;
     if (lane == 0) {
         uint32_t mode = kModeStored, bits = 8u * (span_len + 5u);
@@ -1880,6 +1963,9 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
     const uint64_t len = a.in_lens[c];
     const uint64_t sb = static_cast<uint64_t>(u) * kSpan;
     const uint32_t span_len = static_cast<uint32_t>(len - sb < kSpan ? len - sb : kSpan);
+#ifdef KCDC_TRACE
+    if (FMT == kFmtDeflate) KCDC_DSTAMP(0);
+#endif
     // Stage [A0, A0 + 16 ng) with A0 = A & ~15: every 16-byte granule holds a byte of the span.
     const uint32_t d = stage_span(L, a.in + a.in_offs[c] + sb, span_len, lane);
     {
@@ -2143,7 +2229,15 @@ __global__ __launch_bounds__(64) void lz_spans_kernel(CompArgs a) {
     return over ? (kStored | seg_len) : seg_len;
     }();
     if constexpr (FMT == kFmtDeflate) {
+#ifdef KCDC_TRACE
+        __syncthreads();
+        KCDC_DSTAMP(1);
+#endif
         deflate_plan(a, b, lane, span_len, x0, word, nm, hist, reinterpret_cast<uint32_t*>(tab), L, d);
+#ifdef KCDC_TRACE
+        __syncthreads();
+        KCDC_DSTAMP(6);
+#endif
         return;
     }
     if constexpr (FMT == kFmtZstd)

@@ -3,7 +3,8 @@
 Runs one zstd compression of the mixed bench data through build/libkcdc_trace.so, reads lane
 0's s_memtime stamps (descriptor words 64.. of each span: kcdc_compress.hip KCDC_ZSTAMP) back
 from the workspace, and prints each phase's mean cycles per span.
-usage: KCDC_LIB=build/libkcdc_trace.so KCDC_ALLOW_VARIANT_LIB=1 python tools/ztrace.py [MiB]
+usage: KCDC_LIB=build/libkcdc_trace.so KCDC_ALLOW_VARIANT_LIB=1 python tools/ztrace.py [MiB] [name]
+(a deflate name: the parse and plan cycles of lz_spans_kernel<deflate> instead)
 """
 import json
 import os
@@ -40,6 +41,7 @@ def ws(n, spans):  # kcdc_compress.hip comp_ws
 
 def main():
     mib = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+    name = sys.argv[2] if len(sys.argv) > 2 else "zstd"
     dev = torch.device("cuda:0")
     host = mixed(mib << 20, 9)
     d = torch.from_numpy(host).to(dev)
@@ -56,7 +58,7 @@ def main():
     wb = int(_lib.lib().kcdc_compress_workspace_size(int(sum(lens)), n))
     work = torch.zeros(wb, dtype=torch.uint8, device=dev)
     _lib.check(_lib.lib().kcdc_compress_chunks_device(
-        b"zstd", d.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, out.data_ptr(), d_oo.data_ptr(),
+        name.encode(), d.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, out.data_ptr(), d_oo.data_ptr(),
         ol.data_ptr(), ids.data_ptr(), work.data_ptr(), wb, None))
     torch.cuda.synchronize()
     fixed = ws(n, 0)[1]
@@ -68,6 +70,19 @@ def main():
     spans = sum((L + SPAN - 1) // SPAN for L in lens)
     w = work.cpu().numpy()
     desc = w[desc_off:desc_off + spans * 4 * DESC_WORDS].view(np.uint32).reshape(spans, DESC_WORDS)
+    if name.startswith("deflate"):  # lz_spans_kernel<deflate>: u32 stamps at words 281..287
+        tw = desc[:, 281:288].astype(np.int64)
+        dd = (np.diff(tw, axis=1) % (1 << 32)).astype(np.float64)
+        names = ["parse", "plan: counts", "plan: code lengths", "plan: header", "plan: segment bits",
+                 "plan: layout and descriptor"]
+        out = {"name": name, "spans": int(spans), "ratio": float(ol.sum().item()) / host.size}
+        dyn = tw[:, 3] != 0  # spans with a dynamic code (the other spans skip stamps 3)
+        for i, n in enumerate(names):
+            rows = dyn if i in (2, 3) else np.ones(len(dd), bool)
+            out[n] = round(float(dd[rows, i].mean()), 1) if rows.any() else None
+        out["dynamic_spans"] = int(dyn.sum())
+        print(json.dumps(out, indent=1))
+        return
     st = desc[:, 64:84].copy().view(np.uint64).astype(np.int64)  # [spans, 10]
     dt = np.diff(st, axis=1)
     res = {"spans": int(spans), "ratio": float(ol.sum().item()) / host.size,
