@@ -379,59 +379,118 @@ __device__ void canon_codes(const uint8_t* len, uint32_t n, uint32_t* out, uint3
     }
 }
 
-// Code lengths (<= maxb bits) of a minimum-redundancy code for the n counts cnt[] (LDS), into
-// len[] (LDS bytes); unused symbols get 0, a single used symbol 1.  The wave ranks the used
-// symbols by (count, symbol); lane 0 then runs Moffat and Katajainen's in-place construction
-// ("In-place calculation of minimum-redundancy codes", WADS 1995) over the sorted counts and, if
-// a depth exceeds maxb, clamps the depths and moves leaves down until the Kraft sum is exactly 1
-// (the zlib/miniz limiting heuristic).  Scratch (LDS): sa[n], ss[n], num[33].  Wave-collective.
+// Code lengths (<= maxb bits) of a minimum-redundancy code for the n <= 512 counts cnt[] (LDS,
+// each < 2^23), into len[] (LDS bytes); unused symbols get 0, a single used symbol 1.  The wave
+// sorts the used symbols by (count, symbol) (a bitonic sort of count << 9 | symbol keys over the
+// next power of two >= n, unused keys last); lane 0 then runs Moffat and Katajainen's in-place
+// construction ("In-place calculation of minimum-redundancy codes", WADS 1995) over the sorted
+// counts and, if a depth exceeds maxb, clamps the depths and moves leaves down until the Kraft sum
+// is exactly 1 (the zlib/miniz limiting heuristic).  Scratch (LDS): sa[max(64, pow2 >= n)] (may
+// alias cnt: the counts are read first), ss[n], num[33].  Wave-collective.
 __device__ void huff_lengths(const uint32_t* cnt, uint32_t n, uint32_t maxb, uint8_t* len, uint32_t* sa, uint16_t* ss,
                              uint32_t* num, uint32_t lane) {
+    uint32_t P = 64u;
+    while (P < n) P <<= 1;
+    uint32_t key[8];
     uint32_t used = 0u;
-    for (uint32_t k = 0; k < n; k += 64u) {
-        const uint32_t s = k + lane;
-        const uint32_t c = s < n ? cnt[s] : 0u;
-        uint32_t r = 0u;
-        for (uint32_t t = 0; t < n; t++) {
-            const uint32_t ct = cnt[t];
-            r += (ct != 0u && (ct < c || (ct == c && t < s))) ? 1u : 0u;
-        }
-        if (s < n) len[s] = 0u;
-        if (c) {
-            sa[r] = c;
-            ss[r] = static_cast<uint16_t>(s);
-        }
+#pragma unroll
+    for (uint32_t t = 0; t < 8u; t++) {
+        const uint32_t s = lane + 64u * t;
+        const uint32_t c = s < n && 64u * t < P ? cnt[s] : 0u;
+        key[t] = c ? ((c << 9) | s) : 0xFFFFFFFFu;
         used += static_cast<uint32_t>(__popcll(__ballot(c != 0u)));
     }
     wave_sync();
-    if (lane == 0 && used == 1u) len[ss[0]] = 1u;
-    if (lane == 0 && used >= 2u) {
-        const int m = static_cast<int>(used);
-        uint32_t* A = sa;
-        A[0] += A[1];
-        int root = 0, leaf = 2;
-        for (int next = 1; next < m - 1; next++) {
-            if (leaf >= m || A[root] < A[leaf]) {
-                A[next] = A[root];
-                A[root++] = static_cast<uint32_t>(next);
-            } else {
-                A[next] = A[leaf++];
+#pragma unroll
+    for (uint32_t t = 0; t < 8u; t++) {
+        const uint32_t s = lane + 64u * t;
+        if (64u * t < P) sa[s] = key[t];
+        if (s < n) len[s] = 0u;
+    }
+    wave_sync();
+    for (uint32_t kk = 2; kk <= P; kk <<= 1)
+        for (uint32_t j = kk >> 1; j > 0u; j >>= 1) {
+            for (uint32_t i = lane; i < P; i += 64u) {
+                const uint32_t pi = i ^ j;
+                if (pi > i) {
+                    const uint32_t x = sa[i], y = sa[pi];
+                    if ((x > y) == ((i & kk) == 0u)) {
+                        sa[i] = y;
+                        sa[pi] = x;
+                    }
+                }
             }
-            if (leaf >= m || (root < next && A[root] < A[leaf])) {
-                A[next] += A[root];
-                A[root++] = static_cast<uint32_t>(next);
-            } else {
-                A[next] += A[leaf++];
+            wave_sync();
+        }
+    for (uint32_t r = lane; r < used; r += 64u) {  // the sorted counts in sa[], their symbols in ss[]
+        const uint32_t x = sa[r];
+        ss[r] = static_cast<uint16_t>(x & 511u);
+        sa[r] = x >> 9;
+    }
+    wave_sync();
+    if (lane == 0 && used == 1u) len[ss[0]] = 1u;
+    if (used < 2u) {
+        wave_sync();
+        return;
+    }
+    const int m = static_cast<int>(used);
+    uint32_t* A = sa;
+    if (lane == 0) {
+        // Phase 1 (lane 0): the internal nodes' weights, two queues (internal nodes from A[root],
+        // leaves from A[leaf]); the next weights of both queues are kept in registers and their
+        // loads issued a step ahead (a node's weight is final once built, leaves are never written).
+        const uint32_t kInf = 0xFFFFFFFFu;
+        uint32_t r0 = A[0] + A[1];  // weight of node root; r1: of node root + 1 once built
+        A[0] = r0;
+        uint32_t r1 = 0u;
+        int root = 0, leaf = 2;
+        uint32_t l0 = leaf < m ? A[leaf] : kInf, l1 = leaf + 1 < m ? A[leaf + 1] : kInf;
+        auto take_root = [&](int next) -> uint32_t {
+            const uint32_t w = r0;
+            A[root] = static_cast<uint32_t>(next);  // consumed: its parent
+            root++;
+            r0 = r1;
+            r1 = root + 1 < next ? A[root + 1] : 0u;
+            return w;
+        };
+        auto take_leaf = [&]() -> uint32_t {
+            const uint32_t w = l0;
+            leaf++;
+            l0 = l1;
+            l1 = leaf + 1 < m ? A[leaf + 1] : kInf;
+            return w;
+        };
+        for (int next = 1; next < m - 1; next++) {
+            const uint32_t w1 = (leaf >= m || r0 < l0) ? take_root(next) : take_leaf();
+            const uint32_t w2 = (leaf >= m || (root < next && r0 < l0)) ? take_root(next) : take_leaf();
+            const uint32_t w = w1 + w2;
+            A[next] = w;
+            if (root == next) r0 = w;
+            else if (root + 1 == next) r1 = w;
+        }
+        // Phase 2: parent pointers to depths, downwards (a parent's depth is final before its
+        // children's; the parent pointer is read an iteration ahead, the previous depth forwarded)
+        A[m - 2] = 0u;
+        if (m >= 3) {
+            uint32_t dprev = 0u, p = A[m - 3];
+            for (int i = m - 3; i >= 0; i--) {
+                const uint32_t pn = i > 0 ? A[i - 1] : 0u;
+                const uint32_t di = (p == static_cast<uint32_t>(i + 1) ? dprev : A[p]) + 1u;
+                A[i] = di;
+                dprev = di;
+                p = pn;
             }
         }
-        A[m - 2] = 0u;
-        for (int next = m - 3; next >= 0; next--) A[next] = A[A[next]] + 1u;
+        // Phase 3: depths to leaf depths (the node at A[root] read a step ahead)
         int avbl = 1, usedc = 0, dpth = 0, next = m - 1;
         root = m - 2;
+        uint32_t ar = A[root], an = root > 0 ? A[root - 1] : 0u;
         while (avbl > 0) {
-            while (root >= 0 && static_cast<int>(A[root]) == dpth) {
+            while (root >= 0 && static_cast<int>(ar) == dpth) {
                 usedc++;
                 root--;
+                ar = an;
+                an = root > 0 ? A[root - 1] : 0u;
             }
             while (avbl > usedc) {
                 A[next--] = static_cast<uint32_t>(dpth);
@@ -441,35 +500,46 @@ __device__ void huff_lengths(const uint32_t* cnt, uint32_t n, uint32_t maxb, uin
             dpth++;
             usedc = 0;
         }
-        // A[i]: depth of the i-th least frequent symbol (non-increasing in i)
-        for (uint32_t l = 0; l <= 32u; l++) num[l] = 0u;
-        uint32_t maxd = 0u;
-        for (int i = 0; i < m; i++) {
-            const uint32_t dd = A[i] < 32u ? A[i] : 32u;
-            num[dd]++;
-            maxd = dd > maxd ? dd : maxd;
+    }
+    wave_sync();
+    // A[i]: depth of the i-th least frequent symbol (non-increasing in i); the depths' histogram
+    if (lane < 33u) num[lane] = 0u;
+    wave_sync();
+    uint32_t maxd = 0u;
+    for (int i = static_cast<int>(lane); i < m; i += 64) {
+        const uint32_t dd = A[i] < 32u ? A[i] : 32u;
+        atomicAdd(&num[dd], 1u);
+        maxd = dd > maxd ? dd : maxd;
+    }
+    for (uint32_t o = 32; o > 0; o >>= 1) maxd = max(maxd, static_cast<uint32_t>(__shfl_xor(maxd, static_cast<int>(o), 64)));
+    wave_sync();
+    if (lane == 0 && maxd > maxb) {
+        for (uint32_t l = maxb + 1u; l <= 32u; l++) {
+            num[maxb] += num[l];
+            num[l] = 0u;
         }
-        if (maxd > maxb) {
-            for (uint32_t l = maxb + 1u; l <= 32u; l++) {
-                num[maxb] += num[l];
-                num[l] = 0u;
-            }
-            uint32_t total = 0u;
-            for (uint32_t l = 1; l <= maxb; l++) total += num[l] << (maxb - l);
-            while (total != (1u << maxb)) {
-                num[maxb]--;
-                for (uint32_t l = maxb - 1u; l > 0u; l--)
-                    if (num[l]) {
-                        num[l]--;
-                        num[l + 1u] += 2u;
-                        break;
-                    }
-                total--;
-            }
+        uint32_t total = 0u;
+        for (uint32_t l = 1; l <= maxb; l++) total += num[l] << (maxb - l);
+        while (total != (1u << maxb)) {
+            num[maxb]--;
+            for (uint32_t l = maxb - 1u; l > 0u; l--)
+                if (num[l]) {
+                    num[l]--;
+                    num[l + 1u] += 2u;
+                    break;
+                }
+            total--;
         }
-        int i = 0;
-        for (uint32_t l = maxb; l >= 1u; l--)
-            for (uint32_t k = num[l]; k > 0u; k--) len[ss[i++]] = static_cast<uint8_t>(l);
+    }
+    wave_sync();
+    // lengths: the least frequent symbols take the longest (sorted index i -> its length's bucket)
+    for (int i = static_cast<int>(lane); i < m; i += 64) {
+        uint32_t l = maxb, acc = num[maxb];
+        while (static_cast<uint32_t>(i) >= acc && l > 1u) {
+            l--;
+            acc += num[l];
+        }
+        len[ss[i]] = static_cast<uint8_t>(l);
     }
     wave_sync();
 }
@@ -765,7 +835,7 @@ __device__ __forceinline__ void deflate_plan(const CompArgs& a, uint32_t b, uint
             }
         }
         __syncthreads();
-        huff_lengths(hist, kNLit, 15u, lens, sa, ss, num, lane);
+        huff_lengths(hist, kNLit, 15u, lens, S + 1232, ss, num, lane);  // (512 words: free from 1228)
         huff_lengths(hist + kNLit, kNDist, 15u, lens + kNLit, sa, ss, num, lane);
         KCDC_DSTAMP(3);
         hb = dyn_header(lens, hdr, cl, clcnt, cllen, clcode, sa, ss, num, misc, lane);
