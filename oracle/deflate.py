@@ -160,6 +160,45 @@ def s2_encode(data: bytes) -> bytes:
     return b"".join(out)
 
 
+def s2_decode_snappy(stream: bytes) -> bytes:
+    """A second, independent reader for the S2 streams the device writes: the framing format is
+    parsed here and every compressed chunk's block is decoded by Google's Snappy library (through
+    pyarrow's codec), which the device's blocks must satisfy since they use only Snappy elements
+    (literals, copy-1, copy-2; no S2 repeat codes).  CRCs are checked by `s2_decode`, not here."""
+    import pyarrow as pa
+
+    codec = pa.Codec("snappy")
+    out, i = [], 0
+    while i < len(stream):
+        if i + 4 > len(stream):
+            raise ValueError("truncated chunk header")
+        t = stream[i]
+        n = int.from_bytes(stream[i + 1:i + 4], "little")
+        body = stream[i + 4:i + 4 + n]
+        if len(body) != n:
+            raise ValueError("truncated chunk")
+        if t == 0xFF:
+            if body != b"S2sTwO":
+                raise ValueError(f"bad stream identifier {body!r}")
+        elif t == 0x00:
+            blk = body[4:]
+            size, shift, j = 0, 0, 0
+            while True:  # the block's uvarint uncompressed length
+                b = blk[j]
+                size |= (b & 0x7F) << shift
+                shift += 7
+                j += 1
+                if b < 0x80:
+                    break
+            out.append(codec.decompress(blk, decompressed_size=size, asbytes=True))
+        elif t == 0x01:
+            out.append(body[4:])
+        elif t < 0x80:
+            raise ValueError(f"reserved chunk type {t:#x}")
+        i += 4 + n
+    return b"".join(out)
+
+
 def crc32c(data: bytes) -> int:
     import ctypes as C
 

@@ -124,3 +124,17 @@ def test_s2_oracle_decoder():
     rep = bytes([8, 3 << 2]) + b"abcd" + bytes([1 | (0 << 2), 0])      # copy-1 offset 0 (S2 repeat)
     with pytest.raises(ValueError):
         deflate.s2_decode(sid + _s2_chunk(rep, b"abcdabcd"))
+
+
+def test_s2_snappy_reader_agrees_with_the_oracle_reader():
+    """The second S2 reader (`deflate.s2_decode_snappy`: the framing parsed in Python, each block
+    decoded by Google's Snappy library through pyarrow) against the C oracle reader, over the
+    oracle's own S2 writer on text-like, periodic, zero and random data."""
+    pytest.importorskip("pyarrow")
+    rng = np.random.default_rng(9)
+    words = [b"kopia", b"snapshot", b"content", b" ", b"\n", b"index"]
+    text = b"".join(words[int(k)] for k in rng.integers(0, len(words), 60000))
+    for data in (text, bytes(100000), (b"0123456789" * 20000), rng.integers(0, 256, 70000, dtype=np.uint8).tobytes()):
+        stream = deflate.s2_encode(data)
+        assert deflate.s2_decode(stream) == data
+        assert deflate.s2_decode_snappy(stream) == data

@@ -38,6 +38,8 @@ def _check(name, host, offs, lens, out, oo, out_lens, ids):
         blob = out[oo[i]:oo[i] + out_lens[i]].tobytes()
         assert 6 <= out_lens[i] <= kc.compress_bound(int(n)), (i, n, out_lens[i])
         assert deflate.decompress(name, blob) == host[o:o + n].tobytes(), (i, n)
+        if name in S2:  # and the blocks through Google's Snappy library (an independent decoder)
+            assert deflate.s2_decode_snappy(blob[4:]) == host[o:o + n].tobytes(), (i, n)
         assert ids[i] == deflate.kept_header_id(name, int(n), int(out_lens[i])), i
 
 
