@@ -990,8 +990,8 @@ __device__ uint32_t zstd_seqs(uint8_t* sb8, uint32_t o, uint32_t nseq, uint32_t 
 // ---------------------------------------------------------------- zstd: span-level blocks (effort >= 1)
 // The parse leaves each segment's sequences in its slot (word 143 - k: literal length << 23 |
 // (match length - 4) << 15 | distance) and their count in the span's descriptor.  zstd_emit_kernel
-// (one wave per span) then writes the span as kZBlks Compressed_Blocks of kZBlkSegs segments
-// (RFC 8878 §3.1.1.2), all sharing the span's codes:
+// (one workgroup per span) then writes the span as kZBlks Compressed_Blocks, runs of segments of
+// about equal sequence counts (RFC 8878 §3.1.1.2), all sharing the span's codes:
 //   literals   one Huffman code for the span (<= 11 bits, direct weights: the largest literal
 //              must be <= 128), its tree carried by the span's first compressed block that uses it
 //              (Compressed_Literals_Block), the later ones Treeless; 1 stream up to 1023 literals,
@@ -1010,16 +1010,18 @@ __device__ uint32_t zstd_seqs(uint8_t* sb8, uint32_t o, uint32_t nseq, uint32_t 
 // lanes go through per-lane edge records merged by the block's leader); the sequences bitstream
 // by the block's leader lane, backwards (ZSTD_encodeSequences order), after a counting pass (the
 // raw-or-compressed choice needs the exact size first).  Block k goes to the slots of its first
-// segment (16 x kSlot bytes, >= any compressed body); its seglen word is its size, 0 for the
+// segment (its segments' kSlot bytes each, > 512); its seglen word is its size, 0 for the
 // other segments (deflate_copy_kernel skips them).  tools/zstd_span_model.py is the host model of
 // this layout (libzstd-decoded; mixed data 0.327 per-segment -> 0.281 span-level).
 // The reference (klauspost/compress/zstd, compressor_zstd.go:15-18) writes the same block types
 // (Huffman literals with table reuse, FSE-compressed or repeated sequence tables, raw fallback).
-constexpr uint32_t kZBlkSegs = 16;                 // segments per block
-constexpr uint32_t kZBlks = 64 / kZBlkSegs;        // blocks per span
+constexpr uint32_t kZBlks = 4;                     // blocks per span (one per wave of zstd_emit_kernel)
+#ifndef KCDC_ZSEGW
+#define KCDC_ZSEGW 4
+#endif
+constexpr uint32_t kZSegW = KCDC_ZSEGW;            // a segment's cost in the block split, in sequences
 constexpr uint32_t kZMaxSeq = kSpan / 4;           // a sequence covers >= 4 bytes
 constexpr uint32_t kZDesc = 80;                    // a table description: <= 53 x 10 bits + 4 + 2 bytes
-constexpr uint32_t kZRegion = kZBlkSegs * kSlot - kZOff;  // a block's bytes: from its first slot + 3
 constexpr uint32_t kZNone = 0xFFFFFFFFu;
 
 struct ZTab {          // FSE encoding table (RFC 8878 §4.1; zstd's FSE_buildCTable formulation)
@@ -1281,7 +1283,6 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     const uint32_t x0 = kSeg * lane;
     const uint32_t seg_len = x0 < span_len ? min(kSeg, span_len - x0) : 0u, xe = x0 + seg_len;
     const uint32_t nseq = seg_len ? a.desc[static_cast<uint64_t>(b) * kDescWords + lane] : 0u;
-    const uint32_t k = lane / kZBlkSegs, lead = k * kZBlkSegs;  // the lane's block, its first lane
     hist[tid] = 0u;
     ln_bits[tid] = 0u;
     if (tid < 36u + 53u + 32u) fcnt[tid] = 0u;
@@ -1301,6 +1302,22 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
         if (lane >= o) incl += y;
     }
     const uint32_t off = incl - nseq;
+    // The blocks: runs of segments of about equal cost (a sequence is a step of its block's
+    // serial FSE chain, a segment with data 4 besides), each at least one segment; cut where a
+    // segment's middle passes each quarter of the span's cost.
+    const uint32_t cost = nseq + (seg_len ? kZSegW : 0u);
+    const uint32_t ci = incl + kZSegW * static_cast<uint32_t>(__popcll(__ballot(seg_len != 0u) & ((2ull << lane) - 1ull)));
+    const uint32_t ctot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ci), 63));
+    const uint32_t mid2 = 2u * ci - cost;  // twice the segment's middle
+    uint32_t b1 = static_cast<uint32_t>(__popcll(__ballot(2u * mid2 <= ctot)));
+    uint32_t b2 = static_cast<uint32_t>(__popcll(__ballot(2u * mid2 <= 2u * ctot)));
+    uint32_t b3 = static_cast<uint32_t>(__popcll(__ballot(2u * mid2 <= 3u * ctot)));
+    b1 = min(max(b1, 1u), 61u);
+    b2 = min(max(b2, b1 + 1u), 62u);
+    b3 = min(max(b3, b2 + 1u), 63u);
+    auto bsel = [&](uint32_t i) -> uint32_t { return i == 0u ? 0u : i == 1u ? b1 : i == 2u ? b2 : i == 3u ? b3 : 64u; };
+    const uint32_t k = (lane >= b1 ? 1u : 0u) + (lane >= b2 ? 1u : 0u) + (lane >= b3 ? 1u : 0u);
+    const uint32_t lead = bsel(k), bend = bsel(k + 1u);  // the lane's block: its first lane, one past its last
     const uint32_t* sq = reinterpret_cast<const uint32_t*>(a.slots + (static_cast<uint64_t>(b) * 64u + lane) * kSlot);
     uint32_t covered = 0, matched = 0;
     for (uint32_t j = 0; j < (w0 ? nseq : 0u); j++) {  // (wave 0: the others use the LDS copies)
@@ -1313,7 +1330,7 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     const uint32_t nlit = seg_len - matched, tail = seg_len - covered;
     // the lane's first literal's index in its block
     uint32_t pin = nlit;
-    for (uint32_t o = 1; o < kZBlkSegs; o <<= 1) {
+    for (uint32_t o = 1; o < 64u; o <<= 1) {
         const uint32_t y = __shfl_up(pin, o, 64);
         if (lane - lead >= o) pin += y;
     }
@@ -1333,7 +1350,7 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     if (tid == 0) {  // literals pending before each segment's first sequence, within its block
         uint32_t cy = 0;
         for (uint32_t j = 0; j < 64u; j++) {
-            if (j % kZBlkSegs == 0u) cy = 0u;
+            if (j == 0u || j == b1 || j == b2 || j == b3) cy = 0u;
             const uint32_t t = ln_carry[j];
             ln_carry[j] = cy;
             cy = ln_nseq[j] ? t : cy + ln_len[j];
@@ -1341,26 +1358,6 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     }
     __syncthreads();
     KCDC_ZSTAMP(1);
-    // the lane's literals, first to last, as byte values: runs read 4 bytes at a time
-    auto lits_fwd = [&](auto f) {
-        auto run = [&](uint32_t x, uint32_t e) {
-            for (; x + 4u <= e; x += 4u) {
-                const uint32_t w = st_ld32(L, d, x);
-                f(w & 255u);
-                f((w >> 8) & 255u);
-                f((w >> 16) & 255u);
-                f(w >> 24);
-            }
-            for (; x < e; x++) f(st_byte(L, d, x));
-        };
-        uint32_t x = x0;
-        for (uint32_t j = 0; j < nseq; j++) {
-            const uint32_t v = seqw[off + j], ll = zseq_ll(v);
-            run(x, x + ll);
-            x += ll + zseq_ml(v);
-        }
-        run(x, xe);
-    };
     // The four waves share the counting passes: wave w takes the lane's literals at bytes
     // [x0 + 128 w, x0 + 128 (w + 1)) of its segment (lits_part: f(value, index in the block)) and
     // its sequences j = w mod 4.
@@ -1597,9 +1594,8 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     const uint32_t tsz = try_huff ? misc[0] : 0u;  // the tree description's bytes
     const bool huff = tsz != 0u;
     // literal streams: each lane's bits per stream of its block
-    const uint32_t p = ln_p[lane];
     uint32_t nl_blk = 0;
-    for (uint32_t j = lead; j < lead + kZBlkSegs; j++) nl_blk += ln_nlit[j];
+    for (uint32_t j = lead; j < bend; j++) nl_blk += ln_nlit[j];
     const uint32_t nstr = nl_blk > 1023u ? 4u : 1u;
     const uint32_t qn = nstr == 4u ? (nl_blk + 3u) / 4u : (nl_blk ? nl_blk : 1u);
     if (huff && ln_nlit[lane]) {  // (the four waves, each its part of the lane's literals)
@@ -1628,13 +1624,14 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     }
     __syncthreads();
     KCDC_ZSTAMP(5);
-    const uint32_t ns_blk = ln_off[lead + kZBlkSegs] - ln_off[lead];
+    const uint32_t ns_blk = ln_off[bend] - ln_off[lead];
     const uint32_t tdesc = nseq_span ? fdlen[0] + fdlen[1] + fdlen[2] : 0u;
     uint8_t* R = a.slots + (static_cast<uint64_t>(b) * 64u + lead) * kSlot + kZOff;  // the block's bytes
+    uint32_t* Sw = reinterpret_cast<uint32_t*>(a.slots + (static_cast<uint64_t>(b) * 64u + lead) * kSlot);  // its dwords
     if (w0 && lane == lead) {
         ZBlk& B = blk[k];
         uint32_t raw = 0;
-        for (uint32_t j = lead; j < lead + kZBlkSegs; j++) raw += ln_len[j];
+        for (uint32_t j = lead; j < bend; j++) raw += ln_len[j];
         B.raw = raw;
         B.nl = nl_blk;
         B.ns = ns_blk;
@@ -1643,7 +1640,7 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
         uint32_t lit = (nl_blk < 32u ? 1u : nl_blk < 4096u ? 2u : 3u) + nl_blk;  // raw literals
         for (uint32_t q = 0; q < 4u; q++) {
             uint32_t s = 0;
-            for (uint32_t j = lead; j < lead + kZBlkSegs; j++) s += ln_bits[j * 4u + q];
+            for (uint32_t j = lead; j < bend; j++) s += ln_bits[j * 4u + q];
             B.sbits[q] = s + 1u;
         }
         if (huff && nl_blk) {  // the Huffman section with the tree: a bound on any literals section chosen
@@ -1665,17 +1662,19 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
         // of the states), then lane 0 runs the state chain over them, reading each lane's values
         // with readlane: per sequence the chain is the three state steps and the bit packing.
         ZBlk& B = blk[wv];
-        const uint32_t lead = wv * kZBlkSegs, fs = B.fscr;
+        const uint32_t lead = bsel(wv), end = bsel(wv + 1u), fs = B.fscr;
         uint8_t* R = a.slots + (static_cast<uint64_t>(b) * 64u + lead) * kSlot + kZOff;
         uint32_t* dst = reinterpret_cast<uint32_t*>(R + fs);
-        const uint32_t lim = (kZRegion - fs - 40u) / 4u;  // words (the chain stops within 7 of it)
+        const uint32_t region = (end - lead) * kSlot - kZOff;  // the block's bytes
+        // words (the chain stops within 7 of it); a block whose scratch starts too high is raw
+        const uint32_t lim = fs + 96u <= region ? (region - fs - 40u) / 4u : 0u;
         const ZTab &tLL = tab[0], &tOF = tab[1], &tML = tab[2];
-        const uint32_t i0 = ln_off[lead], i1 = ln_off[lead + kZBlkSegs];
+        const uint32_t i0 = ln_off[lead], i1 = ln_off[end];
         uint64_t bb = 0;       // lane 0: the bit writer
         uint32_t nb = 0, o = 0;
         uint32_t sLL = 0, sML = 0, sOF = 0;  // lane 0: the states
-        bool over = false;
-        // val < 2^n, n <= 62, with nb < 32 before: both words of the low 64 bits are stored, the
+        bool over = lim == 0u;
+        // val < 2^n, n <= 63, with nb < 32 before: both words of the low 64 bits are stored, the
         // cursor moves by the full words, the rest stays (bits past 64 come from the high part)
         auto put64 = [&](uint64_t val, uint32_t n) {
             const uint64_t low = bb | (val << nb);
@@ -1701,7 +1700,7 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
             // lane t: sequence hi - 1 - t
             const uint32_t idx = hi - 1u - min(lane, cnt - 1u);
             uint32_t cy = 0, cyp = 0;  // its (and the previous one's) segment's carry when it is the segment's first
-            for (uint32_t sg = lead; sg < lead + kZBlkSegs; sg++) {
+            for (uint32_t sg = lead; sg < end; sg++) {
                 const uint32_t lo = ln_off[sg], hs = ln_off[sg + 1u];
                 if (lo < hs && idx == lo) cy = ln_carry[sg];
                 if (lo < hs && idx > i0 && idx - 1u == lo) cyp = ln_carry[sg];
@@ -1722,9 +1721,10 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
             const uint32_t ofc = 31u - static_cast<uint32_t>(__builtin_clz(ov));
             const uint32_t x1 = llx | (mlx << llb), n1 = llb + mlb, x2 = ov - (1u << ofc);
             const uint2 eLL = tLL.dd[llc], eML = tML.dd[mlc], eOF = tOF.dd[ofc];
-            // packed for the chain: dnb (< 2^20) | (dfs + 512) << 20; x1 (< 2^21) | n1 << 21; x2 | ofc << 16
+            // packed for the chain: dnb (< 2^20) | (dfs + 512) << 20; x1 (< 2^22: a literal length < 2^15
+            // and a match length < 2^9) | n1 << 22; x2 | ofc << 16
             uint32_t pLL = eLL.x | ((eLL.y + 512u) << 20), pML = eML.x | ((eML.y + 512u) << 20);
-            uint32_t pOF = eOF.x | ((eOF.y + 512u) << 20), xa = x1 | (n1 << 21), xb = x2 | (ofc << 16);
+            uint32_t pOF = eOF.x | ((eOF.y + 512u) << 20), xa = x1 | (n1 << 22), xb = x2 | (ofc << 16);
             // every lane's values are read across lanes below: keep them computed here, by all
             asm volatile("" : "+v"(pLL), "+v"(pML), "+v"(pOF), "+v"(xa), "+v"(xb));
             if (lane == 0) {
@@ -1758,9 +1758,9 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
                     sOF = tOF.st[(sOF >> nOF) + fOF];
                     sML = tML.st[(sML >> nML) + fML];
                     sLL = tLL.st[(sLL >> nLL) + fLL];
-                    // the sequence's <= 62 bits (states <= 26, extras <= 21 + 15) as one value
-                    const uint32_t ns = nOF + nML + nLL, n1s = ya >> 21;
-                    const uint64_t val = static_cast<uint64_t>(bits) | (static_cast<uint64_t>(ya & 0x1FFFFFu) << ns) |
+                    // the sequence's <= 63 bits (states <= 26, extras <= 22 + 15) as one value
+                    const uint32_t ns = nOF + nML + nLL, n1s = ya >> 22;
+                    const uint64_t val = static_cast<uint64_t>(bits) | (static_cast<uint64_t>(ya & 0x3FFFFFu) << ns) |
                                          (static_cast<uint64_t>(yb & 0xFFFFu) << (ns + n1s));
                     put64(val, ns + n1s + (yb >> 16));
                     if (o > lim) {
@@ -1772,10 +1772,12 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
             over = __builtin_amdgcn_readfirstlane(over ? 1 : 0) != 0;
         }
         if (lane == 0) {
-            const uint32_t am = tML.al, ao = tOF.al, ala = tLL.al;  // initial states, read LL, OF, ML
-            put((sML & ((1u << am) - 1u)) | ((sOF & ((1u << ao) - 1u)) << am), am + ao);
-            put(sLL & ((1u << ala) - 1u), ala);
-            put(1u, 1);  // end marker
+            if (!over) {
+                const uint32_t am = tML.al, ao = tOF.al, ala = tLL.al;  // initial states, read LL, OF, ML
+                put((sML & ((1u << am) - 1u)) | ((sOF & ((1u << ao) - 1u)) << am), am + ao);
+                put(sLL & ((1u << ala) - 1u), ala);
+                put(1u, 1);  // end marker
+            }
             B.fbits = over ? kZNone : 32u * o + nb;
         }
     }
@@ -1861,10 +1863,8 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
     for (uint32_t kb = 0; kb < kZBlks; kb++) {
         const ZBlk& Z = blk[kb];
         if ((Z.role & (kZrCoded | kZrHuff)) != (kZrCoded | kZrHuff)) continue;
-        uint8_t* Rk = a.slots + (static_cast<uint64_t>(b) * 64u + kb * kZBlkSegs) * kSlot + kZOff;
-        uint32_t* w0p = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(Rk + Z.soff[0]) & ~uintptr_t(3));
-        uint32_t* w1p = reinterpret_cast<uint32_t*>((reinterpret_cast<uintptr_t>(Rk + Z.seq0) + 3u) & ~uintptr_t(3));
-        for (uint32_t* wp = w0p + tid; wp < w1p; wp += 256u) *wp = 0u;
+        uint32_t* Sk = reinterpret_cast<uint32_t*>(a.slots + (static_cast<uint64_t>(b) * 64u + bsel(kb)) * kSlot);
+        for (uint32_t w = ((kZOff + Z.soff[0]) >> 2) + tid; w < (kZOff + Z.seq0 + 3u) >> 2; w += 256u) Sk[w] = 0u;
     }
     __syncthreads();
     // The literals, each wave its part of every lane's literals (bytes [x0 + 128 w, + 128) of the
@@ -1879,14 +1879,13 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
             uint32_t bo[4];
             for (uint32_t q = 0; q < 4u; q++) {
                 uint32_t sum = 0;
-                for (uint32_t j = lane + 1u; j < lead + kZBlkSegs; j++) sum += ln_bits[j * 4u + q];
+                for (uint32_t j = lane + 1u; j < bend; j++) sum += ln_bits[j * 4u + q];
                 for (uint32_t w = wv + 1u; w < 4u; w++) sum += pbits[(lane * 4u + w) * 4u + q];
                 bo[q] = sum;
             }
-            auto or_byte = [&](uint32_t q, uint32_t bi, uint32_t v) {
-                uint8_t* p8 = R + B.soff[q] + bi;
-                const uintptr_t ad = reinterpret_cast<uintptr_t>(p8);
-                atomicOr(reinterpret_cast<uint32_t*>(ad & ~uintptr_t(3)), v << (8u * static_cast<uint32_t>(ad & 3u)));
+            auto or_byte = [&](uint32_t q, uint32_t bi, uint32_t v) {  // (slot bases are 4-byte aligned)
+                const uint32_t y = kZOff + B.soff[q] + bi;
+                atomicOr(Sw + (y >> 2), v << (8u * (y & 3u)));
             };
             uint32_t idx = ln_p[lane] + ln_nlit[lane], q = 4u, qlo = 0u;  // idx: one past the next literal back
             uint64_t bb = 0;
@@ -1943,20 +1942,21 @@ __global__ __launch_bounds__(256) void zstd_emit_kernel(CompArgs a) {
             for (uint32_t q = 0; q < B.nstr; q++) {
                 const uint32_t mb = B.sbits[q] - 1u;  // the end marker: the stream's highest bit
                 {
-                    uint8_t* p8 = R + B.soff[q] + (mb >> 3);
-                    const uintptr_t ad = reinterpret_cast<uintptr_t>(p8);
-                    atomicOr(reinterpret_cast<uint32_t*>(ad & ~uintptr_t(3)),
-                             (1u << (mb & 7u)) << (8u * static_cast<uint32_t>(ad & 3u)));
+                    const uint32_t y = kZOff + B.soff[q] + (mb >> 3);
+                    atomicOr(Sw + (y >> 2), (1u << (mb & 7u)) << (8u * (y & 3u)));
                 }
             }
-        // the sequences bitstream down to its place (dst <= src: 256-byte steps, each read before
-        // it is written, never overlap an unread byte)
-        if (w0 && B.ns) {
-            const uint32_t n = (B.fbits + 7u) / 8u;
-            const uint8_t* src = R + B.fscr;
-            uint8_t* dst = R + B.seq0 + B.sh;
-            const uint32_t t = (lane - lead) * 16u;
-            for (uint32_t o = 0; o < n; o += 256u) {
+    }
+    {  // block wv's sequences bitstream down to its place, by wave wv (above the literals; dst <=
+       // src: 1024-byte steps, each read before it is written, never overlap an unread byte)
+        const ZBlk& Z = blk[wv];
+        if ((Z.role & kZrCoded) && Z.ns) {
+            uint8_t* Rw = a.slots + (static_cast<uint64_t>(b) * 64u + bsel(wv)) * kSlot + kZOff;
+            const uint32_t n = (Z.fbits + 7u) / 8u;
+            const uint8_t* src = Rw + Z.fscr;
+            uint8_t* dst = Rw + Z.seq0 + Z.sh;
+            const uint32_t t = lane * 16u;
+            for (uint32_t o = 0; o < n; o += 1024u) {
                 const uint4 w = *reinterpret_cast<const uint4*>(src + o + t);
                 const uint32_t wv4[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
