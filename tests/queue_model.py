@@ -56,6 +56,7 @@ class Region:
     cand: List[bool]                 # per tile: the tile holds a candidate of this region
     half: List[int]                  # per tile with a candidate: its first candidate's sub-tile (0/1)
     forced_ends: bool                # a forced cut at this region's end would finish the stream
+    tail_seed: int = 0               # draws the last tile's step count (seeded, not address-based)
 
     @property
     def K(self):
@@ -107,7 +108,7 @@ def make_streams(rng, n, max_regions, max_tiles):
                 fe = False
             if f is None and not last:
                 fe = False
-            regs.append(Region(cand, half, fe))
+            regs.append(Region(cand, half, fe, rng.randrange(1 << 30)))
         out.append(Stream(regs, rng.random() < 0.7))
     return out
 
@@ -175,7 +176,7 @@ class Launch:
 
     def nb_of(self, reg, ti):  # steps of a tile: full tiles nb_full, a region's last tile shorter
         if ti == reg.K - 1:
-            return 1 + (hash((id(reg), ti)) % self.nb_full)
+            return 1 + (reg.tail_seed % self.nb_full)
         return self.nb_full
 
     def emit(self, cur, tok):
