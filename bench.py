@@ -368,6 +368,8 @@ def bench_batch(args, comm: Comm):
     cfg = f"config{args.config}" + ("-rk" if int(info.kind) == 2 else "")
     if name not in ("DYNAMIC-4M-BUZHASH", "DYNAMIC-4M-RABINKARP"):
         cfg += "-" + name
+    if (ns, args.stream_mib) not in ((4096, 4), (8192, 8)):  # another shape: its own key, too
+        cfg += f"-{ns}x{args.stream_mib}MiB"
     out = {
         "metric": METRIC, "value": agg["value"], "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "warmup_steps_run": warm_steps, "warmup_s": round(warm_s, 3),

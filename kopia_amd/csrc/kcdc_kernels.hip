@@ -3751,6 +3751,16 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
                                (algo.kind == kRabinKarp && s.nstreams < static_cast<uint64_t>(cus) * wg_waves)));
         unsigned grid = helpers || need >= cus ? cus : need;
         if (grid > dev::kMaxPipeGrid) grid = dev::kMaxPipeGrid;  // one claim flag per workgroup
+        // Fewer streams than waves: the waves without a stream of their own live on help tasks
+        // (half tiles of the owners' regions), and 4 KiB buzhash lanes (tiles and help tasks twice
+        // as long, half the claims, posts and warm-ups per region) win there, while with more
+        // streams than waves they lose (the coarser tail).  Same-process A/B,
+        // bit-exact, 2 KiB -> 4 KiB (profiles/r06/lane4k/): 4M 2048 x 8 MiB 1.864 -> 1.753 ms,
+        // 1024 x 16 MiB 2.855 -> 2.516, 512 x 32 MiB 9.72 -> 7.69; 2M 1024 x 16 MiB 3.09 -> 2.84;
+        // 1M loses at 2048 x 8 MiB (2.22 -> 2.29) and gains from 1024 x 16 MiB on (3.67 -> 3.61).
+        if (algo.kind == kBuzhash && !g_test.lane_cap && a.lane_cap == dev::kBuzLaneMax && helpers &&
+            s.nstreams * (algo.avg >= (2u << 20) ? 1u : 2u) <= static_cast<uint64_t>(grid) * wg_waves)
+            a.lane_cap = 2 * dev::kBuzLaneMax;
         uint64_t ring = 1;
         // every push (yields, tombstones) takes a fresh slot; a launch pushes at most
         // a few entries per wave beyond the initial n: size the ring with ample margin
