@@ -488,6 +488,11 @@ struct BatchArgs {
     // a chunk's region stops at the tile holding its first candidate, and a tile of avg bytes
     // overshoots by ~58 % on average (exponential candidate gaps), one of avg/4 by ~13 %.
     uint32_t lane_cap;
+    // Buzhash batch kernel: a region is published to helpers in windows of this many tiles (0:
+    // the whole region).  Helpers claim a published window's tiles from its top down, so over a
+    // whole region they scan its far end, which the owner's first candidate usually makes moot;
+    // a window keeps them just ahead of the owner (re-published as the owner passes it).
+    uint32_t help_window;
 };
 
 // End of stream sid's cut range (exclusive).
@@ -1592,9 +1597,12 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             const uint32_t K = static_cast<uint32_t>((hi - ct + T) / T);
             hs = 0;
             if (a.help && help_phase(budget) && K >= kHelpMinTiles && K <= static_cast<uint32_t>(kHelpTiles)) {
+                // a window of the region (help_window tiles from here), re-published as the owner
+                // passes its end
+                const uint32_t Kw = a.help_window && K > a.help_window ? a.help_window : K;
                 hep++;
-                hs = kHsPub | K;
-                help_publish(a, lane, me, hep, cur, ct, hi, K, T);
+                hs = kHsPub | Kw;
+                help_publish(a, lane, me, hep, cur, ct, Kw < K ? ct + static_cast<int64_t>(Kw) * T - 1 : hi, Kw, T);
             }
         }
         // The owner's claim on its next tile (atomic add on its slot's bottom), issued in step 0
@@ -1760,8 +1768,14 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             const int64_t T = kWave * static_cast<int64_t>(a.lane_cap);
             const int64_t ct0 = ct - static_cast<int64_t>(htile()) * T;  // the published tile 0
             const int64_t r = help_wait(a, lane, me, hep, htile() + 1u, hK(), ct0);
+            const int64_t wend = ct0 + static_cast<int64_t>(hK()) * T;  // past the published window
             if (r >= 0) {
                 cut = r - cur.off0 + 1;
+            } else if (r == -1 && wend <= hi) {  // no candidate in the window: publish the next one
+                cur.ct = wend;
+                help_close(a, lane, me, hep);
+                hs = kHsNeedPub;
+                region_changed = false;
             } else if (r == -1) {
                 cut = forced;
             } else {  // a tile still pending: scan on from it, unshared
@@ -1775,6 +1789,10 @@ __global__ __launch_bounds__(kDmaWaves * kWave, kDmaWaves / 4) void split_batch_
             hs += 1u << 8;  // htile++
             budget -= kWave * g.L;
             region_changed = false;
+            if ((hs & kHsPub) && htile() >= hK()) {  // past its published window: the next one
+                help_close(a, lane, me, hep);
+                hs = kHsNeedPub;
+            }
         }
         if (cut >= 0) {
             emit_cut(a, cur, lane, cut);
@@ -3592,6 +3610,7 @@ struct TestKnobs {
     bool force_error = false;  // mark every pipelined launch as failed
     int help = 0;              // intra-region help: 0 the policy below, 1 off, 2 on (A/B, tests)
     uint32_t lane_cap = 0;     // buzhash batch lane segment cap (256..4096, a power of two); 0: base_args' rule
+    uint32_t help_window = 0;  // buzhash help window in tiles (255: whole regions); 0: launch_split_batch's rule
     char* last_ws = nullptr;   // queue header of the last pipelined launch (kcdc_test_queue_stat)
     int last_dev = 0;
     uint32_t last_waves = 0;   // launch waves of that launch (kcdc_test_queue_stat key 12)
@@ -3761,6 +3780,15 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         if (algo.kind == kBuzhash && !g_test.lane_cap && a.lane_cap == dev::kBuzLaneMax && helpers &&
             s.nstreams * (algo.avg >= (2u << 20) ? 1u : 2u) <= static_cast<uint64_t>(grid) * wg_waves)
             a.lane_cap = 2 * dev::kBuzLaneMax;
+        // Four or more waves per stream: helpers outnumber the owners, and regions published
+        // four tiles at a time keep them just ahead of the owner instead of on the far end of the
+        // region (512 x 32 MiB 4M 7.83 -> 5.89 ms, 1M 8.28 -> 6.93).  With one helper per owner the
+        // windows' re-publishing costs more than they save (1024 x 16 MiB 4M 2.49 -> 2.58 at 8
+        // tiles, 3.10 at 4), so whole regions stay published there (profiles/r06/help_window/).
+        if (g_test.help_window)
+            a.help_window = g_test.help_window == 255u ? 0u : g_test.help_window;
+        else if (algo.kind == kBuzhash && helpers && 4u * s.nstreams <= static_cast<uint64_t>(grid) * wg_waves)
+            a.help_window = 4u;
         uint64_t ring = 1;
         // every push (yields, tombstones) takes a fresh slot; a launch pushes at most
         // a few entries per wave beyond the initial n: size the ring with ample margin
@@ -4220,6 +4248,11 @@ extern "C" int kcdc_test_set(int32_t key, int64_t value) {
             if (value != 0 && (value < 256 || value > 4096 || (value & (value - 1)) != 0))
                 return set_error(-22, "lane cap: 0, or a power of two in [256, 4096]");
             g_test.lane_cap = static_cast<uint32_t>(value);
+            return 0;
+        case 9:                                                            // KCDC_TEST_HELP_WINDOW
+            if (value < 0 || (value != 0 && (value < static_cast<int64_t>(dev::kHelpMinTiles) || value > 255)))
+                return set_error(-22, "help window: 0 (policy), 255 (whole regions), or tiles in [3, 254]");
+            g_test.help_window = static_cast<uint32_t>(value);
             return 0;
         default: return set_error(-22, "unknown test knob");
     }

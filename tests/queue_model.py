@@ -131,7 +131,7 @@ class PStream:
 class Launch:
     def __init__(self, streams, grid, wg_waves, *, kind="buz", help_on=True, quantum=3, min_tiles=3,
                  gap=1, help_every=2, wait_polls=20, spin_cap=4000, steal_spins=16, nb_full=3,
-                 delayed_wgs=(), delay_steps=0, mutations=(), seed=0):
+                 delayed_wgs=(), delay_steps=0, mutations=(), seed=0, window=0):
         self.st = streams
         self.n = len(streams)
         self.grid, self.wg_waves = grid, wg_waves
@@ -139,6 +139,7 @@ class Launch:
         self.kind = kind
         self.help_on = help_on
         self.quantum, self.min_tiles, self.gap = quantum, min_tiles, gap
+        self.window = window if kind == "buz" else 0   # help windows (BatchArgs::help_window; buzhash only)
         self.help_every, self.wait_polls = help_every, wait_polls
         self.spin_cap, self.steal_spins, self.nb_full = spin_cap, steal_spins, nb_full
         self.mut = set(mutations)
@@ -442,9 +443,10 @@ class Launch:
                 K = reg.K - cur.ti
                 hs_pub, hs_k, hs_tile, hs_needpub, hs_helped = False, 0, 0, False, False
                 if self.help_on and self.min_tiles <= K <= HELP_TILES:
+                    Kw = min(K, self.window) if self.window else K   # a window of the region
                     hep += 1
-                    hs_pub, hs_k = True, K
-                    yield from self.help_publish(me, hep, cur, K)
+                    hs_pub, hs_k = True, Kw
+                    yield from self.help_publish(me, hep, cur, Kw)
             claim_next_r = hs_pub and not is_help and not last_of_region and hs_tile + 1 < hs_k
             if MUT_BUDGET_HELP in self.mut:
                 budget_out = not hs_helped and budget - 1 <= 0
@@ -548,6 +550,12 @@ class Launch:
                 res = yield from self.help_wait(me, hep, hs_tile + 1, hs_k, tile0)
                 if res >= 0:
                     cut = ("C", cur.r, res)
+                elif res == -1 and tile0 + hs_k < reg.K:   # no candidate in the window: the next one
+                    self.paths["help_window_next"] += 1
+                    cur.ti = tile0 + hs_k
+                    yield from self.help_close(me, hep)
+                    hs_pub, hs_k, hs_tile, hs_needpub, hs_helped = False, 0, 0, True, False
+                    region_changed = False
                 elif res == -1:
                     cut = ("F", cur.r)
                 else:
@@ -560,6 +568,10 @@ class Launch:
                 hs_tile += 1
                 budget -= 1
                 region_changed = False
+                if hs_pub and hs_tile >= hs_k:            # past its published window: the next one
+                    self.paths["help_window_passed"] += 1
+                    yield from self.help_close(me, hep)
+                    hs_pub, hs_k, hs_tile, hs_needpub, hs_helped = False, 0, 0, True, False
             if cut is not None:
                 self.emit(cur, cut)
                 cur.r += 1
@@ -666,14 +678,16 @@ class Launch:
         return v
 
 
-def random_launch(seed, kind="buz", mutations=()):
+def random_launch(seed, kind="buz", mutations=(), window=None):
     """One launch of a random geometry.  The knobs stand for the kernels' geometry parameters:
     grid x waves per workgroup (the persistent grid), streams against waves (fewer than, equal to,
     a few more, many more: the backlog that turns yields on), regions and tiles per stream (the
     average size / lane cap: tiles per region), steps per tile (nb_full: lane cap / 128 B), the
     visit quantum in tiles (KCDC_QUANTUM_TILES), the smallest published region
     (KCDC_HELP_MIN_TILES), the owner's wait bound (KCDC_HELP_WAIT_TICKS), help on or off (the
-    per-name policy), and a workgroup that starts late (another kernel holds its CU: try_steal)."""
+    per-name policy), a workgroup that starts late (another kernel holds its CU: try_steal), and
+    the help window (BatchArgs::help_window: regions published a few tiles at a time; drawn from
+    its own generator so the other draws of a seed stay as they were)."""
     rng = random.Random(seed)
     grid = rng.choice([1, 2, 3, 4])
     wgw = rng.choice([2, 4, 8])
@@ -683,6 +697,7 @@ def random_launch(seed, kind="buz", mutations=()):
     delayed = {rng.randrange(grid)} if grid > 1 and rng.random() < 0.3 else set()
     L = Launch(streams, grid, wgw, kind=kind, help_on=rng.random() < 0.85, quantum=rng.choice([1, 2, 3, 6]),
                min_tiles=rng.choice([2, 3]), nb_full=rng.choice([1, 2, 3, 4]), wait_polls=rng.choice([3, 20, 200]),
-               delayed_wgs=delayed, delay_steps=rng.choice([100, 2000, 20000]), mutations=mutations, seed=seed)
+               delayed_wgs=delayed, delay_steps=rng.choice([100, 2000, 20000]), mutations=mutations, seed=seed,
+               window=random.Random(seed ^ 0x5A5A).choice([0, 0, 3, 4, 6]) if window is None else window)
     L.run()
     return L

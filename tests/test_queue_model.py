@@ -16,6 +16,7 @@ PATHS = {"claim_ok", "claim_failed", "help_cas_lost", "help_posted", "help_close
          "help_wait_none", "help_wait_pending", "help_params_stale", "switch_entry_ready",
          "switch_entry_polled", "yield", "yield_tomb", "tombstone_taken", "late_requeue", "steal",
          "requeued_first_ticket"}
+WINDOW_PATHS = {"help_window_next", "help_window_passed"}
 
 
 @pytest.mark.parametrize("kind", ["buz", "rk"])
@@ -28,6 +29,21 @@ def test_protocol_invariants_hold(kind):
         paths.update(L.paths)
     # every protocol path was exercised, so the invariants above covered it
     missing = PATHS - {k for k, c in paths.items() if c}
+    assert not missing, missing
+
+
+@pytest.mark.parametrize("window", [3, 4])
+def test_help_windows_keep_the_invariants(window):
+    """Regions published a few tiles at a time (BatchArgs::help_window, the buzhash kernel): the owner
+    re-publishes when it passes a window's end or its helpers hold the window's rest without a
+    candidate; every stream still finishes once with the expected cuts."""
+    paths = Counter()
+    for seed in range(SEEDS):
+        L = qm.random_launch(seed, "buz", window=window)
+        v = L.check()
+        assert not v, (seed, window, v[:5])
+        paths.update(L.paths)
+    missing = (PATHS | WINDOW_PATHS) - {"requeued_first_ticket", "steal"} - {k for k, c in paths.items() if c}
     assert not missing, missing
 
 
