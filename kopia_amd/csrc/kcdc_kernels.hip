@@ -488,7 +488,7 @@ struct BatchArgs {
     // a chunk's region stops at the tile holding its first candidate, and a tile of avg bytes
     // overshoots by ~58 % on average (exponential candidate gaps), one of avg/4 by ~13 %.
     uint32_t lane_cap;
-    // Buzhash batch kernel: a region is published to helpers in windows of this many tiles (0:
+    // Batch kernels: a region is published to helpers in windows of this many tiles (0:
     // the whole region).  Helpers claim a published window's tiles from its top down, so over a
     // whole region they scan its far end, which the owner's first candidate usually makes moot;
     // a window keeps them just ahead of the owner (re-published as the owner passes it).
@@ -2394,9 +2394,10 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             const uint32_t K = static_cast<uint32_t>((hi - ct + T) / T);
             hs = 0;
             if (a.help && help_phase(budget) && K >= kHelpMinTiles && K <= static_cast<uint32_t>(kHelpTiles)) {
+                const uint32_t Kw = a.help_window && K > a.help_window ? a.help_window : K;  // a window
                 hep++;
-                hs = kHsPub | K;
-                help_publish(a, lane, me, hep, cur, ct, hi, K, T);
+                hs = kHsPub | Kw;
+                help_publish(a, lane, me, hep, cur, ct, Kw < K ? ct + static_cast<int64_t>(Kw) * T - 1 : hi, Kw, T);
             }
         }
         // The owner's claim on its next tile: an atomic add on its slot's bottom after fill 1's
@@ -2554,8 +2555,14 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             const int64_t T = kWave * rk_cap;
             const int64_t ct0 = ct - static_cast<int64_t>(htile()) * T;  // the published tile 0
             const int64_t r = help_wait(a, lane, me, hep, htile() + 1u, hK(), ct0);
+            const int64_t wend = ct0 + static_cast<int64_t>(hK()) * T;  // past the published window
             if (r >= 0) {
                 cut = r - cur.off0 + 1;
+            } else if (r == -1 && wend <= hi) {  // no candidate in the window: publish the next one
+                cur.ct = wend;
+                help_close(a, lane, me, hep);
+                hs = kHsNeedPub;
+                region_changed = false;
             } else if (r == -1) {
                 cut = forced;
             } else {  // a tile still pending: scan on from it, unshared
@@ -2569,6 +2576,10 @@ __global__ __launch_bounds__(kRkWaves * kWave, kRkWaves / 4) void split_batch_rk
             hs += 1u << 8;  // htile++
             budget -= kWave * g.L;
             region_changed = false;
+            if ((hs & kHsPub) && htile() >= hK()) {  // past its published window: the next one
+                help_close(a, lane, me, hep);
+                hs = kHsNeedPub;
+            }
         }
         if (cut >= 0) {
             emit_cut(a, cur, lane, cut);
@@ -3780,15 +3791,21 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         if (algo.kind == kBuzhash && !g_test.lane_cap && a.lane_cap == dev::kBuzLaneMax && helpers &&
             s.nstreams * (algo.avg >= (2u << 20) ? 1u : 2u) <= static_cast<uint64_t>(grid) * wg_waves)
             a.lane_cap = 2 * dev::kBuzLaneMax;
-        // Four or more waves per stream: helpers outnumber the owners, and regions published
+        // Four or more waves per stream (both batch kernels): helpers outnumber the owners, and regions published
         // four tiles at a time keep them just ahead of the owner instead of on the far end of the
         // region (512 x 32 MiB 4M 7.83 -> 5.89 ms, 1M 8.28 -> 6.93).  With one helper per owner the
         // windows' re-publishing costs more than they save (1024 x 16 MiB 4M 2.49 -> 2.58 at 8
         // tiles, 3.10 at 4), so whole regions stay published there (profiles/r06/help_window/).
         if (g_test.help_window)
             a.help_window = g_test.help_window == 255u ? 0u : g_test.help_window;
-        else if (algo.kind == kBuzhash && helpers && 4u * s.nstreams <= static_cast<uint64_t>(grid) * wg_waves)
+        else if (helpers && 4u * s.nstreams <= static_cast<uint64_t>(grid) * wg_waves)
             a.help_window = 4u;
+        // Rabin-Karp (a tile is ~2.5x a buzhash tile's time, so re-publishing costs relatively
+        // less): windows of 8 tiles pay from one helper per owner on (1024 x 16 MiB 4M 4.52 ->
+        // 4.05 ms, 1M 5.56 -> 5.46); with four or more, 4 tiles (512 x 32 MiB 8.17 -> 6.33,
+        // 256 x 64 MiB 19.06 -> 11.69; profiles/r06/help_window/rk/)
+        else if (algo.kind == kRabinKarp && helpers && 2u * s.nstreams <= static_cast<uint64_t>(grid) * wg_waves)
+            a.help_window = 8u;
         uint64_t ring = 1;
         // every push (yields, tombstones) takes a fresh slot; a launch pushes at most
         // a few entries per wave beyond the initial n: size the ring with ample margin

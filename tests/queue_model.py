@@ -139,7 +139,7 @@ class Launch:
         self.kind = kind
         self.help_on = help_on
         self.quantum, self.min_tiles, self.gap = quantum, min_tiles, gap
-        self.window = window if kind == "buz" else 0   # help windows (BatchArgs::help_window; buzhash only)
+        self.window = window                       # help windows (BatchArgs::help_window)
         self.help_every, self.wait_polls = help_every, wait_polls
         self.spin_cap, self.steal_spins, self.nb_full = spin_cap, steal_spins, nb_full
         self.mut = set(mutations)

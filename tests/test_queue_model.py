@@ -32,14 +32,14 @@ def test_protocol_invariants_hold(kind):
     assert not missing, missing
 
 
-@pytest.mark.parametrize("window", [3, 4])
-def test_help_windows_keep_the_invariants(window):
-    """Regions published a few tiles at a time (BatchArgs::help_window, the buzhash kernel): the owner
+@pytest.mark.parametrize("kind,window", [("buz", 3), ("buz", 4), ("rk", 4)])
+def test_help_windows_keep_the_invariants(kind, window):
+    """Regions published a few tiles at a time (BatchArgs::help_window, both batch kernels): the owner
     re-publishes when it passes a window's end or its helpers hold the window's rest without a
     candidate; every stream still finishes once with the expected cuts."""
     paths = Counter()
     for seed in range(SEEDS):
-        L = qm.random_launch(seed, "buz", window=window)
+        L = qm.random_launch(seed, kind, window=window)
         v = L.check()
         assert not v, (seed, window, v[:5])
         paths.update(L.paths)
