@@ -3798,8 +3798,12 @@ int launch_split_batch(const Algo& algo, const SplitArgs& s, int device, void* s
         // tiles, 3.10 at 4), so whole regions stay published there (profiles/r06/help_window/).
         if (g_test.help_window)
             a.help_window = g_test.help_window == 255u ? 0u : g_test.help_window;
-        else if (helpers && 4u * s.nstreams <= static_cast<uint64_t>(grid) * wg_waves)
-            a.help_window = 4u;
+        else if (helpers && 4u * s.nstreams <= static_cast<uint64_t>(grid) * wg_waves) {
+            // buzhash: wider windows for more helpers per owner (16 waves per stream, 128 x 128 MiB:
+            // W = 4 19.9 ms, 6 17.3, 8 18.8; 32 per stream, 64 x 256 MiB: 4 33.4, 6 30.4, 8 27.9)
+            const uint64_t wps = static_cast<uint64_t>(grid) * wg_waves / s.nstreams;
+            a.help_window = algo.kind == kBuzhash && wps >= 32 ? 8u : algo.kind == kBuzhash && wps >= 16 ? 6u : 4u;
+        }
         // Rabin-Karp (a tile is ~2.5x a buzhash tile's time, so re-publishing costs relatively
         // less): windows of 8 tiles pay from one helper per owner on (1024 x 16 MiB 4M 4.52 ->
         // 4.05 ms, 1M 5.56 -> 5.46); with four or more, 4 tiles (512 x 32 MiB 8.17 -> 6.33,
